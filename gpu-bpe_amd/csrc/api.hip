@@ -1,0 +1,134 @@
+// Context, errors and device-memory helpers of the gpubpe C-ABI.
+// Replaces the reference's WebGPU device bring-up (engine.js:143-177,
+// engine.js:216-238): one HIP device + one stream per context.
+
+#include "common.h"
+
+#include <cstdarg>
+
+int gbpe_set_error(gbpe_ctx* ctx, int code, const char* fmt, ...) {
+    if (ctx) {
+        char buf[1024];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        ctx->err = buf;
+    }
+    return code;
+}
+
+// Kernel inventory (engine.js:234 logs the pipeline count).  Each entry maps
+// one of this library's kernels to the reference kernel(s) it replaces.
+static const char* const kKernelNames[] = {
+    "k_symbols",         // bpe_word_boundary (train.wgsl:144) + byte widening (trainer.js:49)
+    "k_count_full",      // bpe_clear_table + bpe_pair_count_b (train.wgsl:188, 366): initial / rebuild count
+    "k_refresh",         // bpe_find_max_pair4 (train.wgsl:204): per-block maxima of touched blocks
+    "k_select",          // bpe_find_max_pair_final_det + bpe_setup_merge (train.wgsl:276, 329)
+    "k_delta",           // bpe_merge_reduce_b (train.wgsl:433) + incremental pair-count deltas
+    "k_scan",            // bpe_prefix_sum_scan_blocks_{par,b} (train.wgsl:522, 620)
+    "k_compact",         // bpe_finalize_compact_b (train.wgsl:664) + in-place A-side rewrite
+    "k_tail",            // pairs of the stale tail window left by the reference compaction
+    "k_finish",          // state.symbol_count update (train.wgsl:605-607)
+    "k_trie_walk",       // trie_tokenizer_chunked (tokenize.wgsl:88)
+    "k_chunk_scan",      // trie_prefix_sum (tokenize.wgsl:199)
+    "k_chunk_compact",   // trie_tokenizer_compact (tokenize.wgsl:225)
+};
+
+extern "C" {
+
+const char* gbpe_version(void) { return "gpubpe 0.1 (gfx950, abi 1)"; }
+
+int gbpe_kernel_count(void) { return (int)(sizeof(kKernelNames) / sizeof(kKernelNames[0])); }
+
+const char* gbpe_kernel_name(int i) {
+    if (i < 0 || i >= gbpe_kernel_count()) return nullptr;
+    return kKernelNames[i];
+}
+
+int gbpe_ctx_create(int device_ordinal, gbpe_ctx** out) {
+    if (!out) return GBPE_E_INVALID;
+    *out = nullptr;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0) return GBPE_E_DEVICE;
+    if (device_ordinal < 0 || device_ordinal >= count) return GBPE_E_INVALID;
+    auto* ctx = new (std::nothrow) gbpe_ctx();
+    if (!ctx) return GBPE_E_OOM;
+    ctx->device = device_ordinal;
+    if (hipSetDevice(device_ordinal) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return GBPE_E_DEVICE;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device_ordinal) == hipSuccess) {
+        ctx->total_mem = prop.totalGlobalMem;
+        ctx->num_cu = prop.multiProcessorCount;
+    }
+    for (auto& ev : ctx->ev) hipEventCreate(&ev);
+    if (hipHostMalloc((void**)&ctx->enc_host_total, 16, hipHostMallocDefault) != hipSuccess) {
+        hipStreamDestroy(ctx->stream);
+        delete ctx;
+        return GBPE_E_OOM;
+    }
+    *out = ctx;
+    return GBPE_OK;
+}
+
+void gbpe_ctx_destroy(gbpe_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    hipFree(ctx->enc_scratch);
+    hipFree(ctx->enc_counts);
+    hipFree(ctx->enc_in);
+    hipFree(ctx->enc_out);
+    if (ctx->enc_host_total) hipHostFree(ctx->enc_host_total);
+    for (auto& ev : ctx->ev)
+        if (ev) hipEventDestroy(ev);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int gbpe_ctx_limits(gbpe_ctx* ctx, uint64_t* max_buffer_size) {
+    if (!ctx || !max_buffer_size) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
+    *max_buffer_size = ctx->total_mem;
+    return GBPE_OK;
+}
+
+const char* gbpe_last_error(const gbpe_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int gbpe_device_alloc(gbpe_ctx* ctx, uint64_t bytes, void** dptr) {
+    if (!ctx || !dptr) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
+    GBPE_HIP(ctx, hipMalloc(dptr, bytes ? bytes : 1));
+    return GBPE_OK;
+}
+
+int gbpe_device_free(gbpe_ctx* ctx, void* dptr) {
+    if (!ctx) return GBPE_E_INVALID;
+    GBPE_HIP(ctx, hipFree(dptr));
+    return GBPE_OK;
+}
+
+int gbpe_memcpy_h2d(gbpe_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+    if (!ctx) return GBPE_E_INVALID;
+    GBPE_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    GBPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return GBPE_OK;
+}
+
+int gbpe_memcpy_d2h(gbpe_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+    if (!ctx) return GBPE_E_INVALID;
+    GBPE_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    GBPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return GBPE_OK;
+}
+
+int gbpe_synchronize(gbpe_ctx* ctx) {
+    if (!ctx) return GBPE_E_INVALID;
+    GBPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return GBPE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,52 @@
+// Internal definitions shared by the gpubpe HIP translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gpubpe.h"
+
+struct gbpe_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint64_t total_mem = 0;
+    int num_cu = 0;
+    std::string err;
+    // encode pool (tokenizer.js:30-46 buffer pool: grows, never shrinks)
+    void* enc_scratch = nullptr;  uint64_t enc_scratch_bytes = 0;
+    void* enc_counts = nullptr;   uint64_t enc_counts_bytes = 0;
+    void* enc_in = nullptr;       uint64_t enc_in_bytes = 0;
+    void* enc_out = nullptr;      uint64_t enc_out_bytes = 0;
+    uint32_t* enc_host_total = nullptr;   // pinned
+    hipEvent_t ev[8] = {};
+    double enc_ms[3] = {0, 0, 0};
+};
+
+// ── error helpers ──────────────────────────────────────────────────────────
+int gbpe_set_error(gbpe_ctx* ctx, int code, const char* fmt, ...);
+
+#define GBPE_HIP(ctx, call)                                                              \
+    do {                                                                                 \
+        hipError_t _e = (call);                                                          \
+        if (_e != hipSuccess)                                                            \
+            return gbpe_set_error((ctx), _e == hipErrorOutOfMemory ? GBPE_E_OOM           \
+                                                                   : GBPE_E_DEVICE,      \
+                                  "%s failed: %s (%s:%d)", #call, hipGetErrorString(_e), \
+                                  __FILE__, __LINE__);                                   \
+    } while (0)
+
+#define GBPE_LAUNCH_CHECK(ctx) GBPE_HIP(ctx, hipGetLastError())
+
+// ── device helpers ─────────────────────────────────────────────────────────
+__device__ __forceinline__ uint32_t gbpe_fmix32(uint32_t x) {
+    // Murmur3 finaliser — the reference's pair hash (train.wgsl:62-67)
+    x = (x ^ (x >> 16)) * 0x7feb352du;
+    x = (x ^ (x >> 15)) * 0x846ca68bu;
+    return x ^ (x >> 16);
+}
+
+__host__ __device__ static inline uint64_t gbpe_div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }

@@ -1,0 +1,398 @@
+// Chunked greedy longest-match trie encode on MI355X (gfx950).
+//
+// Replaces tokenize.wgsl (trie_tokenizer_chunked :88-175, trie_prefix_sum
+// :199-208, trie_tokenizer_compact :225-243) and the TrieTokenizer host
+// pass (tokenizer.js:213-335).
+//
+// Layout: the reference walks a BFS trie of {firstChild, numChildren,
+// tokenId} nodes with a binary search over sorted edges per byte
+// (tokenize.wgsl:69-86: up to 8 dependent loads per byte).  On upload we
+// recompile the same trie into a double-array table: state t's record is
+// {check = parent state, base, tokenId}, and the child of state s on byte c
+// is t = base(s) + c iff record[t].check == s — one 16-byte L2-resident load
+// per byte consumed.  The 256 root transitions (and their depth-1 records)
+// live in LDS, as in the reference's root LUT + depth-1 cache
+// (tokenize.wgsl:51-63, 93-119).  Transitions are identical to the
+// reference trie's, so token ids are bit-identical.
+
+#include "common.h"
+
+#include <algorithm>
+
+namespace {
+
+constexpr int WALK_TPB = 256;
+constexpr uint32_t INV = 0xFFFFFFFFu;
+constexpr int SCAN_TPB = 1024;
+constexpr int SCAN_PER = 4;                       // counts per thread in k_chunk_scan1
+constexpr int SCAN_BLK = SCAN_TPB * SCAN_PER;     // 4096 chunks per scan block
+
+template <typename T>
+__global__ __launch_bounds__(WALK_TPB) void k_trie_walk(const uint8_t* __restrict__ in, uint64_t n, uint32_t cs,
+                                                        const uint4* __restrict__ rec, uint32_t nrec,
+                                                        const uint4* __restrict__ root, T* __restrict__ scratch,
+                                                        uint32_t* __restrict__ counts, uint64_t nchunks) {
+    __shared__ uint4 lut[256];   // byte -> {state, base, tokenId, present}
+    lut[threadIdx.x] = root[threadIdx.x];
+    __syncthreads();
+    const uint64_t chunk = (uint64_t)blockIdx.x * WALK_TPB + threadIdx.x;
+    if (chunk >= nchunks) return;
+    const uint64_t c0 = chunk * cs;
+    const uint64_t ce = min(c0 + cs, n);
+    T* out = scratch + c0;
+    const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
+    uint64_t widx = ~0ull;
+    uint32_t word = 0;
+    auto byte_at = [&](uint64_t p) -> uint32_t {
+        const uint64_t wi = p >> 2;
+        if (wi != widx) {
+            word = in32[wi];
+            widx = wi;
+        }
+        return (word >> ((p & 3u) * 8u)) & 0xFFu;
+    };
+    uint32_t cnt = 0;
+    uint64_t pos = c0;
+    while (pos < ce) {
+        const uint32_t c = byte_at(pos);
+        const uint4 e = lut[c];
+        uint32_t lmt = INV;
+        uint64_t lmp = pos;
+        if (e.w) {
+            uint32_t s = e.x, base = e.y;
+            if (e.z != INV) {
+                lmt = e.z;
+                lmp = pos + 1;
+            }
+            uint64_t wp = pos + 1;
+            while (wp < ce) {
+                const uint32_t t = base + byte_at(wp);
+                if (t >= nrec) break;
+                const uint4 r = rec[t];
+                if (r.x != s) break;
+                s = t;
+                base = r.y;
+                ++wp;
+                if (r.z != INV) {
+                    lmt = r.z;
+                    lmp = wp;
+                }
+            }
+        }
+        if (lmt != INV) {
+            out[cnt++] = (T)lmt;
+            pos = lmp;
+        } else {   // no token starts here: emit the raw byte value (tokenize.wgsl:169-171)
+            out[cnt++] = (T)c;
+            ++pos;
+        }
+    }
+    counts[chunk] = cnt;
+}
+
+// per 4096-chunk block: local exclusive prefix (in place) + block total
+__global__ __launch_bounds__(SCAN_TPB) void k_chunk_scan1(const uint32_t* __restrict__ counts, uint64_t nchunks,
+                                                          uint32_t* __restrict__ local, uint64_t* __restrict__ blocksum) {
+    __shared__ uint32_t wsum[SCAN_TPB / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_BLK + (uint64_t)threadIdx.x * SCAN_PER;
+    uint32_t v[SCAN_PER], s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k) {
+        v[k] = (base + k < nchunks) ? counts[base + k] : 0u;
+        s += v[k];
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    uint32_t run = incl - s;
+    for (int w = 0; w < wid; ++w) run += wsum[w];
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k) {
+        if (base + k < nchunks) local[base + k] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == SCAN_TPB - 1) blocksum[blockIdx.x] = run;
+}
+
+// exclusive scan of block totals (one workgroup); writes the grand total
+__global__ __launch_bounds__(SCAN_TPB) void k_chunk_scan2(uint64_t* __restrict__ blocksum, uint64_t nblk,
+                                                          uint64_t* __restrict__ total) {
+    __shared__ uint64_t wsum[SCAN_TPB / 64];
+    const uint64_t per = (nblk + SCAN_TPB - 1) / SCAN_TPB;
+    const uint64_t lo = threadIdx.x * per, hi = min(lo + per, nblk);
+    uint64_t s = 0;
+    for (uint64_t i = lo; i < hi; ++i) s += blocksum[i];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+        uint64_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    uint64_t run = incl - s;
+    for (int w = 0; w < wid; ++w) run += wsum[w];
+    for (uint64_t i = lo; i < hi; ++i) {
+        uint64_t v = blocksum[i];
+        blocksum[i] = run;
+        run += v;
+    }
+    if (threadIdx.x == SCAN_TPB - 1) *total = run;
+}
+
+// one wave per chunk: coalesced copy of its tokens to the final offset
+template <typename T>
+__global__ __launch_bounds__(256) void k_chunk_compact(const T* __restrict__ scratch, const uint32_t* __restrict__ counts,
+                                                       const uint32_t* __restrict__ local,
+                                                       const uint64_t* __restrict__ blocksum, uint64_t nchunks,
+                                                       uint32_t cs, uint32_t* __restrict__ out, uint64_t out_cap) {
+    const uint64_t chunk = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (chunk >= nchunks) return;
+    const int lane = threadIdx.x & 63;
+    const uint64_t off = blocksum[chunk / SCAN_BLK] + local[chunk];
+    const uint32_t cnt = counts[chunk];
+    const T* src = scratch + chunk * (uint64_t)cs;
+    for (uint32_t j = lane; j < cnt; j += 64) {
+        const uint64_t d = off + j;
+        if (d < out_cap) out[d] = (uint32_t)src[j];
+    }
+}
+
+}  // namespace
+
+struct gbpe_trie {
+    gbpe_ctx* ctx = nullptr;
+    uint4* rec = nullptr;      // double-array records {check, base, tokenId, 0}
+    uint32_t nrec = 0;
+    uint4* root = nullptr;     // 256 root transitions {state, base, tokenId, present}
+    uint32_t max_token_len = 0;
+    uint32_t max_token_id = 0;
+    uint32_t n_nodes = 0, n_edges = 0;
+};
+
+extern "C" int gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n_nodes, const uint32_t* edges,
+                                uint32_t n_edges, gbpe_trie** out) {
+    if (!ctx || !out || !nodes || n_nodes == 0 || (!edges && n_edges))
+        return gbpe_set_error(ctx, GBPE_E_INVALID, "trie upload: bad arguments");
+    *out = nullptr;
+    // ── compile the BFS trie into a double array ──
+    // state ids: root = 0 (never a transition target); every other node gets
+    // slot base(parent) + byte.
+    std::vector<uint32_t> state(n_nodes, INV), depth(n_nodes, 0);
+    std::vector<uint4> rec(1, make_uint4(INV, 0, INV, 0));  // slot 0 reserved for the root
+    std::vector<uint8_t> used(1, 1);
+    uint32_t first_free = 1;
+    std::vector<uint32_t> queue;
+    queue.reserve(n_nodes);
+    queue.push_back(0);
+    state[0] = 0;
+    uint32_t max_len = 0, max_tid = 0;
+    auto ensure = [&](uint64_t sz) {
+        if (sz > rec.size()) {
+            rec.resize(sz, make_uint4(INV, 0, INV, 0));
+            used.resize(sz, 0);
+        }
+    };
+    std::vector<uint4> root(256, make_uint4(0, 0, INV, 0));
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const uint32_t u = queue[qi];
+        const uint32_t fc = nodes[3 * (uint64_t)u], nc = nodes[3 * (uint64_t)u + 1] & 0xFFFFu;
+        if (nc && (uint64_t)fc + nc > n_edges)
+            return gbpe_set_error(ctx, GBPE_E_INVALID, "trie upload: node %u edges out of range", u);
+        uint32_t prev = 0;
+        for (uint32_t k = 0; k < nc; ++k) {
+            uint32_t c = edges[2 * ((uint64_t)fc + k)] & 0xFFu;
+            if (k && c <= prev)
+                return gbpe_set_error(ctx, GBPE_E_INVALID, "trie upload: children of node %u not sorted/unique", u);
+            prev = c;
+        }
+        if (nc == 0) continue;
+        const uint32_t cmin = edges[2 * (uint64_t)fc] & 0xFFu;
+        // first-fit base search
+        uint32_t b = first_free > cmin ? first_free - cmin : 1;
+        if (b < 1) b = 1;
+        for (;; ++b) {
+            ensure((uint64_t)b + 256);
+            bool ok = true;
+            for (uint32_t k = 0; k < nc && ok; ++k) ok = !used[b + (edges[2 * ((uint64_t)fc + k)] & 0xFFu)];
+            if (ok) break;
+        }
+        const uint32_t su = state[u];
+        if (u != 0) rec[su].y = b;
+        for (uint32_t k = 0; k < nc; ++k) {
+            const uint32_t c = edges[2 * ((uint64_t)fc + k)] & 0xFFu;
+            const uint32_t v = edges[2 * ((uint64_t)fc + k) + 1];
+            if (v >= n_nodes || v == 0) return gbpe_set_error(ctx, GBPE_E_INVALID, "trie upload: bad edge target %u", v);
+            if (state[v] != INV) return gbpe_set_error(ctx, GBPE_E_INVALID, "trie upload: node %u reached twice (not a tree)", v);
+            const uint32_t t = b + c;
+            used[t] = 1;
+            state[v] = t;
+            depth[v] = depth[u] + 1;
+            const uint32_t tid = nodes[3 * (uint64_t)v + 2];
+            rec[t] = make_uint4(su, 0, tid, 0);
+            if (tid != INV) {
+                max_len = std::max(max_len, depth[v]);
+                max_tid = std::max(max_tid, tid);
+            }
+            queue.push_back(v);
+            if (u == 0) root[c] = make_uint4(t, 0, tid, 1);
+        }
+        while (first_free < used.size() && used[first_free]) ++first_free;
+    }
+    // root LUT entries need their child's base (filled after the BFS)
+    for (int c = 0; c < 256; ++c)
+        if (root[c].w) root[c].y = rec[root[c].x].y;
+    auto* tr = new (std::nothrow) gbpe_trie();
+    if (!tr) return gbpe_set_error(ctx, GBPE_E_OOM, "host allocation failed");
+    tr->ctx = ctx;
+    tr->nrec = (uint32_t)rec.size();
+    tr->max_token_len = max_len;
+    tr->max_token_id = max_tid;
+    tr->n_nodes = n_nodes;
+    tr->n_edges = n_edges;
+    hipError_t e = hipMalloc(&tr->rec, rec.size() * sizeof(uint4));
+    if (e == hipSuccess) e = hipMalloc(&tr->root, 256 * sizeof(uint4));
+    if (e == hipSuccess) e = hipMemcpy(tr->rec, rec.data(), rec.size() * sizeof(uint4), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(tr->root, root.data(), 256 * sizeof(uint4), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        gbpe_trie_free(tr);
+        return gbpe_set_error(ctx, GBPE_E_DEVICE, "trie upload failed: %s", hipGetErrorString(e));
+    }
+    *out = tr;
+    return GBPE_OK;
+}
+
+extern "C" void gbpe_trie_free(gbpe_trie* tr) {
+    if (!tr) return;
+    hipFree(tr->rec);
+    hipFree(tr->root);
+    delete tr;
+}
+
+namespace {
+
+int grow(gbpe_ctx* ctx, void** p, uint64_t* have, uint64_t need) {
+    if (*have >= need) return GBPE_OK;
+    if (*p) {
+        hipStreamSynchronize(ctx->stream);
+        hipFree(*p);
+        *p = nullptr;
+        *have = 0;
+    }
+    const uint64_t sz = need + need / 2;   // 1.5x amortised growth (tokenizer.js:125-128)
+    GBPE_HIP(ctx, hipMalloc(p, sz));
+    *have = sz;
+    return GBPE_OK;
+}
+
+uint32_t effective_cs(const gbpe_trie* tr, uint32_t cs) {
+    if (cs) return cs;
+    // tokenizer.js:67-68 adaptive chunk
+    const uint32_t a = tr->max_token_len * 8u;
+    return std::max<uint32_t>(512u, std::min<uint32_t>(2048u, a));
+}
+
+// runs the three encode kernels on device buffers; *total_dev receives the count
+int encode_device_impl(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* d_in, uint64_t n, uint32_t cs, uint32_t* d_out,
+                       uint64_t out_cap, uint64_t* n_out) {
+    hipStream_t s = ctx->stream;
+    const uint64_t nchunks = gbpe_div_up(n, cs);
+    const bool narrow = tr->max_token_id < 65536u;   // raw-byte fallbacks are < 256
+    const uint64_t esz = narrow ? 2 : 4;
+    const uint64_t nblk = gbpe_div_up(nchunks, SCAN_BLK);
+    int rc = grow(ctx, &ctx->enc_scratch, &ctx->enc_scratch_bytes, nchunks * cs * esz + 16);
+    if (rc == GBPE_OK)
+        rc = grow(ctx, &ctx->enc_counts, &ctx->enc_counts_bytes, nchunks * 8 + nblk * 8 + 64);
+    if (rc != GBPE_OK) return rc;
+    uint32_t* counts = (uint32_t*)ctx->enc_counts;
+    uint32_t* local = counts + nchunks;
+    uint64_t* blocksum = (uint64_t*)(((uintptr_t)(local + nchunks) + 15) & ~(uintptr_t)15);
+    uint64_t* d_total = blocksum + nblk + 1;
+    const uint32_t gw = (uint32_t)gbpe_div_up(nchunks, WALK_TPB);
+    GBPE_HIP(ctx, hipEventRecord(ctx->ev[0], s));
+    if (narrow)
+        hipLaunchKernelGGL(k_trie_walk<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec, tr->nrec,
+                           tr->root, (uint16_t*)ctx->enc_scratch, counts, nchunks);
+    else
+        hipLaunchKernelGGL(k_trie_walk<uint32_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec, tr->nrec,
+                           tr->root, (uint32_t*)ctx->enc_scratch, counts, nchunks);
+    GBPE_LAUNCH_CHECK(ctx);
+    GBPE_HIP(ctx, hipEventRecord(ctx->ev[1], s));
+    hipLaunchKernelGGL(k_chunk_scan1, dim3((uint32_t)nblk), dim3(SCAN_TPB), 0, s, (const uint32_t*)counts, nchunks, local,
+                       blocksum);
+    hipLaunchKernelGGL(k_chunk_scan2, dim3(1), dim3(SCAN_TPB), 0, s, blocksum, nblk, d_total);
+    GBPE_LAUNCH_CHECK(ctx);
+    GBPE_HIP(ctx, hipEventRecord(ctx->ev[2], s));
+    const uint32_t gc = (uint32_t)gbpe_div_up(nchunks, 4);
+    if (narrow)
+        hipLaunchKernelGGL(k_chunk_compact<uint16_t>, dim3(gc), dim3(256), 0, s, (const uint16_t*)ctx->enc_scratch,
+                           (const uint32_t*)counts, (const uint32_t*)local, (const uint64_t*)blocksum, nchunks, cs, d_out,
+                           out_cap);
+    else
+        hipLaunchKernelGGL(k_chunk_compact<uint32_t>, dim3(gc), dim3(256), 0, s, (const uint32_t*)ctx->enc_scratch,
+                           (const uint32_t*)counts, (const uint32_t*)local, (const uint64_t*)blocksum, nchunks, cs, d_out,
+                           out_cap);
+    GBPE_LAUNCH_CHECK(ctx);
+    GBPE_HIP(ctx, hipEventRecord(ctx->ev[3], s));
+    GBPE_HIP(ctx, hipMemcpyAsync(ctx->enc_host_total, d_total, 8, hipMemcpyDeviceToHost, s));
+    GBPE_HIP(ctx, hipStreamSynchronize(s));
+    float a = 0, b = 0, c = 0;
+    hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]);
+    hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]);
+    hipEventElapsedTime(&c, ctx->ev[2], ctx->ev[3]);
+    ctx->enc_ms[0] = a;
+    ctx->enc_ms[1] = b;
+    ctx->enc_ms[2] = c;
+    uint64_t total;
+    memcpy(&total, ctx->enc_host_total, 8);
+    *n_out = total;
+    if (total > out_cap) return gbpe_set_error(ctx, GBPE_E_CAPACITY, "encode: output needs %llu tokens", (unsigned long long)total);
+    return GBPE_OK;
+}
+
+}  // namespace
+
+extern "C" int gbpe_encode_device(gbpe_ctx* ctx, gbpe_trie* tr, const void* d_bytes, uint64_t n, uint32_t chunk_size,
+                                  void* d_out, uint64_t out_cap, uint64_t* n_out) {
+    if (!ctx || !tr || !n_out || (n && (!d_bytes || !d_out))) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
+    if ((uintptr_t)d_bytes & 3u) return gbpe_set_error(ctx, GBPE_E_INVALID, "d_bytes must be 4-byte aligned");
+    *n_out = 0;
+    if (n == 0) return GBPE_OK;
+    return encode_device_impl(ctx, tr, (const uint8_t*)d_bytes, n, effective_cs(tr, chunk_size), (uint32_t*)d_out,
+                              out_cap, n_out);
+}
+
+extern "C" int gbpe_encode(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* bytes, uint64_t n, uint32_t chunk_size,
+                           uint32_t* out, uint64_t out_cap, uint64_t* n_out) {
+    if (!ctx || !tr || !n_out || (n && !bytes)) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
+    *n_out = 0;
+    if (n == 0) return GBPE_OK;   // tokenizer.js:175
+    const uint32_t cs = effective_cs(tr, chunk_size);
+    int rc = grow(ctx, &ctx->enc_in, &ctx->enc_in_bytes, gbpe_div_up(n, 4) * 4 + 16);
+    if (rc == GBPE_OK) rc = grow(ctx, &ctx->enc_out, &ctx->enc_out_bytes, n * 4 + 16);   // <= 1 token per byte
+    if (rc != GBPE_OK) return rc;
+    GBPE_HIP(ctx, hipMemcpyAsync(ctx->enc_in, bytes, n, hipMemcpyHostToDevice, ctx->stream));
+    uint64_t total = 0;
+    rc = encode_device_impl(ctx, tr, (const uint8_t*)ctx->enc_in, n, cs, (uint32_t*)ctx->enc_out, n, &total);
+    *n_out = total;
+    if (rc != GBPE_OK) return rc;
+    if (total > out_cap) return gbpe_set_error(ctx, GBPE_E_CAPACITY, "encode: output needs %llu tokens", (unsigned long long)total);
+    if (total) {
+        GBPE_HIP(ctx, hipMemcpyAsync(out, ctx->enc_out, total * 4, hipMemcpyDeviceToHost, ctx->stream));
+        GBPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return GBPE_OK;
+}
+
+extern "C" int gbpe_encode_last_timing(gbpe_ctx* ctx, double* ms_walk, double* ms_scan, double* ms_compact) {
+    if (!ctx) return GBPE_E_INVALID;
+    if (ms_walk) *ms_walk = ctx->enc_ms[0];
+    if (ms_scan) *ms_scan = ctx->enc_ms[1];
+    if (ms_compact) *ms_compact = ctx->enc_ms[2];
+    return GBPE_OK;
+}

@@ -1,0 +1,1046 @@
+// BPE training merge loop on MI355X (gfx950).
+//
+// Replaces the reference's 8-dispatch-per-merge WGSL pipeline
+// (training-pipeline.js:178-222: clear_table → pair_count_b → find_max_pair4 →
+// find_max_pair_final_det → setup_merge → merge_reduce_b → scan_blocks →
+// finalize_compact_b, train.wgsl) with an incremental design:
+//
+//   * the pair-count table PERSISTS across merges; instead of clearing 2^21
+//     slots and recounting every pair of the stream each merge
+//     (train.wgsl:188-202, 366-431), a merge only emits count deltas at its
+//     merge sites, aggregated per workgroup in LDS, then added into the
+//     global table — exact counts, no silent drops (train.wgsl:422-429);
+//   * argmax is a two-level tournament: per-2048-slot block maxima, only
+//     recomputed for blocks a merge touched, then one workgroup reduces them
+//     with the reference's tie-break (higher count, then smaller a<<16|b,
+//     train.wgsl:83-85);
+//   * the stream pass is two streaming kernels: k_delta (reads the stream,
+//     writes a 1-bit "merge site" mask + per-tile survivor counts + deltas),
+//     k_compact (reads the stream + mask, rewrites merged symbols in place
+//     and scatters survivors into the ping-pong buffer).  Race-free snapshot
+//     semantics (train.wgsl:476) fall out because k_compact never reads a
+//     neighbour;
+//   * symbols are u16 (bit 15 = word start) whenever every token id fits in
+//     15 bits (vocab <= 32768), else u32 with bit 16 (train.wgsl:36-37), so
+//     the common 32K-vocab case moves half the bytes.
+//
+// The reference's compaction quirk (bpe_finalize_compact_b bounded by the
+// NEW symbol count, train.wgsl:605-607 + 698/727) is reproduced by default:
+// survivors whose old index is >= the new count are not scattered and the
+// stale ping-pong contents stay in the stream.  k_tail adds the pairs of
+// that stale window to the count table.
+
+#include "common.h"
+
+#include <chrono>
+#include <cstdarg>
+
+namespace {
+
+constexpr int TPB = 256;              // threads per block
+constexpr int EPT = 16;               // symbols per thread in a tile
+constexpr int TILE = TPB * EPT;       // 4096 symbols per tile
+constexpr int LTAB = 2048;            // LDS delta table slots (k_delta / k_tail)
+constexpr int LTAB_FULL = 8192;       // LDS table slots for the full recount
+constexpr int LPROBE = 24;            // LDS probes before spilling to the global table
+constexpr uint32_t BLK_LOG2 = 11;     // 2048 table slots per argmax block
+constexpr int SEL_THREADS = 1024;
+
+template <typename S> struct Sym;
+template <> struct Sym<uint16_t> { static constexpr uint32_t WS = 0x8000u, TM = 0x7FFFu; };
+template <> struct Sym<uint32_t> { static constexpr uint32_t WS = 0x10000u, TM = 0xFFFFu; };
+
+// device-side loop state (the reference's IterState, train.wgsl:45-58)
+struct DevState {
+    uint32_t n;            // current symbol count
+    uint32_t stop;         // early stop (mc < 2 or id > 0xFFFF)
+    uint32_t next_id;
+    uint32_t a, b, nw;     // merge pair and new id
+    uint32_t mc;           // its count
+    uint32_t new_n;        // n - mc
+    uint32_t m;            // survivors with old index >= new_n (tail window size)
+    uint32_t merges_done;  // in this step (reset by the host, trainer.js:239)
+    uint32_t used;         // occupied table slots
+    uint32_t ndirty;       // dirty-block list length
+    uint32_t err;          // error bits
+    uint32_t valid_total;  // survivors counted by k_delta (must equal new_n)
+    uint32_t budget;       // merges allowed in this step
+    uint32_t live;         // distinct pairs with count > 0 at the last select
+    uint64_t tail_total;   // sum of m
+    uint32_t max_live;     // max of `live` over all selects
+    uint32_t pad[11];
+};
+static_assert(sizeof(DevState) <= 128, "state");
+
+enum : uint32_t { ERR_TABLE_FULL = 1, ERR_COUNT_MISMATCH = 2, ERR_PAIR_MISSING = 4 };
+
+struct Table {
+    uint2* slots;      // .x = pid (0 = empty), .y = count (u32, wraps for transient negatives)
+    uint32_t mask;     // slots - 1
+    uint64_t* bmax;    // per block: (count << 32) | ~pid, 0 when empty
+    uint32_t* dirty;   // per block flag
+    uint32_t* dlist;   // dirty block list
+    uint32_t* blive;   // per block: entries with count > 0
+    uint32_t nblk;
+};
+
+__device__ __forceinline__ void mark_dirty(const Table& tb, DevState* st, uint32_t slot) {
+    uint32_t blk = slot >> BLK_LOG2;
+    if (atomicExch(&tb.dirty[blk], 1u) == 0u) {
+        uint32_t k = atomicAdd(&st->ndirty, 1u);
+        tb.dlist[k] = blk;
+    }
+}
+
+// global insert-or-add (triangular probing visits every slot of a 2^k table)
+__device__ void table_add(const Table& tb, DevState* st, uint32_t pid, uint32_t delta) {
+    uint32_t h = gbpe_fmix32(pid) & tb.mask;
+    for (uint32_t p = 0; p <= tb.mask; ++p) {
+        uint32_t idx = (h + ((p * (p + 1)) >> 1)) & tb.mask;
+        uint32_t k = __hip_atomic_load(&tb.slots[idx].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == 0u) {
+            k = atomicCAS(&tb.slots[idx].x, 0u, pid);
+            if (k == 0u) {
+                atomicAdd(&st->used, 1u);
+                k = pid;
+            }
+        }
+        if (k == pid) {
+            atomicAdd(&tb.slots[idx].y, delta);
+            mark_dirty(tb, st, idx);
+            return;
+        }
+    }
+    atomicOr(&st->err, ERR_TABLE_FULL);
+}
+
+__device__ uint32_t table_find(const Table& tb, uint32_t pid) {
+    uint32_t h = gbpe_fmix32(pid) & tb.mask;
+    for (uint32_t p = 0; p <= tb.mask; ++p) {
+        uint32_t idx = (h + ((p * (p + 1)) >> 1)) & tb.mask;
+        uint32_t k = tb.slots[idx].x;
+        if (k == pid) return idx;
+        if (k == 0u) return 0xFFFFFFFFu;
+    }
+    return 0xFFFFFFFFu;
+}
+
+// per-workgroup LDS aggregation of (pid, delta)
+template <int N>
+struct LdsTab {
+    uint32_t key[N];
+    uint32_t val[N];
+};
+
+template <int N>
+__device__ __forceinline__ void lds_clear(LdsTab<N>& t) {
+    for (int i = threadIdx.x; i < N; i += blockDim.x) { t.key[i] = 0u; t.val[i] = 0u; }
+}
+
+template <int N>
+__device__ __forceinline__ void lds_add(LdsTab<N>& t, const Table& tb, DevState* st, uint32_t pid, uint32_t d) {
+    uint32_t h = gbpe_fmix32(pid);
+#pragma unroll 1
+    for (int p = 0; p < LPROBE; ++p) {
+        uint32_t idx = (h + (uint32_t)((p * (p + 1)) >> 1)) & (N - 1);
+        uint32_t k = atomicCAS(&t.key[idx], 0u, pid);
+        if (k == 0u || k == pid) {
+            atomicAdd(&t.val[idx], d);
+            return;
+        }
+    }
+    table_add(tb, st, pid, d);   // LDS table crowded: go straight to the global table
+}
+
+template <int N>
+__device__ __forceinline__ void lds_flush(LdsTab<N>& t, const Table& tb, DevState* st) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        uint32_t k = t.key[i], v = t.val[i];
+        if (k != 0u && v != 0u) table_add(tb, st, k, v);
+    }
+}
+
+template <typename S>
+__device__ __forceinline__ void load_tile(const S* __restrict__ cur, uint64_t base, S* __restrict__ tile) {
+    // 16 symbols per thread, 16-byte vector loads (buffers are padded to whole tiles)
+    constexpr int V = EPT * sizeof(S) / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(cur + base) + threadIdx.x * V;
+    uint4* dst = reinterpret_cast<uint4*>(tile) + threadIdx.x * V;
+#pragma unroll
+    for (int v = 0; v < V; ++v) dst[v] = src[v];
+}
+
+// ─── kernels ────────────────────────────────────────────────────────────────
+
+// bpe_word_boundary (train.wgsl:111-186) fused with byte→symbol widening
+// (trainer.js:49-53) and external-mask tagging (trainer.js:115-121).
+__device__ __forceinline__ uint32_t byte_class(uint32_t t) {
+    if (t == 0x0Au) return 4u;
+    if (t == 0x20u) return 2u;
+    if (t - 0x30u <= 9u) return 1u;
+    if (t >= 0x80u) return 0u;
+    if ((t | 0x20u) - 0x61u <= 25u) return 0u;
+    return 3u;
+}
+
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_symbols(const uint8_t* __restrict__ bytes, const uint8_t* __restrict__ ws_ext,
+                                                 S* __restrict__ out, uint64_t n, uint8_t* __restrict__ ws_out) {
+    uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    uint32_t tok = bytes[i];
+    bool ws;
+    if (ws_ext) {
+        ws = ws_ext[i] != 0;
+    } else if (i == 0) {
+        ws = true;
+    } else {
+        uint32_t c = byte_class(tok), p = byte_class(bytes[i - 1]);
+        ws = c != p;
+        if (p == 2u && (c == 0u || c == 1u)) ws = false;
+        if (c == 2u && p != 2u) ws = true;
+        if (p == 4u || c == 4u) ws = true;
+    }
+    if (out) out[i] = (S)(tok | (ws ? Sym<S>::WS : 0u));
+    if (ws_out) ws_out[i] = ws ? 1 : 0;
+}
+
+// Full pair count of the current stream into the (cleared) table — once at
+// start and on table rebuilds.  Same counting rule as train.wgsl:393-399.
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_count_full(DevState* st, const S* __restrict__ cur, Table tb) {
+    __shared__ LdsTab<LTAB_FULL> lt;
+    __shared__ __attribute__((aligned(16))) S tile[TILE];
+    __shared__ S prev_last;
+    lds_clear(lt);
+    const uint32_t n = st->n;
+    const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
+    for (uint32_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+        const uint64_t base = (uint64_t)tl * TILE;
+        __syncthreads();
+        load_tile(cur, base, tile);
+        if (threadIdx.x == 0) prev_last = base ? cur[base - 1] : (S)0;
+        __syncthreads();
+#pragma unroll 1
+        for (int k = 0; k < EPT; ++k) {
+            int li = threadIdx.x * EPT + k;
+            uint64_t i = base + li;
+            if (i == 0 || i >= n) continue;
+            uint32_t x1 = tile[li];
+            uint32_t x0 = li ? (uint32_t)tile[li - 1] : (uint32_t)prev_last;
+            uint32_t t0 = x0 & Sym<S>::TM, t1 = x1 & Sym<S>::TM;
+            if (!(x1 & Sym<S>::WS) && t0 && t1) lds_add(lt, tb, st, (t0 << 16) | t1, 1u);
+        }
+    }
+    lds_flush(lt, tb, st);
+}
+
+// recompute block maxima for dirty blocks
+__global__ __launch_bounds__(TPB) void k_refresh(DevState* st, Table tb) {
+    __shared__ uint64_t red[TPB / 64];
+    __shared__ uint32_t rlive[TPB / 64];
+    const uint32_t nd = st->ndirty;
+    for (uint32_t j = blockIdx.x; j < nd; j += gridDim.x) {
+        const uint32_t blk = tb.dlist[j];
+        const uint2* s = tb.slots + ((uint64_t)blk << BLK_LOG2);
+        uint64_t best = 0;
+        uint32_t live = 0;
+        for (uint32_t i = threadIdx.x; i < (1u << BLK_LOG2); i += TPB) {
+            uint2 e = s[i];
+            if (e.x && (int32_t)e.y > 0) {
+                uint64_t key = ((uint64_t)e.y << 32) | (uint32_t)(~e.x);
+                best = key > best ? key : best;
+                ++live;
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            uint64_t o = __shfl_xor(best, off);
+            best = o > best ? o : best;
+            live += __shfl_xor(live, off);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            red[threadIdx.x >> 6] = best;
+            rlive[threadIdx.x >> 6] = live;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < TPB / 64; ++w) {
+                best = red[w] > best ? red[w] : best;
+                live += rlive[w];
+            }
+            tb.bmax[blk] = best;
+            tb.blive[blk] = live;
+            tb.dirty[blk] = 0u;
+        }
+        __syncthreads();
+    }
+}
+
+// argmax over block maxima + the reference's bpe_setup_merge (train.wgsl:340-364)
+__global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, uint32_t* __restrict__ log) {
+    __shared__ uint64_t red[SEL_THREADS / 64];
+    __shared__ uint32_t rlive[SEL_THREADS / 64];
+    if (st->stop) return;
+    uint64_t best = 0;
+    uint32_t live = 0;
+    for (uint32_t i = threadIdx.x; i < tb.nblk; i += SEL_THREADS) {
+        uint64_t v = tb.bmax[i];
+        best = v > best ? v : best;
+        live += tb.blive[i];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        uint64_t o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+        live += __shfl_xor(live, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = best;
+        rlive[threadIdx.x >> 6] = live;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int w = 1; w < SEL_THREADS / 64; ++w) {
+        best = red[w] > best ? red[w] : best;
+        live += rlive[w];
+    }
+    st->live = live;
+    if (live > st->max_live) st->max_live = live;
+    st->ndirty = 0u;
+    st->m = 0u;
+    st->valid_total = 0u;
+    const uint32_t mc = (uint32_t)(best >> 32);
+    const uint32_t pid = ~(uint32_t)best;
+    if (st->merges_done >= st->budget) {   // host asked for fewer merges this step
+        return;
+    }
+    if (mc < 2u || st->next_id > 0xFFFFu) {   // train.wgsl:345-348
+        st->stop = 1u;
+        return;
+    }
+    const uint32_t idx = table_find(tb, pid);
+    if (idx == 0xFFFFFFFFu) {
+        atomicOr(&st->err, ERR_PAIR_MISSING);
+        st->stop = 1u;
+        return;
+    }
+    tb.slots[idx].y = 0u;                  // every (a,b) occurrence is a merge site
+    tb.dirty[idx >> BLK_LOG2] = 1u;
+    tb.dlist[0] = idx >> BLK_LOG2;
+    st->ndirty = 1u;
+    const uint32_t d = st->merges_done;
+    log[d * 4 + 0] = pid >> 16;
+    log[d * 4 + 1] = pid & 0xFFFFu;
+    log[d * 4 + 2] = st->next_id;
+    log[d * 4 + 3] = mc;
+    st->a = pid >> 16;
+    st->b = pid & 0xFFFFu;
+    st->nw = st->next_id;
+    st->mc = mc;
+    st->new_n = st->n - mc;
+    st->next_id += 1u;
+    st->merges_done = d + 1u;
+}
+
+// A merge is "active" for the stream kernels iff k_select logged it this round.
+__device__ __forceinline__ bool merge_active(const DevState* st, uint32_t round) {
+    return !st->stop && st->merges_done == round + 1u;
+}
+
+// Pass 1: merge-site mask, survivor counts per tile, count deltas.
+//   hit(i)  = (i >= 1) && !ws(i) && tok(i-1) == a && tok(i) == b     (B-side, train.wgsl:491-497)
+//   rw(i)   = hit(i+1)                                               (A-side, train.wgsl:482-485)
+//   valid   = !hit(i)
+// Old pair at i is destroyed iff hit(i-1)|hit(i)|hit(i+1) or i >= new_n (tail).
+// New pair at a survivor i < new_n with predecessor u:
+//   hit(i-1): u's token is `nw` (run head / A-side of the previous site)
+//   else if hit(i+1): (tok(i-1), nw)
+template <typename S, bool EXACT>
+__global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, const S* __restrict__ cur, Table tb,
+                                               uint16_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt) {
+    if (!merge_active(st, round)) return;
+    __shared__ LdsTab<LTAB> lt;
+    __shared__ __attribute__((aligned(16))) S tile[TILE];
+    __shared__ S halo[3];
+    __shared__ uint32_t red[TPB / 64];
+    lds_clear(lt);
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    const uint32_t n = st->n, new_n = st->new_n, a = st->a, b = st->b, nw = st->nw;
+    const uint32_t pid_ab = (a << 16) | b;
+    // reference compaction: survivors at old index >= new_n fall in the stale tail window
+    const uint32_t lim = EXACT ? 0xFFFFFFFFu : new_n;
+    const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
+    uint32_t my_valid = 0, my_tail = 0;
+    for (uint32_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+        const uint64_t base = (uint64_t)tl * TILE;
+        __syncthreads();
+        load_tile(cur, base, tile);
+        if (threadIdx.x < 3) {
+            int64_t j = threadIdx.x < 2 ? (int64_t)base - 2 + threadIdx.x : (int64_t)base + TILE;
+            halo[threadIdx.x] = (j >= 0 && (uint64_t)j < n) ? cur[j] : (S)0;
+        }
+        __syncthreads();
+        const int t = threadIdx.x;
+        const uint64_t i0 = base + (uint64_t)t * EPT;
+        uint32_t w[EPT + 3];
+        w[0] = t ? (uint32_t)tile[t * EPT - 2] : (uint32_t)halo[0];
+        w[1] = t ? (uint32_t)tile[t * EPT - 1] : (uint32_t)halo[1];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) w[2 + k] = tile[t * EPT + k];
+        w[EPT + 2] = (t < TPB - 1) ? (uint32_t)tile[t * EPT + EPT] : (uint32_t)halo[2];
+        // hk[k] = hit(i0 - 1 + k), k = 0..EPT+1
+        uint32_t hbits = 0;   // bit k = hk[k]
+#pragma unroll
+        for (int k = 0; k < EPT + 2; ++k) {
+            const uint64_t j1 = i0 + k;   // j + 1
+            bool h = (j1 >= 2) && (j1 - 1 < n) && !(w[k + 1] & WS) && ((w[k] & TM) == a) && ((w[k + 1] & TM) == b);
+            hbits |= (uint32_t)h << k;
+        }
+        hitmask[(uint64_t)tl * TPB + t] = (uint16_t)(hbits >> 1);
+        uint32_t cnt = 0;
+#pragma unroll 1
+        for (int k = 0; k < EPT; ++k) {
+            const uint64_t i = i0 + k;
+            if (i >= n) break;
+            const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+            const uint32_t xp = w[k + 1], xi = w[k + 2];
+            const uint32_t tp = xp & TM, ti = xi & TM;
+            const bool wsi = xi & WS;
+            if (!h0) {
+                ++cnt;
+                if (i >= lim) ++my_tail;
+            }
+            if (i == 0 || wsi) continue;        // no pair ends at i (old or new)
+            if (tp && ti && (hm || h0 || hp || i >= lim)) {
+                const uint32_t pid = (tp << 16) | ti;
+                if (pid != pid_ab) lds_add(lt, tb, st, pid, 0xFFFFFFFFu);
+            }
+            if (!h0 && i < lim) {
+                if (hm) {
+                    const uint32_t t2 = hp ? nw : ti;
+                    if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+                } else if (hp && tp) {
+                    lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+                }
+            }
+        }
+        my_valid += cnt;
+        // tile survivor count
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+        if ((t & 63) == 0) red[t >> 6] = cnt;
+        __syncthreads();
+        if (t == 0) tile_cnt[tl] = red[0] + red[1] + red[2] + red[3];
+    }
+    lds_flush(lt, tb, st);
+    for (int off = 32; off > 0; off >>= 1) {
+        my_valid += __shfl_xor(my_valid, off);
+        my_tail += __shfl_xor(my_tail, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (my_valid) atomicAdd(&st->valid_total, my_valid);
+        if (my_tail) atomicAdd(&st->m, my_tail);
+    }
+}
+
+// exclusive scan of the per-tile survivor counts (one workgroup)
+__global__ __launch_bounds__(SEL_THREADS) void k_scan(DevState* st, uint32_t round, uint32_t* __restrict__ tile_cnt) {
+    if (!merge_active(st, round)) return;
+    __shared__ uint32_t wsum[SEL_THREADS / 64];
+    const uint32_t ntiles = (uint32_t)gbpe_div_up(st->n, TILE);
+    const uint32_t per = (ntiles + SEL_THREADS - 1) / SEL_THREADS;
+    const uint32_t lo = threadIdx.x * per, hi = min(lo + per, ntiles);
+    uint32_t s = 0;
+    for (uint32_t i = lo; i < hi; ++i) s += tile_cnt[i];
+    // block exclusive scan of s
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    uint32_t wpre = 0;
+    for (int w = 0; w < wid; ++w) wpre += wsum[w];
+    uint32_t run = wpre + incl - s;
+    for (uint32_t i = lo; i < hi; ++i) {
+        uint32_t v = tile_cnt[i];
+        tile_cnt[i] = run;
+        run += v;
+    }
+    if (threadIdx.x == SEL_THREADS - 1) {
+        if (run != st->new_n || st->valid_total != st->new_n) atomicOr(&st->err, ERR_COUNT_MISMATCH);
+    }
+}
+
+// Pass 2: in-place A-side rewrite + scatter of survivors with old index < new_n
+// (the reference bound, train.wgsl:727) or all survivors (exact compaction).
+template <typename S, bool EXACT>
+__global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S* __restrict__ cur, S* __restrict__ oth,
+                                                 const uint16_t* __restrict__ hitmask,
+                                                 const uint32_t* __restrict__ tile_off) {
+    if (!merge_active(st, round)) return;
+    __shared__ __attribute__((aligned(16))) S stage[TILE];
+    __shared__ uint32_t wsum[TPB / 64];
+    constexpr uint32_t WS = Sym<S>::WS;
+    const uint32_t n = st->n, new_n = st->new_n, nw = st->nw;
+    const uint32_t limit = EXACT ? n : new_n;
+    const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
+    const uint32_t tl = blockIdx.x;
+    if (tl >= ntiles) return;
+    const int t = threadIdx.x;
+    const uint64_t base = (uint64_t)tl * TILE;
+    const uint64_t i0 = base + (uint64_t)t * EPT;
+    // own symbols (vector load) + mask bits
+    S x[EPT];
+    {
+        constexpr int V = EPT * sizeof(S) / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(cur + i0);
+        uint4 v[V];
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = src[k];
+        memcpy(x, v, sizeof(x));
+    }
+    const uint32_t hm = hitmask[(uint64_t)tl * TPB + t];
+    uint32_t nextbit = 0;
+    if (i0 + EPT < n) nextbit = hitmask[(uint64_t)tl * TPB + t + 1] & 1u;   // t+1 may be the next tile's first word
+    const uint32_t rwm = (hm >> 1) | (nextbit << (EPT - 1));
+    uint32_t keep = 0, cnt = 0;
+    bool any_rw = false;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        const uint64_t i = i0 + k;
+        const bool inb = i < n;
+        const bool valid = inb && !((hm >> k) & 1u);
+        const bool rw = inb && ((rwm >> k) & 1u);
+        if (rw) {
+            x[k] = (S)(nw | ((uint32_t)x[k] & WS));
+            any_rw = true;
+        }
+        if (valid && i < limit) {
+            keep |= 1u << k;
+            ++cnt;
+        }
+    }
+    if (any_rw) {   // in-place A-side rewrite (train.wgsl:486-487): the reference's ping buffer
+#pragma unroll
+        for (int k = 0; k < EPT; ++k)
+            if ((rwm >> k) & 1u && i0 + k < n) cur[i0 + k] = x[k];
+    }
+    // block exclusive scan of cnt
+    const int lane = t & 63, wid = t >> 6;
+    uint32_t incl = cnt;
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    uint32_t pre = incl - cnt;
+    for (int w = 0; w < wid; ++w) pre += wsum[w];
+    const uint32_t total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k)
+        if ((keep >> k) & 1u) stage[pre++] = x[k];
+    __syncthreads();
+    S* dst = oth + tile_off[tl];
+    for (uint32_t j = t; j < total; j += TPB) dst[j] = stage[j];
+}
+
+// Stale tail window [new_n - m, new_n) of the new stream: add its pairs.
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_tail(DevState* st, uint32_t round, const S* __restrict__ s, Table tb) {
+    if (!merge_active(st, round)) return;
+    const uint32_t m = st->m, new_n = st->new_n;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->tail_total += m;
+    }
+    if (m == 0) return;
+    __shared__ LdsTab<LTAB> lt;
+    lds_clear(lt);
+    __syncthreads();
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    const uint32_t lo = new_n - m;
+    for (uint32_t d = lo + blockIdx.x * TPB + threadIdx.x; d < new_n; d += gridDim.x * TPB) {
+        if (d == 0) continue;
+        uint32_t x0 = s[d - 1], x1 = s[d];
+        uint32_t t0 = x0 & TM, t1 = x1 & TM;
+        if (!(x1 & WS) && t0 && t1) lds_add(lt, tb, st, (t0 << 16) | t1, 1u);
+    }
+    lds_flush(lt, tb, st);
+}
+
+// finish a merge: the stream length becomes new_n
+__global__ void k_finish(DevState* st, uint32_t round) {
+    if (!merge_active(st, round)) return;
+    st->n = st->new_n;
+}
+
+__global__ void k_clear_dirty_all(DevState* st, Table tb) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < tb.nblk) {
+        tb.dirty[i] = 0u;
+        tb.dlist[i] = i;
+    }
+    if (i == 0) st->ndirty = tb.nblk;
+}
+
+// dump live (count > 0) pairs
+__global__ void k_dump_pairs(Table tb, uint32_t* pids, uint32_t* counts, uint32_t* nout, uint32_t cap) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > tb.mask) return;
+    uint2 e = tb.slots[i];
+    if (e.x && (int32_t)e.y > 0) {
+        uint32_t k = atomicAdd(nout, 1u);
+        if (k < cap) {
+            pids[k] = e.x;
+            counts[k] = e.y;
+        }
+    }
+}
+
+template <typename S>
+__global__ void k_export_symbols(const S* __restrict__ s, uint32_t* __restrict__ out, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t x = s[i];
+    out[i] = (x & Sym<S>::TM) | ((x & Sym<S>::WS) ? 0x10000u : 0u);
+}
+
+}  // namespace
+
+// ─── host side ──────────────────────────────────────────────────────────────
+
+struct gbpe_trainer {
+    gbpe_ctx* ctx = nullptr;
+    bool u16 = true;
+    uint32_t bps = 2;            // bytes per symbol
+    uint64_t n0 = 0, cap_syms = 0;
+    void* buf[2] = {nullptr, nullptr};
+    int cur = 0;                 // index of the buffer holding the stream
+    uint32_t n = 0;              // host copy of the stream length
+    uint32_t needed = 0, done = 0;
+    bool stop = false;
+    uint32_t flags = 0, batch = GBPE_BATCH_SIZE;
+    DevState* st = nullptr;
+    DevState* h_st = nullptr;    // pinned
+    uint32_t* d_log = nullptr;
+    uint32_t* h_log = nullptr;   // pinned
+    Table tb{};
+    uint32_t table_log2 = 22;
+    uint16_t* hitmask = nullptr;
+    uint32_t* tile_cnt = nullptr;
+    // stats
+    uint64_t bytes_moved = 0;
+    uint64_t max_live = 0;
+    double ms_merge = 0, ms_select = 0, ms_other = 0;
+    uint64_t timed_merges = 0;
+    std::vector<hipEvent_t> evs;
+};
+
+namespace {
+
+int tr_err(gbpe_trainer* t, int code, const char* msg) { return gbpe_set_error(t->ctx, code, "%s", msg); }
+
+#define TR_HIP(t, call) GBPE_HIP((t)->ctx, call)
+
+uint32_t grid_persistent(const gbpe_ctx* ctx, uint64_t work_tiles, uint32_t per_cu) {
+    uint64_t g = (uint64_t)(ctx->num_cu > 0 ? ctx->num_cu : 256) * per_cu;
+    if (work_tiles < g) g = work_tiles;
+    return (uint32_t)(g ? g : 1);
+}
+
+int table_rebuild(gbpe_trainer* t) {
+    hipStream_t s = t->ctx->stream;
+    const uint64_t slots = (uint64_t)t->tb.mask + 1;
+    TR_HIP(t, hipMemsetAsync(t->tb.slots, 0, slots * sizeof(uint2), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.bmax, 0, (uint64_t)t->tb.nblk * sizeof(uint64_t), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.blive, 0, (uint64_t)t->tb.nblk * sizeof(uint32_t), s));
+    TR_HIP(t, hipMemsetAsync(&t->st->used, 0, sizeof(uint32_t), s));
+    const uint64_t ntiles = gbpe_div_up(t->n, TILE);
+    const uint32_t g = grid_persistent(t->ctx, ntiles, 2);
+    if (t->u16)
+        hipLaunchKernelGGL(k_count_full<uint16_t>, dim3(g), dim3(TPB), 0, s, t->st,
+                           (const uint16_t*)t->buf[t->cur], t->tb);
+    else
+        hipLaunchKernelGGL(k_count_full<uint32_t>, dim3(g), dim3(TPB), 0, s, t->st,
+                           (const uint32_t*)t->buf[t->cur], t->tb);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    hipLaunchKernelGGL(k_clear_dirty_all, dim3(gbpe_div_up(t->tb.nblk, 256)), dim3(256), 0, s, t->st, t->tb);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    hipLaunchKernelGGL(k_refresh, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, t->tb);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+
+template <typename S>
+int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delta, uint32_t g_compact,
+                 uint32_t g_tail, uint32_t g_refresh, bool timing, hipEvent_t* ev) {
+    S* cur = (S*)t->buf[t->cur ^ (round & 1)];
+    S* oth = (S*)t->buf[t->cur ^ (round & 1) ^ 1];
+    if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log);
+    if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
+    if (t->flags & GBPE_TRAIN_EXACT_COMPACTION)
+        hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
+                           t->hitmask, t->tile_cnt);
+    else
+        hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
+                           t->hitmask, t->tile_cnt);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(SEL_THREADS), 0, s, t->st, round, t->tile_cnt);
+    if (t->flags & GBPE_TRAIN_EXACT_COMPACTION)
+        hipLaunchKernelGGL((k_compact<S, true>), dim3(g_compact), dim3(TPB), 0, s, t->st, round, cur, oth,
+                           (const uint16_t*)t->hitmask, (const uint32_t*)t->tile_cnt);
+    else
+        hipLaunchKernelGGL((k_compact<S, false>), dim3(g_compact), dim3(TPB), 0, s, t->st, round, cur, oth,
+                           (const uint16_t*)t->hitmask, (const uint32_t*)t->tile_cnt);
+    if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
+    hipLaunchKernelGGL(k_tail<S>, dim3(g_tail), dim3(TPB), 0, s, t->st, round, (const S*)oth, t->tb);
+    hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, s, t->st, round);
+    if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
+    hipLaunchKernelGGL(k_refresh, dim3(g_refresh), dim3(TPB), 0, s, t->st, t->tb);
+    if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
+    GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+
+}  // namespace
+
+extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
+                                   int input_on_device, const gbpe_train_opts* opts, gbpe_trainer** out) {
+    if (!ctx || !out || !opts) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
+    *out = nullptr;
+    if (n == 0) return gbpe_set_error(ctx, GBPE_E_EMPTY, "No symbols to train on — corpus is empty after pre-processing");
+    if (!bytes) return gbpe_set_error(ctx, GBPE_E_INVALID, "bytes is null");
+    if (n >= 0xFFFFFFF0ull) return gbpe_set_error(ctx, GBPE_E_INVALID, "corpus too large for one device (%llu symbols)", (unsigned long long)n);
+    auto* t = new (std::nothrow) gbpe_trainer();
+    if (!t) return gbpe_set_error(ctx, GBPE_E_OOM, "host allocation failed");
+    t->ctx = ctx;
+    t->flags = opts->flags;
+    t->batch = opts->batch_size ? opts->batch_size : GBPE_BATCH_SIZE;
+    const uint32_t vocab_size = opts->vocab_size ? opts->vocab_size : 256u;
+    const uint32_t next_id = opts->next_token_id ? opts->next_token_id : 256u;
+    t->needed = opts->target_vocab_size > vocab_size ? opts->target_vocab_size - vocab_size : 0u;
+    // u16 symbols when every id the run can produce fits in 15 bits
+    const uint64_t max_id = (uint64_t)next_id + t->needed;    // exclusive
+    t->u16 = max_id <= 0x8000ull;
+    t->bps = t->u16 ? 2 : 4;
+    t->n0 = n;
+    t->n = (uint32_t)n;
+    hipStream_t s = ctx->stream;
+    auto fail = [&](int code) {
+        gbpe_trainer_destroy(t);
+        return code;
+    };
+    // buffers padded to whole tiles (+1 tile for the halo / next-word reads)
+    const uint64_t ntiles0 = gbpe_div_up(n, TILE);
+    t->cap_syms = (ntiles0 + 1) * TILE;
+    for (int k = 0; k < 2; ++k) {
+        if (hipMalloc(&t->buf[k], t->cap_syms * t->bps) != hipSuccess)
+            return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(symbols) failed"));
+        // both ping-pong buffers start zeroed, as WebGPU zero-initialises buffers
+        if (hipMemsetAsync(t->buf[k], 0, t->cap_syms * t->bps, s) != hipSuccess)
+            return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "memset failed"));
+    }
+    // pair table
+    uint32_t lg = opts->table_log2;
+    if (lg == 0) {
+        lg = 22;
+        if (n > (64ull << 20)) lg = 23;
+        if (n > (512ull << 20)) lg = 24;
+    }
+    if (lg < BLK_LOG2 + 1) lg = BLK_LOG2 + 1;
+    if (lg > 28) lg = 28;
+    t->table_log2 = lg;
+    const uint64_t slots = 1ull << lg;
+    t->tb.mask = (uint32_t)(slots - 1);
+    t->tb.nblk = (uint32_t)(slots >> BLK_LOG2);
+    if (hipMalloc(&t->tb.slots, slots * sizeof(uint2)) != hipSuccess ||
+        hipMalloc(&t->tb.bmax, t->tb.nblk * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&t->tb.dirty, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->tb.dlist, (t->tb.nblk + 1) * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->hitmask, (ntiles0 + 1) * TPB * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc(&t->tile_cnt, (ntiles0 + 1) * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->st, sizeof(DevState)) != hipSuccess ||
+        hipMalloc(&t->d_log, (size_t)t->batch * 4 * sizeof(uint32_t)) != hipSuccess)
+        return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(training buffers) failed"));
+    if (hipHostMalloc((void**)&t->h_st, sizeof(DevState), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&t->h_log, (size_t)t->batch * 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+        return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipHostMalloc failed"));
+    if (hipMemsetAsync(t->tb.dirty, 0, t->tb.nblk * sizeof(uint32_t), s) != hipSuccess ||
+        hipMemsetAsync(t->hitmask, 0, (ntiles0 + 1) * TPB * sizeof(uint16_t), s) != hipSuccess)
+        return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "memset failed"));
+    DevState init{};
+    init.n = (uint32_t)n;
+    init.next_id = next_id;
+    memcpy(t->h_st, &init, sizeof(init));
+    if (hipMemcpyAsync(t->st, t->h_st, sizeof(DevState), hipMemcpyHostToDevice, s) != hipSuccess)
+        return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "state upload failed"));
+    // symbols: bytes (+ mask) → S with word-start bit; input may be host or device resident
+    const uint8_t* d_bytes = bytes;
+    const uint8_t* d_ws = word_starts;
+    void* tmp = nullptr;
+    if (!input_on_device) {
+        const uint64_t need = n * (word_starts ? 2 : 1);
+        if (hipMalloc(&tmp, need) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(input) failed"));
+        if (hipMemcpyAsync(tmp, bytes, n, hipMemcpyHostToDevice, s) != hipSuccess ||
+            (word_starts && hipMemcpyAsync((uint8_t*)tmp + n, word_starts, n, hipMemcpyHostToDevice, s) != hipSuccess)) {
+            hipFree(tmp);
+            return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "input upload failed"));
+        }
+        d_bytes = (const uint8_t*)tmp;
+        d_ws = word_starts ? (const uint8_t*)tmp + n : nullptr;
+    }
+    const uint32_t gb = (uint32_t)gbpe_div_up(n, TPB);
+    if (t->u16)
+        hipLaunchKernelGGL(k_symbols<uint16_t>, dim3(gb), dim3(TPB), 0, s, d_bytes, d_ws, (uint16_t*)t->buf[0], n,
+                           (uint8_t*)nullptr);
+    else
+        hipLaunchKernelGGL(k_symbols<uint32_t>, dim3(gb), dim3(TPB), 0, s, d_bytes, d_ws, (uint32_t*)t->buf[0], n,
+                           (uint8_t*)nullptr);
+    if (hipGetLastError() != hipSuccess) {
+        if (tmp) hipFree(tmp);
+        return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "symbol kernel launch failed"));
+    }
+    int rc = table_rebuild(t);
+    if (tmp) {
+        hipStreamSynchronize(s);
+        hipFree(tmp);
+    }
+    if (rc != GBPE_OK) return fail(rc);
+    if (t->flags & GBPE_TRAIN_TIMING) {
+        t->evs.resize(5 * t->batch);
+        for (auto& e : t->evs)
+            if (hipEventCreate(&e) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "hipEventCreate failed"));
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "trainer init failed"));
+    *out = t;
+    return GBPE_OK;
+}
+
+extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out, uint32_t* n_done,
+                                 uint32_t* early_stop) {
+    if (!t) return GBPE_E_INVALID;
+    if (n_done) *n_done = 0;
+    if (early_stop) *early_stop = t->stop ? 1u : 0u;
+    uint32_t k = max_merges ? max_merges : t->batch;
+    if (k > t->batch) k = t->batch;
+    if (t->done + k > t->needed) k = t->needed - t->done;
+    if (t->stop || k == 0) return GBPE_OK;
+    hipStream_t s = t->ctx->stream;
+    // rebuild the pair table when it gets crowded (dead pairs accumulate)
+    const uint64_t slots = (uint64_t)t->tb.mask + 1;
+    if ((uint64_t)t->h_st->used * 2 > slots) {
+        int rc = table_rebuild(t);
+        if (rc != GBPE_OK) return rc;
+    }
+    // reset the per-step counter + budget (trainer.js:239)
+    DevState* hs = t->h_st;
+    hs->merges_done = 0;
+    hs->budget = k;
+    TR_HIP(t, hipMemcpyAsync(&t->st->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(&t->st->budget, &hs->budget, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    const uint64_t ntiles = gbpe_div_up(t->n, TILE);
+    const uint32_t g_delta = grid_persistent(t->ctx, ntiles, 4);
+    const uint32_t g_compact = (uint32_t)(ntiles ? ntiles : 1);
+    const uint32_t g_tail = grid_persistent(t->ctx, gbpe_div_up(t->n / 2 + 1, TPB * 8), 2);
+    const uint32_t g_refresh = grid_persistent(t->ctx, t->tb.nblk, 4);
+    const bool timing = (t->flags & GBPE_TRAIN_TIMING) != 0;
+    for (uint32_t r = 0; r < k; ++r) {
+        hipEvent_t* ev = timing ? &t->evs[5 * r] : nullptr;
+        int rc = t->u16 ? launch_merge<uint16_t>(t, r, s, g_delta, g_compact, g_tail, g_refresh, timing, ev)
+                        : launch_merge<uint32_t>(t, r, s, g_delta, g_compact, g_tail, g_refresh, timing, ev);
+        if (rc != GBPE_OK) return rc;
+    }
+    TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipMemcpyAsync(t->h_log, t->d_log, (size_t)k * 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    const uint32_t done = hs->merges_done;
+    if (hs->err) {
+        return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "training invariant violated (err=0x%x: %s%s%s)", hs->err,
+                              (hs->err & ERR_TABLE_FULL) ? "pair table full " : "",
+                              (hs->err & ERR_COUNT_MISMATCH) ? "survivor count mismatch " : "",
+                              (hs->err & ERR_PAIR_MISSING) ? "selected pair missing" : "");
+    }
+    if (timing) {
+        for (uint32_t r = 0; r < done; ++r) {
+            float a = 0, b = 0, c = 0;
+            hipEvent_t* ev = &t->evs[5 * r];
+            hipEventElapsedTime(&a, ev[0], ev[1]);
+            hipEventElapsedTime(&b, ev[1], ev[2]);
+            hipEventElapsedTime(&c, ev[2], ev[4]);
+            t->ms_select += a;
+            t->ms_merge += b;
+            t->ms_other += c;
+        }
+        t->timed_merges += done;
+    }
+    // algorithmic stream bytes: s * (2 N_i + N_{i+1})
+    uint64_t N = t->n;
+    for (uint32_t r = 0; r < done; ++r) {
+        const uint64_t mc = t->h_log[r * 4 + 3];
+        t->bytes_moved += (uint64_t)t->bps * (2 * N + (N - mc));
+        N -= mc;
+        if (merges_out) memcpy(merges_out + 4 * r, t->h_log + 4 * r, 4 * sizeof(uint32_t));
+    }
+    t->n = hs->n;
+    if (N != t->n) return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "host/device symbol count disagree");
+    t->cur ^= (done & 1u);
+    t->done += done;
+    t->stop = hs->stop != 0;
+    if (n_done) *n_done = done;
+    if (early_stop) *early_stop = t->stop ? 1u : 0u;
+    return GBPE_OK;
+}
+
+extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
+    if (!t || !o) return GBPE_E_INVALID;
+    memset(o, 0, sizeof(*o));
+    o->symbol_count = t->n;
+    o->merges_done = t->done;
+    o->stream_bytes_moved = t->bytes_moved;
+    o->tail_dropped = t->h_st->tail_total;
+    o->table_slots = (uint64_t)t->tb.mask + 1;
+    o->table_used = t->h_st->used;
+    o->bytes_per_symbol = t->bps;
+    o->early_stop = t->stop;
+    o->ms_merge = t->ms_merge;
+    o->ms_select = t->ms_select;
+    o->ms_other = t->ms_other;
+    o->timed_merges = t->timed_merges;
+    o->live_pairs = t->h_st->live;
+    o->max_live_pairs = t->h_st->max_live;
+    return GBPE_OK;
+}
+
+extern "C" int gbpe_trainer_symbols(gbpe_trainer* t, uint32_t* out, uint64_t cap, uint64_t* n) {
+    if (!t || !n) return GBPE_E_INVALID;
+    *n = t->n;
+    if (!out) return GBPE_OK;
+    if (cap < t->n) return gbpe_set_error(t->ctx, GBPE_E_CAPACITY, "symbols: need %u", t->n);
+    hipStream_t s = t->ctx->stream;
+    uint32_t* d = nullptr;
+    TR_HIP(t, hipMalloc(&d, (uint64_t)t->n * 4 + 4));
+    const uint32_t g = (uint32_t)gbpe_div_up(t->n, 256);
+    if (t->n) {
+        if (t->u16)
+            hipLaunchKernelGGL(k_export_symbols<uint16_t>, dim3(g), dim3(256), 0, s, (const uint16_t*)t->buf[t->cur], d,
+                               (uint64_t)t->n);
+        else
+            hipLaunchKernelGGL(k_export_symbols<uint32_t>, dim3(g), dim3(256), 0, s, (const uint32_t*)t->buf[t->cur], d,
+                               (uint64_t)t->n);
+    }
+    hipError_t e = hipMemcpyAsync(out, d, (uint64_t)t->n * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipFree(d);
+    if (e != hipSuccess) return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "symbol export failed: %s", hipGetErrorString(e));
+    return GBPE_OK;
+}
+
+extern "C" int gbpe_trainer_pair_counts(gbpe_trainer* t, uint32_t* pids, uint32_t* counts, uint64_t cap, uint64_t* n) {
+    if (!t || !n) return GBPE_E_INVALID;
+    hipStream_t s = t->ctx->stream;
+    uint32_t* d = nullptr;
+    const uint64_t c = cap ? cap : 1;
+    TR_HIP(t, hipMalloc(&d, (2 * c + 1) * sizeof(uint32_t)));
+    hipError_t e = hipMemsetAsync(d, 0, sizeof(uint32_t), s);
+    const uint64_t slots = (uint64_t)t->tb.mask + 1;
+    hipLaunchKernelGGL(k_dump_pairs, dim3((uint32_t)gbpe_div_up(slots, 256)), dim3(256), 0, s, t->tb, d + 1, d + 1 + c,
+                       d, (uint32_t)cap);
+    uint32_t cnt = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&cnt, d, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess && cnt <= cap && cap) {
+        e = hipMemcpy(pids, d + 1, (uint64_t)cnt * 4, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(counts, d + 1 + c, (uint64_t)cnt * 4, hipMemcpyDeviceToHost);
+    }
+    hipFree(d);
+    if (e != hipSuccess) return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "pair dump failed: %s", hipGetErrorString(e));
+    *n = cnt;
+    if (cnt > cap) return gbpe_set_error(t->ctx, GBPE_E_CAPACITY, "pair dump: need %u", cnt);
+    return GBPE_OK;
+}
+
+extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
+    if (!t) return;
+    if (t->ctx && t->ctx->stream) hipStreamSynchronize(t->ctx->stream);
+    for (auto& e : t->evs)
+        if (e) hipEventDestroy(e);
+    hipFree(t->buf[0]);
+    hipFree(t->buf[1]);
+    hipFree(t->tb.slots);
+    hipFree(t->tb.bmax);
+    hipFree(t->tb.dirty);
+    hipFree(t->tb.dlist);
+    hipFree(t->tb.blive);
+    hipFree(t->hitmask);
+    hipFree(t->tile_cnt);
+    hipFree(t->st);
+    hipFree(t->d_log);
+    if (t->h_st) hipHostFree(t->h_st);
+    if (t->h_log) hipHostFree(t->h_log);
+    delete t;
+}
+
+extern "C" int gbpe_train(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
+                          const gbpe_train_opts* opts, gbpe_progress_cb cb, void* user, uint32_t* merges_out,
+                          uint32_t merges_cap, uint32_t* n_merges, uint32_t* early_stop) {
+    if (n_merges) *n_merges = 0;
+    if (early_stop) *early_stop = 0;
+    gbpe_trainer* t = nullptr;
+    int rc = gbpe_trainer_create(ctx, bytes, n, word_starts, 0, opts, &t);
+    if (rc != GBPE_OK) return rc;
+    std::vector<uint32_t> batch((size_t)t->batch * 4);
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t total = 0;
+    bool stopped = false;
+    while (total < t->needed && !stopped) {
+        uint32_t done = 0, es = 0;
+        rc = gbpe_trainer_step(t, t->batch, batch.data(), &done, &es);
+        if (rc != GBPE_OK) break;
+        for (uint32_t i = 0; i < done; ++i) {
+            if (merges_out && total + i < merges_cap) memcpy(merges_out + 4 * (total + i), &batch[4 * i], 16);
+        }
+        total += done;
+        stopped = es != 0;
+        if (cb) {
+            gbpe_progress p{};
+            p.merge_index = total;
+            p.total_merges = t->needed;
+            p.best_count = done ? batch[4 * (done - 1) + 3] : 0u;
+            p.symbol_count = t->n;
+            p.batch_merges = done;
+            p.early_stop = stopped;
+            p.elapsed_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (cb(&p, batch.data(), user) != 0) {
+                rc = gbpe_set_error(ctx, GBPE_E_CANCELLED, "training cancelled by progress callback");
+                break;
+            }
+        }
+        if (done == 0 && !stopped) break;
+    }
+    if (n_merges) *n_merges = total < merges_cap || !merges_out ? total : merges_cap;
+    if (early_stop) *early_stop = stopped ? 1u : 0u;
+    if (rc == GBPE_OK && merges_out && total > merges_cap)
+        rc = gbpe_set_error(ctx, GBPE_E_CAPACITY, "merges_out too small: need %u", total);
+    gbpe_trainer_destroy(t);
+    return rc;
+}
+
+extern "C" int gbpe_word_boundary(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, uint8_t* ws_out) {
+    if (!ctx || (!bytes && n) || (!ws_out && n)) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
+    if (n == 0) return GBPE_OK;
+    hipStream_t s = ctx->stream;
+    uint8_t* d = nullptr;
+    GBPE_HIP(ctx, hipMalloc(&d, 2 * n));
+    hipError_t e = hipMemcpyAsync(d, bytes, n, hipMemcpyHostToDevice, s);
+    hipLaunchKernelGGL(k_symbols<uint32_t>, dim3((uint32_t)gbpe_div_up(n, TPB)), dim3(TPB), 0, s, d,
+                       (const uint8_t*)nullptr, (uint32_t*)nullptr, n, d + n);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(ws_out, d + n, n, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipFree(d);
+    if (e != hipSuccess) return gbpe_set_error(ctx, GBPE_E_DEVICE, "word boundary failed: %s", hipGetErrorString(e));
+    return GBPE_OK;
+}

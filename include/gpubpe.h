@@ -1,0 +1,178 @@
+/*
+ * gpubpe.h — C-ABI of the MI355X-native BPE train + trie-encode engine.
+ *
+ * This is the drop-in boundary for the reference's WebGPU device layer
+ * (toprakdeviren/gpu-bpe: src/bpe/engine.js + the WGSL kernels in
+ * src/bpe/train.wgsl and src/bpe/tokenizer/tokenize.wgsl).  A host binding
+ * (the Node N-API addon in gpu-bpe_amd/js/, the Python ctypes binding in
+ * gpu-bpe_amd/gpubpe/) wraps these entry points and keeps the reference's
+ * JavaScript API (BPEEngine / BPETrainer / TrieTokenizer).
+ *
+ * Conventions
+ *  - Plain C types only; no HIP or torch types cross the boundary.
+ *  - Every function returns an int status (GBPE_OK = 0, negatives = errors);
+ *    gbpe_last_error(ctx) returns a message for the last failure on ctx.
+ *  - The caller owns every host buffer; buffers are borrowed for the call
+ *    and never retained.  The library owns and pools device memory.
+ *  - A context is bound to one HIP device and one stream; it is not
+ *    re-entrant (one thread at a time), like the reference's single queue.
+ *  - Symbols in and out use the reference layout: u32, bits[15:0] = token
+ *    id, bit 16 = word start (train.wgsl:36-37).
+ */
+#ifndef GPUBPE_H
+#define GPUBPE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GBPE_ABI_VERSION 1
+
+/* status codes */
+#define GBPE_OK            0
+#define GBPE_E_INVALID    -1   /* bad argument */
+#define GBPE_E_OOM        -2   /* device or host allocation failed */
+#define GBPE_E_DEVICE     -3   /* HIP runtime / kernel failure */
+#define GBPE_E_CAPACITY   -4   /* output buffer too small; required size returned */
+#define GBPE_E_CANCELLED  -5   /* progress callback returned non-zero */
+#define GBPE_E_EMPTY      -6   /* empty corpus (trainer.js:161-163) */
+#define GBPE_E_INTERNAL   -7   /* invariant violated (reported, never silent) */
+
+/* reference constants (engine.js:10-13, training-pipeline.js:13) */
+#define GBPE_WORKGROUP_SIZE   256u
+#define GBPE_TABLE_SIZE       2097152u
+#define GBPE_INVALID_TOKEN    0xFFFFFFFFu
+#define GBPE_BATCH_SIZE       128u
+#define GBPE_WORD_START_BIT   0x10000u
+
+typedef struct gbpe_ctx gbpe_ctx;
+typedef struct gbpe_trainer gbpe_trainer;
+typedef struct gbpe_trie gbpe_trie;
+
+/* ── context / device (replaces engine.js:143-177 requestGPUDevice and
+ *    engine.js:216-238 BPEEngine.init) ─────────────────────────────────── */
+int  gbpe_ctx_create(int device_ordinal, gbpe_ctx** out);
+void gbpe_ctx_destroy(gbpe_ctx* ctx);
+/* engine.js:207-210 `limits.maxBufferSize` (used by tokenizer.js:181 for
+ * multi-pass slicing).  This engine has no per-buffer cap below HBM size. */
+int  gbpe_ctx_limits(gbpe_ctx* ctx, uint64_t* max_buffer_size);
+const char* gbpe_last_error(const gbpe_ctx* ctx);
+const char* gbpe_version(void);
+/* number of compiled kernels (engine.js:234 logs Object.keys(pipelines).length) */
+int  gbpe_kernel_count(void);
+const char* gbpe_kernel_name(int i);
+
+/* ── word boundaries (train.wgsl:144-186 bpe_word_boundary) ──────────────
+ * ws_out[i] = 1 if byte i starts a word under the reference byte-class
+ * heuristic. */
+int gbpe_word_boundary(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, uint8_t* ws_out);
+
+/* ── training (replaces trainer.js:149-335 BPETrainer.train over the
+ *    train.wgsl kernels, training-pipeline.js:178-222 encodeBatch) ─────── */
+
+/* Reproduce the reference's compaction exactly (default, 0) or use the
+ * intended compaction.  The reference bounds bpe_finalize_compact_b with
+ * the already-updated symbol count (train.wgsl:605-607, 698, 727) so the
+ * last m slots of each compacted stream keep stale ping-pong contents. */
+#define GBPE_TRAIN_EXACT_COMPACTION  (1u << 0)
+/* record per-kernel device time with HIP events (read via gbpe_trainer_stats) */
+#define GBPE_TRAIN_TIMING            (1u << 1)
+
+typedef struct gbpe_train_opts {
+    uint32_t target_vocab_size;  /* trainer.js:149 targetVocabSize (reference default 4096) */
+    uint32_t vocab_size;         /* Vocab.size before training (256 for a fresh Vocab) */
+    uint32_t next_token_id;      /* Vocab.nextTokenId (trainer.js:191) */
+    uint32_t batch_size;         /* merges per host round trip; 0 = 128 (training-pipeline.js:13) */
+    uint32_t flags;              /* GBPE_TRAIN_* */
+    uint32_t table_log2;         /* pair-table slots = 2^table_log2; 0 = automatic */
+} gbpe_train_opts;
+
+typedef struct gbpe_progress {   /* trainer.js:306-315 onProgress payload */
+    uint32_t merge_index;        /* totalMergesDone */
+    uint32_t total_merges;       /* mergesNeeded */
+    uint32_t best_count;         /* count of the batch's last merge */
+    uint32_t symbol_count;       /* current stream length */
+    uint32_t batch_merges;       /* merges in this batch */
+    uint32_t early_stop;
+    double   elapsed_s;          /* since the loop started (trainer.js:230, 291) */
+} gbpe_progress;
+
+/* Called once per batch with that batch's merges as [a, b, id, count] x
+ * batch_merges.  Return non-zero to cancel (gbpe_train returns
+ * GBPE_E_CANCELLED, merges so far are kept). */
+typedef int (*gbpe_progress_cb)(const gbpe_progress* p, const uint32_t* batch, void* user);
+
+/* One-shot training from host bytes.  word_starts may be NULL (use the
+ * heuristic kernel, trainer.js:177-180) or a byte mask (trainer.js:115-121).
+ * merges_out receives [a, b, id, count] x n_merges (capacity merges_cap).
+ * Returns GBPE_E_EMPTY for n == 0. */
+int gbpe_train(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
+               const gbpe_train_opts* opts, gbpe_progress_cb cb, void* user,
+               uint32_t* merges_out, uint32_t merges_cap, uint32_t* n_merges, uint32_t* early_stop);
+
+/* Stepwise trainer.  With input_on_device != 0, `bytes` (and `word_starts`)
+ * are device pointers already resident in HBM (bench path). */
+int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
+                        int input_on_device, const gbpe_train_opts* opts, gbpe_trainer** out);
+/* Run up to max_merges merges (one host sync).  merges_out may be NULL. */
+int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out,
+                      uint32_t* n_done, uint32_t* early_stop);
+
+typedef struct gbpe_trainer_stats {
+    uint64_t symbol_count;        /* current stream length */
+    uint64_t merges_done;         /* total merges so far */
+    uint64_t stream_bytes_moved;  /* sum over merges of s*(2*N_i + N_{i+1}), s = bytes/symbol */
+    uint64_t tail_dropped;        /* sum of m over merges (reference compaction quirk) */
+    uint64_t live_pairs;          /* distinct pairs with count > 0 (last refresh) */
+    uint64_t table_slots;
+    uint64_t table_used;          /* occupied slots (incl. dead) */
+    uint64_t max_live_pairs;      /* max over merges: > ~1.7M means the reference's 2^21
+                                     table would likely have dropped counts (train.wgsl:422-429) */
+    uint32_t bytes_per_symbol;
+    uint32_t early_stop;
+    double   ms_merge;            /* GBPE_TRAIN_TIMING: device ms in the stream merge kernels */
+    double   ms_select;           /* argmax + table refresh */
+    double   ms_other;            /* tail, rewrite, scan */
+    uint64_t timed_merges;
+} gbpe_trainer_stats;
+int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* out);
+/* Current symbol stream in the reference u32 layout (bit16 = word start). */
+int gbpe_trainer_symbols(gbpe_trainer* t, uint32_t* out, uint64_t cap, uint64_t* n);
+/* Live pair counts (count > 0): pids[i] = a<<16|b.  For parity tests. */
+int gbpe_trainer_pair_counts(gbpe_trainer* t, uint32_t* pids, uint32_t* counts, uint64_t cap, uint64_t* n);
+void gbpe_trainer_destroy(gbpe_trainer* t);
+
+/* ── trie encode (replaces tokenizer.js:54-335 TrieTokenizer over the
+ *    tokenize.wgsl kernels) ─────────────────────────────────────────────── */
+
+/* Upload a parsed trie (trie.js:137-160 parseTrieBuffers output): nodes =
+ * u32 x 3 per node {firstChild, numChildren, tokenId}, edges = u32 x 2 per
+ * edge {symbol, targetNode}.  Replaces tokenizer.js:59-71. */
+int  gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n_nodes,
+                      const uint32_t* edges, uint32_t n_edges, gbpe_trie** out);
+void gbpe_trie_free(gbpe_trie* trie);
+
+/* tokenizer.js:173-206 encodeBytes: chunked greedy longest match.
+ * chunk_size 0 = the reference's adaptive size (tokenizer.js:67-68).
+ * On GBPE_E_CAPACITY *n_out holds the required token count. */
+int gbpe_encode(gbpe_ctx* ctx, gbpe_trie* trie, const uint8_t* bytes, uint64_t n, uint32_t chunk_size,
+                uint32_t* out, uint64_t out_cap, uint64_t* n_out);
+/* Device-resident variant: d_bytes / d_out are device pointers (bench path). */
+int gbpe_encode_device(gbpe_ctx* ctx, gbpe_trie* trie, const void* d_bytes, uint64_t n, uint32_t chunk_size,
+                       void* d_out, uint64_t out_cap, uint64_t* n_out);
+/* device ms of the last encode's kernels (walk, scan, compact) */
+int gbpe_encode_last_timing(gbpe_ctx* ctx, double* ms_walk, double* ms_scan, double* ms_compact);
+
+/* ── device memory helpers for device-resident callers ─────────────────── */
+int gbpe_device_alloc(gbpe_ctx* ctx, uint64_t bytes, void** dptr);
+int gbpe_device_free(gbpe_ctx* ctx, void* dptr);
+int gbpe_memcpy_h2d(gbpe_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+int gbpe_memcpy_d2h(gbpe_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+int gbpe_synchronize(gbpe_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPUBPE_H */

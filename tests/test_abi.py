@@ -1,0 +1,98 @@
+"""CPU-side checks of the boundary and the host logic (no GPU needed).
+
+* libgpubpe.so loads and exports every symbol include/gpubpe.h declares;
+* the host-side Vocab / trie compiler of the product match the reference's
+  own vocab.js / trie.js outputs (tests/golden/ref_modules.json);
+* without a HIP device the API fails loudly (no CPU fallback).
+"""
+import ctypes as C
+import json
+import os
+import re
+
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+HEADER = os.path.join(ROOT, "include", "gpubpe.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b(gbpe_[a-z0-9_]+)\s*\(", src)
+    return sorted(set(n for n in names if not n.endswith("_cb")))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from gpubpe import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    return _lib.load()
+
+
+def test_header_declares_the_boundary():
+    names = _declared_functions()
+    for must in ("gbpe_ctx_create", "gbpe_train", "gbpe_trainer_step", "gbpe_trie_upload", "gbpe_encode",
+                 "gbpe_last_error", "gbpe_word_boundary"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(lib):
+    missing = [n for n in _declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header():
+    from gpubpe import _lib
+    assert set(_declared_functions()) <= set(_lib.EXPORTED)
+
+
+def test_kernel_inventory(lib):
+    n = lib.gbpe_kernel_count()
+    names = [lib.gbpe_kernel_name(i).decode() for i in range(n)]
+    assert "k_delta" in names and "k_trie_walk" in names and len(names) == len(set(names))
+    assert lib.gbpe_version().startswith(b"gpubpe")
+
+
+def test_no_device_fails_loudly(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a HIP device is present")
+    from gpubpe import BPEEngine, _lib
+    with pytest.raises(_lib.GpuBpeError):
+        BPEEngine().init()
+
+
+def test_product_vocab_matches_reference_vocab_js():
+    from gpubpe import Vocab
+    ref = json.load(open(os.path.join(GOLDEN, "ref_modules.json")))
+    for inp, out in zip(ref["inputs"]["vocab_cases"], ref["outputs"]["vocab_cases"]):
+        v = Vocab()
+        ids = [v.add_merge(a, b) for a, b in inp["merges"]]
+        assert ids == out["ids"]
+        assert v.entries == out["entries"] and v.strings == out["strings"]
+        assert v.export() == out["export"]
+
+
+def test_product_trie_matches_reference_trie_js():
+    from gpubpe import compile_vocab_to_trie, parse_header, parse_trie_buffers
+    ref = json.load(open(os.path.join(GOLDEN, "ref_modules.json")))
+    for inp, out in zip(ref["inputs"]["trie_cases"], ref["outputs"]["trie_cases"]):
+        blob = compile_vocab_to_trie(inp["vocab"])
+        assert blob.hex() == out["trie_hex"], inp["name"]
+        h = parse_header(blob)
+        assert h == out["header"]
+        nodes, edges = parse_trie_buffers(blob, h)
+        assert nodes.tolist() == out["nodes"] and edges.tolist() == out["edges"]
+
+
+def test_trie_parse_errors():
+    from gpubpe import parse_header
+    with pytest.raises(ValueError, match="magic"):
+        parse_header(b"\0" * 28)
+    import struct
+    with pytest.raises(ValueError, match="version"):
+        parse_header(struct.pack("<7I", 0x54524945, 9, 0, 0, 0, 0, 0))
