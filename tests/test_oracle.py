@@ -202,3 +202,41 @@ def test_chunked_encode_roundtrip_on_byte_complete_vocab():
     for cs in (1, 7, 512):
         toks = O.encode_chunked(data, nodes, edges, cs)
         assert O.decode(toks, voc) == data
+
+
+# ── C restatement (oracle/bpe_oracle.c) agrees with the numpy restatement ──
+
+def test_c_oracle_matches_numpy_oracle():
+    import cpu_ref
+    import sys, os
+    from gpubpe import synth
+    for kind, size, target in (("english", 40000, 700), ("multilingual", 30000, 500), ("code", 30000, 600)):
+        data = getattr(synth, kind)(size, seed=size % 11)
+        for exact in (False, True):
+            a = O.train(data, target, compaction="exact" if exact else "reference")
+            b = cpu_ref.train(data, target, exact=exact, threads=4)
+            assert b["merges"] == a["merges"], (kind, exact)
+            assert np.array_equal(b["symbols"], a["symbols"]), (kind, exact)
+            assert b["tail_total"] == sum(a["tail_drops"])
+
+
+def test_c_oracle_known_answers(ka):
+    import cpu_ref
+    for c in ka["train"]:
+        r = cpu_ref.train(_text(c), c["target"], threads=2)
+        assert r["merges"] == c["merges"], c["name"]
+        if "final_stream" in c:
+            assert r["symbols"].tolist() == c["final_stream"], c["name"]
+
+
+def test_c_oracle_encode_matches_python():
+    import cpu_ref
+    from gpubpe import synth
+    train = synth.english(20000, seed=2)
+    voc = O.vocab_from_merges(O.train(train, 600, compaction="exact")["merges"]).entries
+    blob = O.compile_vocab_to_trie(voc)
+    nodes, edges = O.parse_trie_buffers(blob, O.parse_header(blob))
+    text = synth.english(30000, seed=3)
+    for cs in (1, 5, 512):
+        assert np.array_equal(cpu_ref.encode(text, nodes, edges, cs, threads=4),
+                              O.encode_chunked(text, nodes, edges, cs))
