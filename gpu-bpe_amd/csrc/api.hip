@@ -23,13 +23,10 @@ int gbpe_set_error(gbpe_ctx* ctx, int code, const char* fmt, ...) {
 static const char* const kKernelNames[] = {
     "k_symbols",         // bpe_word_boundary (train.wgsl:144) + byte widening (trainer.js:49)
     "k_count_full",      // bpe_clear_table + bpe_pair_count_b (train.wgsl:188, 366): initial / rebuild count
-    "k_refresh",         // bpe_find_max_pair4 (train.wgsl:204): per-block maxima of touched blocks
     "k_select",          // bpe_find_max_pair_final_det + bpe_setup_merge (train.wgsl:276, 329)
     "k_delta",           // bpe_merge_reduce_b (train.wgsl:433) + incremental pair-count deltas
-    "k_scan",            // bpe_prefix_sum_scan_blocks_{par,b} (train.wgsl:522, 620)
-    "k_compact",         // bpe_finalize_compact_b (train.wgsl:664) + in-place A-side rewrite
-    "k_tail",            // pairs of the stale tail window left by the reference compaction
-    "k_finish",          // state.symbol_count update (train.wgsl:605-607)
+    "k_compact",         // bpe_prefix_sum_scan_blocks_* + bpe_finalize_compact_b (train.wgsl:522-731) + stale-tail pairs
+    "k_refresh",         // bpe_find_max_pair4 (train.wgsl:204) on touched blocks + symbol_count update
     "k_trie_walk",       // trie_tokenizer_chunked (tokenize.wgsl:88)
     "k_chunk_scan",      // trie_prefix_sum (tokenize.wgsl:199)
     "k_chunk_compact",   // trie_tokenizer_compact (tokenize.wgsl:225)

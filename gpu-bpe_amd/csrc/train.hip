@@ -14,12 +14,13 @@
 //     recomputed for blocks a merge touched, then one workgroup reduces them
 //     with the reference's tie-break (higher count, then smaller a<<16|b,
 //     train.wgsl:83-85);
-//   * the stream pass is two streaming kernels: k_delta (reads the stream,
-//     writes a 1-bit "merge site" mask + per-tile survivor counts + deltas),
-//     k_compact (reads the stream + mask, rewrites merged symbols in place
-//     and scatters survivors into the ping-pong buffer).  Race-free snapshot
-//     semantics (train.wgsl:476) fall out because k_compact never reads a
-//     neighbour;
+//   * the stream pass is two streaming kernels over 4096-symbol tiles:
+//     k_delta (reads the stream; writes a 1-bit merge-site mask, per-tile
+//     survivor counts and count deltas) and k_compact (reads stream + mask,
+//     rewrites merged symbols in place, scatters survivors into the
+//     ping-pong buffer at a two-level tile prefix).  k_compact never reads a
+//     neighbour symbol, so snapshot semantics (train.wgsl:476) hold without
+//     the reference's race;
 //   * symbols are u16 (bit 15 = word start) whenever every token id fits in
 //     15 bits (vocab <= 32768), else u32 with bit 16 (train.wgsl:36-37), so
 //     the common 32K-vocab case moves half the bytes.
@@ -27,8 +28,10 @@
 // The reference's compaction quirk (bpe_finalize_compact_b bounded by the
 // NEW symbol count, train.wgsl:605-607 + 698/727) is reproduced by default:
 // survivors whose old index is >= the new count are not scattered and the
-// stale ping-pong contents stay in the stream.  k_tail adds the pairs of
-// that stale window to the count table.
+// stale ping-pong contents stay in the stream; k_compact's tail blocks add
+// the pairs of that stale window to the count table.
+//
+// Per merge: k_select (1 WG) → k_delta → k_compact (tiles + tail) → k_refresh.
 
 #include "common.h"
 
@@ -40,7 +43,7 @@ namespace {
 constexpr int TPB = 256;              // threads per block
 constexpr int EPT = 16;               // symbols per thread in a tile
 constexpr int TILE = TPB * EPT;       // 4096 symbols per tile
-constexpr int LTAB = 2048;            // LDS delta table slots (k_delta / k_tail)
+constexpr int LTAB = 2048;            // LDS delta table slots (tail window)
 constexpr int LTAB_FULL = 8192;       // LDS table slots for the full recount
 constexpr int LPROBE = 24;            // LDS probes before spilling to the global table
 constexpr uint32_t BLK_LOG2 = 11;     // 2048 table slots per argmax block
@@ -63,16 +66,19 @@ struct DevState {
     uint32_t used;         // occupied table slots
     uint32_t ndirty;       // dirty-block list length
     uint32_t err;          // error bits
-    uint32_t valid_total;  // survivors counted by k_delta (must equal new_n)
+    uint32_t valid_total;  // (unused)
     uint32_t budget;       // merges allowed in this step
     uint32_t live;         // distinct pairs with count > 0 at the last select
     uint64_t tail_total;   // sum of m
     uint32_t max_live;     // max of `live` over all selects
-    uint32_t pad[11];
+    uint32_t ticket;       // tile tickets handed out in this merge (look-back order)
+    uint32_t epoch;        // merge sequence number tagging look-back granules
+    uint32_t rw_count;     // deferred in-place A-side rewrites of this merge
+    uint32_t pad[8];
 };
 static_assert(sizeof(DevState) <= 128, "state");
 
-enum : uint32_t { ERR_TABLE_FULL = 1, ERR_COUNT_MISMATCH = 2, ERR_PAIR_MISSING = 4 };
+enum : uint32_t { ERR_TABLE_FULL = 1, ERR_COUNT_MISMATCH = 2, ERR_PAIR_MISSING = 4, ERR_SPIN = 8 };
 
 struct Table {
     uint2* slots;      // .x = pid (0 = empty), .y = count (u32, wraps for transient negatives)
@@ -236,10 +242,21 @@ __global__ __launch_bounds__(TPB) void k_count_full(DevState* st, const S* __res
     lds_flush(lt, tb, st);
 }
 
-// recompute block maxima for dirty blocks
-__global__ __launch_bounds__(TPB) void k_refresh(DevState* st, Table tb) {
+// recompute block maxima for dirty blocks; with `finish`, also closes the
+// merge of `round` (state.symbol_count := new count, train.wgsl:605-607)
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, int finish, Table tb, S* __restrict__ cur,
+                                                 const uint32_t* __restrict__ rwlist) {
     __shared__ uint64_t red[TPB / 64];
     __shared__ uint32_t rlive[TPB / 64];
+    (void)cur;
+    (void)rwlist;
+    if (finish && !st->stop && st->merges_done == round + 1u) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->tail_total += st->m;
+            st->n = st->new_n;
+        }
+    }
     const uint32_t nd = st->ndirty;
     for (uint32_t j = blockIdx.x; j < nd; j += gridDim.x) {
         const uint32_t blk = tb.dlist[j];
@@ -277,11 +294,18 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, Table tb) {
     }
 }
 
+constexpr uint32_t GRP = 64;    // tiles per group sum (two-level tile prefix)
+
 // argmax over block maxima + the reference's bpe_setup_merge (train.wgsl:340-364)
-__global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, uint32_t* __restrict__ log) {
+__global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, uint32_t* __restrict__ log,
+                                                        uint32_t* __restrict__ grpsum) {
     __shared__ uint64_t red[SEL_THREADS / 64];
     __shared__ uint32_t rlive[SEL_THREADS / 64];
     if (st->stop) return;
+    {   // group sums of the coming stream pass start at zero
+        const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(st->n, TILE), GRP);
+        for (uint32_t g = threadIdx.x; g < ngrp; g += SEL_THREADS) grpsum[g] = 0u;
+    }
     uint64_t best = 0;
     uint32_t live = 0;
     for (uint32_t i = threadIdx.x; i < tb.nblk; i += SEL_THREADS) {
@@ -309,6 +333,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
     st->ndirty = 0u;
     st->m = 0u;
     st->valid_total = 0u;
+    st->ticket = 0u;
+    st->rw_count = 0u;
     const uint32_t mc = (uint32_t)(best >> 32);
     const uint32_t pid = ~(uint32_t)best;
     if (st->merges_done >= st->budget) {   // host asked for fewer merges this step
@@ -339,6 +365,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
     st->mc = mc;
     st->new_n = st->n - mc;
     st->next_id += 1u;
+    st->epoch += 1u;
     st->merges_done = d + 1u;
 }
 
@@ -347,233 +374,284 @@ __device__ __forceinline__ bool merge_active(const DevState* st, uint32_t round)
     return !st->stop && st->merges_done == round + 1u;
 }
 
-// Pass 1: merge-site mask, survivor counts per tile, count deltas.
+template <typename S>
+__device__ __forceinline__ void load_own(const S* __restrict__ cur, uint64_t i0, uint32_t* __restrict__ x) {
+    constexpr int V = EPT * sizeof(S) / 16;
+    uint4 v[V];
+    const uint4* src = reinterpret_cast<const uint4*>(cur + i0);
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = src[k];
+    const S* e = reinterpret_cast<const S*>(v);
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) x[k] = e[k];
+}
+
+constexpr int LTAB_T = 1024;          // per-tile LDS delta table of k_delta
+
+// Pass 1 (one tile of TILE symbols per workgroup): merge-site mask, survivor
+// count per tile, count deltas.
 //   hit(i)  = (i >= 1) && !ws(i) && tok(i-1) == a && tok(i) == b     (B-side, train.wgsl:491-497)
 //   rw(i)   = hit(i+1)                                               (A-side, train.wgsl:482-485)
-//   valid   = !hit(i)
-// Old pair at i is destroyed iff hit(i-1)|hit(i)|hit(i+1) or i >= new_n (tail).
-// New pair at a survivor i < new_n with predecessor u:
-//   hit(i-1): u's token is `nw` (run head / A-side of the previous site)
-//   else if hit(i+1): (tok(i-1), nw)
+//   survivor(i) = !hit(i)
+// Old pair at i is destroyed iff hit(i-1)|hit(i)|hit(i+1) or i >= limit (stale tail);
+// new pair at a survivor i < limit: hit(i-1) → (nw, tok'(i)); else hit(i+1) → (tok(i-1), nw).
+// Symbols live in registers (16 per lane); the 2-before / 1-after halo comes from
+// neighbouring lanes by shuffles, wave edges from global (L1/L2 hits).  A lane with
+// no site within reach and no tail element takes the fast path (no delta work).
 template <typename S, bool EXACT>
 __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, const S* __restrict__ cur, Table tb,
-                                               uint16_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt) {
+                                               uint16_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
+                                               uint32_t* __restrict__ grpsum) {
     if (!merge_active(st, round)) return;
-    __shared__ LdsTab<LTAB> lt;
-    __shared__ __attribute__((aligned(16))) S tile[TILE];
-    __shared__ S halo[3];
-    __shared__ uint32_t red[TPB / 64];
-    lds_clear(lt);
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
-    const uint32_t n = st->n, new_n = st->new_n, a = st->a, b = st->b, nw = st->nw;
-    const uint32_t pid_ab = (a << 16) | b;
-    // reference compaction: survivors at old index >= new_n fall in the stale tail window
-    const uint32_t lim = EXACT ? 0xFFFFFFFFu : new_n;
+    const uint32_t n = st->n;
+    const uint32_t tl = blockIdx.x;
     const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
-    uint32_t my_valid = 0, my_tail = 0;
-    for (uint32_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
-        const uint64_t base = (uint64_t)tl * TILE;
-        __syncthreads();
-        load_tile(cur, base, tile);
-        if (threadIdx.x < 3) {
-            int64_t j = threadIdx.x < 2 ? (int64_t)base - 2 + threadIdx.x : (int64_t)base + TILE;
-            halo[threadIdx.x] = (j >= 0 && (uint64_t)j < n) ? cur[j] : (S)0;
+    if (tl >= ntiles) return;
+    __shared__ LdsTab<LTAB_T> lt;
+    __shared__ uint32_t red[TPB / 64];
+    const int t = threadIdx.x, lane = t & 63;
+    const uint32_t new_n = st->new_n, a = st->a, b = st->b, nw = st->nw;
+    const uint32_t pid_ab = (a << 16) | b;
+    const uint32_t lim = EXACT ? 0xFFFFFFFFu : new_n;
+    const uint64_t base = (uint64_t)tl * TILE;
+    const uint64_t i0 = base + (uint64_t)t * EPT;
+    // own 16 symbols + the 2 before (one aligned word) + the 1 after: all loads in
+    // flight together (the halo words hit the same cache lines as the tile)
+    uint32_t w[EPT + 3];
+    uint32_t lh = 0, rh = 0;
+    if (sizeof(S) == 2) {
+        if (i0 >= 2) lh = *reinterpret_cast<const uint32_t*>(cur + i0 - 2);
+    } else {
+        if (i0 >= 2) {
+            const uint2 v2 = *reinterpret_cast<const uint2*>(cur + i0 - 2);
+            lh = v2.x;
+            rh = v2.y;   // temporarily holds element i0-1
         }
+    }
+    const uint32_t nxr = (uint32_t)cur[i0 + EPT];   // padded buffers: always in bounds
+    load_own(cur, i0, w + 2);
+    if (sizeof(S) == 2) {
+        w[0] = lh & 0xFFFFu;
+        w[1] = lh >> 16;
+    } else {
+        w[0] = lh;
+        w[1] = rh;
+    }
+    if (i0 == 1) w[1] = 0;   // unreachable (i0 % 16 == 0); keeps the intent explicit
+    if (i0 < 2) {
+        w[0] = 0;
+        w[1] = i0 >= 1 ? (uint32_t)cur[i0 - 1] : 0u;
+    }
+    w[EPT + 2] = (i0 + EPT < n) ? nxr : 0u;
+    uint32_t hbits = 0;   // bit k = hit(i0 - 1 + k), k = 0..EPT+1
+#pragma unroll
+    for (int k = 0; k < EPT + 2; ++k) {
+        const uint64_t j1 = i0 + k;
+        const bool h = (j1 >= 2) && (j1 - 1 < n) && !(w[k + 1] & WS) && ((w[k] & TM) == a) && ((w[k + 1] & TM) == b);
+        hbits |= (uint32_t)h << k;
+    }
+    const uint32_t inb = (i0 >= n) ? 0u : (i0 + EPT <= n ? 0xFFFFu : ((1u << (n - i0)) - 1u));
+    const uint32_t hitm = (hbits >> 1) & 0xFFFFu;
+    uint32_t cnt = __popc(inb & ~hitm);
+    uint32_t tail = 0;
+    const bool work = hbits != 0 || (i0 + EPT > lim && i0 < n);
+    if (__syncthreads_or(work)) {   // block-uniform: the delta table is only touched when needed
+        lds_clear(lt);
         __syncthreads();
-        const int t = threadIdx.x;
-        const uint64_t i0 = base + (uint64_t)t * EPT;
-        uint32_t w[EPT + 3];
-        w[0] = t ? (uint32_t)tile[t * EPT - 2] : (uint32_t)halo[0];
-        w[1] = t ? (uint32_t)tile[t * EPT - 1] : (uint32_t)halo[1];
-#pragma unroll
-        for (int k = 0; k < EPT; ++k) w[2 + k] = tile[t * EPT + k];
-        w[EPT + 2] = (t < TPB - 1) ? (uint32_t)tile[t * EPT + EPT] : (uint32_t)halo[2];
-        // hk[k] = hit(i0 - 1 + k), k = 0..EPT+1
-        uint32_t hbits = 0;   // bit k = hk[k]
-#pragma unroll
-        for (int k = 0; k < EPT + 2; ++k) {
-            const uint64_t j1 = i0 + k;   // j + 1
-            bool h = (j1 >= 2) && (j1 - 1 < n) && !(w[k + 1] & WS) && ((w[k] & TM) == a) && ((w[k + 1] & TM) == b);
-            hbits |= (uint32_t)h << k;
-        }
-        hitmask[(uint64_t)tl * TPB + t] = (uint16_t)(hbits >> 1);
-        uint32_t cnt = 0;
+        if (work) {
 #pragma unroll 1
-        for (int k = 0; k < EPT; ++k) {
-            const uint64_t i = i0 + k;
-            if (i >= n) break;
-            const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
-            const uint32_t xp = w[k + 1], xi = w[k + 2];
-            const uint32_t tp = xp & TM, ti = xi & TM;
-            const bool wsi = xi & WS;
-            if (!h0) {
-                ++cnt;
-                if (i >= lim) ++my_tail;
-            }
-            if (i == 0 || wsi) continue;        // no pair ends at i (old or new)
-            if (tp && ti && (hm || h0 || hp || i >= lim)) {
-                const uint32_t pid = (tp << 16) | ti;
-                if (pid != pid_ab) lds_add(lt, tb, st, pid, 0xFFFFFFFFu);
-            }
-            if (!h0 && i < lim) {
-                if (hm) {
-                    const uint32_t t2 = hp ? nw : ti;
-                    if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
-                } else if (hp && tp) {
-                    lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+            for (int k = 0; k < EPT; ++k) {
+                const uint64_t i = i0 + k;
+                if (i >= n) break;
+                const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+                const uint32_t xp = w[k + 1], xi = w[k + 2];
+                const uint32_t tp = xp & TM, ti = xi & TM;
+                if (!h0 && i >= lim) ++tail;
+                if (i == 0 || (xi & WS)) continue;   // no pair ends at i (old or new)
+                if (tp && ti && (hm || h0 || hp || i >= lim)) {
+                    const uint32_t pid = (tp << 16) | ti;
+                    if (pid != pid_ab) lds_add(lt, tb, st, pid, 0xFFFFFFFFu);
+                }
+                if (!h0 && i < lim) {
+                    if (hm) {
+                        const uint32_t t2 = hp ? nw : ti;
+                        if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+                    } else if (hp && tp) {
+                        lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+                    }
                 }
             }
         }
-        my_valid += cnt;
-        // tile survivor count
-        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-        if ((t & 63) == 0) red[t >> 6] = cnt;
-        __syncthreads();
-        if (t == 0) tile_cnt[tl] = red[0] + red[1] + red[2] + red[3];
+        lds_flush(lt, tb, st);
     }
-    lds_flush(lt, tb, st);
     for (int off = 32; off > 0; off >>= 1) {
-        my_valid += __shfl_xor(my_valid, off);
-        my_tail += __shfl_xor(my_tail, off);
+        cnt += __shfl_xor(cnt, off);
+        tail += __shfl_xor(tail, off);
     }
-    if ((threadIdx.x & 63) == 0) {
-        if (my_valid) atomicAdd(&st->valid_total, my_valid);
-        if (my_tail) atomicAdd(&st->m, my_tail);
-    }
-}
-
-// exclusive scan of the per-tile survivor counts (one workgroup)
-__global__ __launch_bounds__(SEL_THREADS) void k_scan(DevState* st, uint32_t round, uint32_t* __restrict__ tile_cnt) {
-    if (!merge_active(st, round)) return;
-    __shared__ uint32_t wsum[SEL_THREADS / 64];
-    const uint32_t ntiles = (uint32_t)gbpe_div_up(st->n, TILE);
-    const uint32_t per = (ntiles + SEL_THREADS - 1) / SEL_THREADS;
-    const uint32_t lo = threadIdx.x * per, hi = min(lo + per, ntiles);
-    uint32_t s = 0;
-    for (uint32_t i = lo; i < hi; ++i) s += tile_cnt[i];
-    // block exclusive scan of s
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t incl = s;
-    for (int off = 1; off < 64; off <<= 1) {
-        uint32_t o = __shfl_up(incl, off);
-        if (lane >= off) incl += o;
-    }
-    if (lane == 63) wsum[wid] = incl;
+    if (lane == 0) red[t >> 6] = cnt;
     __syncthreads();
-    uint32_t wpre = 0;
-    for (int w = 0; w < wid; ++w) wpre += wsum[w];
-    uint32_t run = wpre + incl - s;
-    for (uint32_t i = lo; i < hi; ++i) {
-        uint32_t v = tile_cnt[i];
-        tile_cnt[i] = run;
-        run += v;
-    }
-    if (threadIdx.x == SEL_THREADS - 1) {
-        if (run != st->new_n || st->valid_total != st->new_n) atomicOr(&st->err, ERR_COUNT_MISMATCH);
+    // stores last: none of them is waited on before a barrier
+    if (i0 < n) hitmask[(uint64_t)tl * TPB + t] = (uint16_t)hitm;
+    if (lane == 0 && tail) atomicAdd(&st->m, tail);
+    if (t == 0) {
+        const uint32_t tot = red[0] + red[1] + red[2] + red[3];
+        tile_cnt[tl] = tot;
+        atomicAdd(&grpsum[tl / GRP], tot);
     }
 }
 
-// Pass 2: in-place A-side rewrite + scatter of survivors with old index < new_n
-// (the reference bound, train.wgsl:727) or all survivors (exact compaction).
+// Pass 2.  Blocks [0, ntiles): in-place A-side rewrite (train.wgsl:486-487) +
+// scatter of the survivors with old index < new_n (the reference bound,
+// train.wgsl:727; all of them with EXACT) at tile prefix = group sums + the
+// tile counts of this group before the tile.  Blocks >= ntiles (reference
+// compaction only): the stale tail window [new_n - m, new_n) of the new
+// stream — add its pairs to the count table.
 template <typename S, bool EXACT>
 __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S* __restrict__ cur, S* __restrict__ oth,
                                                  const uint16_t* __restrict__ hitmask,
-                                                 const uint32_t* __restrict__ tile_off) {
+                                                 const uint32_t* __restrict__ tile_cnt,
+                                                 const uint32_t* __restrict__ grpsum, Table tb) {
     if (!merge_active(st, round)) return;
-    __shared__ __attribute__((aligned(16))) S stage[TILE];
-    __shared__ uint32_t wsum[TPB / 64];
-    constexpr uint32_t WS = Sym<S>::WS;
+    // one LDS arena: the compaction stage of tile blocks or the delta table of tail blocks
+    constexpr int ARENA = (sizeof(LdsTab<LTAB>) > (TILE + 16) * sizeof(S) ? sizeof(LdsTab<LTAB>) : (TILE + 16) * sizeof(S)) / 16;
+    __shared__ uint4 arena[ARENA];
+    __shared__ uint32_t wsum[TPB / 64], psum[TPB / 64];
+    S* stage = reinterpret_cast<S*>(arena);
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     const uint32_t n = st->n, new_n = st->new_n, nw = st->nw;
     const uint32_t limit = EXACT ? n : new_n;
     const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    if (blockIdx.x >= ntiles) {
+        if (EXACT) return;
+        // ── stale tail window ──
+        const uint32_t m = st->m;
+        if (m == 0) return;
+        LdsTab<LTAB>& lt = *reinterpret_cast<LdsTab<LTAB>*>(arena);
+        __shared__ uint32_t left_val;
+        lds_clear(lt);
+        const uint32_t lo = new_n - m;
+        const uint32_t tb0 = blockIdx.x - ntiles, ntb = gridDim.x - ntiles;
+        if (tb0 == 0 && wid == 0 && lo >= 1) {
+            // the survivor just before the window: last j < new_n with hit(j) == 0; its
+            // value is the A-side-rewritten symbol (the rewrite is idempotent, so racing
+            // with a tile block's in-place write is harmless)
+            int64_t wi = (int64_t)(new_n - 1) / EPT;
+            uint32_t found = 0xFFFFFFFFu;
+            while (wi >= 0 && found == 0xFFFFFFFFu) {
+                const int64_t mywi = wi - lane;
+                uint32_t word = 0xFFFFu;
+                if (mywi >= 0) {
+                    word = hitmask[mywi];
+                    const uint64_t hi_i = (uint64_t)mywi * EPT + EPT;   // exclusive
+                    if (hi_i > new_n) word |= (0xFFFFu << (EPT - (hi_i - new_n))) & 0xFFFFu;
+                }
+                const uint32_t inv = (~word) & 0xFFFFu;   // survivors
+                const unsigned long long has = __ballot(inv != 0u);
+                if (has) {
+                    const int l = __ffsll((long long)has) - 1;   // lowest lane = largest word index
+                    const uint32_t inv_l = __shfl(inv, l);
+                    found = (uint32_t)((wi - l) * EPT + (31 - __clz(inv_l)));
+                }
+                wi -= 64;
+            }
+            if (lane == 0) {
+                uint32_t v = 0;
+                if (found != 0xFFFFFFFFu) {
+                    v = cur[found];
+                    const bool rw = (found + 1 < n) && ((hitmask[(found + 1) / EPT] >> ((found + 1) % EPT)) & 1u);
+                    if (rw) v = nw | (v & WS);
+                }
+                left_val = v;
+            }
+        }
+        __syncthreads();
+        for (uint32_t d = lo + tb0 * TPB + t; d < new_n; d += ntb * TPB) {
+            if (d == 0) continue;
+            const uint32_t x0 = (d == lo) ? left_val : (uint32_t)oth[d - 1];
+            const uint32_t x1 = oth[d];
+            const uint32_t t0 = x0 & TM, t1 = x1 & TM;
+            if (!(x1 & WS) && t0 && t1) lds_add(lt, tb, st, (t0 << 16) | t1, 1u);
+        }
+        lds_flush(lt, tb, st);
+        return;
+    }
     const uint32_t tl = blockIdx.x;
-    if (tl >= ntiles) return;
-    const int t = threadIdx.x;
     const uint64_t base = (uint64_t)tl * TILE;
     const uint64_t i0 = base + (uint64_t)t * EPT;
-    // own symbols (vector load) + mask bits
-    S x[EPT];
+    // every independent load first: prefix terms, mask words, the tile
+    const uint32_t G = tl / GRP;
+    uint32_t part = 0;
     {
-        constexpr int V = EPT * sizeof(S) / 16;
-        const uint4* src = reinterpret_cast<const uint4*>(cur + i0);
-        uint4 v[V];
-#pragma unroll
-        for (int k = 0; k < V; ++k) v[k] = src[k];
-        memcpy(x, v, sizeof(x));
+        const uint32_t j = G * GRP + t;
+        const uint32_t v0 = (t < (int)GRP && j < tl) ? tile_cnt[j] : 0u;
+        const uint32_t g0 = ((uint32_t)t < G) ? grpsum[t] : 0u;
+        const uint32_t g1 = ((uint32_t)t + TPB < G) ? grpsum[t + TPB] : 0u;
+        part = v0 + g0 + g1;
     }
-    const uint32_t hm = hitmask[(uint64_t)tl * TPB + t];
-    uint32_t nextbit = 0;
-    if (i0 + EPT < n) nextbit = hitmask[(uint64_t)tl * TPB + t + 1] & 1u;   // t+1 may be the next tile's first word
-    const uint32_t rwm = (hm >> 1) | (nextbit << (EPT - 1));
-    uint32_t keep = 0, cnt = 0;
-    bool any_rw = false;
+    const uint32_t hm = i0 < n ? hitmask[(uint64_t)tl * TPB + t] : 0xFFFFu;
+    const uint32_t hn = hitmask[(uint64_t)tl * TPB + t + 1];   // may be the next tile's first word
+    uint32_t x[EPT];
+    load_own(cur, i0, x);
+    for (uint32_t g = t + 2 * TPB; g < G; g += TPB) part += grpsum[g];   // only past 2*TPB groups
+    const uint32_t nextbit = (i0 + EPT < n) ? (hn & 1u) : 0u;
+    const uint32_t inb = (i0 >= n) ? 0u : (i0 + EPT <= n ? 0xFFFFu : ((1u << (n - i0)) - 1u));
+    const uint32_t rwm = ((hm >> 1) | (nextbit << (EPT - 1))) & inb;
+    const uint32_t valid = inb & ~hm;
+    uint32_t keep = valid;
+    if (!EXACT) {
+        if (i0 >= limit) keep = 0;
+        else if (i0 + EPT > limit) keep &= (1u << (limit - i0)) - 1u;
+    }
+    if (rwm) {   // in-place A-side rewrite (train.wgsl:486-487): the reference's ping buffer
 #pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-        const uint64_t i = i0 + k;
-        const bool inb = i < n;
-        const bool valid = inb && !((hm >> k) & 1u);
-        const bool rw = inb && ((rwm >> k) & 1u);
-        if (rw) {
-            x[k] = (S)(nw | ((uint32_t)x[k] & WS));
-            any_rw = true;
+        for (int k = 0; k < EPT; ++k) {
+            if ((rwm >> k) & 1u) {
+                x[k] = nw | (x[k] & WS);
+                cur[i0 + k] = (S)x[k];
+            }
         }
-        if (valid && i < limit) {
-            keep |= 1u << k;
-            ++cnt;
-        }
     }
-    if (any_rw) {   // in-place A-side rewrite (train.wgsl:486-487): the reference's ping buffer
-#pragma unroll
-        for (int k = 0; k < EPT; ++k)
-            if ((rwm >> k) & 1u && i0 + k < n) cur[i0 + k] = x[k];
-    }
-    // block exclusive scan of cnt
-    const int lane = t & 63, wid = t >> 6;
+    const uint32_t cnt = __popc(keep);
+    // block exclusive scan of cnt + block sum of part
     uint32_t incl = cnt;
     for (int off = 1; off < 64; off <<= 1) {
         uint32_t o = __shfl_up(incl, off);
         if (lane >= off) incl += o;
     }
+    for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
     if (lane == 63) wsum[wid] = incl;
+    if (lane == 0) psum[wid] = part;
     __syncthreads();
     uint32_t pre = incl - cnt;
-    for (int w = 0; w < wid; ++w) pre += wsum[w];
+    for (int w2 = 0; w2 < wid; ++w2) pre += wsum[w2];
     const uint32_t total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    const uint32_t prefix = psum[0] + psum[1] + psum[2] + psum[3];
+    if (tl == ntiles - 1 && t == 0 && prefix + tile_cnt[tl] != new_n) atomicOr(&st->err, ERR_COUNT_MISMATCH);
+    // stage at the destination's alignment phase so both sides move whole 16-byte words
+    constexpr uint32_t VE = 16 / sizeof(S);           // symbols per 16-byte word
+    const uint32_t ph = prefix & (VE - 1);
+    pre += ph;
 #pragma unroll
     for (int k = 0; k < EPT; ++k)
-        if ((keep >> k) & 1u) stage[pre++] = x[k];
+        if ((keep >> k) & 1u) stage[pre++] = (S)x[k];
     __syncthreads();
-    S* dst = oth + tile_off[tl];
-    for (uint32_t j = t; j < total; j += TPB) dst[j] = stage[j];
-}
-
-// Stale tail window [new_n - m, new_n) of the new stream: add its pairs.
-template <typename S>
-__global__ __launch_bounds__(TPB) void k_tail(DevState* st, uint32_t round, const S* __restrict__ s, Table tb) {
-    if (!merge_active(st, round)) return;
-    const uint32_t m = st->m, new_n = st->new_n;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->tail_total += m;
+    S* dst = oth + (prefix - ph);                      // 16-byte aligned
+    const uint32_t end = ph + total;
+    const uint32_t nvec = end / VE;
+    uint4* dv = reinterpret_cast<uint4*>(dst);
+    const uint4* sv = reinterpret_cast<const uint4*>(stage);
+    for (uint32_t v = t; v < nvec; v += TPB) {
+        if (v == 0 && ph) {
+            for (uint32_t j = ph; j < VE && j < end; ++j) dst[j] = stage[j];   // partial head word
+        } else {
+            dv[v] = sv[v];
+        }
     }
-    if (m == 0) return;
-    __shared__ LdsTab<LTAB> lt;
-    lds_clear(lt);
-    __syncthreads();
-    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
-    const uint32_t lo = new_n - m;
-    for (uint32_t d = lo + blockIdx.x * TPB + threadIdx.x; d < new_n; d += gridDim.x * TPB) {
-        if (d == 0) continue;
-        uint32_t x0 = s[d - 1], x1 = s[d];
-        uint32_t t0 = x0 & TM, t1 = x1 & TM;
-        if (!(x1 & WS) && t0 && t1) lds_add(lt, tb, st, (t0 << 16) | t1, 1u);
+    if (t == 0 && nvec * VE < end) {
+        for (uint32_t j = (nvec * VE > ph ? nvec * VE : ph); j < end; ++j) dst[j] = stage[j];   // partial tail word
     }
-    lds_flush(lt, tb, st);
-}
-
-// finish a merge: the stream length becomes new_n
-__global__ void k_finish(DevState* st, uint32_t round) {
-    if (!merge_active(st, round)) return;
-    st->n = st->new_n;
 }
 
 __global__ void k_clear_dirty_all(DevState* st, Table tb) {
@@ -630,6 +708,10 @@ struct gbpe_trainer {
     uint32_t table_log2 = 22;
     uint16_t* hitmask = nullptr;
     uint32_t* tile_cnt = nullptr;
+    uint32_t* grpsum = nullptr;
+    uint64_t* status = nullptr;    // look-back granules, one per tile
+    uint64_t* tailinfo = nullptr;  // {m, symbol before the stale window}
+    uint32_t* rwlist = nullptr;    // deferred in-place rewrites
     // stats
     uint64_t bytes_moved = 0;
     uint64_t max_live = 0;
@@ -668,37 +750,39 @@ int table_rebuild(gbpe_trainer* t) {
     GBPE_LAUNCH_CHECK(t->ctx);
     hipLaunchKernelGGL(k_clear_dirty_all, dim3(gbpe_div_up(t->tb.nblk, 256)), dim3(256), 0, s, t->st, t->tb);
     GBPE_LAUNCH_CHECK(t->ctx);
-    hipLaunchKernelGGL(k_refresh, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, t->tb);
+    if (t->u16)
+        hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, 0u,
+                           0, t->tb, (uint16_t*)nullptr, (const uint32_t*)nullptr);
+    else
+        hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, 0u,
+                           0, t->tb, (uint32_t*)nullptr, (const uint32_t*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
 }
 
 template <typename S>
 int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delta, uint32_t g_compact,
-                 uint32_t g_tail, uint32_t g_refresh, bool timing, hipEvent_t* ev) {
+                 uint32_t g_refresh, bool timing, hipEvent_t* ev) {
     S* cur = (S*)t->buf[t->cur ^ (round & 1)];
     S* oth = (S*)t->buf[t->cur ^ (round & 1) ^ 1];
+    const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log);
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum);
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
-    if (t->flags & GBPE_TRAIN_EXACT_COMPACTION)
+    if (exact) {
         hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
-                           t->hitmask, t->tile_cnt);
-    else
-        hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
-                           t->hitmask, t->tile_cnt);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(SEL_THREADS), 0, s, t->st, round, t->tile_cnt);
-    if (t->flags & GBPE_TRAIN_EXACT_COMPACTION)
+                           t->hitmask, t->tile_cnt, t->grpsum);
         hipLaunchKernelGGL((k_compact<S, true>), dim3(g_compact), dim3(TPB), 0, s, t->st, round, cur, oth,
-                           (const uint16_t*)t->hitmask, (const uint32_t*)t->tile_cnt);
-    else
+                           (const uint16_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
+    } else {
+        hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
+                           t->hitmask, t->tile_cnt, t->grpsum);
         hipLaunchKernelGGL((k_compact<S, false>), dim3(g_compact), dim3(TPB), 0, s, t->st, round, cur, oth,
-                           (const uint16_t*)t->hitmask, (const uint32_t*)t->tile_cnt);
+                           (const uint16_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
+    }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
-    hipLaunchKernelGGL(k_tail<S>, dim3(g_tail), dim3(TPB), 0, s, t->st, round, (const S*)oth, t->tb);
-    hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, s, t->st, round);
-    if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
-    hipLaunchKernelGGL(k_refresh, dim3(g_refresh), dim3(TPB), 0, s, t->st, t->tb);
+    hipLaunchKernelGGL(k_refresh<S>, dim3(g_refresh), dim3(TPB), 0, s, t->st, round, 1, t->tb, cur,
+                       (const uint32_t*)nullptr);
     if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
@@ -762,6 +846,10 @@ extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t
         hipMalloc(&t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->hitmask, (ntiles0 + 1) * TPB * sizeof(uint16_t)) != hipSuccess ||
         hipMalloc(&t->tile_cnt, (ntiles0 + 1) * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->grpsum, (ntiles0 / GRP + 2) * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->status, (ntiles0 + 2) * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&t->tailinfo, 2 * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&t->rwlist, (n / 2 + 2) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->st, sizeof(DevState)) != hipSuccess ||
         hipMalloc(&t->d_log, (size_t)t->batch * 4 * sizeof(uint32_t)) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(training buffers) failed"));
@@ -769,6 +857,8 @@ extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t
         hipHostMalloc((void**)&t->h_log, (size_t)t->batch * 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipHostMalloc failed"));
     if (hipMemsetAsync(t->tb.dirty, 0, t->tb.nblk * sizeof(uint32_t), s) != hipSuccess ||
+        hipMemsetAsync(t->status, 0, (ntiles0 + 2) * sizeof(uint64_t), s) != hipSuccess ||
+        hipMemsetAsync(t->tailinfo, 0, 2 * sizeof(uint64_t), s) != hipSuccess ||
         hipMemsetAsync(t->hitmask, 0, (ntiles0 + 1) * TPB * sizeof(uint16_t), s) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "memset failed"));
     DevState init{};
@@ -842,15 +932,17 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     TR_HIP(t, hipMemcpyAsync(&t->st->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     TR_HIP(t, hipMemcpyAsync(&t->st->budget, &hs->budget, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     const uint64_t ntiles = gbpe_div_up(t->n, TILE);
-    const uint32_t g_delta = grid_persistent(t->ctx, ntiles, 4);
-    const uint32_t g_compact = (uint32_t)(ntiles ? ntiles : 1);
-    const uint32_t g_tail = grid_persistent(t->ctx, gbpe_div_up(t->n / 2 + 1, TPB * 8), 2);
+    // tile blocks + stale-tail blocks (the window is at most mc <= n/2 symbols)
+    const uint32_t g_tail = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
+                            : grid_persistent(t->ctx, gbpe_div_up(t->n / 2 + 1, TPB * 16), 1);
+    const uint32_t g_delta = (uint32_t)(ntiles ? ntiles : 1);
+    const uint32_t g_compact = (uint32_t)ntiles + g_tail;
     const uint32_t g_refresh = grid_persistent(t->ctx, t->tb.nblk, 4);
     const bool timing = (t->flags & GBPE_TRAIN_TIMING) != 0;
     for (uint32_t r = 0; r < k; ++r) {
         hipEvent_t* ev = timing ? &t->evs[5 * r] : nullptr;
-        int rc = t->u16 ? launch_merge<uint16_t>(t, r, s, g_delta, g_compact, g_tail, g_refresh, timing, ev)
-                        : launch_merge<uint32_t>(t, r, s, g_delta, g_compact, g_tail, g_refresh, timing, ev);
+        int rc = t->u16 ? launch_merge<uint16_t>(t, r, s, g_delta, g_compact, g_refresh, timing, ev)
+                        : launch_merge<uint32_t>(t, r, s, g_delta, g_compact, g_refresh, timing, ev);
         if (rc != GBPE_OK) return rc;
     }
     TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
@@ -976,6 +1068,10 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->tb.blive);
     hipFree(t->hitmask);
     hipFree(t->tile_cnt);
+    hipFree(t->grpsum);
+    hipFree(t->status);
+    hipFree(t->tailinfo);
+    hipFree(t->rwlist);
     hipFree(t->st);
     hipFree(t->d_log);
     if (t->h_st) hipHostFree(t->h_st);
