@@ -1,0 +1,38 @@
+// GPU checks through the N-API addon: BPETrainer / TrieTokenizer results
+// must equal the expectations the CPU oracle produced (argv[2] JSON).
+import fs from 'fs';
+import { BPEEngine, BPETrainer, TrieTokenizer } from '../../gpu-bpe_amd/js/index.js';
+
+const cases = JSON.parse(fs.readFileSync(process.argv[2]));
+function fail(msg) { console.error('FAIL ' + msg); process.exit(1); }
+
+async function main() {
+    const engine = await new BPEEngine().init();
+    if (Object.keys(engine.pipelines).length < 5) fail('pipelines');
+    if (!(engine.limits.maxBufferSize > 0)) fail('limits');
+    let checks = 0;
+    for (const c of cases.train) {
+        const t = new BPETrainer(engine);
+        const bytes = new Uint8Array(Buffer.from(c.b64, 'base64'));
+        let progress = 0;
+        const r = await t.train(bytes, { targetVocabSize: c.target, onProgress: function (p) { progress++; } });
+        if (JSON.stringify(r.merges) !== JSON.stringify(c.merges)) fail('merges ' + c.name);
+        if (r.vocabSize !== 256 + c.merges.length) fail('vocabSize ' + c.name);
+        if (c.merges.length && progress === 0) fail('progress ' + c.name);
+        if (t.exportVocab() !== c.export) fail('export ' + c.name);
+        checks++;
+        const tok = TrieTokenizer.fromVocab(engine, r.vocab, c.chunkSize ? { chunkSize: c.chunkSize } : {});
+        const text = new Uint8Array(Buffer.from(c.text_b64, 'base64'));
+        const ids = await tok.encodeBytes(text);
+        if (JSON.stringify(Array.from(ids)) !== JSON.stringify(c.tokens)) fail('tokens ' + c.name);
+        if (Buffer.compare(Buffer.from(tok.decode(ids)), Buffer.from(text)) !== 0) fail('decode ' + c.name);
+        tok.destroy();
+        checks++;
+    }
+    let threw = false;
+    try { await new BPETrainer(engine).train(new Uint8Array(0)); } catch (e) { threw = /empty/.test(e.message); }
+    if (!threw) fail('empty corpus must throw');
+    engine.destroy();
+    console.log('ok ' + checks + ' checks');
+}
+main().catch(function (e) { fail(e && e.stack || e); });
