@@ -41,8 +41,8 @@
 namespace {
 
 constexpr int TPB = 256;              // threads per block
-constexpr int EPT = 16;               // symbols per thread in a tile
-constexpr int TILE = TPB * EPT;       // 4096 symbols per tile
+constexpr int EPT = 32;               // symbols per thread in a tile
+constexpr int TILE = TPB * EPT;       // 8192 symbols per tile (16 KiB of u16 in flight per workgroup)
 constexpr int LTAB = 2048;            // LDS delta table slots (tail window)
 constexpr int LTAB_FULL = 8192;       // LDS table slots for the full recount
 constexpr int LPROBE = 24;            // LDS probes before spilling to the global table
@@ -90,12 +90,10 @@ struct Table {
     uint32_t nblk;
 };
 
+// a touched block is re-maxed by the next k_refresh: a plain flag store, nothing waits on it
 __device__ __forceinline__ void mark_dirty(const Table& tb, DevState* st, uint32_t slot) {
-    uint32_t blk = slot >> BLK_LOG2;
-    if (atomicExch(&tb.dirty[blk], 1u) == 0u) {
-        uint32_t k = atomicAdd(&st->ndirty, 1u);
-        tb.dlist[k] = blk;
-    }
+    (void)st;
+    tb.dirty[slot >> BLK_LOG2] = 1u;
 }
 
 // global insert-or-add (triangular probing visits every slot of a 2^k table)
@@ -107,7 +105,7 @@ __device__ void table_add(const Table& tb, DevState* st, uint32_t pid, uint32_t 
         if (k == 0u) {
             k = atomicCAS(&tb.slots[idx].x, 0u, pid);
             if (k == 0u) {
-                atomicAdd(&st->used, 1u);
+                __hip_atomic_fetch_add(&st->used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 k = pid;
             }
         }
@@ -257,9 +255,8 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             st->n = st->new_n;
         }
     }
-    const uint32_t nd = st->ndirty;
-    for (uint32_t j = blockIdx.x; j < nd; j += gridDim.x) {
-        const uint32_t blk = tb.dlist[j];
+    for (uint32_t blk = blockIdx.x; blk < tb.nblk; blk += gridDim.x) {
+        if (!tb.dirty[blk]) continue;   // block-uniform
         const uint2* s = tb.slots + ((uint64_t)blk << BLK_LOG2);
         uint64_t best = 0;
         uint32_t live = 0;
@@ -352,8 +349,6 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
     }
     tb.slots[idx].y = 0u;                  // every (a,b) occurrence is a merge site
     tb.dirty[idx >> BLK_LOG2] = 1u;
-    tb.dlist[0] = idx >> BLK_LOG2;
-    st->ndirty = 1u;
     const uint32_t d = st->merges_done;
     log[d * 4 + 0] = pid >> 16;
     log[d * 4 + 1] = pid & 0xFFFFu;
@@ -388,6 +383,11 @@ __device__ __forceinline__ void load_own(const S* __restrict__ cur, uint64_t i0,
 
 constexpr int LTAB_T = 1024;          // per-tile LDS delta table of k_delta
 
+__device__ __forceinline__ uint32_t lane_mask32(uint64_t i0, uint64_t lim) {
+    // bits k with i0 + k < lim, k < 32
+    return i0 >= lim ? 0u : (i0 + 32 <= lim ? 0xFFFFFFFFu : ((1u << (uint32_t)(lim - i0)) - 1u));
+}
+
 // Pass 1 (one tile of TILE symbols per workgroup): merge-site mask, survivor
 // count per tile, count deltas.
 //   hit(i)  = (i >= 1) && !ws(i) && tok(i-1) == a && tok(i) == b     (B-side, train.wgsl:491-497)
@@ -395,42 +395,42 @@ constexpr int LTAB_T = 1024;          // per-tile LDS delta table of k_delta
 //   survivor(i) = !hit(i)
 // Old pair at i is destroyed iff hit(i-1)|hit(i)|hit(i+1) or i >= limit (stale tail);
 // new pair at a survivor i < limit: hit(i-1) → (nw, tok'(i)); else hit(i+1) → (tok(i-1), nw).
-// Symbols live in registers (16 per lane); the 2-before / 1-after halo comes from
-// neighbouring lanes by shuffles, wave edges from global (L1/L2 hits).  A lane with
-// no site within reach and no tail element takes the fast path (no delta work).
+// The tile (32 symbols per lane + the 2 before + 1 after) is loaded before the
+// loop state is read, so the state's scalar load overlaps the HBM latency.  Lanes
+// with no site within reach and no tail element do no delta work; a tile with no
+// such lane passes a single barrier.
 template <typename S, bool EXACT>
 __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, const S* __restrict__ cur, Table tb,
-                                               uint16_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
+                                               uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
                                                uint32_t* __restrict__ grpsum) {
-    if (!merge_active(st, round)) return;
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
-    const uint32_t n = st->n;
+    __shared__ LdsTab<LTAB_T> lt;
+    __shared__ uint32_t red[TPB / 64], s_workw[TPB / 64];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t tl = blockIdx.x;
+    const uint64_t base = (uint64_t)tl * TILE;
+    const uint64_t i0 = base + (uint64_t)t * EPT;
+    // loads first (buffers are padded: every launched tile is in bounds)
+    uint32_t w[EPT + 3];
+    uint32_t lh = 0, rh = 0;
+    if (i0 >= 2) {
+        if (sizeof(S) == 2) {
+            lh = *reinterpret_cast<const uint32_t*>(cur + i0 - 2);
+        } else {
+            const uint2 v2 = *reinterpret_cast<const uint2*>(cur + i0 - 2);
+            lh = v2.x;
+            rh = v2.y;
+        }
+    }
+    const uint32_t nxr = (uint32_t)cur[i0 + EPT];
+    load_own(cur, i0, w + 2);
+    if (!merge_active(st, round)) return;
+    const uint32_t n = st->n;
     const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
     if (tl >= ntiles) return;
-    __shared__ LdsTab<LTAB_T> lt;
-    __shared__ uint32_t red[TPB / 64];
-    const int t = threadIdx.x, lane = t & 63;
     const uint32_t new_n = st->new_n, a = st->a, b = st->b, nw = st->nw;
     const uint32_t pid_ab = (a << 16) | b;
     const uint32_t lim = EXACT ? 0xFFFFFFFFu : new_n;
-    const uint64_t base = (uint64_t)tl * TILE;
-    const uint64_t i0 = base + (uint64_t)t * EPT;
-    // own 16 symbols + the 2 before (one aligned word) + the 1 after: all loads in
-    // flight together (the halo words hit the same cache lines as the tile)
-    uint32_t w[EPT + 3];
-    uint32_t lh = 0, rh = 0;
-    if (sizeof(S) == 2) {
-        if (i0 >= 2) lh = *reinterpret_cast<const uint32_t*>(cur + i0 - 2);
-    } else {
-        if (i0 >= 2) {
-            const uint2 v2 = *reinterpret_cast<const uint2*>(cur + i0 - 2);
-            lh = v2.x;
-            rh = v2.y;   // temporarily holds element i0-1
-        }
-    }
-    const uint32_t nxr = (uint32_t)cur[i0 + EPT];   // padded buffers: always in bounds
-    load_own(cur, i0, w + 2);
     if (sizeof(S) == 2) {
         w[0] = lh & 0xFFFFu;
         w[1] = lh >> 16;
@@ -438,40 +438,53 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
         w[0] = lh;
         w[1] = rh;
     }
-    if (i0 == 1) w[1] = 0;   // unreachable (i0 % 16 == 0); keeps the intent explicit
     if (i0 < 2) {
         w[0] = 0;
-        w[1] = i0 >= 1 ? (uint32_t)cur[i0 - 1] : 0u;
+        w[1] = 0;
     }
     w[EPT + 2] = (i0 + EPT < n) ? nxr : 0u;
-    uint32_t hbits = 0;   // bit k = hit(i0 - 1 + k), k = 0..EPT+1
+    uint64_t hbits = 0;   // bit k = hit(i0 - 1 + k), k = 0..EPT+1
 #pragma unroll
     for (int k = 0; k < EPT + 2; ++k) {
         const uint64_t j1 = i0 + k;
         const bool h = (j1 >= 2) && (j1 - 1 < n) && !(w[k + 1] & WS) && ((w[k] & TM) == a) && ((w[k + 1] & TM) == b);
-        hbits |= (uint32_t)h << k;
+        hbits |= (uint64_t)h << k;
     }
-    const uint32_t inb = (i0 >= n) ? 0u : (i0 + EPT <= n ? 0xFFFFu : ((1u << (n - i0)) - 1u));
-    const uint32_t hitm = (hbits >> 1) & 0xFFFFu;
+    const uint32_t inb = lane_mask32(i0, n);
+    const uint32_t hitm = (uint32_t)(hbits >> 1);
     uint32_t cnt = __popc(inb & ~hitm);
     uint32_t tail = 0;
     const bool work = hbits != 0 || (i0 + EPT > lim && i0 < n);
-    if (__syncthreads_or(work)) {   // block-uniform: the delta table is only touched when needed
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+    const bool wave_work = __any(work);
+    if (lane == 0) {
+        red[wid] = cnt;
+        s_workw[wid] = wave_work;
+    }
+    __syncthreads();
+    if (s_workw[0] | s_workw[1] | s_workw[2] | s_workw[3]) {   // block-uniform: only tiles with a site or a tail element touch the table
         lds_clear(lt);
         __syncthreads();
         if (work) {
-#pragma unroll 1
-            for (int k = 0; k < EPT; ++k) {
+            // only the positions where a pair can change: within one of a site, or in
+            // the stale tail; symbols re-read from the (L1/L2-hot) tile by index so the
+            // register window is never dynamically indexed
+            const uint32_t below = lane_mask32(i0, lim);
+            tail = __popc(inb & ~hitm & ~below);
+            uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2) | ~below) & inb;
+            while (rel) {
+                const int k = __ffs(rel) - 1;
+                rel &= rel - 1;
                 const uint64_t i = i0 + k;
-                if (i >= n) break;
+                if (i == 0) continue;
+                const uint32_t xi = cur[i];
+                if (xi & WS) continue;   // no pair ends at i (old or new)
+                const uint32_t xp = cur[i - 1];
                 const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
-                const uint32_t xp = w[k + 1], xi = w[k + 2];
                 const uint32_t tp = xp & TM, ti = xi & TM;
-                if (!h0 && i >= lim) ++tail;
-                if (i == 0 || (xi & WS)) continue;   // no pair ends at i (old or new)
-                if (tp && ti && (hm || h0 || hp || i >= lim)) {
+                if (tp && ti) {
                     const uint32_t pid = (tp << 16) | ti;
-                    if (pid != pid_ab) lds_add(lt, tb, st, pid, 0xFFFFFFFFu);
+                    if (pid != pid_ab) lds_add(lt, tb, st, pid, 0xFFFFFFFFu);   // old pair destroyed
                 }
                 if (!h0 && i < lim) {
                     if (hm) {
@@ -484,16 +497,11 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
             }
         }
         lds_flush(lt, tb, st);
+        for (int off = 32; off > 0; off >>= 1) tail += __shfl_xor(tail, off);
+        if (lane == 0 && tail) atomicAdd(&st->m, tail);
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        cnt += __shfl_xor(cnt, off);
-        tail += __shfl_xor(tail, off);
-    }
-    if (lane == 0) red[t >> 6] = cnt;
-    __syncthreads();
-    // stores last: none of them is waited on before a barrier
-    if (i0 < n) hitmask[(uint64_t)tl * TPB + t] = (uint16_t)hitm;
-    if (lane == 0 && tail) atomicAdd(&st->m, tail);
+    // stores last: nothing waits on them
+    if (i0 < n) hitmask[(uint64_t)tl * TPB + t] = hitm;
     if (t == 0) {
         const uint32_t tot = red[0] + red[1] + red[2] + red[3];
         tile_cnt[tl] = tot;
@@ -509,21 +517,27 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
 // stream — add its pairs to the count table.
 template <typename S, bool EXACT>
 __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S* __restrict__ cur, S* __restrict__ oth,
-                                                 const uint16_t* __restrict__ hitmask,
+                                                 const uint32_t* __restrict__ hitmask,
                                                  const uint32_t* __restrict__ tile_cnt,
                                                  const uint32_t* __restrict__ grpsum, Table tb) {
-    if (!merge_active(st, round)) return;
     // one LDS arena: the compaction stage of tile blocks or the delta table of tail blocks
-    constexpr int ARENA = (sizeof(LdsTab<LTAB>) > (TILE + 16) * sizeof(S) ? sizeof(LdsTab<LTAB>) : (TILE + 16) * sizeof(S)) / 16;
+    constexpr int STAGE = (TILE + 16) * sizeof(S);
+    constexpr int ARENA = (sizeof(LdsTab<LTAB>) > STAGE ? sizeof(LdsTab<LTAB>) : STAGE) / 16;
     __shared__ uint4 arena[ARENA];
     __shared__ uint32_t wsum[TPB / 64], psum[TPB / 64];
     S* stage = reinterpret_cast<S*>(arena);
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t tl = blockIdx.x;
+    const uint64_t base = (uint64_t)tl * TILE;
+    const uint64_t i0 = base + (uint64_t)t * EPT;
+    const bool tile_block = tl < gridDim.x;   // refined below once n is known
+    (void)tile_block;
+    if (!merge_active(st, round)) return;
     const uint32_t n = st->n, new_n = st->new_n, nw = st->nw;
     const uint32_t limit = EXACT ? n : new_n;
     const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    if (blockIdx.x >= ntiles) {
+    if (tl >= ntiles) {
         if (EXACT) return;
         // ── stale tail window ──
         const uint32_t m = st->m;
@@ -532,27 +546,25 @@ __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S
         __shared__ uint32_t left_val;
         lds_clear(lt);
         const uint32_t lo = new_n - m;
-        const uint32_t tb0 = blockIdx.x - ntiles, ntb = gridDim.x - ntiles;
+        const uint32_t tb0 = tl - ntiles, ntb = gridDim.x - ntiles;
         if (tb0 == 0 && wid == 0 && lo >= 1) {
             // the survivor just before the window: last j < new_n with hit(j) == 0; its
             // value is the A-side-rewritten symbol (the rewrite is idempotent, so racing
             // with a tile block's in-place write is harmless)
-            int64_t wi = (int64_t)(new_n - 1) / EPT;
+            int64_t wi = (int64_t)(new_n - 1) / 32;
             uint32_t found = 0xFFFFFFFFu;
             while (wi >= 0 && found == 0xFFFFFFFFu) {
                 const int64_t mywi = wi - lane;
-                uint32_t word = 0xFFFFu;
+                uint32_t inv = 0;
                 if (mywi >= 0) {
-                    word = hitmask[mywi];
-                    const uint64_t hi_i = (uint64_t)mywi * EPT + EPT;   // exclusive
-                    if (hi_i > new_n) word |= (0xFFFFu << (EPT - (hi_i - new_n))) & 0xFFFFu;
+                    const uint64_t wbase = (uint64_t)mywi * 32;
+                    inv = ~hitmask[mywi] & lane_mask32(wbase, new_n);   // survivors below new_n
                 }
-                const uint32_t inv = (~word) & 0xFFFFu;   // survivors
                 const unsigned long long has = __ballot(inv != 0u);
                 if (has) {
                     const int l = __ffsll((long long)has) - 1;   // lowest lane = largest word index
                     const uint32_t inv_l = __shfl(inv, l);
-                    found = (uint32_t)((wi - l) * EPT + (31 - __clz(inv_l)));
+                    found = (uint32_t)((wi - l) * 32 + (31 - __clz(inv_l)));
                 }
                 wi -= 64;
             }
@@ -560,7 +572,8 @@ __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S
                 uint32_t v = 0;
                 if (found != 0xFFFFFFFFu) {
                     v = cur[found];
-                    const bool rw = (found + 1 < n) && ((hitmask[(found + 1) / EPT] >> ((found + 1) % EPT)) & 1u);
+                    const uint32_t f1 = found + 1;
+                    const bool rw = (f1 < n) && ((hitmask[f1 / 32] >> (f1 % 32)) & 1u);
                     if (rw) v = nw | (v & WS);
                 }
                 left_val = v;
@@ -577,9 +590,6 @@ __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S
         lds_flush(lt, tb, st);
         return;
     }
-    const uint32_t tl = blockIdx.x;
-    const uint64_t base = (uint64_t)tl * TILE;
-    const uint64_t i0 = base + (uint64_t)t * EPT;
     // every independent load first: prefix terms, mask words, the tile
     const uint32_t G = tl / GRP;
     uint32_t part = 0;
@@ -590,20 +600,16 @@ __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S
         const uint32_t g1 = ((uint32_t)t + TPB < G) ? grpsum[t + TPB] : 0u;
         part = v0 + g0 + g1;
     }
-    const uint32_t hm = i0 < n ? hitmask[(uint64_t)tl * TPB + t] : 0xFFFFu;
+    const uint32_t hm = hitmask[(uint64_t)tl * TPB + t];
     const uint32_t hn = hitmask[(uint64_t)tl * TPB + t + 1];   // may be the next tile's first word
     uint32_t x[EPT];
     load_own(cur, i0, x);
     for (uint32_t g = t + 2 * TPB; g < G; g += TPB) part += grpsum[g];   // only past 2*TPB groups
+    const uint32_t inb = lane_mask32(i0, n);
     const uint32_t nextbit = (i0 + EPT < n) ? (hn & 1u) : 0u;
-    const uint32_t inb = (i0 >= n) ? 0u : (i0 + EPT <= n ? 0xFFFFu : ((1u << (n - i0)) - 1u));
     const uint32_t rwm = ((hm >> 1) | (nextbit << (EPT - 1))) & inb;
     const uint32_t valid = inb & ~hm;
-    uint32_t keep = valid;
-    if (!EXACT) {
-        if (i0 >= limit) keep = 0;
-        else if (i0 + EPT > limit) keep &= (1u << (limit - i0)) - 1u;
-    }
+    const uint32_t keep = EXACT ? valid : (valid & lane_mask32(i0, limit));
     if (rwm) {   // in-place A-side rewrite (train.wgsl:486-487): the reference's ping buffer
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
@@ -655,12 +661,9 @@ __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S
 }
 
 __global__ void k_clear_dirty_all(DevState* st, Table tb) {
+    (void)st;
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < tb.nblk) {
-        tb.dirty[i] = 0u;
-        tb.dlist[i] = i;
-    }
-    if (i == 0) st->ndirty = tb.nblk;
+    if (i < tb.nblk) tb.dirty[i] = 1u;   // every block gets re-maxed
 }
 
 // dump live (count > 0) pairs
@@ -706,7 +709,7 @@ struct gbpe_trainer {
     uint32_t* h_log = nullptr;   // pinned
     Table tb{};
     uint32_t table_log2 = 22;
-    uint16_t* hitmask = nullptr;
+    uint32_t* hitmask = nullptr;
     uint32_t* tile_cnt = nullptr;
     uint32_t* grpsum = nullptr;
     uint64_t* status = nullptr;    // look-back granules, one per tile
@@ -773,12 +776,12 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
         hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
                            t->hitmask, t->tile_cnt, t->grpsum);
         hipLaunchKernelGGL((k_compact<S, true>), dim3(g_compact), dim3(TPB), 0, s, t->st, round, cur, oth,
-                           (const uint16_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
+                           (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
     } else {
         hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
                            t->hitmask, t->tile_cnt, t->grpsum);
         hipLaunchKernelGGL((k_compact<S, false>), dim3(g_compact), dim3(TPB), 0, s, t->st, round, cur, oth,
-                           (const uint16_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
+                           (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(k_refresh<S>, dim3(g_refresh), dim3(TPB), 0, s, t->st, round, 1, t->tb, cur,
@@ -844,7 +847,7 @@ extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t
         hipMalloc(&t->tb.dirty, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->tb.dlist, (t->tb.nblk + 1) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->hitmask, (ntiles0 + 1) * TPB * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc(&t->hitmask, (ntiles0 + 1) * TPB * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->tile_cnt, (ntiles0 + 1) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->grpsum, (ntiles0 / GRP + 2) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->status, (ntiles0 + 2) * sizeof(uint64_t)) != hipSuccess ||
@@ -859,7 +862,7 @@ extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t
     if (hipMemsetAsync(t->tb.dirty, 0, t->tb.nblk * sizeof(uint32_t), s) != hipSuccess ||
         hipMemsetAsync(t->status, 0, (ntiles0 + 2) * sizeof(uint64_t), s) != hipSuccess ||
         hipMemsetAsync(t->tailinfo, 0, 2 * sizeof(uint64_t), s) != hipSuccess ||
-        hipMemsetAsync(t->hitmask, 0, (ntiles0 + 1) * TPB * sizeof(uint16_t), s) != hipSuccess)
+        hipMemsetAsync(t->hitmask, 0, (ntiles0 + 1) * TPB * sizeof(uint32_t), s) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "memset failed"));
     DevState init{};
     init.n = (uint32_t)n;

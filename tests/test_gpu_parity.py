@@ -270,3 +270,20 @@ def test_encode_v2_trie_parse(eng):
     blob += b"".join(struct.pack("<2H", s, t) for s, t in edges)
     tok = TrieTokenizer(eng, blob, chunk_size=512)
     assert tok.encode_bytes(b"abcbbx").tolist() == [97, 300, 98, 98, 120]
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_train_large_vs_c_oracle(eng, exact):
+    # 24 MiB: thousands of tiles, so the two-level tile prefix (group sums) and
+    # multi-block stale-tail windows are exercised; checked against the C restatement
+    import cpu_ref
+    from gpubpe import synth
+    data = synth.english(24 << 20, seed=77, fancy_punct=0.005)
+    k = 300
+    ref = cpu_ref.train(data, 256 + k, exact=exact, threads=16)
+    m, s, pairs, st = _train_native(eng, data, 256 + k, exact=exact)
+    assert m == ref["merges"]
+    assert np.array_equal(s, ref["symbols"])
+    _assert_counts_match_stream(pairs, s)
+    if not exact:
+        assert st.tail_dropped == ref["tail_total"]

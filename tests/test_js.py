@@ -51,4 +51,4 @@ def test_js_addon_train_and_encode(tmp_path):
                       "tokens": toks})
     p = tmp_path / "cases.json"
     p.write_text(json.dumps({"train": cases}))
-    assert _run("test_gpu.mjs", str(p)).strip().startswith("ok")
+    assert _run("test_gpu.mjs", str(p)).strip().splitlines()[-1].startswith("ok")
