@@ -255,15 +255,37 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             st->n = st->new_n;
         }
     }
-    for (uint32_t blk = blockIdx.x; blk < tb.nblk; blk += gridDim.x) {
-        if (!tb.dirty[blk]) continue;   // block-uniform
-        const uint2* s = tb.slots + ((uint64_t)blk << BLK_LOG2);
+    // this WG's contiguous run of blocks: all flags in one load, then only the dirty ones
+    __shared__ uint64_t s_dmask;
+    const uint32_t per = (tb.nblk + gridDim.x - 1) / gridDim.x;   // <= 64 (host-sized grid)
+    const uint32_t b0 = blockIdx.x * per;
+    if (threadIdx.x < 64) {
+        const uint32_t blk = b0 + threadIdx.x;
+        const bool d = threadIdx.x < per && blk < tb.nblk && tb.dirty[blk];
+        const unsigned long long m = __ballot(d);
+        if (threadIdx.x == 0) s_dmask = m;
+    }
+    __syncthreads();
+    uint64_t dm = s_dmask;
+    while (dm) {
+        const uint32_t blk = b0 + (uint32_t)(__ffsll((long long)dm) - 1);
+        dm &= dm - 1;
+        const uint4* s = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)blk << BLK_LOG2));
+        constexpr int NV = (1 << BLK_LOG2) / 2 / TPB;   // 16-byte loads per thread
+        uint4 e[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) e[k] = s[threadIdx.x + k * TPB];
         uint64_t best = 0;
         uint32_t live = 0;
-        for (uint32_t i = threadIdx.x; i < (1u << BLK_LOG2); i += TPB) {
-            uint2 e = s[i];
-            if (e.x && (int32_t)e.y > 0) {
-                uint64_t key = ((uint64_t)e.y << 32) | (uint32_t)(~e.x);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            if (e[k].x && (int32_t)e[k].y > 0) {
+                const uint64_t key = ((uint64_t)e[k].y << 32) | (uint32_t)(~e[k].x);
+                best = key > best ? key : best;
+                ++live;
+            }
+            if (e[k].z && (int32_t)e[k].w > 0) {
+                const uint64_t key = ((uint64_t)e[k].w << 32) | (uint32_t)(~e[k].z);
                 best = key > best ? key : best;
                 ++live;
             }
@@ -292,6 +314,7 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
 }
 
 constexpr uint32_t GRP = 64;    // tiles per group sum (two-level tile prefix)
+constexpr uint32_t GSTR = 64;   // group sums 256 B apart: each is its own atomic serialisation point
 
 // argmax over block maxima + the reference's bpe_setup_merge (train.wgsl:340-364)
 __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, uint32_t* __restrict__ log,
@@ -301,7 +324,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
     if (st->stop) return;
     {   // group sums of the coming stream pass start at zero
         const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(st->n, TILE), GRP);
-        for (uint32_t g = threadIdx.x; g < ngrp; g += SEL_THREADS) grpsum[g] = 0u;
+        for (uint32_t g = threadIdx.x; g < ngrp; g += SEL_THREADS) grpsum[g * GSTR] = 0u;
     }
     uint64_t best = 0;
     uint32_t live = 0;
@@ -370,7 +393,7 @@ __device__ __forceinline__ bool merge_active(const DevState* st, uint32_t round)
 }
 
 template <typename S>
-__device__ __forceinline__ void load_own(const S* __restrict__ cur, uint64_t i0, uint32_t* __restrict__ x) {
+__device__ __forceinline__ void load_own(const S* cur, uint64_t i0, uint32_t* __restrict__ x) {
     constexpr int V = EPT * sizeof(S) / 16;
     uint4 v[V];
     const uint4* src = reinterpret_cast<const uint4*>(cur + i0);
@@ -400,7 +423,7 @@ __device__ __forceinline__ uint32_t lane_mask32(uint64_t i0, uint64_t lim) {
 // with no site within reach and no tail element do no delta work; a tile with no
 // such lane passes a single barrier.
 template <typename S, bool EXACT>
-__global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, const S* __restrict__ cur, Table tb,
+__global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, const S* cur, Table tb,
                                                uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
                                                uint32_t* __restrict__ grpsum) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
@@ -410,48 +433,49 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
     const uint32_t tl = blockIdx.x;
     const uint64_t base = (uint64_t)tl * TILE;
     const uint64_t i0 = base + (uint64_t)t * EPT;
-    // loads first (buffers are padded: every launched tile is in bounds)
-    uint32_t w[EPT + 3];
+    // loads first, unconditionally (buffers are padded: every launched tile is in
+    // bounds); the compiler barrier keeps them ahead of the state's scalar loads
+    // so both round trips overlap
+    uint32_t x[EPT];
     uint32_t lh = 0, rh = 0;
-    if (i0 >= 2) {
+    {
+        const uint64_t hi = i0 >= 2 ? i0 - 2 : 0;
         if (sizeof(S) == 2) {
-            lh = *reinterpret_cast<const uint32_t*>(cur + i0 - 2);
+            lh = *reinterpret_cast<const uint32_t*>(cur + hi);
         } else {
-            const uint2 v2 = *reinterpret_cast<const uint2*>(cur + i0 - 2);
+            const uint2 v2 = *reinterpret_cast<const uint2*>(cur + hi);
             lh = v2.x;
             rh = v2.y;
         }
     }
     const uint32_t nxr = (uint32_t)cur[i0 + EPT];
-    load_own(cur, i0, w + 2);
-    if (!merge_active(st, round)) return;
-    const uint32_t n = st->n;
+    load_own(cur, i0, x);
+    // the loop state, one snapshot: fields n .. merges_done (DevState offsets 0..39)
+    const uint4 s0 = reinterpret_cast<const uint4*>(st)[0];   // n, stop, next_id, a
+    const uint4 s1 = reinterpret_cast<const uint4*>(st)[1];   // b, nw, mc, new_n
+    const uint2 s2 = reinterpret_cast<const uint2*>(st)[4];   // m, merges_done
+    asm volatile("" ::: "memory");
+    const uint32_t n = s0.x, a = s0.w, b = s1.x, nw = s1.y, new_n = s1.w;
     const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
-    if (tl >= ntiles) return;
-    const uint32_t new_n = st->new_n, a = st->a, b = st->b, nw = st->nw;
+    if (s0.y || s2.y != round + 1u || tl >= ntiles) return;   // merge_active()
     const uint32_t pid_ab = (a << 16) | b;
     const uint32_t lim = EXACT ? 0xFFFFFFFFu : new_n;
-    if (sizeof(S) == 2) {
-        w[0] = lh & 0xFFFFu;
-        w[1] = lh >> 16;
-    } else {
-        w[0] = lh;
-        w[1] = rh;
-    }
-    if (i0 < 2) {
-        w[0] = 0;
-        w[1] = 0;
-    }
-    w[EPT + 2] = (i0 + EPT < n) ? nxr : 0u;
-    uint64_t hbits = 0;   // bit k = hit(i0 - 1 + k), k = 0..EPT+1
+    uint32_t xm2 = sizeof(S) == 2 ? (lh & 0xFFFFu) : lh;   // symbol at i0 - 2
+    uint32_t xm1 = sizeof(S) == 2 ? (lh >> 16) : rh;       // symbol at i0 - 1
+    if (i0 < 2) xm2 = xm1 = 0;                              // tokens are never 0 = a, b
+    // branch-free site detection: eb bit j = (x_j == b) (a B-side symbol carries no
+    // word-start bit), ea bit j = (tok(x_j) == a)
+    uint32_t eb = 0, ea = 0;
 #pragma unroll
-    for (int k = 0; k < EPT + 2; ++k) {
-        const uint64_t j1 = i0 + k;
-        const bool h = (j1 >= 2) && (j1 - 1 < n) && !(w[k + 1] & WS) && ((w[k] & TM) == a) && ((w[k + 1] & TM) == b);
-        hbits |= (uint64_t)h << k;
+    for (int k = 0; k < EPT; ++k) {
+        eb |= (x[k] == b ? 1u : 0u) << k;
+        ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
     }
     const uint32_t inb = lane_mask32(i0, n);
-    const uint32_t hitm = (uint32_t)(hbits >> 1);
+    const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;   // hit(i0 + j)
+    const uint32_t h_m1 = (xm1 == b && (xm2 & TM) == a && i0 - 1 < n) ? 1u : 0u;  // hit(i0 - 1)
+    const uint32_t h_32 = (nxr == b && (ea >> (EPT - 1)) && i0 + EPT < n) ? 1u : 0u;  // hit(i0 + EPT)
+    const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (EPT + 1));
     uint32_t cnt = __popc(inb & ~hitm);
     uint32_t tail = 0;
     const bool work = hbits != 0 || (i0 + EPT > lim && i0 < n);
@@ -505,7 +529,7 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
     if (t == 0) {
         const uint32_t tot = red[0] + red[1] + red[2] + red[3];
         tile_cnt[tl] = tot;
-        atomicAdd(&grpsum[tl / GRP], tot);
+        atomicAdd(&grpsum[(tl / GRP) * GSTR], tot);
     }
 }
 
@@ -515,8 +539,23 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
 // tile counts of this group before the tile.  Blocks >= ntiles (reference
 // compaction only): the stale tail window [new_n - m, new_n) of the new
 // stream — add its pairs to the count table.
+constexpr int CTPB = 512;             // k_compact threads per tile
+constexpr int CEPT = TILE / CTPB;     // 16 symbols per k_compact thread
+
+template <typename S, int E>
+__device__ __forceinline__ void load_own_n(const S* __restrict__ cur, uint64_t i0, uint32_t* __restrict__ x) {
+    constexpr int V = E * sizeof(S) / 16;
+    uint4 v[V];
+    const uint4* src = reinterpret_cast<const uint4*>(cur + i0);
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = src[k];
+    const S* e = reinterpret_cast<const S*>(v);
+#pragma unroll
+    for (int k = 0; k < E; ++k) x[k] = e[k];
+}
+
 template <typename S, bool EXACT>
-__global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S* __restrict__ cur, S* __restrict__ oth,
+__global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, S* __restrict__ cur, S* __restrict__ oth,
                                                  const uint32_t* __restrict__ hitmask,
                                                  const uint32_t* __restrict__ tile_cnt,
                                                  const uint32_t* __restrict__ grpsum, Table tb) {
@@ -524,15 +563,12 @@ __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S
     constexpr int STAGE = (TILE + 16) * sizeof(S);
     constexpr int ARENA = (sizeof(LdsTab<LTAB>) > STAGE ? sizeof(LdsTab<LTAB>) : STAGE) / 16;
     __shared__ uint4 arena[ARENA];
-    __shared__ uint32_t wsum[TPB / 64], psum[TPB / 64];
+    __shared__ uint32_t wsum[CTPB / 64], psum[CTPB / 64];
     S* stage = reinterpret_cast<S*>(arena);
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t tl = blockIdx.x;
     const uint64_t base = (uint64_t)tl * TILE;
-    const uint64_t i0 = base + (uint64_t)t * EPT;
-    const bool tile_block = tl < gridDim.x;   // refined below once n is known
-    (void)tile_block;
     if (!merge_active(st, round)) return;
     const uint32_t n = st->n, new_n = st->new_n, nw = st->nw;
     const uint32_t limit = EXACT ? n : new_n;
@@ -580,7 +616,7 @@ __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S
             }
         }
         __syncthreads();
-        for (uint32_t d = lo + tb0 * TPB + t; d < new_n; d += ntb * TPB) {
+        for (uint32_t d = lo + tb0 * CTPB + t; d < new_n; d += ntb * CTPB) {
             if (d == 0) continue;
             const uint32_t x0 = (d == lo) ? left_val : (uint32_t)oth[d - 1];
             const uint32_t x1 = oth[d];
@@ -590,32 +626,36 @@ __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S
         lds_flush(lt, tb, st);
         return;
     }
-    // every independent load first: prefix terms, mask words, the tile
+    // 512 threads x 16 symbols cover the 8192-symbol tile; every independent load
+    // first: prefix terms, mask word, the tile
+    const uint64_t j0 = base + (uint64_t)t * CEPT;
     const uint32_t G = tl / GRP;
     uint32_t part = 0;
     {
         const uint32_t j = G * GRP + t;
         const uint32_t v0 = (t < (int)GRP && j < tl) ? tile_cnt[j] : 0u;
-        const uint32_t g0 = ((uint32_t)t < G) ? grpsum[t] : 0u;
-        const uint32_t g1 = ((uint32_t)t + TPB < G) ? grpsum[t + TPB] : 0u;
+        const uint32_t g0 = ((uint32_t)t < G) ? grpsum[t * GSTR] : 0u;
+        const uint32_t g1 = ((uint32_t)t + CTPB < G) ? grpsum[(t + CTPB) * GSTR] : 0u;
         part = v0 + g0 + g1;
     }
-    const uint32_t hm = hitmask[(uint64_t)tl * TPB + t];
-    const uint32_t hn = hitmask[(uint64_t)tl * TPB + t + 1];   // may be the next tile's first word
-    uint32_t x[EPT];
-    load_own(cur, i0, x);
-    for (uint32_t g = t + 2 * TPB; g < G; g += TPB) part += grpsum[g];   // only past 2*TPB groups
-    const uint32_t inb = lane_mask32(i0, n);
-    const uint32_t nextbit = (i0 + EPT < n) ? (hn & 1u) : 0u;
-    const uint32_t rwm = ((hm >> 1) | (nextbit << (EPT - 1))) & inb;
+    const uint32_t hw = hitmask[(uint64_t)tl * TPB + (t >> 1)];
+    const uint32_t hn = (t & 1) ? hitmask[(uint64_t)tl * TPB + (t >> 1) + 1] : 0u;   // may be the next tile's first word
+    uint32_t x[CEPT];
+    load_own_n<S, CEPT>(cur, j0, x);
+    for (uint32_t g = t + 2 * CTPB; g < G; g += CTPB) part += grpsum[g * GSTR];   // only past 2*CTPB groups
+    const uint32_t hm = (t & 1) ? (hw >> 16) : (hw & 0xFFFFu);
+    const uint32_t nb = (t & 1) ? (hn & 1u) : ((hw >> 16) & 1u);
+    const uint32_t inb = lane_mask32(j0, n) & 0xFFFFu;
+    const uint32_t nextbit = (j0 + CEPT < n) ? nb : 0u;
+    const uint32_t rwm = ((hm >> 1) | (nextbit << (CEPT - 1))) & inb;
     const uint32_t valid = inb & ~hm;
-    const uint32_t keep = EXACT ? valid : (valid & lane_mask32(i0, limit));
+    const uint32_t keep = EXACT ? valid : (valid & lane_mask32(j0, limit));
     if (rwm) {   // in-place A-side rewrite (train.wgsl:486-487): the reference's ping buffer
 #pragma unroll
-        for (int k = 0; k < EPT; ++k) {
+        for (int k = 0; k < CEPT; ++k) {
             if ((rwm >> k) & 1u) {
                 x[k] = nw | (x[k] & WS);
-                cur[i0 + k] = (S)x[k];
+                cur[j0 + k] = (S)x[k];
             }
         }
     }
@@ -630,17 +670,20 @@ __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S
     if (lane == 63) wsum[wid] = incl;
     if (lane == 0) psum[wid] = part;
     __syncthreads();
-    uint32_t pre = incl - cnt;
-    for (int w2 = 0; w2 < wid; ++w2) pre += wsum[w2];
-    const uint32_t total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    const uint32_t prefix = psum[0] + psum[1] + psum[2] + psum[3];
+    uint32_t pre = incl - cnt, total = 0, prefix = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < CTPB / 64; ++w2) {
+        pre += w2 < wid ? wsum[w2] : 0u;
+        total += wsum[w2];
+        prefix += psum[w2];
+    }
     if (tl == ntiles - 1 && t == 0 && prefix + tile_cnt[tl] != new_n) atomicOr(&st->err, ERR_COUNT_MISMATCH);
     // stage at the destination's alignment phase so both sides move whole 16-byte words
     constexpr uint32_t VE = 16 / sizeof(S);           // symbols per 16-byte word
     const uint32_t ph = prefix & (VE - 1);
     pre += ph;
 #pragma unroll
-    for (int k = 0; k < EPT; ++k)
+    for (int k = 0; k < CEPT; ++k)
         if ((keep >> k) & 1u) stage[pre++] = (S)x[k];
     __syncthreads();
     S* dst = oth + (prefix - ph);                      // 16-byte aligned
@@ -648,7 +691,7 @@ __global__ __launch_bounds__(TPB) void k_compact(DevState* st, uint32_t round, S
     const uint32_t nvec = end / VE;
     uint4* dv = reinterpret_cast<uint4*>(dst);
     const uint4* sv = reinterpret_cast<const uint4*>(stage);
-    for (uint32_t v = t; v < nvec; v += TPB) {
+    for (uint32_t v = t; v < nvec; v += CTPB) {
         if (v == 0 && ph) {
             for (uint32_t j = ph; j < VE && j < end; ++j) dst[j] = stage[j];   // partial head word
         } else {
@@ -718,7 +761,7 @@ struct gbpe_trainer {
     // stats
     uint64_t bytes_moved = 0;
     uint64_t max_live = 0;
-    double ms_merge = 0, ms_select = 0, ms_other = 0;
+    double ms_merge = 0, ms_select = 0, ms_other = 0, ms_delta = 0, ms_compact = 0;
     uint64_t timed_merges = 0;
     std::vector<hipEvent_t> evs;
 };
@@ -775,12 +818,14 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     if (exact) {
         hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
                            t->hitmask, t->tile_cnt, t->grpsum);
-        hipLaunchKernelGGL((k_compact<S, true>), dim3(g_compact), dim3(TPB), 0, s, t->st, round, cur, oth,
+        if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
+        hipLaunchKernelGGL((k_compact<S, true>), dim3(g_compact), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
     } else {
         hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
                            t->hitmask, t->tile_cnt, t->grpsum);
-        hipLaunchKernelGGL((k_compact<S, false>), dim3(g_compact), dim3(TPB), 0, s, t->st, round, cur, oth,
+        if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
+        hipLaunchKernelGGL((k_compact<S, false>), dim3(g_compact), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
@@ -849,7 +894,7 @@ extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t
         hipMalloc(&t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->hitmask, (ntiles0 + 1) * TPB * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->tile_cnt, (ntiles0 + 1) * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->grpsum, (ntiles0 / GRP + 2) * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->grpsum, (ntiles0 / GRP + 2) * GSTR * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->status, (ntiles0 + 2) * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc(&t->tailinfo, 2 * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc(&t->rwlist, (n / 2 + 2) * sizeof(uint32_t)) != hipSuccess ||
@@ -940,7 +985,7 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
                             : grid_persistent(t->ctx, gbpe_div_up(t->n / 2 + 1, TPB * 16), 1);
     const uint32_t g_delta = (uint32_t)(ntiles ? ntiles : 1);
     const uint32_t g_compact = (uint32_t)ntiles + g_tail;
-    const uint32_t g_refresh = grid_persistent(t->ctx, t->tb.nblk, 4);
+    const uint32_t g_refresh = grid_persistent(t->ctx, t->tb.nblk, 2);
     const bool timing = (t->flags & GBPE_TRAIN_TIMING) != 0;
     for (uint32_t r = 0; r < k; ++r) {
         hipEvent_t* ev = timing ? &t->evs[5 * r] : nullptr;
@@ -960,14 +1005,18 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     }
     if (timing) {
         for (uint32_t r = 0; r < done; ++r) {
-            float a = 0, b = 0, c = 0;
+            float a = 0, b = 0, c = 0, d1 = 0, d2 = 0;
             hipEvent_t* ev = &t->evs[5 * r];
             hipEventElapsedTime(&a, ev[0], ev[1]);
             hipEventElapsedTime(&b, ev[1], ev[2]);
             hipEventElapsedTime(&c, ev[2], ev[4]);
+            hipEventElapsedTime(&d1, ev[1], ev[3]);
+            hipEventElapsedTime(&d2, ev[3], ev[2]);
             t->ms_select += a;
             t->ms_merge += b;
             t->ms_other += c;
+            t->ms_delta += d1;
+            t->ms_compact += d2;
         }
         t->timed_merges += done;
     }
@@ -1001,6 +1050,8 @@ extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
     o->bytes_per_symbol = t->bps;
     o->early_stop = t->stop;
     o->ms_merge = t->ms_merge;
+    o->ms_delta = t->ms_delta;
+    o->ms_compact = t->ms_compact;
     o->ms_select = t->ms_select;
     o->ms_other = t->ms_other;
     o->timed_merges = t->timed_merges;

@@ -45,7 +45,8 @@ class TrainerStats(C.Structure):
                 ("tail_dropped", C.c_uint64), ("live_pairs", C.c_uint64), ("table_slots", C.c_uint64),
                 ("table_used", C.c_uint64), ("max_live_pairs", C.c_uint64), ("bytes_per_symbol", C.c_uint32),
                 ("early_stop", C.c_uint32), ("ms_merge", C.c_double), ("ms_select", C.c_double),
-                ("ms_other", C.c_double), ("timed_merges", C.c_uint64)]
+                ("ms_other", C.c_double), ("timed_merges", C.c_uint64),
+                ("ms_delta", C.c_double), ("ms_compact", C.c_double)]
 
 
 PROGRESS_CB = C.CFUNCTYPE(C.c_int, C.POINTER(Progress), u32p, C.c_void_p)

@@ -132,10 +132,12 @@ typedef struct gbpe_trainer_stats {
                                      table would likely have dropped counts (train.wgsl:422-429) */
     uint32_t bytes_per_symbol;
     uint32_t early_stop;
-    double   ms_merge;            /* GBPE_TRAIN_TIMING: device ms in the stream merge kernels */
-    double   ms_select;           /* argmax + table refresh */
-    double   ms_other;            /* tail, rewrite, scan */
+    double   ms_merge;            /* GBPE_TRAIN_TIMING: device ms in the two stream kernels (k_delta + k_compact) */
+    double   ms_select;           /* k_select: argmax + merge setup */
+    double   ms_other;            /* k_refresh: block maxima of touched table blocks */
     uint64_t timed_merges;
+    double   ms_delta;            /* k_delta alone (HIP events between the two stream kernels) */
+    double   ms_compact;          /* k_compact alone (tiles + stale-tail blocks) */
 } gbpe_trainer_stats;
 int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* out);
 /* Current symbol stream in the reference u32 layout (bit16 = word start). */
