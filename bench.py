@@ -316,6 +316,19 @@ def main():
         "train_detail": tr,
     }
 
+    pmc = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+    if os.path.exists(pmc) and args.train_bytes == 104_857_600 and tr["bytes_per_symbol"] == 2:
+        # HBM bytes per merge of k_delta + k_compact from the committed rocprofv3 --pmc
+        # passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), on the first merges of
+        # this same workload; scaled to the per-merge algorithmic bytes of this run
+        p = json.load(open(pmc))
+        ratio = p["traffic_over_algorithmic"]
+        line["roofline"]["traffic"] = round(ratio * tr["stream_bytes"] / max(1, tr["merges"]))
+        line["roofline"]["traffic_unit"] = "bytes/merge (k_delta + k_compact)"
+        line["roofline"]["traffic_over_algorithmic"] = round(ratio, 4)
+        line["roofline"]["traffic_sample"] = (f"profiles/r1_pmc_traffic.json: first {p['merges']} merges, "
+                                              f"FETCH_SIZE and WRITE_SIZE passes")
+
     enc = None
     if not args.no_encode:
         enc = encode_leg(args, lib, ctx, dist, rank)
@@ -325,7 +338,7 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cpu_ref
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        k = args.cpu_merges or 64
+        k = args.cpu_merges or 256
         t = time.perf_counter()
         r = cpu_ref.train(data, args.vocab, max_merges=k, threads=threads, want_symbols=False)
         dt = time.perf_counter() - t
