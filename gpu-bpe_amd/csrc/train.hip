@@ -14,7 +14,7 @@
 //     recomputed for blocks a merge touched, then one workgroup reduces them
 //     with the reference's tie-break (higher count, then smaller a<<16|b,
 //     train.wgsl:83-85);
-//   * the stream pass is two streaming kernels over 4096-symbol tiles:
+//   * the stream pass is two streaming kernels over 8192-symbol tiles:
 //     k_delta (reads the stream; writes a 1-bit merge-site mask, per-tile
 //     survivor counts and count deltas) and k_compact (reads stream + mask,
 //     rewrites merged symbols in place, scatters survivors into the
