@@ -1,0 +1,239 @@
+"""Sharded BPE training: one process per GPU, bit-exact global merges.
+
+SURVEY §8(e): the corpus is cut at word starts, so pair counts are additive
+across shards (train.wgsl:395; pairs never cross a word start).  Every merge
+still needs a global argmax, and the reference's compaction quirk
+(train.wgsl:605-607 + 698/727) acts on the *global* stream end.  Each rank
+therefore keeps a replica of the global pair-count table, and every merge is
+one fixed-size all-gather of a per-rank *exchange record*:
+
+    header (HDR u32) | count deltas (C x {pid, delta}) | window piece (Cw u32)
+
+* phase 1 (per rank, device): select on the replica (identical on all ranks),
+  find the merge sites in the local stream, aggregate the local count deltas,
+  and copy this rank's piece of the stale-window superset
+  ``[n' - mc, n')`` (global positions; the previous merge's input stream, the
+  ping-pong buffer the reference reads stale symbols from);
+* one all-gather of the records (RCCL over xGMI on MI355X; gloo on CPU);
+* phase 2 (per rank, device, identical decisions on every rank): apply every
+  rank's deltas to the replica, cut the stale window (last ``m`` symbols of the
+  superset) and add its pairs, compact the local stream; the last rank that
+  kept any survivor appends the window, so the global stream stays the
+  concatenation of the rank streams in rank order.
+
+Capacities ``C``/``Cw`` are fixed per step, so no host synchronisation happens
+inside a 128-merge step.  A merge whose record does not fit stalls on every
+rank (its selection is undone), the step ends early, and the host grows the
+capacity from the needs recorded in the gathered headers and continues — the
+merge list is unaffected.
+
+The backend is the C-ABI trainer (``GpuShardBackend``); tests drive the same
+orchestration with a numpy model of one rank over gloo.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+# exchange-record header words (mirrored by csrc/train.hip)
+H_ACTIVE, H_L, H_KEPT, H_M, H_W, H_LASTSYM, H_HASLAST, H_SURV, H_LN, H_MC, H_A, H_B, H_ID = range(13)
+HDR = 16
+BATCH_SIZE = 128
+
+
+def record_words(cap_list: int, cap_win: int) -> int:
+    return HDR + 2 * cap_list + cap_win
+
+
+def _pow2_at_least(x: int, lo: int) -> int:
+    v = lo
+    while v < x:
+        v <<= 1
+    return v
+
+
+class ShardedTrainer:
+    """Host loop over a shard backend (trainer.js:225-335 per rank).
+
+    ``dist`` is ``torch.distributed`` (initialised); ``staged`` copies device
+    records through host memory (gloo with device buffers, e.g. several ranks
+    sharing one GPU in tests)."""
+
+    def __init__(self, backend, dist, device="cpu", staged: bool = False, cap_list: int = 1 << 14,
+                 cap_win: int = 1 << 12):
+        import torch
+        self.torch = torch
+        self.b = backend
+        self.dist = dist
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        self.device = device
+        self.staged = staged
+        self.C = cap_list
+        self.Cw = cap_win
+        self.stalls = 0
+        self._bufs = None
+
+    # ── collectives ──
+    def _all_gather(self, send):
+        torch = self.torch
+        out = torch.empty(self.world * send.numel(), dtype=send.dtype, device=send.device)
+        if self.staged and send.device.type != "cpu":
+            hs = send.cpu()
+            ho = torch.empty(self.world * send.numel(), dtype=send.dtype)
+            self.dist.all_gather_into_tensor(ho, hs)
+            out.copy_(ho)
+        else:
+            self.dist.all_gather_into_tensor(out, send)
+        return out
+
+    def _gather_ints(self, vals):
+        torch = self.torch
+        t = torch.tensor(vals, dtype=torch.int64, device=self.device)
+        return self._all_gather(t).view(self.world, len(vals)).cpu().numpy()
+
+    def setup(self):
+        """Global layout + the initial global pair counts (one variable-size exchange)."""
+        torch = self.torch
+        lens = self._gather_ints([self.b.local_len()])[:, 0]
+        self.b.set_layout([int(x) for x in lens])
+        pairs = self.b.export_counts(self.device)          # int32 [P, 2] (pid, count)
+        P = int(pairs.shape[0])
+        Ps = self._gather_ints([P])[:, 0]
+        pmax = max(1, int(Ps.max()))
+        send = torch.zeros(pmax * 2, dtype=torch.int32, device=self.device)
+        if P:
+            send[: 2 * P] = pairs.reshape(-1)
+        allp = self._all_gather(send).view(self.world, pmax * 2)
+        self.b.import_counts(allp, [int(x) for x in Ps], pmax)
+
+    def _buffers(self):
+        torch = self.torch
+        rw = record_words(self.C, self.Cw)
+        if self._bufs is None or self._bufs[0].numel() != rw:
+            send = torch.zeros(rw, dtype=torch.int32, device=self.device)
+            recv = torch.zeros(self.world * rw, dtype=torch.int32, device=self.device)
+            self._bufs = (send, recv)
+        return self._bufs
+
+    def step(self, max_merges: int = BATCH_SIZE):
+        """Up to ``max_merges`` global merges. Returns (merges, early_stop)."""
+        b = self.b
+        b.step_begin(max_merges)
+        send, recv = self._buffers()
+        for k in range(max_merges):
+            b.phase1(k, send, self.C, self.Cw)
+            if self.staged or send.device.type == "cpu":
+                out = self._all_gather(send)
+            else:
+                self.dist.all_gather_into_tensor(recv, send)
+                out = recv
+            b.phase2(k, out, self.C, self.Cw)
+        res = b.step_end()
+        if res["stalled"]:
+            self.stalls += 1
+            self.C = _pow2_at_least(2 * res["need_list"], self.C)
+            self.Cw = _pow2_at_least(2 * res["need_win"], self.Cw)
+        return res["merges"], res["early_stop"]
+
+    def train(self, target_vocab_size: int, vocab_size: int = 256, batch: int = BATCH_SIZE, on_progress=None):
+        needed = target_vocab_size - vocab_size
+        merges = []
+        early = False
+        while len(merges) < needed:
+            got, early = self.step(min(batch, needed - len(merges)))
+            merges += got
+            if on_progress:
+                on_progress(len(merges), needed, got)
+            if early:
+                break
+        return merges, early
+
+
+class GpuShardBackend:
+    """One rank's trainer over the gpubpe C-ABI (gbpe_shard_* entry points)."""
+
+    def __init__(self, lib, ctx, data, word_starts, rank: int, world: int, target_vocab: int,
+                 exact: bool = False, input_on_device: bool = False, n: int | None = None,
+                 table_log2: int = 0, cap_extra: int = 0):
+        from . import _lib
+        self.lib, self.ctx, self._lib = lib, ctx, _lib
+        flags = _lib.GBPE_TRAIN_EXACT_COMPACTION if exact else 0
+        self.opts = _lib.TrainOpts(target_vocab_size=target_vocab, vocab_size=256, next_token_id=256,
+                                   batch_size=BATCH_SIZE, flags=flags, table_log2=table_log2)
+        t = C.c_void_p()
+        if input_on_device:
+            ptr, nn = data, n
+        else:
+            buf = bytes(data)
+            ptr, nn = buf, len(buf)
+        ws = None
+        if word_starts is not None:
+            wsb = np.ascontiguousarray(np.asarray(word_starts, dtype=np.uint8))
+            ws = wsb.ctypes.data_as(C.POINTER(C.c_uint8))
+            self._ws_keep = wsb
+        _lib.check(lib.gbpe_shard_create(ctx, ptr, nn, ws, 1 if input_on_device else 0, C.byref(self.opts),
+                                         rank, world, cap_extra, C.byref(t)), ctx, "gbpe_shard_create")
+        self.t = t
+        self.rank, self.world = rank, world
+        self._out = (C.c_uint32 * (4 * BATCH_SIZE))()
+
+    def local_len(self) -> int:
+        n = C.c_uint64()
+        self._lib.check(self.lib.gbpe_shard_local_len(self.t, C.byref(n)), self.ctx, "local_len")
+        return int(n.value)
+
+    def set_layout(self, lens):
+        arr = (C.c_uint64 * len(lens))(*lens)
+        self._lib.check(self.lib.gbpe_shard_set_layout(self.t, arr, len(lens)), self.ctx, "set_layout")
+
+    def export_counts(self, device):
+        import torch
+        P = C.c_uint64()
+        self._lib.check(self.lib.gbpe_shard_export_counts(self.t, None, 0, C.byref(P)), self.ctx, "export")
+        out = torch.zeros((max(1, P.value), 2), dtype=torch.int32, device=device)
+        self._lib.check(self.lib.gbpe_shard_export_counts(self.t, C.c_void_p(out.data_ptr()), P.value, C.byref(P)),
+                        self.ctx, "export")
+        return out[: P.value]
+
+    def import_counts(self, allp, counts, pmax):
+        arr = (C.c_uint64 * len(counts))(*counts)
+        self._lib.check(self.lib.gbpe_shard_import_counts(self.t, C.c_void_p(allp.data_ptr()), arr, len(counts),
+                                                          pmax), self.ctx, "import")
+
+    def step_begin(self, max_merges):
+        self._lib.check(self.lib.gbpe_shard_step_begin(self.t, max_merges), self.ctx, "step_begin")
+
+    def phase1(self, k, send, cap_list, cap_win):
+        self._lib.check(self.lib.gbpe_shard_phase1(self.t, k, C.c_void_p(send.data_ptr()), cap_list, cap_win),
+                        self.ctx, "phase1")
+
+    def phase2(self, k, recv, cap_list, cap_win):
+        self._lib.check(self.lib.gbpe_shard_phase2(self.t, k, C.c_void_p(recv.data_ptr()), cap_list, cap_win),
+                        self.ctx, "phase2")
+
+    def step_end(self):
+        nd, es, st, nl, nwn = C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint32()
+        self._lib.check(self.lib.gbpe_shard_step_end(self.t, self._out, C.byref(nd), C.byref(es), C.byref(st),
+                                                     C.byref(nl), C.byref(nwn)), self.ctx, "step_end")
+        merges = [list(self._out[4 * i: 4 * i + 4]) for i in range(nd.value)]
+        return {"merges": merges, "early_stop": bool(es.value), "stalled": bool(st.value),
+                "need_list": int(nl.value), "need_win": int(nwn.value)}
+
+    def symbols(self):
+        n = C.c_uint64()
+        self._lib.check(self.lib.gbpe_trainer_symbols(self.t, None, 0, C.byref(n)), self.ctx, "symbols")
+        out = (C.c_uint32 * max(1, n.value))()
+        self._lib.check(self.lib.gbpe_trainer_symbols(self.t, out, n.value, C.byref(n)), self.ctx, "symbols")
+        return np.frombuffer(out, dtype=np.uint32, count=n.value).copy()
+
+    def stats(self):
+        st = self._lib.TrainerStats()
+        self.lib.gbpe_trainer_stats_get(self.t, C.byref(st))
+        return st
+
+    def close(self):
+        if self.t:
+            self.lib.gbpe_trainer_destroy(self.t)
+            self.t = None
