@@ -58,6 +58,7 @@ int gbpe_ctx_create(int device_ordinal, gbpe_ctx** out) {
         delete ctx;
         return GBPE_E_DEVICE;
     }
+    ctx->own_stream = ctx->stream;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device_ordinal) == hipSuccess) {
         ctx->total_mem = prop.totalGlobalMem;
@@ -84,8 +85,18 @@ void gbpe_ctx_destroy(gbpe_ctx* ctx) {
     if (ctx->enc_host_total) hipHostFree(ctx->enc_host_total);
     for (auto& ev : ctx->ev)
         if (ev) hipEventDestroy(ev);
-    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    if (ctx->own_stream) {
+        hipStreamSynchronize(ctx->own_stream);
+        hipStreamDestroy(ctx->own_stream);
+    }
     delete ctx;
+}
+
+int gbpe_ctx_set_stream(gbpe_ctx* ctx, void* stream) {
+    if (!ctx) return GBPE_E_INVALID;
+    GBPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
+    return GBPE_OK;
 }
 
 int gbpe_ctx_limits(gbpe_ctx* ctx, uint64_t* max_buffer_size) {

@@ -13,6 +13,7 @@
 struct gbpe_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;   // created by gbpe_ctx_create; `stream` may be a caller's
     uint64_t total_mem = 0;
     int num_cu = 0;
     std::string err;

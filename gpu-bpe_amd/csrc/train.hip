@@ -71,14 +71,32 @@ struct DevState {
     uint32_t live;         // distinct pairs with count > 0 at the last select
     uint64_t tail_total;   // sum of m
     uint32_t max_live;     // max of `live` over all selects
-    uint32_t ticket;       // tile tickets handed out in this merge (look-back order)
-    uint32_t epoch;        // merge sequence number tagging look-back granules
-    uint32_t rw_count;     // deferred in-place A-side rewrites of this merge
-    uint32_t pad[8];
+    uint32_t ticket;       // (unused)
+    uint32_t epoch;        // merge sequence number
+    uint32_t rw_count;     // (unused)
+    // ── sharded training (gbpe_shard_*); n / new_n above are then LOCAL: the
+    //    local stream length and the local keep limit ──
+    uint32_t sharded, rank, world, stall;
+    uint32_t dused;        // occupied slots of the per-merge delta table
+    uint32_t dcount;       // delta entries of this merge (the record's list length)
+    uint32_t need_l, need_w;   // capacities a stalled merge asked for (max over ranks)
+    uint32_t owner;        // rank that appended this merge's stale window
+    uint32_t nl_next;      // local length after this merge
+    uint32_t m_glob;       // global stale-window length of this merge
+    uint32_t pln;          // local length of the previous input stream (stale-window source)
+    uint64_t gn;           // global stream length
+    uint64_t off;          // global offset of the local stream
+    uint64_t poff;         // global offset of the previous input stream
+    uint64_t off_next;
+    uint64_t gnew;         // gn - mc
 };
-static_assert(sizeof(DevState) <= 128, "state");
+static_assert(sizeof(DevState) <= 256, "state");
 
-enum : uint32_t { ERR_TABLE_FULL = 1, ERR_COUNT_MISMATCH = 2, ERR_PAIR_MISSING = 4, ERR_SPIN = 8 };
+enum : uint32_t {
+    ERR_TABLE_FULL = 1, ERR_COUNT_MISMATCH = 2, ERR_PAIR_MISSING = 4, ERR_SPIN = 8,
+    ERR_SHARD_CAPACITY = 16,   // a rank's stream outgrew its buffers (stale window appended)
+    ERR_SHARD_RECORD = 32      // exchange records disagree (ranks out of step)
+};
 
 struct Table {
     uint2* slots;      // .x = pid (0 = empty), .y = count (u32, wraps for transient negatives)
@@ -88,6 +106,7 @@ struct Table {
     uint32_t* dlist;   // dirty block list
     uint32_t* blive;   // per block: entries with count > 0
     uint32_t nblk;
+    uint32_t* used;    // occupied-slot counter (DevState::used or ::dused)
 };
 
 // a touched block is re-maxed by the next k_refresh: a plain flag store, nothing waits on it
@@ -105,7 +124,7 @@ __device__ void table_add(const Table& tb, DevState* st, uint32_t pid, uint32_t 
         if (k == 0u) {
             k = atomicCAS(&tb.slots[idx].x, 0u, pid);
             if (k == 0u) {
-                __hip_atomic_fetch_add(&st->used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(tb.used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 k = pid;
             }
         }
@@ -249,10 +268,19 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
     __shared__ uint32_t rlive[TPB / 64];
     (void)cur;
     (void)rwlist;
-    if (finish && !st->stop && st->merges_done == round + 1u) {
+    if (finish && !st->stop && !st->stall && st->merges_done == round + 1u) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
-            st->tail_total += st->m;
-            st->n = st->new_n;
+            if (st->sharded) {   // commit the new global layout computed by k_shard_apply
+                st->tail_total += st->m_glob;
+                st->poff = st->off;
+                st->pln = st->n;
+                st->n = st->nl_next;
+                st->off = st->off_next;
+                st->gn = st->gnew;
+            } else {
+                st->tail_total += st->m;
+                st->n = st->new_n;
+            }
         }
     }
     // this WG's contiguous run of blocks: all flags in one load, then only the dirty ones
@@ -318,10 +346,10 @@ constexpr uint32_t GSTR = 64;   // group sums 256 B apart: each is its own atomi
 
 // argmax over block maxima + the reference's bpe_setup_merge (train.wgsl:340-364)
 __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, uint32_t* __restrict__ log,
-                                                        uint32_t* __restrict__ grpsum) {
+                                                        uint32_t* __restrict__ grpsum, uint32_t* __restrict__ nlog) {
     __shared__ uint64_t red[SEL_THREADS / 64];
     __shared__ uint32_t rlive[SEL_THREADS / 64];
-    if (st->stop) return;
+    if (st->stop || st->stall) return;
     {   // group sums of the coming stream pass start at zero
         const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(st->n, TILE), GRP);
         for (uint32_t g = threadIdx.x; g < ngrp; g += SEL_THREADS) grpsum[g * GSTR] = 0u;
@@ -352,6 +380,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
     if (live > st->max_live) st->max_live = live;
     st->ndirty = 0u;
     st->m = 0u;
+    st->dcount = 0u;
+    st->dused = 0u;
     st->valid_total = 0u;
     st->ticket = 0u;
     st->rw_count = 0u;
@@ -381,7 +411,16 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
     st->b = pid & 0xFFFFu;
     st->nw = st->next_id;
     st->mc = mc;
-    st->new_n = st->n - mc;
+    if (st->sharded) {   // global new length; the local keep limit (train.wgsl:727 on the global stream)
+        const uint64_t gnew = st->gn - mc;
+        st->gnew = gnew;
+        uint64_t lim = st->n;
+        if (!(st->sharded & 2u)) lim = gnew > st->off ? (gnew - st->off < st->n ? gnew - st->off : st->n) : 0u;
+        st->new_n = (uint32_t)lim;
+    } else {
+        st->new_n = st->n - mc;
+    }
+    if (nlog) nlog[d] = st->n;
     st->next_id += 1u;
     st->epoch += 1u;
     st->merges_done = d + 1u;
@@ -574,7 +613,7 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
     const uint32_t limit = EXACT ? n : new_n;
     const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
     if (tl >= ntiles) {
-        if (EXACT) return;
+        if (EXACT || st->sharded) return;   // sharded: the window is handled by k_shard_apply
         // ── stale tail window ──
         const uint32_t m = st->m;
         if (m == 0) return;
@@ -677,7 +716,8 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
         total += wsum[w2];
         prefix += psum[w2];
     }
-    if (tl == ntiles - 1 && t == 0 && prefix + tile_cnt[tl] != new_n) atomicOr(&st->err, ERR_COUNT_MISMATCH);
+    if (tl == ntiles - 1 && t == 0 && !st->sharded && prefix + tile_cnt[tl] != new_n)
+        atomicOr(&st->err, ERR_COUNT_MISMATCH);
     // stage at the destination's alignment phase so both sides move whole 16-byte words
     constexpr uint32_t VE = 16 / sizeof(S);           // symbols per 16-byte word
     const uint32_t ph = prefix & (VE - 1);
@@ -755,9 +795,13 @@ struct gbpe_trainer {
     uint32_t* hitmask = nullptr;
     uint32_t* tile_cnt = nullptr;
     uint32_t* grpsum = nullptr;
-    uint64_t* status = nullptr;    // look-back granules, one per tile
-    uint64_t* tailinfo = nullptr;  // {m, symbol before the stale window}
-    uint32_t* rwlist = nullptr;    // deferred in-place rewrites
+    // sharded training
+    bool sharded = false;
+    uint32_t rank = 0, world = 1;
+    Table dt{};                    // per-merge count-delta table (local deltas before the exchange)
+    uint32_t* d_nlog = nullptr;    // local length before each merge of a step
+    uint32_t* h_nlog = nullptr;    // pinned
+    uint32_t step_k = 0;
     // stats
     uint64_t bytes_moved = 0;
     uint64_t max_live = 0;
@@ -813,7 +857,8 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     S* oth = (S*)t->buf[t->cur ^ (round & 1) ^ 1];
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum);
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
+                       (uint32_t*)nullptr);
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
     if (exact) {
         hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
@@ -838,8 +883,9 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
 
 }  // namespace
 
-extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
-                                   int input_on_device, const gbpe_train_opts* opts, gbpe_trainer** out) {
+namespace {
+int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
+                        int input_on_device, const gbpe_train_opts* opts, uint64_t cap_extra, gbpe_trainer** out) {
     if (!ctx || !out || !opts) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
     *out = nullptr;
     if (n == 0) return gbpe_set_error(ctx, GBPE_E_EMPTY, "No symbols to train on — corpus is empty after pre-processing");
@@ -864,8 +910,11 @@ extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t
         gbpe_trainer_destroy(t);
         return code;
     };
-    // buffers padded to whole tiles (+1 tile for the halo / next-word reads)
-    const uint64_t ntiles0 = gbpe_div_up(n, TILE);
+    // buffers padded to whole tiles (+1 tile for the halo / next-word reads); a
+    // shard may also grow by appended stale windows (cap_extra symbols)
+    if (n + cap_extra >= 0xFFFFFFF0ull - 2 * TILE)
+        return fail(gbpe_set_error(ctx, GBPE_E_INVALID, "shard capacity too large for one device"));
+    const uint64_t ntiles0 = gbpe_div_up(n + cap_extra, TILE);
     t->cap_syms = (ntiles0 + 1) * TILE;
     for (int k = 0; k < 2; ++k) {
         if (hipMalloc(&t->buf[k], t->cap_syms * t->bps) != hipSuccess)
@@ -895,18 +944,14 @@ extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t
         hipMalloc(&t->hitmask, (ntiles0 + 1) * TPB * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->tile_cnt, (ntiles0 + 1) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->grpsum, (ntiles0 / GRP + 2) * GSTR * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->status, (ntiles0 + 2) * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc(&t->tailinfo, 2 * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc(&t->rwlist, (n / 2 + 2) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t->st, sizeof(DevState)) != hipSuccess ||
         hipMalloc(&t->d_log, (size_t)t->batch * 4 * sizeof(uint32_t)) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(training buffers) failed"));
     if (hipHostMalloc((void**)&t->h_st, sizeof(DevState), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&t->h_log, (size_t)t->batch * 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipHostMalloc failed"));
+    t->tb.used = &t->st->used;
     if (hipMemsetAsync(t->tb.dirty, 0, t->tb.nblk * sizeof(uint32_t), s) != hipSuccess ||
-        hipMemsetAsync(t->status, 0, (ntiles0 + 2) * sizeof(uint64_t), s) != hipSuccess ||
-        hipMemsetAsync(t->tailinfo, 0, 2 * sizeof(uint64_t), s) != hipSuccess ||
         hipMemsetAsync(t->hitmask, 0, (ntiles0 + 1) * TPB * sizeof(uint32_t), s) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "memset failed"));
     DevState init{};
@@ -955,6 +1000,12 @@ extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t
     if (hipStreamSynchronize(s) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "trainer init failed"));
     *out = t;
     return GBPE_OK;
+}
+}  // namespace
+
+extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
+                                   int input_on_device, const gbpe_train_opts* opts, gbpe_trainer** out) {
+    return trainer_create_impl(ctx, bytes, n, word_starts, input_on_device, opts, 0, out);
 }
 
 extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out, uint32_t* n_done,
@@ -1123,9 +1174,10 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->hitmask);
     hipFree(t->tile_cnt);
     hipFree(t->grpsum);
-    hipFree(t->status);
-    hipFree(t->tailinfo);
-    hipFree(t->rwlist);
+    hipFree(t->dt.slots);
+    hipFree(t->dt.dirty);
+    hipFree(t->d_nlog);
+    if (t->h_nlog) hipHostFree(t->h_nlog);
     hipFree(t->st);
     hipFree(t->d_log);
     if (t->h_st) hipHostFree(t->h_st);
@@ -1192,5 +1244,624 @@ extern "C" int gbpe_word_boundary(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t 
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     hipFree(d);
     if (e != hipSuccess) return gbpe_set_error(ctx, GBPE_E_DEVICE, "word boundary failed: %s", hipGetErrorString(e));
+    return GBPE_OK;
+}
+
+// ═══ sharded training (gbpe_shard_*) ═════════════════════════════════════════
+//
+// One rank per GPU; every rank keeps a replica of the GLOBAL pair-count table.
+// Per merge (protocol: gpubpe/sharded.py, pinned on CPU by tests/test_sharded.py):
+//   phase 1  k_select (on the replica) → k_delta (local sites; deltas into the
+//            per-merge delta table) → k_shard_list (delta table → record list,
+//            clearing it) → k_shard_header (header + this rank's piece of the
+//            stale-window superset [gnew - mc, gnew) of the previous input stream)
+//   host     one all-gather of the fixed-size records
+//   phase 2  k_shard_apply (every rank's deltas + the window's pairs into the
+//            replica, new global layout) → k_compact (local keep limit) →
+//            k_shard_append (the owner rank appends the window) → k_refresh.
+// A record that does not fit stalls the merge on every rank (selection undone).
+
+namespace {
+
+enum : uint32_t {
+    H_ACTIVE = 0, H_L, H_KEPT, H_M, H_W, H_LASTSYM, H_HASLAST, H_SURV, H_LN, H_MC, H_A, H_B, H_ID, HDR = 16
+};
+
+template <typename S>
+__device__ __forceinline__ uint32_t to_canon(uint32_t x) {
+    return (x & Sym<S>::TM) | ((x & Sym<S>::WS) ? 0x10000u : 0u);
+}
+template <typename S>
+__device__ __forceinline__ uint32_t from_canon(uint32_t x) {
+    return (x & 0xFFFFu) | ((x & 0x10000u) ? Sym<S>::WS : 0u);
+}
+
+// delta table (dirty blocks only) → record list {pid, delta}; clears what it reads
+__global__ __launch_bounds__(TPB) void k_shard_list(DevState* st, uint32_t round, Table dt, uint32_t* __restrict__ rec,
+                                                    uint32_t cap) {
+    __shared__ uint64_t s_dmask;
+    __shared__ uint32_t wcnt[TPB / 64], s_base;
+    if (!merge_active(st, round)) return;
+    const uint32_t per = (dt.nblk + gridDim.x - 1) / gridDim.x;
+    const uint32_t b0 = blockIdx.x * per;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x < 64) {
+        const uint32_t blk = b0 + threadIdx.x;
+        const bool d = threadIdx.x < per && blk < dt.nblk && dt.dirty[blk];
+        const unsigned long long m = __ballot(d);
+        if (threadIdx.x == 0) s_dmask = m;
+    }
+    __syncthreads();
+    uint64_t dm = s_dmask;
+    constexpr int NV = (1 << BLK_LOG2) / 2 / TPB;
+    while (dm) {
+        const uint32_t blk = b0 + (uint32_t)(__ffsll((long long)dm) - 1);
+        dm &= dm - 1;
+        uint4* sl = reinterpret_cast<uint4*>(dt.slots + ((uint64_t)blk << BLK_LOG2));
+        uint4 e[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) e[k] = sl[threadIdx.x + k * TPB];
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) c += (e[k].x && e[k].y) + (e[k].z && e[k].w);
+        uint32_t incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wcnt[wid] = incl;
+        __syncthreads();
+        uint32_t pre = incl - c, tot = 0;
+        for (int w = 0; w < TPB / 64; ++w) {
+            pre += w < wid ? wcnt[w] : 0u;
+            tot += wcnt[w];
+        }
+        if (threadIdx.x == 0) {
+            s_base = tot ? atomicAdd(&st->dcount, tot) : 0u;
+            dt.dirty[blk] = 0u;
+        }
+        __syncthreads();
+        uint32_t o = s_base + pre;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            if (e[k].x && e[k].y) {
+                if (o < cap) { rec[HDR + 2 * o] = e[k].x; rec[HDR + 2 * o + 1] = e[k].y; }
+                ++o;
+            }
+            if (e[k].z && e[k].w) {
+                if (o < cap) { rec[HDR + 2 * o] = e[k].z; rec[HDR + 2 * o + 1] = e[k].w; }
+                ++o;
+            }
+            if (e[k].x || e[k].z) sl[threadIdx.x + k * TPB] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        __syncthreads();
+    }
+}
+
+// record header + this rank's piece of the stale-window superset
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_shard_header(DevState* st, uint32_t round, const S* __restrict__ cur,
+                                                      const S* __restrict__ oth, const uint32_t* __restrict__ hitmask,
+                                                      const uint32_t* __restrict__ grpsum, uint32_t* __restrict__ rec,
+                                                      uint32_t cap_list, uint32_t cap_win) {
+    __shared__ uint32_t wred[TPB / 64];
+    if (!merge_active(st, round)) {
+        if (blockIdx.x == 0 && threadIdx.x < HDR) rec[threadIdx.x] = 0u;   // inactive round: ACTIVE = 0
+        return;
+    }
+    const bool exact = (st->sharded & 2u) != 0;
+    const uint32_t n = st->n, mc = st->mc;
+    // the stale-window superset [gnew - mc, gnew) ∩ this rank's previous input stream
+    uint32_t w = 0, src0 = 0;
+    if (!exact) {
+        const uint64_t hi = st->gnew, lo = hi >= mc ? hi - mc : 0;
+        const uint64_t a0 = lo > st->poff ? lo : st->poff;
+        const uint64_t pe = st->poff + st->pln;
+        const uint64_t a1 = hi < pe ? hi : pe;
+        if (a1 > a0) { w = (uint32_t)(a1 - a0); src0 = (uint32_t)(a0 - st->poff); }
+    }
+    const uint32_t wc = w < cap_win ? w : cap_win;
+    uint32_t* win = rec + HDR + 2 * (uint64_t)cap_list;
+    for (uint32_t i = blockIdx.x * TPB + threadIdx.x; i < wc; i += gridDim.x * TPB) win[i] = to_canon<S>(oth[src0 + i]);
+    if (blockIdx.x != 0) return;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // local survivors = sum of the group sums k_delta accumulated
+    const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(n, TILE), GRP);
+    uint32_t surv = 0;
+    for (uint32_t g = threadIdx.x; g < ngrp; g += TPB) surv += grpsum[g * GSTR];
+    for (int o = 32; o > 0; o >>= 1) surv += __shfl_xor(surv, o);
+    if (lane == 0) wred[wid] = surv;
+    __syncthreads();
+    surv = 0;
+    for (int k = 0; k < TPB / 64; ++k) surv += wred[k];
+    if (wid != 0) return;
+    // the last kept survivor: largest j < limit with hit(j) == 0, after the A-side rewrite
+    const uint32_t limit = st->new_n < n ? st->new_n : n;
+    int64_t wi = limit ? (int64_t)(limit - 1) / 32 : -1;
+    uint32_t found = 0xFFFFFFFFu;
+    while (wi >= 0 && found == 0xFFFFFFFFu) {
+        const int64_t mywi = wi - lane;
+        uint32_t inv = 0;
+        if (mywi >= 0) inv = ~hitmask[mywi] & lane_mask32((uint64_t)mywi * 32, limit);
+        const unsigned long long has = __ballot(inv != 0u);
+        if (has) {
+            const int l = __ffsll((long long)has) - 1;
+            const uint32_t inv_l = __shfl(inv, l);
+            found = (uint32_t)((wi - l) * 32 + (31 - __clz(inv_l)));
+        }
+        wi -= 64;
+    }
+    if (lane != 0) return;
+    uint32_t last = 0;
+    if (found != 0xFFFFFFFFu) {
+        last = cur[found];
+        const uint32_t f1 = found + 1;
+        if (f1 < n && ((hitmask[f1 / 32] >> (f1 % 32)) & 1u)) last = st->nw | (last & Sym<S>::WS);
+        last = to_canon<S>(last);
+    }
+    const uint32_t m_r = st->m;
+    rec[H_ACTIVE] = 1u;
+    rec[H_L] = st->dcount;
+    rec[H_KEPT] = surv - m_r;
+    rec[H_M] = m_r;
+    rec[H_W] = w;
+    rec[H_LASTSYM] = last;
+    rec[H_HASLAST] = found != 0xFFFFFFFFu ? 1u : 0u;
+    rec[H_SURV] = surv;
+    rec[H_LN] = n;
+    rec[H_MC] = mc;
+    rec[H_A] = st->a;
+    rec[H_B] = st->b;
+    rec[H_ID] = st->nw;
+    for (int k = H_ID + 1; k < HDR; ++k) rec[k] = 0u;
+}
+
+struct ShardView {   // per-WG decisions from the gathered headers (identical on every rank)
+    uint32_t L[64], W[64], K[64];
+    uint32_t lpre[65], wpre[65];
+    uint32_t m, owner, x0, has_x0, overflow, bad, max_l, max_w, surv;
+};
+
+__device__ void shard_view(const DevState* st, const uint32_t* __restrict__ recv, uint32_t R, uint32_t rw,
+                           uint32_t cap_list, uint32_t cap_win, ShardView& v) {
+    if (threadIdx.x < 64) {
+        const uint32_t q = threadIdx.x;
+        const uint32_t* h = recv + (uint64_t)q * rw;
+        const bool in = q < R;
+        const uint32_t L = in ? h[H_L] : 0u, W = in ? h[H_W] : 0u, K = in ? h[H_KEPT] : 0u;
+        const uint32_t M = in ? h[H_M] : 0u, S = in ? h[H_SURV] : 0u;
+        const bool bad = in && (h[H_ACTIVE] != 1u || h[H_MC] != st->mc || h[H_A] != st->a || h[H_B] != st->b ||
+                                h[H_ID] != st->nw);
+        const bool ovf = in && (L > cap_list || W > cap_win);
+        uint32_t li = L, wi = W;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t a = __shfl_up(li, o), b = __shfl_up(wi, o);
+            if ((int)q >= o) { li += a; wi += b; }
+        }
+        uint32_t m = M, surv = S, ml = L, mw = W;
+        for (int o = 32; o > 0; o >>= 1) {
+            m += __shfl_xor(m, o);
+            surv += __shfl_xor(surv, o);
+            ml = max(ml, (uint32_t)__shfl_xor(ml, o));
+            mw = max(mw, (uint32_t)__shfl_xor(mw, o));
+        }
+        const unsigned long long kept = __ballot(in && K > 0u);
+        const unsigned long long ob = __ballot(ovf), bb = __ballot(bad);
+        v.L[q] = L;
+        v.W[q] = W;
+        v.K[q] = K;
+        v.lpre[q + 1] = li;
+        v.wpre[q + 1] = wi;
+        if (q == 0) {
+            v.lpre[0] = 0u;
+            v.wpre[0] = 0u;
+            v.m = (st->sharded & 2u) ? 0u : m;
+            v.surv = surv;
+            v.overflow = ob != 0ull;
+            v.bad = bb != 0ull;
+            v.max_l = ml;
+            v.max_w = mw;
+            v.has_x0 = kept != 0ull;
+            v.owner = kept ? 63u - (uint32_t)__clzll((long long)kept) : 0u;
+            v.x0 = kept ? recv[(uint64_t)v.owner * rw + H_LASTSYM] : 0u;
+        }
+    }
+    __syncthreads();
+}
+
+// symbol g of the gathered superset (pieces in rank order)
+__device__ __forceinline__ uint32_t sup_at(const ShardView& v, const uint32_t* __restrict__ recv, uint32_t R,
+                                           uint32_t rw, uint32_t cap_list, uint32_t g) {
+    uint32_t q = 0;
+    while (q + 1 < R && v.wpre[q + 1] <= g) ++q;
+    return recv[(uint64_t)q * rw + HDR + 2 * cap_list + (g - v.wpre[q])];
+}
+
+__global__ __launch_bounds__(TPB) void k_shard_apply(DevState* st, uint32_t round, const uint32_t* __restrict__ recv,
+                                                     uint32_t R, uint32_t cap_list, uint32_t cap_win, Table tb,
+                                                     uint32_t cap_syms) {
+    __shared__ ShardView v;
+    __shared__ LdsTab<LTAB> lt;
+    if (!merge_active(st, round)) return;
+    const uint32_t rw = HDR + 2 * cap_list + cap_win;
+    shard_view(st, recv, R, rw, cap_list, cap_win, v);
+    if (v.bad) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) { atomicOr(&st->err, ERR_SHARD_RECORD); st->stop = 1u; }
+        return;
+    }
+    if (v.overflow) {   // stall on every rank: undo k_select's bookkeeping, ask the host for room
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            const uint32_t pid = (st->a << 16) | st->b;
+            const uint32_t idx = table_find(tb, pid);
+            if (idx != 0xFFFFFFFFu) {
+                tb.slots[idx].y = st->mc;
+                tb.dirty[idx >> BLK_LOG2] = 1u;
+            }
+            st->next_id -= 1u;
+            st->epoch -= 1u;
+            st->merges_done -= 1u;
+            st->stall = 1u;
+            st->need_l = v.max_l;
+            st->need_w = v.max_w;
+        }
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // new global layout
+        uint64_t tot = 0, before = 0;
+        uint32_t mine = 0;
+        for (uint32_t q = 0; q < R; ++q) {
+            const uint64_t nl = (uint64_t)v.K[q] + (q == v.owner ? v.m : 0u);
+            if (q < st->rank) before += nl;
+            if (q == st->rank) mine = (uint32_t)nl;
+            tot += nl;
+        }
+        if (tot != st->gnew || (uint64_t)v.surv != st->gn - st->mc) atomicOr(&st->err, ERR_SHARD_RECORD);
+        if ((uint64_t)mine + TILE > cap_syms) atomicOr(&st->err, ERR_SHARD_CAPACITY);
+        st->owner = v.owner;
+        st->m_glob = v.m;
+        st->nl_next = mine;
+        st->off_next = before;
+    }
+    // every rank's count deltas into the replica
+    const uint32_t total = v.lpre[R];
+    for (uint32_t e = blockIdx.x * TPB + threadIdx.x; e < total; e += gridDim.x * TPB) {
+        uint32_t q = 0;
+        while (q + 1 < R && v.lpre[q + 1] <= e) ++q;
+        const uint32_t* l = recv + (uint64_t)q * rw + HDR + 2 * (e - v.lpre[q]);
+        table_add(tb, st, l[0], l[1]);
+    }
+    // pairs of the stale window = last m symbols of the superset, after x0
+    const uint32_t m = v.m;
+    if (m == 0) return;
+    lds_clear(lt);
+    __syncthreads();
+    const uint32_t sup = v.wpre[R], g0 = sup - m;
+    for (uint32_t j = blockIdx.x * TPB + threadIdx.x; j < m; j += gridDim.x * TPB) {
+        uint32_t xp;
+        if (j == 0) {
+            if (!v.has_x0) continue;
+            xp = v.x0;
+        } else {
+            xp = sup_at(v, recv, R, rw, cap_list, g0 + j - 1);
+        }
+        const uint32_t x = sup_at(v, recv, R, rw, cap_list, g0 + j);
+        const uint32_t t0 = xp & 0xFFFFu, t1 = x & 0xFFFFu;
+        if (!(x & 0x10000u) && t0 && t1) lds_add(lt, tb, st, (t0 << 16) | t1, 1u);
+    }
+    lds_flush(lt, tb, st);
+}
+
+// the owner rank appends the stale window after its kept survivors
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_shard_append(DevState* st, uint32_t round, const uint32_t* __restrict__ recv,
+                                                      uint32_t R, uint32_t cap_list, uint32_t cap_win,
+                                                      S* __restrict__ oth) {
+    __shared__ ShardView v;
+    if (!merge_active(st, round)) return;
+    const uint32_t m = st->m_glob;
+    if (m == 0 || st->owner != st->rank || (st->err & ERR_SHARD_CAPACITY)) return;
+    const uint32_t rw = HDR + 2 * cap_list + cap_win;
+    shard_view(st, recv, R, rw, cap_list, cap_win, v);
+    const uint32_t kept = v.K[st->rank];
+    const uint32_t g0 = v.wpre[R] - m;
+    for (uint32_t j = blockIdx.x * TPB + threadIdx.x; j < m; j += gridDim.x * TPB)
+        oth[kept + j] = (S)from_canon<S>(sup_at(v, recv, R, rw, cap_list, g0 + j));
+}
+
+__global__ void k_add_list(DevState* st, Table tb, const uint2* __restrict__ list, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && list[i].x && list[i].y) table_add(tb, st, list[i].x, list[i].y);
+}
+
+__global__ void k_dump_list(Table tb, uint2* __restrict__ out, uint32_t* __restrict__ nout, uint32_t cap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > tb.mask) return;
+    const uint2 e = tb.slots[i];
+    if (e.x && (int32_t)e.y > 0) {
+        const uint32_t k = atomicAdd(nout, 1u);
+        if (k < cap) out[k] = e;
+    }
+}
+
+}  // namespace
+
+// ─── sharded host API ───────────────────────────────────────────────────────
+
+namespace {
+inline uint32_t shard_record_words(uint32_t cl, uint32_t cw) { return HDR + 2 * cl + cw; }
+}  // namespace
+
+extern "C" int gbpe_shard_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
+                                 int input_on_device, const gbpe_train_opts* opts, uint32_t rank, uint32_t world,
+                                 uint64_t cap_extra, gbpe_trainer** out) {
+    if (!ctx || !out || !opts) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
+    if (world == 0 || world > 64 || rank >= world) return gbpe_set_error(ctx, GBPE_E_INVALID, "rank/world out of range (world <= 64)");
+    int rc = trainer_create_impl(ctx, bytes, n, word_starts, input_on_device, opts, cap_extra, out);
+    if (rc != GBPE_OK) return rc;
+    gbpe_trainer* t = *out;
+    t->sharded = true;
+    t->rank = rank;
+    t->world = world;
+    t->dt.mask = t->tb.mask;
+    t->dt.nblk = t->tb.nblk;
+    t->dt.used = &t->st->dused;
+    const uint64_t slots = (uint64_t)t->tb.mask + 1;
+    hipStream_t s = ctx->stream;
+    if (hipMalloc(&t->dt.slots, slots * sizeof(uint2)) != hipSuccess ||
+        hipMalloc(&t->dt.dirty, t->dt.nblk * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->d_nlog, (size_t)t->batch * sizeof(uint32_t)) != hipSuccess ||
+        hipHostMalloc((void**)&t->h_nlog, (size_t)t->batch * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+        gbpe_trainer_destroy(t);
+        *out = nullptr;
+        return gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(shard buffers) failed");
+    }
+    t->h_st->sharded = 1u | ((t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 2u : 0u);
+    t->h_st->rank = rank;
+    t->h_st->world = world;
+    if (hipMemsetAsync(t->dt.slots, 0, slots * sizeof(uint2), s) != hipSuccess ||
+        hipMemsetAsync(t->dt.dirty, 0, t->dt.nblk * sizeof(uint32_t), s) != hipSuccess ||
+        hipMemcpyAsync(&t->st->sharded, &t->h_st->sharded, 3 * sizeof(uint32_t), hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+        gbpe_trainer_destroy(t);
+        *out = nullptr;
+        return gbpe_set_error(ctx, GBPE_E_DEVICE, "shard init failed");
+    }
+    return GBPE_OK;
+}
+
+extern "C" int gbpe_shard_local_len(gbpe_trainer* t, uint64_t* n) {
+    if (!t || !n) return GBPE_E_INVALID;
+    *n = t->n;
+    return GBPE_OK;
+}
+
+extern "C" int gbpe_shard_set_layout(gbpe_trainer* t, const uint64_t* lens, uint32_t world) {
+    if (!t || !lens || !t->sharded || world != t->world) return t ? gbpe_set_error(t->ctx, GBPE_E_INVALID, "set_layout: bad arguments") : GBPE_E_INVALID;
+    if (lens[t->rank] != t->n) return gbpe_set_error(t->ctx, GBPE_E_INVALID, "set_layout: own length mismatch");
+    uint64_t gn = 0, off = 0;
+    for (uint32_t q = 0; q < world; ++q) {
+        if (q < t->rank) off += lens[q];
+        gn += lens[q];
+    }
+    if (gn >= 0xFFFFFFFFFFull) return gbpe_set_error(t->ctx, GBPE_E_INVALID, "global corpus too large");
+    DevState* hs = t->h_st;
+    hs->gn = gn;
+    hs->off = off;
+    hs->poff = off;      // the previous input stream before merge 1: the zeroed ping-pong buffer
+    hs->pln = t->n;
+    hipStream_t s = t->ctx->stream;
+    const size_t o = offsetof(DevState, sharded);   // only the shard section: the rest lives on the device
+    TR_HIP(t, hipMemcpyAsync((char*)t->st + o, (char*)hs + o, sizeof(DevState) - o, hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    return GBPE_OK;
+}
+
+extern "C" int gbpe_shard_export_counts(gbpe_trainer* t, void* d_out, uint64_t cap, uint64_t* n_pairs) {
+    if (!t || !n_pairs) return GBPE_E_INVALID;
+    hipStream_t s = t->ctx->stream;
+    uint32_t* d_cnt = nullptr;
+    TR_HIP(t, hipMalloc(&d_cnt, sizeof(uint32_t)));
+    hipError_t e = hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), s);
+    const uint64_t slots = (uint64_t)t->tb.mask + 1;
+    hipLaunchKernelGGL(k_dump_list, dim3((uint32_t)gbpe_div_up(slots, 256)), dim3(256), 0, s, t->tb, (uint2*)d_out,
+                       d_cnt, d_out ? (uint32_t)cap : 0u);
+    uint32_t cnt = 0;
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(&cnt, d_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipFree(d_cnt);
+    if (e != hipSuccess) return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "export_counts failed: %s", hipGetErrorString(e));
+    *n_pairs = cnt;
+    if (d_out && cnt > cap) return gbpe_set_error(t->ctx, GBPE_E_CAPACITY, "export_counts: need %u", cnt);
+    return GBPE_OK;
+}
+
+extern "C" int gbpe_shard_import_counts(gbpe_trainer* t, const void* d_lists, const uint64_t* counts, uint32_t world,
+                                        uint64_t stride) {
+    if (!t || !d_lists || !counts || world != t->world) return t ? gbpe_set_error(t->ctx, GBPE_E_INVALID, "import_counts: bad arguments") : GBPE_E_INVALID;
+    hipStream_t s = t->ctx->stream;
+    const uint64_t slots = (uint64_t)t->tb.mask + 1;
+    TR_HIP(t, hipMemsetAsync(t->tb.slots, 0, slots * sizeof(uint2), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.bmax, 0, (uint64_t)t->tb.nblk * sizeof(uint64_t), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.blive, 0, (uint64_t)t->tb.nblk * sizeof(uint32_t), s));
+    TR_HIP(t, hipMemsetAsync(&t->st->used, 0, sizeof(uint32_t), s));
+    const uint2* base = (const uint2*)d_lists;
+    for (uint32_t q = 0; q < world; ++q) {
+        if (counts[q] == 0) continue;
+        hipLaunchKernelGGL(k_add_list, dim3((uint32_t)gbpe_div_up(counts[q], 256)), dim3(256), 0, s, t->st, t->tb,
+                           base + q * stride, counts[q]);
+    }
+    hipLaunchKernelGGL(k_clear_dirty_all, dim3((uint32_t)gbpe_div_up(t->tb.nblk, 256)), dim3(256), 0, s, t->st, t->tb);
+    if (t->u16)
+        hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st,
+                           0u, 0, t->tb, (uint16_t*)nullptr, (const uint32_t*)nullptr);
+    else
+        hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st,
+                           0u, 0, t->tb, (uint32_t*)nullptr, (const uint32_t*)nullptr);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    if (t->h_st->err) return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "import_counts: table error 0x%x", t->h_st->err);
+    return GBPE_OK;
+}
+
+namespace {
+// rebuild a crowded replica without the stream (the table holds GLOBAL counts)
+int shard_rehash(gbpe_trainer* t) {
+    uint64_t P = 0;
+    int rc = gbpe_shard_export_counts(t, nullptr, 0, &P);
+    if (rc != GBPE_OK) return rc;
+    void* d = nullptr;
+    TR_HIP(t, hipMalloc(&d, (P + 1) * sizeof(uint2)));
+    rc = gbpe_shard_export_counts(t, d, P, &P);
+    if (rc == GBPE_OK) {
+        const uint64_t cnt[1] = {P};
+        const uint32_t w = t->world;
+        t->world = 1;   // import a single list
+        rc = gbpe_shard_import_counts(t, d, cnt, 1, 0);
+        t->world = w;
+    }
+    hipFree(d);
+    return rc;
+}
+}  // namespace
+
+extern "C" int gbpe_shard_record_words(uint32_t cap_list, uint32_t cap_win) {
+    return (int)shard_record_words(cap_list, cap_win);
+}
+
+extern "C" int gbpe_shard_step_begin(gbpe_trainer* t, uint32_t max_merges) {
+    if (!t || !t->sharded) return GBPE_E_INVALID;
+    uint32_t k = max_merges ? max_merges : t->batch;
+    if (k > t->batch) k = t->batch;
+    if (t->done + k > t->needed) k = t->needed - t->done;
+    t->step_k = t->stop ? 0u : k;
+    if (t->step_k == 0) return GBPE_OK;
+    const uint64_t slots = (uint64_t)t->tb.mask + 1;
+    if ((uint64_t)t->h_st->used * 2 > slots) {
+        int rc = shard_rehash(t);
+        if (rc != GBPE_OK) return rc;
+    }
+    DevState* hs = t->h_st;
+    hs->merges_done = 0;
+    hs->budget = t->step_k;
+    hs->stall = 0;
+    hipStream_t s = t->ctx->stream;
+    TR_HIP(t, hipMemcpyAsync(&t->st->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(&t->st->budget, &hs->budget, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(&t->st->stall, &hs->stall, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    return GBPE_OK;
+}
+
+namespace {
+template <typename S>
+int shard_phase1(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl, uint32_t cw) {
+    hipStream_t s = t->ctx->stream;
+    S* cur = (S*)t->buf[t->cur ^ (round & 1)];
+    S* oth = (S*)t->buf[t->cur ^ (round & 1) ^ 1];
+    const uint64_t ntiles = gbpe_div_up(t->n, TILE) + 1;   // the stream may have grown by a window
+    const uint32_t g_delta = (uint32_t)gbpe_div_up(t->cap_syms, TILE) - 1;
+    (void)ntiles;
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum, t->d_nlog);
+    if (t->flags & GBPE_TRAIN_EXACT_COMPACTION)
+        hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->dt,
+                           t->hitmask, t->tile_cnt, t->grpsum);
+    else
+        hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->dt,
+                           t->hitmask, t->tile_cnt, t->grpsum);
+    hipLaunchKernelGGL(k_shard_list, dim3(grid_persistent(t->ctx, t->dt.nblk, 2)), dim3(TPB), 0, s, t->st, round, t->dt,
+                       rec, cl);
+    hipLaunchKernelGGL(k_shard_header<S>, dim3(grid_persistent(t->ctx, gbpe_div_up(cw, TPB * 8) + 1, 1)), dim3(TPB), 0,
+                       s, t->st, round, (const S*)cur, (const S*)oth, (const uint32_t*)t->hitmask,
+                       (const uint32_t*)t->grpsum, rec, cl, cw);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+
+template <typename S>
+int shard_phase2(gbpe_trainer* t, uint32_t round, const uint32_t* recv, uint32_t cl, uint32_t cw) {
+    hipStream_t s = t->ctx->stream;
+    S* cur = (S*)t->buf[t->cur ^ (round & 1)];
+    S* oth = (S*)t->buf[t->cur ^ (round & 1) ^ 1];
+    const uint32_t R = t->world;
+    const uint32_t g_tiles = (uint32_t)gbpe_div_up(t->cap_syms, TILE) - 1;
+    const uint32_t cap = (uint32_t)t->cap_syms;
+    hipLaunchKernelGGL(k_shard_apply, dim3(grid_persistent(t->ctx, 1u << 20, 2)), dim3(TPB), 0, s, t->st, round, recv, R,
+                       cl, cw, t->tb, cap);
+    if (t->flags & GBPE_TRAIN_EXACT_COMPACTION)
+        hipLaunchKernelGGL((k_compact<S, true>), dim3(g_tiles), dim3(CTPB), 0, s, t->st, round, cur, oth,
+                           (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
+    else
+        hipLaunchKernelGGL((k_compact<S, false>), dim3(g_tiles), dim3(CTPB), 0, s, t->st, round, cur, oth,
+                           (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
+    hipLaunchKernelGGL(k_shard_append<S>, dim3(grid_persistent(t->ctx, 1u << 20, 1)), dim3(TPB), 0, s, t->st, round,
+                       recv, R, cl, cw, oth);
+    hipLaunchKernelGGL(k_refresh<S>, dim3(grid_persistent(t->ctx, t->tb.nblk, 2)), dim3(TPB), 0, s, t->st, round, 1,
+                       t->tb, cur, (const uint32_t*)nullptr);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+}  // namespace
+
+extern "C" int gbpe_shard_phase1(gbpe_trainer* t, uint32_t round, void* d_send, uint32_t cap_list, uint32_t cap_win) {
+    if (!t || !t->sharded || !d_send) return GBPE_E_INVALID;
+    if (round >= t->batch) return gbpe_set_error(t->ctx, GBPE_E_INVALID, "round out of range");
+    if (round >= t->step_k) {   // nothing to do this round, but the record must say so
+        TR_HIP(t, hipMemsetAsync(d_send, 0, HDR * sizeof(uint32_t), t->ctx->stream));
+        return GBPE_OK;
+    }
+    return t->u16 ? shard_phase1<uint16_t>(t, round, (uint32_t*)d_send, cap_list, cap_win)
+                  : shard_phase1<uint32_t>(t, round, (uint32_t*)d_send, cap_list, cap_win);
+}
+
+extern "C" int gbpe_shard_phase2(gbpe_trainer* t, uint32_t round, const void* d_recv, uint32_t cap_list,
+                                 uint32_t cap_win) {
+    if (!t || !t->sharded || !d_recv) return GBPE_E_INVALID;
+    if (round >= t->step_k) return GBPE_OK;
+    return t->u16 ? shard_phase2<uint16_t>(t, round, (const uint32_t*)d_recv, cap_list, cap_win)
+                  : shard_phase2<uint32_t>(t, round, (const uint32_t*)d_recv, cap_list, cap_win);
+}
+
+extern "C" int gbpe_shard_step_end(gbpe_trainer* t, uint32_t* merges_out, uint32_t* n_done, uint32_t* early_stop,
+                                   uint32_t* stalled, uint32_t* need_list, uint32_t* need_win) {
+    if (!t || !t->sharded) return GBPE_E_INVALID;
+    if (n_done) *n_done = 0;
+    if (stalled) *stalled = 0;
+    if (need_list) *need_list = 0;
+    if (need_win) *need_win = 0;
+    if (early_stop) *early_stop = t->stop ? 1u : 0u;
+    if (t->step_k == 0) return GBPE_OK;
+    hipStream_t s = t->ctx->stream;
+    DevState* hs = t->h_st;
+    TR_HIP(t, hipMemcpyAsync(hs, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipMemcpyAsync(t->h_log, t->d_log, (size_t)t->step_k * 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipMemcpyAsync(t->h_nlog, t->d_nlog, (size_t)t->step_k * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    if (hs->err) {
+        return gbpe_set_error(t->ctx, (hs->err & ERR_SHARD_CAPACITY) ? GBPE_E_CAPACITY : GBPE_E_INTERNAL,
+                              "sharded training invariant violated (err=0x%x: %s%s%s%s)", hs->err,
+                              (hs->err & ERR_TABLE_FULL) ? "pair table full " : "",
+                              (hs->err & ERR_PAIR_MISSING) ? "selected pair missing " : "",
+                              (hs->err & ERR_SHARD_CAPACITY) ? "shard buffer too small for appended windows " : "",
+                              (hs->err & ERR_SHARD_RECORD) ? "exchange records disagree" : "");
+    }
+    const uint32_t done = hs->merges_done;
+    // local algorithmic stream bytes s * (2 N_i + N_{i+1}) with the local lengths
+    for (uint32_t r = 0; r < done; ++r) {
+        const uint64_t N = t->h_nlog[r];
+        const uint64_t N1 = r + 1 < done ? t->h_nlog[r + 1] : hs->n;
+        t->bytes_moved += (uint64_t)t->bps * (2 * N + N1);
+        if (merges_out) memcpy(merges_out + 4 * r, t->h_log + 4 * r, 4 * sizeof(uint32_t));
+    }
+    t->n = hs->n;
+    t->cur ^= (done & 1u);
+    t->done += done;
+    t->stop = hs->stop != 0;
+    t->step_k = 0;
+    if (n_done) *n_done = done;
+    if (early_stop) *early_stop = t->stop ? 1u : 0u;
+    if (stalled) *stalled = hs->stall;
+    if (need_list) *need_list = hs->need_l;
+    if (need_win) *need_win = hs->need_w;
     return GBPE_OK;
 }

@@ -156,9 +156,11 @@ class GpuShardBackend:
 
     def __init__(self, lib, ctx, data, word_starts, rank: int, world: int, target_vocab: int,
                  exact: bool = False, input_on_device: bool = False, n: int | None = None,
-                 table_log2: int = 0, cap_extra: int = 0):
+                 table_log2: int = 0, cap_extra: int = 0, stream=None):
         from . import _lib
         self.lib, self.ctx, self._lib = lib, ctx, _lib
+        if stream is not None:   # run on the caller's stream (torch's), so its collectives and copies are ordered
+            _lib.check(lib.gbpe_ctx_set_stream(ctx, C.c_void_p(stream)), ctx, "gbpe_ctx_set_stream")
         flags = _lib.GBPE_TRAIN_EXACT_COMPACTION if exact else 0
         self.opts = _lib.TrainOpts(target_vocab_size=target_vocab, vocab_size=256, next_token_id=256,
                                    batch_size=BATCH_SIZE, flags=flags, table_log2=table_log2)
@@ -167,11 +169,12 @@ class GpuShardBackend:
             ptr, nn = data, n
         else:
             buf = bytes(data)
-            ptr, nn = buf, len(buf)
+            ptr, nn = C.create_string_buffer(buf, len(buf)), len(buf)
+        self._keep = ptr
         ws = None
         if word_starts is not None:
             wsb = np.ascontiguousarray(np.asarray(word_starts, dtype=np.uint8))
-            ws = wsb.ctypes.data_as(C.POINTER(C.c_uint8))
+            ws = wsb.ctypes.data_as(C.c_void_p)
             self._ws_keep = wsb
         _lib.check(lib.gbpe_shard_create(ctx, ptr, nn, ws, 1 if input_on_device else 0, C.byref(self.opts),
                                          rank, world, cap_extra, C.byref(t)), ctx, "gbpe_shard_create")

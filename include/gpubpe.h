@@ -146,6 +146,38 @@ int gbpe_trainer_symbols(gbpe_trainer* t, uint32_t* out, uint64_t cap, uint64_t*
 int gbpe_trainer_pair_counts(gbpe_trainer* t, uint32_t* pids, uint32_t* counts, uint64_t cap, uint64_t* n);
 void gbpe_trainer_destroy(gbpe_trainer* t);
 
+/* ── sharded training: one rank per GPU ──────────────────────
+ * The reference trains on one WebGPU device (training-pipeline.js:178-222);
+ * these entry points run the same merge loop over a corpus cut at word starts
+ * into one shard per rank, bit-exact to the single-stream run.  Each rank keeps
+ * a replica of the global pair-count table; every merge exchanges one
+ * fixed-size record per rank (gbpe_shard_record_words(C, Cw) u32 words) with
+ * an all-gather the CALLER performs between phase 1 and phase 2 (RCCL via
+ * torch.distributed on the stream set with gbpe_ctx_set_stream; gloo in tests).
+ * Protocol and host loop: gpu-bpe_amd/gpubpe/sharded.py.
+ *   create → local_len → (all-gather lengths) set_layout → export_counts →
+ *   (all-gather lists) import_counts → per step: step_begin, per merge k
+ *   {phase1(k, send) ; all_gather(recv, send) ; phase2(k, recv)}, step_end.
+ * A merge whose record needs more than (C, Cw) stalls on every rank; step_end
+ * reports it with the capacities needed, and the next step redoes it. */
+int gbpe_ctx_set_stream(gbpe_ctx* ctx, void* hip_stream);   /* NULL = the context's own stream */
+int gbpe_shard_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
+                      int input_on_device, const gbpe_train_opts* opts, uint32_t rank, uint32_t world,
+                      uint64_t cap_extra /* symbols of room for appended stale windows */, gbpe_trainer** out);
+int gbpe_shard_local_len(gbpe_trainer* t, uint64_t* n);
+int gbpe_shard_set_layout(gbpe_trainer* t, const uint64_t* lens, uint32_t world);
+/* device list of {pid, count} u32 pairs of the local stream; d_out NULL = count only */
+int gbpe_shard_export_counts(gbpe_trainer* t, void* d_out, uint64_t cap, uint64_t* n_pairs);
+/* d_lists: world lists of {pid, count}, list q at d_lists + q*stride pairs, counts[q] entries */
+int gbpe_shard_import_counts(gbpe_trainer* t, const void* d_lists, const uint64_t* counts, uint32_t world,
+                             uint64_t stride);
+int gbpe_shard_record_words(uint32_t cap_list, uint32_t cap_win);
+int gbpe_shard_step_begin(gbpe_trainer* t, uint32_t max_merges);
+int gbpe_shard_phase1(gbpe_trainer* t, uint32_t round, void* d_send, uint32_t cap_list, uint32_t cap_win);
+int gbpe_shard_phase2(gbpe_trainer* t, uint32_t round, const void* d_recv, uint32_t cap_list, uint32_t cap_win);
+int gbpe_shard_step_end(gbpe_trainer* t, uint32_t* merges_out, uint32_t* n_done, uint32_t* early_stop,
+                        uint32_t* stalled, uint32_t* need_list, uint32_t* need_win);
+
 /* ── trie encode (replaces tokenizer.js:54-335 TrieTokenizer over the
  *    tokenize.wgsl kernels) ─────────────────────────────────────────────── */
 
