@@ -95,9 +95,11 @@ void gbpe_ctx_destroy(gbpe_ctx* ctx) {
 int gbpe_ctx_set_stream(gbpe_ctx* ctx, void* stream) {
     if (!ctx) return GBPE_E_INVALID;
     GBPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
+    ctx->stream = (hipStream_t)stream;   // taken literally: NULL is the device's null stream
     return GBPE_OK;
 }
+
+void* gbpe_ctx_get_stream(gbpe_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 int gbpe_ctx_limits(gbpe_ctx* ctx, uint64_t* max_buffer_size) {
     if (!ctx || !max_buffer_size) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");

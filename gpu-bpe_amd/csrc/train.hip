@@ -95,7 +95,8 @@ static_assert(sizeof(DevState) <= 256, "state");
 enum : uint32_t {
     ERR_TABLE_FULL = 1, ERR_COUNT_MISMATCH = 2, ERR_PAIR_MISSING = 4, ERR_SPIN = 8,
     ERR_SHARD_CAPACITY = 16,   // a rank's stream outgrew its buffers (stale window appended)
-    ERR_SHARD_RECORD = 32      // exchange records disagree (ranks out of step)
+    ERR_SHARD_RECORD = 32,     // exchange records disagree (ranks out of step)
+    ERR_SHARD_LAYOUT = 64      // gathered survivor / length totals do not add up
 };
 
 struct Table {
@@ -1515,7 +1516,11 @@ __global__ __launch_bounds__(TPB) void k_shard_apply(DevState* st, uint32_t roun
             if (q == st->rank) mine = (uint32_t)nl;
             tot += nl;
         }
-        if (tot != st->gnew || (uint64_t)v.surv != st->gn - st->mc) atomicOr(&st->err, ERR_SHARD_RECORD);
+        if (tot != st->gnew || (uint64_t)v.surv != st->gn - st->mc) {
+            atomicOr(&st->err, ERR_SHARD_LAYOUT);
+            st->need_l = (uint32_t)tot;      // diagnostics for the host message
+            st->need_w = v.surv;
+        }
         if ((uint64_t)mine + TILE > cap_syms) atomicOr(&st->err, ERR_SHARD_CAPACITY);
         st->owner = v.owner;
         st->m_glob = v.m;
@@ -1839,11 +1844,15 @@ extern "C" int gbpe_shard_step_end(gbpe_trainer* t, uint32_t* merges_out, uint32
     TR_HIP(t, hipStreamSynchronize(s));
     if (hs->err) {
         return gbpe_set_error(t->ctx, (hs->err & ERR_SHARD_CAPACITY) ? GBPE_E_CAPACITY : GBPE_E_INTERNAL,
-                              "sharded training invariant violated (err=0x%x: %s%s%s%s)", hs->err,
+                              "sharded training invariant violated (err=0x%x: %s%s%s%s%s; merge %u, n %u, gn %llu, "
+                              "gnew %llu, mc %u, new len total %u, survivors %u)", hs->err,
                               (hs->err & ERR_TABLE_FULL) ? "pair table full " : "",
                               (hs->err & ERR_PAIR_MISSING) ? "selected pair missing " : "",
                               (hs->err & ERR_SHARD_CAPACITY) ? "shard buffer too small for appended windows " : "",
-                              (hs->err & ERR_SHARD_RECORD) ? "exchange records disagree" : "");
+                              (hs->err & ERR_SHARD_RECORD) ? "exchange records disagree " : "",
+                              (hs->err & ERR_SHARD_LAYOUT) ? "gathered totals do not add up" : "",
+                              t->done + hs->merges_done, hs->n, (unsigned long long)hs->gn,
+                              (unsigned long long)hs->gnew, hs->mc, hs->need_l, hs->need_w);
     }
     const uint32_t done = hs->merges_done;
     // local algorithmic stream bytes s * (2 N_i + N_{i+1}) with the local lengths

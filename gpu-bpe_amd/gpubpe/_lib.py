@@ -83,6 +83,7 @@ _SIGS = [
     ("gbpe_memcpy_d2h", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     ("gbpe_synchronize", C.c_int, [C.c_void_p]),
     ("gbpe_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("gbpe_ctx_get_stream", C.c_void_p, [C.c_void_p]),
     ("gbpe_shard_create", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int, C.POINTER(TrainOpts),
                                     C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_void_p)]),
     ("gbpe_shard_local_len", C.c_int, [C.c_void_p, u64p]),

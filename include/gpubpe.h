@@ -160,7 +160,8 @@ void gbpe_trainer_destroy(gbpe_trainer* t);
  *   {phase1(k, send) ; all_gather(recv, send) ; phase2(k, recv)}, step_end.
  * A merge whose record needs more than (C, Cw) stalls on every rank; step_end
  * reports it with the capacities needed, and the next step redoes it. */
-int gbpe_ctx_set_stream(gbpe_ctx* ctx, void* hip_stream);   /* NULL = the context's own stream */
+int gbpe_ctx_set_stream(gbpe_ctx* ctx, void* hip_stream);   /* taken literally (NULL = the null stream) */
+void* gbpe_ctx_get_stream(gbpe_ctx* ctx);                    /* current stream (save / restore) */
 int gbpe_shard_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
                       int input_on_device, const gbpe_train_opts* opts, uint32_t rank, uint32_t world,
                       uint64_t cap_extra /* symbols of room for appended stale windows */, gbpe_trainer** out);

@@ -42,6 +42,7 @@ def _worker(rank, world, port, case, outdir):
         d, ws = shards[rank]
         be = GpuShardBackend(lib, ctx, d, ws, rank, world, case["vocab"], exact=case["exact"],
                              table_log2=16, cap_extra=len(data), stream=torch.cuda.current_stream().cuda_stream)
+        assert lib.gbpe_ctx_get_stream(ctx) == (torch.cuda.current_stream().cuda_stream or None)
         tr = ShardedTrainer(be, dist, device="cuda", staged=True, cap_list=case["cap"], cap_win=case["cap"])
         tr.setup()
         merges, early = tr.train(case["vocab"], batch=case.get("batch", 128))
