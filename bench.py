@@ -11,10 +11,15 @@ word boundaries, initial pair count) plus K steps.  `value` = merges / s.
 Secondary leg (configs[2], C3): chunked trie encode of 1 GiB synthetic
 multilingual text with a 32K vocab trained on a 100 MiB sample (seed 4).
 
-Multi-GPU (--gpus N under torch.distributed.run): N>1 is not yet sharded
-(SURVEY §8(e) training needs a per-merge count exchange, planned); each rank
-runs the same single-GPU workload as an independent replica and the line
-reports `"parallelism": "replicas"`.
+Multi-GPU (--gpus N under torch.distributed.run, one rank per GPU): sharded
+training (gpubpe.sharded).  Each rank holds a 104,857,600-byte
+English shard (seed 2 + rank, newline-terminated so shard starts are word
+starts) and the ranks train ONE global 32K vocab over the N-shard corpus,
+bit-exact to a single-stream run, with one RCCL all-gather of a fixed-size
+exchange record per merge.  Weak scaling: `value` = shard-merges/s = N x
+global merges / max wall (one merge applied to one 100 MiB shard is the unit
+of work at every N).  The encode leg runs one 1 GiB corpus per rank (seed
+3 + rank, no collective) and reports the total.
 """
 from __future__ import annotations
 
@@ -31,6 +36,8 @@ sys.path.insert(0, os.path.join(ROOT, "gpu-bpe_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+TILE_SYMS = 8192
+METRIC = "BPE merges/sec + tokenize GB/s, 1 GiB UTF-8 @ 32K vocab, 1/2/4/8 MI355X"
 
 
 def log(*a):
@@ -42,27 +49,36 @@ def dist_env():
 
 
 class Dist:
-    """barrier / max over ranks via torch.distributed (gloo on host — the
-    timing collectives carry a few bytes, no data path)."""
+    """Process groups: the default group carries the sharded trainer's data path
+    (RCCL = backend "nccl" over xGMI; GBPE_SHARD_TRANSPORT=gloo stages records
+    through host memory instead); a gloo group carries the timing scalars
+    (barrier / max / sum of a few bytes)."""
 
-    def __init__(self, world):
+    def __init__(self, world, local):
+        local = int(os.environ.get("GBPE_BENCH_DEVICE", local))   # rehearsal: several ranks on one GPU
         self.world = world
-        self.pg = None
+        self.transport = os.environ.get("GBPE_SHARD_TRANSPORT", "nccl")
         if world > 1:
+            import torch
             import torch.distributed as dist
-            dist.init_process_group("gloo")
+            torch.cuda.set_device(local)
+            if self.transport == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("gloo")
             self.dist = dist
+            self.host = dist.new_group(backend="gloo")
 
     def barrier(self):
         if self.world > 1:
-            self.dist.barrier()
+            self.dist.barrier(group=self.host)
 
     def max(self, x: float) -> float:
         if self.world == 1:
             return x
         import torch
         t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.host)
         return float(t.item())
 
     def sum(self, x: float) -> float:
@@ -70,7 +86,7 @@ class Dist:
             return x
         import torch
         t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.host)
         return float(t.item())
 
 
@@ -174,6 +190,63 @@ def train_leg(args, lib, ctx, dist, rank):
     return data, res
 
 
+def shard_corpus(args, rank):
+    from gpubpe import synth
+    data = synth.english(args.train_bytes, seed=2 + rank, fancy_punct=0.005)
+    return data[:-1] + b"\n"          # shard starts stay word starts in the global stream
+
+
+def run_sharded(args, lib, ctx, dist, rank, world, d, n, steps, table_log2):
+    import torch
+    from gpubpe.sharded import GpuShardBackend, ShardedTrainer
+    be = GpuShardBackend(lib, ctx, d, None, rank, world, args.vocab, input_on_device=True, n=n,
+                         table_log2=table_log2, cap_extra=max(TILE_SYMS, n // 4),
+                         stream=torch.cuda.current_stream().cuda_stream)
+    tr = ShardedTrainer(be, dist.dist, device="cuda", staged=dist.transport != "nccl")
+    tr.setup()
+    merges, done_steps, early = [], 0, False
+    needed = args.vocab - 256
+    while done_steps < steps and len(merges) < needed and not early:
+        got, early = tr.step(min(128, needed - len(merges)))
+        merges += got
+        done_steps += 1
+    return be, tr, merges, done_steps, early
+
+
+def train_leg_sharded(args, lib, ctx, dist, rank, world):
+    """C2-size shard per rank, one global vocab (weak scaling)."""
+    t = time.time()
+    data = shard_corpus(args, rank)
+    log(f"[bench] rank {rank}: shard {len(data)} B generated in {time.time() - t:.1f}s")
+    d = device_buffer(lib, ctx, data)
+    n = len(data)
+    table_log2 = 23
+    if args.warmup > 0:   # RCCL communicators, code paths: W steps on an 8 MiB prefix of every shard
+        be, _, _, _, _ = run_sharded(args, lib, ctx, dist, rank, world, d, min(n, 8 << 20), args.warmup, table_log2)
+        be.close()
+    lib.gbpe_synchronize(ctx)
+    dist.barrier()
+    lib.gbpe_synchronize(ctx)
+    t0 = time.perf_counter()
+    be, tr, merges, steps, early = run_sharded(args, lib, ctx, dist, rank, world, d, n, args.steps, table_log2)
+    lib.gbpe_synchronize(ctx)
+    t1 = time.perf_counter()
+    dist.barrier()
+    st = be.stats()
+    be.close()
+    lib.gbpe_device_free(ctx, d)
+    wall = dist.max(t1 - t0)
+    stream_bytes = int(dist.sum(float(st.stream_bytes_moved)))
+    res = {
+        "merges": len(merges), "steps": steps, "early_stop": early, "wall_s": wall,
+        "final_symbols_rank": int(st.symbol_count), "bytes_per_symbol": int(st.bytes_per_symbol),
+        "stream_bytes": stream_bytes, "stalls": tr.stalls, "record_caps": [tr.C, tr.Cw],
+        "transport": dist.transport, "last_merge": merges[-1] if merges else [],
+        "tail_dropped": int(st.tail_dropped),
+    }
+    return data, merges, res
+
+
 def encode_leg(args, lib, ctx, dist, rank):
     """C3: train a 32K vocab on a 100 MiB multilingual sample (seed 4), then
     encode 1 GiB multilingual text (seed 3) with the chunked trie walk."""
@@ -202,7 +275,7 @@ def encode_leg(args, lib, ctx, dist, rank):
     nodes, edges = parse_trie_buffers(blob, hdr)
     log(f"[bench] C3 vocab {voc.size} tokens, trie {hdr['nodeCount']} nodes in {time.time() - t:.1f}s")
     t = time.time()
-    text = synth.multilingual(args.encode_bytes, seed=3)
+    text = synth.multilingual(args.encode_bytes, seed=3 + rank)   # one corpus per rank (no collective)
     n = len(text)
     log(f"[bench] C3 corpus {n} B generated in {time.time() - t:.1f}s")
     trie = C.c_void_p()
@@ -254,7 +327,87 @@ def encode_leg(args, lib, ctx, dist, rank):
                      "frac": round(alg / 1e9 / (k_all / 1e3) / HBM_PEAK_GBPS, 4), "algorithmic_bytes": alg,
                      "traffic": None},
     }
+    if dist.world > 1:   # weak scaling: every rank encodes its own 1 GiB
+        res["ranks"] = dist.world
+        res["gbps_kernels_total"] = round(dist.sum(res["gbps_kernels"]), 2)
+        res["gbps_device_wall_total"] = round(dist.sum(n) / 1e9 / wall, 2)
     return text, nodes, edges, cs, tokens, res
+
+
+def single_line(args, tr):
+    value = tr["merges"] / tr["wall_s"]
+    ms_stream = tr["ms_stream_kernels"]
+    achieved = (tr["stream_bytes"] / 1e9) / (ms_stream / 1e3) if ms_stream > 0 else None
+    return {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "merges/s",
+        "n_gpus": 1,
+        "steps": tr["steps"],
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * tr["wall_s"] / max(1, tr["steps"]), 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": f"u{8 * tr['bytes_per_symbol']}",
+        "data": "synthetic (seeded Zipf English-like corpus, gpubpe.synth)",
+        "config": {"workload": "C2: 32K-vocab BPE train on 104,857,600 B English UTF-8 (seed 2), heuristic "
+                               "word boundaries, reference compaction; step = 128 merges",
+                   "train_bytes": args.train_bytes, "target_vocab": args.vocab,
+                   "merges_timed": tr["merges"], "early_stop": tr["early_stop"], "parallelism": "single"},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "stream pass per merge: k_delta + k_compact",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
+            "algorithmic_bytes": tr["stream_bytes"],
+            "traffic": None,
+        },
+        "train_detail": tr,
+    }
+
+
+def sharded_line(args, lib, ctx, dist, rank, world):
+    data, merges, tr = train_leg_sharded(args, lib, ctx, dist, rank, world)
+    value = world * tr["merges"] / tr["wall_s"]
+    achieved = tr["stream_bytes"] / 1e9 / tr["wall_s"]
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "merges/s",
+        "n_gpus": world,
+        "steps": tr["steps"],
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * tr["wall_s"] / max(1, tr["steps"]), 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": f"u{8 * tr['bytes_per_symbol']}",
+        "data": "synthetic (seeded Zipf English-like corpus per shard, gpubpe.synth)",
+        "config": {"workload": f"C2 x {world}: one global 32K-vocab BPE train over {world} shards of "
+                               f"{args.train_bytes:,} B English UTF-8 (seeds 2..{1 + world}), heuristic word "
+                               "boundaries, reference compaction, bit-exact to one stream; value = shard-merges/s "
+                               "(global merges x shards / wall); step = 128 merges",
+                   "train_bytes_per_rank": args.train_bytes, "target_vocab": args.vocab,
+                   "merges_timed": tr["merges"], "early_stop": tr["early_stop"],
+                   "parallelism": f"shard{world} ({tr['transport']} all-gather per merge)"},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "whole sharded loop (algorithmic stream bytes of all ranks / wall)",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS * world, "unit": "GB/s",
+            "frac": round(achieved / (HBM_PEAK_GBPS * world), 4),
+            "algorithmic_bytes": tr["stream_bytes"], "traffic": None,
+        },
+        "train_detail": tr,
+    }
+    if rank == 0 and not args.no_parity:
+        # the first merges equal a single-GPU run on the concatenated corpus
+        full = b"".join(shard_corpus(args, r) for r in range(world))
+        k = min(128, len(merges))
+        g = first_merges(lib, ctx, full, args.vocab, k)
+        line["parity"] = {"sharded_vs_single_stream_first_merges_equal": g == merges[:k], "merges_checked": k}
+    return line, data
 
 
 def main():
@@ -270,54 +423,26 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP-event roofline pass")
     ap.add_argument("--cpu-merges", type=int, default=0, help="CPU baseline merges (0 = auto, ~10-30 s)")
+    ap.add_argument("--no-parity", action="store_true", help="N>1: skip the single-stream parity check")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
-    dist = Dist(world)
+    dist = Dist(world, local)
     from gpubpe import _lib
     lib = _lib.load()
     ctx = C.c_void_p()
-    rc = lib.gbpe_ctx_create(local if world > 1 else 0, C.byref(ctx))
+    rc = lib.gbpe_ctx_create(int(os.environ.get("GBPE_BENCH_DEVICE", local)) if world > 1 else 0, C.byref(ctx))
     if rc != 0:
         raise SystemExit(f"gbpe_ctx_create failed ({rc}): no MI355X visible")
 
-    data, tr = train_leg(args, lib, ctx, dist, rank)
-    total_merges = dist.sum(tr["merges"]) if world > 1 else tr["merges"]
-    value = total_merges / tr["wall_s"]
-    ms_stream = tr["ms_stream_kernels"]
-    achieved = (tr["stream_bytes"] / 1e9) / (ms_stream / 1e3) if ms_stream > 0 else None
-    line = {
-        "metric": "BPE merges/sec + tokenize GB/s, 1 GiB UTF-8 @ 32K vocab, 1/2/4/8 MI355X",
-        "value": round(value, 1),
-        "unit": "merges/s",
-        "n_gpus": world,
-        "steps": tr["steps"],
-        "warmup": args.warmup,
-        "ms_per_step": round(1e3 * tr["wall_s"] / max(1, tr["steps"]), 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": f"u{8 * tr['bytes_per_symbol']}",
-        "data": "synthetic (seeded Zipf English-like corpus, gpubpe.synth)",
-        "config": {"workload": "C2: 32K-vocab BPE train on 104,857,600 B English UTF-8 (seed 2), heuristic "
-                               "word boundaries, reference compaction; step = 128 merges",
-                   "train_bytes": args.train_bytes, "target_vocab": args.vocab,
-                   "merges_timed": tr["merges"], "early_stop": tr["early_stop"],
-                   "parallelism": "single" if world == 1 else "replicas"},
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "stream pass per merge: k_delta + k_compact",
-            "achieved": round(achieved, 1) if achieved else None,
-            "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
-            "algorithmic_bytes": tr["stream_bytes"],
-            "traffic": None,
-        },
-        "train_detail": tr,
-    }
+    if world > 1:
+        line, data = sharded_line(args, lib, ctx, dist, rank, world)
+    else:
+        data, tr = train_leg(args, lib, ctx, dist, rank)
+        line = single_line(args, tr)
 
     pmc = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
-    if os.path.exists(pmc) and args.train_bytes == 104_857_600 and tr["bytes_per_symbol"] == 2:
+    if world == 1 and os.path.exists(pmc) and args.train_bytes == 104_857_600 and tr["bytes_per_symbol"] == 2:
         # HBM bytes per merge of k_delta + k_compact from the committed rocprofv3 --pmc
         # passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), on the first merges of
         # this same workload; scaled to the per-merge algorithmic bytes of this run
@@ -334,7 +459,7 @@ def main():
         enc = encode_leg(args, lib, ctx, dist, rank)
         line["tokenize"] = enc[-1]
 
-    if rank == 0 and not args.no_cpu:
+    if world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cpu_ref
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)

@@ -89,6 +89,7 @@ struct DevState {
     uint64_t poff;         // global offset of the previous input stream
     uint64_t off_next;
     uint64_t gnew;         // gn - mc
+    uint32_t peak_l, peak_w;   // largest record list / window piece of this step (capacity sizing)
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
@@ -1524,6 +1525,8 @@ __global__ __launch_bounds__(TPB) void k_shard_apply(DevState* st, uint32_t roun
         if ((uint64_t)mine + TILE > cap_syms) atomicOr(&st->err, ERR_SHARD_CAPACITY);
         st->owner = v.owner;
         st->m_glob = v.m;
+        st->peak_l = max(st->peak_l, v.max_l);
+        st->peak_w = max(st->peak_w, v.max_w);
         st->nl_next = mine;
         st->off_next = before;
     }
@@ -1751,10 +1754,12 @@ extern "C" int gbpe_shard_step_begin(gbpe_trainer* t, uint32_t max_merges) {
     hs->merges_done = 0;
     hs->budget = t->step_k;
     hs->stall = 0;
+    hs->peak_l = hs->peak_w = 0;
     hipStream_t s = t->ctx->stream;
     TR_HIP(t, hipMemcpyAsync(&t->st->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     TR_HIP(t, hipMemcpyAsync(&t->st->budget, &hs->budget, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     TR_HIP(t, hipMemcpyAsync(&t->st->stall, &hs->stall, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(&t->st->peak_l, &hs->peak_l, 2 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     return GBPE_OK;
 }
 
@@ -1870,7 +1875,8 @@ extern "C" int gbpe_shard_step_end(gbpe_trainer* t, uint32_t* merges_out, uint32
     if (n_done) *n_done = done;
     if (early_stop) *early_stop = t->stop ? 1u : 0u;
     if (stalled) *stalled = hs->stall;
-    if (need_list) *need_list = hs->need_l;
-    if (need_win) *need_win = hs->need_w;
+    // a stalled step reports what the stalled merge needs; otherwise the step's peaks
+    if (need_list) *need_list = hs->stall ? hs->need_l : hs->peak_l;
+    if (need_win) *need_win = hs->stall ? hs->need_w : hs->peak_w;
     return GBPE_OK;
 }

@@ -72,6 +72,8 @@ class ShardedTrainer:
         self.staged = staged
         self.C = cap_list
         self.Cw = cap_win
+        self.min_list, self.min_win = min(cap_list, 1 << 12), min(cap_win, 1 << 10)
+        self.adaptive = True
         self.stalls = 0
         self._bufs = None
 
@@ -135,6 +137,11 @@ class ShardedTrainer:
             self.stalls += 1
             self.C = _pow2_at_least(2 * res["need_list"], self.C)
             self.Cw = _pow2_at_least(2 * res["need_win"], self.Cw)
+        elif res["merges"] and self.adaptive:
+            # shrink towards 2x this step's largest record (merges get rarer; the
+            # all-gather moves the full capacity every merge); identical on all ranks
+            self.C = min(self.C, _pow2_at_least(2 * res["need_list"], self.min_list))
+            self.Cw = min(self.Cw, _pow2_at_least(2 * res["need_win"], self.min_win))
         return res["merges"], res["early_stop"]
 
     def train(self, target_vocab_size: int, vocab_size: int = 256, batch: int = BATCH_SIZE, on_progress=None):

@@ -159,7 +159,9 @@ void gbpe_trainer_destroy(gbpe_trainer* t);
  *   (all-gather lists) import_counts → per step: step_begin, per merge k
  *   {phase1(k, send) ; all_gather(recv, send) ; phase2(k, recv)}, step_end.
  * A merge whose record needs more than (C, Cw) stalls on every rank; step_end
- * reports it with the capacities needed, and the next step redoes it. */
+ * reports it with the capacities needed, and the next step redoes it.  A step
+ * without a stall reports the largest list / window piece it exchanged, so
+ * the host can shrink (C, Cw) as merges get rarer. */
 int gbpe_ctx_set_stream(gbpe_ctx* ctx, void* hip_stream);   /* taken literally (NULL = the null stream) */
 void* gbpe_ctx_get_stream(gbpe_ctx* ctx);                    /* current stream (save / restore) */
 int gbpe_shard_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,

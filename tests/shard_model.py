@@ -77,6 +77,7 @@ class ModelShardBackend:
         self.log = []
         self.stalled = False
         self.need = (0, 0)
+        self.peak = (0, 0)
         self.active = False
 
     def _select(self):
@@ -168,6 +169,7 @@ class ModelShardBackend:
             self.active = False
             return
         assert int(hd[:, H_SURV].sum()) == self.gn - mc
+        self.peak = (max(self.peak[0], int(hd[:, H_L].max())), max(self.peak[1], int(hd[:, H_W].max())))
         gnew = self.gn - mc
         m = int(hd[:, H_M].sum())
         pieces = [recs[q, HDR + 2 * C: HDR + 2 * C + hd[q, H_W]] for q in range(R)]
@@ -225,8 +227,9 @@ class ModelShardBackend:
         self.active = False
 
     def step_end(self):
+        need = self.need if self.stalled else self.peak
         return {"merges": self.log, "early_stop": self.stop, "stalled": self.stalled,
-                "need_list": self.need[0], "need_win": self.need[1]}
+                "need_list": need[0], "need_win": need[1]}
 
     def symbols(self):
         return self.cur[: self.ln].copy()
