@@ -54,11 +54,15 @@ class Dist:
     through host memory instead); a gloo group carries the timing scalars
     (barrier / max / sum of a few bytes)."""
 
-    def __init__(self, world, local):
+    def __init__(self, world, local, force=False):
         local = int(os.environ.get("GBPE_BENCH_DEVICE", local))   # rehearsal: several ranks on one GPU
         self.world = world
         self.transport = os.environ.get("GBPE_SHARD_TRANSPORT", "nccl")
-        if world > 1:
+        if world > 1 or force:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29571")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
             import torch
             import torch.distributed as dist
             torch.cuda.set_device(local)
@@ -70,7 +74,7 @@ class Dist:
             self.host = dist.new_group(backend="gloo")
 
     def barrier(self):
-        if self.world > 1:
+        if hasattr(self, "host"):
             self.dist.barrier(group=self.host)
 
     def max(self, x: float) -> float:
@@ -205,8 +209,8 @@ def run_sharded(args, lib, ctx, dist, rank, world, d, n, steps, table_log2):
     tr = ShardedTrainer(be, dist.dist, device="cuda", staged=dist.transport != "nccl")
     tr.setup()
     merges, done_steps, early = [], 0, False
-    needed = args.vocab - 256
-    while done_steps < steps and len(merges) < needed and not early:
+    needed = min(args.vocab - 256, 128 * steps)     # stalled steps are redone: count merges, not steps
+    while len(merges) < needed and not early:
         got, early = tr.step(min(128, needed - len(merges)))
         merges += got
         done_steps += 1
@@ -424,10 +428,11 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP-event roofline pass")
     ap.add_argument("--cpu-merges", type=int, default=0, help="CPU baseline merges (0 = auto, ~10-30 s)")
     ap.add_argument("--no-parity", action="store_true", help="N>1: skip the single-stream parity check")
+    ap.add_argument("--sharded", action="store_true", help="use the sharded trainer even at N=1 (RCCL rehearsal)")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
-    dist = Dist(world, local)
+    dist = Dist(world, local, force=args.sharded)
     from gpubpe import _lib
     lib = _lib.load()
     ctx = C.c_void_p()
@@ -435,14 +440,14 @@ def main():
     if rc != 0:
         raise SystemExit(f"gbpe_ctx_create failed ({rc}): no MI355X visible")
 
-    if world > 1:
+    if world > 1 or args.sharded:
         line, data = sharded_line(args, lib, ctx, dist, rank, world)
     else:
         data, tr = train_leg(args, lib, ctx, dist, rank)
         line = single_line(args, tr)
 
     pmc = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
-    if world == 1 and os.path.exists(pmc) and args.train_bytes == 104_857_600 and tr["bytes_per_symbol"] == 2:
+    if world == 1 and not args.sharded and os.path.exists(pmc) and args.train_bytes == 104_857_600 and tr["bytes_per_symbol"] == 2:
         # HBM bytes per merge of k_delta + k_compact from the committed rocprofv3 --pmc
         # passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), on the first merges of
         # this same workload; scaled to the per-merge algorithmic bytes of this run
@@ -459,7 +464,7 @@ def main():
         enc = encode_leg(args, lib, ctx, dist, rank)
         line["tokenize"] = enc[-1]
 
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not args.sharded and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cpu_ref
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)

@@ -90,6 +90,7 @@ struct DevState {
     uint64_t off_next;
     uint64_t gnew;         // gn - mc
     uint32_t peak_l, peak_w;   // largest record list / window piece of this step (capacity sizing)
+    uint32_t dfull;            // the delta table overflowed this merge
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
@@ -109,6 +110,7 @@ struct Table {
     uint32_t* blive;   // per block: entries with count > 0
     uint32_t nblk;
     uint32_t* used;    // occupied-slot counter (DevState::used or ::dused)
+    uint32_t* full;    // non-null: a full table sets *full instead of the fatal error (delta table)
 };
 
 // a touched block is re-maxed by the next k_refresh: a plain flag store, nothing waits on it
@@ -126,7 +128,7 @@ __device__ void table_add(const Table& tb, DevState* st, uint32_t pid, uint32_t 
         if (k == 0u) {
             k = atomicCAS(&tb.slots[idx].x, 0u, pid);
             if (k == 0u) {
-                __hip_atomic_fetch_add(tb.used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tb.used) __hip_atomic_fetch_add(tb.used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 k = pid;
             }
         }
@@ -136,7 +138,8 @@ __device__ void table_add(const Table& tb, DevState* st, uint32_t pid, uint32_t 
             return;
         }
     }
-    atomicOr(&st->err, ERR_TABLE_FULL);
+    if (tb.full) *tb.full = 1u;   // per-merge delta table sized too small: the merge stalls and retries bigger
+    else atomicOr(&st->err, ERR_TABLE_FULL);
 }
 
 __device__ uint32_t table_find(const Table& tb, uint32_t pid) {
@@ -384,6 +387,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
     st->m = 0u;
     st->dcount = 0u;
     st->dused = 0u;
+    st->dfull = 0u;
     st->valid_total = 0u;
     st->ticket = 0u;
     st->rw_count = 0u;
@@ -466,12 +470,15 @@ __device__ __forceinline__ uint32_t lane_mask32(uint64_t i0, uint64_t lim) {
 template <typename S, bool EXACT>
 __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, const S* cur, Table tb,
                                                uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
-                                               uint32_t* __restrict__ grpsum) {
+                                               uint32_t* __restrict__ grpsum, uint32_t eager_tiles) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     __shared__ LdsTab<LTAB_T> lt;
     __shared__ uint32_t red[TPB / 64], s_workw[TPB / 64];
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t tl = blockIdx.x;
+    // tiles past the host's view of the stream (a shard that may have grown by an
+    // appended window) check the length before loading anything
+    if (tl >= eager_tiles && (uint64_t)tl * TILE >= st->n) return;
     const uint64_t base = (uint64_t)tl * TILE;
     const uint64_t i0 = base + (uint64_t)t * EPT;
     // loads first, unconditionally (buffers are padded: every launched tile is in
@@ -864,13 +871,13 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
     if (exact) {
         hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
-                           t->hitmask, t->tile_cnt, t->grpsum);
+                           t->hitmask, t->tile_cnt, t->grpsum, g_delta);
         if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
         hipLaunchKernelGGL((k_compact<S, true>), dim3(g_compact), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
     } else {
         hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
-                           t->hitmask, t->tile_cnt, t->grpsum);
+                           t->hitmask, t->tile_cnt, t->grpsum, g_delta);
         if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
         hipLaunchKernelGGL((k_compact<S, false>), dim3(g_compact), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
@@ -1403,7 +1410,8 @@ __global__ __launch_bounds__(TPB) void k_shard_header(DevState* st, uint32_t rou
     }
     const uint32_t m_r = st->m;
     rec[H_ACTIVE] = 1u;
-    rec[H_L] = st->dcount;
+    // an overflowed delta table (sized 4x the list capacity) reports a list that cannot fit
+    rec[H_L] = st->dfull ? max(st->dcount, 4u * cap_list) : st->dcount;
     rec[H_KEPT] = surv - m_r;
     rec[H_M] = m_r;
     rec[H_W] = w;
@@ -1540,7 +1548,7 @@ __global__ __launch_bounds__(TPB) void k_shard_apply(DevState* st, uint32_t roun
     }
     // pairs of the stale window = last m symbols of the superset, after x0
     const uint32_t m = v.m;
-    if (m == 0) return;
+    if (m <= blockIdx.x * TPB) return;   // no window symbols for this block (uniform)
     lds_clear(lt);
     __syncthreads();
     const uint32_t sup = v.wpre[R], g0 = sup - m;
@@ -1612,7 +1620,8 @@ extern "C" int gbpe_shard_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n
     t->world = world;
     t->dt.mask = t->tb.mask;
     t->dt.nblk = t->tb.nblk;
-    t->dt.used = &t->st->dused;
+    t->dt.used = nullptr;   // every key is new each merge: no shared counter on the state line
+    t->dt.full = &t->st->dfull;
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
     hipStream_t s = ctx->stream;
     if (hipMalloc(&t->dt.slots, slots * sizeof(uint2)) != hipSuccess ||
@@ -1764,22 +1773,33 @@ extern "C" int gbpe_shard_step_begin(gbpe_trainer* t, uint32_t max_merges) {
 }
 
 namespace {
+// the per-merge delta table only has to hold one merge's distinct deltas: size it
+// 4x the record's list capacity (>= 2 blocks) so k_shard_list scans few blocks
+Table delta_view(const gbpe_trainer* t, uint32_t cl) {
+    Table d = t->dt;
+    uint64_t want = 4ull * cl, sl = 1ull << (BLK_LOG2 + 1);
+    while (sl < want && sl < (uint64_t)t->dt.mask + 1) sl <<= 1;
+    d.mask = (uint32_t)(sl - 1);
+    d.nblk = (uint32_t)(sl >> BLK_LOG2);
+    return d;
+}
+
 template <typename S>
 int shard_phase1(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl, uint32_t cw) {
     hipStream_t s = t->ctx->stream;
     S* cur = (S*)t->buf[t->cur ^ (round & 1)];
     S* oth = (S*)t->buf[t->cur ^ (round & 1) ^ 1];
-    const uint64_t ntiles = gbpe_div_up(t->n, TILE) + 1;   // the stream may have grown by a window
+    const uint32_t eager = (uint32_t)gbpe_div_up(t->n, TILE);   // the stream may grow by appended windows
     const uint32_t g_delta = (uint32_t)gbpe_div_up(t->cap_syms, TILE) - 1;
-    (void)ntiles;
+    const Table dt = delta_view(t, cl);
     hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum, t->d_nlog);
     if (t->flags & GBPE_TRAIN_EXACT_COMPACTION)
-        hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->dt,
-                           t->hitmask, t->tile_cnt, t->grpsum);
+        hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, dt,
+                           t->hitmask, t->tile_cnt, t->grpsum, eager);
     else
-        hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->dt,
-                           t->hitmask, t->tile_cnt, t->grpsum);
-    hipLaunchKernelGGL(k_shard_list, dim3(grid_persistent(t->ctx, t->dt.nblk, 2)), dim3(TPB), 0, s, t->st, round, t->dt,
+        hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, dt,
+                           t->hitmask, t->tile_cnt, t->grpsum, eager);
+    hipLaunchKernelGGL(k_shard_list, dim3(grid_persistent(t->ctx, dt.nblk, 2)), dim3(TPB), 0, s, t->st, round, dt,
                        rec, cl);
     hipLaunchKernelGGL(k_shard_header<S>, dim3(grid_persistent(t->ctx, gbpe_div_up(cw, TPB * 8) + 1, 1)), dim3(TPB), 0,
                        s, t->st, round, (const S*)cur, (const S*)oth, (const uint32_t*)t->hitmask,
