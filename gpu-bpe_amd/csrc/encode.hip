@@ -18,6 +18,8 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 
 namespace {
 
@@ -87,6 +89,145 @@ __global__ __launch_bounds__(WALK_TPB) void k_trie_walk(const uint8_t* __restric
             ++pos;
         }
     }
+    counts[chunk] = cnt;
+}
+
+// Packed 8-byte double-array records (built by gbpe_trie_upload):
+//   x = check (22 bits) | tokenId bits 0-9 << 22,  y = base (22 bits) | tokenId bits 10-19 << 22
+// check 0x3FFFFF = empty slot, tokenId 0xFFFFF = none, base 0 = leaf (no children).
+__device__ __forceinline__ uint32_t rec_check(uint2 r) { return r.x & 0x3FFFFFu; }
+__device__ __forceinline__ uint32_t rec_base(uint2 r) { return r.y & 0x3FFFFFu; }
+__device__ __forceinline__ uint32_t rec_tid(uint2 r) { return (r.x >> 22) | ((r.y >> 22) << 10); }
+constexpr uint32_t TID_NONE = 0xFFFFFu;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t win_byte(uint4 w, uint32_t o) {
+    const uint32_t d = (o & 8u) ? ((o & 4u) ? w.w : w.z) : ((o & 4u) ? w.y : w.x);
+    return (d >> ((o & 3u) * 8u)) & 0xFFu;
+}
+
+__device__ __forceinline__ uint4 load_win(const uint8_t* __restrict__ in, uint64_t n, uint64_t ab) {
+    if (ab + 16 <= n) return *reinterpret_cast<const uint4*>(in + ab);
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;   // the last partial block: byte loads inside [0, n)
+    for (uint32_t j = 0; j < 16 && ab + j < n; ++j) {
+        const uint32_t v = (uint32_t)in[ab + j] << ((j & 3) * 8);
+        if (j < 4) w0 |= v; else if (j < 8) w1 |= v; else if (j < 12) w2 |= v; else w3 |= v;
+    }
+    return make_uint4(w0, w1, w2, w3);
+}
+
+// token vector: slot j of a 16-byte register vector (8 x u16 or 4 x u32), stored whole
+template <typename T>
+__device__ __forceinline__ void vec_put(uint4& a, uint32_t j, uint32_t tok) {
+    if (sizeof(T) == 2) {
+        const uint32_t sh = (j & 1u) * 16u, q = (j >> 1) & 3u;
+        const uint32_t v = (tok & 0xFFFFu) << sh;
+        a.x |= q == 0 ? v : 0u;
+        a.y |= q == 1 ? v : 0u;
+        a.z |= q == 2 ? v : 0u;
+        a.w |= q == 3 ? v : 0u;
+    } else {
+        const uint32_t q = j & 3u;
+        a.x = q == 0 ? tok : a.x;
+        a.y = q == 1 ? tok : a.y;
+        a.z = q == 2 ? tok : a.z;
+        a.w = q == 3 ? tok : a.w;
+    }
+}
+
+// Production walk.  One lane per chunk (as tokenize.wgsl:88), packed 8-byte
+// double-array records, and one L2 record load per loop iteration: token starts
+// resolve from the root transitions cached in LDS inside the same iteration
+// (runs of raw bytes and one-byte leaf tokens included), and a walk that
+// enters a leaf (base == 0: no children) ends its token without the extra
+// probe that would only discover the mismatch.
+template <typename T>
+__global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v3(const uint8_t* __restrict__ in, uint64_t n, uint32_t cs,
+                                                           const uint2* __restrict__ rec, uint32_t nrec,
+                                                           uint32_t root_base, T* __restrict__ scratch,
+                                                           uint32_t* __restrict__ counts, uint64_t nchunks) {
+    constexpr uint32_t PER = 16 / sizeof(T);
+    __shared__ uint2 lut[256];   // root transitions: the packed record of child c, check == 0 when present
+    {
+        const uint32_t t = root_base + threadIdx.x;
+        lut[threadIdx.x] = t < nrec ? rec[t] : make_uint2(0x3FFFFFu, 0u);
+    }
+    __syncthreads();
+    const uint64_t chunk = (uint64_t)blockIdx.x * WALK_TPB + threadIdx.x;
+    if (chunk >= nchunks) return;
+    const uint64_t c0 = chunk * cs;
+    const uint32_t ce = (uint32_t)(min(c0 + cs, n) - c0);
+    T* out = scratch + c0;
+    uint32_t cb = ~0u;
+    uint4 win = make_uint4(0, 0, 0, 0), acc = make_uint4(0, 0, 0, 0);
+    uint32_t cnt = 0, pos = 0, wp = 0, lmp = 0, st = 0, base = 0, lmt = TID_NONE, first = 0;
+    auto byte_at = [&](uint32_t p) -> uint32_t {
+        const uint32_t b = p & ~15u;
+        if (b != cb) {
+            cb = b;
+            win = load_win(in, n, c0 + b);
+        }
+        return win_byte(win, p & 15u);
+    };
+    auto emit = [&](uint32_t tok) {
+        vec_put<T>(acc, cnt % PER, tok);
+        if (++cnt % PER == 0) {
+            *reinterpret_cast<uint4*>(out + cnt - PER) = acc;
+            acc = make_uint4(0, 0, 0, 0);
+        }
+    };
+    bool need_start = true;
+    while (true) {
+        // token starts: LDS only
+        while (need_start && pos < ce) {
+            first = byte_at(pos);
+            const uint2 e = lut[first];
+            if (rec_check(e) != 0u) {   // no token starts with this byte: emit it raw (tokenize.wgsl:169-171)
+                emit(first);
+                ++pos;
+                continue;
+            }
+            const uint32_t tid = rec_tid(e);
+            if (rec_base(e) == 0u) {    // one-byte leaf token
+                emit(tid != TID_NONE ? tid : first);
+                ++pos;
+                continue;
+            }
+            st = root_base + first;
+            base = rec_base(e);
+            lmt = tid;
+            lmp = pos + 1;
+            wp = pos + 1;
+            need_start = false;
+        }
+        if (need_start) break;   // chunk done
+        // one trie transition: the iteration's single L2 load
+        bool adv = false, leaf = false;
+        if (wp < ce) {
+            const uint32_t t = base + byte_at(wp);
+            const uint2 r = t < nrec ? rec[t] : make_uint2(0x3FFFFFu, 0u);
+            if (rec_check(r) == st) {
+                adv = true;
+                st = t;
+                base = rec_base(r);
+                ++wp;
+                const uint32_t tid = rec_tid(r);
+                if (tid != TID_NONE) {
+                    lmt = tid;
+                    lmp = wp;
+                }
+                leaf = base == 0u;
+            }
+        }
+        if (!adv || leaf) {   // the longest match ends: emit it (or the raw first byte), restart after it
+            const bool hit = lmt != TID_NONE;
+            emit(hit ? lmt : first);
+            pos = hit ? lmp : pos + 1;
+            need_start = true;
+        }
+    }
+    if (cnt % PER) *reinterpret_cast<uint4*>(out + (cnt / PER) * PER) = acc;
     counts[chunk] = cnt;
 }
 
@@ -168,6 +309,8 @@ __global__ __launch_bounds__(256) void k_chunk_compact(const T* __restrict__ scr
 struct gbpe_trie {
     gbpe_ctx* ctx = nullptr;
     uint4* rec = nullptr;      // double-array records {check, base, tokenId, 0}
+    uint2* rec2 = nullptr;     // packed 8-byte records (pack_rec); null when ids / states do not fit
+    uint32_t root_base = 0;    // base of the root state
     uint32_t nrec = 0;
     uint4* root = nullptr;     // 256 root transitions {state, base, tokenId, present}
     uint32_t max_token_len = 0;
@@ -191,7 +334,7 @@ extern "C" int gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n
     queue.reserve(n_nodes);
     queue.push_back(0);
     state[0] = 0;
-    uint32_t max_len = 0, max_tid = 0;
+    uint32_t max_len = 0, max_tid = 0, root_base = 0;
     auto ensure = [&](uint64_t sz) {
         if (sz > rec.size()) {
             rec.resize(sz, make_uint4(INV, 0, INV, 0));
@@ -224,6 +367,7 @@ extern "C" int gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n
         }
         const uint32_t su = state[u];
         if (u != 0) rec[su].y = b;
+        else root_base = b;
         for (uint32_t k = 0; k < nc; ++k) {
             const uint32_t c = edges[2 * ((uint64_t)fc + k)] & 0xFFu;
             const uint32_t v = edges[2 * ((uint64_t)fc + k) + 1];
@@ -255,10 +399,24 @@ extern "C" int gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n
     tr->max_token_id = max_tid;
     tr->n_nodes = n_nodes;
     tr->n_edges = n_edges;
+    tr->root_base = root_base;
     hipError_t e = hipMalloc(&tr->rec, rec.size() * sizeof(uint4));
     if (e == hipSuccess) e = hipMalloc(&tr->root, 256 * sizeof(uint4));
     if (e == hipSuccess) e = hipMemcpy(tr->rec, rec.data(), rec.size() * sizeof(uint4), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(tr->root, root.data(), 256 * sizeof(uint4), hipMemcpyHostToDevice);
+    // packed records: check (22 bits) | tid low 10 << 22, base (22 bits) | tid high 10 << 22
+    const bool packable = rec.size() + 256 < 0x3FFFFFu && max_tid < 0xFFFFFu;
+    if (e == hipSuccess && packable) {
+        std::vector<uint2> r2(rec.size() + 256);
+        for (size_t i = 0; i < r2.size(); ++i) {
+            const uint4 q = i < rec.size() ? rec[i] : make_uint4(INV, 0, INV, 0);
+            const uint32_t chk = q.x == INV ? 0x3FFFFFu : q.x;
+            const uint32_t tid = q.z == INV ? 0xFFFFFu : q.z;
+            r2[i] = make_uint2(chk | ((tid & 0x3FFu) << 22), (q.y & 0x3FFFFFu) | ((tid >> 10) << 22));
+        }
+        e = hipMalloc(&tr->rec2, r2.size() * sizeof(uint2));
+        if (e == hipSuccess) e = hipMemcpy(tr->rec2, r2.data(), r2.size() * sizeof(uint2), hipMemcpyHostToDevice);
+    }
     if (e != hipSuccess) {
         gbpe_trie_free(tr);
         return gbpe_set_error(ctx, GBPE_E_DEVICE, "trie upload failed: %s", hipGetErrorString(e));
@@ -270,6 +428,7 @@ extern "C" int gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n
 extern "C" void gbpe_trie_free(gbpe_trie* tr) {
     if (!tr) return;
     hipFree(tr->rec);
+    hipFree(tr->rec2);
     hipFree(tr->root);
     delete tr;
 }
@@ -315,12 +474,26 @@ int encode_device_impl(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* d_in, uint64
     uint64_t* d_total = blocksum + nblk + 1;
     const uint32_t gw = (uint32_t)gbpe_div_up(nchunks, WALK_TPB);
     GBPE_HIP(ctx, hipEventRecord(ctx->ev[0], s));
-    if (narrow)
-        hipLaunchKernelGGL(k_trie_walk<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec, tr->nrec,
-                           tr->root, (uint16_t*)ctx->enc_scratch, counts, nchunks);
-    else
-        hipLaunchKernelGGL(k_trie_walk<uint32_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec, tr->nrec,
-                           tr->root, (uint32_t*)ctx->enc_scratch, counts, nchunks);
+    // packed-record walk when the trie packs and chunks are whole 16-byte token
+    // vectors; otherwise the plain per-token walk (GBPE_ENCODE_WALK=nested forces it)
+    static const bool force_nested = getenv("GBPE_ENCODE_WALK") && std::string(getenv("GBPE_ENCODE_WALK")) == "nested";
+    const bool v3 = !force_nested && (cs % 8u) == 0u && tr->rec2;
+    const uint32_t nrec2 = tr->nrec + 256;
+    if (v3) {
+        if (narrow)
+            hipLaunchKernelGGL(k_trie_walk_v3<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
+                               tr->root_base, (uint16_t*)ctx->enc_scratch, counts, nchunks);
+        else
+            hipLaunchKernelGGL(k_trie_walk_v3<uint32_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
+                               tr->root_base, (uint32_t*)ctx->enc_scratch, counts, nchunks);
+    } else {
+        if (narrow)
+            hipLaunchKernelGGL(k_trie_walk<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec, tr->nrec,
+                               tr->root, (uint16_t*)ctx->enc_scratch, counts, nchunks);
+        else
+            hipLaunchKernelGGL(k_trie_walk<uint32_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec, tr->nrec,
+                               tr->root, (uint32_t*)ctx->enc_scratch, counts, nchunks);
+    }
     GBPE_LAUNCH_CHECK(ctx);
     GBPE_HIP(ctx, hipEventRecord(ctx->ev[1], s));
     hipLaunchKernelGGL(k_chunk_scan1, dim3((uint32_t)nblk), dim3(SCAN_TPB), 0, s, (const uint32_t*)counts, nchunks, local,
