@@ -286,6 +286,8 @@ def encode_leg(args, lib, ctx, dist, rank):
     _lib.check(lib.gbpe_trie_upload(ctx, nodes.ctypes.data_as(_lib.u32p), hdr["nodeCount"],
                                     edges.ctypes.data_as(_lib.u32p), hdr["edgeCount"], C.byref(trie)), ctx, "trie")
     cs = max(512, min(2048, hdr["maxTokenLen"] * 8))            # tokenizer.js:67-68
+    nrec = C.c_uint32()
+    lib.gbpe_trie_info(trie, C.byref(nrec), None, None)
     d_in = device_buffer(lib, ctx, text)
     d_out = C.c_void_p()
     _lib.check(lib.gbpe_device_alloc(ctx, 4 * n + 64, C.byref(d_out)), ctx, "alloc out")
@@ -320,7 +322,8 @@ def encode_leg(args, lib, ctx, dist, rank):
     res = {
         "workload": "C3: chunked greedy trie encode of 1,073,741,824 B multilingual UTF-8 (seed 3), 32K vocab "
                     f"trained on a {args.vocab_sample_bytes} B sample (seed 4), chunk {cs}",
-        "bytes": n, "tokens": T, "chunk_size": cs,
+        "bytes": n, "tokens": T, "chunk_size": cs, "trie_nodes": int(hdr["nodeCount"]),
+        "trie_records": int(nrec.value),
         "gbps_kernels": round(n / 1e9 / (k_all / 1e3), 2),
         "gbps_device_wall": round(n / 1e9 / wall, 2),
         "gbps_end_to_end": round(n / 1e9 / e2e, 2),

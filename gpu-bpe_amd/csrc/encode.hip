@@ -425,6 +425,14 @@ extern "C" int gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n
     return GBPE_OK;
 }
 
+extern "C" int gbpe_trie_info(const gbpe_trie* tr, uint32_t* n_records, uint32_t* max_token_len, uint32_t* max_token_id) {
+    if (!tr) return GBPE_E_INVALID;
+    if (n_records) *n_records = tr->nrec;
+    if (max_token_len) *max_token_len = tr->max_token_len;
+    if (max_token_id) *max_token_id = tr->max_token_id;
+    return GBPE_OK;
+}
+
 extern "C" void gbpe_trie_free(gbpe_trie* tr) {
     if (!tr) return;
     hipFree(tr->rec);

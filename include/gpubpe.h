@@ -190,6 +190,8 @@ int gbpe_shard_step_end(gbpe_trainer* t, uint32_t* merges_out, uint32_t* n_done,
 int  gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n_nodes,
                       const uint32_t* edges, uint32_t n_edges, gbpe_trie** out);
 void gbpe_trie_free(gbpe_trie* trie);
+/* double-array size of the uploaded trie; maxTokenLen (tokenizer.js maxTokenLen getter) and max id */
+int  gbpe_trie_info(const gbpe_trie* trie, uint32_t* n_records, uint32_t* max_token_len, uint32_t* max_token_id);
 
 /* tokenizer.js:173-206 encodeBytes: chunked greedy longest match.
  * chunk_size 0 = the reference's adaptive size (tokenizer.js:67-68).
