@@ -82,6 +82,7 @@ void gbpe_ctx_destroy(gbpe_ctx* ctx) {
     hipFree(ctx->enc_counts);
     hipFree(ctx->enc_in);
     hipFree(ctx->enc_out);
+    hipFree(ctx->pt_agg);
     if (ctx->enc_host_total) hipHostFree(ctx->enc_host_total);
     for (auto& ev : ctx->ev)
         if (ev) hipEventDestroy(ev);

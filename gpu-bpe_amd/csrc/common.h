@@ -23,6 +23,7 @@ struct gbpe_ctx {
     void* enc_in = nullptr;       uint64_t enc_in_bytes = 0;
     void* enc_out = nullptr;      uint64_t enc_out_bytes = 0;
     uint32_t* enc_host_total = nullptr;   // pinned
+    void* pt_agg = nullptr;       uint64_t pt_agg_bytes = 0;   // pre-tokenizer block aggregates
     hipEvent_t ev[8] = {};
     double enc_ms[3] = {0, 0, 0};
 };
@@ -51,3 +52,6 @@ __device__ __forceinline__ uint32_t gbpe_fmix32(uint32_t x) {
 }
 
 __host__ __device__ static inline uint64_t gbpe_div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+// GPT-4 rule word starts of device bytes on ctx->stream (pretok.hip)
+int gbpe_pretok_gpt4_launch(gbpe_ctx* ctx, const uint8_t* d_bytes, uint64_t n, uint8_t* d_ws);

@@ -984,6 +984,16 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         d_bytes = (const uint8_t*)tmp;
         d_ws = word_starts ? (const uint8_t*)tmp + n : nullptr;
     }
+    uint8_t* d_gpt4 = nullptr;   // GPT-4 rule word starts computed on the device (pre_tokenizer.mjs:226-292)
+    if (!d_ws && (opts->flags & GBPE_TRAIN_GPT4_BOUNDARIES)) {
+        int rc2 = hipMalloc(&d_gpt4, n) == hipSuccess ? gbpe_pretok_gpt4_launch(ctx, d_bytes, n, d_gpt4) : GBPE_E_OOM;
+        if (rc2 != GBPE_OK) {
+            if (tmp) hipFree(tmp);
+            hipFree(d_gpt4);
+            return fail(rc2 == GBPE_E_OOM ? gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(word starts) failed") : rc2);
+        }
+        d_ws = d_gpt4;
+    }
     const uint32_t gb = (uint32_t)gbpe_div_up(n, TPB);
     if (t->u16)
         hipLaunchKernelGGL(k_symbols<uint16_t>, dim3(gb), dim3(TPB), 0, s, d_bytes, d_ws, (uint16_t*)t->buf[0], n,
@@ -996,9 +1006,10 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "symbol kernel launch failed"));
     }
     int rc = table_rebuild(t);
-    if (tmp) {
+    if (tmp || d_gpt4) {
         hipStreamSynchronize(s);
         hipFree(tmp);
+        hipFree(d_gpt4);
     }
     if (rc != GBPE_OK) return fail(rc);
     if (t->flags & GBPE_TRAIN_TIMING) {

@@ -6,6 +6,7 @@ BPEEngine (engine.js), BPETrainer (trainer.js), TrieTokenizer
 (tokenizer/tokenizer.js), Vocab (vocab.js), trie compile/parse (trie.js).
 """
 from .engine import BPEEngine, INVALID_TOKEN, MAX_WG_DIM, TABLE_SIZE, WORKGROUP_SIZE  # noqa: F401
+from .pretokenizer import GpuPreTokenizer  # noqa: F401
 from .tokenizer import TrieTokenizer  # noqa: F401
 from .trainer import BATCH_SIZE, BPETrainer  # noqa: F401
 from .trie import compile_vocab_to_trie, parse_header, parse_trie_buffers  # noqa: F401

@@ -23,6 +23,7 @@ GBPE_E_INTERNAL = -7
 
 GBPE_TRAIN_EXACT_COMPACTION = 1 << 0
 GBPE_TRAIN_TIMING = 1 << 1
+GBPE_TRAIN_GPT4_BOUNDARIES = 1 << 2
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)
@@ -83,6 +84,8 @@ _SIGS = [
     ("gbpe_memcpy_h2d", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     ("gbpe_memcpy_d2h", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     ("gbpe_synchronize", C.c_int, [C.c_void_p]),
+    ("gbpe_pretokenize_gpt4", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    ("gbpe_pretokenize_gpt4_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     ("gbpe_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("gbpe_ctx_get_stream", C.c_void_p, [C.c_void_p]),
     ("gbpe_shard_create", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int, C.POINTER(TrainOpts),

@@ -69,6 +69,12 @@ const char* gbpe_kernel_name(int i);
  * heuristic. */
 int gbpe_word_boundary(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, uint8_t* ws_out);
 
+/* PreTokenizer.preTokenizeBytes (src/wasm/pre_tokenizer.mjs:459-509) word-start
+ * mask for NFC UTF-8 bytes (the reference also NFC-normalises: identity on NFC
+ * input).  Classes: Unicode general categories (unicode_classes.h). */
+int gbpe_pretokenize_gpt4(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, uint8_t* ws_out);
+int gbpe_pretokenize_gpt4_device(gbpe_ctx* ctx, const void* d_bytes, uint64_t n, void* d_ws);
+
 /* ── training (replaces trainer.js:149-335 BPETrainer.train over the
  *    train.wgsl kernels, training-pipeline.js:178-222 encodeBatch) ─────── */
 
@@ -79,6 +85,10 @@ int gbpe_word_boundary(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, uint8_t*
 #define GBPE_TRAIN_EXACT_COMPACTION  (1u << 0)
 /* record per-kernel device time with HIP events (read via gbpe_trainer_stats) */
 #define GBPE_TRAIN_TIMING            (1u << 1)
+/* word starts from the GPT-4 rules of the reference's PreTokenizer
+ * (src/wasm/pre_tokenizer.mjs:226-292) computed on the device, for NFC UTF-8
+ * input; ignored when word_starts is given */
+#define GBPE_TRAIN_GPT4_BOUNDARIES   (1u << 2)
 
 typedef struct gbpe_train_opts {
     uint32_t target_vocab_size;  /* trainer.js:149 targetVocabSize (reference default 4096) */

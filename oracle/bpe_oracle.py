@@ -452,3 +452,149 @@ def dxft_bin(tokens, vocab_size: int, vocab_json: dict | None) -> bytes:
     vb = json.dumps(vocab_json, separators=(",", ":")).encode() if vocab_json is not None else b""
     hdr = np.array([0x44584654, vocab_size, len(tokens), len(vb)], dtype="<u4")
     return hdr.tobytes() + np.asarray(tokens, dtype="<u4").tobytes() + vb
+
+
+# ─────────────────────── GPT-4 rule pre-tokenizer (word starts) ─────────────────
+# Restates src/wasm/pre_tokenizer.mjs (PreTokenizer.preTokenizeBytes, :459-509)
+# for already-NFC UTF-8 input: utf8ToCodepoints (:517-551), classify (:128-136),
+# findWordBoundaries (:226-292), byte mapping (:497-506).  Classes come from
+# Python's unicodedata here; the reference uses its Decoder WASM tables
+# (Unicode 17), so non-ASCII codepoints whose category changed are unpinned.
+
+import unicodedata as _ud
+
+PT_LETTER, PT_DIGIT, PT_WHITESPACE, PT_PUNCT, PT_SYMBOL, PT_NEWLINE, PT_OTHER = range(7)   # :34-42
+_PT_NEWLINES = {0x0A, 0x0D, 0x0085, 0x2028, 0x2029}                                        # :44
+_PT_WHITE_SPACE = set(range(0x09, 0x0E)) | {0x20, 0x85, 0xA0, 0x1680} | set(range(0x2000, 0x200B)) | \
+    {0x2028, 0x2029, 0x202F, 0x205F, 0x3000}                                               # PropList White_Space
+_PT_SINGLE = {0x73, 0x53, 0x74, 0x54, 0x6D, 0x4D, 0x64, 0x44}                              # :56-61
+_PT_TWO = [(0x72, 0x52, 0x65, 0x45), (0x76, 0x56, 0x65, 0x45), (0x6C, 0x4C, 0x6C, 0x4C)]    # :68-72
+_PT_APOS = {0x27, 0x2019}                                                                  # :75
+
+
+def pt_classify(cp: int) -> int:
+    """classify(), pre_tokenizer.mjs:128-136 (decoder predicates as general categories)."""
+    if cp in _PT_NEWLINES:
+        return PT_NEWLINE
+    try:
+        cat = _ud.category(chr(cp))
+    except ValueError:
+        return PT_OTHER
+    if cat[0] in "LM":
+        return PT_LETTER
+    if cat[0] == "N":
+        return PT_DIGIT
+    if cp in _PT_WHITE_SPACE:
+        return PT_WHITESPACE
+    if cat[0] == "P":
+        return PT_PUNCT
+    if cat[0] == "S":
+        return PT_SYMBOL
+    return PT_OTHER
+
+
+def utf8_to_codepoints(b: bytes):
+    """utf8ToCodepoints, pre_tokenizer.mjs:517-551: the lead byte picks the size;
+    bytes past the end read as 0 (JS `undefined & 0x3F`).  Returns (cps, sizes)."""
+    cps, sizes = [], []
+    i, n = 0, len(b)
+    at = lambda k: b[k] if k < n else 0
+    while i < n:
+        c = b[i]
+        if c < 0x80:
+            cp, sz = c, 1
+        elif (c & 0xE0) == 0xC0:
+            cp, sz = ((c & 0x1F) << 6) | (at(i + 1) & 0x3F), 2
+        elif (c & 0xF0) == 0xE0:
+            cp, sz = ((c & 0x0F) << 12) | ((at(i + 1) & 0x3F) << 6) | (at(i + 2) & 0x3F), 3
+        else:
+            cp, sz = (((c & 0x07) << 18) | ((at(i + 1) & 0x3F) << 12) | ((at(i + 2) & 0x3F) << 6) |
+                      (at(i + 3) & 0x3F)), 4
+        cps.append(cp)
+        sizes.append(sz)
+        i += sz
+    return cps, sizes
+
+
+def _utf8_len(cp: int) -> int:
+    """utf8ByteLength, pre_tokenizer.mjs:301-306."""
+    return 1 if cp <= 0x7F else 2 if cp <= 0x7FF else 3 if cp <= 0xFFFF else 4
+
+
+def _match_contraction(cps, cls, i):
+    """matchContraction, pre_tokenizer.mjs:85-114."""
+    n = len(cps)
+    if i + 1 >= n:
+        return 0
+    nxt = cps[i + 1]
+    after_non_letter = i + 2 >= n or cls[i + 2] != PT_LETTER
+    if nxt in _PT_SINGLE and after_non_letter:
+        return 2
+    if i + 2 < n:
+        nn = cps[i + 2]
+        after_two = i + 3 >= n or cls[i + 3] != PT_LETTER
+        for lo1, hi1, lo2, hi2 in _PT_TWO:
+            if nxt in (lo1, hi1) and nn in (lo2, hi2) and after_two:
+                return 3
+    return 0
+
+
+def _class_transition(prev, curr):
+    """isClassTransitionBoundary, pre_tokenizer.mjs:185-200."""
+    ps = lambda c: c in (PT_PUNCT, PT_SYMBOL)
+    return ((prev == PT_LETTER and curr == PT_DIGIT) or (prev == PT_DIGIT and curr == PT_LETTER) or
+            (prev == PT_LETTER and ps(curr)) or (ps(prev) and curr == PT_LETTER) or
+            (ps(prev) and curr == PT_DIGIT) or (prev == PT_DIGIT and ps(curr)))
+
+
+def gpt4_word_starts(data: bytes) -> np.ndarray:
+    """Byte-level word-start mask of PreTokenizer.preTokenizeBytes for NFC input
+    (findWordBoundaries, pre_tokenizer.mjs:226-292; byte mapping :497-506)."""
+    b = bytes(data)
+    out = np.zeros(len(b), dtype=np.uint8)
+    if not b:
+        return out
+    cps, _ = utf8_to_codepoints(b)
+    cls = [pt_classify(c) for c in cps]
+    n = len(cps)
+    starts = [0] * n
+    starts[0] = 1
+    i = 1
+    while i < n:
+        prev, curr = cls[i - 1], cls[i]
+        if curr == PT_NEWLINE or prev == PT_NEWLINE:
+            starts[i] = 1
+            i += 1
+            continue
+        if curr == PT_WHITESPACE:
+            if prev != PT_WHITESPACE:
+                starts[i] = 1
+            i += 1
+            continue
+        if prev == PT_WHITESPACE:
+            i += 1
+            continue
+        if prev == PT_LETTER and cps[i] in _PT_APOS:
+            k = _match_contraction(cps, cls, i)
+            if k > 0:
+                i += k
+                continue
+        if _class_transition(prev, curr):
+            starts[i] = 1
+            i += 1
+            continue
+        if curr == PT_DIGIT and prev == PT_DIGIT:
+            rs = i - 1
+            while rs > 0 and cls[rs - 1] == PT_DIGIT:
+                rs -= 1
+            if (i - rs) % 3 == 0:
+                starts[i] = 1
+            i += 1
+            continue
+        i += 1
+    pos = 0                                   # byte mapping by the codepoint's own length (:497-506)
+    for k in range(n):
+        if starts[k] and pos < len(b):
+            out[pos] = 1
+        pos += _utf8_len(cps[k])
+    return out

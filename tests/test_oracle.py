@@ -240,3 +240,13 @@ def test_c_oracle_encode_matches_python():
     for cs in (1, 5, 512):
         assert np.array_equal(cpu_ref.encode(text, nodes, edges, cs, threads=4),
                               O.encode_chunked(text, nodes, edges, cs))
+
+
+def test_gpt4_pretokenizer_oracle_vs_reference_goldens():
+    """oracle.gpt4_word_starts vs the reference pre_tokenizer.mjs (tests/golden/ref_pretok.json)."""
+    d = json.load(open(os.path.join(GOLDEN, "ref_pretok.json")))
+    for inp, out in zip(d["inputs"], d["outputs"]):
+        b = bytes.fromhex(inp["hex"])
+        assert out["bytes"] == inp["hex"]          # NFC input: bytes pass through
+        exp = np.frombuffer(bytes.fromhex(out["word_starts"]), np.uint8)
+        np.testing.assert_array_equal(O.gpt4_word_starts(b), exp, err_msg=inp["name"])
