@@ -218,6 +218,27 @@ napi_value WordBoundary(napi_env env, napi_callback_info info) {
     return ta;
 }
 
+// GPT-4 rule word starts (PreTokenizer.preTokenizeBytes, pre_tokenizer.mjs:459-509)
+napi_value PretokenizeGpt4(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    Ctx* c = argc >= 1 ? unwrap_external<Ctx>(env, argv[0]) : nullptr;
+    const uint8_t* data = nullptr;
+    size_t len = 0;
+    if (!c || !c->ctx || argc < 2 || !get_bytes(env, argv[1], &data, &len)) {
+        napi_throw_type_error(env, nullptr, "pretokenizeGpt4(ctx, Uint8Array)");
+        return nullptr;
+    }
+    napi_value ab, ta;
+    void* dst = nullptr;
+    NAPI_CALL(env, napi_create_arraybuffer(env, len, &dst, &ab));
+    int rc = gbpe_pretokenize_gpt4(c->ctx, data, len, static_cast<uint8_t*>(dst));
+    if (rc != GBPE_OK) return throw_status(env, c->ctx, "pretokenizeGpt4", rc);
+    NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, len, ab, 0, &ta));
+    return ta;
+}
+
 // ── trainer ──────────────────────────────────────────────────────────────
 
 void trainer_finalize(napi_env, void* data, void*) {
@@ -467,6 +488,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"limits", nullptr, Limits, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"kernelNames", nullptr, KernelNames, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"wordBoundary", nullptr, WordBoundary, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"pretokenizeGpt4", nullptr, PretokenizeGpt4, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"trainerCreate", nullptr, TrainerCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"trainerStep", nullptr, TrainerStep, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"trainerDestroy", nullptr, TrainerDestroy, nullptr, nullptr, nullptr, napi_default, nullptr},

@@ -3,3 +3,4 @@ export { BPETrainer, BATCH_SIZE } from './trainer.js';
 export { TrieTokenizer } from './tokenizer.js';
 export { Vocab, displayString } from './vocab.js';
 export { compileVocabToTrie, parseHeader, parseTrieBuffers } from './trie.js';
+export { GpuPreTokenizer } from './pretokenizer.js';

@@ -1,7 +1,7 @@
 // GPU checks through the N-API addon: BPETrainer / TrieTokenizer results
 // must equal the expectations the CPU oracle produced (argv[2] JSON).
 import fs from 'fs';
-import { BPEEngine, BPETrainer, TrieTokenizer } from '../../gpu-bpe_amd/js/index.js';
+import { BPEEngine, BPETrainer, TrieTokenizer, GpuPreTokenizer } from '../../gpu-bpe_amd/js/index.js';
 
 const cases = JSON.parse(fs.readFileSync(process.argv[2]));
 function fail(msg) { console.error('FAIL ' + msg); process.exit(1); }
@@ -28,6 +28,16 @@ async function main() {
         if (Buffer.compare(Buffer.from(tok.decode(ids)), Buffer.from(text)) !== 0) fail('decode ' + c.name);
         tok.destroy();
         checks++;
+    }
+    if (cases.pretok) {   // GPT-4 rule word starts + training through the preTokenizer option
+        const p = cases.pretok;
+        const bytes = new Uint8Array(Buffer.from(p.b64, 'base64'));
+        const pt = new GpuPreTokenizer(engine);
+        const r = pt.preTokenizeBytes(bytes);
+        if (JSON.stringify(Array.from(r.wordStarts)) !== JSON.stringify(p.word_starts)) fail('pretok wordStarts');
+        const t = await new BPETrainer(engine).train(bytes, { targetVocabSize: p.target, preTokenizer: pt });
+        if (JSON.stringify(t.merges) !== JSON.stringify(p.merges)) fail('pretok merges');
+        checks += 2;
     }
     let threw = false;
     try { await new BPETrainer(engine).train(new Uint8Array(0)); } catch (e) { threw = /empty/.test(e.message); }

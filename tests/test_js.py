@@ -49,6 +49,10 @@ def test_js_addon_train_and_encode(tmp_path):
         cases.append({"name": name, "b64": base64.b64encode(data).decode(), "target": target, "merges": merges,
                       "export": voc.export(), "text_b64": base64.b64encode(text).decode(), "chunkSize": cs,
                       "tokens": toks})
+    code = synth.code(30000, seed=45)
+    ws = O.gpt4_word_starts(code)
+    pre = {"b64": base64.b64encode(code).decode(), "word_starts": ws.tolist(), "target": 500,
+           "merges": [m[:3] for m in O.train(code, 500, word_starts=ws)["merges"]]}
     p = tmp_path / "cases.json"
-    p.write_text(json.dumps({"train": cases}))
+    p.write_text(json.dumps({"train": cases, "pretok": pre}))
     assert _run("test_gpu.mjs", str(p)).strip().splitlines()[-1].startswith("ok")
