@@ -200,6 +200,9 @@ def shard_corpus(args, rank):
     return data[:-1] + b"\n"          # shard starts stay word starts in the global stream
 
 
+_COMM = {}   # one RCCL communicator per process, created in the warmup (outside the timed region)
+
+
 def run_sharded(args, lib, ctx, dist, rank, world, d, n, steps, table_log2):
     import torch
     from gpubpe.sharded import GpuShardBackend, ShardedTrainer
@@ -208,6 +211,10 @@ def run_sharded(args, lib, ctx, dist, rank, world, d, n, steps, table_log2):
                          stream=torch.cuda.current_stream().cuda_stream)
     tr = ShardedTrainer(be, dist.dist, device="cuda", staged=dist.transport != "nccl")
     tr.setup()
+    if dist.transport == "nccl" and os.environ.get("GBPE_SHARD_LOOP", "native") == "native":
+        # whole steps inside the library: RCCL all-gather on its own stream
+        _COMM["c"] = tr.attach_native_comm(_COMM.get("c"))
+        be.owns_comm = False
     merges, done_steps, early = [], 0, False
     needed = min(args.vocab - 256, 128 * steps)     # stalled steps are redone: count merges, not steps
     while len(merges) < needed and not early:
@@ -245,7 +252,7 @@ def train_leg_sharded(args, lib, ctx, dist, rank, world):
         "merges": len(merges), "steps": steps, "early_stop": early, "wall_s": wall,
         "final_symbols_rank": int(st.symbol_count), "bytes_per_symbol": int(st.bytes_per_symbol),
         "stream_bytes": stream_bytes, "stalls": tr.stalls, "record_caps": [tr.C, tr.Cw],
-        "transport": dist.transport, "last_merge": merges[-1] if merges else [],
+        "transport": dist.transport + (" (native step loop)" if tr.native else " (host loop)"), "last_merge": merges[-1] if merges else [],
         "tail_dropped": int(st.tail_dropped),
     }
     return data, merges, res
@@ -494,6 +501,8 @@ def main():
             line["parity"]["encode_tokens_checked"] = int(len(ref_tokens))
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if _COMM.get("c"):
+        lib.gbpe_comm_destroy(_COMM["c"])
     lib.gbpe_ctx_destroy(ctx)
 
 

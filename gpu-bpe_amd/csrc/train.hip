@@ -94,6 +94,11 @@ struct DevState {
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
+// exchange-record header words of sharded training (gpubpe/sharded.py mirrors them)
+enum : uint32_t {
+    H_ACTIVE = 0, H_L, H_KEPT, H_M, H_W, H_LASTSYM, H_HASLAST, H_SURV, H_LN, H_MC, H_A, H_B, H_ID, H_DFULL, HDR = 16
+};
+
 enum : uint32_t {
     ERR_TABLE_FULL = 1, ERR_COUNT_MISMATCH = 2, ERR_PAIR_MISSING = 4, ERR_SPIN = 8,
     ERR_SHARD_CAPACITY = 16,   // a rank's stream outgrew its buffers (stale window appended)
@@ -275,7 +280,7 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
     (void)rwlist;
     if (finish && !st->stop && !st->stall && st->merges_done == round + 1u) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
-            if (st->sharded) {   // commit the new global layout computed by k_shard_apply
+            if (st->sharded) {   // commit the new global layout computed by k_shard_recv
                 st->tail_total += st->m_glob;
                 st->poff = st->off;
                 st->pln = st->n;
@@ -351,9 +356,11 @@ constexpr uint32_t GSTR = 64;   // group sums 256 B apart: each is its own atomi
 
 // argmax over block maxima + the reference's bpe_setup_merge (train.wgsl:340-364)
 __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, uint32_t* __restrict__ log,
-                                                        uint32_t* __restrict__ grpsum, uint32_t* __restrict__ nlog) {
+                                                        uint32_t* __restrict__ grpsum, uint32_t* __restrict__ nlog,
+                                                        uint32_t* __restrict__ rec) {
     __shared__ uint64_t red[SEL_THREADS / 64];
     __shared__ uint32_t rlive[SEL_THREADS / 64];
+    if (rec && threadIdx.x == 0) rec[H_L] = 0u;   // the send kernel's list blocks add their counts into it
     if (st->stop || st->stall) return;
     {   // group sums of the coming stream pass start at zero
         const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(st->n, TILE), GRP);
@@ -622,7 +629,7 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
     const uint32_t limit = EXACT ? n : new_n;
     const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
     if (tl >= ntiles) {
-        if (EXACT || st->sharded) return;   // sharded: the window is handled by k_shard_apply
+        if (EXACT || st->sharded) return;   // sharded: the window is handled by k_shard_recv
         // ── stale tail window ──
         const uint32_t m = st->m;
         if (m == 0) return;
@@ -811,6 +818,9 @@ struct gbpe_trainer {
     uint32_t* d_nlog = nullptr;    // local length before each merge of a step
     uint32_t* h_nlog = nullptr;    // pinned
     uint32_t step_k = 0;
+    uint32_t* rec_send = nullptr;  // exchange records of gbpe_shard_step_comm
+    uint32_t* rec_recv = nullptr;
+    uint64_t rec_words = 0;
     // stats
     uint64_t bytes_moved = 0;
     uint64_t max_live = 0;
@@ -867,7 +877,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
     hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
-                       (uint32_t*)nullptr);
+                       (uint32_t*)nullptr, (uint32_t*)nullptr);
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
     if (exact) {
         hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
@@ -1197,6 +1207,8 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->dt.slots);
     hipFree(t->dt.dirty);
     hipFree(t->d_nlog);
+    hipFree(t->rec_send);
+    hipFree(t->rec_recv);
     if (t->h_nlog) hipHostFree(t->h_nlog);
     hipFree(t->st);
     hipFree(t->d_log);
@@ -1272,20 +1284,18 @@ extern "C" int gbpe_word_boundary(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t 
 // One rank per GPU; every rank keeps a replica of the GLOBAL pair-count table.
 // Per merge (protocol: gpubpe/sharded.py, pinned on CPU by tests/test_sharded.py):
 //   phase 1  k_select (on the replica) → k_delta (local sites; deltas into the
-//            per-merge delta table) → k_shard_list (delta table → record list,
-//            clearing it) → k_shard_header (header + this rank's piece of the
-//            stale-window superset [gnew - mc, gnew) of the previous input stream)
-//   host     one all-gather of the fixed-size records
-//   phase 2  k_shard_apply (every rank's deltas + the window's pairs into the
-//            replica, new global layout) → k_compact (local keep limit) →
-//            k_shard_append (the owner rank appends the window) → k_refresh.
+//            per-merge delta table) → k_shard_send (delta table → record list,
+//            clearing it; the header; this rank's piece of the stale-window
+//            superset [gnew - mc, gnew) of the previous input stream)
+//   exchange one all-gather of the fixed-size records (host loop or
+//            gbpe_shard_step_comm's ncclAllGather)
+//   phase 2  k_shard_recv (every rank's deltas + the window's pairs into the
+//            replica, new global layout; the owner rank appends the window) →
+//            k_compact (local keep limit) → k_refresh.
 // A record that does not fit stalls the merge on every rank (selection undone).
 
 namespace {
 
-enum : uint32_t {
-    H_ACTIVE = 0, H_L, H_KEPT, H_M, H_W, H_LASTSYM, H_HASLAST, H_SURV, H_LN, H_MC, H_A, H_B, H_ID, HDR = 16
-};
 
 template <typename S>
 __device__ __forceinline__ uint32_t to_canon(uint32_t x) {
@@ -1296,77 +1306,78 @@ __device__ __forceinline__ uint32_t from_canon(uint32_t x) {
     return (x & 0xFFFFu) | ((x & 0x10000u) ? Sym<S>::WS : 0u);
 }
 
-// delta table (dirty blocks only) → record list {pid, delta}; clears what it reads
-__global__ __launch_bounds__(TPB) void k_shard_list(DevState* st, uint32_t round, Table dt, uint32_t* __restrict__ rec,
-                                                    uint32_t cap) {
+// Phase-1 send kernel, three block roles:
+//   [0, nlb)        delta table (dirty blocks only) → record list {pid, delta},
+//                   clearing what they read; each adds its count to rec[H_L]
+//   nlb             the header (survivors, kept / tail counts, last kept symbol)
+//   (nlb, grid)     this rank's piece of the stale-window superset
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_shard_send(DevState* st, uint32_t round, Table dt, const S* __restrict__ cur,
+                                                    const S* __restrict__ oth, const uint32_t* __restrict__ hitmask,
+                                                    const uint32_t* __restrict__ grpsum, uint32_t* __restrict__ rec,
+                                                    uint32_t cap_list, uint32_t cap_win, uint32_t nlb) {
     __shared__ uint64_t s_dmask;
     __shared__ uint32_t wcnt[TPB / 64], s_base;
-    if (!merge_active(st, round)) return;
-    const uint32_t per = (dt.nblk + gridDim.x - 1) / gridDim.x;
-    const uint32_t b0 = blockIdx.x * per;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (threadIdx.x < 64) {
-        const uint32_t blk = b0 + threadIdx.x;
-        const bool d = threadIdx.x < per && blk < dt.nblk && dt.dirty[blk];
-        const unsigned long long m = __ballot(d);
-        if (threadIdx.x == 0) s_dmask = m;
-    }
-    __syncthreads();
-    uint64_t dm = s_dmask;
-    constexpr int NV = (1 << BLK_LOG2) / 2 / TPB;
-    while (dm) {
-        const uint32_t blk = b0 + (uint32_t)(__ffsll((long long)dm) - 1);
-        dm &= dm - 1;
-        uint4* sl = reinterpret_cast<uint4*>(dt.slots + ((uint64_t)blk << BLK_LOG2));
-        uint4 e[NV];
-#pragma unroll
-        for (int k = 0; k < NV; ++k) e[k] = sl[threadIdx.x + k * TPB];
-        uint32_t c = 0;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) c += (e[k].x && e[k].y) + (e[k].z && e[k].w);
-        uint32_t incl = c;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t v = __shfl_up(incl, o);
-            if (lane >= o) incl += v;
-        }
-        if (lane == 63) wcnt[wid] = incl;
-        __syncthreads();
-        uint32_t pre = incl - c, tot = 0;
-        for (int w = 0; w < TPB / 64; ++w) {
-            pre += w < wid ? wcnt[w] : 0u;
-            tot += wcnt[w];
-        }
-        if (threadIdx.x == 0) {
-            s_base = tot ? atomicAdd(&st->dcount, tot) : 0u;
-            dt.dirty[blk] = 0u;
-        }
-        __syncthreads();
-        uint32_t o = s_base + pre;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-            if (e[k].x && e[k].y) {
-                if (o < cap) { rec[HDR + 2 * o] = e[k].x; rec[HDR + 2 * o + 1] = e[k].y; }
-                ++o;
-            }
-            if (e[k].z && e[k].w) {
-                if (o < cap) { rec[HDR + 2 * o] = e[k].z; rec[HDR + 2 * o + 1] = e[k].w; }
-                ++o;
-            }
-            if (e[k].x || e[k].z) sl[threadIdx.x + k * TPB] = make_uint4(0u, 0u, 0u, 0u);
-        }
-        __syncthreads();
-    }
-}
-
-// record header + this rank's piece of the stale-window superset
-template <typename S>
-__global__ __launch_bounds__(TPB) void k_shard_header(DevState* st, uint32_t round, const S* __restrict__ cur,
-                                                      const S* __restrict__ oth, const uint32_t* __restrict__ hitmask,
-                                                      const uint32_t* __restrict__ grpsum, uint32_t* __restrict__ rec,
-                                                      uint32_t cap_list, uint32_t cap_win) {
-    __shared__ uint32_t wred[TPB / 64];
     if (!merge_active(st, round)) {
-        if (blockIdx.x == 0 && threadIdx.x < HDR) rec[threadIdx.x] = 0u;   // inactive round: ACTIVE = 0
+        if (blockIdx.x == nlb && threadIdx.x < HDR) rec[threadIdx.x] = 0u;   // inactive round: ACTIVE = 0
+        return;
+    }
+    if (blockIdx.x < nlb) {   // ── list role ──
+        const uint32_t per = (dt.nblk + nlb - 1) / nlb;
+        const uint32_t b0 = blockIdx.x * per;
+        if (threadIdx.x < 64) {
+            const uint32_t blk = b0 + threadIdx.x;
+            const bool d = threadIdx.x < per && blk < dt.nblk && dt.dirty[blk];
+            const unsigned long long m = __ballot(d);
+            if (threadIdx.x == 0) s_dmask = m;
+        }
+        __syncthreads();
+        uint64_t dm = s_dmask;
+        constexpr int NV = (1 << BLK_LOG2) / 2 / TPB;
+        while (dm) {
+            const uint32_t blk = b0 + (uint32_t)(__ffsll((long long)dm) - 1);
+            dm &= dm - 1;
+            uint4* sl = reinterpret_cast<uint4*>(dt.slots + ((uint64_t)blk << BLK_LOG2));
+            uint4 e[NV];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) e[k] = sl[threadIdx.x + k * TPB];
+            uint32_t c = 0;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) c += (e[k].x && e[k].y) + (e[k].z && e[k].w);
+            uint32_t incl = c;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = __shfl_up(incl, o);
+                if (lane >= o) incl += v;
+            }
+            if (lane == 63) wcnt[wid] = incl;
+            __syncthreads();
+            uint32_t pre = incl - c, tot = 0;
+            for (int w = 0; w < TPB / 64; ++w) {
+                pre += w < wid ? wcnt[w] : 0u;
+                tot += wcnt[w];
+            }
+            if (threadIdx.x == 0) {
+                s_base = tot ? atomicAdd(&st->dcount, tot) : 0u;
+                if (tot) atomicAdd(&rec[H_L], tot);
+                dt.dirty[blk] = 0u;
+            }
+            __syncthreads();
+            uint32_t o = s_base + pre;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {
+                if (e[k].x && e[k].y) {
+                    if (o < cap_list) { rec[HDR + 2 * o] = e[k].x; rec[HDR + 2 * o + 1] = e[k].y; }
+                    ++o;
+                }
+                if (e[k].z && e[k].w) {
+                    if (o < cap_list) { rec[HDR + 2 * o] = e[k].z; rec[HDR + 2 * o + 1] = e[k].w; }
+                    ++o;
+                }
+                if (e[k].x || e[k].z) sl[threadIdx.x + k * TPB] = make_uint4(0u, 0u, 0u, 0u);
+            }
+            __syncthreads();
+        }
         return;
     }
     const bool exact = (st->sharded & 2u) != 0;
@@ -1380,14 +1391,17 @@ __global__ __launch_bounds__(TPB) void k_shard_header(DevState* st, uint32_t rou
         const uint64_t a1 = hi < pe ? hi : pe;
         if (a1 > a0) { w = (uint32_t)(a1 - a0); src0 = (uint32_t)(a0 - st->poff); }
     }
-    const uint32_t wc = w < cap_win ? w : cap_win;
-    uint32_t* win = rec + HDR + 2 * (uint64_t)cap_list;
-    for (uint32_t i = blockIdx.x * TPB + threadIdx.x; i < wc; i += gridDim.x * TPB) win[i] = to_canon<S>(oth[src0 + i]);
-    if (blockIdx.x != 0) return;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    // local survivors = sum of the group sums k_delta accumulated
+    if (blockIdx.x > nlb) {   // ── window role ──
+        const uint32_t wc = w < cap_win ? w : cap_win;
+        uint32_t* win = rec + HDR + 2 * (uint64_t)cap_list;
+        const uint32_t nb = gridDim.x - nlb - 1, b = blockIdx.x - nlb - 1;
+        for (uint32_t i = b * TPB + threadIdx.x; i < wc; i += nb * TPB) win[i] = to_canon<S>(oth[src0 + i]);
+        return;
+    }
+    // ── header role ──
+    __shared__ uint32_t wred[TPB / 64];
     const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(n, TILE), GRP);
-    uint32_t surv = 0;
+    uint32_t surv = 0;   // local survivors = sum of the group sums k_delta accumulated
     for (uint32_t g = threadIdx.x; g < ngrp; g += TPB) surv += grpsum[g * GSTR];
     for (int o = 32; o > 0; o >>= 1) surv += __shfl_xor(surv, o);
     if (lane == 0) wred[wid] = surv;
@@ -1421,8 +1435,6 @@ __global__ __launch_bounds__(TPB) void k_shard_header(DevState* st, uint32_t rou
     }
     const uint32_t m_r = st->m;
     rec[H_ACTIVE] = 1u;
-    // an overflowed delta table (sized 4x the list capacity) reports a list that cannot fit
-    rec[H_L] = st->dfull ? max(st->dcount, 4u * cap_list) : st->dcount;
     rec[H_KEPT] = surv - m_r;
     rec[H_M] = m_r;
     rec[H_W] = w;
@@ -1434,7 +1446,8 @@ __global__ __launch_bounds__(TPB) void k_shard_header(DevState* st, uint32_t rou
     rec[H_A] = st->a;
     rec[H_B] = st->b;
     rec[H_ID] = st->nw;
-    for (int k = H_ID + 1; k < HDR; ++k) rec[k] = 0u;
+    rec[H_DFULL] = st->dfull;   // an overflowed delta table: the list in this record is incomplete
+    for (int k = H_DFULL + 1; k < HDR; ++k) rec[k] = 0u;
 }
 
 struct ShardView {   // per-WG decisions from the gathered headers (identical on every rank)
@@ -1453,13 +1466,14 @@ __device__ void shard_view(const DevState* st, const uint32_t* __restrict__ recv
         const uint32_t M = in ? h[H_M] : 0u, S = in ? h[H_SURV] : 0u;
         const bool bad = in && (h[H_ACTIVE] != 1u || h[H_MC] != st->mc || h[H_A] != st->a || h[H_B] != st->b ||
                                 h[H_ID] != st->nw);
-        const bool ovf = in && (L > cap_list || W > cap_win);
+        const bool dfull = in && h[H_DFULL] != 0u;
+        const bool ovf = in && (L > cap_list || W > cap_win || dfull);
         uint32_t li = L, wi = W;
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t a = __shfl_up(li, o), b = __shfl_up(wi, o);
             if ((int)q >= o) { li += a; wi += b; }
         }
-        uint32_t m = M, surv = S, ml = L, mw = W;
+        uint32_t m = M, surv = S, ml = dfull ? max(L, 4u * cap_list) : L, mw = W;
         for (int o = 32; o > 0; o >>= 1) {
             m += __shfl_xor(m, o);
             surv += __shfl_xor(surv, o);
@@ -1498,14 +1512,28 @@ __device__ __forceinline__ uint32_t sup_at(const ShardView& v, const uint32_t* _
     return recv[(uint64_t)q * rw + HDR + 2 * cap_list + (g - v.wpre[q])];
 }
 
-__global__ __launch_bounds__(TPB) void k_shard_apply(DevState* st, uint32_t round, const uint32_t* __restrict__ recv,
-                                                     uint32_t R, uint32_t cap_list, uint32_t cap_win, Table tb,
-                                                     uint32_t cap_syms) {
+// Phase-2 receive kernel, two block roles (after one all-gather of the records):
+//   [0, nab)     every rank's count deltas + the stale window's pairs into the
+//                replica; block 0 also commits the new global layout
+//   [nab, grid)  the owner rank (last one that kept a survivor) appends the window
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_shard_recv(DevState* st, uint32_t round, const uint32_t* __restrict__ recv,
+                                                    uint32_t R, uint32_t cap_list, uint32_t cap_win, Table tb,
+                                                    uint32_t cap_syms, S* __restrict__ oth, uint32_t nab) {
     __shared__ ShardView v;
     __shared__ LdsTab<LTAB> lt;
     if (!merge_active(st, round)) return;
     const uint32_t rw = HDR + 2 * cap_list + cap_win;
     shard_view(st, recv, R, rw, cap_list, cap_win, v);
+    if (blockIdx.x >= nab) {   // ── append role ──
+        if (v.bad || v.overflow || v.m == 0 || v.owner != st->rank) return;
+        const uint32_t kept = v.K[st->rank];
+        if ((uint64_t)kept + v.m + TILE > cap_syms) return;   // block 0 flags ERR_SHARD_CAPACITY
+        const uint32_t g0 = v.wpre[R] - v.m, nb = gridDim.x - nab, b = blockIdx.x - nab;
+        for (uint32_t j = b * TPB + threadIdx.x; j < v.m; j += nb * TPB)
+            oth[kept + j] = (S)from_canon<S>(sup_at(v, recv, R, rw, cap_list, g0 + j));
+        return;
+    }
     if (v.bad) {
         if (blockIdx.x == 0 && threadIdx.x == 0) { atomicOr(&st->err, ERR_SHARD_RECORD); st->stop = 1u; }
         return;
@@ -1551,7 +1579,7 @@ __global__ __launch_bounds__(TPB) void k_shard_apply(DevState* st, uint32_t roun
     }
     // every rank's count deltas into the replica
     const uint32_t total = v.lpre[R];
-    for (uint32_t e = blockIdx.x * TPB + threadIdx.x; e < total; e += gridDim.x * TPB) {
+    for (uint32_t e = blockIdx.x * TPB + threadIdx.x; e < total; e += nab * TPB) {
         uint32_t q = 0;
         while (q + 1 < R && v.lpre[q + 1] <= e) ++q;
         const uint32_t* l = recv + (uint64_t)q * rw + HDR + 2 * (e - v.lpre[q]);
@@ -1563,7 +1591,7 @@ __global__ __launch_bounds__(TPB) void k_shard_apply(DevState* st, uint32_t roun
     lds_clear(lt);
     __syncthreads();
     const uint32_t sup = v.wpre[R], g0 = sup - m;
-    for (uint32_t j = blockIdx.x * TPB + threadIdx.x; j < m; j += gridDim.x * TPB) {
+    for (uint32_t j = blockIdx.x * TPB + threadIdx.x; j < m; j += nab * TPB) {
         uint32_t xp;
         if (j == 0) {
             if (!v.has_x0) continue;
@@ -1576,23 +1604,6 @@ __global__ __launch_bounds__(TPB) void k_shard_apply(DevState* st, uint32_t roun
         if (!(x & 0x10000u) && t0 && t1) lds_add(lt, tb, st, (t0 << 16) | t1, 1u);
     }
     lds_flush(lt, tb, st);
-}
-
-// the owner rank appends the stale window after its kept survivors
-template <typename S>
-__global__ __launch_bounds__(TPB) void k_shard_append(DevState* st, uint32_t round, const uint32_t* __restrict__ recv,
-                                                      uint32_t R, uint32_t cap_list, uint32_t cap_win,
-                                                      S* __restrict__ oth) {
-    __shared__ ShardView v;
-    if (!merge_active(st, round)) return;
-    const uint32_t m = st->m_glob;
-    if (m == 0 || st->owner != st->rank || (st->err & ERR_SHARD_CAPACITY)) return;
-    const uint32_t rw = HDR + 2 * cap_list + cap_win;
-    shard_view(st, recv, R, rw, cap_list, cap_win, v);
-    const uint32_t kept = v.K[st->rank];
-    const uint32_t g0 = v.wpre[R] - m;
-    for (uint32_t j = blockIdx.x * TPB + threadIdx.x; j < m; j += gridDim.x * TPB)
-        oth[kept + j] = (S)from_canon<S>(sup_at(v, recv, R, rw, cap_list, g0 + j));
 }
 
 __global__ void k_add_list(DevState* st, Table tb, const uint2* __restrict__ list, uint64_t n) {
@@ -1785,7 +1796,7 @@ extern "C" int gbpe_shard_step_begin(gbpe_trainer* t, uint32_t max_merges) {
 
 namespace {
 // the per-merge delta table only has to hold one merge's distinct deltas: size it
-// 4x the record's list capacity (>= 2 blocks) so k_shard_list scans few blocks
+// 4x the record's list capacity (>= 2 blocks) so k_shard_send scans few blocks
 Table delta_view(const gbpe_trainer* t, uint32_t cl) {
     Table d = t->dt;
     uint64_t want = 4ull * cl, sl = 1ull << (BLK_LOG2 + 1);
@@ -1803,18 +1814,17 @@ int shard_phase1(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl, ui
     const uint32_t eager = (uint32_t)gbpe_div_up(t->n, TILE);   // the stream may grow by appended windows
     const uint32_t g_delta = (uint32_t)gbpe_div_up(t->cap_syms, TILE) - 1;
     const Table dt = delta_view(t, cl);
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum, t->d_nlog);
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum, t->d_nlog, rec);
     if (t->flags & GBPE_TRAIN_EXACT_COMPACTION)
         hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, dt,
                            t->hitmask, t->tile_cnt, t->grpsum, eager);
     else
         hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, dt,
                            t->hitmask, t->tile_cnt, t->grpsum, eager);
-    hipLaunchKernelGGL(k_shard_list, dim3(grid_persistent(t->ctx, dt.nblk, 2)), dim3(TPB), 0, s, t->st, round, dt,
-                       rec, cl);
-    hipLaunchKernelGGL(k_shard_header<S>, dim3(grid_persistent(t->ctx, gbpe_div_up(cw, TPB * 8) + 1, 1)), dim3(TPB), 0,
-                       s, t->st, round, (const S*)cur, (const S*)oth, (const uint32_t*)t->hitmask,
-                       (const uint32_t*)t->grpsum, rec, cl, cw);
+    const uint32_t nlb = grid_persistent(t->ctx, dt.nblk, 2);
+    const uint32_t nwb = grid_persistent(t->ctx, gbpe_div_up(cw, TPB * 8) + 1, 1);
+    hipLaunchKernelGGL(k_shard_send<S>, dim3(nlb + 1 + nwb), dim3(TPB), 0, s, t->st, round, dt, (const S*)cur,
+                       (const S*)oth, (const uint32_t*)t->hitmask, (const uint32_t*)t->grpsum, rec, cl, cw, nlb);
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
 }
@@ -1827,16 +1837,15 @@ int shard_phase2(gbpe_trainer* t, uint32_t round, const uint32_t* recv, uint32_t
     const uint32_t R = t->world;
     const uint32_t g_tiles = (uint32_t)gbpe_div_up(t->cap_syms, TILE) - 1;
     const uint32_t cap = (uint32_t)t->cap_syms;
-    hipLaunchKernelGGL(k_shard_apply, dim3(grid_persistent(t->ctx, 1u << 20, 2)), dim3(TPB), 0, s, t->st, round, recv, R,
-                       cl, cw, t->tb, cap);
+    const uint32_t nab = grid_persistent(t->ctx, 1u << 20, 2), npb = grid_persistent(t->ctx, 1u << 20, 1);
+    hipLaunchKernelGGL(k_shard_recv<S>, dim3(nab + npb), dim3(TPB), 0, s, t->st, round, recv, R, cl, cw, t->tb, cap, oth,
+                       nab);
     if (t->flags & GBPE_TRAIN_EXACT_COMPACTION)
         hipLaunchKernelGGL((k_compact<S, true>), dim3(g_tiles), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
     else
         hipLaunchKernelGGL((k_compact<S, false>), dim3(g_tiles), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
-    hipLaunchKernelGGL(k_shard_append<S>, dim3(grid_persistent(t->ctx, 1u << 20, 1)), dim3(TPB), 0, s, t->st, round,
-                       recv, R, cl, cw, oth);
     hipLaunchKernelGGL(k_refresh<S>, dim3(grid_persistent(t->ctx, t->tb.nblk, 2)), dim3(TPB), 0, s, t->st, round, 1,
                        t->tb, cur, (const uint32_t*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
@@ -1910,4 +1919,127 @@ extern "C" int gbpe_shard_step_end(gbpe_trainer* t, uint32_t* merges_out, uint32
     if (need_list) *need_list = hs->stall ? hs->need_l : hs->peak_l;
     if (need_win) *need_win = hs->stall ? hs->need_w : hs->peak_w;
     return GBPE_OK;
+}
+
+// ─── native exchange: RCCL all-gather on the trainer's own stream ───────────
+//
+// The host loop of gpubpe/sharded.py issues three calls per merge (phase 1,
+// torch all-gather, phase 2) and pays a cross-stream event wait per merge.
+// gbpe_shard_step_comm runs the same protocol for a whole step inside the
+// library: phase-1 kernels, ncclAllGather, phase-2 kernels, all enqueued on one
+// stream with no host involvement.  RCCL is opened at run time (dlopen of
+// librccl.so.1: the copy torch already loaded, or ROCm's), so the library has
+// no link-time RCCL dependency.
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+struct gbpe_comm {
+    ncclComm_t comm = nullptr;
+    int device = 0;
+    uint32_t rank = 0, world = 1;
+};
+
+namespace {
+struct RcclApi {
+    bool ok = false;
+    std::string err;
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclGetErrorString) errstr = nullptr;
+};
+
+RcclApi& rccl() {
+    static RcclApi api = [] {
+        RcclApi a;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            a.err = dlerror() ? dlerror() : "dlopen(librccl.so.1) failed";
+            return a;
+        }
+        a.get_id = (decltype(a.get_id))dlsym(h, "ncclGetUniqueId");
+        a.init = (decltype(a.init))dlsym(h, "ncclCommInitRank");
+        a.destroy = (decltype(a.destroy))dlsym(h, "ncclCommDestroy");
+        a.all_gather = (decltype(a.all_gather))dlsym(h, "ncclAllGather");
+        a.errstr = (decltype(a.errstr))dlsym(h, "ncclGetErrorString");
+        a.ok = a.get_id && a.init && a.destroy && a.all_gather && a.errstr;
+        if (!a.ok) a.err = "librccl.so.1 lacks the nccl* entry points";
+        return a;
+    }();
+    return api;
+}
+}  // namespace
+
+extern "C" int gbpe_comm_unique_id(uint8_t* out, uint32_t len) {
+    if (!out || len < NCCL_UNIQUE_ID_BYTES) return GBPE_E_INVALID;
+    RcclApi& r = rccl();
+    if (!r.ok) return GBPE_E_DEVICE;
+    ncclUniqueId id;
+    if (r.get_id(&id) != ncclSuccess) return GBPE_E_DEVICE;
+    memcpy(out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return GBPE_OK;
+}
+
+extern "C" int gbpe_comm_create(gbpe_ctx* ctx, const uint8_t* id, uint32_t len, uint32_t rank, uint32_t world,
+                                gbpe_comm** out) {
+    if (!ctx || !id || !out || len < NCCL_UNIQUE_ID_BYTES || world == 0 || rank >= world)
+        return gbpe_set_error(ctx, GBPE_E_INVALID, "comm_create: bad arguments");
+    *out = nullptr;
+    RcclApi& r = rccl();
+    if (!r.ok) return gbpe_set_error(ctx, GBPE_E_DEVICE, "RCCL unavailable: %s", r.err.c_str());
+    GBPE_HIP(ctx, hipSetDevice(ctx->device));
+    ncclUniqueId uid;
+    memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+    auto* c = new (std::nothrow) gbpe_comm();
+    if (!c) return gbpe_set_error(ctx, GBPE_E_OOM, "host allocation failed");
+    ncclResult_t e = r.init(&c->comm, (int)world, uid, (int)rank);
+    if (e != ncclSuccess) {
+        delete c;
+        return gbpe_set_error(ctx, GBPE_E_DEVICE, "ncclCommInitRank: %s", r.errstr(e));
+    }
+    c->device = ctx->device;
+    c->rank = rank;
+    c->world = world;
+    *out = c;
+    return GBPE_OK;
+}
+
+extern "C" void gbpe_comm_destroy(gbpe_comm* c) {
+    if (!c) return;
+    if (c->comm && rccl().ok) rccl().destroy(c->comm);
+    delete c;
+}
+
+extern "C" int gbpe_shard_step_comm(gbpe_trainer* t, gbpe_comm* comm, uint32_t max_merges, uint32_t cap_list,
+                                    uint32_t cap_win, uint32_t* merges_out, uint32_t* n_done, uint32_t* early_stop,
+                                    uint32_t* stalled, uint32_t* need_list, uint32_t* need_win) {
+    if (!t || !t->sharded || !comm || comm->world != t->world || comm->rank != t->rank)
+        return t ? gbpe_set_error(t->ctx, GBPE_E_INVALID, "step_comm: trainer / communicator mismatch") : GBPE_E_INVALID;
+    int rc = gbpe_shard_step_begin(t, max_merges);
+    if (rc != GBPE_OK) return rc;
+    const uint64_t rw = shard_record_words(cap_list, cap_win);
+    if (t->rec_words < rw) {   // library-owned exchange records (grow only)
+        hipStream_t s0 = t->ctx->stream;
+        TR_HIP(t, hipStreamSynchronize(s0));
+        hipFree(t->rec_send);
+        hipFree(t->rec_recv);
+        t->rec_send = t->rec_recv = nullptr;
+        t->rec_words = 0;
+        TR_HIP(t, hipMalloc(&t->rec_send, rw * sizeof(uint32_t)));
+        TR_HIP(t, hipMalloc(&t->rec_recv, rw * t->world * sizeof(uint32_t)));
+        t->rec_words = rw;
+    }
+    hipStream_t s = t->ctx->stream;
+    for (uint32_t k = 0; k < t->step_k; ++k) {
+        rc = gbpe_shard_phase1(t, k, t->rec_send, cap_list, cap_win);
+        if (rc != GBPE_OK) return rc;
+        const ncclResult_t e = rccl().all_gather(t->rec_send, t->rec_recv, rw, ncclUint32, comm->comm, s);
+        if (e != ncclSuccess) return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "ncclAllGather: %s", rccl().errstr(e));
+        rc = gbpe_shard_phase2(t, k, t->rec_recv, cap_list, cap_win);
+        if (rc != GBPE_OK) return rc;
+    }
+    return gbpe_shard_step_end(t, merges_out, n_done, early_stop, stalled, need_list, need_win);
 }

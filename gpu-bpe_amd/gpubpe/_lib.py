@@ -99,6 +99,12 @@ _SIGS = [
     ("gbpe_shard_phase1", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]),
     ("gbpe_shard_phase2", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]),
     ("gbpe_shard_step_end", C.c_int, [C.c_void_p, u32p, u32p, u32p, u32p, u32p, u32p]),
+    ("gbpe_comm_unique_id", C.c_int, [C.c_void_p, C.c_uint32]),
+    ("gbpe_comm_create", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                   C.POINTER(C.c_void_p)]),
+    ("gbpe_comm_destroy", None, [C.c_void_p]),
+    ("gbpe_shard_step_comm", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, u32p, u32p, u32p,
+                                       u32p, u32p, u32p]),
 ]
 
 EXPORTED = [s[0] for s in _SIGS]

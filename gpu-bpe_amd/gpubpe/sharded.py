@@ -37,7 +37,7 @@ import ctypes as C
 import numpy as np
 
 # exchange-record header words (mirrored by csrc/train.hip)
-H_ACTIVE, H_L, H_KEPT, H_M, H_W, H_LASTSYM, H_HASLAST, H_SURV, H_LN, H_MC, H_A, H_B, H_ID = range(13)
+H_ACTIVE, H_L, H_KEPT, H_M, H_W, H_LASTSYM, H_HASLAST, H_SURV, H_LN, H_MC, H_A, H_B, H_ID, H_DFULL = range(14)
 HDR = 16
 BATCH_SIZE = 128
 
@@ -119,20 +119,48 @@ class ShardedTrainer:
             self._bufs = (send, recv)
         return self._bufs
 
+    def attach_native_comm(self, comm=None):
+        """Let the backend run whole steps natively (RCCL all-gather on its own
+        stream).  The 128-byte communicator id travels over ``dist``.  Pass a
+        communicator from an earlier trainer (``backend.comm``) to reuse it:
+        creating one costs far more than a step."""
+        if comm is not None:
+            self.b.comm, self.b.owns_comm = comm, False
+            self.native = True
+            return comm
+        torch = self.torch
+        idt = torch.zeros(128, dtype=torch.uint8, device=self.device)
+        if self.rank == 0:
+            idt.copy_(torch.from_numpy(self.b.comm_unique_id()))
+        if self.staged and idt.device.type != "cpu":
+            h = idt.cpu()
+            self.dist.broadcast(h, src=0)
+            idt = h
+        else:
+            self.dist.broadcast(idt, src=0)
+        self.b.comm_create(idt.cpu().numpy())
+        self.native = True
+        return self.b.comm
+
+    native = False
+
     def step(self, max_merges: int = BATCH_SIZE):
         """Up to ``max_merges`` global merges. Returns (merges, early_stop)."""
         b = self.b
-        b.step_begin(max_merges)
-        send, recv = self._buffers()
-        for k in range(max_merges):
-            b.phase1(k, send, self.C, self.Cw)
-            if self.staged or send.device.type == "cpu":
-                out = self._all_gather(send)
-            else:
-                self.dist.all_gather_into_tensor(recv, send)
-                out = recv
-            b.phase2(k, out, self.C, self.Cw)
-        res = b.step_end()
+        if self.native:
+            res = b.step_comm(max_merges, self.C, self.Cw)
+        else:
+            b.step_begin(max_merges)
+            send, recv = self._buffers()
+            for k in range(max_merges):
+                b.phase1(k, send, self.C, self.Cw)
+                if self.staged or send.device.type == "cpu":
+                    out = self._all_gather(send)
+                else:
+                    self.dist.all_gather_into_tensor(recv, send)
+                    out = recv
+                b.phase2(k, out, self.C, self.Cw)
+            res = b.step_end()
         if res["stalled"]:
             self.stalls += 1
             self.C = _pow2_at_least(2 * res["need_list"], self.C)
@@ -231,6 +259,33 @@ class GpuShardBackend:
         return {"merges": merges, "early_stop": bool(es.value), "stalled": bool(st.value),
                 "need_list": int(nl.value), "need_win": int(nwn.value)}
 
+    # ── native exchange (gbpe_shard_step_comm) ──
+    comm = None
+    owns_comm = True
+
+    def comm_unique_id(self):
+        buf = (C.c_uint8 * 128)()
+        rc = self.lib.gbpe_comm_unique_id(buf, 128)
+        if rc != 0:
+            raise self._lib.GpuBpeError(rc, "gbpe_comm_unique_id failed (RCCL unavailable)")
+        return np.frombuffer(bytes(buf), dtype=np.uint8).copy()
+
+    def comm_create(self, uid):
+        arr = (C.c_uint8 * 128)(*[int(x) for x in uid])
+        c = C.c_void_p()
+        self._lib.check(self.lib.gbpe_comm_create(self.ctx, arr, 128, self.rank, self.world, C.byref(c)), self.ctx,
+                        "gbpe_comm_create")
+        self.comm = c
+
+    def step_comm(self, max_merges, cap_list, cap_win):
+        nd, es, st, nl, nwn = C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint32()
+        self._lib.check(self.lib.gbpe_shard_step_comm(self.t, self.comm, max_merges, cap_list, cap_win, self._out,
+                                                      C.byref(nd), C.byref(es), C.byref(st), C.byref(nl),
+                                                      C.byref(nwn)), self.ctx, "gbpe_shard_step_comm")
+        merges = [list(self._out[4 * i: 4 * i + 4]) for i in range(nd.value)]
+        return {"merges": merges, "early_stop": bool(es.value), "stalled": bool(st.value),
+                "need_list": int(nl.value), "need_win": int(nwn.value)}
+
     def symbols(self):
         n = C.c_uint64()
         self._lib.check(self.lib.gbpe_trainer_symbols(self.t, None, 0, C.byref(n)), self.ctx, "symbols")
@@ -247,3 +302,6 @@ class GpuShardBackend:
         if self.t:
             self.lib.gbpe_trainer_destroy(self.t)
             self.t = None
+        if self.comm and self.owns_comm:
+            self.lib.gbpe_comm_destroy(self.comm)
+        self.comm = None

@@ -191,6 +191,18 @@ int gbpe_shard_phase2(gbpe_trainer* t, uint32_t round, const void* d_recv, uint3
 int gbpe_shard_step_end(gbpe_trainer* t, uint32_t* merges_out, uint32_t* n_done, uint32_t* early_stop,
                         uint32_t* stalled, uint32_t* need_list, uint32_t* need_win);
 
+/* Native exchange: the library runs a whole step (phase 1, ncclAllGather,
+ * phase 2 per merge) on its stream over an RCCL communicator (RCCL is opened
+ * at run time).  Rank 0 makes the id, the caller broadcasts it (any channel),
+ * every rank creates its communicator on its own device. */
+typedef struct gbpe_comm gbpe_comm;
+int  gbpe_comm_unique_id(uint8_t* out, uint32_t len /* >= 128 */);
+int  gbpe_comm_create(gbpe_ctx* ctx, const uint8_t* id, uint32_t len, uint32_t rank, uint32_t world, gbpe_comm** out);
+void gbpe_comm_destroy(gbpe_comm* comm);
+int  gbpe_shard_step_comm(gbpe_trainer* t, gbpe_comm* comm, uint32_t max_merges, uint32_t cap_list, uint32_t cap_win,
+                          uint32_t* merges_out, uint32_t* n_done, uint32_t* early_stop, uint32_t* stalled,
+                          uint32_t* need_list, uint32_t* need_win);
+
 /* ── trie encode (replaces tokenizer.js:54-335 TrieTokenizer over the
  *    tokenize.wgsl kernels) ─────────────────────────────────────────────── */
 
