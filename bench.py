@@ -211,10 +211,23 @@ def run_sharded(args, lib, ctx, dist, rank, world, d, n, steps, table_log2):
                          stream=torch.cuda.current_stream().cuda_stream)
     tr = ShardedTrainer(be, dist.dist, device="cuda", staged=dist.transport != "nccl")
     tr.setup()
-    if dist.transport == "nccl" and os.environ.get("GBPE_SHARD_LOOP", "native") == "native":
-        # whole steps inside the library: RCCL all-gather on its own stream
-        _COMM["c"] = tr.attach_native_comm(_COMM.get("c"))
-        be.owns_comm = False
+    if dist.transport == "nccl" and os.environ.get("GBPE_SHARD_LOOP", "native") == "native" and \
+            _COMM.get("ok", True):
+        # whole steps inside the library: RCCL all-gather on its own stream; every
+        # rank must agree, else all fall back to the host loop
+        ok = 1.0
+        try:
+            _COMM["c"] = tr.attach_native_comm(_COMM.get("c"))
+            be.owns_comm = False
+        except Exception as e:  # noqa: BLE001
+            log(f"[bench] rank {rank}: native step loop unavailable ({e}); using the host loop")
+            ok = 0.0
+        if world > 1:
+            ok = -dist.max(-ok)   # min over ranks
+        if ok < 1.0:
+            tr.native = False
+            be.comm = None
+            _COMM["ok"] = False
     merges, done_steps, early = [], 0, False
     needed = min(args.vocab - 256, 128 * steps)     # stalled steps are redone: count merges, not steps
     while len(merges) < needed and not early:
