@@ -73,6 +73,9 @@ _SIGS = [
     ("gbpe_trainer_destroy", None, [C.c_void_p]),
     ("gbpe_trie_upload", C.c_int, [C.c_void_p, u32p, C.c_uint32, u32p, C.c_uint32, C.POINTER(C.c_void_p)]),
     ("gbpe_trie_free", None, [C.c_void_p]),
+    ("gbpe_trie_compile", C.c_int, [C.c_void_p, u64p, C.c_uint32, C.c_void_p, C.c_uint64, u64p]),
+    ("gbpe_dxft_pack", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                 u64p]),
     ("gbpe_trie_info", C.c_int, [C.c_void_p, u32p, u32p, u32p]),
     ("gbpe_encode", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, u32p, C.c_uint64, u64p]),
     ("gbpe_encode_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,

@@ -10,7 +10,6 @@ v2 (8-byte nodes, 4-byte edges) is accepted on parse (trie.js:140-141).
 from __future__ import annotations
 
 import struct
-from collections import deque
 
 import numpy as np
 
@@ -20,46 +19,24 @@ HEADER_SIZE = 28
 INVALID_TOKEN = 0xFFFFFFFF
 
 
-class _Node:
-    __slots__ = ("kids", "tid")
-
-    def __init__(self):
-        self.kids = {}
-        self.tid = INVALID_TOKEN
-
-
 def compile_vocab_to_trie(vocab) -> bytes:
-    root = _Node()
-    max_len = 0
-    for tid, seq in enumerate(vocab):
-        if not seq:
-            continue
-        node = root
-        for byte in seq:
-            nxt = node.kids.get(byte)
-            if nxt is None:
-                nxt = node.kids[byte] = _Node()
-            node = nxt
-        node.tid = tid
-        max_len = max(max_len, len(seq))
-    nodes = []          # (firstChild, numChildren, tokenId) in BFS order
-    edges = []          # (symbol, target)
-    order = deque([root])
-    next_index = 1
-    while order:
-        node = order.popleft()
-        first = len(edges)
-        for sym in sorted(node.kids):
-            edges.append((sym, next_index))
-            next_index += 1
-            order.append(node.kids[sym])
-        nodes.append((first, len(node.kids), node.tid))
-    head = struct.pack("<7I", TRIE_MAGIC, TRIE_VERSION, len(nodes), len(edges), max_len, len(vocab), 0)
-    nb = np.asarray(nodes, dtype="<u4").reshape(-1, 3).tobytes()
-    eb = np.zeros((len(edges), 2), dtype="<u4")
-    if edges:
-        eb[:] = np.asarray(edges, dtype="<u4")
-    return head + nb + eb.tobytes()
+    """compileVocabToTrie (trie.js:39-98) through the library's native compiler
+    (gbpe_trie_compile): vocab[i] = byte list of token id i."""
+    import ctypes as C
+
+    from . import _lib
+    lib = _lib.load()
+    lens = np.fromiter((len(v) if v else 0 for v in vocab), dtype=np.uint64, count=len(vocab))
+    offs = np.zeros(len(vocab) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    flat = np.fromiter((b for v in vocab if v for b in v), dtype=np.uint8, count=int(offs[-1]))
+    need = C.c_uint64()
+    _lib.check(lib.gbpe_trie_compile(flat.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(_lib.u64p), len(vocab),
+                                     None, 0, C.byref(need)), None, "trie compile")
+    out = (C.c_uint8 * need.value)()
+    _lib.check(lib.gbpe_trie_compile(flat.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(_lib.u64p), len(vocab),
+                                     out, need.value, C.byref(need)), None, "trie compile")
+    return bytes(out)
 
 
 def parse_header(data: bytes) -> dict:

@@ -4,3 +4,4 @@ export { TrieTokenizer } from './tokenizer.js';
 export { Vocab, displayString } from './vocab.js';
 export { compileVocabToTrie, parseHeader, parseTrieBuffers } from './trie.js';
 export { GpuPreTokenizer } from './pretokenizer.js';
+export { modelToJSON, loadModelJSON, dxftBin, exportDXFT } from './export.js';

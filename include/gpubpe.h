@@ -209,6 +209,15 @@ int  gbpe_shard_step_comm(gbpe_trainer* t, gbpe_comm* comm, uint32_t max_merges,
 /* Upload a parsed trie (trie.js:137-160 parseTrieBuffers output): nodes =
  * u32 x 3 per node {firstChild, numChildren, tokenId}, edges = u32 x 2 per
  * edge {symbol, targetNode}.  Replaces tokenizer.js:59-71. */
+/* native compileVocabToTrie (trie.js:39-98 + serializeTrie :167-206): token id i
+ * has bytes[offsets[i] .. offsets[i+1]) (empty = skipped); writes the v3 blob.
+ * out == NULL: *out_len = the size needed.  Host only (no context). */
+int  gbpe_trie_compile(const uint8_t* bytes, const uint64_t* offsets, uint32_t n_tokens, uint8_t* out, uint64_t cap,
+                       uint64_t* out_len);
+/* DXFT .bin (export-controller.js:221-248): u32 [0x44584654, vocabSize,
+ * tokenCount, vocabJsonLen] + tokens + vocab JSON bytes.  out == NULL: size only. */
+int  gbpe_dxft_pack(const uint32_t* tokens, uint64_t n_tokens, uint32_t vocab_size, const uint8_t* vocab_json,
+                    uint64_t json_len, uint8_t* out, uint64_t cap, uint64_t* out_len);
 int  gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n_nodes,
                       const uint32_t* edges, uint32_t n_edges, gbpe_trie** out);
 void gbpe_trie_free(gbpe_trie* trie);

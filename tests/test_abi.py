@@ -12,6 +12,8 @@ import re
 
 import pytest
 
+import sys
+
 from conftest import GOLDEN, ROOT
 
 HEADER = os.path.join(ROOT, "include", "gpubpe.h")
@@ -96,3 +98,28 @@ def test_trie_parse_errors():
     import struct
     with pytest.raises(ValueError, match="version"):
         parse_header(struct.pack("<7I", 0x54524945, 9, 0, 0, 0, 0, 0))
+
+
+def test_dxft_pack_matches_oracle():
+    """gbpe_dxft_pack (native .bin writer) == the oracle's restatement of export-controller.js:221-248."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bpe_oracle as O
+    from gpubpe.export import dxft_bin
+    vocab_export = {"version": 1, "vocabSize": 259, "vocab": [[i] for i in range(256)] + [[116, 104], [104], []],
+                    "merges": [[116, 104, 256]]}
+    for toks in ([], [1, 2, 3, 256, 65535], list(range(1000))):
+        assert dxft_bin(toks, 259, vocab_export) == O.dxft_bin(toks, 259, vocab_export)
+    assert dxft_bin([5], 256, None) == O.dxft_bin([5], 256, None)
+
+
+def test_model_json_round_trip():
+    from gpubpe.export import load_model_json, model_json
+    model = {"vocabSize": 258, "vocab": [[i] for i in range(256)] + [[104, 105], [0xE2, 0x82]],
+             "merges": [[104, 105, 256, 7], [0xE2, 0x82, 257, 3]]}
+    s = model_json(model)
+    assert s.startswith('{"version":1,"vocabSize":258,"vocab":[[0],[1],')     # JSON.stringify layout
+    m = load_model_json(s)
+    assert m["vocabSize"] == 258 and m["merges"] == [[104, 105, 256], [0xE2, 0x82, 257]]
+    assert m["vocabStrings"][256] == "hi" and m["vocabStrings"][257] == "�"   # non-fatal UTF-8 decode
+    with pytest.raises(ValueError, match="missing vocab or merges"):
+        load_model_json({"vocab": [[1]]})
