@@ -80,6 +80,9 @@ _SIGS = [
     ("gbpe_encode", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, u32p, C.c_uint64, u64p]),
     ("gbpe_encode_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
                                      C.c_uint64, u64p]),
+    ("gbpe_bpe_upload", C.c_int, [C.c_void_p, u32p, C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("gbpe_bpe_encode", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, u32p, C.c_uint64, u64p]),
+    ("gbpe_bpe_free", None, [C.c_void_p]),
     ("gbpe_encode_last_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                           C.POINTER(C.c_double)]),
     ("gbpe_device_alloc", C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),

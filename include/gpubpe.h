@@ -233,6 +233,15 @@ int gbpe_encode(gbpe_ctx* ctx, gbpe_trie* trie, const uint8_t* bytes, uint64_t n
 int gbpe_encode_device(gbpe_ctx* ctx, gbpe_trie* trie, const void* d_bytes, uint64_t n, uint32_t chunk_size,
                        void* d_out, uint64_t out_cap, uint64_t* n_out);
 /* device ms of the last encode's kernels (walk, scan, compact) */
+/* ── merge-rank encode: TokenizerManager.encode (tokenizer-manager.js:13-61) ──
+ * merges = [a, b, newId] x n in learned order.  Exact for any merge list: a
+ * merge whose operand is only created later never fires (as in the reference). */
+typedef struct gbpe_bpe gbpe_bpe;
+int  gbpe_bpe_upload(gbpe_ctx* ctx, const uint32_t* merges, uint32_t n_merges, gbpe_bpe** out);
+int  gbpe_bpe_encode(gbpe_ctx* ctx, gbpe_bpe* bpe, const uint8_t* bytes, uint64_t n, uint32_t* out, uint64_t out_cap,
+                     uint64_t* n_out);
+void gbpe_bpe_free(gbpe_bpe* bpe);
+
 int gbpe_encode_last_timing(gbpe_ctx* ctx, double* ms_walk, double* ms_scan, double* ms_compact);
 
 /* ── device memory helpers for device-resident callers ─────────────────── */
