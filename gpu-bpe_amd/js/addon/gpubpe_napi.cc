@@ -413,6 +413,59 @@ napi_value TrieFree(napi_env env, napi_callback_info info) {
     return nullptr;
 }
 
+// ── merge-rank encoder (TokenizerManager.encode, tokenizer-manager.js:13-61) ──
+
+struct Bpe {
+    gbpe_bpe* bpe = nullptr;
+};
+
+void bpe_finalize(napi_env, void* data, void*) {
+    Bpe* b = static_cast<Bpe*>(data);
+    if (b->bpe) gbpe_bpe_free(b->bpe);
+    delete b;
+}
+
+napi_value BpeUpload(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    Ctx* c = argc >= 1 ? unwrap_external<Ctx>(env, argv[0]) : nullptr;
+    const uint32_t* m = nullptr;
+    size_t nm = 0;
+    if (!c || !c->ctx || argc < 2 || !get_u32s(env, argv[1], &m, &nm)) {
+        napi_throw_type_error(env, nullptr, "bpeUpload(ctx, merges: Uint32Array [a,b,id]*)");
+        return nullptr;
+    }
+    auto* b = new Bpe();
+    int rc = gbpe_bpe_upload(c->ctx, m, (uint32_t)(nm / 3), &b->bpe);
+    if (rc != GBPE_OK) {
+        delete b;
+        return throw_status(env, c->ctx, "bpe upload", rc);
+    }
+    napi_value ext;
+    NAPI_CALL(env, napi_create_external(env, b, bpe_finalize, nullptr, &ext));
+    return ext;
+}
+
+napi_value BpeEncode(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    Ctx* c = argc >= 1 ? unwrap_external<Ctx>(env, argv[0]) : nullptr;
+    Bpe* b = argc >= 2 ? unwrap_external<Bpe>(env, argv[1]) : nullptr;
+    const uint8_t* data = nullptr;
+    size_t len = 0;
+    if (!c || !c->ctx || !b || !b->bpe || argc < 3 || !get_bytes(env, argv[2], &data, &len)) {
+        napi_throw_type_error(env, nullptr, "bpeEncode(ctx, bpe, Uint8Array)");
+        return nullptr;
+    }
+    std::vector<uint32_t> out(len ? len : 1);
+    uint64_t n = 0;
+    int rc = gbpe_bpe_encode(c->ctx, b->bpe, data, len, out.data(), out.size(), &n);
+    if (rc != GBPE_OK) return throw_status(env, c->ctx, "bpe encode", rc);
+    return make_u32_array(env, out.data(), (size_t)n);
+}
+
 struct EncodeWork {
     napi_async_work work = nullptr;
     napi_deferred deferred = nullptr;
@@ -493,6 +546,8 @@ napi_value Init(napi_env env, napi_value exports) {
         {"trainerStep", nullptr, TrainerStep, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"trainerDestroy", nullptr, TrainerDestroy, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"trieUpload", nullptr, TrieUpload, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"bpeUpload", nullptr, BpeUpload, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"bpeEncode", nullptr, BpeEncode, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"trieFree", nullptr, TrieFree, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"encode", nullptr, Encode, nullptr, nullptr, nullptr, napi_default, nullptr},
     };

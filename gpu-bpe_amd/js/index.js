@@ -5,3 +5,4 @@ export { Vocab, displayString } from './vocab.js';
 export { compileVocabToTrie, parseHeader, parseTrieBuffers } from './trie.js';
 export { GpuPreTokenizer } from './pretokenizer.js';
 export { modelToJSON, loadModelJSON, dxftBin, exportDXFT } from './export.js';
+export { MergeEncoder } from './merge-encoder.js';

@@ -1,7 +1,7 @@
 // GPU checks through the N-API addon: BPETrainer / TrieTokenizer results
 // must equal the expectations the CPU oracle produced (argv[2] JSON).
 import fs from 'fs';
-import { BPEEngine, BPETrainer, TrieTokenizer, GpuPreTokenizer } from '../../gpu-bpe_amd/js/index.js';
+import { BPEEngine, BPETrainer, TrieTokenizer, GpuPreTokenizer, MergeEncoder } from '../../gpu-bpe_amd/js/index.js';
 
 const cases = JSON.parse(fs.readFileSync(process.argv[2]));
 function fail(msg) { console.error('FAIL ' + msg); process.exit(1); }
@@ -38,6 +38,13 @@ async function main() {
         const t = await new BPETrainer(engine).train(bytes, { targetVocabSize: p.target, preTokenizer: pt });
         if (JSON.stringify(t.merges) !== JSON.stringify(p.merges)) fail('pretok merges');
         checks += 2;
+    }
+    if (cases.merge_encode) {   // TokenizerManager.encode semantics on the GPU
+        const c = cases.merge_encode;
+        const enc = new MergeEncoder(engine, { vocab: [], vocabStrings: [], merges: c.merges });
+        const r = await enc.encode(c.text);
+        if (JSON.stringify(r.tokens) !== JSON.stringify(c.tokens)) fail('merge encode');
+        checks++;
     }
     let threw = false;
     try { await new BPETrainer(engine).train(new Uint8Array(0)); } catch (e) { threw = /empty/.test(e.message); }

@@ -53,6 +53,10 @@ def test_js_addon_train_and_encode(tmp_path):
     ws = O.gpt4_word_starts(code)
     pre = {"b64": base64.b64encode(code).decode(), "word_starts": ws.tolist(), "target": 500,
            "merges": [m[:3] for m in O.train(code, 500, word_starts=ws)["merges"]]}
+    me_text = synth.english(8000, seed=46)
+    me_merges = cases[0]["merges"]
+    me = {"merges": me_merges, "text": me_text.decode("utf-8", "replace"),
+          "tokens": O.encode_merge_order(me_text.decode("utf-8", "replace").encode(), me_merges)}
     p = tmp_path / "cases.json"
-    p.write_text(json.dumps({"train": cases, "pretok": pre}))
+    p.write_text(json.dumps({"train": cases, "pretok": pre, "merge_encode": me}))
     assert _run("test_gpu.mjs", str(p)).strip().splitlines()[-1].startswith("ok")
