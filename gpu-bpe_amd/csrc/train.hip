@@ -34,6 +34,7 @@
 // Per merge: k_select (1 WG) → k_delta → k_compact (tiles + tail) → k_refresh.
 
 #include "common.h"
+#include "scan.h"
 
 #include <chrono>
 #include <cstdarg>
@@ -91,6 +92,11 @@ struct DevState {
     uint64_t gnew;         // gn - mc
     uint32_t peak_l, peak_w;   // largest record list / window piece of this step (capacity sizing)
     uint32_t dfull;            // the delta table overflowed this merge
+    // ── sector-sparse loop (n / new_n above stay GLOBAL; the zone has its own DevState) ──
+    uint32_t B;            // body length: symbols in the word-aligned sectors before the zone
+    uint32_t Bp;           // body length during the previous merge (stale-window source offset)
+    uint32_t body_rm;      // B-sides removed from the body by this merge
+    uint32_t sp_abort;     // a selected merge does not fit the zone: not run, host goes dense
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
@@ -103,7 +109,8 @@ enum : uint32_t {
     ERR_TABLE_FULL = 1, ERR_COUNT_MISMATCH = 2, ERR_PAIR_MISSING = 4, ERR_SPIN = 8,
     ERR_SHARD_CAPACITY = 16,   // a rank's stream outgrew its buffers (stale window appended)
     ERR_SHARD_RECORD = 32,     // exchange records disagree (ranks out of step)
-    ERR_SHARD_LAYOUT = 64      // gathered survivor / length totals do not add up
+    ERR_SHARD_LAYOUT = 64,     // gathered survivor / length totals do not add up
+    ERR_SPARSE_WINDOW = 128    // sector-sparse: a stale window reaches past the zone's stale buffer
 };
 
 struct Table {
@@ -273,14 +280,20 @@ __global__ __launch_bounds__(TPB) void k_count_full(DevState* st, const S* __res
 // merge of `round` (state.symbol_count := new count, train.wgsl:605-607)
 template <typename S>
 __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, int finish, Table tb, S* __restrict__ cur,
-                                                 const uint32_t* __restrict__ rwlist) {
+                                                 const uint32_t* __restrict__ rwlist, DevState* zst) {
     __shared__ uint64_t red[TPB / 64];
     __shared__ uint32_t rlive[TPB / 64];
     (void)cur;
     (void)rwlist;
     if (finish && !st->stop && !st->stall && st->merges_done == round + 1u) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
-            if (st->sharded) {   // commit the new global layout computed by k_shard_recv
+            if (zst) {   // sector-sparse: global length, body length, zone length
+                st->tail_total += zst->m;
+                st->n = st->new_n;
+                st->Bp = st->B;
+                st->B -= st->body_rm;
+                zst->n = st->n - st->B;
+            } else if (st->sharded) {   // commit the new global layout computed by k_shard_recv
                 st->tail_total += st->m_glob;
                 st->poff = st->off;
                 st->pln = st->n;
@@ -357,13 +370,13 @@ constexpr uint32_t GSTR = 64;   // group sums 256 B apart: each is its own atomi
 // argmax over block maxima + the reference's bpe_setup_merge (train.wgsl:340-364)
 __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, uint32_t* __restrict__ log,
                                                         uint32_t* __restrict__ grpsum, uint32_t* __restrict__ nlog,
-                                                        uint32_t* __restrict__ rec) {
+                                                        uint32_t* __restrict__ rec, DevState* zst, uint32_t exact) {
     __shared__ uint64_t red[SEL_THREADS / 64];
     __shared__ uint32_t rlive[SEL_THREADS / 64];
     if (rec && threadIdx.x == 0) rec[H_L] = 0u;   // the send kernel's list blocks add their counts into it
-    if (st->stop || st->stall) return;
-    {   // group sums of the coming stream pass start at zero
-        const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(st->n, TILE), GRP);
+    if (st->stop || st->stall || st->sp_abort) return;
+    {   // group sums of the coming stream pass (the zone's, when sector-sparse) start at zero
+        const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(zst ? zst->n : st->n, TILE), GRP);
         for (uint32_t g = threadIdx.x; g < ngrp; g += SEL_THREADS) grpsum[g * GSTR] = 0u;
     }
     uint64_t best = 0;
@@ -407,6 +420,22 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
         st->stop = 1u;
         return;
     }
+    if (zst && !exact) {
+        // sector-sparse zone invariants: this merge's stale window
+        // [new_n - m, new_n) of the previous stream lies in the zone's stale buffer
+        // (n - 2mc >= Bp), and the zone stays >= 5 mc long so the next merge's window
+        // does too (its count is <= mc + m <= 2 mc).  Otherwise the merge is not run
+        // and the host returns to the dense loop.
+        if ((uint64_t)st->n < 2ull * mc + st->Bp) {   // cannot happen after the check below held
+            atomicOr(&st->err, ERR_SPARSE_WINDOW);
+            st->stop = 1u;
+            return;
+        }
+        if ((uint64_t)zst->n < 5ull * mc + 2u) {
+            st->sp_abort = 1u;
+            return;
+        }
+    }
     const uint32_t idx = table_find(tb, pid);
     if (idx == 0xFFFFFFFFu) {
         atomicOr(&st->err, ERR_PAIR_MISSING);
@@ -434,6 +463,16 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
         st->new_n = st->n - mc;
     }
     if (nlog) nlog[d] = st->n;
+    if (zst) {   // the zone's view of the merge: k_delta / k_compact run on it unchanged
+        zst->a = st->a;
+        zst->b = st->b;
+        zst->nw = st->nw;
+        zst->mc = mc;
+        zst->new_n = exact ? zst->n : zst->n - mc;   // zone keep limit: global new_n - B
+        zst->m = 0u;
+        zst->merges_done = d + 1u;
+        st->body_rm = 0u;
+    }
     st->next_id += 1u;
     st->epoch += 1u;
     st->merges_done = d + 1u;
@@ -609,11 +648,16 @@ __device__ __forceinline__ void load_own_n(const S* __restrict__ cur, uint64_t i
     for (int k = 0; k < E; ++k) x[k] = e[k];
 }
 
-template <typename S, bool EXACT>
+// ZONE (sector-sparse loop): st is the zone's view; the stale window is not in
+// place in `oth` (the zone's coordinates shift with the body) but copied to `win`
+// by k_body before this pass: window symbol j = win[mc - m + j], stored at zone
+// position (zone survivors - m) + j.  gst is the global state (count check).
+template <typename S, bool EXACT, bool ZONE = false>
 __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, S* __restrict__ cur, S* __restrict__ oth,
                                                  const uint32_t* __restrict__ hitmask,
                                                  const uint32_t* __restrict__ tile_cnt,
-                                                 const uint32_t* __restrict__ grpsum, Table tb) {
+                                                 const uint32_t* __restrict__ grpsum, Table tb,
+                                                 const S* __restrict__ win = nullptr, const DevState* gst = nullptr) {
     // one LDS arena: the compaction stage of tile blocks or the delta table of tail blocks
     constexpr int STAGE = (TILE + 16) * sizeof(S);
     constexpr int ARENA = (sizeof(LdsTab<LTAB>) > STAGE ? sizeof(LdsTab<LTAB>) : STAGE) / 16;
@@ -636,8 +680,23 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
         LdsTab<LTAB>& lt = *reinterpret_cast<LdsTab<LTAB>*>(arena);
         __shared__ uint32_t left_val;
         lds_clear(lt);
-        const uint32_t lo = new_n - m;
+        uint32_t lo = new_n - m;
         const uint32_t tb0 = tl - ntiles, ntb = gridDim.x - ntiles;
+        uint32_t woff = 0;
+        if (ZONE) {   // window start = zone survivors - m (the group sums hold the survivors)
+            __shared__ uint32_t s_surv[CTPB / 64];
+            const uint32_t ngrp = (uint32_t)gbpe_div_up(ntiles, GRP);
+            uint32_t sv = 0;
+            for (uint32_t g = t; g < ngrp; g += CTPB) sv += grpsum[g * GSTR];
+            for (int off = 32; off > 0; off >>= 1) sv += __shfl_xor(sv, off);
+            if (lane == 0) s_surv[wid] = sv;
+            __syncthreads();
+            sv = 0;
+            for (int w2 = 0; w2 < CTPB / 64; ++w2) sv += s_surv[w2];
+            lo = sv - m;
+            woff = st->mc - m;
+        }
+        const uint32_t hi = lo + m;
         if (tb0 == 0 && wid == 0 && lo >= 1) {
             // the survivor just before the window: last j < new_n with hit(j) == 0; its
             // value is the A-side-rewritten symbol (the rewrite is idempotent, so racing
@@ -671,10 +730,17 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
             }
         }
         __syncthreads();
-        for (uint32_t d = lo + tb0 * CTPB + t; d < new_n; d += ntb * CTPB) {
+        for (uint32_t d = lo + tb0 * CTPB + t; d < hi; d += ntb * CTPB) {
             if (d == 0) continue;
-            const uint32_t x0 = (d == lo) ? left_val : (uint32_t)oth[d - 1];
-            const uint32_t x1 = oth[d];
+            uint32_t x0, x1;
+            if (ZONE) {
+                x1 = win[woff + (d - lo)];
+                x0 = (d == lo) ? left_val : (uint32_t)win[woff + (d - lo) - 1];
+                oth[d] = (S)x1;
+            } else {
+                x0 = (d == lo) ? left_val : (uint32_t)oth[d - 1];
+                x1 = oth[d];
+            }
             const uint32_t t0 = x0 & TM, t1 = x1 & TM;
             if (!(x1 & WS) && t0 && t1) lds_add(lt, tb, st, (t0 << 16) | t1, 1u);
         }
@@ -732,8 +798,9 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
         total += wsum[w2];
         prefix += psum[w2];
     }
-    if (tl == ntiles - 1 && t == 0 && !st->sharded && prefix + tile_cnt[tl] != new_n)
-        atomicOr(&st->err, ERR_COUNT_MISMATCH);
+    if (tl == ntiles - 1 && t == 0 && !st->sharded &&
+        prefix + tile_cnt[tl] != (ZONE ? gst->new_n - (gst->B - gst->body_rm) : new_n))
+        atomicOr(ZONE ? (uint32_t*)&gst->err : &st->err, ERR_COUNT_MISMATCH);
     // stage at the destination's alignment phase so both sides move whole 16-byte words
     constexpr uint32_t VE = 16 / sizeof(S);           // symbols per 16-byte word
     const uint32_t ph = prefix & (VE - 1);
@@ -787,6 +854,264 @@ __global__ void k_export_symbols(const S* __restrict__ s, uint32_t* __restrict__
     out[i] = (x & Sym<S>::TM) | ((x & Sym<S>::WS) ? 0x10000u : 0u);
 }
 
+// ─── sector-sparse merge loop ──────────────────────────────────
+//
+// Late in training a merge's count is a tiny fraction of the stream, yet the
+// dense pass above reads the whole stream twice per merge.  The sparse loop
+// re-lays the stream out as
+//   * a BODY of word-aligned sectors: sector k starts at the first word start at
+//     or after k*SEC and keeps its symbols compacted at its own start.  Pairs
+//     never cross a word start (train.wgsl:395, 483, 493), so sectors merge
+//     independently and their first symbol is never a B-side;
+//   * a token-presence bitmap (row = token id, bit = sector): a merge (a, b) can
+//     only have sites in sectors whose a-row and b-row bits are both set.  Bits
+//     are set when a token appears in a sector and never cleared (a superset);
+//   * a dense ZONE: the last >= 5*mc symbols, run by the dense kernels on their
+//     own ping-pong buffers.  It carries the reference's compaction quirk (the
+//     stale window always lands at the end of the stream).  Its coordinates are
+//     global position - B (body length), which shifts as the body loses
+//     symbols, so the stale window is copied out (k_body's copy blocks) instead
+//     of being left in place.
+// Per merge: k_select → k_body (candidate sectors + window copy) → k_delta (zone)
+// → k_compact<ZONE> → k_refresh.
+constexpr uint32_t SP_WPW = 2;       // bitmap words (32 sectors each) per k_body workgroup
+constexpr uint32_t SP_CH = 256;      // symbols per wave pass over a sector (4 per lane)
+constexpr uint32_t SP_INV = 0xFFFFFFFFu;
+
+// One wave merges one sector in place (snapshot semantics, k_delta's delta rule,
+// survivors compacted to the sector's front).  Returns the B-sides removed.
+template <typename S>
+__device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uint32_t b, uint32_t nw,
+                                LdsTab<LTAB_T>& lt, const Table& tb, DevState* st, uint32_t& out_cnt) {
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    const int lane = threadIdx.x & 63;
+    const uint32_t pid_ab = (a << 16) | b;
+    uint32_t c1 = 0, c2 = 0, out = 0, removed = 0;
+    for (uint32_t c0 = 0; c0 < cnt; c0 += SP_CH) {
+        const uint32_t i0 = c0 + 4u * lane;
+        // X[0..1] = the two symbols before this lane's four, X[6] = the one after
+        uint32_t X[7];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) X[2 + k] = (i0 + k < cnt) ? (uint32_t)p[i0 + k] : 0u;
+        const uint32_t nx = (c0 + SP_CH < cnt) ? (uint32_t)p[c0 + SP_CH] : 0u;
+        uint32_t pm1 = __shfl_up(X[5], 1), pm2 = __shfl_up(X[4], 1);
+        uint32_t np = __shfl_down(X[2], 1);
+        if (lane == 0) {
+            pm1 = c1;
+            pm2 = c2;
+        }
+        if (lane == 63) np = nx;
+        X[0] = pm2;
+        X[1] = pm1;
+        X[6] = np;
+        c1 = __shfl(X[5], 63);
+        c2 = __shfl(X[4], 63);
+        // h[j] = hit at the position of X[j]: a B-side (no word-start bit) after an a
+        bool h[7];
+        h[0] = false;
+#pragma unroll
+        for (int j = 1; j < 7; ++j) h[j] = X[j] == b && (X[j - 1] & TM) == a;
+        uint32_t keep = 0, vals[4];
+        bool touched = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = k + 2;
+            const bool valid = i0 + k < cnt;
+            if (valid && !h[j]) keep |= 1u << k;
+            vals[k] = h[j + 1] ? (nw | (X[j] & WS)) : X[j];
+            touched |= valid && (h[j] || h[j + 1]);
+            if (valid && !(X[j] & WS) && (h[j - 1] || h[j] || h[j + 1])) {
+                const uint32_t tp = X[j - 1] & TM, ti = X[j] & TM;
+                if (tp && ti) {
+                    const uint32_t pid = (tp << 16) | ti;
+                    if (pid != pid_ab) lds_add(lt, tb, st, pid, 0xFFFFFFFFu);   // old pair destroyed
+                }
+                if (!h[j]) {
+                    if (h[j - 1]) {
+                        const uint32_t t2 = h[j + 1] ? nw : ti;
+                        if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+                    } else if (h[j + 1] && tp) {
+                        lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+                    }
+                }
+            }
+        }
+        const uint32_t kc = __popc(keep);
+        uint32_t incl = kc;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off);
+            if (lane >= off) incl += o;
+        }
+        const uint32_t tot = __shfl(incl, 63);
+        // every read of this pass happened above; writes land at or before their source
+        if (out != c0 || __any(touched)) {
+            uint32_t w = out + incl - kc;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((keep >> k) & 1u) p[w++] = (S)vals[k];
+        }
+        const uint32_t nvalid = cnt - c0 < SP_CH ? cnt - c0 : SP_CH;
+        removed += nvalid - tot;
+        out += tot;
+    }
+    out_cnt = out;
+    return removed;
+}
+
+// Body pass: blocks [0, nbody) each test SP_WPW bitmap words of (a-row & b-row)
+// and merge the candidate sectors (one wave per sector); blocks >= nbody copy the
+// stale-window source [n - 2mc - Bp, + mc) of the zone's other buffer to `wtmp`.
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
+                                              uint32_t* __restrict__ bits, uint32_t W, Table tb, uint32_t nbody,
+                                              const S* __restrict__ zoth, S* __restrict__ wtmp) {
+    __shared__ LdsTab<LTAB_T> lt;
+    __shared__ uint32_t s_list[SP_WPW * 32];
+    __shared__ uint32_t s_n, s_rm[TPB / 64];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    if (!merge_active(st, round)) return;
+    const uint32_t a = st->a, b = st->b, nw = st->nw;
+    if (blockIdx.x >= nbody) {
+        const uint32_t mc = st->mc;
+        const uint64_t src0 = (uint64_t)st->n - 2ull * mc - st->Bp;
+        const uint64_t stride = (uint64_t)(gridDim.x - nbody) * TPB;
+        for (uint64_t u = (uint64_t)(blockIdx.x - nbody) * TPB + t; u < mc; u += stride) wtmp[u] = zoth[src0 + u];
+        return;
+    }
+    if (wid == 0) {
+        const uint32_t w = blockIdx.x * SP_WPW + lane;
+        uint32_t c = 0;
+        if (lane < (int)SP_WPW && w < W) c = bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w];
+        const uint32_t pc = __popc(c);
+        uint32_t incl = pc;
+        for (int off = 1; off < (int)SP_WPW; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off);
+            if (lane >= off) incl += o;
+        }
+        uint32_t pos = incl - pc;
+        while (c) {
+            const int bit = __ffs(c) - 1;
+            c &= c - 1;
+            s_list[pos++] = w * 32u + (uint32_t)bit;
+        }
+        if (lane == (int)SP_WPW - 1) s_n = incl;
+    }
+    __syncthreads();
+    const uint32_t ncand = s_n;
+    if (ncand == 0) return;
+    lds_clear(lt);
+    __syncthreads();
+    uint32_t removed = 0;
+    for (uint32_t j = wid; j < ncand; j += TPB / 64) {
+        const uint32_t s = s_list[j];
+        const uint2 e = sec[s];
+        uint32_t out = 0;
+        const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, tb, st, out);
+        if (r) {
+            removed += r;
+            if (lane == 0) {
+                sec[s].y = out;
+                atomicOr(&bits[(uint64_t)nw * W + (s >> 5)], 1u << (s & 31u));
+            }
+        }
+    }
+    lds_flush(lt, tb, st);
+    if (lane == 0) s_rm[wid] = removed;
+    __syncthreads();
+    if (t == 0) {
+        const uint32_t r = s_rm[0] + s_rm[1] + s_rm[2] + s_rm[3];
+        if (r) atomicAdd(&st->body_rm, r);
+    }
+}
+
+// dense → sparse: the last word start at or before `lim` (one workgroup, backwards)
+template <typename S>
+__global__ __launch_bounds__(1024) void k_sp_zone_start(const S* __restrict__ cur, uint32_t lim, uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_found;
+    if (threadIdx.x == 0) s_found = 0u;
+    __syncthreads();
+    for (int64_t hi = lim; hi >= 1; hi -= 1024) {
+        const int64_t i = hi - (int64_t)threadIdx.x;
+        if (i >= 1 && (cur[i] & Sym<S>::WS)) atomicMax(&s_found, (uint32_t)i);
+        __syncthreads();
+        const uint32_t f = s_found;
+        __syncthreads();
+        if (f) break;
+    }
+    if (threadIdx.x == 0) *out = s_found;   // 0 = none
+}
+
+// sector k's start: first word start in [k*SEC, (k+1)*SEC) (one wave per window)
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_sectors(const S* __restrict__ body, uint32_t Zs, uint32_t SEC,
+                                                    uint32_t* __restrict__ starts, uint32_t nsec) {
+    const uint32_t k = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (k >= nsec) return;
+    const uint64_t lo = (uint64_t)k * SEC, hi = lo + SEC < Zs ? lo + SEC : Zs;
+    uint32_t found = SP_INV;
+    if (k == 0) found = 0;   // the stream's first symbol starts sector 0
+    for (uint64_t base = lo; base < hi && found == SP_INV; base += 64) {
+        const uint64_t i = base + lane;
+        const bool ws = i < hi && (body[i] & Sym<S>::WS);
+        const unsigned long long m = __ballot(ws);
+        if (m) found = (uint32_t)(base + (uint64_t)(__ffsll((long long)m) - 1));
+    }
+    if (lane == 0) starts[k] = found;
+}
+
+__global__ void k_sp_sector_len(const uint32_t* __restrict__ starts, uint32_t nsec, uint32_t Zs, uint2* __restrict__ sec) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nsec) return;
+    const uint32_t st = starts[k];
+    if (st == SP_INV) {
+        sec[k] = make_uint2(0u, 0u);
+        return;
+    }
+    uint32_t end = Zs;
+    for (uint32_t j = k + 1; j < nsec; ++j)   // windows inside one long word have no start
+        if (starts[j] != SP_INV) {
+            end = starts[j];
+            break;
+        }
+    sec[k] = make_uint2(st, end - st);
+}
+
+// presence bits of every token of every sector (one wave per sector)
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_bits(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t nsec,
+                                                 uint32_t* __restrict__ bits, uint32_t W) {
+    const uint32_t k = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (k >= nsec) return;
+    const uint2 e = sec[k];
+    const uint32_t bit = 1u << (k & 31u);
+    uint32_t* col = bits + (k >> 5);
+    for (uint32_t j = lane; j < e.y; j += 64) {
+        const uint32_t tok = body[e.x + j] & Sym<S>::TM;
+        uint32_t* wp = col + (uint64_t)tok * W;
+        if (!(*wp & bit)) atomicOr(wp, bit);
+    }
+}
+
+// sparse → dense: sector counts, then a gather at the scanned offsets (one wave per sector)
+__global__ void k_sp_counts(const uint2* __restrict__ sec, uint32_t nsec, uint32_t* __restrict__ cnt) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nsec) cnt[k] = sec[k].y;
+}
+
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_gather(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t nsec,
+                                                   const uint32_t* __restrict__ loc, const uint64_t* __restrict__ blk,
+                                                   S* __restrict__ dst) {
+    const uint32_t k = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (k >= nsec) return;
+    const uint2 e = sec[k];
+    const uint64_t off = (uint64_t)loc[k] + blk[k / SCAN_BLK];
+    for (uint32_t j = lane; j < e.y; j += 64) dst[off + j] = body[e.x + j];
+}
+
 }  // namespace
 
 // ─── host side ──────────────────────────────────────────────────────────────
@@ -827,6 +1152,32 @@ struct gbpe_trainer {
     double ms_merge = 0, ms_select = 0, ms_other = 0, ms_delta = 0, ms_compact = 0;
     uint64_t timed_merges = 0;
     std::vector<hipEvent_t> evs;
+    // sector-sparse loop
+    bool sp = false;             // the stream is in the sector layout
+    uint32_t sp_secw = 256;      // sector window (symbols)
+    uint32_t max_id = 0;         // exclusive bound of every token id of the run (bitmap rows)
+    uint32_t last_mc = 0;        // count of the last merge run
+    int bcur = 0;                // dense buffer holding the body sectors
+    uint32_t nsec = 0;
+    uint64_t nsec_cap = 0;
+    uint2* sec = nullptr;        // {start, count} per sector
+    uint32_t* sp_loc = nullptr;  // per-sector scratch (starts / scan)
+    uint64_t* sp_blk = nullptr;  // scan block totals
+    uint32_t* bits = nullptr;    // presence bitmap, rows = token ids, W words per row
+    uint64_t bits_cap = 0;       // words
+    uint32_t W = 0;
+    void* zbuf[2] = {nullptr, nullptr};
+    void* wtmp = nullptr;        // stale-window source copy
+    uint64_t zcap = 0;           // zone buffer capacity (symbols)
+    int zcur = 0;                // zone buffer holding the zone
+    DevState* zst = nullptr;     // the zone's loop state
+    DevState* h_zst = nullptr;   // pinned
+    uint32_t* d_u32 = nullptr;   // small device scratch
+    uint64_t sp_merges = 0, sp_sectors = 0, sp_zone = 0;
+    uint32_t sp_enters = 0, sp_exits = 0;
+    uint32_t sp_div = 64;        // enter when last_mc * sp_div <= n
+    uint32_t sp_cooldown = 0;    // steps to stay dense after an abort
+    uint32_t sp_zt = 10;         // zone target = sp_zt * last_mc + 64 (>= 5: see sp_enter)
 };
 
 namespace {
@@ -861,10 +1212,10 @@ int table_rebuild(gbpe_trainer* t) {
     GBPE_LAUNCH_CHECK(t->ctx);
     if (t->u16)
         hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, 0u,
-                           0, t->tb, (uint16_t*)nullptr, (const uint32_t*)nullptr);
+                           0, t->tb, (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
     else
         hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, 0u,
-                           0, t->tb, (uint32_t*)nullptr, (const uint32_t*)nullptr);
+                           0, t->tb, (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
 }
@@ -877,7 +1228,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
     hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
-                       (uint32_t*)nullptr, (uint32_t*)nullptr);
+                       (uint32_t*)nullptr, (uint32_t*)nullptr, (DevState*)nullptr, 0u);
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
     if (exact) {
         hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
@@ -894,11 +1245,205 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(k_refresh<S>, dim3(g_refresh), dim3(TPB), 0, s, t->st, round, 1, t->tb, cur,
-                       (const uint32_t*)nullptr);
+                       (const uint32_t*)nullptr, (DevState*)nullptr);
     if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
 }
+
+// ── sector-sparse loop: launches and re-layouts ──
+
+struct SpGrid {
+    uint32_t body, copy, zdelta, zcompact, refresh;
+};
+
+template <typename S>
+int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const SpGrid& g, bool timing, hipEvent_t* ev) {
+    S* zc = (S*)t->zbuf[t->zcur ^ (round & 1)];
+    S* zo = (S*)t->zbuf[t->zcur ^ (round & 1) ^ 1];
+    const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
+    if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
+                       (uint32_t*)nullptr, (uint32_t*)nullptr, t->zst, exact ? 1u : 0u);
+    if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
+    hipLaunchKernelGGL(k_body<S>, dim3(g.body + g.copy), dim3(TPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
+                       t->bits, t->W, t->tb, g.body, (const S*)zo, (S*)t->wtmp);
+    if (exact)
+        hipLaunchKernelGGL((k_delta<S, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc, t->tb,
+                           t->hitmask, t->tile_cnt, t->grpsum, g.zdelta);
+    else
+        hipLaunchKernelGGL((k_delta<S, false>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc, t->tb,
+                           t->hitmask, t->tile_cnt, t->grpsum, g.zdelta);
+    if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
+    if (exact)
+        hipLaunchKernelGGL((k_compact<S, true, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
+                           (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb,
+                           (const S*)t->wtmp, (const DevState*)t->st);
+    else
+        hipLaunchKernelGGL((k_compact<S, false, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
+                           (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb,
+                           (const S*)t->wtmp, (const DevState*)t->st);
+    if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
+    hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 1, t->tb, (S*)nullptr,
+                       (const uint32_t*)nullptr, t->zst);
+    if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
+    GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+
+template <typename T>
+int sp_grow(gbpe_trainer* t, T** p, uint64_t* cap, uint64_t need) {
+    if (*p && *cap >= need) return GBPE_OK;
+    hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc((void**)p, need * sizeof(T)) != hipSuccess) {
+        *p = nullptr;
+        return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sparse layout, %llu B) failed",
+                              (unsigned long long)(need * sizeof(T)));
+    }
+    *cap = need;
+    return GBPE_OK;
+}
+
+// dense → sparse at a step boundary.  The zone is the stream from the last word
+// start at or before n - zt (zt = 10 * last_mc + 64 >= 5 * the next merge's
+// count); the dense stale buffer's tail becomes the zone's stale buffer.
+template <typename S>
+int sp_enter(gbpe_trainer* t) {
+    hipStream_t s = t->ctx->stream;
+    const uint32_t n = t->n;
+    const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
+    if (zt + 2 >= n) return GBPE_OK;
+    const S* cur = (const S*)t->buf[t->cur];
+    const S* stale = (const S*)t->buf[t->cur ^ 1];
+    if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
+    hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, cur, (uint32_t)(n - zt), t->d_u32);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    uint32_t Zs = 0;
+    TR_HIP(t, hipMemcpyAsync(&Zs, t->d_u32, 4, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    if (Zs < t->sp_secw) return GBPE_OK;   // the whole stream is one long word (or tiny): stay dense
+    const uint32_t z = n - Zs;
+    // sectors
+    const uint32_t nsec = (uint32_t)gbpe_div_up(Zs, t->sp_secw);
+    uint64_t cap_blk = 0;
+    int rc = sp_grow(t, &t->sec, &t->nsec_cap, nsec);
+    uint64_t loc_cap = t->nsec_cap;
+    if (rc == GBPE_OK && (!t->sp_loc || loc_cap < nsec)) {
+        hipFree(t->sp_loc);
+        hipFree(t->sp_blk);
+        t->sp_loc = nullptr;
+        t->sp_blk = nullptr;
+        if (hipMalloc(&t->sp_loc, (uint64_t)t->nsec_cap * 4) != hipSuccess ||
+            hipMalloc(&t->sp_blk, (gbpe_div_up(t->nsec_cap, SCAN_BLK) + 1) * 8) != hipSuccess)
+            rc = gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sector scratch) failed");
+    }
+    (void)cap_blk;
+    if (rc != GBPE_OK) return rc;
+    t->nsec = nsec;
+    hipLaunchKernelGGL(k_sp_sectors<S>, dim3((uint32_t)gbpe_div_up(nsec, TPB / 64)), dim3(TPB), 0, s, cur, Zs,
+                       t->sp_secw, t->sp_loc, nsec);
+    hipLaunchKernelGGL(k_sp_sector_len, dim3((uint32_t)gbpe_div_up(nsec, 256)), dim3(256), 0, s,
+                       (const uint32_t*)t->sp_loc, nsec, Zs, t->sec);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    // presence bitmap
+    t->W = (uint32_t)gbpe_div_up(nsec, 32);
+    const uint64_t words = (uint64_t)t->max_id * t->W;
+    rc = sp_grow(t, &t->bits, &t->bits_cap, words);
+    if (rc != GBPE_OK) return rc;
+    TR_HIP(t, hipMemsetAsync(t->bits, 0, words * 4, s));
+    hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(nsec, TPB / 64)), dim3(TPB), 0, s, cur,
+                       (const uint2*)t->sec, nsec, t->bits, t->W);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    // zone buffers: the zone, and the stale source (previous stream, n_prev - Zs <= z + last_mc symbols)
+    const uint64_t zneed = (gbpe_div_up((uint64_t)z + t->last_mc + 1, TILE) + 2) * TILE;
+    if (zneed > t->zcap) {
+        for (int k = 0; k < 2; ++k) {
+            hipFree(t->zbuf[k]);
+            t->zbuf[k] = nullptr;
+        }
+        hipFree(t->wtmp);
+        t->wtmp = nullptr;
+        t->zcap = 0;
+        if (hipMalloc(&t->zbuf[0], zneed * t->bps) != hipSuccess || hipMalloc(&t->zbuf[1], zneed * t->bps) != hipSuccess ||
+            hipMalloc(&t->wtmp, zneed * t->bps) != hipSuccess)
+            return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(zone) failed");
+        t->zcap = zneed;
+    }
+    for (int k = 0; k < 2; ++k) TR_HIP(t, hipMemsetAsync(t->zbuf[k], 0, t->zcap * t->bps, s));
+    TR_HIP(t, hipMemcpyAsync(t->zbuf[0], cur + Zs, (uint64_t)z * t->bps, hipMemcpyDeviceToDevice, s));
+    uint64_t sl = (uint64_t)z + t->last_mc;
+    if (Zs + sl > t->cap_syms) sl = t->cap_syms - Zs;
+    if (sl > t->zcap) sl = t->zcap;
+    TR_HIP(t, hipMemcpyAsync(t->zbuf[1], stale + Zs, sl * t->bps, hipMemcpyDeviceToDevice, s));
+    // states
+    if (!t->zst) {
+        TR_HIP(t, hipMalloc(&t->zst, sizeof(DevState)));
+        TR_HIP(t, hipHostMalloc((void**)&t->h_zst, sizeof(DevState), hipHostMallocDefault));
+    }
+    memset(t->h_zst, 0, sizeof(DevState));
+    t->h_zst->n = z;
+    TR_HIP(t, hipMemcpyAsync(t->zst, t->h_zst, sizeof(DevState), hipMemcpyHostToDevice, s));
+    t->h_st->B = Zs;
+    t->h_st->Bp = Zs;
+    t->h_st->body_rm = 0;
+    t->h_st->sp_abort = 0;
+    TR_HIP(t, hipMemcpyAsync(&t->st->B, &t->h_st->B, 4 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    t->sp = true;
+    t->bcur = t->cur;
+    t->zcur = 0;
+    ++t->sp_enters;
+    t->sp_sectors = nsec;
+    t->sp_zone = z;
+    return GBPE_OK;
+}
+
+// sparse → dense: the body sectors gathered in order into the other dense
+// buffer, the zone appended; the old body buffer becomes the stale buffer, with
+// the zone's stale buffer at its global place (positions >= Bp: the only ones the
+// next merge's stale window can read).
+template <typename S>
+int sp_exit(gbpe_trainer* t) {
+    hipStream_t s = t->ctx->stream;
+    DevState* hs = t->h_st;
+    TR_HIP(t, hipMemcpyAsync(hs, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    const uint32_t B = hs->B, Bp = hs->Bp, n = hs->n;
+    const uint32_t z = n - B;
+    S* body = (S*)t->buf[t->bcur];
+    S* dst = (S*)t->buf[t->bcur ^ 1];
+    const uint32_t nsec = t->nsec;
+    hipLaunchKernelGGL(k_sp_counts, dim3((uint32_t)gbpe_div_up(nsec, 256)), dim3(256), 0, s, (const uint2*)t->sec, nsec,
+                       t->sp_loc);
+    const uint64_t nblk = gbpe_div_up(nsec, SCAN_BLK);
+    hipLaunchKernelGGL(k_chunk_scan1, dim3((uint32_t)nblk), dim3(SCAN_TPB), 0, s, (const uint32_t*)t->sp_loc,
+                       (uint64_t)nsec, t->sp_loc, t->sp_blk);
+    hipLaunchKernelGGL(k_chunk_scan2, dim3(1), dim3(SCAN_TPB), 0, s, t->sp_blk, nblk, t->sp_blk + nblk);
+    hipLaunchKernelGGL(k_sp_gather<S>, dim3((uint32_t)gbpe_div_up(nsec, TPB / 64)), dim3(TPB), 0, s, (const S*)body,
+                       (const uint2*)t->sec, nsec, (const uint32_t*)t->sp_loc, (const uint64_t*)t->sp_blk, dst);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    uint64_t btot = 0;
+    TR_HIP(t, hipMemcpyAsync(&btot, t->sp_blk + nblk, 8, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipMemcpyAsync(dst + B, t->zbuf[t->zcur], (uint64_t)z * t->bps, hipMemcpyDeviceToDevice, s));
+    // zero the rest of the dense buffer's padding the kernels may read (halo / look-ahead)
+    TR_HIP(t, hipMemsetAsync(dst + n, 0, (t->cap_syms - n) * t->bps, s));
+    uint64_t sl = t->zcap;
+    if (Bp + sl > t->cap_syms) sl = t->cap_syms - Bp;
+    TR_HIP(t, hipMemcpyAsync(body + Bp, t->zbuf[t->zcur ^ 1], sl * t->bps, hipMemcpyDeviceToDevice, s));
+    hs->sp_abort = 0;
+    TR_HIP(t, hipMemcpyAsync(&t->st->sp_abort, &hs->sp_abort, 4, hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    if (btot != B) return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "sparse exit: body sectors hold %llu symbols, expected %u",
+                                         (unsigned long long)btot, B);
+    t->cur = t->bcur ^ 1;
+    t->sp = false;
+    ++t->sp_exits;
+    return GBPE_OK;
+}
+
+int sp_exit_any(gbpe_trainer* t) { return !t->sp ? GBPE_OK : (t->u16 ? sp_exit<uint16_t>(t) : sp_exit<uint32_t>(t)); }
 
 }  // namespace
 
@@ -921,6 +1466,10 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     // u16 symbols when every id the run can produce fits in 15 bits
     const uint64_t max_id = (uint64_t)next_id + t->needed;    // exclusive
     t->u16 = max_id <= 0x8000ull;
+    t->max_id = (uint32_t)(max_id < 0x10000ull ? max_id : 0x10000ull);
+    if (const char* e = getenv("GBPE_SPARSE_DIV")) t->sp_div = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
+    if (t->sp_zt < 5) t->sp_zt = 5;
     t->bps = t->u16 ? 2 : 4;
     t->n0 = n;
     t->n = (uint32_t)n;
@@ -1051,7 +1600,16 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     // rebuild the pair table when it gets crowded (dead pairs accumulate)
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
     if ((uint64_t)t->h_st->used * 2 > slots) {
-        int rc = table_rebuild(t);
+        int rc = sp_exit_any(t);   // the full recount runs on the dense stream
+        if (rc == GBPE_OK) rc = table_rebuild(t);
+        if (rc != GBPE_OK) return rc;
+    }
+    // sector-sparse loop once merges touch a small fraction of the stream
+    if (t->sp_cooldown) {
+        --t->sp_cooldown;
+    } else if (!t->sp && !t->sharded && !(t->flags & GBPE_TRAIN_DENSE_ONLY) && t->last_mc &&
+        ((t->flags & GBPE_TRAIN_SPARSE_EARLY) || (uint64_t)t->last_mc * t->sp_div <= t->n)) {
+        int rc = t->u16 ? sp_enter<uint16_t>(t) : sp_enter<uint32_t>(t);
         if (rc != GBPE_OK) return rc;
     }
     // reset the per-step counter + budget (trainer.js:239)
@@ -1060,6 +1618,7 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     hs->budget = k;
     TR_HIP(t, hipMemcpyAsync(&t->st->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     TR_HIP(t, hipMemcpyAsync(&t->st->budget, &hs->budget, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    if (t->sp) TR_HIP(t, hipMemcpyAsync(&t->zst->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     const uint64_t ntiles = gbpe_div_up(t->n, TILE);
     // tile blocks + stale-tail blocks (the window is at most mc <= n/2 symbols)
     const uint32_t g_tail = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
@@ -1068,21 +1627,41 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     const uint32_t g_compact = (uint32_t)ntiles + g_tail;
     const uint32_t g_refresh = grid_persistent(t->ctx, t->tb.nblk, 2);
     const bool timing = (t->flags & GBPE_TRAIN_TIMING) != 0;
+    const bool sparse = t->sp;
+    SpGrid sg{};
+    if (sparse) {
+        const uint32_t zn = t->n - hs->B;   // zone length (it only shrinks within a step)
+        const uint64_t zt = gbpe_div_up(zn, TILE);
+        sg.body = (uint32_t)gbpe_div_up(t->W, SP_WPW);
+        sg.copy = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u : grid_persistent(t->ctx, gbpe_div_up(zn / 5 + 1, TPB * 8), 1);
+        sg.zdelta = (uint32_t)(zt ? zt : 1);
+        sg.zcompact = (uint32_t)zt + ((t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
+                                      : grid_persistent(t->ctx, gbpe_div_up(zn / 2 + 1, TPB * 16), 1));
+        sg.refresh = g_refresh;
+    }
     for (uint32_t r = 0; r < k; ++r) {
         hipEvent_t* ev = timing ? &t->evs[5 * r] : nullptr;
-        int rc = t->u16 ? launch_merge<uint16_t>(t, r, s, g_delta, g_compact, g_refresh, timing, ev)
+        int rc;
+        if (sparse)
+            rc = t->u16 ? launch_merge_sparse<uint16_t>(t, r, s, sg, timing, ev)
+                        : launch_merge_sparse<uint32_t>(t, r, s, sg, timing, ev);
+        else
+            rc = t->u16 ? launch_merge<uint16_t>(t, r, s, g_delta, g_compact, g_refresh, timing, ev)
                         : launch_merge<uint32_t>(t, r, s, g_delta, g_compact, g_refresh, timing, ev);
         if (rc != GBPE_OK) return rc;
     }
     TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipMemcpyAsync(t->h_log, t->d_log, (size_t)k * 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (sparse) TR_HIP(t, hipMemcpyAsync(t->h_zst, t->zst, sizeof(DevState), hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipStreamSynchronize(s));
     const uint32_t done = hs->merges_done;
-    if (hs->err) {
-        return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "training invariant violated (err=0x%x: %s%s%s)", hs->err,
-                              (hs->err & ERR_TABLE_FULL) ? "pair table full " : "",
-                              (hs->err & ERR_COUNT_MISMATCH) ? "survivor count mismatch " : "",
-                              (hs->err & ERR_PAIR_MISSING) ? "selected pair missing" : "");
+    const uint32_t err = hs->err | (sparse ? t->h_zst->err : 0u);
+    if (err) {
+        return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "training invariant violated (err=0x%x: %s%s%s%s)", err,
+                              (err & ERR_TABLE_FULL) ? "pair table full " : "",
+                              (err & ERR_COUNT_MISMATCH) ? "survivor count mismatch " : "",
+                              (err & ERR_PAIR_MISSING) ? "selected pair missing " : "",
+                              (err & ERR_SPARSE_WINDOW) ? "sparse stale window outside the zone" : "");
     }
     if (timing) {
         for (uint32_t r = 0; r < done; ++r) {
@@ -1111,7 +1690,19 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     }
     t->n = hs->n;
     if (N != t->n) return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "host/device symbol count disagree");
-    t->cur ^= (done & 1u);
+    if (done) t->last_mc = t->h_log[(done - 1) * 4 + 3];
+    if (sparse) {
+        t->zcur ^= (int)(done & 1u);
+        t->sp_merges += done;
+        if (hs->sp_abort) {   // a merge outgrew the zone: it was not run; continue dense
+            int rc = sp_exit_any(t);
+            if (rc != GBPE_OK) return rc;
+            t->sp_cooldown = 1;
+            if (done == 0 && !hs->stop) return gbpe_trainer_step(t, max_merges, merges_out, n_done, early_stop);
+        }
+    } else {
+        t->cur ^= (done & 1u);
+    }
     t->done += done;
     t->stop = hs->stop != 0;
     if (n_done) *n_done = done;
@@ -1138,6 +1729,11 @@ extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
     o->timed_merges = t->timed_merges;
     o->live_pairs = t->h_st->live;
     o->max_live_pairs = t->h_st->max_live;
+    o->sparse_merges = t->sp_merges;
+    o->sparse_enters = t->sp_enters;
+    o->sparse_exits = t->sp_exits;
+    o->sparse_sectors = t->sp_sectors;
+    o->sparse_zone = t->sp_zone;
     return GBPE_OK;
 }
 
@@ -1146,6 +1742,10 @@ extern "C" int gbpe_trainer_symbols(gbpe_trainer* t, uint32_t* out, uint64_t cap
     *n = t->n;
     if (!out) return GBPE_OK;
     if (cap < t->n) return gbpe_set_error(t->ctx, GBPE_E_CAPACITY, "symbols: need %u", t->n);
+    {
+        int rc = sp_exit_any(t);   // back to one dense stream (training may go on; it re-enters later)
+        if (rc != GBPE_OK) return rc;
+    }
     hipStream_t s = t->ctx->stream;
     uint32_t* d = nullptr;
     TR_HIP(t, hipMalloc(&d, (uint64_t)t->n * 4 + 4));
@@ -1204,6 +1804,16 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->hitmask);
     hipFree(t->tile_cnt);
     hipFree(t->grpsum);
+    hipFree(t->sec);
+    hipFree(t->sp_loc);
+    hipFree(t->sp_blk);
+    hipFree(t->bits);
+    hipFree(t->zbuf[0]);
+    hipFree(t->zbuf[1]);
+    hipFree(t->wtmp);
+    hipFree(t->zst);
+    hipFree(t->d_u32);
+    if (t->h_zst) hipHostFree(t->h_zst);
     hipFree(t->dt.slots);
     hipFree(t->dt.dirty);
     hipFree(t->d_nlog);
@@ -1733,10 +2343,10 @@ extern "C" int gbpe_shard_import_counts(gbpe_trainer* t, const void* d_lists, co
     hipLaunchKernelGGL(k_clear_dirty_all, dim3((uint32_t)gbpe_div_up(t->tb.nblk, 256)), dim3(256), 0, s, t->st, t->tb);
     if (t->u16)
         hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st,
-                           0u, 0, t->tb, (uint16_t*)nullptr, (const uint32_t*)nullptr);
+                           0u, 0, t->tb, (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
     else
         hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st,
-                           0u, 0, t->tb, (uint32_t*)nullptr, (const uint32_t*)nullptr);
+                           0u, 0, t->tb, (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipStreamSynchronize(s));
@@ -1814,7 +2424,8 @@ int shard_phase1(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl, ui
     const uint32_t eager = (uint32_t)gbpe_div_up(t->n, TILE);   // the stream may grow by appended windows
     const uint32_t g_delta = (uint32_t)gbpe_div_up(t->cap_syms, TILE) - 1;
     const Table dt = delta_view(t, cl);
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum, t->d_nlog, rec);
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum, t->d_nlog, rec,
+                       (DevState*)nullptr, 0u);
     if (t->flags & GBPE_TRAIN_EXACT_COMPACTION)
         hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, dt,
                            t->hitmask, t->tile_cnt, t->grpsum, eager);
@@ -1847,7 +2458,7 @@ int shard_phase2(gbpe_trainer* t, uint32_t round, const uint32_t* recv, uint32_t
         hipLaunchKernelGGL((k_compact<S, false>), dim3(g_tiles), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
     hipLaunchKernelGGL(k_refresh<S>, dim3(grid_persistent(t->ctx, t->tb.nblk, 2)), dim3(TPB), 0, s, t->st, round, 1,
-                       t->tb, cur, (const uint32_t*)nullptr);
+                       t->tb, cur, (const uint32_t*)nullptr, (DevState*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
 }

@@ -22,6 +22,8 @@ GBPE_E_EMPTY = -6
 GBPE_E_INTERNAL = -7
 
 GBPE_TRAIN_EXACT_COMPACTION = 1 << 0
+GBPE_TRAIN_DENSE_ONLY = 1 << 3
+GBPE_TRAIN_SPARSE_EARLY = 1 << 4
 GBPE_TRAIN_TIMING = 1 << 1
 GBPE_TRAIN_GPT4_BOUNDARIES = 1 << 2
 
@@ -47,7 +49,9 @@ class TrainerStats(C.Structure):
                 ("table_used", C.c_uint64), ("max_live_pairs", C.c_uint64), ("bytes_per_symbol", C.c_uint32),
                 ("early_stop", C.c_uint32), ("ms_merge", C.c_double), ("ms_select", C.c_double),
                 ("ms_other", C.c_double), ("timed_merges", C.c_uint64),
-                ("ms_delta", C.c_double), ("ms_compact", C.c_double)]
+                ("ms_delta", C.c_double), ("ms_compact", C.c_double),
+                ("sparse_merges", C.c_uint64), ("sparse_enters", C.c_uint32), ("sparse_exits", C.c_uint32),
+                ("sparse_sectors", C.c_uint64), ("sparse_zone", C.c_uint64)]
 
 
 PROGRESS_CB = C.CFUNCTYPE(C.c_int, C.POINTER(Progress), u32p, C.c_void_p)

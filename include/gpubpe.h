@@ -89,6 +89,15 @@ int gbpe_pretokenize_gpt4_device(gbpe_ctx* ctx, const void* d_bytes, uint64_t n,
  * (src/wasm/pre_tokenizer.mjs:226-292) computed on the device, for NFC UTF-8
  * input; ignored when word_starts is given */
 #define GBPE_TRAIN_GPT4_BOUNDARIES   (1u << 2)
+/* Sector-sparse merge loop.  Once the merge counts have fallen
+ * far below the stream length, the stream is re-laid out as word-aligned
+ * sectors with a token-presence bitmap: a merge then touches only the sectors
+ * holding both of its tokens, plus a dense zone at the end of the stream that
+ * carries the reference's compaction quirk.  On by default (same results as
+ * the dense loop); DENSE_ONLY disables it, SPARSE_EARLY enters it at the first
+ * step boundary where the zone fits (tests). */
+#define GBPE_TRAIN_DENSE_ONLY        (1u << 3)
+#define GBPE_TRAIN_SPARSE_EARLY      (1u << 4)
 
 typedef struct gbpe_train_opts {
     uint32_t target_vocab_size;  /* trainer.js:149 targetVocabSize (reference default 4096) */
@@ -148,6 +157,11 @@ typedef struct gbpe_trainer_stats {
     uint64_t timed_merges;
     double   ms_delta;            /* k_delta alone (HIP events between the two stream kernels) */
     double   ms_compact;          /* k_compact alone (tiles + stale-tail blocks) */
+    uint64_t sparse_merges;       /* merges run by the sector-sparse loop */
+    uint32_t sparse_enters;       /* dense -> sparse re-layouts */
+    uint32_t sparse_exits;        /* sparse -> dense re-layouts (export, table rebuild, zone too small) */
+    uint64_t sparse_sectors;      /* sectors of the last sparse layout */
+    uint64_t sparse_zone;         /* zone length at the last sparse entry */
 } gbpe_trainer_stats;
 int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* out);
 /* Current symbol stream in the reference u32 layout (bit16 = word start). */

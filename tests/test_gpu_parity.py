@@ -21,12 +21,15 @@ def eng():
 
 
 def _train_native(eng, data: bytes, target: int, exact=False, word_starts=None, batch=128, next_id=256,
-                  vocab_size=None, table_log2=0, max_steps=None):
-    """Drive the stepwise C-ABI directly; returns merges, final stream, live pair counts, stats."""
+                  vocab_size=None, table_log2=0, max_steps=None, sparse=None):
+    """Drive the stepwise C-ABI directly; returns merges, final stream, live pair counts, stats.
+    sparse: None = the library's policy, "dense" = dense loop only, "early" = sector-sparse
+    loop from the first step boundary where its zone fits."""
     from gpubpe import _lib
     lib = _lib.load()
     ctx = eng.device
     flags = _lib.GBPE_TRAIN_EXACT_COMPACTION if exact else 0
+    flags |= {None: 0, "dense": _lib.GBPE_TRAIN_DENSE_ONLY, "early": _lib.GBPE_TRAIN_SPARSE_EARLY}[sparse]
     opts = _lib.TrainOpts(target_vocab_size=target, vocab_size=vocab_size or next_id, next_token_id=next_id,
                           batch_size=batch, flags=flags, table_log2=table_log2)
     tr = C.c_void_p()
