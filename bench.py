@@ -190,6 +190,8 @@ def train_leg(args, lib, ctx, dist, rank):
         "ms_delta": sk.ms_delta, "ms_compact": sk.ms_compact, "timed_merges": int(sk.timed_merges),
         "tail_dropped": int(st.tail_dropped), "max_live_pairs": int(st.max_live_pairs),
         "last_merge": last,
+        "sparse": {"merges": int(st.sparse_merges), "enters": int(st.sparse_enters), "exits": int(st.sparse_exits),
+                   "sectors": int(st.sparse_sectors), "zone_at_entry": int(st.sparse_zone)},
     }
     return data, res
 

@@ -36,6 +36,7 @@
 #include "common.h"
 #include "scan.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdarg>
 
@@ -97,6 +98,9 @@ struct DevState {
     uint32_t Bp;           // body length during the previous merge (stale-window source offset)
     uint32_t body_rm;      // B-sides removed from the body by this merge
     uint32_t sp_abort;     // a selected merge does not fit the zone: not run, host goes dense
+    uint32_t rticket;      // k_refresh workgroups done (fused selection)
+    uint32_t cand;         // candidate sectors of this merge (trace)
+    uint32_t hitsec;       // sectors with a site (trace)
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
@@ -192,13 +196,44 @@ __device__ __forceinline__ void lds_add(LdsTab<N>& t, const Table& tb, DevState*
     table_add(tb, st, pid, d);   // LDS table crowded: go straight to the global table
 }
 
+// Flush the workgroup's aggregated deltas into the global table.  Small tables
+// (<= 8 slots per thread) are first compacted to a list so every thread does at
+// most a few global adds instead of one per slot it owns: a merge's few live
+// entries then cost one global round trip, not a serial chain.  The table's
+// contents are consumed (callers clear it before reuse).
 template <int N>
 __device__ __forceinline__ void lds_flush(LdsTab<N>& t, const Table& tb, DevState* st) {
     __syncthreads();
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
-        uint32_t k = t.key[i], v = t.val[i];
-        if (k != 0u && v != 0u) table_add(tb, st, k, v);
+    const uint32_t nt = blockDim.x;
+    if (N > 8 * (int)nt) {
+        for (int i = threadIdx.x; i < N; i += nt) {
+            uint32_t k = t.key[i], v = t.val[i];
+            if (k != 0u && v != 0u) table_add(tb, st, k, v);
+        }
+        return;
     }
+    __shared__ uint32_t s_cnt;
+    uint32_t kk[8], vv[8], live = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t i = threadIdx.x + j * nt;
+        kk[j] = i < (uint32_t)N ? t.key[i] : 0u;
+        vv[j] = i < (uint32_t)N ? t.val[i] : 0u;
+        if (kk[j] && vv[j]) live |= 1u << j;
+    }
+    if (threadIdx.x == 0) s_cnt = 0u;
+    __syncthreads();
+    uint32_t off = live ? atomicAdd(&s_cnt, (uint32_t)__popc(live)) : 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if ((live >> j) & 1u) {
+            t.key[off] = kk[j];
+            t.val[off] = vv[j];
+            ++off;
+        }
+    __syncthreads();
+    const uint32_t total = s_cnt;
+    for (uint32_t i = threadIdx.x; i < total; i += nt) table_add(tb, st, t.key[i], t.val[i]);
 }
 
 template <typename S>
@@ -276,11 +311,23 @@ __global__ __launch_bounds__(TPB) void k_count_full(DevState* st, const S* __res
     lds_flush(lt, tb, st);
 }
 
+__device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log, uint32_t* __restrict__ grpsum,
+                             uint32_t* __restrict__ nlog, uint32_t* __restrict__ rec, DevState* zst, uint32_t exact);
+
+// Selection fused into k_refresh (FusedSel::log != nullptr): the last workgroup
+// to finish re-maxing selects the NEXT merge, saving a launch per merge.
+struct FusedSel {
+    uint32_t* log = nullptr;
+    uint32_t* grpsum = nullptr;
+    uint32_t exact = 0;
+};
+
 // recompute block maxima for dirty blocks; with `finish`, also closes the
 // merge of `round` (state.symbol_count := new count, train.wgsl:605-607)
 template <typename S>
 __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, int finish, Table tb, S* __restrict__ cur,
-                                                 const uint32_t* __restrict__ rwlist, DevState* zst) {
+                                                 const uint32_t* __restrict__ rwlist, DevState* zst,
+                                                 uint32_t* __restrict__ clog = nullptr, FusedSel fs = FusedSel()) {
     __shared__ uint64_t red[TPB / 64];
     __shared__ uint32_t rlive[TPB / 64];
     (void)cur;
@@ -288,11 +335,16 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
     if (finish && !st->stop && !st->stall && st->merges_done == round + 1u) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             if (zst) {   // sector-sparse: global length, body length, zone length
+                if (clog) {
+                    clog[2 * round] = st->cand;
+                    clog[2 * round + 1] = st->hitsec;
+                }
                 st->tail_total += zst->m;
                 st->n = st->new_n;
                 st->Bp = st->B;
                 st->B -= st->body_rm;
                 zst->n = st->n - st->B;
+                if (zst->valid_total && zst->valid_total != zst->n + 1u) atomicOr(&st->err, ERR_COUNT_MISMATCH);
             } else if (st->sharded) {   // commit the new global layout computed by k_shard_recv
                 st->tail_total += st->m_glob;
                 st->poff = st->off;
@@ -362,26 +414,40 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
         }
         __syncthreads();
     }
+    if (fs.log) {   // last workgroup out selects the next merge
+        __shared__ uint32_t s_last;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();   // this block's maxima (and block 0's finish) before the ticket
+            s_last = atomicAdd(&st->rticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();       // acquire: every block's writes, L1 invalidated
+        if (threadIdx.x == 0) st->rticket = 0u;
+        select_merge(st, tb, fs.log, fs.grpsum, nullptr, nullptr, zst, fs.exact);
+    }
 }
 
 constexpr uint32_t GRP = 64;    // tiles per group sum (two-level tile prefix)
 constexpr uint32_t GSTR = 64;   // group sums 256 B apart: each is its own atomic serialisation point
 
-// argmax over block maxima + the reference's bpe_setup_merge (train.wgsl:340-364)
-__global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, uint32_t* __restrict__ log,
-                                                        uint32_t* __restrict__ grpsum, uint32_t* __restrict__ nlog,
-                                                        uint32_t* __restrict__ rec, DevState* zst, uint32_t exact) {
+// argmax over block maxima + the reference's bpe_setup_merge (train.wgsl:340-364),
+// by one workgroup of any size <= SEL_THREADS
+__device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log, uint32_t* __restrict__ grpsum,
+                             uint32_t* __restrict__ nlog, uint32_t* __restrict__ rec, DevState* zst, uint32_t exact) {
     __shared__ uint64_t red[SEL_THREADS / 64];
     __shared__ uint32_t rlive[SEL_THREADS / 64];
+    const uint32_t nt = blockDim.x;
     if (rec && threadIdx.x == 0) rec[H_L] = 0u;   // the send kernel's list blocks add their counts into it
     if (st->stop || st->stall || st->sp_abort) return;
     {   // group sums of the coming stream pass (the zone's, when sector-sparse) start at zero
         const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(zst ? zst->n : st->n, TILE), GRP);
-        for (uint32_t g = threadIdx.x; g < ngrp; g += SEL_THREADS) grpsum[g * GSTR] = 0u;
+        for (uint32_t g = threadIdx.x; g < ngrp; g += nt) grpsum[g * GSTR] = 0u;
     }
     uint64_t best = 0;
     uint32_t live = 0;
-    for (uint32_t i = threadIdx.x; i < tb.nblk; i += SEL_THREADS) {
+    for (uint32_t i = threadIdx.x; i < tb.nblk; i += nt) {
         uint64_t v = tb.bmax[i];
         best = v > best ? v : best;
         live += tb.blive[i];
@@ -397,7 +463,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
-    for (int w = 1; w < SEL_THREADS / 64; ++w) {
+    for (uint32_t w = 1; w < nt / 64; ++w) {
         best = red[w] > best ? red[w] : best;
         live += rlive[w];
     }
@@ -470,12 +536,21 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
         zst->mc = mc;
         zst->new_n = exact ? zst->n : zst->n - mc;   // zone keep limit: global new_n - B
         zst->m = 0u;
+        zst->valid_total = 0u;
         zst->merges_done = d + 1u;
         st->body_rm = 0u;
+        st->cand = 0u;
+        st->hitsec = 0u;
     }
     st->next_id += 1u;
     st->epoch += 1u;
     st->merges_done = d + 1u;
+}
+
+__global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, uint32_t* __restrict__ log,
+                                                        uint32_t* __restrict__ grpsum, uint32_t* __restrict__ nlog,
+                                                        uint32_t* __restrict__ rec, DevState* zst, uint32_t exact) {
+    select_merge(st, tb, log, grpsum, nlog, rec, zst, exact);
 }
 
 // A merge is "active" for the stream kernels iff k_select logged it this round.
@@ -497,6 +572,7 @@ __device__ __forceinline__ void load_own(const S* cur, uint64_t i0, uint32_t* __
 
 constexpr int LTAB_T = 1024;          // per-tile LDS delta table of k_delta
 
+
 __device__ __forceinline__ uint32_t lane_mask32(uint64_t i0, uint64_t lim) {
     // bits k with i0 + k < lim, k < 32
     return i0 >= lim ? 0u : (i0 + 32 <= lim ? 0xFFFFFFFFu : ((1u << (uint32_t)(lim - i0)) - 1u));
@@ -513,12 +589,15 @@ __device__ __forceinline__ uint32_t lane_mask32(uint64_t i0, uint64_t lim) {
 // loop state is read, so the state's scalar load overlaps the HBM latency.  Lanes
 // with no site within reach and no tail element do no delta work; a tile with no
 // such lane passes a single barrier.
-template <typename S, bool EXACT>
+// STAGE (the sector-sparse zone: few tiles, latency-bound): the work loop reads
+// the lane's symbols from an LDS copy instead of re-reading L2 per position.
+template <typename S, bool EXACT, bool STAGE = false>
 __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, const S* cur, Table tb,
                                                uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
                                                uint32_t* __restrict__ grpsum, uint32_t eager_tiles) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     __shared__ LdsTab<LTAB_T> lt;
+    __shared__ uint32_t stg[STAGE ? EPT * TPB : 1];
     __shared__ uint32_t red[TPB / 64], s_workw[TPB / 64];
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t tl = blockIdx.x;
@@ -583,6 +662,10 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
     if (s_workw[0] | s_workw[1] | s_workw[2] | s_workw[3]) {   // block-uniform: only tiles with a site or a tail element touch the table
         lds_clear(lt);
         __syncthreads();
+        if (STAGE && work) {
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) stg[k * TPB + t] = x[k];
+        }
         if (work) {
             // only the positions where a pair can change: within one of a site, or in
             // the stale tail; symbols re-read from the (L1/L2-hot) tile by index so the
@@ -595,9 +678,15 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
                 rel &= rel - 1;
                 const uint64_t i = i0 + k;
                 if (i == 0) continue;
-                const uint32_t xi = cur[i];
+                uint32_t xi, xp;
+                if (STAGE) {   // the lane's own symbols, staged in LDS below
+                    xi = stg[k * TPB + t];
+                    xp = k ? stg[(k - 1) * TPB + t] : xm1;
+                } else {   // L1/L2-hot re-read (keeps the streaming kernel's LDS small)
+                    xi = cur[i];
+                    xp = cur[i - 1];
+                }
                 if (xi & WS) continue;   // no pair ends at i (old or new)
-                const uint32_t xp = cur[i - 1];
                 const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
                 const uint32_t tp = xp & TM, ti = xi & TM;
                 if (tp && ti) {
@@ -874,15 +963,34 @@ __global__ void k_export_symbols(const S* __restrict__ s, uint32_t* __restrict__
 //     of being left in place.
 // Per merge: k_select → k_body (candidate sectors + window copy) → k_delta (zone)
 // → k_compact<ZONE> → k_refresh.
-constexpr uint32_t SP_WPW = 2;       // bitmap words (32 sectors each) per k_body workgroup
+constexpr uint32_t SP_WPW = 4;       // bitmap words (32 sectors each) per k_body workgroup
 constexpr uint32_t SP_CH = 256;      // symbols per wave pass over a sector (4 per lane)
 constexpr uint32_t SP_INV = 0xFFFFFFFFu;
+constexpr uint32_t SP_SHRINKS = 64;  // zone shrinks per sparse entry (sector capacity)
+
+// Per-sector pair signature: a 1024-bit Bloom filter (2 hash bits) of every pair
+// the sector has held since the filters were last rebuilt.  The token bitmap
+// gives candidate sectors; the signature drops most of those where a and b are
+// both present but never adjacent.
+constexpr uint32_t SP_SIGW = 32;     // u32 words per sector signature
+__device__ __forceinline__ uint32_t sig_hash(uint32_t pid) { return gbpe_fmix32(pid ^ 0x9E3779B9u); }
+__device__ __forceinline__ bool sig_has(const uint32_t* __restrict__ sig, uint32_t pid) {
+    const uint32_t h = sig_hash(pid), b1 = h & 1023u, b2 = (h >> 16) & 1023u;
+    return ((sig[b1 >> 5] >> (b1 & 31u)) & (sig[b2 >> 5] >> (b2 & 31u)) & 1u) != 0u;
+}
+__device__ __forceinline__ void sig_set(uint32_t* __restrict__ sig, uint32_t pid) {
+    const uint32_t h = sig_hash(pid), b1 = h & 1023u, b2 = (h >> 16) & 1023u;
+    const uint32_t m1 = 1u << (b1 & 31u), m2 = 1u << (b2 & 31u);
+    if (!(sig[b1 >> 5] & m1)) atomicOr(&sig[b1 >> 5], m1);
+    if (!(sig[b2 >> 5] & m2)) atomicOr(&sig[b2 >> 5], m2);
+}
 
 // One wave merges one sector in place (snapshot semantics, k_delta's delta rule,
 // survivors compacted to the sector's front).  Returns the B-sides removed.
 template <typename S>
 __device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uint32_t b, uint32_t nw,
-                                LdsTab<LTAB_T>& lt, const Table& tb, DevState* st, uint32_t& out_cnt) {
+                                LdsTab<LTAB_T>& lt, const Table& tb, DevState* st, uint32_t* __restrict__ sig,
+                                uint32_t& out_cnt) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     const int lane = threadIdx.x & 63;
     const uint32_t pid_ab = (a << 16) | b;
@@ -929,9 +1037,13 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uin
                 if (!h[j]) {
                     if (h[j - 1]) {
                         const uint32_t t2 = h[j + 1] ? nw : ti;
-                        if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+                        if (t2) {
+                            lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+                            sig_set(sig, (nw << 16) | t2);
+                        }
                     } else if (h[j + 1] && tp) {
                         lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+                        sig_set(sig, (tp << 16) | nw);
                     }
                 }
             }
@@ -958,19 +1070,155 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uin
     return removed;
 }
 
-// Body pass: blocks [0, nbody) each test SP_WPW bitmap words of (a-row & b-row)
-// and merge the candidate sectors (one wave per sector); blocks >= nbody copy the
-// stale-window source [n - 2mc - Bp, + mc) of the zone's other buffer to `wtmp`.
+// Single-workgroup zone pass (zone <= ZMAX symbols): k_delta + k_compact<ZONE>
+// in one workgroup.  Each thread holds 32 consecutive zone symbols in registers
+// and builds k_delta's branch-free site masks; only positions next to a site or
+// in the stale tail touch the LDS copy and the delta table.  Kept survivors
+// (A-sides rewritten, also in place: the reference's ping buffer) are compacted
+// into the other zone buffer and the stale window follows them.  The window
+// source is read from the other buffer before anything is written to it.
+constexpr uint32_t ZMAX = 8192;             // zone symbols handled by one workgroup
+constexpr uint32_t ZWIN = 2048;             // >= ZMAX / 5 >= mc (k_select keeps zone >= 5 mc)
 template <typename S>
+struct ZoneLds {
+    uint4 xv[ZMAX * sizeof(S) / 16];        // the zone (symbol i = ((S*)xv)[i])
+    S wb[ZWIN];
+    uint32_t wsum[TPB / 64], wtail[TPB / 64], left;
+};
+
+template <typename S, bool EXACT>
+__device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __restrict__ zo, ZoneLds<S>& L,
+                         LdsTab<LTAB_T>& lt, const Table& tb) {
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    constexpr int V = EPT * sizeof(S) / 16;  // 16-byte vectors per thread
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t z = zst->n, mc = st->mc, a = st->a, b = st->b, nw = st->nw;
+    const uint32_t lim = EXACT ? z : z - mc;
+    const uint32_t pid_ab = (a << 16) | b;
+    const uint32_t i0 = (uint32_t)t * EPT;
+    S* xs = reinterpret_cast<S*>(L.xv);
+    uint32_t x[EPT];
+    {
+        uint4 v[V];
+        const uint4* src = reinterpret_cast<const uint4*>(zc + i0);   // zone buffers hold >= 2 tiles
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = src[k];
+#pragma unroll
+        for (int k = 0; k < V; ++k) L.xv[t * V + k] = v[k];
+        const S* e = reinterpret_cast<const S*>(v);
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
+    }
+    if (!EXACT) {
+        const uint64_t src0 = (uint64_t)st->n - 2ull * mc - st->Bp;
+        for (uint32_t u = t; u < mc; u += TPB) L.wb[u] = zo[src0 + u];
+    }
+    lds_clear(lt);
+    __syncthreads();
+    const uint32_t xm2 = i0 >= 2 ? (uint32_t)xs[i0 - 2] : 0u, xm1 = i0 >= 1 ? (uint32_t)xs[i0 - 1] : 0u;
+    const uint32_t nxr = i0 + EPT < z ? (uint32_t)xs[i0 + EPT] : 0u;
+    uint32_t eb = 0, ea = 0;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        eb |= (x[k] == b ? 1u : 0u) << k;
+        ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
+    }
+    const uint32_t inb = lane_mask32(i0, z);
+    const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;
+    const uint32_t h_m1 = (i0 >= 1 && i0 - 1 < z && xm1 == b && (xm2 & TM) == a) ? 1u : 0u;
+    const uint32_t h_32 = (nxr == b && (ea >> (EPT - 1))) ? 1u : 0u;
+    const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (EPT + 1));
+    const uint32_t below = lane_mask32(i0, lim);
+    const uint32_t surv = inb & ~hitm, keep = surv & below;
+    const uint32_t rwm = ((hitm >> 1) | (h_32 << (EPT - 1))) & inb;
+    uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2) | ~below) & inb;
+    while (rel) {
+        const int k = __ffs(rel) - 1;
+        rel &= rel - 1;
+        const uint32_t i = i0 + k;
+        if (i == 0) continue;
+        const uint32_t xi = xs[i];
+        if (xi & WS) continue;
+        const uint32_t xp = xs[i - 1];
+        const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+        const uint32_t tp = xp & TM, ti = xi & TM;
+        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        if (!h0 && i < lim) {
+            if (hm) {
+                const uint32_t t2 = hp ? nw : ti;
+                if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+            } else if (hp && tp) {
+                lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+            }
+        }
+    }
+    // block exclusive scan of the kept counts; tail survivors sum to m
+    const uint32_t kc = __popc(keep);
+    uint32_t incl = kc, tl = __popc(surv & ~below);
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    for (int off = 32; off > 0; off >>= 1) tl += __shfl_xor(tl, off);
+    if (lane == 63) L.wsum[wid] = incl;
+    if (lane == 0) L.wtail[wid] = tl;
+    __syncthreads();
+    uint32_t pre = incl - kc, Kz = 0, m = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < TPB / 64; ++w2) {
+        pre += w2 < wid ? L.wsum[w2] : 0u;
+        Kz += L.wsum[w2];
+        m += L.wtail[w2];
+    }
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        const bool rw = (rwm >> k) & 1u;
+        const uint32_t v = rw ? (nw | (x[k] & WS)) : x[k];
+        if (rw) zc[i0 + k] = (S)v;                  // the reference's in-place ping buffer
+        if ((keep >> k) & 1u) {
+            if (pre == Kz - 1) L.left = v;         // the survivor just before the window
+            zo[pre++] = (S)v;
+        }
+    }
+    if (!EXACT && m) {
+        __syncthreads();
+        const uint32_t woff = mc - m;
+        for (uint32_t j = t; j < m; j += TPB) {
+            const uint32_t x1 = L.wb[woff + j];
+            const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : L.left;
+            zo[Kz + j] = (S)x1;
+            if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) lds_add(lt, tb, st, ((x0 & TM) << 16) | (x1 & TM), 1u);
+        }
+    }
+    lds_flush(lt, tb, st);
+    if (t == 0) {
+        zst->m = m;
+        zst->valid_total = Kz + m + 1u;   // survivors + 1 (k_refresh checks it against the new layout)
+    }
+}
+
+// Body pass: blocks [0, nbody) each test SP_WPW bitmap words of (a-row & b-row),
+// keep the candidate sectors whose pair signature may hold (a, b), and merge them
+// (one wave per sector); blocks >= nbody copy the stale-window source
+// [n - 2mc - Bp, + mc) of the zone's other buffer to `wtmp`.
+// With `zst` (zone <= ZMAX), block nbody runs the whole zone pass (zone_one) and
+// there are no copy blocks: one launch merges body and zone.
+template <typename S, bool EXACT>
 __global__ __launch_bounds__(TPB) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
-                                              uint32_t* __restrict__ bits, uint32_t W, Table tb, uint32_t nbody,
-                                              const S* __restrict__ zoth, S* __restrict__ wtmp) {
+                                              uint32_t* __restrict__ bits, uint32_t W, uint32_t* __restrict__ sig,
+                                              Table tb, uint32_t nbody, const S* __restrict__ zoth, S* __restrict__ wtmp,
+                                              uint32_t clog, DevState* zst, S* __restrict__ zcur) {
     __shared__ LdsTab<LTAB_T> lt;
-    __shared__ uint32_t s_list[SP_WPW * 32];
-    __shared__ uint32_t s_n, s_rm[TPB / 64];
+    __shared__ uint32_t s_tok[SP_WPW * 32], s_list[SP_WPW * 32];
+    __shared__ uint32_t s_ntok, s_n, s_rm[TPB / 64];
+    __shared__ ZoneLds<S> zl;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     if (!merge_active(st, round)) return;
     const uint32_t a = st->a, b = st->b, nw = st->nw;
+    if (zst && blockIdx.x == nbody) {
+        zone_one<S, EXACT>(st, zst, zcur, (S*)zoth, zl, lt, tb);
+        return;
+    }
     if (blockIdx.x >= nbody) {
         const uint32_t mc = st->mc;
         const uint64_t src0 = (uint64_t)st->n - 2ull * mc - st->Bp;
@@ -978,40 +1226,50 @@ __global__ __launch_bounds__(TPB) void k_body(DevState* st, uint32_t round, S* _
         for (uint64_t u = (uint64_t)(blockIdx.x - nbody) * TPB + t; u < mc; u += stride) wtmp[u] = zoth[src0 + u];
         return;
     }
-    if (wid == 0) {
-        const uint32_t w = blockIdx.x * SP_WPW + lane;
+    const uint32_t pid_ab = (a << 16) | b;
+    if (t == 0) {
+        s_ntok = 0u;
+        s_n = 0u;
+    }
+    __syncthreads();
+    if (t < (int)SP_WPW) {   // token candidates
+        const uint32_t w = blockIdx.x * SP_WPW + t;
         uint32_t c = 0;
-        if (lane < (int)SP_WPW && w < W) c = bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w];
-        const uint32_t pc = __popc(c);
-        uint32_t incl = pc;
-        for (int off = 1; off < (int)SP_WPW; off <<= 1) {
-            const uint32_t o = __shfl_up(incl, off);
-            if (lane >= off) incl += o;
+        if (w < W) c = bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w];
+        if (c) {
+            uint32_t pos = atomicAdd(&s_ntok, (uint32_t)__popc(c));
+            while (c) {
+                const int bit = __ffs(c) - 1;
+                c &= c - 1;
+                s_tok[pos++] = w * 32u + (uint32_t)bit;
+            }
         }
-        uint32_t pos = incl - pc;
-        while (c) {
-            const int bit = __ffs(c) - 1;
-            c &= c - 1;
-            s_list[pos++] = w * 32u + (uint32_t)bit;
-        }
-        if (lane == (int)SP_WPW - 1) s_n = incl;
+    }
+    __syncthreads();
+    const uint32_t ntok = s_ntok;
+    if (ntok == 0) return;
+    for (uint32_t j = t; j < ntok; j += TPB) {   // signature filter
+        const uint32_t sct = s_tok[j];
+        if (sig_has(sig + (uint64_t)sct * SP_SIGW, pid_ab)) s_list[atomicAdd(&s_n, 1u)] = sct;
     }
     __syncthreads();
     const uint32_t ncand = s_n;
     if (ncand == 0) return;
+    if (t == 0 && clog) atomicAdd(&st->cand, ncand);
     lds_clear(lt);
     __syncthreads();
     uint32_t removed = 0;
     for (uint32_t j = wid; j < ncand; j += TPB / 64) {
-        const uint32_t s = s_list[j];
-        const uint2 e = sec[s];
+        const uint32_t sct = s_list[j];
+        const uint2 e = sec[sct];
         uint32_t out = 0;
-        const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, tb, st, out);
+        const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, tb, st, sig + (uint64_t)sct * SP_SIGW, out);
         if (r) {
             removed += r;
             if (lane == 0) {
-                sec[s].y = out;
-                atomicOr(&bits[(uint64_t)nw * W + (s >> 5)], 1u << (s & 31u));
+                if (clog) atomicAdd(&st->hitsec, 1u);
+                sec[sct].y = out;
+                atomicOr(&bits[(uint64_t)nw * W + (sct >> 5)], 1u << (sct & 31u));
             }
         }
     }
@@ -1041,56 +1299,65 @@ __global__ __launch_bounds__(1024) void k_sp_zone_start(const S* __restrict__ cu
     if (threadIdx.x == 0) *out = s_found;   // 0 = none
 }
 
-// sector k's start: first word start in [k*SEC, (k+1)*SEC) (one wave per window)
+// window j of a body region [base, base + len) covers [base + j*SEC, +SEC); its
+// sector starts at the window's first word start (window 0: at `base`, which is
+// a word start or the stream's first symbol).  One wave per window.
 template <typename S>
-__global__ __launch_bounds__(TPB) void k_sp_sectors(const S* __restrict__ body, uint32_t Zs, uint32_t SEC,
-                                                    uint32_t* __restrict__ starts, uint32_t nsec) {
-    const uint32_t k = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+__global__ __launch_bounds__(TPB) void k_sp_sectors(const S* __restrict__ body, uint32_t base, uint32_t len, uint32_t SEC,
+                                                    uint32_t* __restrict__ starts, uint32_t nwin) {
+    const uint32_t j = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (k >= nsec) return;
-    const uint64_t lo = (uint64_t)k * SEC, hi = lo + SEC < Zs ? lo + SEC : Zs;
-    uint32_t found = SP_INV;
-    if (k == 0) found = 0;   // the stream's first symbol starts sector 0
-    for (uint64_t base = lo; base < hi && found == SP_INV; base += 64) {
-        const uint64_t i = base + lane;
+    if (j >= nwin) return;
+    const uint64_t end = (uint64_t)base + len;
+    const uint64_t lo = (uint64_t)base + (uint64_t)j * SEC, hi = lo + SEC < end ? lo + SEC : end;
+    uint32_t found = j == 0 ? base : SP_INV;
+    for (uint64_t b0 = lo; b0 < hi && found == SP_INV; b0 += 64) {
+        const uint64_t i = b0 + lane;
         const bool ws = i < hi && (body[i] & Sym<S>::WS);
         const unsigned long long m = __ballot(ws);
-        if (m) found = (uint32_t)(base + (uint64_t)(__ffsll((long long)m) - 1));
+        if (m) found = (uint32_t)(b0 + (uint64_t)(__ffsll((long long)m) - 1));
     }
-    if (lane == 0) starts[k] = found;
+    if (lane == 0) starts[j] = found;
 }
 
-__global__ void k_sp_sector_len(const uint32_t* __restrict__ starts, uint32_t nsec, uint32_t Zs, uint2* __restrict__ sec) {
+__global__ void k_sp_sector_len(const uint32_t* __restrict__ starts, uint32_t nwin, uint32_t end, uint2* __restrict__ sec) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= nsec) return;
+    if (k >= nwin) return;
     const uint32_t st = starts[k];
     if (st == SP_INV) {
         sec[k] = make_uint2(0u, 0u);
         return;
     }
-    uint32_t end = Zs;
-    for (uint32_t j = k + 1; j < nsec; ++j)   // windows inside one long word have no start
+    uint32_t e = end;
+    for (uint32_t j = k + 1; j < nwin; ++j)   // windows inside one long word have no start
         if (starts[j] != SP_INV) {
-            end = starts[j];
+            e = starts[j];
             break;
         }
-    sec[k] = make_uint2(st, end - st);
+    sec[k] = make_uint2(st, e - st);
 }
 
-// presence bits of every token of every sector (one wave per sector)
+// presence bits of every token and the pair signature of sectors [k0, k0 + nk) (one wave per sector)
 template <typename S>
-__global__ __launch_bounds__(TPB) void k_sp_bits(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t nsec,
-                                                 uint32_t* __restrict__ bits, uint32_t W) {
-    const uint32_t k = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+__global__ __launch_bounds__(TPB) void k_sp_bits(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t k0,
+                                                 uint32_t nk, uint32_t* __restrict__ bits, uint32_t W,
+                                                 uint32_t* __restrict__ sig) {
+    const uint32_t k = k0 + blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (k >= nsec) return;
+    if (k >= k0 + nk) return;
     const uint2 e = sec[k];
     const uint32_t bit = 1u << (k & 31u);
     uint32_t* col = bits + (k >> 5);
+    uint32_t* sg = sig + (uint64_t)k * SP_SIGW;
     for (uint32_t j = lane; j < e.y; j += 64) {
-        const uint32_t tok = body[e.x + j] & Sym<S>::TM;
+        const uint32_t x = body[e.x + j];
+        const uint32_t tok = x & Sym<S>::TM;
         uint32_t* wp = col + (uint64_t)tok * W;
         if (!(*wp & bit)) atomicOr(wp, bit);
+        if (j && !(x & Sym<S>::WS)) {
+            const uint32_t tp = body[e.x + j - 1] & Sym<S>::TM;
+            if (tp && tok) sig_set(sg, (tp << 16) | tok);
+        }
     }
 }
 
@@ -1115,6 +1382,18 @@ __global__ __launch_bounds__(TPB) void k_sp_gather(const S* __restrict__ body, c
 }  // namespace
 
 // ─── host side ──────────────────────────────────────────────────────────────
+
+// launch configuration of one captured step (gbpe_trainer_step)
+struct GraphKey {
+    bool sparse = false;
+    uint32_t k = 0;
+    int cur = 0, zcur = 0, bcur = 0;
+    uint32_t gd = 0, gc = 0, gr = 0, sb = 0, sc = 0, szd = 0, szc = 0;
+    bool z1 = false;
+    void *z0 = nullptr, *z1p = nullptr, *b0 = nullptr, *b1 = nullptr;
+    uint32_t W = 0;
+    bool operator==(const GraphKey& o) const { return memcmp(this, &o, sizeof(*this)) == 0; }
+};
 
 struct gbpe_trainer {
     gbpe_ctx* ctx = nullptr;
@@ -1159,11 +1438,16 @@ struct gbpe_trainer {
     uint32_t last_mc = 0;        // count of the last merge run
     int bcur = 0;                // dense buffer holding the body sectors
     uint32_t nsec = 0;
-    uint64_t nsec_cap = 0;
+    uint64_t nsec_cap = 0, loc_cap = 0;
+    uint32_t bend = 0;           // end of the body's sector windows in the body buffer
+    uint32_t sp_shrinks = 0;     // zone shrinks since the last entry
     uint2* sec = nullptr;        // {start, count} per sector
     uint32_t* sp_loc = nullptr;  // per-sector scratch (starts / scan)
     uint64_t* sp_blk = nullptr;  // scan block totals
     uint32_t* bits = nullptr;    // presence bitmap, rows = token ids, W words per row
+    uint32_t* sig = nullptr;     // per-sector pair signatures (SP_SIGW words each)
+    uint64_t sig_cap = 0;
+    uint64_t sp_age = 0;         // sparse merges since the filters were built
     uint64_t bits_cap = 0;       // words
     uint32_t W = 0;
     void* zbuf[2] = {nullptr, nullptr};
@@ -1178,6 +1462,15 @@ struct gbpe_trainer {
     uint32_t sp_div = 64;        // enter when last_mc * sp_div <= n
     uint32_t sp_cooldown = 0;    // steps to stay dense after an abort
     uint32_t sp_zt = 10;         // zone target = sp_zt * last_mc + 64 (>= 5: see sp_enter)
+    bool fuse_sel = false;       // GBPE_FUSE_SELECT=1: select in k_refresh's last workgroup (measured slower: DESIGN §2b)
+    uint32_t refresh_blocks = 0; // GBPE_REFRESH_BLOCKS: k_refresh grid (0 = 2 per CU)
+    bool use_graph = false;      // replay steps as HIP graphs (GBPE_GRAPH=1): measured slower on ROCm 7
+    hipGraphExec_t graph_exec = nullptr;
+    GraphKey graph_key;
+    uint32_t graph_builds = 0;
+    uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
+    uint32_t* h_clog = nullptr;
+    FILE* trace = nullptr;
 };
 
 namespace {
@@ -1227,8 +1520,9 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     S* oth = (S*)t->buf[t->cur ^ (round & 1) ^ 1];
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
-                       (uint32_t*)nullptr, (uint32_t*)nullptr, (DevState*)nullptr, 0u);
+    if (round == 0 || !t->fuse_sel)   // with fuse_sel, later merges are selected by the previous k_refresh
+        hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
+                           (uint32_t*)nullptr, (uint32_t*)nullptr, (DevState*)nullptr, exact ? 1u : 0u);
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
     if (exact) {
         hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
@@ -1244,8 +1538,12 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
+    FusedSel fs;
+    fs.log = t->fuse_sel ? t->d_log : nullptr;
+    fs.grpsum = t->grpsum;
+    fs.exact = exact ? 1u : 0u;
     hipLaunchKernelGGL(k_refresh<S>, dim3(g_refresh), dim3(TPB), 0, s, t->st, round, 1, t->tb, cur,
-                       (const uint32_t*)nullptr, (DevState*)nullptr);
+                       (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, fs);
     if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
@@ -1255,6 +1553,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
 
 struct SpGrid {
     uint32_t body, copy, zdelta, zcompact, refresh;
+    bool zone1;   // the zone fits one workgroup: it runs inside k_body
 };
 
 template <typename S>
@@ -1263,29 +1562,44 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     S* zo = (S*)t->zbuf[t->zcur ^ (round & 1) ^ 1];
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
-                       (uint32_t*)nullptr, (uint32_t*)nullptr, t->zst, exact ? 1u : 0u);
+    if (round == 0 || !t->fuse_sel)   // with fuse_sel, later merges are selected by the previous k_refresh
+        hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
+                           (uint32_t*)nullptr, (uint32_t*)nullptr, t->zst, exact ? 1u : 0u);
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
-    hipLaunchKernelGGL(k_body<S>, dim3(g.body + g.copy), dim3(TPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
-                       t->bits, t->W, t->tb, g.body, (const S*)zo, (S*)t->wtmp);
+    const uint32_t gb = g.body + (g.zone1 ? 1u : g.copy);
+    DevState* z1 = g.zone1 ? t->zst : nullptr;
     if (exact)
-        hipLaunchKernelGGL((k_delta<S, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc, t->tb,
-                           t->hitmask, t->tile_cnt, t->grpsum, g.zdelta);
+        hipLaunchKernelGGL((k_body<S, true>), dim3(gb), dim3(TPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
+                           t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, z1, zc);
     else
-        hipLaunchKernelGGL((k_delta<S, false>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc, t->tb,
-                           t->hitmask, t->tile_cnt, t->grpsum, g.zdelta);
+        hipLaunchKernelGGL((k_body<S, false>), dim3(gb), dim3(TPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
+                           t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, z1, zc);
+    if (!g.zone1) {
+        if (exact)
+            hipLaunchKernelGGL((k_delta<S, true, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc,
+                               t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta);
+        else
+            hipLaunchKernelGGL((k_delta<S, false, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc,
+                               t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta);
+    }
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
-    if (exact)
-        hipLaunchKernelGGL((k_compact<S, true, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
-                           (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb,
-                           (const S*)t->wtmp, (const DevState*)t->st);
-    else
-        hipLaunchKernelGGL((k_compact<S, false, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
-                           (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb,
-                           (const S*)t->wtmp, (const DevState*)t->st);
+    if (!g.zone1) {
+        if (exact)
+            hipLaunchKernelGGL((k_compact<S, true, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
+                               (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
+                               t->tb, (const S*)t->wtmp, (const DevState*)t->st);
+        else
+            hipLaunchKernelGGL((k_compact<S, false, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
+                               (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
+                               t->tb, (const S*)t->wtmp, (const DevState*)t->st);
+    }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
+    FusedSel fs;
+    fs.log = t->fuse_sel ? t->d_log : nullptr;
+    fs.grpsum = t->grpsum;
+    fs.exact = exact ? 1u : 0u;
     hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 1, t->tb, (S*)nullptr,
-                       (const uint32_t*)nullptr, t->zst);
+                       (const uint32_t*)nullptr, t->zst, t->d_clog, fs);
     if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
@@ -1303,6 +1617,41 @@ int sp_grow(gbpe_trainer* t, T** p, uint64_t* cap, uint64_t need) {
                               (unsigned long long)(need * sizeof(T)));
     }
     *cap = need;
+    return GBPE_OK;
+}
+
+// sectors over body positions [base, base + len) appended after sector t->nsec
+// (their token bits and signatures too); base is a word start
+template <typename S>
+int sp_add_sectors(gbpe_trainer* t, uint32_t base, uint32_t len) {
+    hipStream_t s = t->ctx->stream;
+    const uint32_t nw = (uint32_t)gbpe_div_up(len, t->sp_secw);
+    if ((uint64_t)t->nsec + nw > t->nsec_cap || (uint64_t)t->nsec + nw > (uint64_t)t->W * 32 ||
+        ((uint64_t)t->nsec + nw) * SP_SIGW > t->sig_cap || nw > t->loc_cap)
+        return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "sector capacity exceeded");
+    const S* body = (const S*)t->buf[t->bcur];
+    hipLaunchKernelGGL(k_sp_sectors<S>, dim3((uint32_t)gbpe_div_up(nw, TPB / 64)), dim3(TPB), 0, s, body, base, len,
+                       t->sp_secw, t->sp_loc, nw);
+    hipLaunchKernelGGL(k_sp_sector_len, dim3((uint32_t)gbpe_div_up(nw, 256)), dim3(256), 0, s, (const uint32_t*)t->sp_loc,
+                       nw, base + len, t->sec + t->nsec);
+    hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(nw, TPB / 64)), dim3(TPB), 0, s, body,
+                       (const uint2*)t->sec, t->nsec, nw, t->bits, t->W, t->sig);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    t->nsec += nw;
+    t->bend = base + len;
+    return GBPE_OK;
+}
+
+// (re)build the token bitmap and the pair signatures from the body sectors
+template <typename S>
+int sp_filters(gbpe_trainer* t) {
+    hipStream_t s = t->ctx->stream;
+    TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
+    TR_HIP(t, hipMemsetAsync(t->sig, 0, t->sig_cap * 4, s));
+    hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(t->nsec, TPB / 64)), dim3(TPB), 0, s,
+                       (const S*)t->buf[t->bcur], (const uint2*)t->sec, 0u, t->nsec, t->bits, t->W, t->sig);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    t->sp_age = 0;
     return GBPE_OK;
 }
 
@@ -1325,37 +1674,35 @@ int sp_enter(gbpe_trainer* t) {
     TR_HIP(t, hipStreamSynchronize(s));
     if (Zs < t->sp_secw) return GBPE_OK;   // the whole stream is one long word (or tiny): stay dense
     const uint32_t z = n - Zs;
-    // sectors
-    const uint32_t nsec = (uint32_t)gbpe_div_up(Zs, t->sp_secw);
-    uint64_t cap_blk = 0;
-    int rc = sp_grow(t, &t->sec, &t->nsec_cap, nsec);
-    uint64_t loc_cap = t->nsec_cap;
-    if (rc == GBPE_OK && (!t->sp_loc || loc_cap < nsec)) {
+    // capacities for every sector the body can ever hold: windows over [0, n) plus
+    // one partial window per zone shrink (at most SP_SHRINKS per entry)
+    const uint64_t cap = gbpe_div_up(n, t->sp_secw) + SP_SHRINKS + 1;
+    int rc = sp_grow(t, &t->sec, &t->nsec_cap, cap);
+    if (rc == GBPE_OK && (!t->sp_loc || t->loc_cap < cap)) {
         hipFree(t->sp_loc);
         hipFree(t->sp_blk);
         t->sp_loc = nullptr;
         t->sp_blk = nullptr;
-        if (hipMalloc(&t->sp_loc, (uint64_t)t->nsec_cap * 4) != hipSuccess ||
-            hipMalloc(&t->sp_blk, (gbpe_div_up(t->nsec_cap, SCAN_BLK) + 1) * 8) != hipSuccess)
+        t->loc_cap = 0;
+        if (hipMalloc(&t->sp_loc, cap * 4) != hipSuccess ||
+            hipMalloc(&t->sp_blk, (gbpe_div_up(cap, SCAN_BLK) + 1) * 8) != hipSuccess)
             rc = gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sector scratch) failed");
+        else
+            t->loc_cap = cap;
     }
-    (void)cap_blk;
     if (rc != GBPE_OK) return rc;
-    t->nsec = nsec;
-    hipLaunchKernelGGL(k_sp_sectors<S>, dim3((uint32_t)gbpe_div_up(nsec, TPB / 64)), dim3(TPB), 0, s, cur, Zs,
-                       t->sp_secw, t->sp_loc, nsec);
-    hipLaunchKernelGGL(k_sp_sector_len, dim3((uint32_t)gbpe_div_up(nsec, 256)), dim3(256), 0, s,
-                       (const uint32_t*)t->sp_loc, nsec, Zs, t->sec);
-    GBPE_LAUNCH_CHECK(t->ctx);
-    // presence bitmap
-    t->W = (uint32_t)gbpe_div_up(nsec, 32);
-    const uint64_t words = (uint64_t)t->max_id * t->W;
-    rc = sp_grow(t, &t->bits, &t->bits_cap, words);
+    t->W = (uint32_t)gbpe_div_up(cap, 32);
+    rc = sp_grow(t, &t->bits, &t->bits_cap, (uint64_t)t->max_id * t->W);
+    if (rc == GBPE_OK) rc = sp_grow(t, &t->sig, &t->sig_cap, cap * SP_SIGW);
     if (rc != GBPE_OK) return rc;
-    TR_HIP(t, hipMemsetAsync(t->bits, 0, words * 4, s));
-    hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(nsec, TPB / 64)), dim3(TPB), 0, s, cur,
-                       (const uint2*)t->sec, nsec, t->bits, t->W);
-    GBPE_LAUNCH_CHECK(t->ctx);
+    t->bcur = t->cur;
+    t->nsec = 0;
+    TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
+    TR_HIP(t, hipMemsetAsync(t->sig, 0, cap * SP_SIGW * 4, s));
+    rc = sp_add_sectors<S>(t, 0u, Zs);
+    if (rc != GBPE_OK) return rc;
+    t->sp_age = 0;
+    t->sp_shrinks = 0;
     // zone buffers: the zone, and the stale source (previous stream, n_prev - Zs <= z + last_mc symbols)
     const uint64_t zneed = (gbpe_div_up((uint64_t)z + t->last_mc + 1, TILE) + 2) * TILE;
     if (zneed > t->zcap) {
@@ -1392,11 +1739,51 @@ int sp_enter(gbpe_trainer* t) {
     TR_HIP(t, hipMemcpyAsync(&t->st->B, &t->h_st->B, 4 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     TR_HIP(t, hipStreamSynchronize(s));
     t->sp = true;
-    t->bcur = t->cur;
     t->zcur = 0;
     ++t->sp_enters;
-    t->sp_sectors = nsec;
+    t->sp_sectors = t->nsec;
     t->sp_zone = z;
+    return GBPE_OK;
+}
+
+// Zone shrink at a step boundary: the zone keeps >= zt = sp_zt * last_mc + 64
+// symbols (from a word start); its front moves into the body as new sectors and
+// both zone buffers shift down by the moved length (B and Bp with them, so the
+// stale buffer keeps its global coordinates).
+template <typename S>
+int sp_shrink(gbpe_trainer* t) {
+    hipStream_t s = t->ctx->stream;
+    DevState* hs = t->h_st;
+    const uint32_t z = t->n - hs->B;
+    const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
+    if (t->sp_shrinks >= SP_SHRINKS || (uint64_t)z < 2 * zt + 4096) return GBPE_OK;
+    S* zc = (S*)t->zbuf[t->zcur];
+    S* zo = (S*)t->zbuf[t->zcur ^ 1];
+    hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, (const S*)zc, (uint32_t)(z - zt), t->d_u32);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    uint32_t L = 0;
+    TR_HIP(t, hipMemcpyAsync(&L, t->d_u32, 4, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    if (L < 4096) return GBPE_OK;
+    if ((uint64_t)t->bend + L > t->cap_syms) return GBPE_OK;
+    S* body = (S*)t->buf[t->bcur];
+    TR_HIP(t, hipMemcpyAsync(body + t->bend, zc, (uint64_t)L * t->bps, hipMemcpyDeviceToDevice, s));
+    int rc = sp_add_sectors<S>(t, t->bend, L);
+    if (rc != GBPE_OK) return rc;
+    const uint64_t rest = t->zcap - L;
+    TR_HIP(t, hipMemcpyAsync(t->wtmp, zc + L, rest * t->bps, hipMemcpyDeviceToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(zc, t->wtmp, rest * t->bps, hipMemcpyDeviceToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(t->wtmp, zo + L, rest * t->bps, hipMemcpyDeviceToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(zo, t->wtmp, rest * t->bps, hipMemcpyDeviceToDevice, s));
+    TR_HIP(t, hipMemsetAsync(zc + rest, 0, (uint64_t)L * t->bps, s));
+    TR_HIP(t, hipMemsetAsync(zo + rest, 0, (uint64_t)L * t->bps, s));
+    hs->B += L;
+    hs->Bp += L;
+    t->h_zst->n = z - L;
+    TR_HIP(t, hipMemcpyAsync(&t->st->B, &hs->B, 2 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(&t->zst->n, &t->h_zst->n, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    ++t->sp_shrinks;
     return GBPE_OK;
 }
 
@@ -1468,8 +1855,17 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     t->u16 = max_id <= 0x8000ull;
     t->max_id = (uint32_t)(max_id < 0x10000ull ? max_id : 0x10000ull);
     if (const char* e = getenv("GBPE_SPARSE_DIV")) t->sp_div = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_GRAPH")) t->use_graph = atoi(e) != 0;
+    if (const char* e = getenv("GBPE_FUSE_SELECT")) t->fuse_sel = atoi(e) != 0;
+    if (const char* e = getenv("GBPE_REFRESH_BLOCKS")) t->refresh_blocks = (uint32_t)atoi(e);
     if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
     if (t->sp_zt < 5) t->sp_zt = 5;
+    if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
+        t->trace = fopen(e, "w");
+        if (t->trace && (hipMalloc(&t->d_clog, (size_t)t->batch * 8) != hipSuccess ||
+                         hipHostMalloc((void**)&t->h_clog, (size_t)t->batch * 8, hipHostMallocDefault) != hipSuccess))
+            t->d_clog = nullptr, t->h_clog = nullptr;   // trace without candidate counts
+    }
     t->bps = t->u16 ? 2 : 4;
     t->n0 = n;
     t->n = (uint32_t)n;
@@ -1612,6 +2008,15 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
         int rc = t->u16 ? sp_enter<uint16_t>(t) : sp_enter<uint32_t>(t);
         if (rc != GBPE_OK) return rc;
     }
+    // keep the zone near its minimum, then rebuild stale filters now and then
+    if (t->sp) {
+        int rc = t->u16 ? sp_shrink<uint16_t>(t) : sp_shrink<uint32_t>(t);
+        if (rc != GBPE_OK) return rc;
+    }
+    if (t->sp && t->sp_age >= 4096) {
+        int rc = t->u16 ? sp_filters<uint16_t>(t) : sp_filters<uint32_t>(t);
+        if (rc != GBPE_OK) return rc;
+    }
     // reset the per-step counter + budget (trainer.js:239)
     DevState* hs = t->h_st;
     hs->merges_done = 0;
@@ -1625,34 +2030,90 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
                             : grid_persistent(t->ctx, gbpe_div_up(t->n / 2 + 1, TPB * 16), 1);
     const uint32_t g_delta = (uint32_t)(ntiles ? ntiles : 1);
     const uint32_t g_compact = (uint32_t)ntiles + g_tail;
-    const uint32_t g_refresh = grid_persistent(t->ctx, t->tb.nblk, 2);
+    uint32_t g_refresh = grid_persistent(t->ctx, t->tb.nblk, 2);
+    if (t->refresh_blocks) g_refresh = std::max<uint32_t>(t->refresh_blocks, (uint32_t)gbpe_div_up(t->tb.nblk, 64));
     const bool timing = (t->flags & GBPE_TRAIN_TIMING) != 0;
     const bool sparse = t->sp;
     SpGrid sg{};
     if (sparse) {
         const uint32_t zn = t->n - hs->B;   // zone length (it only shrinks within a step)
         const uint64_t zt = gbpe_div_up(zn, TILE);
-        sg.body = (uint32_t)gbpe_div_up(t->W, SP_WPW);
+        sg.body = (uint32_t)gbpe_div_up(gbpe_div_up(t->nsec, 32), SP_WPW);
+        sg.zone1 = zn <= ZMAX;
         sg.copy = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u : grid_persistent(t->ctx, gbpe_div_up(zn / 5 + 1, TPB * 8), 1);
         sg.zdelta = (uint32_t)(zt ? zt : 1);
         sg.zcompact = (uint32_t)zt + ((t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
                                       : grid_persistent(t->ctx, gbpe_div_up(zn / 2 + 1, TPB * 16), 1));
         sg.refresh = g_refresh;
     }
-    for (uint32_t r = 0; r < k; ++r) {
-        hipEvent_t* ev = timing ? &t->evs[5 * r] : nullptr;
-        int rc;
-        if (sparse)
-            rc = t->u16 ? launch_merge_sparse<uint16_t>(t, r, s, sg, timing, ev)
-                        : launch_merge_sparse<uint32_t>(t, r, s, sg, timing, ev);
-        else
-            rc = t->u16 ? launch_merge<uint16_t>(t, r, s, g_delta, g_compact, g_refresh, timing, ev)
-                        : launch_merge<uint32_t>(t, r, s, g_delta, g_compact, g_refresh, timing, ev);
+    auto launch_all = [&]() -> int {
+        for (uint32_t r = 0; r < k; ++r) {
+            hipEvent_t* ev = timing ? &t->evs[5 * r] : nullptr;
+            int rc;
+            if (sparse)
+                rc = t->u16 ? launch_merge_sparse<uint16_t>(t, r, s, sg, timing, ev)
+                            : launch_merge_sparse<uint32_t>(t, r, s, sg, timing, ev);
+            else
+                rc = t->u16 ? launch_merge<uint16_t>(t, r, s, g_delta, g_compact, g_refresh, timing, ev)
+                            : launch_merge<uint32_t>(t, r, s, g_delta, g_compact, g_refresh, timing, ev);
+            if (rc != GBPE_OK) return rc;
+        }
+        return GBPE_OK;
+    };
+    // A step is the same few hundred launches step after step: replay it as a HIP
+    // graph (captured once per launch configuration) instead of paying the host
+    // launch path per kernel.  Event timing launches directly.
+    if (timing || !t->use_graph) {
+        int rc = launch_all();
         if (rc != GBPE_OK) return rc;
+    } else {
+        GraphKey key;
+        memset(&key, 0, sizeof(key));   // padding too: keys compare bytewise
+        key.sparse = sparse;
+        key.k = k;
+        key.cur = t->cur;
+        key.zcur = t->zcur;
+        key.bcur = t->bcur;
+        key.gd = g_delta;
+        key.gc = g_compact;
+        key.gr = g_refresh;
+        key.sb = sg.body;
+        key.sc = sg.copy;
+        key.szd = sg.zdelta;
+        key.szc = sg.zcompact;
+        key.z1 = sg.zone1;
+        key.z0 = t->zbuf[0];
+        key.z1p = t->zbuf[1];
+        key.b0 = t->buf[0];
+        key.b1 = t->buf[1];
+        key.W = t->W;
+        if (!t->graph_exec || !(key == t->graph_key)) {
+            if (t->graph_exec) hipGraphExecDestroy(t->graph_exec);
+            t->graph_exec = nullptr;
+            hipGraph_t g = nullptr;
+            TR_HIP(t, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            int rc = launch_all();
+            hipError_t e = hipStreamEndCapture(s, &g);
+            if (rc != GBPE_OK) {
+                if (g) hipGraphDestroy(g);
+                return rc;
+            }
+            if (e != hipSuccess) return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "step capture failed: %s", hipGetErrorString(e));
+            e = hipGraphInstantiate(&t->graph_exec, g, nullptr, nullptr, 0);
+            hipGraphDestroy(g);
+            if (e != hipSuccess) {
+                t->graph_exec = nullptr;
+                return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "step graph instantiate failed: %s", hipGetErrorString(e));
+            }
+            memcpy(&t->graph_key, &key, sizeof(key));
+            ++t->graph_builds;
+        }
+        TR_HIP(t, hipGraphLaunch(t->graph_exec, s));
     }
     TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipMemcpyAsync(t->h_log, t->d_log, (size_t)k * 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     if (sparse) TR_HIP(t, hipMemcpyAsync(t->h_zst, t->zst, sizeof(DevState), hipMemcpyDeviceToHost, s));
+    if (sparse && t->d_clog) TR_HIP(t, hipMemcpyAsync(t->h_clog, t->d_clog, (size_t)k * 8, hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipStreamSynchronize(s));
     const uint32_t done = hs->merges_done;
     const uint32_t err = hs->err | (sparse ? t->h_zst->err : 0u);
@@ -1691,9 +2152,19 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     t->n = hs->n;
     if (N != t->n) return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "host/device symbol count disagree");
     if (done) t->last_mc = t->h_log[(done - 1) * 4 + 3];
+    if (t->trace) {   // merge index, count, stream length before, sparse, candidate sectors, sectors with sites
+        uint64_t nn = N;
+        for (uint32_t r = done; r-- > 0;) nn += t->h_log[r * 4 + 3];
+        for (uint32_t r = 0; r < done; ++r) {
+            fprintf(t->trace, "%u %u %llu %d %u %u\n", t->done + r, t->h_log[r * 4 + 3], (unsigned long long)nn,
+                    sparse ? 1 : 0, sparse && t->h_clog ? t->h_clog[2 * r] : 0u, sparse && t->h_clog ? t->h_clog[2 * r + 1] : 0u);
+            nn -= t->h_log[r * 4 + 3];
+        }
+    }
     if (sparse) {
         t->zcur ^= (int)(done & 1u);
         t->sp_merges += done;
+        t->sp_age += done;
         if (hs->sp_abort) {   // a merge outgrew the zone: it was not run; continue dense
             int rc = sp_exit_any(t);
             if (rc != GBPE_OK) return rc;
@@ -1808,12 +2279,17 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->sp_loc);
     hipFree(t->sp_blk);
     hipFree(t->bits);
+    hipFree(t->sig);
     hipFree(t->zbuf[0]);
     hipFree(t->zbuf[1]);
     hipFree(t->wtmp);
     hipFree(t->zst);
     hipFree(t->d_u32);
     if (t->h_zst) hipHostFree(t->h_zst);
+    if (t->graph_exec) hipGraphExecDestroy(t->graph_exec);
+    hipFree(t->d_clog);
+    if (t->h_clog) hipHostFree(t->h_clog);
+    if (t->trace) fclose(t->trace);
     hipFree(t->dt.slots);
     hipFree(t->dt.dirty);
     hipFree(t->d_nlog);
