@@ -99,6 +99,7 @@ struct DevState {
     uint32_t body_rm;      // B-sides removed from the body by this merge
     uint32_t sp_abort;     // a selected merge does not fit the zone: not run, host goes dense
     uint32_t rticket;      // k_refresh workgroups done (fused selection)
+    uint32_t sel_round;    // sector-sparse: round + 1 of the merge k_body selected
     uint32_t cand;         // candidate sectors of this merge (trace)
     uint32_t hitsec;       // sectors with a site (trace)
 };
@@ -327,22 +328,35 @@ struct FusedSel {
 template <typename S>
 __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, int finish, Table tb, S* __restrict__ cur,
                                                  const uint32_t* __restrict__ rwlist, DevState* zst,
-                                                 uint32_t* __restrict__ clog = nullptr, FusedSel fs = FusedSel()) {
+                                                 uint32_t* __restrict__ clog = nullptr, FusedSel fs = FusedSel(),
+                                                 uint64_t* __restrict__ part = nullptr) {
     __shared__ uint64_t red[TPB / 64];
     __shared__ uint32_t rlive[TPB / 64];
     (void)cur;
     (void)rwlist;
-    if (finish && !st->stop && !st->stall && st->merges_done == round + 1u) {
+    // finish == 2: the sector-sparse loop, whose merge was selected inside k_body
+    // (sel_inline): the step counters move on here
+    const bool fin = finish == 2 ? (!st->stop && !st->sp_abort && st->sel_round == round + 1u)
+                                 : (finish && !st->stop && !st->stall && st->merges_done == round + 1u);
+    if (fin) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             if (zst) {   // sector-sparse: global length, body length, zone length
+                if (finish == 2) {
+                    st->merges_done = round + 1u;
+                    st->next_id += 1u;
+                    st->epoch += 1u;
+                }
                 if (clog) {
                     clog[2 * round] = st->cand;
                     clog[2 * round + 1] = st->hitsec;
                 }
+                st->cand = 0u;
+                st->hitsec = 0u;
                 st->tail_total += zst->m;
                 st->n = st->new_n;
                 st->Bp = st->B;
                 st->B -= st->body_rm;
+                st->body_rm = 0u;
                 zst->n = st->n - st->B;
                 if (zst->valid_total && zst->valid_total != zst->n + 1u) atomicOr(&st->err, ERR_COUNT_MISMATCH);
             } else if (st->sharded) {   // commit the new global layout computed by k_shard_recv
@@ -413,6 +427,15 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             tb.dirty[blk] = 0u;
         }
         __syncthreads();
+    }
+    if (part && threadIdx.x < 64) {   // this workgroup's maximum, for sel_inline
+        const uint32_t blk = b0 + threadIdx.x;
+        uint64_t best = (threadIdx.x < per && blk < tb.nblk) ? tb.bmax[blk] : 0ull;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(best, off);
+            best = o > best ? o : best;
+        }
+        if (threadIdx.x == 0) part[blockIdx.x] = best;
     }
     if (fs.log) {   // last workgroup out selects the next merge
         __shared__ uint32_t s_last;
@@ -672,7 +695,9 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
             // register window is never dynamically indexed
             const uint32_t below = lane_mask32(i0, lim);
             tail = __popc(inb & ~hitm & ~below);
-            uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2) | ~below) & inb;
+            // positions next to a site below the keep limit; the stale tail (old pairs
+            // destroyed, nothing new) is spread over the whole workgroup below
+            uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
             while (rel) {
                 const int k = __ffs(rel) - 1;
                 rel &= rel - 1;
@@ -701,6 +726,16 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
                         lds_add(lt, tb, st, (tp << 16) | nw, 1u);
                     }
                 }
+            }
+        }
+        if (!EXACT && (uint64_t)base + TILE > lim && base < n) {
+            const uint64_t hi = (uint64_t)n < base + TILE ? (uint64_t)n : base + TILE;
+            for (uint64_t i = (lim > base ? (uint64_t)lim : base) + t; i < hi; i += TPB) {
+                if (i == 0) continue;
+                const uint32_t xi = cur[i];
+                if (xi & WS) continue;
+                const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
+                if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
             }
         }
         lds_flush(lt, tb, st);
@@ -1088,11 +1123,11 @@ struct ZoneLds {
 
 template <typename S, bool EXACT>
 __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __restrict__ zo, ZoneLds<S>& L,
-                         LdsTab<LTAB_T>& lt, const Table& tb) {
+                         LdsTab<LTAB_T>& lt, const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     constexpr int V = EPT * sizeof(S) / 16;  // 16-byte vectors per thread
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const uint32_t z = zst->n, mc = st->mc, a = st->a, b = st->b, nw = st->nw;
+    const uint32_t z = zst->n;
     const uint32_t lim = EXACT ? z : z - mc;
     const uint32_t pid_ab = (a << 16) | b;
     const uint32_t i0 = (uint32_t)t * EPT;
@@ -1131,7 +1166,13 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
     const uint32_t below = lane_mask32(i0, lim);
     const uint32_t surv = inb & ~hitm, keep = surv & below;
     const uint32_t rwm = ((hitm >> 1) | (h_32 << (EPT - 1))) & inb;
-    uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2) | ~below) & inb;
+    uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+    for (uint32_t i = (lim > 1u ? lim : 1u) + t; i < z; i += TPB) {   // stale tail: old pairs destroyed
+        const uint32_t xi = xs[i];
+        if (xi & WS) continue;
+        const uint32_t tp = xs[i - 1] & TM, ti = xi & TM;
+        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+    }
     while (rel) {
         const int k = __ffs(rel) - 1;
         rel &= rel - 1;
@@ -1143,7 +1184,7 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
         const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
         const uint32_t tp = xp & TM, ti = xi & TM;
         if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
-        if (!h0 && i < lim) {
+        if (!h0) {
             if (hm) {
                 const uint32_t t2 = hp ? nw : ti;
                 if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
@@ -1197,6 +1238,92 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
     }
 }
 
+// Selection inside k_body (sector-sparse loop): every workgroup reduces the
+// k_refresh partial maxima itself and gets the same merge; workgroup 0 commits
+// it (log, table slot zeroed, state for k_refresh and the zone kernels).  The
+// step counters move on in k_refresh (finish == 2), so nothing a workgroup reads
+// here changes under it.  Saves the k_select launch per merge.
+__device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
+                           uint32_t round, bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
+                           uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc) {
+    __shared__ uint64_t s_red[TPB / 64];
+    __shared__ uint32_t s_ok;
+    const int t = threadIdx.x;
+    if (t == 0) s_ok = (round < st->budget && st->merges_done == round && !st->stop && !st->sp_abort) ? 1u : 0u;
+    __syncthreads();
+    if (!s_ok) return false;
+    uint64_t best = 0;
+    for (uint32_t i = t; i < npart; i += TPB) {
+        const uint64_t v = part[i];
+        best = v > best ? v : best;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    if ((t & 63) == 0) s_red[t >> 6] = best;
+    __syncthreads();
+    best = s_red[0];
+#pragma unroll
+    for (int w = 1; w < TPB / 64; ++w) best = s_red[w] > best ? s_red[w] : best;
+    mc = (uint32_t)(best >> 32);
+    const uint32_t pid = ~(uint32_t)best;
+    a = pid >> 16;
+    b = pid & 0xFFFFu;
+    nw = st->next_id;
+    const bool stop = mc < 2u || nw > 0xFFFFu;                                          // train.wgsl:345-348
+    const bool bad = !stop && !exact && (uint64_t)st->n < 2ull * mc + st->Bp;            // cannot happen
+    const bool abort = !stop && !bad && !exact && (uint64_t)zst->n < 5ull * mc + 2u;    // zone too small
+    const bool go = !stop && !bad && !abort;
+    if (blockIdx.x == 0) {
+        if (t == 0) {
+            if (stop) {
+                st->stop = 1u;
+            } else if (bad) {
+                atomicOr(&st->err, ERR_SPARSE_WINDOW);
+                st->stop = 1u;
+            } else if (abort) {
+                st->sp_abort = 1u;
+            } else {
+                const uint32_t idx = table_find(tb, pid);
+                if (idx == 0xFFFFFFFFu) {
+                    atomicOr(&st->err, ERR_PAIR_MISSING);
+                } else {
+                    // every (a,b) occurrence is a merge site: count -= mc, atomically, since
+                    // other workgroups may already add this merge's stale-window pairs
+                    atomicSub(&tb.slots[idx].y, mc);
+                    tb.dirty[idx >> BLK_LOG2] = 1u;
+                }
+                log[round * 4 + 0] = a;
+                log[round * 4 + 1] = b;
+                log[round * 4 + 2] = nw;
+                log[round * 4 + 3] = mc;
+                st->a = a;
+                st->b = b;
+                st->nw = nw;
+                st->mc = mc;
+                st->new_n = st->n - mc;
+                zst->a = a;
+                zst->b = b;
+                zst->nw = nw;
+                zst->mc = mc;
+                zst->new_n = exact ? zst->n : zst->n - mc;
+                if (!zone1) {   // zone_one (another workgroup of this launch) sets both itself
+                    zst->m = 0u;
+                    zst->valid_total = 0u;
+                }
+                zst->merges_done = round + 1u;
+                st->sel_round = round + 1u;
+            }
+        }
+        if (go) {   // group sums of a multi-tile zone pass start at zero
+            const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(zst->n, TILE), GRP);
+            for (uint32_t g = t; g < ngrp; g += TPB) grpsum[g * GSTR] = 0u;
+        }
+    }
+    return go;
+}
+
 // Body pass: blocks [0, nbody) each test SP_WPW bitmap words of (a-row & b-row),
 // keep the candidate sectors whose pair signature may hold (a, b), and merge them
 // (one wave per sector); blocks >= nbody copy the stale-window source
@@ -1207,20 +1334,21 @@ template <typename S, bool EXACT>
 __global__ __launch_bounds__(TPB) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
                                               uint32_t* __restrict__ bits, uint32_t W, uint32_t* __restrict__ sig,
                                               Table tb, uint32_t nbody, const S* __restrict__ zoth, S* __restrict__ wtmp,
-                                              uint32_t clog, DevState* zst, S* __restrict__ zcur) {
+                                              uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
+                                              const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
+                                              uint32_t* __restrict__ grpsum) {
     __shared__ LdsTab<LTAB_T> lt;
     __shared__ uint32_t s_tok[SP_WPW * 32], s_list[SP_WPW * 32];
     __shared__ uint32_t s_ntok, s_n, s_rm[TPB / 64];
     __shared__ ZoneLds<S> zl;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    if (!merge_active(st, round)) return;
-    const uint32_t a = st->a, b = st->b, nw = st->nw;
-    if (zst && blockIdx.x == nbody) {
-        zone_one<S, EXACT>(st, zst, zcur, (S*)zoth, zl, lt, tb);
+    uint32_t a, b, nw, mc;
+    if (!sel_inline(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc)) return;
+    if (zone1 && blockIdx.x == nbody) {
+        zone_one<S, EXACT>(st, zst, zcur, (S*)zoth, zl, lt, tb, a, b, nw, mc);
         return;
     }
     if (blockIdx.x >= nbody) {
-        const uint32_t mc = st->mc;
         const uint64_t src0 = (uint64_t)st->n - 2ull * mc - st->Bp;
         const uint64_t stride = (uint64_t)(gridDim.x - nbody) * TPB;
         for (uint64_t u = (uint64_t)(blockIdx.x - nbody) * TPB + t; u < mc; u += stride) wtmp[u] = zoth[src0 + u];
@@ -1457,6 +1585,8 @@ struct gbpe_trainer {
     DevState* zst = nullptr;     // the zone's loop state
     DevState* h_zst = nullptr;   // pinned
     uint32_t* d_u32 = nullptr;   // small device scratch
+    uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
+    uint32_t g_refresh = 0;
     uint64_t sp_merges = 0, sp_sectors = 0, sp_zone = 0;
     uint32_t sp_enters = 0, sp_exits = 0;
     uint32_t sp_div = 64;        // enter when last_mc * sp_div <= n
@@ -1562,18 +1692,16 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     S* zo = (S*)t->zbuf[t->zcur ^ (round & 1) ^ 1];
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
-    if (round == 0 || !t->fuse_sel)   // with fuse_sel, later merges are selected by the previous k_refresh
-        hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
-                           (uint32_t*)nullptr, (uint32_t*)nullptr, t->zst, exact ? 1u : 0u);
-    if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
+    if (timing) TR_HIP(t, hipEventRecord(ev[1], s));   // selection runs inside k_body (sel_inline)
     const uint32_t gb = g.body + (g.zone1 ? 1u : g.copy);
-    DevState* z1 = g.zone1 ? t->zst : nullptr;
     if (exact)
         hipLaunchKernelGGL((k_body<S, true>), dim3(gb), dim3(TPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
-                           t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, z1, zc);
+                           t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst,
+                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum);
     else
         hipLaunchKernelGGL((k_body<S, false>), dim3(gb), dim3(TPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
-                           t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, z1, zc);
+                           t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst,
+                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum);
     if (!g.zone1) {
         if (exact)
             hipLaunchKernelGGL((k_delta<S, true, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc,
@@ -1594,12 +1722,8 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
                                t->tb, (const S*)t->wtmp, (const DevState*)t->st);
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
-    FusedSel fs;
-    fs.log = t->fuse_sel ? t->d_log : nullptr;
-    fs.grpsum = t->grpsum;
-    fs.exact = exact ? 1u : 0u;
-    hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 1, t->tb, (S*)nullptr,
-                       (const uint32_t*)nullptr, t->zst, t->d_clog, fs);
+    hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,
+                       (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part);
     if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
@@ -1737,6 +1861,11 @@ int sp_enter(gbpe_trainer* t) {
     t->h_st->body_rm = 0;
     t->h_st->sp_abort = 0;
     TR_HIP(t, hipMemcpyAsync(&t->st->B, &t->h_st->B, 4 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    // per-k_refresh-workgroup maxima the sparse merges select from (sel_inline)
+    if (!t->part) TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
+    hipLaunchKernelGGL(k_refresh<S>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
+                       (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part);
+    GBPE_LAUNCH_CHECK(t->ctx);
     TR_HIP(t, hipStreamSynchronize(s));
     t->sp = true;
     t->zcur = 0;
@@ -1915,6 +2044,8 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         hipHostMalloc((void**)&t->h_log, (size_t)t->batch * 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipHostMalloc failed"));
     t->tb.used = &t->st->used;
+    t->g_refresh = grid_persistent(ctx, t->tb.nblk, 2);
+    if (t->refresh_blocks) t->g_refresh = std::max<uint32_t>(t->refresh_blocks, (uint32_t)gbpe_div_up(t->tb.nblk, 64));
     if (hipMemsetAsync(t->tb.dirty, 0, t->tb.nblk * sizeof(uint32_t), s) != hipSuccess ||
         hipMemsetAsync(t->hitmask, 0, (ntiles0 + 1) * TPB * sizeof(uint32_t), s) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "memset failed"));
@@ -2023,15 +2154,18 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     hs->budget = k;
     TR_HIP(t, hipMemcpyAsync(&t->st->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     TR_HIP(t, hipMemcpyAsync(&t->st->budget, &hs->budget, sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    if (t->sp) TR_HIP(t, hipMemcpyAsync(&t->zst->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    if (t->sp) {
+        hs->sel_round = 0;
+        TR_HIP(t, hipMemcpyAsync(&t->zst->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        TR_HIP(t, hipMemcpyAsync(&t->st->sel_round, &hs->sel_round, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    }
     const uint64_t ntiles = gbpe_div_up(t->n, TILE);
     // tile blocks + stale-tail blocks (the window is at most mc <= n/2 symbols)
     const uint32_t g_tail = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
                             : grid_persistent(t->ctx, gbpe_div_up(t->n / 2 + 1, TPB * 16), 1);
     const uint32_t g_delta = (uint32_t)(ntiles ? ntiles : 1);
     const uint32_t g_compact = (uint32_t)ntiles + g_tail;
-    uint32_t g_refresh = grid_persistent(t->ctx, t->tb.nblk, 2);
-    if (t->refresh_blocks) g_refresh = std::max<uint32_t>(t->refresh_blocks, (uint32_t)gbpe_div_up(t->tb.nblk, 64));
+    const uint32_t g_refresh = t->g_refresh;
     const bool timing = (t->flags & GBPE_TRAIN_TIMING) != 0;
     const bool sparse = t->sp;
     SpGrid sg{};
@@ -2285,6 +2419,7 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->wtmp);
     hipFree(t->zst);
     hipFree(t->d_u32);
+    hipFree(t->part);
     if (t->h_zst) hipHostFree(t->h_zst);
     if (t->graph_exec) hipGraphExecDestroy(t->graph_exec);
     hipFree(t->d_clog);
