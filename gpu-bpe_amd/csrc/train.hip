@@ -998,7 +998,10 @@ __global__ void k_export_symbols(const S* __restrict__ s, uint32_t* __restrict__
 //     of being left in place.
 // Per merge: k_select → k_body (candidate sectors + window copy) → k_delta (zone)
 // → k_compact<ZONE> → k_refresh.
-constexpr uint32_t SP_WPW = 4;       // bitmap words (32 sectors each) per k_body workgroup
+#ifndef GBPE_SP_WPW
+#define GBPE_SP_WPW 16
+#endif
+constexpr uint32_t SP_WPW = GBPE_SP_WPW;   // bitmap words (32 sectors each) per k_body workgroup
 constexpr uint32_t SP_CH = 256;      // symbols per wave pass over a sector (4 per lane)
 constexpr uint32_t SP_INV = 0xFFFFFFFFu;
 constexpr uint32_t SP_SHRINKS = 64;  // zone shrinks per sparse entry (sector capacity)
@@ -1339,6 +1342,7 @@ __global__ __launch_bounds__(TPB) void k_body(DevState* st, uint32_t round, S* _
                                               uint32_t* __restrict__ grpsum) {
     __shared__ LdsTab<LTAB_T> lt;
     __shared__ uint32_t s_tok[SP_WPW * 32], s_list[SP_WPW * 32];
+    __shared__ uint2 s_ext[SP_WPW * 32];
     __shared__ uint32_t s_ntok, s_n, s_rm[TPB / 64];
     __shared__ ZoneLds<S> zl;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -1376,9 +1380,14 @@ __global__ __launch_bounds__(TPB) void k_body(DevState* st, uint32_t round, S* _
     __syncthreads();
     const uint32_t ntok = s_ntok;
     if (ntok == 0) return;
-    for (uint32_t j = t; j < ntok; j += TPB) {   // signature filter
+    for (uint32_t j = t; j < ntok; j += TPB) {   // signature filter; the sector's extent loads alongside
         const uint32_t sct = s_tok[j];
-        if (sig_has(sig + (uint64_t)sct * SP_SIGW, pid_ab)) s_list[atomicAdd(&s_n, 1u)] = sct;
+        const uint2 e = sec[sct];
+        if (sig_has(sig + (uint64_t)sct * SP_SIGW, pid_ab)) {
+            const uint32_t q = atomicAdd(&s_n, 1u);
+            s_list[q] = sct;
+            s_ext[q] = e;
+        }
     }
     __syncthreads();
     const uint32_t ncand = s_n;
@@ -1389,7 +1398,7 @@ __global__ __launch_bounds__(TPB) void k_body(DevState* st, uint32_t round, S* _
     uint32_t removed = 0;
     for (uint32_t j = wid; j < ncand; j += TPB / 64) {
         const uint32_t sct = s_list[j];
-        const uint2 e = sec[sct];
+        const uint2 e = s_ext[j];
         uint32_t out = 0;
         const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, tb, st, sig + (uint64_t)sct * SP_SIGW, out);
         if (r) {
