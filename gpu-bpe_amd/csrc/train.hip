@@ -100,6 +100,7 @@ struct DevState {
     uint32_t sp_abort;     // a selected merge does not fit the zone: not run, host goes dense
     uint32_t rticket;      // k_refresh workgroups done (fused selection)
     uint32_t sel_round;    // sector-sparse: round + 1 of the merge k_body selected
+    uint64_t sp_bytes;     // sector-sparse: bytes moved by the multi-tile zone passes (k_refresh adds them)
     uint32_t cand;         // candidate sectors of this merge (trace)
     uint32_t hitsec;       // sectors with a site (trace)
 };
@@ -357,7 +358,10 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
                 st->Bp = st->B;
                 st->B -= st->body_rm;
                 st->body_rm = 0u;
+                const uint32_t zold = zst->n;
                 zst->n = st->n - st->B;
+                if (!zst->valid_total)   // multi-tile zone: k_delta + k_compact stream it twice, plus the window copy
+                    st->sp_bytes += (uint64_t)sizeof(S) * (2ull * zold + zst->n + 2ull * st->mc);
                 if (zst->valid_total && zst->valid_total != zst->n + 1u) atomicOr(&st->err, ERR_COUNT_MISMATCH);
             } else if (st->sharded) {   // commit the new global layout computed by k_shard_recv
                 st->tail_total += st->m_glob;
@@ -999,7 +1003,7 @@ __global__ void k_export_symbols(const S* __restrict__ s, uint32_t* __restrict__
 // Per merge: k_select → k_body (candidate sectors + window copy) → k_delta (zone)
 // → k_compact<ZONE> → k_refresh.
 #ifndef GBPE_SP_WPW
-#define GBPE_SP_WPW 16
+#define GBPE_SP_WPW 32
 #endif
 constexpr uint32_t SP_WPW = GBPE_SP_WPW;   // bitmap words (32 sectors each) per k_body workgroup
 constexpr uint32_t SP_CH = 256;      // symbols per wave pass over a sector (4 per lane)
@@ -1115,27 +1119,39 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uin
 // (A-sides rewritten, also in place: the reference's ping buffer) are compacted
 // into the other zone buffer and the stale window follows them.  The window
 // source is read from the other buffer before anything is written to it.
-constexpr uint32_t ZMAX = 8192;             // zone symbols handled by one workgroup
-constexpr uint32_t ZWIN = 2048;             // >= ZMAX / 5 >= mc (k_select keeps zone >= 5 mc)
+constexpr int BTPB = 1024;                  // k_body workgroup (16 waves)
+template <typename S> struct ZoneDim {
+    static constexpr int ZPT = sizeof(S) == 2 ? 32 : 16;        // zone positions per thread
+    static constexpr uint32_t ZMAX = (uint32_t)BTPB * ZPT;      // 32768 (u16) / 16384 (u32) symbols: 64 KiB
+    static constexpr uint32_t ZWIN = ZMAX / 4;                   // >= ZMAX / 5 >= mc (zone >= 5 mc)
+};
 template <typename S>
 struct ZoneLds {
-    uint4 xv[ZMAX * sizeof(S) / 16];        // the zone (symbol i = ((S*)xv)[i])
-    S wb[ZWIN];
-    uint32_t wsum[TPB / 64], wtail[TPB / 64], left;
+    uint4 xv[ZoneDim<S>::ZMAX * sizeof(S) / 16];   // the zone (symbol i = ((S*)xv)[i])
+    S wb[ZoneDim<S>::ZWIN];
+    uint32_t wsum[BTPB / 64], wtail[BTPB / 64], left;
 };
+
+__device__ __forceinline__ uint32_t lane_mask_n(uint64_t i0, uint64_t lim, int n) {
+    // bits k with i0 + k < lim, k < n (n <= 32)
+    const uint32_t full = n == 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    return i0 >= lim ? 0u : (i0 + n <= lim ? full : ((1u << (uint32_t)(lim - i0)) - 1u));
+}
 
 template <typename S, bool EXACT>
 __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __restrict__ zo, ZoneLds<S>& L,
-                         LdsTab<LTAB_T>& lt, const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc) {
+                         LdsTab<LTAB_T>& lt, const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
+                         uint64_t* __restrict__ bytes) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
-    constexpr int V = EPT * sizeof(S) / 16;  // 16-byte vectors per thread
+    constexpr int ZPT = ZoneDim<S>::ZPT;
+    constexpr int V = ZPT * sizeof(S) / 16;  // 16-byte vectors per thread
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t z = zst->n;
     const uint32_t lim = EXACT ? z : z - mc;
     const uint32_t pid_ab = (a << 16) | b;
-    const uint32_t i0 = (uint32_t)t * EPT;
+    const uint32_t i0 = (uint32_t)t * ZPT;
     S* xs = reinterpret_cast<S*>(L.xv);
-    uint32_t x[EPT];
+    uint32_t x[ZPT];
     {
         uint4 v[V];
         const uint4* src = reinterpret_cast<const uint4*>(zc + i0);   // zone buffers hold >= 2 tiles
@@ -1145,32 +1161,32 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
         for (int k = 0; k < V; ++k) L.xv[t * V + k] = v[k];
         const S* e = reinterpret_cast<const S*>(v);
 #pragma unroll
-        for (int k = 0; k < EPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
+        for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
     }
     if (!EXACT) {
         const uint64_t src0 = (uint64_t)st->n - 2ull * mc - st->Bp;
-        for (uint32_t u = t; u < mc; u += TPB) L.wb[u] = zo[src0 + u];
+        for (uint32_t u = t; u < mc; u += BTPB) L.wb[u] = zo[src0 + u];
     }
     lds_clear(lt);
     __syncthreads();
     const uint32_t xm2 = i0 >= 2 ? (uint32_t)xs[i0 - 2] : 0u, xm1 = i0 >= 1 ? (uint32_t)xs[i0 - 1] : 0u;
-    const uint32_t nxr = i0 + EPT < z ? (uint32_t)xs[i0 + EPT] : 0u;
+    const uint32_t nxr = i0 + ZPT < z ? (uint32_t)xs[i0 + ZPT] : 0u;
     uint32_t eb = 0, ea = 0;
 #pragma unroll
-    for (int k = 0; k < EPT; ++k) {
+    for (int k = 0; k < ZPT; ++k) {
         eb |= (x[k] == b ? 1u : 0u) << k;
         ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
     }
-    const uint32_t inb = lane_mask32(i0, z);
+    const uint32_t inb = lane_mask_n(i0, z, ZPT);
     const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;
     const uint32_t h_m1 = (i0 >= 1 && i0 - 1 < z && xm1 == b && (xm2 & TM) == a) ? 1u : 0u;
-    const uint32_t h_32 = (nxr == b && (ea >> (EPT - 1))) ? 1u : 0u;
-    const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (EPT + 1));
-    const uint32_t below = lane_mask32(i0, lim);
+    const uint32_t h_32 = (nxr == b && (ea >> (ZPT - 1))) ? 1u : 0u;
+    const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (ZPT + 1));
+    const uint32_t below = lane_mask_n(i0, lim, ZPT);
     const uint32_t surv = inb & ~hitm, keep = surv & below;
-    const uint32_t rwm = ((hitm >> 1) | (h_32 << (EPT - 1))) & inb;
+    const uint32_t rwm = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
     uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
-    for (uint32_t i = (lim > 1u ? lim : 1u) + t; i < z; i += TPB) {   // stale tail: old pairs destroyed
+    for (uint32_t i = (lim > 1u ? lim : 1u) + t; i < z; i += BTPB) {   // stale tail: old pairs destroyed
         const uint32_t xi = xs[i];
         if (xi & WS) continue;
         const uint32_t tp = xs[i - 1] & TM, ti = xi & TM;
@@ -1209,13 +1225,13 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
     __syncthreads();
     uint32_t pre = incl - kc, Kz = 0, m = 0;
 #pragma unroll
-    for (int w2 = 0; w2 < TPB / 64; ++w2) {
+    for (int w2 = 0; w2 < BTPB / 64; ++w2) {
         pre += w2 < wid ? L.wsum[w2] : 0u;
         Kz += L.wsum[w2];
         m += L.wtail[w2];
     }
 #pragma unroll
-    for (int k = 0; k < EPT; ++k) {
+    for (int k = 0; k < ZPT; ++k) {
         const bool rw = (rwm >> k) & 1u;
         const uint32_t v = rw ? (nw | (x[k] & WS)) : x[k];
         if (rw) zc[i0 + k] = (S)v;                  // the reference's in-place ping buffer
@@ -1227,7 +1243,7 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
     if (!EXACT && m) {
         __syncthreads();
         const uint32_t woff = mc - m;
-        for (uint32_t j = t; j < m; j += TPB) {
+        for (uint32_t j = t; j < m; j += BTPB) {
             const uint32_t x1 = L.wb[woff + j];
             const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : L.left;
             zo[Kz + j] = (S)x1;
@@ -1238,6 +1254,8 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
     if (t == 0) {
         zst->m = m;
         zst->valid_total = Kz + m + 1u;   // survivors + 1 (k_refresh checks it against the new layout)
+        // zone read, window source read, kept survivors + window written
+        *bytes += (uint64_t)sizeof(S) * ((uint64_t)z + (EXACT ? 0u : mc) + Kz + m);
     }
 }
 
@@ -1249,14 +1267,14 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
 __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
                            uint32_t round, bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
                            uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc) {
-    __shared__ uint64_t s_red[TPB / 64];
+    __shared__ uint64_t s_red[BTPB / 64];
     __shared__ uint32_t s_ok;
     const int t = threadIdx.x;
     if (t == 0) s_ok = (round < st->budget && st->merges_done == round && !st->stop && !st->sp_abort) ? 1u : 0u;
     __syncthreads();
     if (!s_ok) return false;
     uint64_t best = 0;
-    for (uint32_t i = t; i < npart; i += TPB) {
+    for (uint32_t i = t; i < npart; i += BTPB) {
         const uint64_t v = part[i];
         best = v > best ? v : best;
     }
@@ -1268,7 +1286,7 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     __syncthreads();
     best = s_red[0];
 #pragma unroll
-    for (int w = 1; w < TPB / 64; ++w) best = s_red[w] > best ? s_red[w] : best;
+    for (int w = 1; w < BTPB / 64; ++w) best = s_red[w] > best ? s_red[w] : best;
     mc = (uint32_t)(best >> 32);
     const uint32_t pid = ~(uint32_t)best;
     a = pid >> 16;
@@ -1321,7 +1339,7 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
         }
         if (go) {   // group sums of a multi-tile zone pass start at zero
             const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(zst->n, TILE), GRP);
-            for (uint32_t g = t; g < ngrp; g += TPB) grpsum[g * GSTR] = 0u;
+            for (uint32_t g = t; g < ngrp; g += BTPB) grpsum[g * GSTR] = 0u;
         }
     }
     return go;
@@ -1334,28 +1352,29 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
 // With `zst` (zone <= ZMAX), block nbody runs the whole zone pass (zone_one) and
 // there are no copy blocks: one launch merges body and zone.
 template <typename S, bool EXACT>
-__global__ __launch_bounds__(TPB) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
+__global__ __launch_bounds__(BTPB) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
                                               uint32_t* __restrict__ bits, uint32_t W, uint32_t* __restrict__ sig,
                                               Table tb, uint32_t nbody, const S* __restrict__ zoth, S* __restrict__ wtmp,
                                               uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
-                                              uint32_t* __restrict__ grpsum) {
+                                              uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes) {
     __shared__ LdsTab<LTAB_T> lt;
     __shared__ uint32_t s_tok[SP_WPW * 32], s_list[SP_WPW * 32];
     __shared__ uint2 s_ext[SP_WPW * 32];
-    __shared__ uint32_t s_ntok, s_n, s_rm[TPB / 64];
+    __shared__ uint32_t s_ntok, s_n, s_rm[BTPB / 64];
+    __shared__ uint64_t s_mv[BTPB / 64];
     __shared__ ZoneLds<S> zl;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     uint32_t a, b, nw, mc;
     if (!sel_inline(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc)) return;
     if (zone1 && blockIdx.x == nbody) {
-        zone_one<S, EXACT>(st, zst, zcur, (S*)zoth, zl, lt, tb, a, b, nw, mc);
+        zone_one<S, EXACT>(st, zst, zcur, (S*)zoth, zl, lt, tb, a, b, nw, mc, wg_bytes + nbody);
         return;
     }
     if (blockIdx.x >= nbody) {
         const uint64_t src0 = (uint64_t)st->n - 2ull * mc - st->Bp;
-        const uint64_t stride = (uint64_t)(gridDim.x - nbody) * TPB;
-        for (uint64_t u = (uint64_t)(blockIdx.x - nbody) * TPB + t; u < mc; u += stride) wtmp[u] = zoth[src0 + u];
+        const uint64_t stride = (uint64_t)(gridDim.x - nbody) * BTPB;
+        for (uint64_t u = (uint64_t)(blockIdx.x - nbody) * BTPB + t; u < mc; u += stride) wtmp[u] = zoth[src0 + u];
         return;
     }
     const uint32_t pid_ab = (a << 16) | b;
@@ -1380,7 +1399,8 @@ __global__ __launch_bounds__(TPB) void k_body(DevState* st, uint32_t round, S* _
     __syncthreads();
     const uint32_t ntok = s_ntok;
     if (ntok == 0) return;
-    for (uint32_t j = t; j < ntok; j += TPB) {   // signature filter; the sector's extent loads alongside
+    if (t == 0) wg_bytes[blockIdx.x] += 16ull * ntok;   // extents + signature words read
+    for (uint32_t j = t; j < ntok; j += BTPB) {   // signature filter; the sector's extent loads alongside
         const uint32_t sct = s_tok[j];
         const uint2 e = sec[sct];
         if (sig_has(sig + (uint64_t)sct * SP_SIGW, pid_ab)) {
@@ -1396,11 +1416,13 @@ __global__ __launch_bounds__(TPB) void k_body(DevState* st, uint32_t round, S* _
     lds_clear(lt);
     __syncthreads();
     uint32_t removed = 0;
-    for (uint32_t j = wid; j < ncand; j += TPB / 64) {
+    uint64_t moved = 0;   // sector symbols read + rewritten (wave-uniform)
+    for (uint32_t j = wid; j < ncand; j += BTPB / 64) {
         const uint32_t sct = s_list[j];
         const uint2 e = s_ext[j];
         uint32_t out = 0;
         const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, tb, st, sig + (uint64_t)sct * SP_SIGW, out);
+        moved += (uint64_t)sizeof(S) * (e.y + (r ? out : 0u));
         if (r) {
             removed += r;
             if (lane == 0) {
@@ -1411,11 +1433,20 @@ __global__ __launch_bounds__(TPB) void k_body(DevState* st, uint32_t round, S* _
         }
     }
     lds_flush(lt, tb, st);
-    if (lane == 0) s_rm[wid] = removed;
+    if (lane == 0) {
+        s_rm[wid] = removed;
+        s_mv[wid] = moved;
+    }
     __syncthreads();
     if (t == 0) {
-        const uint32_t r = s_rm[0] + s_rm[1] + s_rm[2] + s_rm[3];
+        uint32_t r = 0;
+        uint64_t mv = 0;
+        for (int w2 = 0; w2 < BTPB / 64; ++w2) {
+            r += s_rm[w2];
+            mv += s_mv[w2];
+        }
         if (r) atomicAdd(&st->body_rm, r);
+        wg_bytes[blockIdx.x] += mv;   // this workgroup's own counter
     }
 }
 
@@ -1474,28 +1505,38 @@ __global__ void k_sp_sector_len(const uint32_t* __restrict__ starts, uint32_t nw
     sec[k] = make_uint2(st, e - st);
 }
 
-// presence bits of every token and the pair signature of sectors [k0, k0 + nk) (one wave per sector)
+// presence bits of every token (with `bits`) and the pair signature of sectors
+// [k0, k0 + nk), one wave per sector.  The signature is built in LDS and stored
+// whole (one 128-B line per sector); bitmap words are tested before the atomic.
 template <typename S>
 __global__ __launch_bounds__(TPB) void k_sp_bits(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t k0,
                                                  uint32_t nk, uint32_t* __restrict__ bits, uint32_t W,
                                                  uint32_t* __restrict__ sig) {
-    const uint32_t k = k0 + blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (k >= k0 + nk) return;
-    const uint2 e = sec[k];
-    const uint32_t bit = 1u << (k & 31u);
-    uint32_t* col = bits + (k >> 5);
-    uint32_t* sg = sig + (uint64_t)k * SP_SIGW;
-    for (uint32_t j = lane; j < e.y; j += 64) {
-        const uint32_t x = body[e.x + j];
-        const uint32_t tok = x & Sym<S>::TM;
-        uint32_t* wp = col + (uint64_t)tok * W;
-        if (!(*wp & bit)) atomicOr(wp, bit);
-        if (j && !(x & Sym<S>::WS)) {
-            const uint32_t tp = body[e.x + j - 1] & Sym<S>::TM;
-            if (tp && tok) sig_set(sg, (tp << 16) | tok);
+    __shared__ uint32_t ssig[TPB / 64][SP_SIGW];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t k = k0 + blockIdx.x * (TPB / 64) + wid;
+    const bool live = k < k0 + nk;
+    if (lane < (int)SP_SIGW) ssig[wid][lane] = 0u;
+    __syncthreads();
+    if (live) {
+        const uint2 e = sec[k];
+        const uint32_t bit = 1u << (k & 31u);
+        uint32_t* col = bits ? bits + (k >> 5) : nullptr;
+        for (uint32_t j = lane; j < e.y; j += 64) {
+            const uint32_t x = body[e.x + j];
+            const uint32_t tok = x & Sym<S>::TM;
+            if (col) {
+                uint32_t* wp = col + (uint64_t)tok * W;
+                if (!(*wp & bit)) atomicOr(wp, bit);
+            }
+            if (j && !(x & Sym<S>::WS)) {
+                const uint32_t tp = body[e.x + j - 1] & Sym<S>::TM;
+                if (tp && tok) sig_set(ssig[wid], (tp << 16) | tok);
+            }
         }
     }
+    __syncthreads();
+    if (live && lane < (int)SP_SIGW) sig[(uint64_t)k * SP_SIGW + lane] = ssig[wid][lane];
 }
 
 // sparse → dense: sector counts, then a gather at the scanned offsets (one wave per sector)
@@ -1584,7 +1625,8 @@ struct gbpe_trainer {
     uint32_t* bits = nullptr;    // presence bitmap, rows = token ids, W words per row
     uint32_t* sig = nullptr;     // per-sector pair signatures (SP_SIGW words each)
     uint64_t sig_cap = 0;
-    uint64_t sp_age = 0;         // sparse merges since the filters were built
+    uint64_t sp_age = 0;         // sparse merges since the signatures were built
+    uint64_t sp_bits_age = 0;    // ... since the token bitmap was built
     uint64_t bits_cap = 0;       // words
     uint32_t W = 0;
     void* zbuf[2] = {nullptr, nullptr};
@@ -1595,6 +1637,11 @@ struct gbpe_trainer {
     DevState* h_zst = nullptr;   // pinned
     uint32_t* d_u32 = nullptr;   // small device scratch
     uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
+    uint64_t* wg_bytes = nullptr;   // bytes moved per k_body workgroup (each its own counter)
+    uint64_t wg_cap = 0;
+    double ms_sparse = 0, ms_dense = 0;   // GBPE_TRAIN_TIMING: merge passes (without selection / refresh) by mode
+    double ms_body = 0;          // GBPE_TRAIN_TIMING: k_body alone
+    uint64_t dense_bytes = 0;    // algorithmic stream bytes of the dense merges
     uint32_t g_refresh = 0;
     uint64_t sp_merges = 0, sp_sectors = 0, sp_zone = 0;
     uint32_t sp_enters = 0, sp_exits = 0;
@@ -1703,14 +1750,16 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));   // selection runs inside k_body (sel_inline)
     const uint32_t gb = g.body + (g.zone1 ? 1u : g.copy);
+    // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
-        hipLaunchKernelGGL((k_body<S, true>), dim3(gb), dim3(TPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
+        hipLaunchKernelGGL((k_body<S, true>), dim3(gb), dim3(BTPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
                            t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst,
-                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum);
+                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes);
     else
-        hipLaunchKernelGGL((k_body<S, false>), dim3(gb), dim3(TPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
+        hipLaunchKernelGGL((k_body<S, false>), dim3(gb), dim3(BTPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
                            t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst,
-                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum);
+                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes);
+    if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
     if (!g.zone1) {
         if (exact)
             hipLaunchKernelGGL((k_delta<S, true, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc,
@@ -1719,7 +1768,6 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
             hipLaunchKernelGGL((k_delta<S, false, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc,
                                t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta);
     }
-    if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
     if (!g.zone1) {
         if (exact)
             hipLaunchKernelGGL((k_compact<S, true, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
@@ -1775,16 +1823,18 @@ int sp_add_sectors(gbpe_trainer* t, uint32_t base, uint32_t len) {
     return GBPE_OK;
 }
 
-// (re)build the token bitmap and the pair signatures from the body sectors
+// (re)build the pair signatures (and, with `with_bits`, the token bitmap) from the
+// body sectors: stale entries make the filters looser, never wrong
 template <typename S>
-int sp_filters(gbpe_trainer* t) {
+int sp_filters(gbpe_trainer* t, bool with_bits) {
     hipStream_t s = t->ctx->stream;
-    TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
-    TR_HIP(t, hipMemsetAsync(t->sig, 0, t->sig_cap * 4, s));
+    if (with_bits) TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
     hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(t->nsec, TPB / 64)), dim3(TPB), 0, s,
-                       (const S*)t->buf[t->bcur], (const uint2*)t->sec, 0u, t->nsec, t->bits, t->W, t->sig);
+                       (const S*)t->buf[t->bcur], (const uint2*)t->sec, 0u, t->nsec, with_bits ? t->bits : nullptr, t->W,
+                       t->sig);
     GBPE_LAUNCH_CHECK(t->ctx);
     t->sp_age = 0;
+    if (with_bits) t->sp_bits_age = 0;
     return GBPE_OK;
 }
 
@@ -1835,9 +1885,13 @@ int sp_enter(gbpe_trainer* t) {
     rc = sp_add_sectors<S>(t, 0u, Zs);
     if (rc != GBPE_OK) return rc;
     t->sp_age = 0;
+    t->sp_bits_age = 0;
     t->sp_shrinks = 0;
     // zone buffers: the zone, and the stale source (previous stream, n_prev - Zs <= z + last_mc symbols)
-    const uint64_t zneed = (gbpe_div_up((uint64_t)z + t->last_mc + 1, TILE) + 2) * TILE;
+    // (>= the one-workgroup zone pass's full register window, which it loads unconditionally)
+    uint64_t zneed = (gbpe_div_up((uint64_t)z + t->last_mc + 1, TILE) + 2) * TILE;
+    const uint64_t zmin = (uint64_t)(t->u16 ? ZoneDim<uint16_t>::ZMAX : ZoneDim<uint32_t>::ZMAX) + TILE;
+    if (zneed < zmin) zneed = zmin;
     if (zneed > t->zcap) {
         for (int k = 0; k < 2; ++k) {
             hipFree(t->zbuf[k]);
@@ -1870,6 +1924,19 @@ int sp_enter(gbpe_trainer* t) {
     t->h_st->body_rm = 0;
     t->h_st->sp_abort = 0;
     TR_HIP(t, hipMemcpyAsync(&t->st->B, &t->h_st->B, 4 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    {   // one byte counter per k_body workgroup, kept across entries (summed by gbpe_trainer_stats_get)
+        const uint64_t need = gbpe_div_up(gbpe_div_up(cap, 32), SP_WPW) + 2;
+        if (need > t->wg_cap) {
+            uint64_t* nb = nullptr;
+            TR_HIP(t, hipMalloc(&nb, need * sizeof(uint64_t)));
+            TR_HIP(t, hipMemsetAsync(nb, 0, need * sizeof(uint64_t), s));
+            if (t->wg_bytes) TR_HIP(t, hipMemcpyAsync(nb, t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+            TR_HIP(t, hipStreamSynchronize(s));
+            hipFree(t->wg_bytes);
+            t->wg_bytes = nb;
+            t->wg_cap = need;
+        }
+    }
     // per-k_refresh-workgroup maxima the sparse merges select from (sel_inline)
     if (!t->part) TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
     hipLaunchKernelGGL(k_refresh<S>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
@@ -2153,8 +2220,9 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
         int rc = t->u16 ? sp_shrink<uint16_t>(t) : sp_shrink<uint32_t>(t);
         if (rc != GBPE_OK) return rc;
     }
-    if (t->sp && t->sp_age >= 4096) {
-        int rc = t->u16 ? sp_filters<uint16_t>(t) : sp_filters<uint32_t>(t);
+    if (t->sp && t->sp_age >= 4096) {   // signatures saturate faster than the token bitmap goes stale
+        const bool wb = t->sp_bits_age >= 16384;
+        int rc = t->u16 ? sp_filters<uint16_t>(t, wb) : sp_filters<uint32_t>(t, wb);
         if (rc != GBPE_OK) return rc;
     }
     // reset the per-step counter + budget (trainer.js:239)
@@ -2182,7 +2250,7 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
         const uint32_t zn = t->n - hs->B;   // zone length (it only shrinks within a step)
         const uint64_t zt = gbpe_div_up(zn, TILE);
         sg.body = (uint32_t)gbpe_div_up(gbpe_div_up(t->nsec, 32), SP_WPW);
-        sg.zone1 = zn <= ZMAX;
+        sg.zone1 = zn <= (t->u16 ? ZoneDim<uint16_t>::ZMAX : ZoneDim<uint32_t>::ZMAX);
         sg.copy = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u : grid_persistent(t->ctx, gbpe_div_up(zn / 5 + 1, TPB * 8), 1);
         sg.zdelta = (uint32_t)(zt ? zt : 1);
         sg.zcompact = (uint32_t)zt + ((t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
@@ -2281,6 +2349,8 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
             t->ms_other += c;
             t->ms_delta += d1;
             t->ms_compact += d2;
+            (sparse ? t->ms_sparse : t->ms_dense) += b;
+            if (sparse) t->ms_body += d1;
         }
         t->timed_merges += done;
     }
@@ -2289,6 +2359,7 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     for (uint32_t r = 0; r < done; ++r) {
         const uint64_t mc = t->h_log[r * 4 + 3];
         t->bytes_moved += (uint64_t)t->bps * (2 * N + (N - mc));
+        if (!sparse) t->dense_bytes += (uint64_t)t->bps * (2 * N + (N - mc));
         N -= mc;
         if (merges_out) memcpy(merges_out + 4 * r, t->h_log + 4 * r, 4 * sizeof(uint32_t));
     }
@@ -2308,6 +2379,7 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
         t->zcur ^= (int)(done & 1u);
         t->sp_merges += done;
         t->sp_age += done;
+        t->sp_bits_age += done;
         if (hs->sp_abort) {   // a merge outgrew the zone: it was not run; continue dense
             int rc = sp_exit_any(t);
             if (rc != GBPE_OK) return rc;
@@ -2348,6 +2420,16 @@ extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
     o->sparse_exits = t->sp_exits;
     o->sparse_sectors = t->sp_sectors;
     o->sparse_zone = t->sp_zone;
+    o->dense_bytes = t->dense_bytes;
+    o->ms_dense = t->ms_dense;
+    o->ms_sparse = t->ms_sparse;
+    o->ms_body = t->ms_body;
+    o->zone_bytes = t->h_st->sp_bytes;
+    if (t->wg_bytes && t->wg_cap) {   // the per-workgroup counters of k_body (and its zone workgroup)
+        std::vector<uint64_t> h(t->wg_cap);
+        if (hipMemcpy(h.data(), t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess)
+            for (uint64_t v : h) o->body_bytes += v;
+    }
     return GBPE_OK;
 }
 
@@ -2429,6 +2511,7 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->zst);
     hipFree(t->d_u32);
     hipFree(t->part);
+    hipFree(t->wg_bytes);
     if (t->h_zst) hipHostFree(t->h_zst);
     if (t->graph_exec) hipGraphExecDestroy(t->graph_exec);
     hipFree(t->d_clog);

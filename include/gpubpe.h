@@ -162,6 +162,14 @@ typedef struct gbpe_trainer_stats {
     uint32_t sparse_exits;        /* sparse -> dense re-layouts (export, table rebuild, zone too small) */
     uint64_t sparse_sectors;      /* sectors of the last sparse layout */
     uint64_t sparse_zone;         /* zone length at the last sparse entry */
+    uint64_t body_bytes;          /* bytes k_body actually moved: candidate extents + signature words, sector
+                                     symbols read and rewritten, the single-workgroup zone pass (pair-table
+                                     traffic excluded) */
+    uint64_t zone_bytes;          /* bytes of the multi-tile zone passes (zone k_delta + k_compact + window copy) */
+    uint64_t dense_bytes;         /* s*(2*N_i + N_{i+1}) summed over the dense merges only */
+    double   ms_dense;            /* GBPE_TRAIN_TIMING: merge-pass device ms of the dense merges (k_delta + k_compact) */
+    double   ms_sparse;           /* GBPE_TRAIN_TIMING: merge-pass device ms of the sparse merges (k_body + zone passes) */
+    double   ms_body;             /* GBPE_TRAIN_TIMING: k_body alone */
 } gbpe_trainer_stats;
 int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* out);
 /* Current symbol stream in the reference u32 layout (bit16 = word start). */
