@@ -229,6 +229,155 @@ __global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v3(const uint8_t* __rest
     counts[chunk] = cnt;
 }
 
+// Interleaved walk: each lane walks ILP chunks in lock step, so every loop trip
+// has ILP independent record loads in flight instead of one.  Per chunk the
+// semantics and the output are exactly k_trie_walk_v3's.  Measured slower than
+// v3 on C3 (82 VGPRs: occupancy 5 instead of 8, and twice the divergent paths
+// per wave), so it is opt-in (GBPE_ENCODE_ILP=2).
+template <typename T>
+struct WalkLane {
+    uint64_t c0;
+    uint32_t ce, cb, cnt, pos, wp, lmp, st, base, lmt, first;
+    uint4 win, acc;
+    bool need_start;
+    T* out;
+};
+
+template <typename T>
+__device__ __forceinline__ uint32_t wl_byte(WalkLane<T>& L, const uint8_t* __restrict__ in, uint64_t n, uint32_t p) {
+    const uint32_t b = p & ~15u;
+    if (b != L.cb) {
+        L.cb = b;
+        L.win = load_win(in, n, L.c0 + b);
+    }
+    return win_byte(L.win, p & 15u);
+}
+
+template <typename T>
+__device__ __forceinline__ void wl_emit(WalkLane<T>& L, uint32_t tok) {
+    constexpr uint32_t PER = 16 / sizeof(T);
+    vec_put<T>(L.acc, L.cnt % PER, tok);
+    if (++L.cnt % PER == 0) {
+        *reinterpret_cast<uint4*>(L.out + L.cnt - PER) = L.acc;
+        L.acc = make_uint4(0, 0, 0, 0);
+    }
+}
+
+// token starts (LDS only) until the walk needs a record: returns its index, or
+// INV when the chunk is done
+template <typename T>
+__device__ __forceinline__ uint32_t wl_prepare(WalkLane<T>& L, const uint8_t* __restrict__ in, uint64_t n,
+                                               const uint2* lut, uint32_t root_base) {
+    while (true) {
+        while (L.need_start && L.pos < L.ce) {
+            L.first = wl_byte(L, in, n, L.pos);
+            const uint2 e = lut[L.first];
+            if (rec_check(e) != 0u) {   // no token starts with this byte: emit it raw (tokenize.wgsl:169-171)
+                wl_emit(L, L.first);
+                ++L.pos;
+                continue;
+            }
+            const uint32_t tid = rec_tid(e);
+            if (rec_base(e) == 0u) {    // one-byte leaf token
+                wl_emit(L, tid != TID_NONE ? tid : L.first);
+                ++L.pos;
+                continue;
+            }
+            L.st = root_base + L.first;
+            L.base = rec_base(e);
+            L.lmt = tid;
+            L.lmp = L.pos + 1;
+            L.wp = L.pos + 1;
+            L.need_start = false;
+        }
+        if (L.need_start) return INV;   // chunk done
+        if (L.wp < L.ce) return L.base + wl_byte(L, in, n, L.wp);
+        const bool hit = L.lmt != TID_NONE;   // the chunk ends inside a match: emit it, restart
+        wl_emit(L, hit ? L.lmt : L.first);
+        L.pos = hit ? L.lmp : L.pos + 1;
+        L.need_start = true;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void wl_consume(WalkLane<T>& L, uint2 r, uint32_t t) {
+    bool adv = false, leaf = false;
+    if (rec_check(r) == L.st) {
+        adv = true;
+        L.st = t;
+        L.base = rec_base(r);
+        ++L.wp;
+        const uint32_t tid = rec_tid(r);
+        if (tid != TID_NONE) {
+            L.lmt = tid;
+            L.lmp = L.wp;
+        }
+        leaf = L.base == 0u;
+    }
+    if (!adv || leaf) {   // the longest match ends: emit it (or the raw first byte), restart after it
+        const bool hit = L.lmt != TID_NONE;
+        wl_emit(L, hit ? L.lmt : L.first);
+        L.pos = hit ? L.lmp : L.pos + 1;
+        L.need_start = true;
+    }
+}
+
+template <typename T, int ILP>
+__global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v4(const uint8_t* __restrict__ in, uint64_t n, uint32_t cs,
+                                                           const uint2* __restrict__ rec, uint32_t nrec,
+                                                           uint32_t root_base, T* __restrict__ scratch,
+                                                           uint32_t* __restrict__ counts, uint64_t nchunks) {
+    constexpr uint32_t PER = 16 / sizeof(T);
+    __shared__ uint2 lut[256];
+    {
+        const uint32_t t = root_base + threadIdx.x;
+        lut[threadIdx.x] = t < nrec ? rec[t] : make_uint2(0x3FFFFFu, 0u);
+    }
+    __syncthreads();
+    const uint64_t g = (uint64_t)blockIdx.x * WALK_TPB + threadIdx.x;
+    const uint64_t half = (nchunks + ILP - 1) / ILP;   // lane g walks chunks g, g + half, ...
+    if (g >= half) return;
+    WalkLane<T> L[ILP];
+    uint32_t tp[ILP];
+#pragma unroll
+    for (int j = 0; j < ILP; ++j) {
+        const uint64_t chunk = g + (uint64_t)j * half;
+        const bool live = chunk < nchunks;
+        L[j].c0 = chunk * cs;
+        L[j].ce = live ? (uint32_t)(min(L[j].c0 + cs, n) - L[j].c0) : 0u;
+        L[j].cb = ~0u;
+        L[j].cnt = L[j].pos = L[j].wp = L[j].lmp = L[j].st = L[j].base = L[j].first = 0;
+        L[j].lmt = TID_NONE;
+        L[j].win = L[j].acc = make_uint4(0, 0, 0, 0);
+        L[j].need_start = true;
+        L[j].out = scratch + (live ? L[j].c0 : 0);
+        tp[j] = wl_prepare(L[j], in, n, lut, root_base);
+    }
+    while (true) {
+        bool any = false;
+        uint2 r[ILP];
+#pragma unroll
+        for (int j = 0; j < ILP; ++j) {   // all of this trip's record loads first
+            any |= tp[j] != INV;
+            r[j] = (tp[j] != INV && tp[j] < nrec) ? rec[tp[j]] : make_uint2(0x3FFFFFu, 0u);
+        }
+        if (!any) break;
+#pragma unroll
+        for (int j = 0; j < ILP; ++j) {
+            if (tp[j] == INV) continue;
+            wl_consume(L[j], r[j], tp[j]);
+            tp[j] = wl_prepare(L[j], in, n, lut, root_base);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < ILP; ++j) {
+        const uint64_t chunk = g + (uint64_t)j * half;
+        if (chunk >= nchunks) continue;
+        if (L[j].cnt % PER) *reinterpret_cast<uint4*>(L[j].out + (L[j].cnt / PER) * PER) = L[j].acc;
+        counts[chunk] = L[j].cnt;
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_chunk_compact(const T* __restrict__ scratch, const uint32_t* __restrict__ counts,
                                                        const uint32_t* __restrict__ local,
@@ -429,7 +578,17 @@ int encode_device_impl(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* d_in, uint64
     static const bool force_nested = getenv("GBPE_ENCODE_WALK") && std::string(getenv("GBPE_ENCODE_WALK")) == "nested";
     const bool v3 = !force_nested && (cs % 8u) == 0u && tr->rec2;
     const uint32_t nrec2 = tr->nrec + 256;
-    if (v3) {
+    // GBPE_ENCODE_ILP=2: the interleaved walk (measured slower on C3: 7.0 vs 5.1 ms, occupancy 5 vs 8)
+    static const int ilp = getenv("GBPE_ENCODE_ILP") ? atoi(getenv("GBPE_ENCODE_ILP")) : 1;
+    if (v3 && ilp >= 2) {
+        const uint32_t g2 = (uint32_t)gbpe_div_up(gbpe_div_up(nchunks, 2), WALK_TPB);
+        if (narrow)
+            hipLaunchKernelGGL((k_trie_walk_v4<uint16_t, 2>), dim3(g2), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2,
+                               nrec2, tr->root_base, (uint16_t*)ctx->enc_scratch, counts, nchunks);
+        else
+            hipLaunchKernelGGL((k_trie_walk_v4<uint32_t, 2>), dim3(g2), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2,
+                               nrec2, tr->root_base, (uint32_t*)ctx->enc_scratch, counts, nchunks);
+    } else if (v3) {
         if (narrow)
             hipLaunchKernelGGL(k_trie_walk_v3<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
                                tr->root_base, (uint16_t*)ctx->enc_scratch, counts, nchunks);
