@@ -101,6 +101,9 @@ struct DevState {
     uint32_t rticket;      // k_refresh workgroups done (fused selection)
     uint32_t sel_round;    // sector-sparse: round + 1 of the merge k_body selected
     uint64_t sp_bytes;     // sector-sparse: bytes moved by the multi-tile zone passes (k_refresh adds them)
+    uint32_t zlast;        // sector-sparse: zone length of the rank that holds the zone (global knowledge)
+    uint32_t ln_last;      // sharded: the last rank's local length after the last merge (from the records)
+    uint32_t is_last;      // sector-sparse: this rank holds the zone (single GPU: always)
     uint32_t cand;         // candidate sectors of this merge (trace)
     uint32_t hitsec;       // sectors with a site (trace)
 };
@@ -108,7 +111,9 @@ static_assert(sizeof(DevState) <= 256, "state");
 
 // exchange-record header words of sharded training (gpubpe/sharded.py mirrors them)
 enum : uint32_t {
-    H_ACTIVE = 0, H_L, H_KEPT, H_M, H_W, H_LASTSYM, H_HASLAST, H_SURV, H_LN, H_MC, H_A, H_B, H_ID, H_DFULL, HDR = 16
+    H_ACTIVE = 0, H_L, H_KEPT, H_M, H_W, H_LASTSYM, H_HASLAST, H_SURV, H_LN, H_MC, H_A, H_B, H_ID, H_DFULL,
+    H_ZN = 14,             // sector-sparse records: the zone length after the merge (last rank), its window m
+    H_ZM = 15, HDR = 16
 };
 
 enum : uint32_t {
@@ -360,7 +365,8 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
                 st->body_rm = 0u;
                 const uint32_t zold = zst->n;
                 zst->n = st->n - st->B;
-                if (!zst->valid_total)   // multi-tile zone: k_delta + k_compact stream it twice, plus the window copy
+                if (!st->sharded) st->zlast = zst->n;   // sharded: from the records (k_shard_apply)
+                if (!zst->valid_total && st->is_last)   // multi-tile zone: k_delta + k_compact stream it twice, plus the window copy
                     st->sp_bytes += (uint64_t)sizeof(S) * (2ull * zold + zst->n + 2ull * st->mc);
                 if (zst->valid_total && zst->valid_total != zst->n + 1u) atomicOr(&st->err, ERR_COUNT_MISMATCH);
             } else if (st->sharded) {   // commit the new global layout computed by k_shard_recv
@@ -1163,8 +1169,8 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
 #pragma unroll
         for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
     }
-    if (!EXACT) {
-        const uint64_t src0 = (uint64_t)st->n - 2ull * mc - st->Bp;
+    if (!EXACT) {   // window source: global n - 2mc in the previous stream (sharded: it began at poff, now off)
+        const uint64_t src0 = (uint64_t)st->n + st->off - st->poff - 2ull * mc - st->Bp;
         for (uint32_t u = t; u < mc; u += BTPB) L.wb[u] = zo[src0 + u];
     }
     lds_clear(lt);
@@ -1264,13 +1270,26 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
 // it (log, table slot zeroed, state for k_refresh and the zone kernels).  The
 // step counters move on in k_refresh (finish == 2), so nothing a workgroup reads
 // here changes under it.  Saves the k_select launch per merge.
+// Sharded (cap_list != 0): the zone sits on the last rank only, so the zone checks
+// use st->zlast, the zone length every rank learned from the last exchange; a
+// merge whose count could overflow the exchange record stalls here, before any
+// sector is touched, on every rank alike (the count is global).
+struct SelShard {
+    uint32_t cap_list = 0;   // 0 = single GPU
+    uint32_t zmax = 0;       // the one-workgroup zone limit (sharded zones never run multi-tile)
+    uint32_t* nlog = nullptr;
+    uint32_t* rec = nullptr; // this rank's exchange record (its list length restarts at 0)
+};
+
 __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
                            uint32_t round, bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
-                           uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc) {
+                           uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc,
+                           const SelShard sh = SelShard()) {
     __shared__ uint64_t s_red[BTPB / 64];
     __shared__ uint32_t s_ok;
     const int t = threadIdx.x;
-    if (t == 0) s_ok = (round < st->budget && st->merges_done == round && !st->stop && !st->sp_abort) ? 1u : 0u;
+    if (t == 0)
+        s_ok = (round < st->budget && st->merges_done == round && !st->stop && !st->sp_abort && !st->stall) ? 1u : 0u;
     __syncthreads();
     if (!s_ok) return false;
     uint64_t best = 0;
@@ -1293,9 +1312,13 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     b = pid & 0xFFFFu;
     nw = st->next_id;
     const bool stop = mc < 2u || nw > 0xFFFFu;                                          // train.wgsl:345-348
-    const bool bad = !stop && !exact && (uint64_t)st->n < 2ull * mc + st->Bp;            // cannot happen
-    const bool abort = !stop && !bad && !exact && (uint64_t)zst->n < 5ull * mc + 2u;    // zone too small
-    const bool go = !stop && !bad && !abort;
+    const bool bad = !stop && !exact && st->is_last &&
+                     (uint64_t)st->n + st->off - st->poff < 2ull * mc + st->Bp;   // cannot happen
+    const bool abort = !stop && !bad && !exact &&
+                       ((uint64_t)st->zlast < 5ull * mc + 2u || (sh.zmax && st->zlast > sh.zmax));   // zone misfit
+    const uint32_t need = 6u * mc + 64u;   // distinct deltas of one merge <= 4 per site + tail + window
+    const bool stall = !stop && !bad && !abort && sh.cap_list && need > sh.cap_list;
+    const bool go = !stop && !bad && !abort && !stall;
     if (blockIdx.x == 0) {
         if (t == 0) {
             if (stop) {
@@ -1305,7 +1328,18 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
                 st->stop = 1u;
             } else if (abort) {
                 st->sp_abort = 1u;
+            } else if (stall) {   // the host grows the records and redoes this merge
+                st->stall = 1u;
+                st->need_l = need;
+                st->need_w = 0u;
             } else {
+                if (sh.nlog) sh.nlog[round] = st->n;
+                if (sh.rec) {
+                    sh.rec[H_L] = 0u;
+                    st->dcount = 0u;
+                    st->dused = 0u;
+                    st->dfull = 0u;
+                }
                 const uint32_t idx = table_find(tb, pid);
                 if (idx == 0xFFFFFFFFu) {
                     atomicOr(&st->err, ERR_PAIR_MISSING);
@@ -1357,7 +1391,8 @@ __global__ __launch_bounds__(BTPB) void k_body(DevState* st, uint32_t round, S* 
                                               Table tb, uint32_t nbody, const S* __restrict__ zoth, S* __restrict__ wtmp,
                                               uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
-                                              uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes) {
+                                              uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
+                                              Table dtb, SelShard sh) {
     __shared__ LdsTab<LTAB_T> lt;
     __shared__ uint32_t s_tok[SP_WPW * 32], s_list[SP_WPW * 32];
     __shared__ uint2 s_ext[SP_WPW * 32];
@@ -1366,13 +1401,14 @@ __global__ __launch_bounds__(BTPB) void k_body(DevState* st, uint32_t round, S* 
     __shared__ ZoneLds<S> zl;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     uint32_t a, b, nw, mc;
-    if (!sel_inline(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc)) return;
+    if (!sel_inline(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, sh)) return;
+    // deltas go to the replica (single GPU) or to the per-merge delta table (sharded)
     if (zone1 && blockIdx.x == nbody) {
-        zone_one<S, EXACT>(st, zst, zcur, (S*)zoth, zl, lt, tb, a, b, nw, mc, wg_bytes + nbody);
+        zone_one<S, EXACT>(st, zst, zcur, (S*)zoth, zl, lt, dtb, a, b, nw, mc, wg_bytes + nbody);
         return;
     }
     if (blockIdx.x >= nbody) {
-        const uint64_t src0 = (uint64_t)st->n - 2ull * mc - st->Bp;
+        const uint64_t src0 = (uint64_t)st->n + st->off - st->poff - 2ull * mc - st->Bp;
         const uint64_t stride = (uint64_t)(gridDim.x - nbody) * BTPB;
         for (uint64_t u = (uint64_t)(blockIdx.x - nbody) * BTPB + t; u < mc; u += stride) wtmp[u] = zoth[src0 + u];
         return;
@@ -1421,7 +1457,7 @@ __global__ __launch_bounds__(BTPB) void k_body(DevState* st, uint32_t round, S* 
         const uint32_t sct = s_list[j];
         const uint2 e = s_ext[j];
         uint32_t out = 0;
-        const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, tb, st, sig + (uint64_t)sct * SP_SIGW, out);
+        const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, dtb, st, sig + (uint64_t)sct * SP_SIGW, out);
         moved += (uint64_t)sizeof(S) * (e.y + (r ? out : 0u));
         if (r) {
             removed += r;
@@ -1432,7 +1468,7 @@ __global__ __launch_bounds__(BTPB) void k_body(DevState* st, uint32_t round, S* 
             }
         }
     }
-    lds_flush(lt, tb, st);
+    lds_flush(lt, dtb, st);
     if (lane == 0) {
         s_rm[wid] = removed;
         s_mv[wid] = moved;
@@ -1754,11 +1790,13 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     if (exact)
         hipLaunchKernelGGL((k_body<S, true>), dim3(gb), dim3(BTPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
                            t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst,
-                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes);
+                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes,
+                           t->tb, SelShard());
     else
         hipLaunchKernelGGL((k_body<S, false>), dim3(gb), dim3(BTPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
                            t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst,
-                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes);
+                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes,
+                           t->tb, SelShard());
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
     if (!g.zone1) {
         if (exact)
@@ -1842,20 +1880,22 @@ int sp_filters(gbpe_trainer* t, bool with_bits) {
 // start at or before n - zt (zt = 10 * last_mc + 64 >= 5 * the next merge's
 // count); the dense stale buffer's tail becomes the zone's stale buffer.
 template <typename S>
-int sp_enter(gbpe_trainer* t) {
+int sp_enter(gbpe_trainer* t, bool with_zone = true) {
     hipStream_t s = t->ctx->stream;
     const uint32_t n = t->n;
     const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
-    if (zt + 2 >= n) return GBPE_OK;
     const S* cur = (const S*)t->buf[t->cur];
     const S* stale = (const S*)t->buf[t->cur ^ 1];
     if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
-    hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, cur, (uint32_t)(n - zt), t->d_u32);
-    GBPE_LAUNCH_CHECK(t->ctx);
-    uint32_t Zs = 0;
-    TR_HIP(t, hipMemcpyAsync(&Zs, t->d_u32, 4, hipMemcpyDeviceToHost, s));
-    TR_HIP(t, hipStreamSynchronize(s));
-    if (Zs < t->sp_secw) return GBPE_OK;   // the whole stream is one long word (or tiny): stay dense
+    uint32_t Zs = n;   // sharded ranks before the last: all body, no zone
+    if (with_zone) {
+        if (zt + 2 >= n) return GBPE_OK;
+        hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, cur, (uint32_t)(n - zt), t->d_u32);
+        GBPE_LAUNCH_CHECK(t->ctx);
+        TR_HIP(t, hipMemcpyAsync(&Zs, t->d_u32, 4, hipMemcpyDeviceToHost, s));
+        TR_HIP(t, hipStreamSynchronize(s));
+        if (Zs < t->sp_secw) return GBPE_OK;   // the whole stream is one long word (or tiny): stay dense
+    }
     const uint32_t z = n - Zs;
     // capacities for every sector the body can ever hold: windows over [0, n) plus
     // one partial window per zone shrink (at most SP_SHRINKS per entry)
@@ -1906,11 +1946,13 @@ int sp_enter(gbpe_trainer* t) {
         t->zcap = zneed;
     }
     for (int k = 0; k < 2; ++k) TR_HIP(t, hipMemsetAsync(t->zbuf[k], 0, t->zcap * t->bps, s));
-    TR_HIP(t, hipMemcpyAsync(t->zbuf[0], cur + Zs, (uint64_t)z * t->bps, hipMemcpyDeviceToDevice, s));
-    uint64_t sl = (uint64_t)z + t->last_mc;
-    if (Zs + sl > t->cap_syms) sl = t->cap_syms - Zs;
-    if (sl > t->zcap) sl = t->zcap;
-    TR_HIP(t, hipMemcpyAsync(t->zbuf[1], stale + Zs, sl * t->bps, hipMemcpyDeviceToDevice, s));
+    if (z) {
+        TR_HIP(t, hipMemcpyAsync(t->zbuf[0], cur + Zs, (uint64_t)z * t->bps, hipMemcpyDeviceToDevice, s));
+        uint64_t sl = (uint64_t)z + t->last_mc;
+        if (Zs + sl > t->cap_syms) sl = t->cap_syms - Zs;
+        if (sl > t->zcap) sl = t->zcap;
+        TR_HIP(t, hipMemcpyAsync(t->zbuf[1], stale + Zs, sl * t->bps, hipMemcpyDeviceToDevice, s));
+    }
     // states
     if (!t->zst) {
         TR_HIP(t, hipMalloc(&t->zst, sizeof(DevState)));
@@ -1924,6 +1966,12 @@ int sp_enter(gbpe_trainer* t) {
     t->h_st->body_rm = 0;
     t->h_st->sp_abort = 0;
     TR_HIP(t, hipMemcpyAsync(&t->st->B, &t->h_st->B, 4 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    // every rank checks the zone against the same length: the zone rank's target
+    // until the first exchange reports the real one (single GPU: the real one)
+    t->h_st->zlast = t->sharded ? (uint32_t)zt : z;
+    t->h_st->is_last = z ? 1u : 0u;
+    TR_HIP(t, hipMemcpyAsync(&t->st->zlast, &t->h_st->zlast, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(&t->st->is_last, &t->h_st->is_last, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     {   // one byte counter per k_body workgroup, kept across entries (summed by gbpe_trainer_stats_get)
         const uint64_t need = gbpe_div_up(gbpe_div_up(cap, 32), SP_WPW) + 2;
         if (need > t->wg_cap) {
@@ -2619,6 +2667,69 @@ __device__ __forceinline__ uint32_t from_canon(uint32_t x) {
     return (x & 0xFFFFu) | ((x & 0x10000u) ? Sym<S>::WS : 0u);
 }
 
+// list role of the send kernels: the per-merge delta table's dirty blocks become
+// the record's {pid, delta} list (clearing what they read); each block adds its
+// entries to rec[H_L]
+__device__ void shard_list_role(DevState* st, Table dt, uint32_t* __restrict__ rec, uint32_t cap_list, uint32_t nlb) {
+    __shared__ uint64_t s_dmask;
+    __shared__ uint32_t wcnt[TPB / 64], s_base;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t per = (dt.nblk + nlb - 1) / nlb;
+    const uint32_t b0 = blockIdx.x * per;
+    if (threadIdx.x < 64) {
+        const uint32_t blk = b0 + threadIdx.x;
+        const bool d = threadIdx.x < per && blk < dt.nblk && dt.dirty[blk];
+        const unsigned long long m = __ballot(d);
+        if (threadIdx.x == 0) s_dmask = m;
+    }
+    __syncthreads();
+    uint64_t dm = s_dmask;
+    constexpr int NV = (1 << BLK_LOG2) / 2 / TPB;
+    while (dm) {
+        const uint32_t blk = b0 + (uint32_t)(__ffsll((long long)dm) - 1);
+        dm &= dm - 1;
+        uint4* sl = reinterpret_cast<uint4*>(dt.slots + ((uint64_t)blk << BLK_LOG2));
+        uint4 e[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) e[k] = sl[threadIdx.x + k * TPB];
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) c += (e[k].x && e[k].y) + (e[k].z && e[k].w);
+        uint32_t incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wcnt[wid] = incl;
+        __syncthreads();
+        uint32_t pre = incl - c, tot = 0;
+        for (int w = 0; w < TPB / 64; ++w) {
+            pre += w < wid ? wcnt[w] : 0u;
+            tot += wcnt[w];
+        }
+        if (threadIdx.x == 0) {
+            s_base = tot ? atomicAdd(&st->dcount, tot) : 0u;
+            if (tot) atomicAdd(&rec[H_L], tot);
+            dt.dirty[blk] = 0u;
+        }
+        __syncthreads();
+        uint32_t o = s_base + pre;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            if (e[k].x && e[k].y) {
+                if (o < cap_list) { rec[HDR + 2 * o] = e[k].x; rec[HDR + 2 * o + 1] = e[k].y; }
+                ++o;
+            }
+            if (e[k].z && e[k].w) {
+                if (o < cap_list) { rec[HDR + 2 * o] = e[k].z; rec[HDR + 2 * o + 1] = e[k].w; }
+                ++o;
+            }
+            if (e[k].x || e[k].z) sl[threadIdx.x + k * TPB] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        __syncthreads();
+    }
+}
+
 // Phase-1 send kernel, three block roles:
 //   [0, nlb)        delta table (dirty blocks only) → record list {pid, delta},
 //                   clearing what they read; each adds its count to rec[H_L]
@@ -2629,68 +2740,13 @@ __global__ __launch_bounds__(TPB) void k_shard_send(DevState* st, uint32_t round
                                                     const S* __restrict__ oth, const uint32_t* __restrict__ hitmask,
                                                     const uint32_t* __restrict__ grpsum, uint32_t* __restrict__ rec,
                                                     uint32_t cap_list, uint32_t cap_win, uint32_t nlb) {
-    __shared__ uint64_t s_dmask;
-    __shared__ uint32_t wcnt[TPB / 64], s_base;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (!merge_active(st, round)) {
         if (blockIdx.x == nlb && threadIdx.x < HDR) rec[threadIdx.x] = 0u;   // inactive round: ACTIVE = 0
         return;
     }
     if (blockIdx.x < nlb) {   // ── list role ──
-        const uint32_t per = (dt.nblk + nlb - 1) / nlb;
-        const uint32_t b0 = blockIdx.x * per;
-        if (threadIdx.x < 64) {
-            const uint32_t blk = b0 + threadIdx.x;
-            const bool d = threadIdx.x < per && blk < dt.nblk && dt.dirty[blk];
-            const unsigned long long m = __ballot(d);
-            if (threadIdx.x == 0) s_dmask = m;
-        }
-        __syncthreads();
-        uint64_t dm = s_dmask;
-        constexpr int NV = (1 << BLK_LOG2) / 2 / TPB;
-        while (dm) {
-            const uint32_t blk = b0 + (uint32_t)(__ffsll((long long)dm) - 1);
-            dm &= dm - 1;
-            uint4* sl = reinterpret_cast<uint4*>(dt.slots + ((uint64_t)blk << BLK_LOG2));
-            uint4 e[NV];
-#pragma unroll
-            for (int k = 0; k < NV; ++k) e[k] = sl[threadIdx.x + k * TPB];
-            uint32_t c = 0;
-#pragma unroll
-            for (int k = 0; k < NV; ++k) c += (e[k].x && e[k].y) + (e[k].z && e[k].w);
-            uint32_t incl = c;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t v = __shfl_up(incl, o);
-                if (lane >= o) incl += v;
-            }
-            if (lane == 63) wcnt[wid] = incl;
-            __syncthreads();
-            uint32_t pre = incl - c, tot = 0;
-            for (int w = 0; w < TPB / 64; ++w) {
-                pre += w < wid ? wcnt[w] : 0u;
-                tot += wcnt[w];
-            }
-            if (threadIdx.x == 0) {
-                s_base = tot ? atomicAdd(&st->dcount, tot) : 0u;
-                if (tot) atomicAdd(&rec[H_L], tot);
-                dt.dirty[blk] = 0u;
-            }
-            __syncthreads();
-            uint32_t o = s_base + pre;
-#pragma unroll
-            for (int k = 0; k < NV; ++k) {
-                if (e[k].x && e[k].y) {
-                    if (o < cap_list) { rec[HDR + 2 * o] = e[k].x; rec[HDR + 2 * o + 1] = e[k].y; }
-                    ++o;
-                }
-                if (e[k].z && e[k].w) {
-                    if (o < cap_list) { rec[HDR + 2 * o] = e[k].z; rec[HDR + 2 * o + 1] = e[k].w; }
-                    ++o;
-                }
-                if (e[k].x || e[k].z) sl[threadIdx.x + k * TPB] = make_uint4(0u, 0u, 0u, 0u);
-            }
-            __syncthreads();
-        }
+        shard_list_role(st, dt, rec, cap_list, nlb);
         return;
     }
     const bool exact = (st->sharded & 2u) != 0;
@@ -2889,6 +2945,7 @@ __global__ __launch_bounds__(TPB) void k_shard_recv(DevState* st, uint32_t round
         st->peak_w = max(st->peak_w, v.max_w);
         st->nl_next = mine;
         st->off_next = before;
+        st->ln_last = (uint32_t)((uint64_t)v.K[R - 1] + (R - 1 == v.owner ? v.m : 0u));
     }
     // every rank's count deltas into the replica
     const uint32_t total = v.lpre[R];
@@ -2917,6 +2974,96 @@ __global__ __launch_bounds__(TPB) void k_shard_recv(DevState* st, uint32_t round
         if (!(x & 0x10000u) && t0 && t1) lds_add(lt, tb, st, (t0 << 16) | t1, 1u);
     }
     lds_flush(lt, tb, st);
+}
+
+// ── sector-sparse sharded loop ──
+// Phase 1 is k_body on the local sectors (deltas into the per-merge delta table;
+// the last rank also runs the zone, which carries the global stream's stale
+// window) followed by k_shard_send_sp: the delta list and a header with the
+// local length after the merge.  Phase 2, after the all-gather, is
+// k_shard_apply_sp (every rank's deltas into the replica, the new global
+// layout) and k_refresh (finish == 2).  Nothing crosses ranks but deltas and
+// lengths: the zone rank is the only one whose pairs depend on the quirk.
+__device__ __forceinline__ bool sp_round_active(const DevState* st, uint32_t round) {
+    return !st->stop && !st->sp_abort && !st->stall && st->sel_round == round + 1u;
+}
+
+__global__ __launch_bounds__(TPB) void k_shard_send_sp(DevState* st, DevState* zst, uint32_t round, Table dt,
+                                                       uint32_t* __restrict__ rec, uint32_t cap_list, uint32_t nlb) {
+    if (!sp_round_active(st, round)) {
+        if (blockIdx.x == nlb && threadIdx.x < HDR) rec[threadIdx.x] = 0u;   // inactive round: ACTIVE = 0
+        return;
+    }
+    if (blockIdx.x < nlb) {
+        shard_list_role(st, dt, rec, cap_list, nlb);
+        return;
+    }
+    if (threadIdx.x != 0) return;
+    const uint32_t zn = st->is_last && zst->valid_total ? zst->valid_total - 1u : 0u;   // zone survivors
+    const uint32_t ln = (st->B - st->body_rm) + zn;   // local length after the merge
+    st->new_n = ln;
+    rec[H_ACTIVE] = 1u;
+    rec[H_KEPT] = ln;
+    rec[H_M] = 0u;
+    rec[H_W] = 0u;
+    rec[H_LASTSYM] = 0u;
+    rec[H_HASLAST] = 0u;
+    rec[H_SURV] = ln;
+    rec[H_LN] = ln;
+    rec[H_MC] = st->mc;
+    rec[H_A] = st->a;
+    rec[H_B] = st->b;
+    rec[H_ID] = st->nw;
+    rec[H_DFULL] = st->dfull;
+    rec[H_ZN] = st->is_last ? zn : 0u;
+    rec[H_ZM] = st->is_last ? zst->m : 0u;
+}
+
+__global__ __launch_bounds__(TPB) void k_shard_apply_sp(DevState* st, uint32_t round, const uint32_t* __restrict__ recv,
+                                                        uint32_t R, uint32_t cap_list, uint32_t cap_win, Table tb,
+                                                        uint32_t nab) {
+    __shared__ ShardView v;
+    if (!sp_round_active(st, round)) return;
+    const uint32_t rw = HDR + 2 * cap_list + cap_win;
+    shard_view(st, recv, R, rw, cap_list, cap_win, v);
+    if (v.bad || v.overflow) {   // records disagree, or a list did not fit (k_body's bound should prevent it)
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            atomicOr(&st->err, v.bad ? ERR_SHARD_RECORD : ERR_SHARD_CAPACITY);
+            st->stop = 1u;
+        }
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // new global layout (rank order)
+        uint64_t tot = 0, before = 0;
+        uint32_t mine = 0, zm = 0;
+        for (uint32_t q = 0; q < R; ++q) {
+            const uint32_t nl = recv[(uint64_t)q * rw + H_LN];
+            if (q < st->rank) before += nl;
+            if (q == st->rank) mine = nl;
+            tot += nl;
+            zm += recv[(uint64_t)q * rw + H_ZM];
+        }
+        if (tot != st->gn - st->mc || mine != st->new_n) {
+            atomicOr(&st->err, ERR_SHARD_LAYOUT);
+            st->need_l = (uint32_t)tot;
+            st->need_w = mine;
+        }
+        st->m_glob = zm;
+        st->peak_l = max(st->peak_l, max(v.max_l, 6u * st->mc + 64u));   // what k_body's stall bound asks for
+        st->poff = st->off;
+        st->pln = st->n;
+        st->off = before;
+        st->gn = tot;
+        st->ln_last = recv[(uint64_t)(R - 1) * rw + H_LN];
+        st->zlast = recv[(uint64_t)(R - 1) * rw + H_ZN];
+    }
+    const uint32_t total = v.lpre[R];   // every rank's count deltas into the replica
+    for (uint32_t e = blockIdx.x * TPB + threadIdx.x; e < total; e += nab * TPB) {
+        uint32_t q = 0;
+        while (q + 1 < R && v.lpre[q + 1] <= e) ++q;
+        const uint32_t* l = recv + (uint64_t)q * rw + HDR + 2 * (e - v.lpre[q]);
+        table_add(tb, st, l[0], l[1]);
+    }
 }
 
 __global__ void k_add_list(DevState* st, Table tb, const uint2* __restrict__ list, uint64_t n) {
@@ -3090,11 +3237,38 @@ extern "C" int gbpe_shard_step_begin(gbpe_trainer* t, uint32_t max_merges) {
     t->step_k = t->stop ? 0u : k;
     if (t->step_k == 0) return GBPE_OK;
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
-    if ((uint64_t)t->h_st->used * 2 > slots) {
-        int rc = shard_rehash(t);
+    if ((uint64_t)t->h_st->used * 2 > slots) {   // identical on every rank (replica tables)
+        int rc = sp_exit_any(t);
+        if (rc == GBPE_OK) rc = shard_rehash(t);
         if (rc != GBPE_OK) return rc;
     }
     DevState* hs = t->h_st;
+    // sector-sparse loop: decided from global state only, so every rank
+    // enters together; the last rank holds the zone, which must fit one workgroup
+    if (t->sp_cooldown) {
+        --t->sp_cooldown;
+    } else if (!t->sp && !(t->flags & GBPE_TRAIN_DENSE_ONLY) && t->last_mc && hs->ln_last) {
+        const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
+        const uint32_t zmax = t->u16 ? ZoneDim<uint16_t>::ZMAX : ZoneDim<uint32_t>::ZMAX;
+        if (((t->flags & GBPE_TRAIN_SPARSE_EARLY) || (uint64_t)t->last_mc * t->sp_div <= hs->gn) &&
+            2 * zt + 4096 <= zmax && (uint64_t)hs->ln_last >= 4 * zt) {
+            const bool last = t->rank + 1 == t->world;
+            int rc = t->u16 ? sp_enter<uint16_t>(t, last) : sp_enter<uint32_t>(t, last);
+            if (rc != GBPE_OK) return rc;
+            if (!t->sp) return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "sharded sparse entry failed on rank %u", t->rank);
+        }
+    }
+    if (t->sp) {
+        int rc = t->u16 ? sp_shrink<uint16_t>(t) : sp_shrink<uint32_t>(t);
+        if (rc == GBPE_OK && t->sp_age >= 4096) {
+            const bool wb = t->sp_bits_age >= 16384;
+            rc = t->u16 ? sp_filters<uint16_t>(t, wb) : sp_filters<uint32_t>(t, wb);
+        }
+        if (rc != GBPE_OK) return rc;
+        hs->sel_round = 0;
+        TR_HIP(t, hipMemcpyAsync(&t->st->sel_round, &hs->sel_round, sizeof(uint32_t), hipMemcpyHostToDevice,
+                                 t->ctx->stream));
+    }
     hs->merges_done = 0;
     hs->budget = t->step_k;
     hs->stall = 0;
@@ -3167,6 +3341,53 @@ int shard_phase2(gbpe_trainer* t, uint32_t round, const uint32_t* recv, uint32_t
 }
 }  // namespace
 
+namespace {
+// sector-sparse sharded merge, phase 1: k_body (deltas into the per-merge delta
+// table; the zone on the last rank) + k_shard_send_sp
+template <typename S>
+int shard_phase1_sp(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl) {
+    hipStream_t s = t->ctx->stream;
+    S* zc = (S*)t->zbuf[t->zcur ^ (round & 1)];
+    S* zo = (S*)t->zbuf[t->zcur ^ (round & 1) ^ 1];
+    const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
+    const Table dt = delta_view(t, cl);
+    const uint32_t nbody = (uint32_t)gbpe_div_up(gbpe_div_up(t->nsec, 32), SP_WPW);
+    const bool zone = t->h_st->is_last != 0;
+    SelShard sh;
+    sh.cap_list = cl;
+    sh.zmax = t->u16 ? ZoneDim<uint16_t>::ZMAX : ZoneDim<uint32_t>::ZMAX;
+    sh.nlog = t->d_nlog;
+    sh.rec = rec;
+    const uint32_t gb = nbody + (zone ? 1u : 0u);
+    if (exact)
+        hipLaunchKernelGGL((k_body<S, true>), dim3(gb), dim3(BTPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
+                           t->bits, t->W, t->sig, t->tb, nbody, (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc,
+                           zone ? 1u : 0u, (const uint64_t*)t->part, t->g_refresh, t->d_log, t->grpsum, t->wg_bytes,
+                           dt, sh);
+    else
+        hipLaunchKernelGGL((k_body<S, false>), dim3(gb), dim3(BTPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
+                           t->bits, t->W, t->sig, t->tb, nbody, (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc,
+                           zone ? 1u : 0u, (const uint64_t*)t->part, t->g_refresh, t->d_log, t->grpsum, t->wg_bytes,
+                           dt, sh);
+    const uint32_t nlb = grid_persistent(t->ctx, dt.nblk, 2);
+    hipLaunchKernelGGL(k_shard_send_sp, dim3(nlb + 1), dim3(TPB), 0, s, t->st, t->zst, round, dt, rec, cl, nlb);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+
+// phase 2: every rank's deltas into the replica, the new layout, then k_refresh
+template <typename S>
+int shard_phase2_sp(gbpe_trainer* t, uint32_t round, const uint32_t* recv, uint32_t cl, uint32_t cw) {
+    hipStream_t s = t->ctx->stream;
+    const uint32_t nab = grid_persistent(t->ctx, 1u << 20, 2);
+    hipLaunchKernelGGL(k_shard_apply_sp, dim3(nab), dim3(TPB), 0, s, t->st, round, recv, t->world, cl, cw, t->tb, nab);
+    hipLaunchKernelGGL(k_refresh<S>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,
+                       (const uint32_t*)nullptr, t->zst, (uint32_t*)nullptr, FusedSel(), t->part);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+}  // namespace
+
 extern "C" int gbpe_shard_phase1(gbpe_trainer* t, uint32_t round, void* d_send, uint32_t cap_list, uint32_t cap_win) {
     if (!t || !t->sharded || !d_send) return GBPE_E_INVALID;
     if (round >= t->batch) return gbpe_set_error(t->ctx, GBPE_E_INVALID, "round out of range");
@@ -3174,6 +3395,9 @@ extern "C" int gbpe_shard_phase1(gbpe_trainer* t, uint32_t round, void* d_send, 
         TR_HIP(t, hipMemsetAsync(d_send, 0, HDR * sizeof(uint32_t), t->ctx->stream));
         return GBPE_OK;
     }
+    if (t->sp)
+        return t->u16 ? shard_phase1_sp<uint16_t>(t, round, (uint32_t*)d_send, cap_list)
+                      : shard_phase1_sp<uint32_t>(t, round, (uint32_t*)d_send, cap_list);
     return t->u16 ? shard_phase1<uint16_t>(t, round, (uint32_t*)d_send, cap_list, cap_win)
                   : shard_phase1<uint32_t>(t, round, (uint32_t*)d_send, cap_list, cap_win);
 }
@@ -3182,6 +3406,9 @@ extern "C" int gbpe_shard_phase2(gbpe_trainer* t, uint32_t round, const void* d_
                                  uint32_t cap_win) {
     if (!t || !t->sharded || !d_recv) return GBPE_E_INVALID;
     if (round >= t->step_k) return GBPE_OK;
+    if (t->sp)
+        return t->u16 ? shard_phase2_sp<uint16_t>(t, round, (const uint32_t*)d_recv, cap_list, cap_win)
+                      : shard_phase2_sp<uint32_t>(t, round, (const uint32_t*)d_recv, cap_list, cap_win);
     return t->u16 ? shard_phase2<uint16_t>(t, round, (const uint32_t*)d_recv, cap_list, cap_win)
                   : shard_phase2<uint32_t>(t, round, (const uint32_t*)d_recv, cap_list, cap_win);
 }
@@ -3222,10 +3449,23 @@ extern "C" int gbpe_shard_step_end(gbpe_trainer* t, uint32_t* merges_out, uint32
         if (merges_out) memcpy(merges_out + 4 * r, t->h_log + 4 * r, 4 * sizeof(uint32_t));
     }
     t->n = hs->n;
-    t->cur ^= (done & 1u);
+    if (done) t->last_mc = t->h_log[(done - 1) * 4 + 3];
+    if (t->sp) {
+        t->zcur ^= (int)(done & 1u);
+        t->sp_merges += done;
+        t->sp_age += done;
+        t->sp_bits_age += done;
+    } else {
+        t->cur ^= (done & 1u);
+    }
     t->done += done;
     t->stop = hs->stop != 0;
     t->step_k = 0;
+    if (t->sp && hs->sp_abort) {   // the zone outgrew its bounds on the last rank: every rank goes dense
+        int rc = sp_exit_any(t);
+        if (rc != GBPE_OK) return rc;
+        t->sp_cooldown = 1;
+    }
     if (n_done) *n_done = done;
     if (early_stop) *early_stop = t->stop ? 1u : 0u;
     if (stalled) *stalled = hs->stall;

@@ -191,12 +191,12 @@ class GpuShardBackend:
 
     def __init__(self, lib, ctx, data, word_starts, rank: int, world: int, target_vocab: int,
                  exact: bool = False, input_on_device: bool = False, n: int | None = None,
-                 table_log2: int = 0, cap_extra: int = 0, stream=None):
+                 table_log2: int = 0, cap_extra: int = 0, stream=None, flags: int = 0):
         from . import _lib
         self.lib, self.ctx, self._lib = lib, ctx, _lib
         if stream is not None:   # run on the caller's stream (torch's), so its collectives and copies are ordered
             _lib.check(lib.gbpe_ctx_set_stream(ctx, C.c_void_p(stream)), ctx, "gbpe_ctx_set_stream")
-        flags = _lib.GBPE_TRAIN_EXACT_COMPACTION if exact else 0
+        flags |= _lib.GBPE_TRAIN_EXACT_COMPACTION if exact else 0
         self.opts = _lib.TrainOpts(target_vocab_size=target_vocab, vocab_size=256, next_token_id=256,
                                    batch_size=BATCH_SIZE, flags=flags, table_log2=table_log2)
         t = C.c_void_p()

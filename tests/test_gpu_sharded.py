@@ -40,15 +40,20 @@ def _worker(rank, world, port, case, outdir):
         data = synth.english(case["bytes"], seed=case["seed"])
         shards, _ = cut_at_word_starts(data, case["fracs"])
         d, ws = shards[rank]
+        flags = {None: 0, "dense": _lib.GBPE_TRAIN_DENSE_ONLY, "early": _lib.GBPE_TRAIN_SPARSE_EARLY}[case.get("sparse")]
         be = GpuShardBackend(lib, ctx, d, ws, rank, world, case["vocab"], exact=case["exact"],
-                             table_log2=16, cap_extra=len(data), stream=torch.cuda.current_stream().cuda_stream)
+                             table_log2=16, cap_extra=len(data), stream=torch.cuda.current_stream().cuda_stream,
+                             flags=flags)
         assert lib.gbpe_ctx_get_stream(ctx) == (torch.cuda.current_stream().cuda_stream or None)
         tr = ShardedTrainer(be, dist, device="cuda", staged=True, cap_list=case["cap"], cap_win=case["cap"])
         tr.setup()
         merges, early = tr.train(case["vocab"], batch=case.get("batch", 128))
         np.save(os.path.join(outdir, f"sym{rank}.npy"), be.symbols())
+        st = _lib.TrainerStats()
+        lib.gbpe_trainer_stats_get(be.t, C.byref(st))
         with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
-            json.dump({"merges": merges, "early": early, "stalls": tr.stalls}, f)
+            json.dump({"merges": merges, "early": early, "stalls": tr.stalls, "sparse_merges": int(st.sparse_merges)},
+                      f)
         be.close()
     finally:
         lib.gbpe_ctx_destroy(ctx)
@@ -65,12 +70,25 @@ def run_case(world, case):
     return res, syms
 
 
+# sparse: None = the library's policy (dense, then the sector-sparse loop once the
+# counts allow), "dense" = the dense loop only, "early" = sparse from the first
+# step boundary where the last rank's zone fits
 CASES = [
     ("ref_w2", 2, dict(bytes=60_000, seed=21, fracs=[0.5], vocab=700, exact=False, cap=1 << 14)),
     ("exact_w2", 2, dict(bytes=60_000, seed=22, fracs=[0.5], vocab=700, exact=True, cap=1 << 14)),
     ("ref_w3_tiny_middle", 3, dict(bytes=20_000, seed=13, fracs=[0.945, 0.965], vocab=480, exact=False,
                                    cap=1 << 14)),
     ("ref_w2_stalls", 2, dict(bytes=16_000, seed=14, fracs=[0.6], vocab=420, exact=False, cap=8, batch=32)),
+    ("dense_ref_w2", 2, dict(bytes=60_000, seed=21, fracs=[0.5], vocab=700, exact=False, cap=1 << 14,
+                             sparse="dense")),
+    ("dense_ref_w3_tiny_middle", 3, dict(bytes=20_000, seed=13, fracs=[0.945, 0.965], vocab=480, exact=False,
+                                         cap=1 << 14, sparse="dense")),
+    ("sparse_ref_w2", 2, dict(bytes=80_000, seed=23, fracs=[0.5], vocab=1200, exact=False, cap=1 << 14,
+                              sparse="early", batch=16)),
+    ("sparse_exact_w3", 3, dict(bytes=80_000, seed=24, fracs=[0.3, 0.7], vocab=1000, exact=True, cap=1 << 14,
+                                sparse="early", batch=32)),
+    ("sparse_ref_w3_stalls", 3, dict(bytes=40_000, seed=25, fracs=[0.4, 0.75], vocab=800, exact=False, cap=8,
+                                     sparse="early", batch=16)),
 ]
 
 
@@ -85,3 +103,7 @@ def test_gpu_sharded_matches_single_stream(name, world, case):
     np.testing.assert_array_equal(np.concatenate(syms), exp["symbols"])
     if name.endswith("stalls"):
         assert res[0]["stalls"] > 0
+    if case.get("sparse") == "early":
+        assert all(r["sparse_merges"] > 0 for r in res), "the sector-sparse loop never ran"
+    if case.get("sparse") == "dense":
+        assert all(r["sparse_merges"] == 0 for r in res)
