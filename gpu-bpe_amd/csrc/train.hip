@@ -603,7 +603,8 @@ __device__ __forceinline__ void load_own(const S* cur, uint64_t i0, uint32_t* __
     for (int k = 0; k < EPT; ++k) x[k] = e[k];
 }
 
-constexpr int LTAB_T = 1024;          // per-tile LDS delta table of k_delta
+constexpr int LTAB_T = 1024;          // per-workgroup LDS delta table of k_body / the zone pass
+constexpr int LTAB_Z = 4096;          // k_delta on a sparse zone: its stale tail holds many distinct pairs
 
 
 __device__ __forceinline__ uint32_t lane_mask32(uint64_t i0, uint64_t lim) {
@@ -629,7 +630,7 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
                                                uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
                                                uint32_t* __restrict__ grpsum, uint32_t eager_tiles) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
-    __shared__ LdsTab<LTAB_T> lt;
+    __shared__ LdsTab<STAGE ? LTAB_Z : LTAB_T> lt;
     __shared__ uint32_t stg[STAGE ? EPT * TPB : 1];
     __shared__ uint32_t red[TPB / 64], s_workw[TPB / 64];
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -1008,10 +1009,7 @@ __global__ void k_export_symbols(const S* __restrict__ s, uint32_t* __restrict__
 //     of being left in place.
 // Per merge: k_select → k_body (candidate sectors + window copy) → k_delta (zone)
 // → k_compact<ZONE> → k_refresh.
-#ifndef GBPE_SP_WPW
-#define GBPE_SP_WPW 32
-#endif
-constexpr uint32_t SP_WPW = GBPE_SP_WPW;   // bitmap words (32 sectors each) per k_body workgroup
+constexpr uint32_t SP_WPW_MIN = 16;  // fewest bitmap words per k_body workgroup (sizes its byte counters)
 constexpr uint32_t SP_CH = 256;      // symbols per wave pass over a sector (4 per lane)
 constexpr uint32_t SP_INV = 0xFFFFFFFFu;
 constexpr uint32_t SP_SHRINKS = 64;  // zone shrinks per sparse entry (sector capacity)
@@ -1125,17 +1123,20 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uin
 // (A-sides rewritten, also in place: the reference's ping buffer) are compacted
 // into the other zone buffer and the stale window follows them.  The window
 // source is read from the other buffer before anything is written to it.
-constexpr int BTPB = 1024;                  // k_body workgroup (16 waves)
-template <typename S> struct ZoneDim {
-    static constexpr int ZPT = sizeof(S) == 2 ? 32 : 16;        // zone positions per thread
-    static constexpr uint32_t ZMAX = (uint32_t)BTPB * ZPT;      // 32768 (u16) / 16384 (u32) symbols: 64 KiB
-    static constexpr uint32_t ZWIN = ZMAX / 4;                   // >= ZMAX / 5 >= mc (zone >= 5 mc)
+// k_body runs as 1024-thread workgroups (16 waves: more sectors in flight, a
+// zone up to 32K symbols in one workgroup) while the zone is large, and as
+// 256-thread ones late in training (small zone, lower latency per launch).
+template <typename S, int BT> struct ZoneDim {
+    static constexpr int ZPT = (BT == 1024 && sizeof(S) == 4) ? 16 : 32;   // zone positions per thread
+    static constexpr uint32_t ZMAX = (uint32_t)BT * ZPT;   // 8192 (256) / 32768 or 16384 (1024) symbols
+    static constexpr uint32_t ZWIN = ZMAX / 4;              // >= ZMAX / 5 >= mc (zone >= 5 mc)
+    static constexpr uint32_t WPW = BT == 1024 ? 32 : 16;  // bitmap words (32 sectors each) per workgroup
 };
-template <typename S>
+template <typename S, int BT>
 struct ZoneLds {
-    uint4 xv[ZoneDim<S>::ZMAX * sizeof(S) / 16];   // the zone (symbol i = ((S*)xv)[i])
-    S wb[ZoneDim<S>::ZWIN];
-    uint32_t wsum[BTPB / 64], wtail[BTPB / 64], left;
+    uint4 xv[ZoneDim<S, BT>::ZMAX * sizeof(S) / 16];   // the zone (symbol i = ((S*)xv)[i])
+    S wb[ZoneDim<S, BT>::ZWIN];
+    uint32_t wsum[BT / 64], wtail[BT / 64], left;
 };
 
 __device__ __forceinline__ uint32_t lane_mask_n(uint64_t i0, uint64_t lim, int n) {
@@ -1144,12 +1145,12 @@ __device__ __forceinline__ uint32_t lane_mask_n(uint64_t i0, uint64_t lim, int n
     return i0 >= lim ? 0u : (i0 + n <= lim ? full : ((1u << (uint32_t)(lim - i0)) - 1u));
 }
 
-template <typename S, bool EXACT>
-__device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __restrict__ zo, ZoneLds<S>& L,
+template <typename S, bool EXACT, int BT>
+__device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __restrict__ zo, ZoneLds<S, BT>& L,
                          LdsTab<LTAB_T>& lt, const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
                          uint64_t* __restrict__ bytes) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
-    constexpr int ZPT = ZoneDim<S>::ZPT;
+    constexpr int ZPT = ZoneDim<S, BT>::ZPT;
     constexpr int V = ZPT * sizeof(S) / 16;  // 16-byte vectors per thread
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t z = zst->n;
@@ -1171,7 +1172,7 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
     }
     if (!EXACT) {   // window source: global n - 2mc in the previous stream (sharded: it began at poff, now off)
         const uint64_t src0 = (uint64_t)st->n + st->off - st->poff - 2ull * mc - st->Bp;
-        for (uint32_t u = t; u < mc; u += BTPB) L.wb[u] = zo[src0 + u];
+        for (uint32_t u = t; u < mc; u += BT) L.wb[u] = zo[src0 + u];
     }
     lds_clear(lt);
     __syncthreads();
@@ -1192,7 +1193,7 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
     const uint32_t surv = inb & ~hitm, keep = surv & below;
     const uint32_t rwm = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
     uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
-    for (uint32_t i = (lim > 1u ? lim : 1u) + t; i < z; i += BTPB) {   // stale tail: old pairs destroyed
+    for (uint32_t i = (lim > 1u ? lim : 1u) + t; i < z; i += BT) {   // stale tail: old pairs destroyed
         const uint32_t xi = xs[i];
         if (xi & WS) continue;
         const uint32_t tp = xs[i - 1] & TM, ti = xi & TM;
@@ -1231,7 +1232,7 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
     __syncthreads();
     uint32_t pre = incl - kc, Kz = 0, m = 0;
 #pragma unroll
-    for (int w2 = 0; w2 < BTPB / 64; ++w2) {
+    for (int w2 = 0; w2 < BT / 64; ++w2) {
         pre += w2 < wid ? L.wsum[w2] : 0u;
         Kz += L.wsum[w2];
         m += L.wtail[w2];
@@ -1249,7 +1250,7 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
     if (!EXACT && m) {
         __syncthreads();
         const uint32_t woff = mc - m;
-        for (uint32_t j = t; j < m; j += BTPB) {
+        for (uint32_t j = t; j < m; j += BT) {
             const uint32_t x1 = L.wb[woff + j];
             const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : L.left;
             zo[Kz + j] = (S)x1;
@@ -1281,11 +1282,12 @@ struct SelShard {
     uint32_t* rec = nullptr; // this rank's exchange record (its list length restarts at 0)
 };
 
+template <int BT>
 __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
                            uint32_t round, bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
                            uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc,
                            const SelShard sh = SelShard()) {
-    __shared__ uint64_t s_red[BTPB / 64];
+    __shared__ uint64_t s_red[BT / 64];
     __shared__ uint32_t s_ok;
     const int t = threadIdx.x;
     if (t == 0)
@@ -1293,7 +1295,7 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     __syncthreads();
     if (!s_ok) return false;
     uint64_t best = 0;
-    for (uint32_t i = t; i < npart; i += BTPB) {
+    for (uint32_t i = t; i < npart; i += BT) {
         const uint64_t v = part[i];
         best = v > best ? v : best;
     }
@@ -1305,7 +1307,7 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     __syncthreads();
     best = s_red[0];
 #pragma unroll
-    for (int w = 1; w < BTPB / 64; ++w) best = s_red[w] > best ? s_red[w] : best;
+    for (int w = 1; w < BT / 64; ++w) best = s_red[w] > best ? s_red[w] : best;
     mc = (uint32_t)(best >> 32);
     const uint32_t pid = ~(uint32_t)best;
     a = pid >> 16;
@@ -1373,7 +1375,7 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
         }
         if (go) {   // group sums of a multi-tile zone pass start at zero
             const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(zst->n, TILE), GRP);
-            for (uint32_t g = t; g < ngrp; g += BTPB) grpsum[g * GSTR] = 0u;
+            for (uint32_t g = t; g < ngrp; g += BT) grpsum[g * GSTR] = 0u;
         }
     }
     return go;
@@ -1385,8 +1387,8 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
 // [n - 2mc - Bp, + mc) of the zone's other buffer to `wtmp`.
 // With `zst` (zone <= ZMAX), block nbody runs the whole zone pass (zone_one) and
 // there are no copy blocks: one launch merges body and zone.
-template <typename S, bool EXACT>
-__global__ __launch_bounds__(BTPB) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
+template <typename S, bool EXACT, int BT>
+__global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
                                               uint32_t* __restrict__ bits, uint32_t W, uint32_t* __restrict__ sig,
                                               Table tb, uint32_t nbody, const S* __restrict__ zoth, S* __restrict__ wtmp,
                                               uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
@@ -1394,23 +1396,24 @@ __global__ __launch_bounds__(BTPB) void k_body(DevState* st, uint32_t round, S* 
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
                                               Table dtb, SelShard sh) {
     __shared__ LdsTab<LTAB_T> lt;
+    constexpr uint32_t SP_WPW = ZoneDim<S, BT>::WPW;
     __shared__ uint32_t s_tok[SP_WPW * 32], s_list[SP_WPW * 32];
     __shared__ uint2 s_ext[SP_WPW * 32];
-    __shared__ uint32_t s_ntok, s_n, s_rm[BTPB / 64];
-    __shared__ uint64_t s_mv[BTPB / 64];
-    __shared__ ZoneLds<S> zl;
+    __shared__ uint32_t s_ntok, s_n, s_rm[BT / 64];
+    __shared__ uint64_t s_mv[BT / 64];
+    __shared__ ZoneLds<S, BT> zl;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     uint32_t a, b, nw, mc;
-    if (!sel_inline(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, sh)) return;
+    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, sh)) return;
     // deltas go to the replica (single GPU) or to the per-merge delta table (sharded)
     if (zone1 && blockIdx.x == nbody) {
-        zone_one<S, EXACT>(st, zst, zcur, (S*)zoth, zl, lt, dtb, a, b, nw, mc, wg_bytes + nbody);
+        zone_one<S, EXACT, BT>(st, zst, zcur, (S*)zoth, zl, lt, dtb, a, b, nw, mc, wg_bytes + nbody);
         return;
     }
     if (blockIdx.x >= nbody) {
         const uint64_t src0 = (uint64_t)st->n + st->off - st->poff - 2ull * mc - st->Bp;
-        const uint64_t stride = (uint64_t)(gridDim.x - nbody) * BTPB;
-        for (uint64_t u = (uint64_t)(blockIdx.x - nbody) * BTPB + t; u < mc; u += stride) wtmp[u] = zoth[src0 + u];
+        const uint64_t stride = (uint64_t)(gridDim.x - nbody) * BT;
+        for (uint64_t u = (uint64_t)(blockIdx.x - nbody) * BT + t; u < mc; u += stride) wtmp[u] = zoth[src0 + u];
         return;
     }
     const uint32_t pid_ab = (a << 16) | b;
@@ -1436,7 +1439,7 @@ __global__ __launch_bounds__(BTPB) void k_body(DevState* st, uint32_t round, S* 
     const uint32_t ntok = s_ntok;
     if (ntok == 0) return;
     if (t == 0) wg_bytes[blockIdx.x] += 16ull * ntok;   // extents + signature words read
-    for (uint32_t j = t; j < ntok; j += BTPB) {   // signature filter; the sector's extent loads alongside
+    for (uint32_t j = t; j < ntok; j += BT) {   // signature filter; the sector's extent loads alongside
         const uint32_t sct = s_tok[j];
         const uint2 e = sec[sct];
         if (sig_has(sig + (uint64_t)sct * SP_SIGW, pid_ab)) {
@@ -1453,7 +1456,7 @@ __global__ __launch_bounds__(BTPB) void k_body(DevState* st, uint32_t round, S* 
     __syncthreads();
     uint32_t removed = 0;
     uint64_t moved = 0;   // sector symbols read + rewritten (wave-uniform)
-    for (uint32_t j = wid; j < ncand; j += BTPB / 64) {
+    for (uint32_t j = wid; j < ncand; j += BT / 64) {
         const uint32_t sct = s_list[j];
         const uint2 e = s_ext[j];
         uint32_t out = 0;
@@ -1477,7 +1480,7 @@ __global__ __launch_bounds__(BTPB) void k_body(DevState* st, uint32_t round, S* 
     if (t == 0) {
         uint32_t r = 0;
         uint64_t mv = 0;
-        for (int w2 = 0; w2 < BTPB / 64; ++w2) {
+        for (int w2 = 0; w2 < BT / 64; ++w2) {
             r += s_rm[w2];
             mv += s_mv[w2];
         }
@@ -1776,7 +1779,21 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
 struct SpGrid {
     uint32_t body, copy, zdelta, zcompact, refresh;
     bool zone1;   // the zone fits one workgroup: it runs inside k_body
+    int bt;       // k_body workgroup size (256 or 1024)
 };
+
+template <typename S>
+uint32_t zone_max(int bt) { return bt == 1024 ? ZoneDim<S, 1024>::ZMAX : ZoneDim<S, 256>::ZMAX; }
+inline uint32_t body_wpw(int bt) { return bt == 1024 ? ZoneDim<uint16_t, 1024>::WPW : ZoneDim<uint16_t, 256>::WPW; }
+
+// launch k_body<S, EXACT, bt> (one instantiation per workgroup size)
+template <typename S, bool EXACT, typename... A>
+void launch_body(int bt, uint32_t grid, hipStream_t s, A... args) {
+    if (bt == 1024)
+        hipLaunchKernelGGL((k_body<S, EXACT, 1024>), dim3(grid), dim3(1024), 0, s, args...);
+    else
+        hipLaunchKernelGGL((k_body<S, EXACT, 256>), dim3(grid), dim3(256), 0, s, args...);
+}
 
 template <typename S>
 int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const SpGrid& g, bool timing, hipEvent_t* ev) {
@@ -1788,15 +1805,13 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const uint32_t gb = g.body + (g.zone1 ? 1u : g.copy);
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
-        hipLaunchKernelGGL((k_body<S, true>), dim3(gb), dim3(BTPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
-                           t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst,
-                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes,
-                           t->tb, SelShard());
+        launch_body<S, true>(g.bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, t->sig, t->tb,
+                             g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, g.zone1 ? 1u : 0u,
+                             (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, SelShard());
     else
-        hipLaunchKernelGGL((k_body<S, false>), dim3(gb), dim3(BTPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
-                           t->bits, t->W, t->sig, t->tb, g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst,
-                           zc, g.zone1 ? 1u : 0u, (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes,
-                           t->tb, SelShard());
+        launch_body<S, false>(g.bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, t->sig, t->tb,
+                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, g.zone1 ? 1u : 0u,
+                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, SelShard());
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
     if (!g.zone1) {
         if (exact)
@@ -1930,7 +1945,7 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true) {
     // zone buffers: the zone, and the stale source (previous stream, n_prev - Zs <= z + last_mc symbols)
     // (>= the one-workgroup zone pass's full register window, which it loads unconditionally)
     uint64_t zneed = (gbpe_div_up((uint64_t)z + t->last_mc + 1, TILE) + 2) * TILE;
-    const uint64_t zmin = (uint64_t)(t->u16 ? ZoneDim<uint16_t>::ZMAX : ZoneDim<uint32_t>::ZMAX) + TILE;
+    const uint64_t zmin = (uint64_t)(t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024)) + TILE;
     if (zneed < zmin) zneed = zmin;
     if (zneed > t->zcap) {
         for (int k = 0; k < 2; ++k) {
@@ -1973,7 +1988,7 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true) {
     TR_HIP(t, hipMemcpyAsync(&t->st->zlast, &t->h_st->zlast, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     TR_HIP(t, hipMemcpyAsync(&t->st->is_last, &t->h_st->is_last, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     {   // one byte counter per k_body workgroup, kept across entries (summed by gbpe_trainer_stats_get)
-        const uint64_t need = gbpe_div_up(gbpe_div_up(cap, 32), SP_WPW) + 2;
+        const uint64_t need = gbpe_div_up(gbpe_div_up(cap, 32), SP_WPW_MIN) + 2;
         if (need > t->wg_cap) {
             uint64_t* nb = nullptr;
             TR_HIP(t, hipMalloc(&nb, need * sizeof(uint64_t)));
@@ -2297,8 +2312,10 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     if (sparse) {
         const uint32_t zn = t->n - hs->B;   // zone length (it only shrinks within a step)
         const uint64_t zt = gbpe_div_up(zn, TILE);
-        sg.body = (uint32_t)gbpe_div_up(gbpe_div_up(t->nsec, 32), SP_WPW);
-        sg.zone1 = zn <= (t->u16 ? ZoneDim<uint16_t>::ZMAX : ZoneDim<uint32_t>::ZMAX);
+        const uint32_t z256 = t->u16 ? zone_max<uint16_t>(256) : zone_max<uint32_t>(256);
+        sg.bt = zn <= z256 ? 256 : 1024;   // small zone: the low-latency 256-thread workgroups
+        sg.body = (uint32_t)gbpe_div_up(gbpe_div_up(t->nsec, 32), body_wpw(sg.bt));
+        sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt));
         sg.copy = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u : grid_persistent(t->ctx, gbpe_div_up(zn / 5 + 1, TPB * 8), 1);
         sg.zdelta = (uint32_t)(zt ? zt : 1);
         sg.zcompact = (uint32_t)zt + ((t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
@@ -3249,7 +3266,7 @@ extern "C" int gbpe_shard_step_begin(gbpe_trainer* t, uint32_t max_merges) {
         --t->sp_cooldown;
     } else if (!t->sp && !(t->flags & GBPE_TRAIN_DENSE_ONLY) && t->last_mc && hs->ln_last) {
         const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
-        const uint32_t zmax = t->u16 ? ZoneDim<uint16_t>::ZMAX : ZoneDim<uint32_t>::ZMAX;
+        const uint32_t zmax = t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024);
         if (((t->flags & GBPE_TRAIN_SPARSE_EARLY) || (uint64_t)t->last_mc * t->sp_div <= hs->gn) &&
             2 * zt + 4096 <= zmax && (uint64_t)hs->ln_last >= 4 * zt) {
             const bool last = t->rank + 1 == t->world;
@@ -3351,24 +3368,24 @@ int shard_phase1_sp(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl)
     S* zo = (S*)t->zbuf[t->zcur ^ (round & 1) ^ 1];
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     const Table dt = delta_view(t, cl);
-    const uint32_t nbody = (uint32_t)gbpe_div_up(gbpe_div_up(t->nsec, 32), SP_WPW);
     const bool zone = t->h_st->is_last != 0;
+    const uint32_t zn = zone ? t->n - t->h_st->B : 0u;   // the zone only shrinks within a step
+    const int bt = zn <= (t->u16 ? zone_max<uint16_t>(256) : zone_max<uint32_t>(256)) ? 256 : 1024;
+    const uint32_t nbody = (uint32_t)gbpe_div_up(gbpe_div_up(t->nsec, 32), body_wpw(bt));
     SelShard sh;
     sh.cap_list = cl;
-    sh.zmax = t->u16 ? ZoneDim<uint16_t>::ZMAX : ZoneDim<uint32_t>::ZMAX;
+    sh.zmax = t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024);
     sh.nlog = t->d_nlog;
     sh.rec = rec;
     const uint32_t gb = nbody + (zone ? 1u : 0u);
     if (exact)
-        hipLaunchKernelGGL((k_body<S, true>), dim3(gb), dim3(BTPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
-                           t->bits, t->W, t->sig, t->tb, nbody, (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc,
-                           zone ? 1u : 0u, (const uint64_t*)t->part, t->g_refresh, t->d_log, t->grpsum, t->wg_bytes,
-                           dt, sh);
+        launch_body<S, true>(bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, t->sig, t->tb, nbody,
+                             (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc, zone ? 1u : 0u, (const uint64_t*)t->part,
+                             t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh);
     else
-        hipLaunchKernelGGL((k_body<S, false>), dim3(gb), dim3(BTPB), 0, s, t->st, round, (S*)t->buf[t->bcur], t->sec,
-                           t->bits, t->W, t->sig, t->tb, nbody, (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc,
-                           zone ? 1u : 0u, (const uint64_t*)t->part, t->g_refresh, t->d_log, t->grpsum, t->wg_bytes,
-                           dt, sh);
+        launch_body<S, false>(bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, t->sig, t->tb, nbody,
+                              (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc, zone ? 1u : 0u, (const uint64_t*)t->part,
+                              t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh);
     const uint32_t nlb = grid_persistent(t->ctx, dt.nblk, 2);
     hipLaunchKernelGGL(k_shard_send_sp, dim3(nlb + 1), dim3(TPB), 0, s, t->st, t->zst, round, dt, rec, cl, nlb);
     GBPE_LAUNCH_CHECK(t->ctx);
