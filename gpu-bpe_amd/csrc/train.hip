@@ -1507,8 +1507,12 @@ __global__ __launch_bounds__(1024) void k_sp_zone_start(const S* __restrict__ cu
 }
 
 // window j of a body region [base, base + len) covers [base + j*SEC, +SEC); its
-// sector starts at the window's first word start (window 0: at `base`, which is
-// a word start or the stream's first symbol).  One wave per window.
+// sector starts at the window's first word start or 0 symbol (window 0: at
+// `base`, which is a word start or the stream's first symbol).  No counted pair
+// spans either: pairs never cross a word start, and none holds token 0 — the
+// stale windows the reference compaction leaves are long 0 runs
+// that would otherwise make one sector of up to ~10^6 symbols.  One wave per
+// window.
 template <typename S>
 __global__ __launch_bounds__(TPB) void k_sp_sectors(const S* __restrict__ body, uint32_t base, uint32_t len, uint32_t SEC,
                                                     uint32_t* __restrict__ starts, uint32_t nwin) {
@@ -1520,7 +1524,8 @@ __global__ __launch_bounds__(TPB) void k_sp_sectors(const S* __restrict__ body, 
     uint32_t found = j == 0 ? base : SP_INV;
     for (uint64_t b0 = lo; b0 < hi && found == SP_INV; b0 += 64) {
         const uint64_t i = b0 + lane;
-        const bool ws = i < hi && (body[i] & Sym<S>::WS);
+        uint32_t x = i < hi ? (uint32_t)body[i] : 1u;
+        const bool ws = (x & Sym<S>::WS) || x == 0u;
         const unsigned long long m = __ballot(ws);
         if (m) found = (uint32_t)(b0 + (uint64_t)(__ffsll((long long)m) - 1));
     }

@@ -6,7 +6,8 @@ its last kernel) follows it, so dense merges (k_delta + k_compact) and
 sector-sparse merges (k_body + zone k_delta + zone k_compact) share one table.  Only the last run of
 the workload in the trace is used (the one BENCH_DUMP_MERGES dumped).
 
-usage: python tools/merge_profile.py <rocprof csv dir> <merges.npy>
+usage: [EDGES=0,10,100] python tools/merge_profile.py <rocprof csv dir> <merges.npy>
+(k_sp_ = the sparse loop's entry / shrink / filter-rebuild kernels)
 """
 import csv
 import glob
@@ -15,7 +16,7 @@ import sys
 
 import numpy as np
 
-KS = ["k_select", "k_body", "k_delta", "k_compact", "k_refresh"]
+KS = ["k_select", "k_body", "k_delta", "k_compact", "k_refresh", "k_sp_"]
 
 
 def main():
@@ -45,7 +46,8 @@ def main():
     starts = np.array([int(rows[i]["Start_Timestamp"]) for i in sel], dtype=np.float64)
     period = np.diff(starts) / 1e3
     print(f"{'merges':<14}{'count':>9}" + "".join(f"{k:>11}" for k in KS) + f"{'sum':>9}{'period':>9}")
-    edges = [0, 100, 500, 1000, 2000, 4000, 8000, 16000, 24000, nm]
+    edges = [int(e) for e in os.environ["EDGES"].split(",")] + [nm] if os.environ.get("EDGES") else \
+        [0, 100, 500, 1000, 2000, 4000, 8000, 16000, 24000, nm]
     for a, b in zip(edges[:-1], edges[1:]):
         if a >= nm:
             break
