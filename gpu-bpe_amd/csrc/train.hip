@@ -109,6 +109,29 @@ struct DevState {
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
+// Phase timestamps of the sector-sparse kernels (diagnostic builds only:
+// -DGBPE_KTRACE; tools/ktrace.sh).  Every KT_EVERY-th merge, each workgroup
+// stores its own wall-clock stamps (plain stores, no shared counters that
+// would serialise the launch): k_body workgroups at [m][wg][slot], k_refresh
+// workgroups at [m][KT_WG + wg][slot].
+#ifdef GBPE_KTRACE
+constexpr uint32_t KT_MERGES = 40000, KT_EVERY = 16, KT_WG = 2048, KT_SLOTS = 8;
+__device__ unsigned long long* g_ktr;
+__device__ uint32_t g_kt_base;
+__device__ __forceinline__ void kt_put(uint32_t round, uint32_t wg, int i, unsigned long long v) {
+    const uint32_t m = g_kt_base + round;
+    if (g_ktr && m < KT_MERGES && m % KT_EVERY == 0 && wg < 2 * KT_WG)
+        g_ktr[((uint64_t)(m / KT_EVERY) * 2 * KT_WG + wg) * KT_SLOTS + i] = v;
+}
+#define KT(i) kt_put(round, blockIdx.x, (i), wall_clock64())
+#define KTV(i, v) kt_put(round, blockIdx.x, (i), (v))
+#define KTR(i) kt_put(round, KT_WG + blockIdx.x, (i), wall_clock64())
+#else
+#define KT(i) ((void)0)
+#define KTV(i, v) ((void)0)
+#define KTR(i) ((void)0)
+#endif
+
 // exchange-record header words of sharded training (gpubpe/sharded.py mirrors them)
 enum : uint32_t {
     H_ACTIVE = 0, H_L, H_KEPT, H_M, H_W, H_LASTSYM, H_HASLAST, H_SURV, H_LN, H_MC, H_A, H_B, H_ID, H_DFULL,
@@ -340,55 +363,72 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
     __shared__ uint32_t rlive[TPB / 64];
     (void)cur;
     (void)rwlist;
+    if (part && finish == 2 && threadIdx.x == 0) KTR(0);
     // finish == 2: the sector-sparse loop, whose merge was selected inside k_body
     // (sel_inline): the step counters move on here
-    const bool fin = finish == 2 ? (!st->stop && !st->sp_abort && st->sel_round == round + 1u)
-                                 : (finish && !st->stop && !st->stall && st->merges_done == round + 1u);
-    if (fin) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // block 0 closes the merge from one snapshot of both states: every field is
+    // read (one round trip) before any is written, not one round trip per field
+    if (finish && blockIdx.x == 0) {
+        constexpr int NW = sizeof(DevState) / 4;
+        __shared__ union {
+            DevState d;
+            uint32_t w[NW];
+        } s_g, s_z;
+        if (threadIdx.x < NW) s_g.w[threadIdx.x] = reinterpret_cast<const uint32_t*>(st)[threadIdx.x];
+        else if (zst && threadIdx.x < 2 * NW) s_z.w[threadIdx.x - NW] = reinterpret_cast<const uint32_t*>(zst)[threadIdx.x - NW];
+        __syncthreads();
+        const DevState& g = s_g.d;
+        const DevState& z = s_z.d;
+        const bool fin = finish == 2 ? (!g.stop && !g.sp_abort && g.sel_round == round + 1u)
+                                     : (!g.stop && !g.stall && g.merges_done == round + 1u);
+        if (fin && threadIdx.x == 0) {
             if (zst) {   // sector-sparse: global length, body length, zone length
                 if (finish == 2) {
                     st->merges_done = round + 1u;
-                    st->next_id += 1u;
-                    st->epoch += 1u;
+                    st->next_id = g.next_id + 1u;
+                    st->epoch = g.epoch + 1u;
                 }
                 if (clog) {
-                    clog[2 * round] = st->cand;
-                    clog[2 * round + 1] = st->hitsec;
+                    clog[2 * round] = g.cand;
+                    clog[2 * round + 1] = g.hitsec;
                 }
                 st->cand = 0u;
                 st->hitsec = 0u;
-                st->tail_total += zst->m;
-                st->n = st->new_n;
-                st->Bp = st->B;
-                st->B -= st->body_rm;
+                st->tail_total = g.tail_total + z.m;
+                const uint32_t n = g.new_n, B = g.B - g.body_rm, zn = n - B;
+                st->n = n;
+                st->Bp = g.B;
+                st->B = B;
                 st->body_rm = 0u;
-                const uint32_t zold = zst->n;
-                zst->n = st->n - st->B;
-                if (!st->sharded) st->zlast = zst->n;   // sharded: from the records (k_shard_apply)
-                if (!zst->valid_total && st->is_last)   // multi-tile zone: k_delta + k_compact stream it twice, plus the window copy
-                    st->sp_bytes += (uint64_t)sizeof(S) * (2ull * zold + zst->n + 2ull * st->mc);
-                if (zst->valid_total && zst->valid_total != zst->n + 1u) atomicOr(&st->err, ERR_COUNT_MISMATCH);
-            } else if (st->sharded) {   // commit the new global layout computed by k_shard_recv
-                st->tail_total += st->m_glob;
-                st->poff = st->off;
-                st->pln = st->n;
-                st->n = st->nl_next;
-                st->off = st->off_next;
-                st->gn = st->gnew;
+                zst->n = zn;
+                if (!g.sharded) st->zlast = zn;   // sharded: from the records (k_shard_apply)
+                if (!z.valid_total && g.is_last)   // multi-tile zone: k_delta + k_compact stream it twice, plus the window copy
+                    st->sp_bytes = g.sp_bytes + (uint64_t)sizeof(S) * (2ull * z.n + zn + 2ull * g.mc);
+                if (z.valid_total && z.valid_total != zn + 1u) atomicOr(&st->err, ERR_COUNT_MISMATCH);
+            } else if (g.sharded) {   // commit the new global layout computed by k_shard_recv
+                st->tail_total = g.tail_total + g.m_glob;
+                st->poff = g.off;
+                st->pln = g.n;
+                st->n = g.nl_next;
+                st->off = g.off_next;
+                st->gn = g.gnew;
             } else {
-                st->tail_total += st->m;
-                st->n = st->new_n;
+                st->tail_total = g.tail_total + g.m;
+                st->n = g.new_n;
             }
         }
     }
-    // this WG's contiguous run of blocks: all flags in one load, then only the dirty ones
+    // this WG's contiguous run of blocks: all flags (and, for `part`, the maxima
+    // kept from before) in one load, then only the dirty ones
     __shared__ uint64_t s_dmask;
+    __shared__ uint64_t s_bm[64];
     const uint32_t per = (tb.nblk + gridDim.x - 1) / gridDim.x;   // <= 64 (host-sized grid)
     const uint32_t b0 = blockIdx.x * per;
     if (threadIdx.x < 64) {
         const uint32_t blk = b0 + threadIdx.x;
-        const bool d = threadIdx.x < per && blk < tb.nblk && tb.dirty[blk];
+        const bool in = threadIdx.x < per && blk < tb.nblk;
+        if (part) s_bm[threadIdx.x] = in ? tb.bmax[blk] : 0ull;
+        const bool d = in && tb.dirty[blk];
         const unsigned long long m = __ballot(d);
         if (threadIdx.x == 0) s_dmask = m;
     }
@@ -435,17 +475,20 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             tb.bmax[blk] = best;
             tb.blive[blk] = live;
             tb.dirty[blk] = 0u;
+            s_bm[blk - b0] = best;
         }
         __syncthreads();
     }
     if (part && threadIdx.x < 64) {   // this workgroup's maximum, for sel_inline
-        const uint32_t blk = b0 + threadIdx.x;
-        uint64_t best = (threadIdx.x < per && blk < tb.nblk) ? tb.bmax[blk] : 0ull;
+        uint64_t best = s_bm[threadIdx.x];
         for (int off = 32; off > 0; off >>= 1) {
             const uint64_t o = __shfl_xor(best, off);
             best = o > best ? o : best;
         }
-        if (threadIdx.x == 0) part[blockIdx.x] = best;
+        if (threadIdx.x == 0) {
+            part[blockIdx.x] = best;
+            if (finish == 2) KTR(5);
+        }
     }
     if (fs.log) {   // last workgroup out selects the next merge
         __shared__ uint32_t s_last;
@@ -1024,6 +1067,13 @@ __device__ __forceinline__ bool sig_has(const uint32_t* __restrict__ sig, uint32
     const uint32_t h = sig_hash(pid), b1 = h & 1023u, b2 = (h >> 16) & 1023u;
     return ((sig[b1 >> 5] >> (b1 & 31u)) & (sig[b2 >> 5] >> (b2 & 31u)) & 1u) != 0u;
 }
+// global signature (k_body): no-return atomics, no test load on the merge's critical path
+__device__ __forceinline__ void sig_or(uint32_t* __restrict__ sig, uint32_t pid) {
+    const uint32_t h = sig_hash(pid), b1 = h & 1023u, b2 = (h >> 16) & 1023u;
+    atomicOr(&sig[b1 >> 5], 1u << (b1 & 31u));
+    atomicOr(&sig[b2 >> 5], 1u << (b2 & 31u));
+}
+// LDS signature (k_sp_bits): test first, most bits are already set
 __device__ __forceinline__ void sig_set(uint32_t* __restrict__ sig, uint32_t pid) {
     const uint32_t h = sig_hash(pid), b1 = h & 1023u, b2 = (h >> 16) & 1023u;
     const uint32_t m1 = 1u << (b1 & 31u), m2 = 1u << (b2 & 31u);
@@ -1085,11 +1135,11 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uin
                         const uint32_t t2 = h[j + 1] ? nw : ti;
                         if (t2) {
                             lds_add(lt, tb, st, (nw << 16) | t2, 1u);
-                            sig_set(sig, (nw << 16) | t2);
+                            sig_or(sig, (nw << 16) | t2);
                         }
                     } else if (h[j + 1] && tp) {
                         lds_add(lt, tb, st, (tp << 16) | nw, 1u);
-                        sig_set(sig, (tp << 16) | nw);
+                        sig_or(sig, (tp << 16) | nw);
                     }
                 }
             }
@@ -1146,14 +1196,15 @@ __device__ __forceinline__ uint32_t lane_mask_n(uint64_t i0, uint64_t lim, int n
 }
 
 template <typename S, bool EXACT, int BT>
-__device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __restrict__ zo, ZoneLds<S, BT>& L,
+__device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
+                         S* __restrict__ zo, ZoneLds<S, BT>& L,
                          LdsTab<LTAB_T>& lt, const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
                          uint64_t* __restrict__ bytes) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     constexpr int ZPT = ZoneDim<S, BT>::ZPT;
     constexpr int V = ZPT * sizeof(S) / 16;  // 16-byte vectors per thread
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const uint32_t z = zst->n;
+    const uint32_t z = zs.n;   // launch snapshots (LDS): no state round trip before the zone loads
     const uint32_t lim = EXACT ? z : z - mc;
     const uint32_t pid_ab = (a << 16) | b;
     const uint32_t i0 = (uint32_t)t * ZPT;
@@ -1171,7 +1222,7 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
         for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
     }
     if (!EXACT) {   // window source: global n - 2mc in the previous stream (sharded: it began at poff, now off)
-        const uint64_t src0 = (uint64_t)st->n + st->off - st->poff - 2ull * mc - st->Bp;
+        const uint64_t src0 = (uint64_t)gs.n + gs.off - gs.poff - 2ull * mc - gs.Bp;
         for (uint32_t u = t; u < mc; u += BT) L.wb[u] = zo[src0 + u];
     }
     lds_clear(lt);
@@ -1262,7 +1313,7 @@ __device__ void zone_one(DevState* st, DevState* zst, S* __restrict__ zc, S* __r
         zst->m = m;
         zst->valid_total = Kz + m + 1u;   // survivors + 1 (k_refresh checks it against the new layout)
         // zone read, window source read, kept survivors + window written
-        *bytes += (uint64_t)sizeof(S) * ((uint64_t)z + (EXACT ? 0u : mc) + Kz + m);
+        atomicAdd(bytes, (uint64_t)sizeof(S) * ((uint64_t)z + (EXACT ? 0u : mc) + Kz + m));
     }
 }
 
@@ -1286,19 +1337,28 @@ template <int BT>
 __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
                            uint32_t round, bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
                            uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc,
-                           const SelShard sh = SelShard()) {
+                           const DevState*& gsnap, const DevState*& zsnap, const SelShard sh = SelShard()) {
     __shared__ uint64_t s_red[BT / 64];
-    __shared__ uint32_t s_ok;
+    constexpr int NW = sizeof(DevState) / 4;
+    __shared__ union {
+        DevState d;
+        uint32_t w[NW];
+    } s_g, s_z;
     const int t = threadIdx.x;
-    if (t == 0)
-        s_ok = (round < st->budget && st->merges_done == round && !st->stop && !st->sp_abort && !st->stall) ? 1u : 0u;
-    __syncthreads();
-    if (!s_ok) return false;
+    // the partial maxima and snapshots of both states load together (one round
+    // trip, not one per field)
+    if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
+    else if (zst && t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
     uint64_t best = 0;
     for (uint32_t i = t; i < npart; i += BT) {
         const uint64_t v = part[i];
         best = v > best ? v : best;
     }
+    __syncthreads();
+    const DevState& g = s_g.d;
+    gsnap = &s_g.d;
+    zsnap = &s_z.d;
+    if (!(round < g.budget && g.merges_done == round && !g.stop && !g.sp_abort && !g.stall)) return false;
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t o = __shfl_xor(best, off);
         best = o > best ? o : best;
@@ -1312,12 +1372,12 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     const uint32_t pid = ~(uint32_t)best;
     a = pid >> 16;
     b = pid & 0xFFFFu;
-    nw = st->next_id;
+    nw = g.next_id;
     const bool stop = mc < 2u || nw > 0xFFFFu;                                          // train.wgsl:345-348
-    const bool bad = !stop && !exact && st->is_last &&
-                     (uint64_t)st->n + st->off - st->poff < 2ull * mc + st->Bp;   // cannot happen
+    const bool bad = !stop && !exact && g.is_last &&
+                     (uint64_t)g.n + g.off - g.poff < 2ull * mc + g.Bp;   // cannot happen
     const bool abort = !stop && !bad && !exact &&
-                       ((uint64_t)st->zlast < 5ull * mc + 2u || (sh.zmax && st->zlast > sh.zmax));   // zone misfit
+                       ((uint64_t)g.zlast < 5ull * mc + 2u || (sh.zmax && g.zlast > sh.zmax));   // zone misfit
     const uint32_t need = 6u * mc + 64u;   // distinct deltas of one merge <= 4 per site + tail + window
     const bool stall = !stop && !bad && !abort && sh.cap_list && need > sh.cap_list;
     const bool go = !stop && !bad && !abort && !stall;
@@ -1335,7 +1395,7 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
                 st->need_l = need;
                 st->need_w = 0u;
             } else {
-                if (sh.nlog) sh.nlog[round] = st->n;
+                if (sh.nlog) sh.nlog[round] = g.n;
                 if (sh.rec) {
                     sh.rec[H_L] = 0u;
                     st->dcount = 0u;
@@ -1359,12 +1419,12 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
                 st->b = b;
                 st->nw = nw;
                 st->mc = mc;
-                st->new_n = st->n - mc;
+                st->new_n = g.n - mc;
                 zst->a = a;
                 zst->b = b;
                 zst->nw = nw;
                 zst->mc = mc;
-                zst->new_n = exact ? zst->n : zst->n - mc;
+                zst->new_n = exact ? s_z.d.n : s_z.d.n - mc;
                 if (!zone1) {   // zone_one (another workgroup of this launch) sets both itself
                     zst->m = 0u;
                     zst->valid_total = 0u;
@@ -1374,8 +1434,8 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
             }
         }
         if (go) {   // group sums of a multi-tile zone pass start at zero
-            const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(zst->n, TILE), GRP);
-            for (uint32_t g = t; g < ngrp; g += BT) grpsum[g * GSTR] = 0u;
+            const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(s_z.d.n, TILE), GRP);
+            for (uint32_t q = t; q < ngrp; q += BT) grpsum[q * GSTR] = 0u;
         }
     }
     return go;
@@ -1404,16 +1464,27 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     __shared__ ZoneLds<S, BT> zl;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     uint32_t a, b, nw, mc;
-    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, sh)) return;
+    if (t == 0) KT(0);
+    const DevState *gs, *zs;   // this workgroup's snapshots of the states at launch (LDS)
+    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh)) return;
+    if (t == 0) KT(1);
     // deltas go to the replica (single GPU) or to the per-merge delta table (sharded)
     if (zone1 && blockIdx.x == nbody) {
-        zone_one<S, EXACT, BT>(st, zst, zcur, (S*)zoth, zl, lt, dtb, a, b, nw, mc, wg_bytes + nbody);
+        zone_one<S, EXACT, BT>(st, zst, *gs, *zs, zcur, (S*)zoth, zl, lt, dtb, a, b, nw, mc, wg_bytes + nbody);
+        if (t == 0) {
+            KT(5);
+            KTV(6, 2);
+        }
         return;
     }
     if (blockIdx.x >= nbody) {
-        const uint64_t src0 = (uint64_t)st->n + st->off - st->poff - 2ull * mc - st->Bp;
+        const uint64_t src0 = (uint64_t)gs->n + gs->off - gs->poff - 2ull * mc - gs->Bp;
         const uint64_t stride = (uint64_t)(gridDim.x - nbody) * BT;
         for (uint64_t u = (uint64_t)(blockIdx.x - nbody) * BT + t; u < mc; u += stride) wtmp[u] = zoth[src0 + u];
+        if (t == 0) {
+            KT(5);
+            KTV(6, 3);
+        }
         return;
     }
     const uint32_t pid_ab = (a << 16) | b;
@@ -1437,8 +1508,15 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     }
     __syncthreads();
     const uint32_t ntok = s_ntok;
-    if (ntok == 0) return;
-    if (t == 0) wg_bytes[blockIdx.x] += 16ull * ntok;   // extents + signature words read
+    if (t == 0) KT(2);
+    if (ntok == 0) {
+        if (t == 0) {
+            KT(5);
+            KTV(6, 0);
+        }
+        return;
+    }
+    if (t == 0) atomicAdd(&wg_bytes[blockIdx.x], 16ull * ntok);   // extents + signature words read (no-return add: no round trip)
     for (uint32_t j = t; j < ntok; j += BT) {   // signature filter; the sector's extent loads alongside
         const uint32_t sct = s_tok[j];
         const uint2 e = sec[sct];
@@ -1450,7 +1528,14 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     }
     __syncthreads();
     const uint32_t ncand = s_n;
-    if (ncand == 0) return;
+    if (t == 0) KT(3);
+    if (ncand == 0) {
+        if (t == 0) {
+            KT(5);
+            KTV(6, 0);
+        }
+        return;
+    }
     if (t == 0 && clog) atomicAdd(&st->cand, ncand);
     lds_clear(lt);
     __syncthreads();
@@ -1471,6 +1556,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
             }
         }
     }
+    if (t == 0) KT(4);
     lds_flush(lt, dtb, st);
     if (lane == 0) {
         s_rm[wid] = removed;
@@ -1485,7 +1571,9 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
             mv += s_mv[w2];
         }
         if (r) atomicAdd(&st->body_rm, r);
-        wg_bytes[blockIdx.x] += mv;   // this workgroup's own counter
+        atomicAdd(&wg_bytes[blockIdx.x], mv);   // this workgroup's own counter
+        KT(5);
+        KTV(6, 1 | (ncand << 8));
     }
 }
 
@@ -2299,6 +2387,19 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     hs->budget = k;
     TR_HIP(t, hipMemcpyAsync(&t->st->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     TR_HIP(t, hipMemcpyAsync(&t->st->budget, &hs->budget, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+#ifdef GBPE_KTRACE
+    if (getenv("GBPE_KTRACE_OUT")) {
+        static unsigned long long* kbuf = nullptr;
+        if (!kbuf) {
+            const size_t nb = (size_t)(KT_MERGES / KT_EVERY) * 2 * KT_WG * KT_SLOTS * 8;
+            TR_HIP(t, hipMalloc(&kbuf, nb));
+            TR_HIP(t, hipMemsetAsync(kbuf, 0, nb, s));
+            TR_HIP(t, hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ktr), &kbuf, sizeof(kbuf), 0, hipMemcpyHostToDevice, s));
+        }
+        const uint32_t kb = (uint32_t)t->done;
+        TR_HIP(t, hipMemcpyToSymbolAsync(HIP_SYMBOL(g_kt_base), &kb, 4, 0, hipMemcpyHostToDevice, s));
+    }
+#endif
     if (t->sp) {
         hs->sel_round = 0;
         TR_HIP(t, hipMemcpyAsync(&t->zst->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
@@ -2558,6 +2659,22 @@ extern "C" int gbpe_trainer_pair_counts(gbpe_trainer* t, uint32_t* pids, uint32_
 extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     if (!t) return;
     if (t->ctx && t->ctx->stream) hipStreamSynchronize(t->ctx->stream);
+#ifdef GBPE_KTRACE
+    if (const char* path = getenv("GBPE_KTRACE_OUT")) {   // one file per trainer: path.<done merges>
+        std::vector<unsigned long long> h((size_t)(KT_MERGES / KT_EVERY) * 2 * KT_WG * KT_SLOTS);
+        unsigned long long* kbuf = nullptr;
+        if (hipMemcpyFromSymbol(&kbuf, HIP_SYMBOL(g_ktr), sizeof(kbuf), 0, hipMemcpyDeviceToHost) == hipSuccess && kbuf &&
+            hipMemcpy(h.data(), kbuf, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            char fn[512];
+            snprintf(fn, sizeof(fn), "%s.%llu", path, (unsigned long long)t->done);
+            if (FILE* f = fopen(fn, "wb")) {
+                fwrite(h.data(), 8, h.size(), f);
+                fclose(f);
+            }
+        }
+        if (kbuf) hipMemset(kbuf, 0, h.size() * 8);
+    }
+#endif
     for (auto& e : t->evs)
         if (e) hipEventDestroy(e);
     hipFree(t->buf[0]);

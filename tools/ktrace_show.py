@@ -1,0 +1,53 @@
+"""Per-phase timeline of the sector-sparse kernels from a -DGBPE_KTRACE build
+(tools/ktrace.sh): every 16th merge, each workgroup's wall-clock stamps (100 MHz).
+Times in µs from the first k_body workgroup start; medians over merge buckets.
+
+  start_max  last k_body workgroup to start      sel     last to finish selection
+  zone       zone workgroup end                  hit_*   workgroups with candidate sectors:
+  idle_end   last workgroup without candidates   end     cand / sig / sectors done, end (max)
+  ref_*      k_refresh first start, last end     nhit, ncand  workgroups with candidates, sectors
+
+usage: python tools/ktrace_show.py <dump file>
+"""
+import os
+import sys
+
+import numpy as np
+
+EVERY, WG, SLOTS, HZ = 16, 2048, 8, 100e6
+
+
+def main():
+    raw = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 2 * WG, SLOTS)
+    rows = []
+    for i in range(raw.shape[0]):
+        body, ref = raw[i, :WG], raw[i, WG:]
+        on = body[:, 0] > 0
+        if not on.any():
+            continue
+        b = body[on].astype(np.float64)
+        t0 = b[:, 0].min()
+        us = lambda x: (x - t0) / HZ * 1e6
+        role = body[on, 6] & 0xFF
+        hit, idle, zone = role == 1, (role == 0) & (b[:, 5] > 0), role == 2
+        r = ref[ref[:, 0] > 0].astype(np.float64)
+        mx = lambda m, c: us(b[m, c].max()) if m.any() else np.nan
+        rows.append([i * EVERY, us(b[:, 0].max()), us(b[b[:, 1] > 0, 1].max()), mx(zone, 5), mx(idle, 5),
+                     mx(hit, 2), mx(hit, 3), mx(hit, 4), mx(hit, 5),
+                     us(r[:, 0].min()) if len(r) else np.nan, us(r[:, 5].max()) if len(r) else np.nan,
+                     hit.sum(), (body[on, 6][hit] >> 8).sum(), on.sum()])
+    a = np.array(rows)
+    names = ["start_max", "sel", "zone", "idle_end", "hit_cand", "hit_sig", "hit_sect", "hit_end", "ref_start",
+             "ref_end", "nhit", "ncand", "nwg"]
+    edges = [int(e) for e in os.environ.get("EDGES", "0,150,300,500,1000,2000,4000,8000,16000,24000,40000").split(",")]
+    print(f"{'merges':<13}{'n':>5}" + "".join(f"{k:>10}" for k in names))
+    for lo, hi in zip(edges[:-1], edges[1:]):
+        sel = (a[:, 0] >= lo) & (a[:, 0] < hi)
+        if not sel.any():
+            continue
+        med = [np.nanmedian(a[sel, j]) if np.isfinite(a[sel, j]).any() else np.nan for j in range(1, a.shape[1])]
+        print(f"{lo:>6}-{hi:<6}{int(sel.sum()):>5}" + "".join(f"{v:>10.2f}" for v in med))
+
+
+if __name__ == "__main__":
+    main()
