@@ -805,6 +805,117 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
     }
 }
 
+// k_delta over TPW consecutive tiles per workgroup, one LDS delta table for all
+// of them, flushed once: the dense loop's early merges (10^5-10^6 sites) add to
+// the same hot pairs from every tile, and same-address device atomics serialise
+// at the memory side, so TPW x fewer flushes is TPW x fewer of them.  Same
+// per-tile outputs and delta rule as k_delta.
+template <typename S, bool EXACT, int DELTA_TPW>
+__global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, const S* cur, Table tb,
+                                                  uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
+                                                  uint32_t* __restrict__ grpsum, uint32_t eager_tiles) {
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    __shared__ LdsTab<LTAB_Z> lt;
+    __shared__ uint32_t red[TPB / 64];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint4 s0 = reinterpret_cast<const uint4*>(st)[0];   // n, stop, next_id, a
+    const uint4 s1 = reinterpret_cast<const uint4*>(st)[1];   // b, nw, mc, new_n
+    const uint2 s2 = reinterpret_cast<const uint2*>(st)[4];   // m, merges_done
+    const uint32_t n = s0.x, a = s0.w, b = s1.x, nw = s1.y, new_n = s1.w;
+    const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
+    if (s0.y || s2.y != round + 1u) return;   // merge_active()
+    const uint32_t pid_ab = (a << 16) | b;
+    const uint32_t lim = EXACT ? 0xFFFFFFFFu : new_n;
+    lds_clear(lt);
+    __syncthreads();
+    uint32_t tail = 0;
+    for (int q = 0; q < DELTA_TPW; ++q) {
+        const uint32_t tl = blockIdx.x * DELTA_TPW + q;
+        if (tl >= ntiles || (tl >= eager_tiles && (uint64_t)tl * TILE >= n)) break;   // block-uniform
+        const uint64_t base = (uint64_t)tl * TILE;
+        const uint64_t i0 = base + (uint64_t)t * EPT;
+        uint32_t x[EPT];
+        uint32_t lh = 0, rh = 0;
+        {
+            const uint64_t hi = i0 >= 2 ? i0 - 2 : 0;
+            if (sizeof(S) == 2) {
+                lh = *reinterpret_cast<const uint32_t*>(cur + hi);
+            } else {
+                const uint2 v2 = *reinterpret_cast<const uint2*>(cur + hi);
+                lh = v2.x;
+                rh = v2.y;
+            }
+        }
+        const uint32_t nxr = (uint32_t)cur[i0 + EPT];
+        load_own(cur, i0, x);
+        uint32_t xm2 = sizeof(S) == 2 ? (lh & 0xFFFFu) : lh;
+        uint32_t xm1 = sizeof(S) == 2 ? (lh >> 16) : rh;
+        if (i0 < 2) xm2 = xm1 = 0;
+        uint32_t eb = 0, ea = 0;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            eb |= (x[k] == b ? 1u : 0u) << k;
+            ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
+        }
+        const uint32_t inb = lane_mask32(i0, n);
+        const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;
+        const uint32_t h_m1 = (xm1 == b && (xm2 & TM) == a && i0 - 1 < n) ? 1u : 0u;
+        const uint32_t h_32 = (nxr == b && (ea >> (EPT - 1)) && i0 + EPT < n) ? 1u : 0u;
+        const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (EPT + 1));
+        uint32_t cnt = __popc(inb & ~hitm);
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+        if (hbits != 0 || (i0 + EPT > lim && i0 < n)) {
+            const uint32_t below = lane_mask32(i0, lim);
+            tail += __popc(inb & ~hitm & ~below);
+            uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+            while (rel) {
+                const int k = __ffs(rel) - 1;
+                rel &= rel - 1;
+                const uint64_t i = i0 + k;
+                if (i == 0) continue;
+                const uint32_t xi = cur[i], xp = cur[i - 1];
+                if (xi & WS) continue;
+                const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+                const uint32_t tp = xp & TM, ti = xi & TM;
+                if (tp && ti) {
+                    const uint32_t pid = (tp << 16) | ti;
+                    if (pid != pid_ab) lds_add(lt, tb, st, pid, 0xFFFFFFFFu);
+                }
+                if (!h0 && i < lim) {
+                    if (hm) {
+                        const uint32_t t2 = hp ? nw : ti;
+                        if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+                    } else if (hp && tp) {
+                        lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+                    }
+                }
+            }
+        }
+        if (!EXACT && base + TILE > lim && base < n) {   // stale tail: old pairs destroyed
+            const uint64_t hi = (uint64_t)n < base + TILE ? (uint64_t)n : base + TILE;
+            for (uint64_t i = (lim > base ? (uint64_t)lim : base) + t; i < hi; i += TPB) {
+                if (i == 0) continue;
+                const uint32_t xi = cur[i];
+                if (xi & WS) continue;
+                const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
+                if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+            }
+        }
+        if (i0 < n) hitmask[(uint64_t)tl * TPB + t] = hitm;
+        if (lane == 0) red[wid] = cnt;
+        __syncthreads();
+        if (t == 0) {
+            const uint32_t tot = red[0] + red[1] + red[2] + red[3];
+            tile_cnt[tl] = tot;
+            atomicAdd(&grpsum[(tl / GRP) * GSTR], tot);
+        }
+        __syncthreads();   // red[] is rewritten by the next tile
+    }
+    lds_flush(lt, tb, st);
+    for (int off = 32; off > 0; off >>= 1) tail += __shfl_xor(tail, off);
+    if (lane == 0 && tail) atomicAdd(&st->m, tail);
+}
+
 // Pass 2.  Blocks [0, ntiles): in-place A-side rewrite (train.wgsl:486-487) +
 // scatter of the survivors with old index < new_n (the reference bound,
 // train.wgsl:727; all of them with EXACT) at tile prefix = group sums + the
@@ -1770,6 +1881,8 @@ struct gbpe_trainer {
     uint32_t* d_u32 = nullptr;   // small device scratch
     uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
     uint64_t* wg_bytes = nullptr;   // bytes moved per k_body workgroup (each its own counter)
+    uint32_t delta_mt = 2048;       // dense k_delta: multi-tile workgroups from this many tiles (0 = never; GBPE_DELTA_MT)
+    uint32_t delta_tpw = 8;         // ... of 8, 16 or 32 tiles (GBPE_DELTA_TPW)
     uint64_t wg_cap = 0;
     double ms_sparse = 0, ms_dense = 0;   // GBPE_TRAIN_TIMING: merge passes (without selection / refresh) by mode
     double ms_body = 0;          // GBPE_TRAIN_TIMING: k_body alone
@@ -1842,15 +1955,29 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
         hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
                            (uint32_t*)nullptr, (uint32_t*)nullptr, (DevState*)nullptr, exact ? 1u : 0u);
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
+    // many tiles: TPW tiles per k_delta workgroup (fewer hot-pair flushes)
+    const bool mt = t->delta_mt && g_delta >= t->delta_mt;
+    const uint32_t tpw = t->delta_tpw;
+    const uint32_t g_mt = (uint32_t)gbpe_div_up(g_delta, tpw);
     if (exact) {
-        hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
-                           t->hitmask, t->tile_cnt, t->grpsum, g_delta);
+        if (mt)
+            hipLaunchKernelGGL(tpw == 32 ? (k_delta_mt<S, true, 32>) : tpw == 16 ? (k_delta_mt<S, true, 16>) : (k_delta_mt<S, true, 8>),
+                               dim3(g_mt), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask, t->tile_cnt,
+                               t->grpsum, g_delta);
+        else
+            hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
+                               t->hitmask, t->tile_cnt, t->grpsum, g_delta);
         if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
         hipLaunchKernelGGL((k_compact<S, true>), dim3(g_compact), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
     } else {
-        hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
-                           t->hitmask, t->tile_cnt, t->grpsum, g_delta);
+        if (mt)
+            hipLaunchKernelGGL(tpw == 32 ? (k_delta_mt<S, false, 32>) : tpw == 16 ? (k_delta_mt<S, false, 16>) : (k_delta_mt<S, false, 8>),
+                               dim3(g_mt), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask, t->tile_cnt,
+                               t->grpsum, g_delta);
+        else
+            hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
+                               t->hitmask, t->tile_cnt, t->grpsum, g_delta);
         if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
         hipLaunchKernelGGL((k_compact<S, false>), dim3(g_compact), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
@@ -2220,6 +2347,11 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     if (const char* e = getenv("GBPE_FUSE_SELECT")) t->fuse_sel = atoi(e) != 0;
     if (const char* e = getenv("GBPE_REFRESH_BLOCKS")) t->refresh_blocks = (uint32_t)atoi(e);
     if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_DELTA_MT")) t->delta_mt = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_DELTA_TPW")) {
+        const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
+        t->delta_tpw = v >= 32 ? 32 : v >= 16 ? 16 : 8;
+    }
     if (t->sp_zt < 5) t->sp_zt = 5;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
         t->trace = fopen(e, "w");

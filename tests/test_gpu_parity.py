@@ -106,6 +106,22 @@ def test_train_matches_oracle(eng, kind, size, target, exact):
         assert st.tail_dropped == sum(ref["tail_drops"])
 
 
+@pytest.mark.parametrize("exact", [False, True])
+def test_train_multitile_delta(eng, monkeypatch, exact):
+    # GBPE_DELTA_MT=1: every dense merge runs k_delta_mt (8 tiles per workgroup,
+    # the last workgroup partial), which the library otherwise keeps for >= 2048 tiles
+    from gpubpe import synth
+    monkeypatch.setenv("GBPE_DELTA_MT", "1")
+    data = synth.english(300000, seed=41)
+    ref = O.train(data, 1500, compaction="exact" if exact else "reference")
+    m, s, pairs, st = _train_native(eng, data, 1500, exact=exact, sparse="dense")
+    assert m == ref["merges"]
+    assert np.array_equal(s, ref["symbols"])
+    _assert_counts_match_stream(pairs, s)
+    if not exact:
+        assert st.tail_dropped == sum(ref["tail_drops"])
+
+
 def test_u32_symbol_path(eng):
     # target > 32768 forces 32-bit symbols (bit 16 = word start)
     from gpubpe import synth
