@@ -1782,6 +1782,46 @@ __global__ __launch_bounds__(TPB) void k_sp_bits(const S* __restrict__ body, con
     if (live && lane < (int)SP_SIGW) sig[(uint64_t)k * SP_SIGW + lane] = ssig[wid][lane];
 }
 
+// token bitmap of whole columns (a full rebuild over a zeroed bitmap): one
+// workgroup per 32-sector column gathers token -> sector mask in LDS, then
+// writes each present token's word once (plain stores; the column is its own).
+// Tokens beyond the LDS table's reach take a global atomicOr instead.
+constexpr int COLT = 8192;
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_colbits(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t nsec,
+                                                    uint32_t* __restrict__ bits, uint32_t W) {
+    __shared__ uint32_t key[COLT], msk[COLT];
+    for (int i = threadIdx.x; i < COLT; i += TPB) {
+        key[i] = 0xFFFFFFFFu;
+        msk[i] = 0u;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t c = blockIdx.x;
+    for (uint32_t q = wid; q < 32; q += TPB / 64) {
+        const uint32_t k = c * 32 + q;
+        if (k >= nsec) break;
+        const uint2 e = sec[k];
+        for (uint32_t j = lane; j < e.y; j += 64) {
+            const uint32_t tok = body[e.x + j] & Sym<S>::TM;
+            uint32_t h = gbpe_fmix32(tok) & (COLT - 1);
+            bool done = false;
+            for (int p = 0; p < 32 && !done; ++p) {
+                const uint32_t o = atomicCAS(&key[h], 0xFFFFFFFFu, tok);
+                if (o == 0xFFFFFFFFu || o == tok) {
+                    atomicOr(&msk[h], 1u << q);
+                    done = true;
+                }
+                h = (h + 1) & (COLT - 1);
+            }
+            if (!done) atomicOr(&bits[(uint64_t)tok * W + c], 1u << q);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < COLT; i += TPB)
+        if (key[i] != 0xFFFFFFFFu) atomicOr(&bits[(uint64_t)key[i] * W + c], msk[i]);
+}
+
 // sparse → dense: sector counts, then a gather at the scanned offsets (one wave per sector)
 __global__ void k_sp_counts(const uint2* __restrict__ sec, uint32_t nsec, uint32_t* __restrict__ cnt) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2088,8 +2128,15 @@ int sp_add_sectors(gbpe_trainer* t, uint32_t base, uint32_t len) {
                        t->sp_secw, t->sp_loc, nw);
     hipLaunchKernelGGL(k_sp_sector_len, dim3((uint32_t)gbpe_div_up(nw, 256)), dim3(256), 0, s, (const uint32_t*)t->sp_loc,
                        nw, base + len, t->sec + t->nsec);
-    hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(nw, TPB / 64)), dim3(TPB), 0, s, body,
-                       (const uint2*)t->sec, t->nsec, nw, t->bits, t->W, t->sig);
+    if (t->nsec == 0) {   // a fresh build (sp_enter): whole columns
+        hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(nw, TPB / 64)), dim3(TPB), 0, s, body,
+                           (const uint2*)t->sec, 0u, nw, (uint32_t*)nullptr, t->W, t->sig);
+        hipLaunchKernelGGL(k_sp_colbits<S>, dim3((uint32_t)gbpe_div_up(nw, 32)), dim3(TPB), 0, s, body,
+                           (const uint2*)t->sec, nw, t->bits, t->W);
+    } else {
+        hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(nw, TPB / 64)), dim3(TPB), 0, s, body,
+                           (const uint2*)t->sec, t->nsec, nw, t->bits, t->W, t->sig);
+    }
     GBPE_LAUNCH_CHECK(t->ctx);
     t->nsec += nw;
     t->bend = base + len;
@@ -2101,10 +2148,13 @@ int sp_add_sectors(gbpe_trainer* t, uint32_t base, uint32_t len) {
 template <typename S>
 int sp_filters(gbpe_trainer* t, bool with_bits) {
     hipStream_t s = t->ctx->stream;
-    if (with_bits) TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
     hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(t->nsec, TPB / 64)), dim3(TPB), 0, s,
-                       (const S*)t->buf[t->bcur], (const uint2*)t->sec, 0u, t->nsec, with_bits ? t->bits : nullptr, t->W,
-                       t->sig);
+                       (const S*)t->buf[t->bcur], (const uint2*)t->sec, 0u, t->nsec, (uint32_t*)nullptr, t->W, t->sig);
+    if (with_bits) {
+        TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
+        hipLaunchKernelGGL(k_sp_colbits<S>, dim3((uint32_t)gbpe_div_up(t->nsec, 32)), dim3(TPB), 0, s,
+                           (const S*)t->buf[t->bcur], (const uint2*)t->sec, t->nsec, t->bits, t->W);
+    }
     GBPE_LAUNCH_CHECK(t->ctx);
     t->sp_age = 0;
     if (with_bits) t->sp_bits_age = 0;
