@@ -1932,7 +1932,7 @@ struct gbpe_trainer {
     uint32_t sp_enters = 0, sp_exits = 0;
     uint32_t sp_div = 64;        // enter when last_mc * sp_div <= n
     uint32_t sp_cooldown = 0;    // steps to stay dense after an abort
-    uint32_t sp_zt = 10;         // zone target = sp_zt * last_mc + 64 (>= 5: see sp_enter)
+    uint32_t sp_zt = 7;          // zone target = sp_zt * last_mc + 64 (>= 5: see sp_enter; 7 measured best, GBPE_SPARSE_ZT)
     bool fuse_sel = false;       // GBPE_FUSE_SELECT=1: select in k_refresh's last workgroup (measured slower: DESIGN §2b)
     uint32_t refresh_blocks = 0; // GBPE_REFRESH_BLOCKS: k_refresh grid (0 = 2 per CU)
     bool use_graph = false;      // replay steps as HIP graphs (GBPE_GRAPH=1): measured slower on ROCm 7
@@ -2162,8 +2162,10 @@ int sp_filters(gbpe_trainer* t, bool with_bits) {
 }
 
 // dense → sparse at a step boundary.  The zone is the stream from the last word
-// start at or before n - zt (zt = 10 * last_mc + 64 >= 5 * the next merge's
-// count); the dense stale buffer's tail becomes the zone's stale buffer.
+// start at or before n - zt (zt = sp_zt * last_mc + 64: >= 5 x the next merge's
+// count while counts fall; a merge that would not fit is not run and the host
+// goes dense, sp_abort); the dense stale buffer's tail becomes the zone's stale
+// buffer.
 template <typename S>
 int sp_enter(gbpe_trainer* t, bool with_zone = true) {
     hipStream_t s = t->ctx->stream;
