@@ -115,7 +115,7 @@ static_assert(sizeof(DevState) <= 256, "state");
 // would serialise the launch): k_body workgroups at [m][wg][slot], k_refresh
 // workgroups at [m][KT_WG + wg][slot].
 #ifdef GBPE_KTRACE
-constexpr uint32_t KT_MERGES = 40000, KT_EVERY = 16, KT_WG = 2048, KT_SLOTS = 8;
+constexpr uint32_t KT_MERGES = 40000, KT_EVERY = 16, KT_WG = 2048, KT_SLOTS = 12;
 __device__ unsigned long long* g_ktr;
 __device__ uint32_t g_kt_base;
 __device__ __forceinline__ void kt_put(uint32_t round, uint32_t wg, int i, unsigned long long v) {
@@ -1310,7 +1310,8 @@ template <typename S, bool EXACT, int BT>
 __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
                          S* __restrict__ zo, ZoneLds<S, BT>& L,
                          LdsTab<LTAB_T>& lt, const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
-                         uint64_t* __restrict__ bytes) {
+                         uint64_t* __restrict__ bytes, uint32_t round) {
+    (void)round;   // phase stamps only (-DGBPE_KTRACE)
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     constexpr int ZPT = ZoneDim<S, BT>::ZPT;
     constexpr int V = ZPT * sizeof(S) / 16;  // 16-byte vectors per thread
@@ -1338,6 +1339,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
     }
     lds_clear(lt);
     __syncthreads();
+    if (t == 0) KT(2);
     const uint32_t xm2 = i0 >= 2 ? (uint32_t)xs[i0 - 2] : 0u, xm1 = i0 >= 1 ? (uint32_t)xs[i0 - 1] : 0u;
     const uint32_t nxr = i0 + ZPT < z ? (uint32_t)xs[i0 + ZPT] : 0u;
     uint32_t eb = 0, ea = 0;
@@ -1381,6 +1383,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
             }
         }
     }
+    if (t == 0) KT(3);
     // block exclusive scan of the kept counts; tail survivors sum to m
     const uint32_t kc = __popc(keep);
     uint32_t incl = kc, tl = __popc(surv & ~below);
@@ -1392,6 +1395,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
     if (lane == 63) L.wsum[wid] = incl;
     if (lane == 0) L.wtail[wid] = tl;
     __syncthreads();
+    if (t == 0) KT(7);
     uint32_t pre = incl - kc, Kz = 0, m = 0;
 #pragma unroll
     for (int w2 = 0; w2 < BT / 64; ++w2) {
@@ -1399,6 +1403,9 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
         Kz += L.wsum[w2];
         m += L.wtail[w2];
     }
+    // the new zone is assembled in LDS over the old copy (every read of it is
+    // done) and leaves in whole 16-byte stores: per-symbol global stores at a
+    // lane stride of ZPT symbols cost a cache line per lane and instruction
 #pragma unroll
     for (int k = 0; k < ZPT; ++k) {
         const bool rw = (rwm >> k) & 1u;
@@ -1406,19 +1413,30 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
         if (rw) zc[i0 + k] = (S)v;                  // the reference's in-place ping buffer
         if ((keep >> k) & 1u) {
             if (pre == Kz - 1) L.left = v;         // the survivor just before the window
-            zo[pre++] = (S)v;
+            xs[pre++] = (S)v;
         }
     }
+    if (t == 0) KT(8);
     if (!EXACT && m) {
         __syncthreads();
         const uint32_t woff = mc - m;
         for (uint32_t j = t; j < m; j += BT) {
             const uint32_t x1 = L.wb[woff + j];
             const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : L.left;
-            zo[Kz + j] = (S)x1;
+            xs[Kz + j] = (S)x1;
             if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) lds_add(lt, tb, st, ((x0 & TM) << 16) | (x1 & TM), 1u);
         }
     }
+    __syncthreads();
+    if (t == 0) KT(9);
+    {
+        constexpr uint32_t PV = 16 / sizeof(S);
+        const uint32_t tot = Kz + m, nfull = tot / PV;
+        uint4* dst = reinterpret_cast<uint4*>(zo);
+        for (uint32_t q = t; q < nfull; q += BT) dst[q] = L.xv[q];
+        for (uint32_t j = nfull * PV + t; j < tot; j += BT) zo[j] = xs[j];
+    }
+    if (t == 0) KT(4);
     lds_flush(lt, tb, st);
     if (t == 0) {
         zst->m = m;
@@ -1581,7 +1599,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     if (t == 0) KT(1);
     // deltas go to the replica (single GPU) or to the per-merge delta table (sharded)
     if (zone1 && blockIdx.x == nbody) {
-        zone_one<S, EXACT, BT>(st, zst, *gs, *zs, zcur, (S*)zoth, zl, lt, dtb, a, b, nw, mc, wg_bytes + nbody);
+        zone_one<S, EXACT, BT>(st, zst, *gs, *zs, zcur, (S*)zoth, zl, lt, dtb, a, b, nw, mc, wg_bytes + nbody, round);
         if (t == 0) {
             KT(5);
             KTV(6, 2);

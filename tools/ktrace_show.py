@@ -6,6 +6,8 @@ Times in µs from the first k_body workgroup start; medians over merge buckets.
   zone       zone workgroup end                  hit_*   workgroups with candidate sectors:
   idle_end   last workgroup without candidates   end     cand / sig / sectors done, end (max)
   ref_*      k_refresh first start, last end     nhit, ncand  workgroups with candidates, sectors
+  z_*        zone workgroup (thread 0): selection done, zone loaded, site deltas done, scan, survivors
+             staged, window staged, zone stored (then flush)
 
 usage: python tools/ktrace_show.py <dump file>
 """
@@ -14,7 +16,7 @@ import sys
 
 import numpy as np
 
-EVERY, WG, SLOTS, HZ = 16, 2048, 8, 100e6
+EVERY, WG, SLOTS, HZ = 16, 2048, 12, 100e6
 
 
 def main():
@@ -35,10 +37,11 @@ def main():
         rows.append([i * EVERY, us(b[:, 0].max()), us(b[b[:, 1] > 0, 1].max()), mx(zone, 5), mx(idle, 5),
                      mx(hit, 2), mx(hit, 3), mx(hit, 4), mx(hit, 5),
                      us(r[:, 0].min()) if len(r) else np.nan, us(r[:, 5].max()) if len(r) else np.nan,
-                     hit.sum(), (body[on, 6][hit] >> 8).sum(), on.sum()])
+                     hit.sum(), (body[on, 6][hit] >> 8).sum(), on.sum(),
+                     mx(zone, 1), mx(zone, 2), mx(zone, 3), mx(zone, 7), mx(zone, 8), mx(zone, 9), mx(zone, 4)])
     a = np.array(rows)
     names = ["start_max", "sel", "zone", "idle_end", "hit_cand", "hit_sig", "hit_sect", "hit_end", "ref_start",
-             "ref_end", "nhit", "ncand", "nwg"]
+             "ref_end", "nhit", "ncand", "nwg", "z_sel", "z_load", "z_sites", "z_scan", "z_keep", "z_win", "z_wrote"]
     edges = [int(e) for e in os.environ.get("EDGES", "0,150,300,500,1000,2000,4000,8000,16000,24000,40000").split(",")]
     print(f"{'merges':<13}{'n':>5}" + "".join(f"{k:>10}" for k in names))
     for lo, hi in zip(edges[:-1], edges[1:]):
