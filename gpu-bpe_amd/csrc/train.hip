@@ -116,8 +116,11 @@ static_assert(sizeof(DevState) <= 256, "state");
 // workgroups at [m][KT_WG + wg][slot].
 #ifdef GBPE_KTRACE
 constexpr uint32_t KT_MERGES = 40000, KT_EVERY = 16, KT_WG = 2048, KT_SLOTS = 12;
-__device__ unsigned long long* g_ktr;
-__device__ uint32_t g_kt_base;
+// __constant__: scalar loads the compiler can hoist, so a stamp is a clock read
+// and a store (a __device__ global reloads with a vmcnt wait per stamp, which
+// drained the wave's outstanding stores and inflated every phase by ~1 µs)
+__constant__ unsigned long long* g_ktr;
+__constant__ uint32_t g_kt_base;
 __device__ __forceinline__ void kt_put(uint32_t round, uint32_t wg, int i, unsigned long long v) {
     const uint32_t m = g_kt_base + round;
     if (g_ktr && m < KT_MERGES && m % KT_EVERY == 0 && wg < 2 * KT_WG)
@@ -1297,7 +1300,8 @@ template <typename S, int BT>
 struct ZoneLds {
     uint4 xv[ZoneDim<S, BT>::ZMAX * sizeof(S) / 16];   // the zone (symbol i = ((S*)xv)[i])
     S wb[ZoneDim<S, BT>::ZWIN];
-    uint32_t wsum[BT / 64], wtail[BT / 64], left;
+    uint32_t wsum[BT / 64], wtail[BT / 64];
+    S trash[64];   // the zone pass's unconditional stores of dropped symbols
 };
 
 __device__ __forceinline__ uint32_t lane_mask_n(uint64_t i0, uint64_t lim, int n) {
@@ -1403,18 +1407,33 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
         Kz += L.wsum[w2];
         m += L.wtail[w2];
     }
-    // the new zone is assembled in LDS over the old copy (every read of it is
+    // The new zone is assembled in LDS over the old copy (every read of it is
     // done) and leaves in whole 16-byte stores: per-symbol global stores at a
-    // lane stride of ZPT symbols cost a cache line per lane and instruction
+    // lane stride of ZPT symbols cost a cache line per lane and instruction.
+    // In LDS the 16-byte chunks are XOR-swizzled within groups of 8: lanes
+    // write ZPT symbols apart, which unswizzled lands every lane of a wave on
+    // the same two banks.
+    constexpr uint32_t PV = 16 / sizeof(S), PVL = sizeof(S) == 2 ? 3 : 2;
+    auto swz = [](uint32_t o) -> uint32_t {
+        const uint32_t c = o >> PVL;
+        return ((c ^ ((c >> 3) & 7u)) << PVL) | (o & (PV - 1u));
+    };
+    // branch-free: every position stores (dropped ones into a per-lane trash
+    // slot); the A-side rewrites of the reference's in-place ping buffer are
+    // the only global stores, one per rewritten position
+    uint32_t wsm = 0;
 #pragma unroll
     for (int k = 0; k < ZPT; ++k) {
         const bool rw = (rwm >> k) & 1u;
         const uint32_t v = rw ? (nw | (x[k] & WS)) : x[k];
-        if (rw) zc[i0 + k] = (S)v;                  // the reference's in-place ping buffer
-        if ((keep >> k) & 1u) {
-            if (pre == Kz - 1) L.left = v;         // the survivor just before the window
-            xs[pre++] = (S)v;
-        }
+        wsm |= ((x[k] & WS) ? 1u : 0u) << k;
+        const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
+        S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
+        *dst = (S)v;
+    }
+    for (uint32_t r = rwm; r; r &= r - 1) {
+        const int k = __ffs(r) - 1;
+        zc[i0 + k] = (S)(nw | (((wsm >> k) & 1u) ? WS : 0u));
     }
     if (t == 0) KT(8);
     if (!EXACT && m) {
@@ -1422,19 +1441,19 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
         const uint32_t woff = mc - m;
         for (uint32_t j = t; j < m; j += BT) {
             const uint32_t x1 = L.wb[woff + j];
-            const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : L.left;
-            xs[Kz + j] = (S)x1;
+            // left of the window: the last kept survivor (Kz > 0: the zone holds >= 5 mc)
+            const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : (Kz ? (uint32_t)xs[swz(Kz - 1)] : 0u);
+            xs[swz(Kz + j)] = (S)x1;
             if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) lds_add(lt, tb, st, ((x0 & TM) << 16) | (x1 & TM), 1u);
         }
     }
     __syncthreads();
     if (t == 0) KT(9);
     {
-        constexpr uint32_t PV = 16 / sizeof(S);
         const uint32_t tot = Kz + m, nfull = tot / PV;
         uint4* dst = reinterpret_cast<uint4*>(zo);
-        for (uint32_t q = t; q < nfull; q += BT) dst[q] = L.xv[q];
-        for (uint32_t j = nfull * PV + t; j < tot; j += BT) zo[j] = xs[j];
+        for (uint32_t q = t; q < nfull; q += BT) dst[q] = L.xv[q ^ ((q >> 3) & 7u)];
+        for (uint32_t j = nfull * PV + t; j < tot; j += BT) zo[j] = xs[swz(j)];
     }
     if (t == 0) KT(4);
     lds_flush(lt, tb, st);
