@@ -229,19 +229,51 @@ __device__ __forceinline__ void lds_add(LdsTab<N>& t, const Table& tb, DevState*
     table_add(tb, st, pid, d);   // LDS table crowded: go straight to the global table
 }
 
+// Up to 8 (pid, delta) adds with their home-slot key loads issued together: at
+// the table's low load factor nearly every live pair sits in its home slot, so
+// a batch costs one round trip instead of one per entry; the rest (new keys,
+// collisions) take the full probe.  Entries with pid or delta 0 are skipped.
+__device__ __forceinline__ void table_add8(const Table& tb, DevState* st, const uint32_t (&kk)[8],
+                                           const uint32_t (&vv)[8]) {
+    uint32_t hs[8], hk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        hs[j] = (kk[j] && vv[j]) ? (gbpe_fmix32(kk[j]) & tb.mask) : 0u;
+        hk[j] = __hip_atomic_load(&tb.slots[hs[j]].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (!kk[j] || !vv[j]) continue;
+        if (hk[j] == kk[j]) {
+            atomicAdd(&tb.slots[hs[j]].y, vv[j]);
+            mark_dirty(tb, st, hs[j]);
+        } else {
+            table_add(tb, st, kk[j], vv[j]);
+        }
+    }
+}
+
 // Flush the workgroup's aggregated deltas into the global table.  Small tables
 // (<= 8 slots per thread) are first compacted to a list so every thread does at
 // most a few global adds instead of one per slot it owns: a merge's few live
-// entries then cost one global round trip, not a serial chain.  The table's
-// contents are consumed (callers clear it before reuse).
+// entries then cost one global round trip, not a serial chain.  Large tables
+// (the multi-tile and zone k_delta, the full count) add in batches of 8 per
+// thread (table_add8).  The table's contents are consumed (callers clear it
+// before reuse).
 template <int N>
 __device__ __forceinline__ void lds_flush(LdsTab<N>& t, const Table& tb, DevState* st) {
     __syncthreads();
     const uint32_t nt = blockDim.x;
     if (N > 8 * (int)nt) {
-        for (int i = threadIdx.x; i < N; i += nt) {
-            uint32_t k = t.key[i], v = t.val[i];
-            if (k != 0u && v != 0u) table_add(tb, st, k, v);
+        for (uint32_t i0 = threadIdx.x; i0 < (uint32_t)N; i0 += 8 * nt) {
+            uint32_t kk[8], vv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t i = i0 + j * nt;
+                kk[j] = i < (uint32_t)N ? t.key[i] : 0u;
+                vv[j] = i < (uint32_t)N ? t.val[i] : 0u;
+            }
+            table_add8(tb, st, kk, vv);
         }
         return;
     }
