@@ -469,14 +469,28 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
     }
     __syncthreads();
     uint64_t dm = s_dmask;
-    while (dm) {
-        const uint32_t blk = b0 + (uint32_t)(__ffsll((long long)dm) - 1);
+    // software-pipelined: the next dirty block's slots load while this one reduces
+    constexpr int NV = (1 << BLK_LOG2) / 2 / TPB;   // 16-byte loads per thread
+    uint4 en[NV];
+    uint32_t nblk = 0xFFFFFFFFu;
+    auto fetch = [&]() {
+        if (!dm) {
+            nblk = 0xFFFFFFFFu;
+            return;
+        }
+        nblk = b0 + (uint32_t)(__ffsll((long long)dm) - 1);
         dm &= dm - 1;
-        const uint4* s = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)blk << BLK_LOG2));
-        constexpr int NV = (1 << BLK_LOG2) / 2 / TPB;   // 16-byte loads per thread
+        const uint4* s = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)nblk << BLK_LOG2));
+#pragma unroll
+        for (int k = 0; k < NV; ++k) en[k] = s[threadIdx.x + k * TPB];
+    };
+    fetch();
+    while (nblk != 0xFFFFFFFFu) {
+        const uint32_t blk = nblk;
         uint4 e[NV];
 #pragma unroll
-        for (int k = 0; k < NV; ++k) e[k] = s[threadIdx.x + k * TPB];
+        for (int k = 0; k < NV; ++k) e[k] = en[k];
+        fetch();
         uint64_t best = 0;
         uint32_t live = 0;
 #pragma unroll
