@@ -1241,12 +1241,21 @@ __device__ __forceinline__ void sig_set(uint32_t* __restrict__ sig, uint32_t pid
     if (!(sig[b2 >> 5] & m2)) atomicOr(&sig[b2 >> 5], m2);
 }
 
+// a sector's first wave pass: 4 symbols per lane and the one after the pass
+template <typename S>
+__device__ __forceinline__ void sector_first(const S* __restrict__ p, uint32_t cnt, uint32_t (&f)[5]) {
+    const uint32_t i0 = 4u * (uint32_t)(threadIdx.x & 63);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] = (i0 + k < cnt) ? (uint32_t)p[i0 + k] : 0u;
+    f[4] = (SP_CH < cnt) ? (uint32_t)p[SP_CH] : 0u;
+}
+
 // One wave merges one sector in place (snapshot semantics, k_delta's delta rule,
 // survivors compacted to the sector's front).  Returns the B-sides removed.
 template <typename S>
 __device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uint32_t b, uint32_t nw,
                                 LdsTab<LTAB_T>& lt, const Table& tb, DevState* st, uint32_t* __restrict__ sig,
-                                uint32_t& out_cnt) {
+                                uint32_t& out_cnt, const uint32_t (&first)[5]) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     const int lane = threadIdx.x & 63;
     const uint32_t pid_ab = (a << 16) | b;
@@ -1254,10 +1263,16 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uin
     for (uint32_t c0 = 0; c0 < cnt; c0 += SP_CH) {
         const uint32_t i0 = c0 + 4u * lane;
         // X[0..1] = the two symbols before this lane's four, X[6] = the one after
-        uint32_t X[7];
+        uint32_t X[7], nx;
+        if (c0 == 0) {   // the first pass's symbols were loaded by the caller (sector_first)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) X[2 + k] = (i0 + k < cnt) ? (uint32_t)p[i0 + k] : 0u;
-        const uint32_t nx = (c0 + SP_CH < cnt) ? (uint32_t)p[c0 + SP_CH] : 0u;
+            for (int k = 0; k < 4; ++k) X[2 + k] = first[k];
+            nx = first[4];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) X[2 + k] = (i0 + k < cnt) ? (uint32_t)p[i0 + k] : 0u;
+            nx = (c0 + SP_CH < cnt) ? (uint32_t)p[c0 + SP_CH] : 0u;
+        }
         uint32_t pm1 = __shfl_up(X[5], 1), pm2 = __shfl_up(X[4], 1);
         uint32_t np = __shfl_down(X[2], 1);
         if (lane == 0) {
@@ -1735,11 +1750,18 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     __syncthreads();
     uint32_t removed = 0;
     uint64_t moved = 0;   // sector symbols read + rewritten (wave-uniform)
+    // software-pipelined: a wave's next sector loads while it merges this one
+    uint32_t nf[5];
+    if (wid < ncand) sector_first<S>(body + s_ext[wid].x, s_ext[wid].y, nf);
     for (uint32_t j = wid; j < ncand; j += BT / 64) {
         const uint32_t sct = s_list[j];
         const uint2 e = s_ext[j];
+        uint32_t cf[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) cf[k] = nf[k];
+        if (j + BT / 64 < ncand) sector_first<S>(body + s_ext[j + BT / 64].x, s_ext[j + BT / 64].y, nf);
         uint32_t out = 0;
-        const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, dtb, st, sig + (uint64_t)sct * SP_SIGW, out);
+        const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, dtb, st, sig + (uint64_t)sct * SP_SIGW, out, cf);
         moved += (uint64_t)sizeof(S) * (e.y + (r ? out : 0u));
         if (r) {
             removed += r;
