@@ -99,3 +99,20 @@ def test_sparse_default_policy_large_vs_c_oracle(eng, exact):
     _assert_counts_match_stream(pairs, s)
     if not exact:
         assert st.tail_dropped == ref["tail_total"]
+
+
+def test_sparse_vs_dense_full_c2(eng):
+    # BASELINE C2 at full size (100 MiB English, seed 2, all 32,512 merges to a
+    # 32K vocab): the library's policy (dense, then sector-sparse) and the dense
+    # loop alone (oracle-pinned at smaller sizes above and in test_gpu_parity)
+    # must agree on every merge, the final stream and every live pair count
+    from gpubpe import synth
+    data = synth.english(104_857_600, seed=2)
+    m1, s1, p1, st1 = _train_native(eng, data, 32768)
+    m2, s2, p2, st2 = _train_native(eng, data, 32768, sparse="dense")
+    assert st1.sparse_merges > 30000 and st2.sparse_merges == 0
+    assert len(m1) == 32512
+    assert m1 == m2
+    assert np.array_equal(s1, s2)
+    assert np.array_equal(p1[0], p2[0]) and np.array_equal(p1[1], p2[1])
+    assert st1.tail_dropped == st2.tail_dropped
