@@ -862,7 +862,7 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
 template <typename S, bool EXACT, int DELTA_TPW>
 __global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, const S* cur, Table tb,
                                                   uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
-                                                  uint32_t* __restrict__ grpsum, uint32_t eager_tiles) {
+                                                  uint32_t* __restrict__ grpsum, uint32_t eager_tiles, uint32_t ngroups) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     __shared__ LdsTab<LTAB_Z> lt;
     __shared__ uint32_t red[TPB / 64];
@@ -877,6 +877,27 @@ __global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, 
     const uint32_t lim = EXACT ? 0xFFFFFFFFu : new_n;
     lds_clear(lt);
     __syncthreads();
+    if (blockIdx.x >= ngroups) {
+        // stale tail [new_n, n): every old pair there is destroyed.  Blocks past
+        // the tile groups take one contiguous slice each (up to ~2K symbols, so
+        // their LDS table holds every distinct pair), instead of the few tile
+        // workgroups the tail falls in walking all of it with an overflowing table.
+        if (EXACT || n <= lim) return;
+        const uint32_t nt2 = gridDim.x - ngroups, q = blockIdx.x - ngroups;
+        const uint32_t len = n - lim, per = (len + nt2 - 1) / nt2;
+        const uint64_t a0 = (uint64_t)lim + (uint64_t)q * per;
+        const uint64_t a1 = a0 + per < (uint64_t)n ? a0 + per : (uint64_t)n;
+        if (a0 >= a1) return;   // block-uniform
+        for (uint64_t i = a0 + t; i < a1; i += TPB) {
+            if (i == 0) continue;
+            const uint32_t xi = cur[i];
+            if (xi & WS) continue;
+            const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
+            if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        }
+        lds_flush(lt, tb, st);
+        return;
+    }
     uint32_t tail = 0;
     for (int q = 0; q < DELTA_TPW; ++q) {
         const uint32_t tl = blockIdx.x * DELTA_TPW + q;
@@ -940,16 +961,7 @@ __global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, 
                 }
             }
         }
-        if (!EXACT && base + TILE > lim && base < n) {   // stale tail: old pairs destroyed
-            const uint64_t hi = (uint64_t)n < base + TILE ? (uint64_t)n : base + TILE;
-            for (uint64_t i = (lim > base ? (uint64_t)lim : base) + t; i < hi; i += TPB) {
-                if (i == 0) continue;
-                const uint32_t xi = cur[i];
-                if (xi & WS) continue;
-                const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
-                if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
-            }
-        }
+        // (the stale tail's destroyed pairs: the tail blocks above)
         if (i0 < n) hitmask[(uint64_t)tl * TPB + t] = hitm;
         if (lane == 0) red[wid] = cnt;
         __syncthreads();
@@ -2104,11 +2116,14 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     const bool mt = t->delta_mt && g_delta >= t->delta_mt;
     const uint32_t tpw = t->delta_tpw;
     const uint32_t g_mt = (uint32_t)gbpe_div_up(g_delta, tpw);
+    // stale-tail blocks (reference compaction): ~2K symbols each of the largest
+    // possible tail (n/2), at most 1024
+    const uint32_t g_mtail = exact ? 0u : (uint32_t)std::min<uint64_t>(1024, gbpe_div_up((uint64_t)t->n / 2 + 1, 2048));
     if (exact) {
         if (mt)
             hipLaunchKernelGGL(tpw == 32 ? (k_delta_mt<S, true, 32>) : tpw == 16 ? (k_delta_mt<S, true, 16>) : (k_delta_mt<S, true, 8>),
-                               dim3(g_mt), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask, t->tile_cnt,
-                               t->grpsum, g_delta);
+                               dim3(g_mt + g_mtail), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask,
+                               t->tile_cnt, t->grpsum, g_delta, g_mt);
         else
             hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
                                t->hitmask, t->tile_cnt, t->grpsum, g_delta);
@@ -2118,8 +2133,8 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     } else {
         if (mt)
             hipLaunchKernelGGL(tpw == 32 ? (k_delta_mt<S, false, 32>) : tpw == 16 ? (k_delta_mt<S, false, 16>) : (k_delta_mt<S, false, 8>),
-                               dim3(g_mt), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask, t->tile_cnt,
-                               t->grpsum, g_delta);
+                               dim3(g_mt + g_mtail), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask,
+                               t->tile_cnt, t->grpsum, g_delta, g_mt);
         else
             hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
                                t->hitmask, t->tile_cnt, t->grpsum, g_delta);
