@@ -720,13 +720,37 @@ __device__ __forceinline__ uint32_t lane_mask32(uint64_t i0, uint64_t lim) {
 template <typename S, bool EXACT, bool STAGE = false>
 __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, const S* cur, Table tb,
                                                uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
-                                               uint32_t* __restrict__ grpsum, uint32_t eager_tiles) {
+                                               uint32_t* __restrict__ grpsum, uint32_t eager_tiles,
+                                               uint32_t ngroups = 0xFFFFFFFFu) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     __shared__ LdsTab<STAGE ? LTAB_Z : LTAB_T> lt;
     __shared__ uint32_t stg[STAGE ? EPT * TPB : 1];
     __shared__ uint32_t red[TPB / 64], s_workw[TPB / 64];
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t tl = blockIdx.x;
+    if (tl >= ngroups) {   // a stale-tail slice block (as in k_delta_mt); tiles skip their tail loop
+        const uint4 s0 = reinterpret_cast<const uint4*>(st)[0];
+        const uint4 s1 = reinterpret_cast<const uint4*>(st)[1];
+        const uint2 s2 = reinterpret_cast<const uint2*>(st)[4];
+        const uint32_t n = s0.x, lim = s1.w, pid_ab = (s0.w << 16) | s1.x;
+        if (EXACT || s0.y || s2.y != round + 1u || n <= lim) return;
+        const uint32_t nt2 = gridDim.x - ngroups, q = tl - ngroups;
+        const uint32_t len = n - lim, per = (len + nt2 - 1) / nt2;
+        const uint64_t a0 = (uint64_t)lim + (uint64_t)q * per;
+        const uint64_t a1 = a0 + per < (uint64_t)n ? a0 + per : (uint64_t)n;
+        if (a0 >= a1) return;
+        lds_clear(lt);
+        __syncthreads();
+        for (uint64_t i = a0 + t; i < a1; i += TPB) {
+            if (i == 0) continue;
+            const uint32_t xi = cur[i];
+            if (xi & WS) continue;
+            const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
+            if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        }
+        lds_flush(lt, tb, st);
+        return;
+    }
     // tiles past the host's view of the stream (a shard that may have grown by an
     // appended window) check the length before loading anything
     if (tl >= eager_tiles && (uint64_t)tl * TILE >= st->n) return;
@@ -831,7 +855,7 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
                 }
             }
         }
-        if (!EXACT && (uint64_t)base + TILE > lim && base < n) {
+        if (!EXACT && ngroups == 0xFFFFFFFFu && (uint64_t)base + TILE > lim && base < n) {
             const uint64_t hi = (uint64_t)n < base + TILE ? (uint64_t)n : base + TILE;
             for (uint64_t i = (lim > base ? (uint64_t)lim : base) + t; i < hi; i += TPB) {
                 if (i == 0) continue;
@@ -2119,6 +2143,8 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     // stale-tail blocks (reference compaction): ~2K symbols each of the largest
     // possible tail (n/2), at most 1024
     const uint32_t g_mtail = exact ? 0u : (uint32_t)std::min<uint64_t>(1024, gbpe_div_up((uint64_t)t->n / 2 + 1, 2048));
+    // the single-tile k_delta's tail blocks (1024-slot LDS table: ~1K-symbol slices)
+    const uint32_t g_dtail = exact ? 0u : (uint32_t)std::min<uint64_t>(1024, gbpe_div_up((uint64_t)t->n / 2 + 1, 1024));
     if (exact) {
         if (mt)
             hipLaunchKernelGGL(tpw == 32 ? (k_delta_mt<S, true, 32>) : tpw == 16 ? (k_delta_mt<S, true, 16>) : (k_delta_mt<S, true, 8>),
@@ -2126,7 +2152,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
                                t->tile_cnt, t->grpsum, g_delta, g_mt);
         else
             hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
-                               t->hitmask, t->tile_cnt, t->grpsum, g_delta);
+                               t->hitmask, t->tile_cnt, t->grpsum, g_delta, 0xFFFFFFFFu);
         if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
         hipLaunchKernelGGL((k_compact<S, true>), dim3(g_compact), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
@@ -2136,8 +2162,8 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
                                dim3(g_mt + g_mtail), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask,
                                t->tile_cnt, t->grpsum, g_delta, g_mt);
         else
-            hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
-                               t->hitmask, t->tile_cnt, t->grpsum, g_delta);
+            hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta + g_dtail), dim3(TPB), 0, s, t->st, round, (const S*)cur,
+                               t->tb, t->hitmask, t->tile_cnt, t->grpsum, g_delta, g_delta);
         if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
         hipLaunchKernelGGL((k_compact<S, false>), dim3(g_compact), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
@@ -2158,6 +2184,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
 
 struct SpGrid {
     uint32_t body, copy, zdelta, zcompact, refresh;
+    uint32_t ztail = 0;   // stale-tail slice blocks of the multi-tile zone k_delta
     bool zone1;   // the zone fits one workgroup: it runs inside k_body
     int bt;       // k_body workgroup size (256 or 1024)
 };
@@ -2196,10 +2223,10 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     if (!g.zone1) {
         if (exact)
             hipLaunchKernelGGL((k_delta<S, true, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc,
-                               t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta);
-        else
-            hipLaunchKernelGGL((k_delta<S, false, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc,
-                               t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta);
+                               t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, 0xFFFFFFFFu);
+        else   // + stale-tail slice blocks: the zone's tail (<= mc <= zone/5) in ~2K-symbol slices
+            hipLaunchKernelGGL((k_delta<S, false, true>), dim3(g.zdelta + g.ztail), dim3(TPB), 0, s, t->zst, round,
+                               (const S*)zc, t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g.zdelta);
     }
     if (!g.zone1) {
         if (exact)
@@ -2728,6 +2755,8 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
         sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt));
         sg.copy = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u : grid_persistent(t->ctx, gbpe_div_up(zn / 5 + 1, TPB * 8), 1);
         sg.zdelta = (uint32_t)(zt ? zt : 1);
+        sg.ztail = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
+                                                           : (uint32_t)std::min<uint64_t>(1024, gbpe_div_up(zn / 5 + 1, 2048));
         sg.zcompact = (uint32_t)zt + ((t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
                                       : grid_persistent(t->ctx, gbpe_div_up(zn / 2 + 1, TPB * 16), 1));
         sg.refresh = g_refresh;
