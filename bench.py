@@ -1,30 +1,35 @@
 #!/usr/bin/env python3
 """Benchmark: BPE merges/sec (+ tokenize GB/s) on MI355X through the C-ABI.
 
-Workload (BASELINE.json configs[1]): 32K-vocab training
-on 104,857,600 bytes of synthetic English UTF-8 (seed 2), heuristic word
-boundaries, reference compaction semantics.  A "step" is one batch of 128
-merges (the reference's GPU round trip, training-pipeline.js:13); the timed
-region covers trainer creation on the HBM-resident corpus (symbol widening,
-word boundaries, initial pair count) plus K steps.  `value` = merges / s.
+Headline workload (BASELINE.json metric: "1 GiB UTF-8 @ 32K vocab"): 32K-vocab
+BPE training on 1,073,741,824 bytes of synthetic English-like UTF-8 (seed 2,
+0.5 % 3-byte punctuation), heuristic word boundaries (train.wgsl:87-186),
+reference compaction semantics.  A "step" is one complete training run on the
+HBM-resident corpus: trainer creation (symbol widening, word boundaries, the
+initial pair count) plus all 32,512 merges (every 128-merge host round trip of
+trainer.js:225-335).  `value` = merges of the K timed runs / their wall time.
 
-Secondary leg (configs[2], C3): chunked trie encode of 1 GiB synthetic
-multilingual text with a 32K vocab trained on a 100 MiB sample (seed 4).
+Secondary legs (same JSON line):
+  * c2: BASELINE configs[1] (100 MiB English, seed 2, 32K vocab), full runs;
+  * tokenize (configs[2], C3): chunked trie encode of 1 GiB multilingual text
+    with a 32K vocab trained on a 100 MiB sample (seed 4);
+  * cpu_baseline: the reference algorithm restated on the CPU
+    (oracle/bpe_oracle.c: full pair recount every merge), a bounded sample of
+    the same workload on the box's CPU share and on 1 core;
+  * parity: the timed runs' merge list against the committed oracle fixture
+    (tests/golden/train_en1g.npz, all 32,512 merges), the encode tokens against
+    the fixture and the CPU restatement.
 
-Multi-GPU (--gpus N under torch.distributed.run, one rank per GPU): sharded
-training (gpubpe.sharded).  Each rank holds a 104,857,600-byte
-English shard (seed 2 + rank, newline-terminated so shard starts are word
-starts) and the ranks train ONE global 32K vocab over the N-shard corpus,
-bit-exact to a single-stream run, with one RCCL all-gather of a fixed-size
-exchange record per merge.  Weak scaling: `value` = shard-merges/s = N x
-global merges / max wall (one merge applied to one 100 MiB shard is the unit
-of work at every N).  The encode leg runs one 1 GiB corpus per rank (seed
-3 + rank, no collective) and reports the total.
+Multi-GPU (--gpus N under torch.distributed.run, one rank per GPU): the same
+1 GiB corpus cut at word starts into N shards (strong scaling, `value` =
+global merges / max wall over ranks), sharded training with one RCCL exchange
+per merge (gpubpe/sharded.py).
 """
 from __future__ import annotations
 
 import argparse
 import ctypes as C
+import hashlib
 import json
 import os
 import sys
@@ -38,6 +43,10 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 TILE_SYMS = 8192
 METRIC = "BPE merges/sec + tokenize GB/s, 1 GiB UTF-8 @ 32K vocab, 1/2/4/8 MI355X"
+HEADLINE = {"gen": "english", "n": 1 << 30, "seed": 2, "fancy_punct": 0.005}
+C2 = {"gen": "english", "n": 104_857_600, "seed": 2, "fancy_punct": 0.005}
+PMC_FILE = os.path.join(ROOT, "profiles", "r2_pmc_kbody.json")
+GOLD = os.path.join(ROOT, "tests", "golden")
 
 
 def log(*a):
@@ -48,11 +57,19 @@ def dist_env():
     return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def make_corpus(spec: dict) -> bytes:
+    from gpubpe import synth
+    if spec["gen"] == "english":
+        return synth.english(spec["n"], seed=spec["seed"], fancy_punct=spec.get("fancy_punct", 0.0))
+    if spec["gen"] == "multilingual":
+        return synth.multilingual(spec["n"], seed=spec["seed"])
+    return synth.code(spec["n"], seed=spec["seed"])
+
+
 class Dist:
     """Process groups: the default group carries the sharded trainer's data path
     (RCCL = backend "nccl" over xGMI; GBPE_SHARD_TRANSPORT=gloo stages records
-    through host memory instead); a gloo group carries the timing scalars
-    (barrier / max / sum of a few bytes)."""
+    through host memory instead); a gloo group carries the timing scalars."""
 
     def __init__(self, world, local, force=False):
         local = int(os.environ.get("GBPE_BENCH_DEVICE", local))   # rehearsal: several ranks on one GPU
@@ -77,21 +94,19 @@ class Dist:
         if hasattr(self, "host"):
             self.dist.barrier(group=self.host)
 
-    def max(self, x: float) -> float:
+    def _reduce(self, x: float, op) -> float:
         if self.world == 1:
             return x
         import torch
         t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.host)
+        self.dist.all_reduce(t, op=op, group=self.host)
         return float(t.item())
 
+    def max(self, x: float) -> float:
+        return x if self.world == 1 else self._reduce(x, self.dist.ReduceOp.MAX)
+
     def sum(self, x: float) -> float:
-        if self.world == 1:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.host)
-        return float(t.item())
+        return x if self.world == 1 else self._reduce(x, self.dist.ReduceOp.SUM)
 
 
 def device_buffer(lib, ctx, data: bytes):
@@ -102,212 +117,180 @@ def device_buffer(lib, ctx, data: bytes):
     return p
 
 
-def run_train(lib, ctx, d_bytes, n, vocab, steps, flags, batch=128):
-    """Create a trainer on HBM-resident bytes and run up to `steps` batches."""
+def train_run(lib, ctx, d_bytes, n, vocab, flags=0, max_merges=0, batch=128):
+    """One training run on HBM-resident bytes: create + every step.  Returns
+    (merges [k, 4] uint32, stats)."""
     from gpubpe import _lib
     opts = _lib.TrainOpts(target_vocab_size=vocab, vocab_size=256, next_token_id=256, batch_size=batch,
                           flags=flags, table_log2=0)
     tr = C.c_void_p()
     _lib.check(lib.gbpe_trainer_create(ctx, d_bytes, n, None, 1, C.byref(opts), C.byref(tr)), ctx, "trainer_create")
-    merges = 0
-    done_steps = 0
-    stop = False
     out = (C.c_uint32 * (4 * batch))()
-    last = []
-    dump = [] if os.environ.get("BENCH_DUMP_MERGES") and flags else None
-    while done_steps < steps and not stop:
-        nd, es = C.c_uint32(), C.c_uint32()
-        _lib.check(lib.gbpe_trainer_step(tr, batch, out, C.byref(nd), C.byref(es)), ctx, "trainer_step")
-        merges += nd.value
-        done_steps += 1
-        stop = bool(es.value) or nd.value == 0
-        if nd.value:
-            last = list(out[4 * (nd.value - 1): 4 * nd.value])
-            if dump is not None:
-                dump += list(out[: 4 * nd.value])
-    if dump is not None:   # diagnostic: per-merge (a, b, id, count) of the timed run
-        import numpy as np
-        np.save(os.environ["BENCH_DUMP_MERGES"], np.array(dump, dtype=np.uint32).reshape(-1, 4))
-    return tr, merges, done_steps, stop, last
-
-
-def first_merges(lib, ctx, data: bytes, vocab: int, k: int):
-    from gpubpe import _lib
-    d = device_buffer(lib, ctx, data)
-    opts = _lib.TrainOpts(target_vocab_size=vocab, vocab_size=256, next_token_id=256, batch_size=128, flags=0,
-                          table_log2=0)
-    tr = C.c_void_p()
-    _lib.check(lib.gbpe_trainer_create(ctx, d, len(data), None, 1, C.byref(opts), C.byref(tr)), ctx, "create")
-    out = (C.c_uint32 * (4 * 128))()
-    got = []
-    while len(got) < k:
-        nd, es = C.c_uint32(), C.c_uint32()
-        _lib.check(lib.gbpe_trainer_step(tr, min(128, k - len(got)), out, C.byref(nd), C.byref(es)), ctx, "step")
-        got += [list(out[4 * i: 4 * i + 4]) for i in range(nd.value)]
-        if nd.value == 0 or es.value:
-            break
-    lib.gbpe_trainer_destroy(tr)
-    lib.gbpe_device_free(ctx, d)
-    return got
-
-
-def train_leg(args, lib, ctx, dist, rank):
-    from gpubpe import _lib, synth
-    n = args.train_bytes
-    t = time.time()
-    data = synth.english(n, seed=2, fancy_punct=0.005)
-    log(f"[bench] C2 corpus {n} B generated in {time.time() - t:.1f}s")
-    d = device_buffer(lib, ctx, data)
-    # warmup: W batches on a 8 MiB prefix (code paths, allocator, caches)
-    if args.warmup > 0:
-        tr, _, _, _, _ = run_train(lib, ctx, d, min(n, 8 << 20), args.vocab, args.warmup, 0)
+    merges = []
+    try:
+        while True:
+            k = batch if not max_merges else min(batch, max_merges - len(merges) // 4)
+            nd, es = C.c_uint32(), C.c_uint32()
+            _lib.check(lib.gbpe_trainer_step(tr, k, out, C.byref(nd), C.byref(es)), ctx, "trainer_step")
+            merges += out[: 4 * nd.value]
+            if nd.value == 0 or es.value or (max_merges and len(merges) // 4 >= max_merges):
+                break
+        st = _lib.TrainerStats()
+        lib.gbpe_trainer_stats_get(tr, C.byref(st))
+    finally:
         lib.gbpe_trainer_destroy(tr)
+    return np.array(merges, dtype=np.uint32).reshape(-1, 4), st
+
+
+def fixture(name: str):
+    p = os.path.join(GOLD, f"train_{name}.npz")
+    if not os.path.exists(p):
+        return None, None
+    z = np.load(p, allow_pickle=False)
+    return z["merges"], json.loads(str(z["meta"]))
+
+
+def timed_runs(args, lib, ctx, dist, d, n, vocab, steps, warmup):
+    """W untimed + K timed full runs, barrier + sync on both sides of the timed ones."""
+    for _ in range(warmup):
+        train_run(lib, ctx, d, n, vocab)
     lib.gbpe_synchronize(ctx)
     dist.barrier()
     lib.gbpe_synchronize(ctx)
     t0 = time.perf_counter()
-    tr, merges, steps, stop, last = run_train(lib, ctx, d, n, args.vocab, args.steps, 0)
+    total, last, st = 0, None, None
+    for _ in range(steps):
+        last, st = train_run(lib, ctx, d, n, vocab)
+        total += last.shape[0]
     lib.gbpe_synchronize(ctx)
     t1 = time.perf_counter()
     dist.barrier()
-    st = _lib.TrainerStats()
-    lib.gbpe_trainer_stats_get(tr, C.byref(st))
-    lib.gbpe_trainer_destroy(tr)
-    wall = dist.max(t1 - t0)
-    # roofline pass: the same run again with HIP events around every launch (the
-    # event markers add inter-kernel gaps, so they stay out of the timed run)
-    sk = _lib.TrainerStats()
-    if not args.no_kernel_timing:
-        tr2, _, _, _, _ = run_train(lib, ctx, d, n, args.vocab, args.steps, _lib.GBPE_TRAIN_TIMING)
-        lib.gbpe_trainer_stats_get(tr2, C.byref(sk))
-        lib.gbpe_trainer_destroy(tr2)
-    lib.gbpe_device_free(ctx, d)
-    res = {
-        "merges": merges, "steps": steps, "early_stop": stop, "wall_s": wall,
+    return dist.max(t1 - t0), total, last, st
+
+
+def train_detail(st, sk):
+    """Per-run stats of a timed run (st) and of the HIP-event run (sk)."""
+    return {
         "final_symbols": int(st.symbol_count), "bytes_per_symbol": int(st.bytes_per_symbol),
-        "stream_bytes": int(st.stream_bytes_moved), "ms_stream_kernels": sk.ms_merge,
-        "ms_select": sk.ms_select, "ms_refresh": sk.ms_other,
-        "ms_delta": sk.ms_delta, "ms_compact": sk.ms_compact, "timed_merges": int(sk.timed_merges),
-        "tail_dropped": int(st.tail_dropped), "max_live_pairs": int(st.max_live_pairs),
-        "last_merge": last,
+        "stream_bytes": int(st.stream_bytes_moved), "tail_dropped": int(st.tail_dropped),
+        "max_live_pairs": int(st.max_live_pairs), "table_slots": int(st.table_slots),
         "sparse": {"merges": int(st.sparse_merges), "enters": int(st.sparse_enters), "exits": int(st.sparse_exits),
                    "sectors": int(st.sparse_sectors), "zone_at_entry": int(st.sparse_zone)},
-        # by mode, from the HIP-event pass: the dense merges' stream kernels and the
-        # sector-sparse merges' k_body (+ multi-tile zone passes); bytes actually moved
-        "dense_merges": int(sk.timed_merges - sk.sparse_merges), "dense_bytes": int(sk.dense_bytes),
-        "ms_dense": sk.ms_dense, "sparse_merges": int(sk.sparse_merges), "body_bytes": int(sk.body_bytes),
-        "zone_bytes": int(sk.zone_bytes), "ms_body": sk.ms_body, "ms_sparse": sk.ms_sparse,
-        "body_bytes_run": int(st.body_bytes),   # the timed run's k_body bytes (PMC comparisons)
+        "events": None if sk is None else {
+            "merges": int(sk.timed_merges), "dense_merges": int(sk.timed_merges - sk.sparse_merges),
+            "dense_bytes": int(sk.dense_bytes), "ms_dense": sk.ms_dense,
+            "sparse_merges": int(sk.sparse_merges), "body_bytes": int(sk.body_bytes), "zone_bytes": int(sk.zone_bytes),
+            "ms_body": sk.ms_body, "ms_sparse": sk.ms_sparse, "ms_select": sk.ms_select, "ms_refresh": sk.ms_other,
+            "ms_delta": sk.ms_delta, "ms_compact": sk.ms_compact},
     }
-    return data, res
 
 
-def shard_corpus(args, rank):
-    from gpubpe import synth
-    data = synth.english(args.train_bytes, seed=2 + rank, fancy_punct=0.005)
-    return data[:-1] + b"\n"          # shard starts stay word starts in the global stream
+def train_roofline(det, wall_per_run):
+    """Roofline of the dominant training kernel from the HIP-event run.
+
+    Sector-sparse merges (32,384 of 32,512) spend their time in k_body; its bytes
+    are the ones it moves (candidate extents and signatures, sector symbols read
+    and rewritten, the one-workgroup zone pass) — pair-table traffic excluded as
+    in SURVEY §8(d).  The dense merges' stream kernels are reported beside it with
+    the SURVEY bytes s*(2N_i + N_{i+1}); the SURVEY formula over the whole run and
+    its wall time is given as the bandwidth a stream-per-merge loop would need to
+    match this merge rate (not credited as moved)."""
+    ev = det["events"]
+    dense = None
+    if ev and ev["ms_dense"] > 0:
+        a = ev["dense_bytes"] / 1e9 / (ev["ms_dense"] / 1e3)
+        dense = {"kernel": "k_delta + k_compact (dense merges)", "merges": ev["dense_merges"], "achieved": round(a, 1),
+                 "frac": round(a / HBM_PEAK_GBPS, 4), "algorithmic_bytes": ev["dense_bytes"],
+                 "ms": round(ev["ms_dense"], 2)}
+    equiv = det["stream_bytes"] / 1e9 / wall_per_run
+    roof = {"bound": "hbm", "kernel": "k_body (sector-sparse merge pass, one launch per merge)", "achieved": None,
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None, "traffic": None}
+    if ev and ev["ms_body"] > 0 and ev["sparse_merges"] > 0:
+        a = ev["body_bytes"] / 1e9 / (ev["ms_body"] / 1e3)
+        roof.update({"achieved": round(a, 1), "frac": round(a / HBM_PEAK_GBPS, 4),
+                     "algorithmic_bytes_per_launch": round(ev["body_bytes"] / ev["sparse_merges"]),
+                     "us_per_launch": round(1e3 * ev["ms_body"] / ev["sparse_merges"], 2),
+                     "launches": ev["sparse_merges"],
+                     "timing": "HIP events around every k_body launch of one extra full run of the same workload "
+                               "(events add inter-kernel gaps, so they stay out of the timed runs)",
+                     "note": "latency-bound by design: a late merge touches a few hundred sectors, so it moves "
+                             "kilobytes, not the stream; the loop avoids the bytes rather than streaming them"})
+    roof["dense_stream"] = dense
+    roof["dense_equivalent"] = {"gbps": round(equiv, 1), "frac": round(equiv / HBM_PEAK_GBPS, 4),
+                                "bytes": det["stream_bytes"],
+                                "meaning": "SURVEY s*(2N_i+N_{i+1}) over all merges / wall per run: the HBM rate a "
+                                           "full-stream-per-merge loop would need for this merge rate"}
+    if os.path.exists(PMC_FILE):
+        p = json.load(open(PMC_FILE))
+        if p.get("workload") == "en1g-full-run":
+            roof["traffic"] = round(p["hbm_bytes_per_launch"])
+            roof["traffic_unit"] = "bytes/launch (k_body)"
+            roof["traffic_over_algorithmic"] = round(p["traffic_over_algorithmic"], 4)
+            roof["traffic_window"] = (f"{os.path.relpath(PMC_FILE, ROOT)}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and "
+                                      f"WRITE_SIZE passes over one full run of this workload ({p['launches']} k_body "
+                                      f"launches); algorithmic bytes from the same run")
+    return roof
 
 
-_COMM = {}   # one RCCL communicator per process, created in the warmup (outside the timed region)
-
-
-def run_sharded(args, lib, ctx, dist, rank, world, d, n, steps, table_log2):
-    import torch
-    from gpubpe.sharded import GpuShardBackend, ShardedTrainer
-    be = GpuShardBackend(lib, ctx, d, None, rank, world, args.vocab, input_on_device=True, n=n,
-                         table_log2=table_log2, cap_extra=max(TILE_SYMS, n // 4),
-                         stream=torch.cuda.current_stream().cuda_stream)
-    tr = ShardedTrainer(be, dist.dist, device="cuda", staged=dist.transport != "nccl")
-    tr.setup()
-    if dist.transport == "nccl" and os.environ.get("GBPE_SHARD_LOOP", "native") == "native" and \
-            _COMM.get("ok", True):
-        # whole steps inside the library: RCCL all-gather on its own stream; every
-        # rank must agree, else all fall back to the host loop
-        ok = 1.0
-        try:
-            _COMM["c"] = tr.attach_native_comm(_COMM.get("c"))
-            be.owns_comm = False
-        except Exception as e:  # noqa: BLE001
-            log(f"[bench] rank {rank}: native step loop unavailable ({e}); using the host loop")
-            ok = 0.0
-        if world > 1:
-            ok = -dist.max(-ok)   # min over ranks
-        if ok < 1.0:
-            tr.native = False
-            be.comm = None
-            _COMM["ok"] = False
-    merges, done_steps, early = [], 0, False
-    needed = min(args.vocab - 256, 128 * steps)     # stalled steps are redone: count merges, not steps
-    while len(merges) < needed and not early:
-        got, early = tr.step(min(128, needed - len(merges)))
-        merges += got
-        done_steps += 1
-    return be, tr, merges, done_steps, early
-
-
-def train_leg_sharded(args, lib, ctx, dist, rank, world):
-    """C2-size shard per rank, one global vocab (weak scaling)."""
+def headline_leg(args, lib, ctx, dist):
     t = time.time()
-    data = shard_corpus(args, rank)
-    log(f"[bench] rank {rank}: shard {len(data)} B generated in {time.time() - t:.1f}s")
+    data = make_corpus(HEADLINE)
+    log(f"[bench] headline corpus {len(data)} B generated in {time.time() - t:.1f}s")
     d = device_buffer(lib, ctx, data)
     n = len(data)
-    table_log2 = 23
-    if args.warmup > 0:   # RCCL communicators, code paths: W steps on an 8 MiB prefix of every shard
-        be, _, _, _, _ = run_sharded(args, lib, ctx, dist, rank, world, d, min(n, 8 << 20), args.warmup, table_log2)
-        be.close()
-    lib.gbpe_synchronize(ctx)
-    dist.barrier()
-    lib.gbpe_synchronize(ctx)
-    t0 = time.perf_counter()
-    be, tr, merges, steps, early = run_sharded(args, lib, ctx, dist, rank, world, d, n, args.steps, table_log2)
-    lib.gbpe_synchronize(ctx)
-    t1 = time.perf_counter()
-    dist.barrier()
-    st = be.stats()
-    be.close()
+    wall, total, last, st = timed_runs(args, lib, ctx, dist, d, n, args.vocab, args.steps, args.warmup)
+    sk = None
+    if not args.no_kernel_timing:
+        from gpubpe import _lib
+        _, sk = train_run(lib, ctx, d, n, args.vocab, flags=_lib.GBPE_TRAIN_TIMING)
     lib.gbpe_device_free(ctx, d)
-    wall = dist.max(t1 - t0)
-    stream_bytes = int(dist.sum(float(st.stream_bytes_moved)))
-    res = {
-        "merges": len(merges), "steps": steps, "early_stop": early, "wall_s": wall,
-        "final_symbols_rank": int(st.symbol_count), "bytes_per_symbol": int(st.bytes_per_symbol),
-        "stream_bytes": stream_bytes, "stalls": tr.stalls, "record_caps": [tr.C, tr.Cw],
-        "transport": dist.transport + (" (native step loop)" if tr.native else " (host loop)"), "last_merge": merges[-1] if merges else [],
-        "tail_dropped": int(st.tail_dropped),
-    }
-    return data, merges, res
+    det = train_detail(st, sk)
+    det["merges_per_run"] = int(last.shape[0])
+    det["last_merge"] = last[-1].tolist() if last.shape[0] else []
+    parity = {}
+    want, meta = fixture("en1g")
+    if want is not None and args.vocab == 32768:
+        parity["train_fixture"] = "tests/golden/train_en1g.npz (oracle/bpe_oracle_inc.c)"
+        parity["train_corpus_sha256_equal"] = hashlib.sha256(data).hexdigest() == meta["corpus_sha256"]
+        parity["train_merges_equal_fixture"] = bool(last.shape == want.shape and np.array_equal(last, want))
+        parity["train_merges_checked"] = int(want.shape[0])
+        parity["train_final_symbols_equal"] = int(st.symbol_count) == meta["final_n"]
+    return data, wall, total, last, det, parity
+
+
+def c2_leg(args, lib, ctx, dist):
+    data = make_corpus(C2)
+    d = device_buffer(lib, ctx, data)
+    wall, total, last, st = timed_runs(args, lib, ctx, dist, d, len(data), args.vocab, 3, 1)
+    lib.gbpe_device_free(ctx, d)
+    want, _ = fixture("c2")
+    res = {"workload": "C2 (BASELINE configs[1]): 32K-vocab train on 104,857,600 B English UTF-8 (seed 2), full runs",
+           "value": round(total / wall, 1), "unit": "merges/s", "runs": 3, "merges_per_run": int(last.shape[0]),
+           "ms_per_run": round(1e3 * wall / 3, 2)}
+    if want is not None:
+        res["merges_equal_fixture"] = bool(last.shape == want.shape and np.array_equal(last, want))
+    return data, res
 
 
 def encode_leg(args, lib, ctx, dist, rank):
     """C3: train a 32K vocab on a 100 MiB multilingual sample (seed 4), then
     encode 1 GiB multilingual text (seed 3) with the chunked trie walk."""
-    from gpubpe import _lib, synth, compile_vocab_to_trie, parse_header, parse_trie_buffers
+    from gpubpe import _lib, compile_vocab_to_trie, parse_header, parse_trie_buffers
     from gpubpe.vocab import Vocab
     t = time.time()
-    sample = synth.multilingual(args.vocab_sample_bytes, seed=4)
+    sample = make_corpus({"gen": "multilingual", "n": args.vocab_sample_bytes, "seed": 4})
     d = device_buffer(lib, ctx, sample)
-    opts = _lib.TrainOpts(target_vocab_size=args.vocab, vocab_size=256, next_token_id=256, batch_size=128, flags=0,
-                          table_log2=0)
-    tr = C.c_void_p()
-    _lib.check(lib.gbpe_trainer_create(ctx, d, len(sample), None, 1, C.byref(opts), C.byref(tr)), ctx, "create")
-    voc = Vocab()
-    out = (C.c_uint32 * 512)()
-    while True:
-        nd, es = C.c_uint32(), C.c_uint32()
-        _lib.check(lib.gbpe_trainer_step(tr, 128, out, C.byref(nd), C.byref(es)), ctx, "step")
-        for i in range(nd.value):
-            voc.add_merge(out[4 * i], out[4 * i + 1])
-        if nd.value == 0 or es.value:
-            break
-    lib.gbpe_trainer_destroy(tr)
+    merges, _ = train_run(lib, ctx, d, len(sample), args.vocab)
     lib.gbpe_device_free(ctx, d)
+    voc = Vocab()
+    for a, b in merges[:, :2].tolist():
+        voc.add_merge(a, b)
     blob = compile_vocab_to_trie(voc.entries)
     hdr = parse_header(blob)
     nodes, edges = parse_trie_buffers(blob, hdr)
     log(f"[bench] C3 vocab {voc.size} tokens, trie {hdr['nodeCount']} nodes in {time.time() - t:.1f}s")
     t = time.time()
-    text = synth.multilingual(args.encode_bytes, seed=3 + rank)   # one corpus per rank (no collective)
+    text = make_corpus({"gen": "multilingual", "n": args.encode_bytes, "seed": 3})
     n = len(text)
     log(f"[bench] C3 corpus {n} B generated in {time.time() - t:.1f}s")
     trie = C.c_void_p()
@@ -321,7 +304,7 @@ def encode_leg(args, lib, ctx, dist, rank):
     _lib.check(lib.gbpe_device_alloc(ctx, 4 * n + 64, C.byref(d_out)), ctx, "alloc out")
     n_out = C.c_uint64()
     _lib.check(lib.gbpe_encode_device(ctx, trie, d_in, n, cs, d_out, n, C.byref(n_out)), ctx, "encode warmup")
-    reps = 3
+    reps = 5
     kms = []
     dist.barrier()
     lib.gbpe_synchronize(ctx)
@@ -338,10 +321,12 @@ def encode_leg(args, lib, ctx, dist, rank):
     k_all = float(np.mean([sum(k) for k in kms]))
     # end-to-end host -> tokens -> host (the reference's MB/s definition, export-controller.js:210-213)
     host_out = np.empty(n, dtype=np.uint32)
-    t0 = time.perf_counter()
-    _lib.check(lib.gbpe_encode(ctx, trie, text, n, cs, host_out.ctypes.data_as(_lib.u32p), n, C.byref(n_out)),
-               ctx, "encode e2e")
-    e2e = time.perf_counter() - t0
+    e2e = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        _lib.check(lib.gbpe_encode(ctx, trie, text, n, cs, host_out.ctypes.data_as(_lib.u32p), n, C.byref(n_out)),
+                   ctx, "encode e2e")
+        e2e.append(time.perf_counter() - t0)
     tokens = host_out[: n_out.value]
     lib.gbpe_device_free(ctx, d_in)
     lib.gbpe_device_free(ctx, d_out)
@@ -349,145 +334,235 @@ def encode_leg(args, lib, ctx, dist, rank):
     alg = n + 4 * T
     res = {
         "workload": "C3: chunked greedy trie encode of 1,073,741,824 B multilingual UTF-8 (seed 3), 32K vocab "
-                    f"trained on a {args.vocab_sample_bytes} B sample (seed 4), chunk {cs}",
+                    f"trained on the GPU on a {args.vocab_sample_bytes} B sample (seed 4), chunk {cs}",
         "bytes": n, "tokens": T, "chunk_size": cs, "trie_nodes": int(hdr["nodeCount"]),
         "trie_records": int(nrec.value),
         "gbps_kernels": round(n / 1e9 / (k_all / 1e3), 2),
         "gbps_device_wall": round(n / 1e9 / wall, 2),
-        "gbps_end_to_end": round(n / 1e9 / e2e, 2),
+        "gbps_end_to_end": round(n / 1e9 / min(e2e), 2),
         "ms_walk": round(k_walk, 3), "ms_scan": round(float(np.mean([k[1] for k in kms])), 3),
         "ms_compact": round(float(np.mean([k[2] for k in kms])), 3),
-        "roofline": {"bound": "hbm", "kernel": "k_trie_walk + k_chunk_scan + k_chunk_compact",
+        "roofline": {"bound": "hbm", "kernel": "encode kernels (walk + scan + compact), n + 4T bytes",
                      "achieved": round(alg / 1e9 / (k_all / 1e3), 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(alg / 1e9 / (k_all / 1e3) / HBM_PEAK_GBPS, 4), "algorithmic_bytes": alg,
                      "traffic": None},
     }
-    if dist.world > 1:   # weak scaling: every rank encodes its own 1 GiB
-        res["ranks"] = dist.world
-        res["gbps_kernels_total"] = round(dist.sum(res["gbps_kernels"]), 2)
-        res["gbps_device_wall_total"] = round(dist.sum(n) / 1e9 / wall, 2)
+    pmc = os.path.join(ROOT, "profiles", "r2_pmc_encode.json")
+    if os.path.exists(pmc):
+        p = json.load(open(pmc))
+        if p.get("workload") == "c3-1g" and p.get("chunk_size") == cs:
+            res["roofline"]["traffic"] = round(p["hbm_bytes_per_encode"])
+            res["roofline"]["traffic_unit"] = "bytes/encode (all encode kernels)"
+            res["roofline"]["traffic_over_algorithmic"] = round(p["hbm_bytes_per_encode"] / alg, 4)
+            res["roofline"]["traffic_window"] = f"{os.path.relpath(pmc, ROOT)}: FETCH_SIZE (x2) + WRITE_SIZE passes"
+    fx = os.path.join(GOLD, "encode_c3enc1g.json")
+    if os.path.exists(fx) and args.encode_bytes == 1 << 30 and args.vocab_sample_bytes == 104_857_600:
+        meta = json.load(open(fx))
+        res["fixture_tokens_equal"] = (T == meta["n_tokens"] and
+                                       hashlib.sha256(np.ascontiguousarray(tokens, "<u4").tobytes()).hexdigest()
+                                       == meta["tokens_sha256"])
     return text, nodes, edges, cs, tokens, res
 
 
-def train_roofline(tr):
-    """Roofline of the dominant training kernel, from the HIP-event pass.
-
-    Sector-sparse merges (most of the run) spend their time in k_body; its bytes are
-    what it actually moved (candidate extents and signatures, sector symbols read and
-    rewritten, the one-workgroup zone pass).  The dense merges' stream kernels are
-    reported beside it with the SURVEY §8(d) bytes s*(2N_i + N_{i+1}).  The SURVEY
-    formula over the whole run and its wall time is also given as the bandwidth a
-    dense loop would need to match this merge rate (it is not credited as moved)."""
-    dense = None
-    if tr.get("ms_dense", 0) > 0:
-        a = tr["dense_bytes"] / 1e9 / (tr["ms_dense"] / 1e3)
-        dense = {"kernel": "k_delta + k_compact (dense merges)", "merges": tr["dense_merges"],
-                 "achieved": round(a, 1), "frac": round(a / HBM_PEAK_GBPS, 4), "algorithmic_bytes": tr["dense_bytes"],
-                 "ms": round(tr["ms_dense"], 2)}
-    equiv = tr["stream_bytes"] / 1e9 / tr["wall_s"]
-    if tr.get("ms_body", 0) > 0 and tr.get("sparse_merges", 0) > 0:
-        a = tr["body_bytes"] / 1e9 / (tr["ms_body"] / 1e3)
-        roof = {"bound": "hbm", "kernel": "k_body (sector-sparse merge pass, one launch per merge)",
-                "achieved": round(a, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(a / HBM_PEAK_GBPS, 4),
-                "algorithmic_bytes": tr["body_bytes"],
-                "bytes_per_launch": round(tr["body_bytes"] / tr["sparse_merges"]),
-                "us_per_launch": round(1e3 * tr["ms_body"] / tr["sparse_merges"], 2),
-                "launches": tr["sparse_merges"], "traffic": None,
-                "note": "latency-bound by design: a late merge touches ~100 sectors, so it moves kilobytes, "
-                        "not the stream; frac is low because the loop avoids the bytes, not because it wastes them"}
-    else:
-        a = dense["achieved"] if dense else None
-        roof = {"bound": "hbm", "kernel": "stream pass per merge: k_delta + k_compact", "achieved": a,
-                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(a / HBM_PEAK_GBPS, 4) if a else None,
-                "algorithmic_bytes": tr["dense_bytes"], "traffic": None}
-    roof["dense_stream"] = dense
-    roof["dense_equivalent"] = {"gbps": round(equiv, 1), "frac": round(equiv / HBM_PEAK_GBPS, 4),
-                                "bytes": tr["stream_bytes"],
-                                "meaning": "SURVEY s*(2N_i+N_{i+1}) over all merges / wall: the HBM rate a "
-                                           "full-stream-per-merge loop would need for this merge rate"}
-    return roof
+def cpu_baselines(args, data, enc):
+    """The reference algorithm on the host (oracle/bpe_oracle.c, 'port'): first K
+    merges of the SAME headline corpus, full pair recount per merge, on the box's
+    CPU share (OMP_NUM_THREADS, 16 per GPU on the pool) and on 1 core."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_ref
+    share = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    nproc = os.cpu_count()
+    out = {}
+    for cores, k in ((share, args.cpu_merges or 24), (1, max(1, (args.cpu_merges or 24) // 12))):
+        t = time.perf_counter()
+        r = cpu_ref.train(data, args.vocab, max_merges=k, threads=cores, want_symbols=False)
+        dt = time.perf_counter() - t
+        out[cores] = (len(r["merges"]) / dt, r["merges"], dt)
+    v, merges, dt = out[share]
+    base = {"value": round(v, 3), "unit": "merges/s", "cores": share, "kind": "port",
+            "sample": f"first {len(merges)} merges of the same 1 GiB corpus, full pair recount per merge (reference "
+                      f"algorithm, oracle/bpe_oracle.c, OpenMP), {dt:.1f}s",
+            "nproc": nproc, "cpu_share": share,
+            "one_core": {"value": round(out[1][0], 4), "merges": len(out[1][1]), "seconds": round(out[1][2], 1)},
+            "note": "early merges are the most expensive for a full recount (the stream is longest), so this is a "
+                    "lower bound of the whole-run CPU rate; it is a baseline, not a target"}
+    enc_base = None
+    if enc is not None:
+        text, nodes, edges, cs, tokens, er = enc
+        t = time.perf_counter()
+        ref_tokens = cpu_ref.encode(text, nodes, edges, cs, threads=share)
+        dt = time.perf_counter() - t
+        enc_base = {"value": round(len(text) / 1e9 / dt, 3), "unit": "GB/s", "cores": share, "kind": "port",
+                    "sample": f"full {len(text)} B encode, chunked greedy trie walk (oracle/bpe_oracle.c), {dt:.1f}s",
+                    "nproc": nproc, "tokens_equal": bool(np.array_equal(tokens, ref_tokens))}
+    return base, merges, enc_base
 
 
-def single_line(args, tr):
-    value = tr["merges"] / tr["wall_s"]
-    return {
-        "metric": METRIC,
-        "value": round(value, 1),
-        "unit": "merges/s",
-        "n_gpus": 1,
-        "steps": tr["steps"],
-        "warmup": args.warmup,
-        "ms_per_step": round(1e3 * tr["wall_s"] / max(1, tr["steps"]), 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": f"u{8 * tr['bytes_per_symbol']}",
-        "data": "synthetic (seeded Zipf English-like corpus, gpubpe.synth)",
-        "config": {"workload": "C2: 32K-vocab BPE train on 104,857,600 B English UTF-8 (seed 2), heuristic "
-                               "word boundaries, reference compaction; step = 128 merges",
-                   "train_bytes": args.train_bytes, "target_vocab": args.vocab,
-                   "merges_timed": tr["merges"], "early_stop": tr["early_stop"], "parallelism": "single"},
-        "roofline": train_roofline(tr),
-        "train_detail": tr,
-    }
-
-
-def sharded_line(args, lib, ctx, dist, rank, world):
-    data, merges, tr = train_leg_sharded(args, lib, ctx, dist, rank, world)
-    value = world * tr["merges"] / tr["wall_s"]
-    achieved = tr["stream_bytes"] / 1e9 / tr["wall_s"]
+def single_line(args, lib, ctx, dist, rank):
+    data, wall, total, last, det, parity = headline_leg(args, lib, ctx, dist)
+    value = total / wall
     line = {
         "metric": METRIC,
         "value": round(value, 1),
         "unit": "merges/s",
-        "n_gpus": world,
-        "steps": tr["steps"],
+        "n_gpus": 1,
+        "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1e3 * tr["wall_s"] / max(1, tr["steps"]), 3),
+        "ms_per_step": round(1e3 * wall / max(1, args.steps), 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
-        "dtype": f"u{8 * tr['bytes_per_symbol']}",
-        "data": "synthetic (seeded Zipf English-like corpus per shard, gpubpe.synth)",
-        "config": {"workload": f"C2 x {world}: one global 32K-vocab BPE train over {world} shards of "
-                               f"{args.train_bytes:,} B English UTF-8 (seeds 2..{1 + world}), heuristic word "
-                               "boundaries, reference compaction, bit-exact to one stream; value = shard-merges/s "
-                               "(global merges x shards / wall); step = 128 merges",
-                   "train_bytes_per_rank": args.train_bytes, "target_vocab": args.vocab,
-                   "merges_timed": tr["merges"], "early_stop": tr["early_stop"],
-                   "parallelism": f"shard{world} ({tr['transport']} all-gather per merge)"},
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "whole sharded loop (algorithmic stream bytes of all ranks / wall)",
-            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS * world, "unit": "GB/s",
-            "frac": round(achieved / (HBM_PEAK_GBPS * world), 4),
-            "algorithmic_bytes": tr["stream_bytes"], "traffic": None,
-        },
-        "train_detail": tr,
+        "dtype": f"u{8 * det['bytes_per_symbol']}",
+        "data": "synthetic (seeded Zipf English-like corpus, gpubpe.synth)",
+        "config": {"workload": "headline: 32K-vocab BPE train on 1,073,741,824 B English-like UTF-8 (seed 2, 0.5% "
+                               "3-byte punctuation), heuristic word boundaries, reference compaction; step = one "
+                               "complete training run (trainer creation + all 32,512 merges) on the HBM-resident "
+                               "corpus",
+                   "train_bytes": HEADLINE["n"], "target_vocab": args.vocab,
+                   "merges_per_step": det["merges_per_run"], "parallelism": "single"},
+        "roofline": train_roofline(det, wall / max(1, args.steps)),
+        "train_detail": det,
+        "parity": parity,
     }
-    if rank == 0 and not args.no_parity:
-        # the first merges equal a single-GPU run on the concatenated corpus
-        full = b"".join(shard_corpus(args, r) for r in range(world))
-        k = min(128, len(merges))
-        g = first_merges(lib, ctx, full, args.vocab, k)
-        line["parity"] = {"sharded_vs_single_stream_first_merges_equal": g == merges[:k], "merges_checked": k}
-    return line, data
+    if not args.no_c2:
+        _, line["c2"] = c2_leg(args, lib, ctx, dist)
+    enc = None
+    if not args.no_encode:
+        enc = encode_leg(args, lib, ctx, dist, rank)
+        line["tokenize"] = enc[-1]
+    if not args.no_cpu:
+        base, cpu_merges, enc_base = cpu_baselines(args, data, enc)
+        line["cpu_baseline"] = base
+        line["parity"]["train_cpu_first_merges_equal"] = cpu_merges == last[: len(cpu_merges)].tolist()
+        if enc_base is not None:
+            line["tokenize"]["cpu_baseline"] = enc_base
+    return line
+
+
+# ── multi-GPU: strong scaling over one corpus ──────────────────────────────────
+
+_COMM = {}   # one RCCL communicator per process, created in the warmup (outside the timed region)
+
+
+def shard_of(data: bytes, rank: int, world: int) -> bytes:
+    """Rank r's contiguous slice of the corpus, cut right after a newline (a word
+    start under the reference heuristic: train.wgsl:166-170), so pair counts add
+    up across ranks and the concatenation is the original stream."""
+    n = len(data)
+    arr = np.frombuffer(data, dtype=np.uint8)
+    nl = np.flatnonzero(arr == 0x0A)
+    cuts = [0]
+    for r in range(1, world):
+        k = int(np.searchsorted(nl, n * r // world))
+        cuts.append(max(cuts[-1], int(nl[k]) + 1 if k < nl.shape[0] else n))
+    cuts.append(n)
+    return data[cuts[rank]:cuts[rank + 1]]
+
+
+def run_sharded(args, lib, ctx, dist, rank, world, d, n, max_merges, table_log2):
+    import torch
+    from gpubpe.sharded import GpuShardBackend, ShardedTrainer
+    be = GpuShardBackend(lib, ctx, d, None, rank, world, args.vocab, input_on_device=True, n=n,
+                         table_log2=table_log2, cap_extra=max(TILE_SYMS, n // 4),
+                         stream=torch.cuda.current_stream().cuda_stream)
+    tr = ShardedTrainer(be, dist.dist, device="cuda", staged=dist.transport != "nccl")
+    tr.setup()
+    if dist.transport == "nccl" and os.environ.get("GBPE_SHARD_LOOP", "native") == "native" and _COMM.get("ok", True):
+        ok = 1.0
+        try:
+            _COMM["c"] = tr.attach_native_comm(_COMM.get("c"))
+            be.owns_comm = False
+        except Exception as e:  # noqa: BLE001
+            log(f"[bench] rank {rank}: native step loop unavailable ({e}); using the host loop")
+            ok = 0.0
+        if world > 1:
+            ok = -dist.max(-ok)   # min over ranks
+        if ok < 1.0:
+            tr.native = False
+            be.comm = None
+            _COMM["ok"] = False
+    merges, early = [], False
+    needed = min(args.vocab - 256, max_merges)
+    while len(merges) < needed and not early:
+        got, early = tr.step(min(128, needed - len(merges)))
+        merges += got
+    return be, tr, merges, early
+
+
+def sharded_line(args, lib, ctx, dist, rank, world):
+    t = time.time()
+    full = make_corpus(HEADLINE)
+    data = shard_of(full, rank, world)
+    log(f"[bench] rank {rank}: shard {len(data)} B of {len(full)} in {time.time() - t:.1f}s")
+    d = device_buffer(lib, ctx, data)
+    n = len(data)
+    table_log2 = 24
+    for _ in range(args.warmup):   # RCCL communicators, code paths: W runs on an 8 MiB prefix of every shard
+        be, _, _, _ = run_sharded(args, lib, ctx, dist, rank, world, d, min(n, 8 << 20), 1 << 30, table_log2)
+        be.close()
+    lib.gbpe_synchronize(ctx)
+    dist.barrier()
+    lib.gbpe_synchronize(ctx)
+    t0 = time.perf_counter()
+    total, merges, early, st, tr = 0, [], False, None, None
+    for _ in range(args.steps):
+        be, tr, merges, early = run_sharded(args, lib, ctx, dist, rank, world, d, n, 1 << 30, table_log2)
+        total += len(merges)
+        st = be.stats()
+        be.close()
+    lib.gbpe_synchronize(ctx)
+    t1 = time.perf_counter()
+    dist.barrier()
+    lib.gbpe_device_free(ctx, d)
+    wall = dist.max(t1 - t0)
+    line = {
+        "metric": METRIC,
+        "value": round(total / wall, 1),
+        "unit": "merges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * wall / max(1, args.steps), 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": f"u{8 * int(st.bytes_per_symbol)}",
+        "data": "synthetic (seeded Zipf English-like corpus, gpubpe.synth)",
+        "config": {"workload": f"headline corpus (1,073,741,824 B English-like UTF-8, seed 2) cut at word starts "
+                               f"into {world} shards, one global 32K vocab, bit-exact to one stream; step = one "
+                               "complete training run",
+                   "train_bytes": HEADLINE["n"], "target_vocab": args.vocab, "merges_per_step": len(merges),
+                   "parallelism": f"shard{world} ({dist.transport} exchange per merge"
+                                  f"{', native step loop' if tr is not None and tr.native else ''})"},
+        "roofline": {"bound": "hbm", "kernel": "whole sharded loop (algorithmic stream bytes of all ranks / wall)",
+                     "achieved": None, "peak": HBM_PEAK_GBPS * world, "unit": "GB/s", "frac": None, "traffic": None},
+        "train_detail": {"stalls": tr.stalls if tr else 0, "record_caps": [tr.C, tr.Cw] if tr else None,
+                         "final_symbols_rank": int(st.symbol_count), "tail_dropped": int(st.tail_dropped),
+                         "last_merge": merges[-1] if merges else []},
+    }
+    sb = dist.sum(float(st.stream_bytes_moved))
+    line["roofline"]["achieved"] = round(sb / 1e9 / (wall / max(1, args.steps)), 1)
+    line["roofline"]["frac"] = round(line["roofline"]["achieved"] / (HBM_PEAK_GBPS * world), 4)
+    want, _ = fixture("en1g")
+    if want is not None:
+        line["parity"] = {"merges_equal_fixture": bool(np.array_equal(np.array(merges, dtype=np.uint32), want)),
+                          "merges_checked": int(want.shape[0])}
+    return line
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=254, help="timed batches of 128 merges (254 = full 32K vocab)")
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=5, help="timed steps: complete training runs of the headline corpus")
+    ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--vocab", type=int, default=32768)
-    ap.add_argument("--train-bytes", type=int, default=104_857_600)
     ap.add_argument("--encode-bytes", type=int, default=1 << 30)
     ap.add_argument("--vocab-sample-bytes", type=int, default=104_857_600)
     ap.add_argument("--no-encode", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP-event roofline pass")
-    ap.add_argument("--cpu-merges", type=int, default=0, help="CPU baseline merges (0 = auto, ~10-30 s)")
-    ap.add_argument("--no-parity", action="store_true", help="N>1: skip the single-stream parity check")
+    ap.add_argument("--no-c2", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP-event roofline run")
+    ap.add_argument("--cpu-merges", type=int, default=0, help="CPU baseline merges on the CPU share (0 = 24)")
     ap.add_argument("--sharded", action="store_true", help="use the sharded trainer even at N=1 (RCCL rehearsal)")
     args = ap.parse_args()
 
@@ -499,55 +574,10 @@ def main():
     rc = lib.gbpe_ctx_create(int(os.environ.get("GBPE_BENCH_DEVICE", local)) if world > 1 else 0, C.byref(ctx))
     if rc != 0:
         raise SystemExit(f"gbpe_ctx_create failed ({rc}): no MI355X visible")
-
     if world > 1 or args.sharded:
-        line, data = sharded_line(args, lib, ctx, dist, rank, world)
+        line = sharded_line(args, lib, ctx, dist, rank, world)
     else:
-        data, tr = train_leg(args, lib, ctx, dist, rank)
-        line = single_line(args, tr)
-
-    pmc = os.path.join(ROOT, "profiles", "r1_pmc_kbody.json")
-    if world == 1 and not args.sharded and os.path.exists(pmc) and args.train_bytes == 104_857_600 and \
-            tr["bytes_per_symbol"] == 2 and "bytes_per_launch" in line["roofline"]:
-        # HBM bytes per k_body launch from the committed rocprofv3 --pmc passes
-        # (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction) of this same workload
-        p = json.load(open(pmc))
-        line["roofline"]["traffic"] = round(p["hbm_bytes_per_launch"])
-        line["roofline"]["traffic_unit"] = "bytes/launch (k_body)"
-        line["roofline"]["traffic_over_algorithmic"] = round(p["hbm_bytes_per_launch"] / p["algorithmic_bytes_per_launch"], 4)
-        line["roofline"]["traffic_sample"] = (f"profiles/r1_pmc_kbody.json: {p['launches']} k_body launches, "
-                                              f"FETCH_SIZE and WRITE_SIZE passes")
-
-    enc = None
-    if not args.no_encode:
-        enc = encode_leg(args, lib, ctx, dist, rank)
-        line["tokenize"] = enc[-1]
-
-    if world == 1 and not args.sharded and not args.no_cpu:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import cpu_ref
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        k = args.cpu_merges or 256
-        t = time.perf_counter()
-        r = cpu_ref.train(data, args.vocab, max_merges=k, threads=threads, want_symbols=False)
-        dt = time.perf_counter() - t
-        line["cpu_baseline"] = {"value": round(len(r["merges"]) / dt, 3), "unit": "merges/s", "cores": threads,
-                                "kind": "port",
-                                "sample": f"first {len(r['merges'])} merges of the same C2 corpus, full pair "
-                                          f"recount per merge (reference algorithm, oracle/bpe_oracle.c), {dt:.1f}s"}
-        # full-size parity: the GPU run's first k merges equal the CPU restatement's
-        g = first_merges(lib, ctx, data, args.vocab, len(r["merges"]))
-        line["parity"] = {"train_first_merges_equal": g == r["merges"], "train_merges_checked": len(r["merges"])}
-        if enc is not None:
-            text, nodes, edges, cs, tokens, er = enc
-            t = time.perf_counter()
-            ref_tokens = cpu_ref.encode(text, nodes, edges, cs, threads=threads)
-            dt = time.perf_counter() - t
-            er["cpu_baseline"] = {"value": round(len(text) / 1e9 / dt, 3), "unit": "GB/s", "cores": threads,
-                                  "kind": "port", "sample": f"full {len(text)} B encode, chunked greedy trie walk "
-                                                            f"(oracle/bpe_oracle.c), {dt:.1f}s"}
-            line["parity"]["encode_tokens_equal"] = bool(np.array_equal(tokens, ref_tokens))
-            line["parity"]["encode_tokens_checked"] = int(len(ref_tokens))
+        line = single_line(args, lib, ctx, dist, rank)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if _COMM.get("c"):

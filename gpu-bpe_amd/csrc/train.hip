@@ -1391,7 +1391,6 @@ template <typename S, int BT> struct ZoneDim {
     static constexpr int ZPT = (BT == 1024 && sizeof(S) == 4) ? 16 : 32;   // zone positions per thread
     static constexpr uint32_t ZMAX = (uint32_t)BT * ZPT;   // 8192 (256) / 32768 or 16384 (1024) symbols
     static constexpr uint32_t ZWIN = ZMAX / 4;              // >= ZMAX / 5 >= mc (zone >= 5 mc)
-    static constexpr uint32_t WPW = BT == 1024 ? 32 : 16;  // bitmap words (32 sectors each) per workgroup
 };
 template <typename S, int BT>
 struct ZoneLds {
@@ -1686,46 +1685,64 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     return go;
 }
 
-// Body pass: blocks [0, nbody) each test SP_WPW bitmap words of (a-row & b-row),
-// keep the candidate sectors whose pair signature may hold (a, b), and merge them
-// (one wave per sector); blocks >= nbody copy the stale-window source
-// [n - 2mc - Bp, + mc) of the zone's other buffer to `wtmp`.
+// Body pass: blocks [0, nbody) each own `wpg` consecutive bitmap words of
+// (a-row & b-row), tested PW words at a time: the candidate sectors whose pair
+// signature may hold (a, b) are merged (one wave per sector).  A fixed grid of
+// wide workgroups (about 4 per CU at 1 GiB) instead of one workgroup per 16
+// words: the selection each workgroup repeats, and the rounds of workgroup
+// scheduling, cost more than the bitmap words themselves (75K words per row at
+// 1 GiB).  Blocks >= nbody copy the stale-window source [n - 2mc - Bp, + mc) of
+// the zone's other buffer to `wtmp`.
 // With `zst` (zone <= ZMAX), block nbody runs the whole zone pass (zone_one) and
 // there are no copy blocks: one launch merges body and zone.
+constexpr uint32_t SP_PW = 64;               // bitmap words tested per pass (one per lane of wave 0)
+constexpr uint32_t SP_CAP = SP_PW * 32;      // candidate sectors per pass
+struct BodyCand {
+    uint32_t sec[SP_CAP];
+    uint2 ext[SP_CAP];
+};
+template <typename S, int BT>
+union BodyLds {   // body workgroups use the candidate arrays, the zone workgroup the zone
+    ZoneLds<S, BT> z;
+    BodyCand c;
+};
+
 template <typename S, bool EXACT, int BT>
 __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
-                                              uint32_t* __restrict__ bits, uint32_t W, uint32_t* __restrict__ sig,
-                                              Table tb, uint32_t nbody, const S* __restrict__ zoth, S* __restrict__ wtmp,
+                                              uint32_t* __restrict__ bits, uint32_t W, uint32_t wpg,
+                                              uint32_t* __restrict__ sig, Table tb, uint32_t nbody,
+                                              const S* __restrict__ zoth, S* __restrict__ wtmp,
                                               uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
                                               Table dtb, SelShard sh) {
     __shared__ LdsTab<LTAB_T> lt;
-    constexpr uint32_t SP_WPW = ZoneDim<S, BT>::WPW;
-    __shared__ uint32_t s_tok[SP_WPW * 32], s_list[SP_WPW * 32];
-    __shared__ uint2 s_ext[SP_WPW * 32];
-    __shared__ uint32_t s_ntok, s_n, s_rm[BT / 64];
+    __shared__ BodyLds<S, BT> u;
+    __shared__ uint32_t s_ntok, s_n, s_any, s_rm[BT / 64];
     __shared__ uint64_t s_mv[BT / 64];
-    __shared__ ZoneLds<S, BT> zl;
+    constexpr int QPT = SP_CAP / BT;   // candidates per thread in the signature test
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     uint32_t a, b, nw, mc;
     if (t == 0) KT(0);
     const DevState *gs, *zs;   // this workgroup's snapshots of the states at launch (LDS)
     if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh)) return;
     if (t == 0) KT(1);
+    // the zone workgroup is dispatched first (block 0): it is the longest single
+    // chain of the merge, and later blocks of a large grid start later
+    const uint32_t bid = zone1 ? (blockIdx.x == 0 ? nbody : blockIdx.x - 1u) : blockIdx.x;
     // deltas go to the replica (single GPU) or to the per-merge delta table (sharded)
-    if (zone1 && blockIdx.x == nbody) {
-        zone_one<S, EXACT, BT>(st, zst, *gs, *zs, zcur, (S*)zoth, zl, lt, dtb, a, b, nw, mc, wg_bytes + nbody, round);
+    if (zone1 && bid == nbody) {
+        zone_one<S, EXACT, BT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, dtb, a, b, nw, mc, wg_bytes + nbody, round);
         if (t == 0) {
             KT(5);
             KTV(6, 2);
         }
         return;
     }
-    if (blockIdx.x >= nbody) {
+    if (bid >= nbody) {
         const uint64_t src0 = (uint64_t)gs->n + gs->off - gs->poff - 2ull * mc - gs->Bp;
         const uint64_t stride = (uint64_t)(gridDim.x - nbody) * BT;
-        for (uint64_t u = (uint64_t)(blockIdx.x - nbody) * BT + t; u < mc; u += stride) wtmp[u] = zoth[src0 + u];
+        for (uint64_t v = (uint64_t)(bid - nbody) * BT + t; v < mc; v += stride) wtmp[v] = zoth[src0 + v];
         if (t == 0) {
             KT(5);
             KTV(6, 3);
@@ -1733,82 +1750,102 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         return;
     }
     const uint32_t pid_ab = (a << 16) | b;
-    if (t == 0) {
-        s_ntok = 0u;
-        s_n = 0u;
-    }
-    __syncthreads();
-    if (t < (int)SP_WPW) {   // token candidates
-        const uint32_t w = blockIdx.x * SP_WPW + t;
-        uint32_t c = 0;
-        if (w < W) c = bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w];
-        if (c) {
-            uint32_t pos = atomicAdd(&s_ntok, (uint32_t)__popc(c));
-            while (c) {
-                const int bit = __ffs(c) - 1;
-                c &= c - 1;
-                s_tok[pos++] = w * 32u + (uint32_t)bit;
-            }
-        }
-    }
-    __syncthreads();
-    const uint32_t ntok = s_ntok;
-    if (t == 0) KT(2);
-    if (ntok == 0) {
-        if (t == 0) {
-            KT(5);
-            KTV(6, 0);
-        }
-        return;
-    }
-    if (t == 0) atomicAdd(&wg_bytes[blockIdx.x], 16ull * ntok);   // extents + signature words read (no-return add: no round trip)
-    for (uint32_t j = t; j < ntok; j += BT) {   // signature filter; the sector's extent loads alongside
-        const uint32_t sct = s_tok[j];
-        const uint2 e = sec[sct];
-        if (sig_has(sig + (uint64_t)sct * SP_SIGW, pid_ab)) {
-            const uint32_t q = atomicAdd(&s_n, 1u);
-            s_list[q] = sct;
-            s_ext[q] = e;
-        }
-    }
-    __syncthreads();
-    const uint32_t ncand = s_n;
-    if (t == 0) KT(3);
-    if (ncand == 0) {
-        if (t == 0) {
-            KT(5);
-            KTV(6, 0);
-        }
-        return;
-    }
-    if (t == 0 && clog) atomicAdd(&st->cand, ncand);
+    BodyCand& cb = u.c;
     lds_clear(lt);
-    __syncthreads();
-    uint32_t removed = 0;
-    uint64_t moved = 0;   // sector symbols read + rewritten (wave-uniform)
-    // software-pipelined: a wave's next sector loads while it merges this one
-    uint32_t nf[5];
-    if (wid < ncand) sector_first<S>(body + s_ext[wid].x, s_ext[wid].y, nf);
-    for (uint32_t j = wid; j < ncand; j += BT / 64) {
-        const uint32_t sct = s_list[j];
-        const uint2 e = s_ext[j];
-        uint32_t cf[5];
+    if (t == 0) s_any = 0u;
+    uint32_t removed = 0, ncand_all = 0;
+    uint64_t moved = 0, rd = 0;   // sector symbols read + rewritten (wave-uniform); extents + signature words read
+    const uint32_t w_beg = bid * wpg, w_end = w_beg + wpg < W ? w_beg + wpg : W;
+    for (uint32_t w0 = w_beg; w0 < w_end; w0 += SP_PW) {
+        __syncthreads();   // the previous pass is done with s_ntok / s_n / the candidate arrays
+        if (t == 0) {
+            s_ntok = 0u;
+            s_n = 0u;
+        }
+        __syncthreads();
+        if (t < (int)SP_PW && w0 + t < w_end) {   // token candidates
+            const uint32_t w = w0 + t;
+            uint32_t c = bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w];
+            if (c) {
+                uint32_t pos = atomicAdd(&s_ntok, (uint32_t)__popc(c));
+                while (c) {
+                    const int bit = __ffs(c) - 1;
+                    c &= c - 1;
+                    cb.sec[pos++] = w * 32u + (uint32_t)bit;
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t ntok = s_ntok;
+        if (t == 0) KT(2);
+        if (ntok == 0) continue;   // block-uniform
+        rd += 16ull * ntok;
+        // signature filter: this thread's candidates (their extents load alongside)
+        // into registers, then compacted in place
+        uint32_t cs[QPT];
+        uint2 ce[QPT];
+        bool ck[QPT];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) cf[k] = nf[k];
-        if (j + BT / 64 < ncand) sector_first<S>(body + s_ext[j + BT / 64].x, s_ext[j + BT / 64].y, nf);
-        uint32_t out = 0;
-        const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, dtb, st, sig + (uint64_t)sct * SP_SIGW, out, cf);
-        moved += (uint64_t)sizeof(S) * (e.y + (r ? out : 0u));
-        if (r) {
-            removed += r;
-            if (lane == 0) {
-                if (clog) atomicAdd(&st->hitsec, 1u);
-                sec[sct].y = out;
-                atomicOr(&bits[(uint64_t)nw * W + (sct >> 5)], 1u << (sct & 31u));
+        for (int q = 0; q < QPT; ++q) {
+            const uint32_t j = (uint32_t)t + (uint32_t)q * BT;
+            cs[q] = j < ntok ? cb.sec[j] : SP_INV;
+        }
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) {
+            ck[q] = false;
+            if (cs[q] != SP_INV) {
+                ce[q] = sec[cs[q]];
+                ck[q] = sig_has(sig + (uint64_t)cs[q] * SP_SIGW, pid_ab);
+            }
+        }
+        __syncthreads();   // every candidate is read before the list is rewritten
+#pragma unroll
+        for (int q = 0; q < QPT; ++q)
+            if (ck[q]) {
+                const uint32_t qq = atomicAdd(&s_n, 1u);
+                cb.sec[qq] = cs[q];
+                cb.ext[qq] = ce[q];
+            }
+        __syncthreads();
+        const uint32_t ncand = s_n;
+        if (t == 0) KT(3);
+        if (ncand == 0) continue;   // block-uniform
+        ncand_all += ncand;
+        if (t == 0) s_any = 1u;
+        // software-pipelined: a wave's next sector loads while it merges this one
+        uint32_t nf[5];
+        if ((uint32_t)wid < ncand) sector_first<S>(body + cb.ext[wid].x, cb.ext[wid].y, nf);
+        for (uint32_t j = wid; j < ncand; j += BT / 64) {
+            const uint32_t sct = cb.sec[j];
+            const uint2 e = cb.ext[j];
+            uint32_t cf[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) cf[k] = nf[k];
+            if (j + BT / 64 < ncand) sector_first<S>(body + cb.ext[j + BT / 64].x, cb.ext[j + BT / 64].y, nf);
+            uint32_t out = 0;
+            const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, dtb, st, sig + (uint64_t)sct * SP_SIGW, out, cf);
+            moved += (uint64_t)sizeof(S) * (e.y + (r ? out : 0u));
+            if (r) {
+                removed += r;
+                if (lane == 0) {
+                    if (clog) atomicAdd(&st->hitsec, 1u);
+                    sec[sct].y = out;
+                    atomicOr(&bits[(uint64_t)nw * W + (sct >> 5)], 1u << (sct & 31u));
+                }
             }
         }
     }
+    __syncthreads();
     if (t == 0) KT(4);
+    if (!s_any) {   // block-uniform: no candidate survived the filters
+        if (t == 0) {
+            if (rd) atomicAdd(&wg_bytes[bid], rd);
+            KT(5);
+            KTV(6, 0);
+        }
+        return;
+    }
+    if (t == 0 && clog) atomicAdd(&st->cand, ncand_all);
     lds_flush(lt, dtb, st);
     if (lane == 0) {
         s_rm[wid] = removed;
@@ -1817,15 +1854,15 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     __syncthreads();
     if (t == 0) {
         uint32_t r = 0;
-        uint64_t mv = 0;
+        uint64_t mv = rd;
         for (int w2 = 0; w2 < BT / 64; ++w2) {
             r += s_rm[w2];
             mv += s_mv[w2];
         }
         if (r) atomicAdd(&st->body_rm, r);
-        atomicAdd(&wg_bytes[blockIdx.x], mv);   // this workgroup's own counter
+        atomicAdd(&wg_bytes[bid], mv);   // this workgroup's own counter
         KT(5);
-        KTV(6, 1 | (ncand << 8));
+        KTV(6, 1 | (ncand_all << 8));
     }
 }
 
@@ -2076,6 +2113,7 @@ struct gbpe_trainer {
     uint32_t sp_zt = 7;          // zone target = sp_zt * last_mc + 64 (>= 5: see sp_enter; 7 measured best, GBPE_SPARSE_ZT)
     bool fuse_sel = false;       // GBPE_FUSE_SELECT=1: select in k_refresh's last workgroup (measured slower: DESIGN §2b)
     uint32_t refresh_blocks = 0; // GBPE_REFRESH_BLOCKS: k_refresh grid (0 = 2 per CU)
+    uint32_t body_cap = 256;     // GBPE_BODY_WG: most k_body workgroups (default one per CU)
     bool use_graph = false;      // replay steps as HIP graphs (GBPE_GRAPH=1): measured slower on ROCm 7
     hipGraphExec_t graph_exec = nullptr;
     GraphKey graph_key;
@@ -2184,6 +2222,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
 
 struct SpGrid {
     uint32_t body, copy, zdelta, zcompact, refresh;
+    uint32_t wpg = 16;    // bitmap words per k_body workgroup
     uint32_t ztail = 0;   // stale-tail slice blocks of the multi-tile zone k_delta
     bool zone1;   // the zone fits one workgroup: it runs inside k_body
     int bt;       // k_body workgroup size (256 or 1024)
@@ -2191,7 +2230,19 @@ struct SpGrid {
 
 template <typename S>
 uint32_t zone_max(int bt) { return bt == 1024 ? ZoneDim<S, 1024>::ZMAX : ZoneDim<S, 256>::ZMAX; }
-inline uint32_t body_wpw(int bt) { return bt == 1024 ? ZoneDim<uint16_t, 1024>::WPW : ZoneDim<uint16_t, 256>::WPW; }
+// k_body grid: bitmap words per workgroup (>= the measured best 16 / 32 at C2 size),
+// at most `cap` workgroups (GBPE_BODY_WG; default 4 per CU)
+inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* wpg) {
+    const uint32_t W = (uint32_t)gbpe_div_up(t->nsec, 32);
+    const uint32_t minw = bt == 1024 ? 32u : 16u;
+    uint32_t g = (uint32_t)gbpe_div_up(W, minw);
+    if (g > t->body_cap) g = t->body_cap;
+    if (g == 0) g = 1;
+    *wpg = (uint32_t)gbpe_div_up(W, g);
+    if (*wpg == 0) *wpg = 1;
+    *nbody = (uint32_t)gbpe_div_up(W, *wpg);
+    if (*nbody == 0) *nbody = 1;
+}
 
 // launch k_body<S, EXACT, bt> (one instantiation per workgroup size)
 template <typename S, bool EXACT, typename... A>
@@ -2212,11 +2263,11 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const uint32_t gb = g.body + (g.zone1 ? 1u : g.copy);
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
-        launch_body<S, true>(g.bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, t->sig, t->tb,
+        launch_body<S, true>(g.bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, g.zone1 ? 1u : 0u,
                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, SelShard());
     else
-        launch_body<S, false>(g.bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, t->sig, t->tb,
+        launch_body<S, false>(g.bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                               g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, g.zone1 ? 1u : 0u,
                               (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, SelShard());
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
@@ -2545,6 +2596,8 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     if (const char* e = getenv("GBPE_GRAPH")) t->use_graph = atoi(e) != 0;
     if (const char* e = getenv("GBPE_FUSE_SELECT")) t->fuse_sel = atoi(e) != 0;
     if (const char* e = getenv("GBPE_REFRESH_BLOCKS")) t->refresh_blocks = (uint32_t)atoi(e);
+    t->body_cap = (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
+    if (const char* e = getenv("GBPE_BODY_WG")) t->body_cap = std::max<uint32_t>(1, (uint32_t)atoi(e));
     if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_DELTA_MT")) t->delta_mt = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_DELTA_TPW")) {
@@ -2751,7 +2804,7 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
         const uint64_t zt = gbpe_div_up(zn, TILE);
         const uint32_t z256 = t->u16 ? zone_max<uint16_t>(256) : zone_max<uint32_t>(256);
         sg.bt = zn <= z256 ? 256 : 1024;   // small zone: the low-latency 256-thread workgroups
-        sg.body = (uint32_t)gbpe_div_up(gbpe_div_up(t->nsec, 32), body_wpw(sg.bt));
+        body_grid(t, sg.bt, &sg.body, &sg.wpg);
         sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt));
         sg.copy = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u : grid_persistent(t->ctx, gbpe_div_up(zn / 5 + 1, TPB * 8), 1);
         sg.zdelta = (uint32_t)(zt ? zt : 1);
@@ -3826,7 +3879,8 @@ int shard_phase1_sp(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl)
     const bool zone = t->h_st->is_last != 0;
     const uint32_t zn = zone ? t->n - t->h_st->B : 0u;   // the zone only shrinks within a step
     const int bt = zn <= (t->u16 ? zone_max<uint16_t>(256) : zone_max<uint32_t>(256)) ? 256 : 1024;
-    const uint32_t nbody = (uint32_t)gbpe_div_up(gbpe_div_up(t->nsec, 32), body_wpw(bt));
+    uint32_t nbody = 0, wpg = 0;
+    body_grid(t, bt, &nbody, &wpg);
     SelShard sh;
     sh.cap_list = cl;
     sh.zmax = t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024);
@@ -3834,11 +3888,11 @@ int shard_phase1_sp(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl)
     sh.rec = rec;
     const uint32_t gb = nbody + (zone ? 1u : 0u);
     if (exact)
-        launch_body<S, true>(bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, t->sig, t->tb, nbody,
+        launch_body<S, true>(bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, wpg, t->sig, t->tb, nbody,
                              (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc, zone ? 1u : 0u, (const uint64_t*)t->part,
                              t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh);
     else
-        launch_body<S, false>(bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, t->sig, t->tb, nbody,
+        launch_body<S, false>(bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, wpg, t->sig, t->tb, nbody,
                               (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc, zone ? 1u : 0u, (const uint64_t*)t->part,
                               t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh);
     const uint32_t nlb = grid_persistent(t->ctx, dt.nblk, 2);

@@ -158,7 +158,7 @@ static uint64_t merge_step(uint32_t* cur, uint32_t* oth, uint64_t n, uint32_t a,
     return new_n;
 }
 
-static void heuristic_ws(const uint8_t* d, uint64_t n, uint32_t* out) {
+void oracle_heuristic_ws(const uint8_t* d, uint64_t n, uint32_t* out) {
 #define CLS(t) ((t) == 0x0Au ? 4u : (t) == 0x20u ? 2u : ((t) - 0x30u <= 9u) ? 1u : (t) >= 0x80u ? 0u : (((t) | 0x20u) - 0x61u <= 25u) ? 0u : 3u)
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < (int64_t)n; ++i) {
@@ -194,7 +194,7 @@ int oracle_train(const uint8_t* bytes, uint64_t n, const uint8_t* ws_ext, uint32
     if (ws_ext) {
         for (uint64_t i = 0; i < n; ++i) A[i] = bytes[i] | (ws_ext[i] ? WS : 0u);
     } else {
-        heuristic_ws(bytes, n, A);
+        oracle_heuristic_ws(bytes, n, A);
     }
     uint32_t needed = target > vocab_size ? target - vocab_size : 0;
     if (max_merges && max_merges < needed) needed = max_merges;

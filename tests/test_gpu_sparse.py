@@ -102,17 +102,21 @@ def test_sparse_default_policy_large_vs_c_oracle(eng, exact):
 
 
 def test_sparse_vs_dense_full_c2(eng):
-    # BASELINE C2 at full size (100 MiB English, seed 2, all 32,512 merges to a
-    # 32K vocab): the library's policy (dense, then sector-sparse) and the dense
-    # loop alone (oracle-pinned at smaller sizes above and in test_gpu_parity)
-    # must agree on every merge, the final stream and every live pair count
-    from gpubpe import synth
-    data = synth.english(104_857_600, seed=2)
+    # BASELINE C2 at full size, the bench's own corpus (100 MiB English, seed 2,
+    # 0.5 % 3-byte punctuation; all 32,512 merges to a 32K vocab): the library's
+    # policy (dense, then sector-sparse) and the dense loop alone must each equal
+    # the committed oracle fixture (tests/golden/train_c2.npz, every merge), and
+    # agree with each other on the final stream and every live pair count
+    import gen_golden_train as G
+    want, meta = G.load_train("c2")
+    data = G.corpus(meta["corpus"])
     m1, s1, p1, st1 = _train_native(eng, data, 32768)
     m2, s2, p2, st2 = _train_native(eng, data, 32768, sparse="dense")
     assert st1.sparse_merges > 30000 and st2.sparse_merges == 0
-    assert len(m1) == 32512
-    assert m1 == m2
+    assert m1 == want.tolist()
+    assert m2 == want.tolist()
+    assert s1.shape[0] == meta["final_n"]
     assert np.array_equal(s1, s2)
     assert np.array_equal(p1[0], p2[0]) and np.array_equal(p1[1], p2[1])
-    assert st1.tail_dropped == st2.tail_dropped
+    _assert_counts_match_stream(p1, s1)
+    assert st1.tail_dropped == st2.tail_dropped == meta["tail_total"]
