@@ -1,0 +1,378 @@
+// Word-lexicon body of the sector-sparse loop.  Included by
+// train.hip inside its anonymous namespace (uses Sym, TILE, TPB, EPT, SP_INV).
+//
+// No counted pair ever spans a word start (train.wgsl:395, 483, 493) or holds
+// token 0, and 0 tokens never merge, so the body is a multiset of WORDS: two
+// occurrences with the same symbols merge identically at every merge.  The
+// body is therefore kept as one copy of every distinct word (the "store"),
+// each followed by a 0 separator (which, like a word start, blocks every
+// pair), with a per-symbol multiplicity array.  A merge then touches each
+// distinct word once and weights its count deltas by the word's multiplicity:
+// the pair counts stay exactly the stream's (1 GiB English: ~3*10^8 words,
+// ~2*10^5 distinct).  The stream order lives in an occurrence list (one uid or
+// literal per body word), expanded back to the dense stream on exit/export.
+// The reference compaction quirk only ever acts on the stream's tail, which
+// stays in the dense zone.
+
+constexpr uint32_t LX_LIT = 0x80000000u;   // occurrence of a token-0 symbol: the symbol itself (low bits)
+constexpr uint32_t LX_LONG = 0x40000000u;  // build only: a word longer than LX_LMAX (index into the long list)
+constexpr uint32_t LX_LMAX = 64;           // words up to this many symbols are deduplicated
+constexpr int LX_WPT = 16;                 // words per thread in k_lx_hash
+constexpr int LX_LT = 2048;                // LDS word-table slots per workgroup
+constexpr uint32_t LX_PROBES = 4096;       // global word-table probes before the build gives up
+
+// a body word starts at i iff no counted pair can ever span (i-1, i)
+template <typename S>
+__device__ __forceinline__ bool lx_is_start(uint32_t prev, uint32_t cur, bool first) {
+    return first || (cur & Sym<S>::WS) || !(cur & Sym<S>::TM) || !(prev & Sym<S>::TM);
+}
+
+// per 8192-symbol tile: number of word starts
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_lx_count(const S* __restrict__ x, uint32_t len, uint32_t* __restrict__ tilecnt) {
+    __shared__ uint32_t s[TPB / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    uint32_t c = 0;
+#pragma unroll 4
+    for (int k = 0; k < EPT; ++k) {
+        const uint64_t i = base + (uint64_t)k * TPB + threadIdx.x;
+        if (i < len) c += lx_is_start<S>(i ? (uint32_t)x[i - 1] : 0u, (uint32_t)x[i], i == 0) ? 1u : 0u;
+    }
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < TPB / 64; ++w) t += s[w];
+        tilecnt[blockIdx.x] = t;
+    }
+}
+
+// word start positions in stream order (tile prefix from k_chunk_scan1/2)
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_lx_wpos(const S* __restrict__ x, uint32_t len, const uint32_t* __restrict__ tpre,
+                                                 const uint64_t* __restrict__ tblk, uint32_t* __restrict__ wpos) {
+    __shared__ uint32_t pre[EPT * (TPB / 64)];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    uint32_t f = 0;   // bit k: position base + k*TPB + threadIdx.x starts a word
+#pragma unroll 4
+    for (int k = 0; k < EPT; ++k) {
+        const uint64_t i = base + (uint64_t)k * TPB + threadIdx.x;
+        const bool st = i < len && lx_is_start<S>(i ? (uint32_t)x[i - 1] : 0u, (uint32_t)x[i], i == 0);
+        f |= (st ? 1u : 0u) << k;
+        const unsigned long long m = __ballot(st);
+        if (lane == 0) pre[k * (TPB / 64) + wid] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = tpre[blockIdx.x] + (uint32_t)tblk[blockIdx.x / SCAN_BLK];
+        for (int q = 0; q < EPT * (TPB / 64); ++q) {
+            const uint32_t v = pre[q];
+            pre[q] = run;
+            run += v;
+        }
+    }
+    __syncthreads();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int k = 0; k < EPT; ++k) {
+        const bool st = (f >> k) & 1u;
+        const unsigned long long m = __ballot(st);
+        if (st) wpos[pre[k * (TPB / 64) + wid] + (uint32_t)__popcll(m & lt)] = (uint32_t)(base + (uint64_t)k * TPB + threadIdx.x);
+    }
+}
+
+// 64-bit content hash of a word (its symbols with their word-start bits, and its length)
+template <typename S>
+__device__ __forceinline__ unsigned long long lx_hash(const S* __restrict__ x, uint32_t s, uint32_t L) {
+    unsigned long long h = 0x9E3779B97F4A7C15ull ^ (unsigned long long)L;
+    for (uint32_t i = 0; i < L; ++i) {
+        h ^= (unsigned long long)x[s + i];
+        h *= 0x100000001B3ull;
+        h ^= h >> 29;
+    }
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    h *= 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 33;
+    return h ? h : 1ull;
+}
+
+__device__ __forceinline__ uint32_t lx_home(unsigned long long h, uint32_t mask) { return (uint32_t)(h ^ (h >> 32)) & mask; }
+
+// global word table (linear probing on 64-bit keys): insert-or-add `c` occurrences
+__device__ bool lx_insert(unsigned long long* __restrict__ keys, uint2* __restrict__ vals, uint32_t P,
+                          unsigned long long h, uint32_t rep, uint32_t c) {
+    uint32_t slot = lx_home(h, P - 1);
+    for (uint32_t p = 0; p < LX_PROBES; ++p, slot = (slot + 1) & (P - 1)) {
+        unsigned long long k = __hip_atomic_load(&keys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == 0ull) {
+            k = atomicCAS(&keys[slot], 0ull, h);
+            if (k == 0ull) {
+                vals[slot].x = rep;   // any occurrence represents the word
+                atomicAdd(&vals[slot].y, c);
+                return true;
+            }
+        }
+        if (k == h) {
+            atomicAdd(&vals[slot].y, c);
+            return true;
+        }
+    }
+    return false;
+}
+
+__device__ uint32_t lx_find(const unsigned long long* __restrict__ keys, uint32_t P, unsigned long long h) {
+    uint32_t slot = lx_home(h, P - 1);
+    for (uint32_t p = 0; p < LX_PROBES; ++p, slot = (slot + 1) & (P - 1)) {
+        const unsigned long long k = keys[slot];
+        if (k == h) return slot;
+        if (k == 0ull) return SP_INV;
+    }
+    return SP_INV;
+}
+
+// Word multiplicities: every workgroup aggregates 4096 words in an LDS table
+// (hot words cost one global add per workgroup, not one per occurrence), then
+// adds them into the global table.  Token-0 words become literals, long words
+// entries of their own.  ctr[0] = long words, ctr[1] = failure flag.
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32_t len, const uint32_t* __restrict__ wpos,
+                                                 uint32_t nw, unsigned long long* __restrict__ keys, uint2* __restrict__ vals,
+                                                 uint32_t P, uint32_t* __restrict__ otmp, uint32_t* __restrict__ longs,
+                                                 uint32_t* __restrict__ ctr) {
+    __shared__ unsigned long long lk[LX_LT];
+    __shared__ uint32_t lc[LX_LT], lr[LX_LT];
+    for (int i = threadIdx.x; i < LX_LT; i += TPB) {
+        lk[i] = 0ull;
+        lc[i] = 0u;
+    }
+    __syncthreads();
+    const uint64_t j0 = (uint64_t)blockIdx.x * (TPB * LX_WPT);
+    for (int q = 0; q < LX_WPT; ++q) {
+        const uint64_t j = j0 + (uint64_t)q * TPB + threadIdx.x;
+        if (j >= nw) break;
+        const uint32_t s = wpos[j], e = j + 1 < nw ? wpos[j + 1] : len, L = e - s;
+        const uint32_t v0 = x[s];
+        if (!(v0 & Sym<S>::TM)) {
+            otmp[j] = LX_LIT | v0;
+            continue;
+        }
+        if (L > LX_LMAX) {
+            const uint32_t li = atomicAdd(&ctr[0], 1u);
+            longs[li] = (uint32_t)j;
+            otmp[j] = LX_LONG | li;
+            continue;
+        }
+        otmp[j] = 0u;
+        const unsigned long long h = lx_hash<S>(x, s, L);
+        uint32_t slot = lx_home(h, LX_LT - 1);
+        bool done = false;
+        for (int p = 0; p < 32 && !done; ++p, slot = (slot + 1) & (LX_LT - 1)) {
+            const unsigned long long o = atomicCAS(&lk[slot], 0ull, h);
+            if (o == 0ull) {
+                lr[slot] = (uint32_t)j;
+                atomicAdd(&lc[slot], 1u);
+                done = true;
+            } else if (o == h) {
+                atomicAdd(&lc[slot], 1u);
+                done = true;
+            }
+        }
+        if (!done && !lx_insert(keys, vals, P, h, (uint32_t)j, 1u)) ctr[1] = 1u;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < LX_LT; i += TPB)
+        if (lk[i] && !lx_insert(keys, vals, P, lk[i], lr[i], lc[i])) ctr[1] = 1u;
+}
+
+constexpr uint32_t LX_TB = TPB * 16;   // word-table slots per uid-assignment block
+
+__global__ __launch_bounds__(TPB) void k_lx_tabcount(const unsigned long long* __restrict__ keys, uint32_t P,
+                                                     uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t s[TPB / 64];
+    const uint64_t b0 = (uint64_t)blockIdx.x * LX_TB + (uint64_t)threadIdx.x * 16;
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c += (b0 + k < P && keys[b0 + k]) ? 1u : 0u;
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < TPB / 64; ++w) t += s[w];
+        cnt[blockIdx.x] = t;
+    }
+}
+
+// word length of word j of the segment
+__device__ __forceinline__ uint32_t lx_wlen(const uint32_t* __restrict__ wpos, uint32_t nw, uint32_t len, uint32_t j) {
+    return (j + 1 < nw ? wpos[j + 1] : len) - wpos[j];
+}
+
+// uids in slot order: usz = length + 1 (its separator), umul = occurrences,
+// urep = a representative's position; the slot's count becomes the uid
+__global__ __launch_bounds__(TPB) void k_lx_tabuid(const unsigned long long* __restrict__ keys, uint2* __restrict__ vals,
+                                                   uint32_t P, const uint32_t* __restrict__ bpre,
+                                                   const uint64_t* __restrict__ bblk, const uint32_t* __restrict__ wpos,
+                                                   uint32_t nw, uint32_t len, uint32_t* __restrict__ usz,
+                                                   uint32_t* __restrict__ umul, uint32_t* __restrict__ urep) {
+    __shared__ uint32_t s[TPB / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t b0 = (uint64_t)blockIdx.x * LX_TB + (uint64_t)threadIdx.x * 16;
+    uint32_t occ = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) occ |= ((b0 + k < P && keys[b0 + k]) ? 1u : 0u) << k;
+    const uint32_t c = (uint32_t)__popc(occ);
+    uint32_t incl = c;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) s[wid] = incl;
+    __syncthreads();
+    uint32_t u = bpre[blockIdx.x] + (uint32_t)bblk[blockIdx.x / SCAN_BLK] + incl - c;
+    for (int w = 0; w < wid; ++w) u += s[w];
+    for (uint32_t r = occ; r; r &= r - 1) {
+        const uint64_t slot = b0 + (uint64_t)(__ffs(r) - 1);
+        const uint2 v = vals[slot];
+        usz[u] = lx_wlen(wpos, nw, len, v.x) + 1u;
+        umul[u] = v.y;
+        urep[u] = wpos[v.x];
+        vals[slot].y = u;
+        ++u;
+    }
+}
+
+// long words: an entry each (uids after the deduplicated ones)
+__global__ void k_lx_longs(const uint32_t* __restrict__ longs, const uint32_t* __restrict__ ctr, uint32_t nshort,
+                           const uint32_t* __restrict__ wpos, uint32_t nw, uint32_t len, uint32_t* __restrict__ usz,
+                           uint32_t* __restrict__ umul, uint32_t* __restrict__ urep) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ctr[0]) return;
+    const uint32_t j = longs[i];
+    usz[nshort + i] = lx_wlen(wpos, nw, len, j) + 1u;
+    umul[nshort + i] = 1u;
+    urep[nshort + i] = wpos[j];
+}
+
+// store layout: word u at off(u) (scanned sizes), its separator after it; the
+// multiplicity of every symbol (0 for separators)
+template <typename S>
+__global__ void k_lx_fill(const S* __restrict__ x, const uint32_t* __restrict__ urep, const uint32_t* __restrict__ usz,
+                          const uint32_t* __restrict__ umul, const uint32_t* __restrict__ upre,
+                          const uint64_t* __restrict__ ublk, uint32_t nu, S* __restrict__ store, uint32_t* __restrict__ mul) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nu) return;
+    const uint32_t off = upre[u] + (uint32_t)ublk[u / SCAN_BLK], L = usz[u] - 1u, r = urep[u], m = umul[u];
+    for (uint32_t i = 0; i < L; ++i) {
+        store[off + i] = x[r + i];
+        mul[off + i] = m;
+    }
+    store[off + L] = (S)0;
+    mul[off + L] = 0u;
+}
+
+// sector windows over the new store region [sbase, sbase + T): window k's
+// sector starts at its first word (starts[] preset to SP_INV); w0 = its first uid
+__global__ void k_lx_secstart(const uint32_t* __restrict__ upre, const uint64_t* __restrict__ ublk, uint32_t nu,
+                              uint32_t SEC, uint32_t sbase, uint32_t uid_base, uint32_t* __restrict__ starts,
+                              uint32_t* __restrict__ w0) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nu) return;
+    const uint32_t o = upre[u] + (uint32_t)ublk[u / SCAN_BLK], k = o / SEC;
+    const bool first = u == 0 || (upre[u - 1] + (uint32_t)ublk[(u - 1) / SCAN_BLK]) / SEC != k;
+    if (first) {
+        starts[k] = sbase + o;
+        w0[k] = uid_base + u;
+    }
+}
+
+// occurrence list of the segment's words (stream order): the uid of each word,
+// after checking its symbols against the representative's (a hash collision
+// fails the build instead of merging two different words)
+template <typename S>
+__global__ void k_lx_occ(const S* __restrict__ x, const uint32_t* __restrict__ wpos, uint32_t nw, uint32_t len,
+                         const uint32_t* __restrict__ otmp, const unsigned long long* __restrict__ keys,
+                         const uint2* __restrict__ vals, uint32_t P, const uint32_t* __restrict__ urep,
+                         const uint32_t* __restrict__ usz, uint32_t nshort, uint32_t uid_base, uint32_t* __restrict__ occ,
+                         uint32_t* __restrict__ ctr) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nw) return;
+    const uint32_t o = otmp[j];
+    if (o & LX_LIT) {
+        occ[j] = o;
+        return;
+    }
+    if (o & LX_LONG) {
+        occ[j] = uid_base + nshort + (o & ~LX_LONG);
+        return;
+    }
+    const uint32_t s = wpos[j], L = lx_wlen(wpos, nw, len, (uint32_t)j);
+    const uint32_t slot = lx_find(keys, P, lx_hash<S>(x, s, L));
+    bool ok = slot != SP_INV;
+    uint32_t u = 0;
+    if (ok) {
+        u = vals[slot].y;
+        const uint32_t r = urep[u];
+        ok = usz[u] == L + 1u;
+        for (uint32_t i = 0; ok && i < L; ++i) ok = x[r + i] == x[s + i];
+    }
+    if (!ok) ctr[1] = 1u;
+    occ[j] = uid_base + u;
+}
+
+// ── store → stream (sparse exit, symbol export) ──
+
+// current offset and length of every word, from the separators (one wave per sector)
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_lx_wordpos(const S* __restrict__ store, const uint2* __restrict__ sec,
+                                                    uint32_t nsec, const uint32_t* __restrict__ w0,
+                                                    uint32_t* __restrict__ coff, uint32_t* __restrict__ clen) {
+    const uint32_t k = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (k >= nsec) return;
+    const uint2 e = sec[k];
+    if (!e.y) return;
+    uint32_t uid = w0[k], cs = e.x;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (uint32_t c0 = 0; c0 < e.y; c0 += 64) {
+        const uint32_t i = e.x + c0 + (uint32_t)lane;
+        const bool sep = c0 + (uint32_t)lane < e.y && store[i] == (S)0;
+        const unsigned long long m = __ballot(sep);
+        if (sep) {
+            const unsigned long long below = m & lt;
+            const uint32_t st0 = below ? e.x + c0 + (uint32_t)(63 - __clzll((long long)below)) + 1u : cs;
+            const uint32_t u = uid + (uint32_t)__popcll(below);
+            coff[u] = st0;
+            clen[u] = i - st0;
+        }
+        uid += (uint32_t)__popcll(m);
+        if (m) cs = e.x + c0 + (uint32_t)(63 - __clzll((long long)m)) + 1u;
+    }
+}
+
+__global__ void k_lx_olen(const uint32_t* __restrict__ occ, uint64_t nocc, const uint32_t* __restrict__ clen,
+                          uint32_t* __restrict__ olen) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nocc) return;
+    const uint32_t o = occ[j];
+    olen[j] = (o & LX_LIT) ? 1u : clen[o];
+}
+
+template <typename S>
+__global__ void k_lx_expand(const uint32_t* __restrict__ occ, uint64_t nocc, const uint32_t* __restrict__ coff,
+                            const uint32_t* __restrict__ clen, const S* __restrict__ store,
+                            const uint32_t* __restrict__ opre, const uint64_t* __restrict__ oblk, S* __restrict__ dst) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nocc) return;
+    const uint64_t off = (uint64_t)opre[j] + oblk[j / SCAN_BLK];
+    const uint32_t o = occ[j];
+    if (o & LX_LIT) {
+        dst[off] = (S)(o & ((Sym<S>::WS << 1) - 1u));
+        return;
+    }
+    const uint32_t c = coff[o], L = clen[o];
+    for (uint32_t i = 0; i < L; ++i) dst[off + i] = store[c + i];
+}

@@ -1278,20 +1278,26 @@ __device__ __forceinline__ void sig_set(uint32_t* __restrict__ sig, uint32_t pid
 }
 
 // a sector's first wave pass: 4 symbols per lane and the one after the pass
+// (+ their word multiplicities in the lexicon body, else 1)
 template <typename S>
-__device__ __forceinline__ void sector_first(const S* __restrict__ p, uint32_t cnt, uint32_t (&f)[5]) {
+__device__ __forceinline__ void sector_first(const S* __restrict__ p, const uint32_t* __restrict__ mp, uint32_t cnt,
+                                             uint32_t (&f)[5], uint32_t (&fm)[4]) {
     const uint32_t i0 = 4u * (uint32_t)(threadIdx.x & 63);
 #pragma unroll
     for (int k = 0; k < 4; ++k) f[k] = (i0 + k < cnt) ? (uint32_t)p[i0 + k] : 0u;
     f[4] = (SP_CH < cnt) ? (uint32_t)p[SP_CH] : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) fm[k] = mp ? ((i0 + k < cnt) ? mp[i0 + k] : 0u) : 1u;
 }
 
 // One wave merges one sector in place (snapshot semantics, k_delta's delta rule,
-// survivors compacted to the sector's front).  Returns the B-sides removed.
+// survivors compacted to the sector's front).  In the lexicon body (mp != null)
+// every symbol carries its word's multiplicity, which weights its count deltas
+// and moves with it.  Returns the B-sides removed (weighted: stream symbols).
 template <typename S>
-__device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uint32_t b, uint32_t nw,
-                                LdsTab<LTAB_T>& lt, const Table& tb, DevState* st, uint32_t* __restrict__ sig,
-                                uint32_t& out_cnt, const uint32_t (&first)[5]) {
+__device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, uint32_t cnt, uint32_t a, uint32_t b,
+                                uint32_t nw, LdsTab<LTAB_T>& lt, const Table& tb, DevState* st, uint32_t* __restrict__ sig,
+                                uint32_t& out_cnt, const uint32_t (&first)[5], const uint32_t (&firstm)[4]) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     const int lane = threadIdx.x & 63;
     const uint32_t pid_ab = (a << 16) | b;
@@ -1299,15 +1305,20 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uin
     for (uint32_t c0 = 0; c0 < cnt; c0 += SP_CH) {
         const uint32_t i0 = c0 + 4u * lane;
         // X[0..1] = the two symbols before this lane's four, X[6] = the one after
-        uint32_t X[7], nx;
+        uint32_t X[7], nx, M[4];
         if (c0 == 0) {   // the first pass's symbols were loaded by the caller (sector_first)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) X[2 + k] = first[k];
+            for (int k = 0; k < 4; ++k) {
+                X[2 + k] = first[k];
+                M[k] = firstm[k];
+            }
             nx = first[4];
         } else {
 #pragma unroll
             for (int k = 0; k < 4; ++k) X[2 + k] = (i0 + k < cnt) ? (uint32_t)p[i0 + k] : 0u;
             nx = (c0 + SP_CH < cnt) ? (uint32_t)p[c0 + SP_CH] : 0u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) M[k] = mp ? ((i0 + k < cnt) ? mp[i0 + k] : 0u) : 1u;
         }
         uint32_t pm1 = __shfl_up(X[5], 1), pm2 = __shfl_up(X[4], 1);
         uint32_t np = __shfl_down(X[2], 1);
@@ -1332,24 +1343,26 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uin
         for (int k = 0; k < 4; ++k) {
             const int j = k + 2;
             const bool valid = i0 + k < cnt;
+            const uint32_t w = M[k];   // a pair's occurrences = its right symbol's word multiplicity
             if (valid && !h[j]) keep |= 1u << k;
+            if (valid && h[j]) removed += w;
             vals[k] = h[j + 1] ? (nw | (X[j] & WS)) : X[j];
             touched |= valid && (h[j] || h[j + 1]);
             if (valid && !(X[j] & WS) && (h[j - 1] || h[j] || h[j + 1])) {
                 const uint32_t tp = X[j - 1] & TM, ti = X[j] & TM;
                 if (tp && ti) {
                     const uint32_t pid = (tp << 16) | ti;
-                    if (pid != pid_ab) lds_add(lt, tb, st, pid, 0xFFFFFFFFu);   // old pair destroyed
+                    if (pid != pid_ab) lds_add(lt, tb, st, pid, 0u - w);   // old pair destroyed
                 }
                 if (!h[j]) {
                     if (h[j - 1]) {
                         const uint32_t t2 = h[j + 1] ? nw : ti;
                         if (t2) {
-                            lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+                            lds_add(lt, tb, st, (nw << 16) | t2, w);
                             sig_or(sig, (nw << 16) | t2);
                         }
                     } else if (h[j + 1] && tp) {
-                        lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+                        lds_add(lt, tb, st, (tp << 16) | nw, w);
                         sig_or(sig, (tp << 16) | nw);
                     }
                 }
@@ -1367,13 +1380,15 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t cnt, uint32_t a, uin
             uint32_t w = out + incl - kc;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if ((keep >> k) & 1u) p[w++] = (S)vals[k];
+                if ((keep >> k) & 1u) {
+                    if (mp) mp[w] = M[k];
+                    p[w++] = (S)vals[k];
+                }
         }
-        const uint32_t nvalid = cnt - c0 < SP_CH ? cnt - c0 : SP_CH;
-        removed += nvalid - tot;
         out += tot;
     }
     out_cnt = out;
+    for (int off = 32; off > 0; off >>= 1) removed += __shfl_xor(removed, off);   // per lane → the wave's
     return removed;
 }
 
@@ -1715,7 +1730,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                                               uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
-                                              Table dtb, SelShard sh) {
+                                              Table dtb, SelShard sh, uint32_t* __restrict__ lmul) {
     __shared__ LdsTab<LTAB_T> lt;
     __shared__ BodyLds<S, BT> u;
     __shared__ uint32_t s_ntok, s_n, s_any, s_rm[BT / 64];
@@ -1813,18 +1828,25 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         ncand_all += ncand;
         if (t == 0) s_any = 1u;
         // software-pipelined: a wave's next sector loads while it merges this one
-        uint32_t nf[5];
-        if ((uint32_t)wid < ncand) sector_first<S>(body + cb.ext[wid].x, cb.ext[wid].y, nf);
+        uint32_t nf[5], nfm[4];
+        if ((uint32_t)wid < ncand)
+            sector_first<S>(body + cb.ext[wid].x, lmul ? lmul + cb.ext[wid].x : nullptr, cb.ext[wid].y, nf, nfm);
         for (uint32_t j = wid; j < ncand; j += BT / 64) {
             const uint32_t sct = cb.sec[j];
             const uint2 e = cb.ext[j];
-            uint32_t cf[5];
+            uint32_t cf[5], cfm[4];
 #pragma unroll
             for (int k = 0; k < 5; ++k) cf[k] = nf[k];
-            if (j + BT / 64 < ncand) sector_first<S>(body + cb.ext[j + BT / 64].x, cb.ext[j + BT / 64].y, nf);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cfm[k] = nfm[k];
+            if (j + BT / 64 < ncand) {
+                const uint2 en = cb.ext[j + BT / 64];
+                sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
+            }
             uint32_t out = 0;
-            const uint32_t r = body_sector<S>(body + e.x, e.y, a, b, nw, lt, dtb, st, sig + (uint64_t)sct * SP_SIGW, out, cf);
-            moved += (uint64_t)sizeof(S) * (e.y + (r ? out : 0u));
+            const uint32_t r = body_sector<S>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, dtb, st,
+                                              sig + (uint64_t)sct * SP_SIGW, out, cf, cfm);
+            moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (r ? out : 0u));
             if (r) {
                 removed += r;
                 if (lane == 0) {
@@ -2018,6 +2040,8 @@ __global__ __launch_bounds__(TPB) void k_sp_gather(const S* __restrict__ body, c
     for (uint32_t j = lane; j < e.y; j += 64) dst[off + j] = body[e.x + j];
 }
 
+#include "lexicon.h"
+
 }  // namespace
 
 // ─── host side ──────────────────────────────────────────────────────────────
@@ -2121,6 +2145,20 @@ struct gbpe_trainer {
     uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
     uint32_t* h_clog = nullptr;
     FILE* trace = nullptr;
+    // word-lexicon body (lexicon.h): the sectors hold one copy of every
+    // distinct body word instead of the body itself
+    bool lex = false;            // the current sparse entry uses it
+    bool lex_on = true;          // GBPE_LEXICON=0: never
+    void* lx_store = nullptr;    // distinct words, each followed by a 0 separator (S symbols)
+    uint32_t* lx_mul = nullptr;  // per store symbol: its word's occurrences (0 = separator / padding)
+    uint64_t lx_cap = 0, lx_len = 0;   // store symbols: capacity, used
+    uint32_t* lx_occ = nullptr;  // body words in stream order: uid, or LX_LIT | symbol
+    uint64_t lx_occ_cap = 0, lx_nocc = 0;
+    uint32_t* lx_w0 = nullptr;   // first uid of each sector window
+    uint32_t lx_nuid = 0, lx_uid_cap = 0;
+    void* lx_tmp = nullptr;      // build / expansion scratch (grown, kept)
+    uint64_t lx_tmp_bytes = 0;
+    uint64_t lx_words = 0, lx_builds = 0, lx_fallbacks = 0;   // stats
 };
 
 namespace {
@@ -2128,6 +2166,11 @@ namespace {
 int tr_err(gbpe_trainer* t, int code, const char* msg) { return gbpe_set_error(t->ctx, code, "%s", msg); }
 
 #define TR_HIP(t, call) GBPE_HIP((t)->ctx, call)
+
+// the symbols the sparse kernels merge: the lexicon store, or the body sectors in place
+inline void* sp_body(const gbpe_trainer* t) { return t->lex ? t->lx_store : t->buf[t->bcur]; }
+inline uint32_t* sp_mul(const gbpe_trainer* t) { return t->lex ? t->lx_mul : nullptr; }
+
 
 uint32_t grid_persistent(const gbpe_ctx* ctx, uint64_t work_tiles, uint32_t per_cu) {
     uint64_t g = (uint64_t)(ctx->num_cu > 0 ? ctx->num_cu : 256) * per_cu;
@@ -2263,13 +2306,15 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const uint32_t gb = g.body + (g.zone1 ? 1u : g.copy);
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
-        launch_body<S, true>(g.bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
+        launch_body<S, true>(g.bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, g.zone1 ? 1u : 0u,
-                             (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, SelShard());
+                             (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, SelShard(),
+                             sp_mul(t));
     else
-        launch_body<S, false>(g.bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
+        launch_body<S, false>(g.bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                               g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, g.zone1 ? 1u : 0u,
-                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, SelShard());
+                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, SelShard(),
+                             sp_mul(t));
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
     if (!g.zone1) {
         if (exact)
@@ -2347,15 +2392,239 @@ template <typename S>
 int sp_filters(gbpe_trainer* t, bool with_bits) {
     hipStream_t s = t->ctx->stream;
     hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(t->nsec, TPB / 64)), dim3(TPB), 0, s,
-                       (const S*)t->buf[t->bcur], (const uint2*)t->sec, 0u, t->nsec, (uint32_t*)nullptr, t->W, t->sig);
+                       (const S*)sp_body(t), (const uint2*)t->sec, 0u, t->nsec, (uint32_t*)nullptr, t->W, t->sig);
     if (with_bits) {
         TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
         hipLaunchKernelGGL(k_sp_colbits<S>, dim3((uint32_t)gbpe_div_up(t->nsec, 32)), dim3(TPB), 0, s,
-                           (const S*)t->buf[t->bcur], (const uint2*)t->sec, t->nsec, t->bits, t->W);
+                           (const S*)sp_body(t), (const uint2*)t->sec, t->nsec, t->bits, t->W);
     }
     GBPE_LAUNCH_CHECK(t->ctx);
     t->sp_age = 0;
     if (with_bits) t->sp_bits_age = 0;
+    return GBPE_OK;
+}
+
+// ── word-lexicon body ──
+
+// bump allocation over the trainer's lexicon scratch
+struct LxCarve {
+    char* base;
+    uint64_t used = 0;
+    template <typename T>
+    T* take(uint64_t n) {
+        const uint64_t b = (used + 255) & ~255ull;
+        used = b + n * sizeof(T);
+        return reinterpret_cast<T*>(base + b);
+    }
+};
+
+int lx_scratch(gbpe_trainer* t, uint64_t bytes) {
+    if (t->lx_tmp && t->lx_tmp_bytes >= bytes) return GBPE_OK;
+    TR_HIP(t, hipStreamSynchronize(t->ctx->stream));
+    hipFree(t->lx_tmp);
+    t->lx_tmp = nullptr;
+    t->lx_tmp_bytes = 0;
+    if (hipMalloc(&t->lx_tmp, bytes) != hipSuccess) {
+        t->lx_tmp = nullptr;
+        return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(lexicon scratch, %llu B) failed", (unsigned long long)bytes);
+    }
+    t->lx_tmp_bytes = bytes;
+    return GBPE_OK;
+}
+
+// exclusive scan of n u32 counts in place (k_chunk_scan1/2); blk gets n/SCAN_BLK + 2
+// entries, the total at blk[nblk]
+inline void lx_scan(hipStream_t s, uint32_t* v, uint64_t n, uint64_t* blk) {
+    const uint64_t nb = gbpe_div_up(n ? n : 1, SCAN_BLK);
+    hipLaunchKernelGGL(k_chunk_scan1, dim3((uint32_t)nb), dim3(SCAN_TPB), 0, s, (const uint32_t*)v, n, v, blk);
+    hipLaunchKernelGGL(k_chunk_scan2, dim3(1), dim3(SCAN_TPB), 0, s, blk, nb, blk + nb);
+}
+
+// What a segment's words would add to the lexicon (nothing is committed yet)
+struct LxPlan {
+    bool ok = false;
+    uint32_t nw = 0, nshort = 0, nlong = 0, nu = 0, T = 0;   // words, distinct short / long, entries, store symbols
+    uint32_t *wpos = nullptr, *usz = nullptr, *umul = nullptr, *urep = nullptr, *occ = nullptr, *upre = nullptr;
+    uint64_t* ublk = nullptr;
+};
+
+// Dedup the words of seg[0, len) (a word starts at 0): word starts, the word
+// table, entries (uids from t->lx_nuid) and the segment's occurrence list, in
+// the scratch.  plan.ok = false when a hash collision or a full word table
+// makes the segment unusable, or (fresh) the store would not be much smaller
+// than the segment.
+template <typename S>
+int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& lp) {
+    hipStream_t s = t->ctx->stream;
+    lp = LxPlan();
+    if (len == 0) return GBPE_OK;
+    const uint64_t ntiles = gbpe_div_up(len, TILE);
+    // word count first (sizes the rest of the scratch)
+    int rc = lx_scratch(t, (ntiles + 64) * 4 + (ntiles / SCAN_BLK + 4) * 8 + 1024);
+    if (rc != GBPE_OK) return rc;
+    {
+        LxCarve c{(char*)t->lx_tmp};
+        uint32_t* tc = c.take<uint32_t>(ntiles);
+        uint64_t* tb = c.take<uint64_t>(ntiles / SCAN_BLK + 4);
+        hipLaunchKernelGGL(k_lx_count<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, tc);
+        lx_scan(s, tc, ntiles, tb);
+        GBPE_LAUNCH_CHECK(t->ctx);
+        uint64_t nw64 = 0;
+        TR_HIP(t, hipMemcpyAsync(&nw64, tb + gbpe_div_up(ntiles, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
+        TR_HIP(t, hipStreamSynchronize(s));
+        lp.nw = (uint32_t)nw64;
+    }
+    const uint32_t nw = lp.nw;
+    uint64_t P = 4096;
+    while (P < 2ull * nw && P < (1ull << 27)) P <<= 1;
+    const uint64_t nbb = gbpe_div_up(P, LX_TB);
+    const uint64_t need = (ntiles + 64) * 4 + (ntiles / SCAN_BLK + 4) * 8 + 9ull * (nw + 64) * 4 + P * 16 +
+                          (nbb + 64) * 4 + 2 * (nbb / SCAN_BLK + (uint64_t)nw / SCAN_BLK + 8) * 8 + 32 * 256;
+    rc = lx_scratch(t, need);
+    if (rc != GBPE_OK) return rc;
+    LxCarve c{(char*)t->lx_tmp};
+    uint32_t* tc = c.take<uint32_t>(ntiles);
+    uint64_t* tb = c.take<uint64_t>(ntiles / SCAN_BLK + 4);
+    lp.wpos = c.take<uint32_t>(nw + 1);
+    uint32_t* otmp = c.take<uint32_t>(nw + 1);
+    uint32_t* longs = c.take<uint32_t>(nw + 1);
+    lp.usz = c.take<uint32_t>(nw + 1);
+    lp.umul = c.take<uint32_t>(nw + 1);
+    lp.urep = c.take<uint32_t>(nw + 1);
+    lp.occ = c.take<uint32_t>(nw + 1);
+    auto* keys = c.take<unsigned long long>(P);
+    auto* vals = c.take<uint2>(P);
+    uint32_t* bc = c.take<uint32_t>(nbb);
+    uint64_t* bb = c.take<uint64_t>(nbb / SCAN_BLK + 4);
+    lp.ublk = c.take<uint64_t>((uint64_t)nw / SCAN_BLK + 4);
+    uint32_t* ctr = c.take<uint32_t>(8);
+    // (the tile counts are recomputed: the scratch may have moved)
+    hipLaunchKernelGGL(k_lx_count<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, tc);
+    lx_scan(s, tc, ntiles, tb);
+    hipLaunchKernelGGL(k_lx_wpos<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, (const uint32_t*)tc,
+                       (const uint64_t*)tb, lp.wpos);
+    TR_HIP(t, hipMemsetAsync(keys, 0, P * 8, s));
+    TR_HIP(t, hipMemsetAsync(vals, 0, P * 8, s));
+    TR_HIP(t, hipMemsetAsync(ctr, 0, 32, s));
+    if (nw)
+        hipLaunchKernelGGL(k_lx_hash<S>, dim3((uint32_t)gbpe_div_up(nw, TPB * LX_WPT)), dim3(TPB), 0, s, seg, len,
+                           (const uint32_t*)lp.wpos, nw, keys, vals, (uint32_t)P, otmp, longs, ctr);
+    hipLaunchKernelGGL(k_lx_tabcount, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const unsigned long long*)keys, (uint32_t)P, bc);
+    lx_scan(s, bc, nbb, bb);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    uint32_t h[4] = {0, 0, 0, 0};
+    uint64_t nshort = 0;
+    TR_HIP(t, hipMemcpyAsync(h, ctr, 8, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipMemcpyAsync(&nshort, bb + gbpe_div_up(nbb, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    if (h[1]) return GBPE_OK;   // word table overflow: not usable
+    lp.nshort = (uint32_t)nshort;
+    lp.nlong = h[0];
+    lp.nu = lp.nshort + lp.nlong;
+    if ((uint64_t)t->lx_nuid + lp.nu >= LX_LONG) return GBPE_OK;
+    hipLaunchKernelGGL(k_lx_tabuid, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const unsigned long long*)keys, vals, (uint32_t)P,
+                       (const uint32_t*)bc, (const uint64_t*)bb, (const uint32_t*)lp.wpos, nw, len, lp.usz, lp.umul, lp.urep);
+    if (lp.nlong)
+        hipLaunchKernelGGL(k_lx_longs, dim3((uint32_t)gbpe_div_up(lp.nlong, 256)), dim3(256), 0, s, (const uint32_t*)longs,
+                           (const uint32_t*)ctr, lp.nshort, (const uint32_t*)lp.wpos, nw, len, lp.usz, lp.umul, lp.urep);
+    if (nw)
+        hipLaunchKernelGGL(k_lx_occ<S>, dim3((uint32_t)gbpe_div_up(nw, 256)), dim3(256), 0, s, seg, (const uint32_t*)lp.wpos, nw,
+                           len, (const uint32_t*)otmp, (const unsigned long long*)keys, (const uint2*)vals, (uint32_t)P,
+                           (const uint32_t*)lp.urep, (const uint32_t*)lp.usz, lp.nshort, t->lx_nuid, lp.occ, ctr);
+    // store offsets: exclusive scan of the entry sizes, in otmp (k_lx_occ, queued
+    // before on the same stream, has consumed it)
+    uint32_t* upre = otmp;
+    TR_HIP(t, hipMemcpyAsync(upre, lp.usz, (uint64_t)lp.nu * 4, hipMemcpyDeviceToDevice, s));
+    lx_scan(s, upre, lp.nu, lp.ublk);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    uint64_t T = 0;
+    TR_HIP(t, hipMemcpyAsync(&T, lp.ublk + gbpe_div_up(lp.nu ? lp.nu : 1, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipMemcpyAsync(h, ctr, 8, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    if (h[1]) return GBPE_OK;   // a hash collision (or a word missing from the table)
+    lp.T = (uint32_t)T;
+    if (fresh && T * 2 > len) return GBPE_OK;   // not worth it: the store would be more than half the body
+    lp.upre = upre;
+    lp.ok = true;
+    return GBPE_OK;
+}
+
+// Append a planned segment to the lexicon: store entries (window-aligned), their
+// sector windows after t->nsec with token bits and signatures, occurrences after
+// t->lx_nocc.  plan.ok = false (nothing changed) when the capacities cannot take it.
+template <typename S>
+int lx_commit(gbpe_trainer* t, LxPlan& lp, const S* seg, bool fresh) {
+    hipStream_t s = t->ctx->stream;
+    const uint32_t SEC = t->sp_secw;
+    const uint64_t sbase = gbpe_div_up(t->lx_len, SEC) * SEC;
+    const uint64_t nwin = gbpe_div_up(lp.T ? lp.T : 1, SEC);
+    const uint64_t kb = sbase / SEC;
+    if (sbase + nwin * SEC > t->lx_cap || kb + nwin > t->nsec_cap || kb + nwin > (uint64_t)t->W * 32 ||
+        (kb + nwin) * SP_SIGW > t->sig_cap || nwin > t->loc_cap || t->lx_nocc + lp.nw > t->lx_occ_cap) {
+        lp.ok = false;
+        return GBPE_OK;
+    }
+    S* store = (S*)t->lx_store;
+    if (sbase > t->lx_len) {   // alignment padding: separators no sector covers
+        TR_HIP(t, hipMemsetAsync(store + t->lx_len, 0, (sbase - t->lx_len) * sizeof(S), s));
+        TR_HIP(t, hipMemsetAsync(t->lx_mul + t->lx_len, 0, (sbase - t->lx_len) * 4, s));
+    }
+    const uint32_t* upre = lp.upre;
+    if (lp.nu) {
+        hipLaunchKernelGGL(k_lx_fill<S>, dim3((uint32_t)gbpe_div_up(lp.nu, 256)), dim3(256), 0, s, seg,
+                           (const uint32_t*)lp.urep, (const uint32_t*)lp.usz, (const uint32_t*)lp.umul, upre,
+                           (const uint64_t*)lp.ublk, lp.nu, store + sbase, t->lx_mul + sbase);
+        TR_HIP(t, hipMemsetAsync(t->sp_loc, 0xFF, nwin * 4, s));
+        hipLaunchKernelGGL(k_lx_secstart, dim3((uint32_t)gbpe_div_up(lp.nu, 256)), dim3(256), 0, s, upre,
+                           (const uint64_t*)lp.ublk, lp.nu, SEC, (uint32_t)sbase, t->lx_nuid, t->sp_loc, t->lx_w0 + kb);
+        hipLaunchKernelGGL(k_sp_sector_len, dim3((uint32_t)gbpe_div_up(nwin, 256)), dim3(256), 0, s,
+                           (const uint32_t*)t->sp_loc, (uint32_t)nwin, (uint32_t)(sbase + lp.T), t->sec + kb);
+    } else {
+        TR_HIP(t, hipMemsetAsync(t->sec + kb, 0, nwin * sizeof(uint2), s));
+    }
+    if (lp.nw)
+        TR_HIP(t, hipMemcpyAsync(t->lx_occ + t->lx_nocc, lp.occ, (uint64_t)lp.nw * 4, hipMemcpyDeviceToDevice, s));
+    // token bits and signatures of the new sectors (a fresh build: whole columns)
+    hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(nwin, TPB / 64)), dim3(TPB), 0, s, (const S*)store,
+                       (const uint2*)t->sec, (uint32_t)kb, (uint32_t)nwin, fresh ? (uint32_t*)nullptr : t->bits, t->W, t->sig);
+    if (fresh)
+        hipLaunchKernelGGL(k_sp_colbits<S>, dim3((uint32_t)gbpe_div_up(nwin, 32)), dim3(TPB), 0, s, (const S*)store,
+                           (const uint2*)t->sec, (uint32_t)nwin, t->bits, t->W);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    t->nsec = (uint32_t)(kb + nwin);
+    t->lx_len = sbase + lp.T;
+    t->lx_nocc += lp.nw;
+    t->lx_nuid += lp.nu;
+    t->lx_words += lp.nw;
+    return GBPE_OK;
+}
+
+// lexicon → dense stream: every body word occurrence's current symbols, in
+// stream order, to dst[0, B); returns the symbol total through *tot
+template <typename S>
+int lx_expand(gbpe_trainer* t, S* dst, uint64_t* tot) {
+    hipStream_t s = t->ctx->stream;
+    const uint64_t nu = t->lx_nuid, no = t->lx_nocc;
+    int rc = lx_scratch(t, (2 * nu + no + 64) * 4 + (no / SCAN_BLK + 8) * 8 + 4096);
+    if (rc != GBPE_OK) return rc;
+    LxCarve c{(char*)t->lx_tmp};
+    uint32_t* coff = c.take<uint32_t>(nu + 1);
+    uint32_t* clen = c.take<uint32_t>(nu + 1);
+    uint32_t* olen = c.take<uint32_t>(no + 1);
+    uint64_t* oblk = c.take<uint64_t>(no / SCAN_BLK + 4);
+    if (t->nsec)
+        hipLaunchKernelGGL(k_lx_wordpos<S>, dim3((uint32_t)gbpe_div_up(t->nsec, TPB / 64)), dim3(TPB), 0, s,
+                           (const S*)t->lx_store, (const uint2*)t->sec, t->nsec, (const uint32_t*)t->lx_w0, coff, clen);
+    if (no)
+        hipLaunchKernelGGL(k_lx_olen, dim3((uint32_t)gbpe_div_up(no, 256)), dim3(256), 0, s, (const uint32_t*)t->lx_occ, no,
+                           (const uint32_t*)clen, olen);
+    lx_scan(s, olen, no, oblk);
+    if (no)
+        hipLaunchKernelGGL(k_lx_expand<S>, dim3((uint32_t)gbpe_div_up(no, 256)), dim3(256), 0, s, (const uint32_t*)t->lx_occ,
+                           no, (const uint32_t*)coff, (const uint32_t*)clen, (const S*)t->lx_store, (const uint32_t*)olen,
+                           (const uint64_t*)oblk, dst);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    TR_HIP(t, hipMemcpyAsync(tot, oblk + gbpe_div_up(no ? no : 1, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
     return GBPE_OK;
 }
 
@@ -2382,9 +2651,22 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true) {
         if (Zs < t->sp_secw) return GBPE_OK;   // the whole stream is one long word (or tiny): stay dense
     }
     const uint32_t z = n - Zs;
-    // capacities for every sector the body can ever hold: windows over [0, n) plus
+    // word lexicon: plan the deduplicated body first; it sizes the sectors
+    t->lex = false;
+    t->lx_len = t->lx_nocc = 0;
+    t->lx_nuid = 0;
+    LxPlan lp;
+    if (t->lex_on && Zs) {
+        int rc0 = lx_analyze<S>(t, cur, Zs, true, lp);
+        if (rc0 != GBPE_OK) return rc0;
+        if (lp.ok) ++t->lx_builds;
+        else ++t->lx_fallbacks;
+    }
+    // capacities for every sector the body can ever hold: windows over [0, n) (the
+    // lexicon: over its store, and twice the zone for the words shrinks append) plus
     // one partial window per zone shrink (at most SP_SHRINKS per entry)
-    const uint64_t cap = gbpe_div_up(n, t->sp_secw) + SP_SHRINKS + 1;
+    const uint64_t cap = lp.ok ? gbpe_div_up((uint64_t)lp.T + 2ull * z, t->sp_secw) + 2 * (SP_SHRINKS + 1)
+                               : gbpe_div_up(n, t->sp_secw) + SP_SHRINKS + 1;
     int rc = sp_grow(t, &t->sec, &t->nsec_cap, cap);
     if (rc == GBPE_OK && (!t->sp_loc || t->loc_cap < cap)) {
         hipFree(t->sp_loc);
@@ -2407,7 +2689,59 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true) {
     t->nsec = 0;
     TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
     TR_HIP(t, hipMemsetAsync(t->sig, 0, cap * SP_SIGW * 4, s));
-    rc = sp_add_sectors<S>(t, 0u, Zs);
+    if (lp.ok) {
+        const uint64_t scap = cap * t->sp_secw, ocap = (uint64_t)lp.nw + z + 1;
+        if (!t->lx_store || t->lx_cap < scap) {
+            hipFree(t->lx_store);
+            hipFree(t->lx_mul);
+            hipFree(t->lx_w0);
+            t->lx_store = nullptr;
+            t->lx_mul = t->lx_w0 = nullptr;
+            t->lx_cap = 0;
+            if (hipMalloc(&t->lx_store, scap * t->bps) != hipSuccess || hipMalloc(&t->lx_mul, scap * 4) != hipSuccess ||
+                hipMalloc(&t->lx_w0, cap * 4) != hipSuccess)
+                return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(word lexicon) failed");
+            t->lx_cap = scap;
+        }
+        rc = sp_grow(t, &t->lx_occ, &t->lx_occ_cap, ocap);
+        if (rc != GBPE_OK) return rc;
+        t->lex = true;
+        rc = lx_commit<S>(t, lp, cur, true);
+        if (rc == GBPE_OK && !lp.ok) rc = gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "word lexicon capacity");
+        if (rc == GBPE_OK && getenv("GBPE_LEX_CHECK")) {   // diagnostic: the lexicon expands back to the body
+            S* chk = nullptr;
+            TR_HIP(t, hipMalloc(&chk, ((uint64_t)Zs + 64) * sizeof(S)));
+            uint64_t tot = 0;
+            rc = lx_expand<S>(t, chk, &tot);
+            std::vector<S> a(Zs), b(Zs);
+            TR_HIP(t, hipStreamSynchronize(s));
+            TR_HIP(t, hipMemcpy(a.data(), chk, (uint64_t)Zs * sizeof(S), hipMemcpyDeviceToHost));
+            TR_HIP(t, hipMemcpy(b.data(), cur, (uint64_t)Zs * sizeof(S), hipMemcpyDeviceToHost));
+            hipFree(chk);
+            uint64_t bad = Zs;
+            for (uint64_t i = 0; i < Zs; ++i)
+                if (a[i] != b[i]) {
+                    bad = i;
+                    break;
+                }
+            std::vector<uint32_t> mm(lp.T);
+            std::vector<S> ss(lp.T);
+            TR_HIP(t, hipMemcpy(mm.data(), t->lx_mul, (uint64_t)lp.T * 4, hipMemcpyDeviceToHost));
+            TR_HIP(t, hipMemcpy(ss.data(), t->lx_store, (uint64_t)lp.T * sizeof(S), hipMemcpyDeviceToHost));
+            uint64_t wsum = 0, nz = 0, badm = 0;
+            for (uint32_t i = 0; i < lp.T; ++i) {
+                wsum += mm[i];
+                if ((ss[i] == 0) != (mm[i] == 0)) ++badm;
+            }
+            for (uint32_t i = 0; i < Zs; ++i) nz += (b[i] & Sym<S>::TM) ? 1 : 0;
+            fprintf(stderr, "[lex-check] Zs=%u words=%u distinct=%u+%u store=%u expanded=%llu first_diff=%llu "
+                    "mult_sum=%llu nonzero_body=%llu sep_mismatch=%llu\n", Zs, lp.nw,
+                    lp.nshort, lp.nlong, lp.T, (unsigned long long)tot, (unsigned long long)bad,
+                    (unsigned long long)wsum, (unsigned long long)nz, (unsigned long long)badm);
+        }
+    } else {
+        rc = sp_add_sectors<S>(t, 0u, Zs);
+    }
     if (rc != GBPE_OK) return rc;
     t->sp_age = 0;
     t->sp_bits_age = 0;
@@ -2503,11 +2837,19 @@ int sp_shrink(gbpe_trainer* t) {
     TR_HIP(t, hipMemcpyAsync(&L, t->d_u32, 4, hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipStreamSynchronize(s));
     if (L < 4096) return GBPE_OK;
-    if ((uint64_t)t->bend + L > t->cap_syms) return GBPE_OK;
-    S* body = (S*)t->buf[t->bcur];
-    TR_HIP(t, hipMemcpyAsync(body + t->bend, zc, (uint64_t)L * t->bps, hipMemcpyDeviceToDevice, s));
-    int rc = sp_add_sectors<S>(t, t->bend, L);
-    if (rc != GBPE_OK) return rc;
+    if (t->lex) {   // the front's words join the lexicon (deduplicated among themselves)
+        LxPlan lp;
+        int rc = lx_analyze<S>(t, (const S*)zc, L, false, lp);
+        if (rc == GBPE_OK && lp.ok) rc = lx_commit<S>(t, lp, (const S*)zc, false);
+        if (rc != GBPE_OK) return rc;
+        if (!lp.ok) return GBPE_OK;   // (a collision or no room): the zone keeps its front this time
+    } else {
+        if ((uint64_t)t->bend + L > t->cap_syms) return GBPE_OK;
+        S* body = (S*)t->buf[t->bcur];
+        TR_HIP(t, hipMemcpyAsync(body + t->bend, zc, (uint64_t)L * t->bps, hipMemcpyDeviceToDevice, s));
+        int rc = sp_add_sectors<S>(t, t->bend, L);
+        if (rc != GBPE_OK) return rc;
+    }
     const uint64_t rest = t->zcap - L;
     TR_HIP(t, hipMemcpyAsync(t->wtmp, zc + L, rest * t->bps, hipMemcpyDeviceToDevice, s));
     TR_HIP(t, hipMemcpyAsync(zc, t->wtmp, rest * t->bps, hipMemcpyDeviceToDevice, s));
@@ -2540,17 +2882,22 @@ int sp_exit(gbpe_trainer* t) {
     S* body = (S*)t->buf[t->bcur];
     S* dst = (S*)t->buf[t->bcur ^ 1];
     const uint32_t nsec = t->nsec;
-    hipLaunchKernelGGL(k_sp_counts, dim3((uint32_t)gbpe_div_up(nsec, 256)), dim3(256), 0, s, (const uint2*)t->sec, nsec,
-                       t->sp_loc);
-    const uint64_t nblk = gbpe_div_up(nsec, SCAN_BLK);
-    hipLaunchKernelGGL(k_chunk_scan1, dim3((uint32_t)nblk), dim3(SCAN_TPB), 0, s, (const uint32_t*)t->sp_loc,
-                       (uint64_t)nsec, t->sp_loc, t->sp_blk);
-    hipLaunchKernelGGL(k_chunk_scan2, dim3(1), dim3(SCAN_TPB), 0, s, t->sp_blk, nblk, t->sp_blk + nblk);
-    hipLaunchKernelGGL(k_sp_gather<S>, dim3((uint32_t)gbpe_div_up(nsec, TPB / 64)), dim3(TPB), 0, s, (const S*)body,
-                       (const uint2*)t->sec, nsec, (const uint32_t*)t->sp_loc, (const uint64_t*)t->sp_blk, dst);
-    GBPE_LAUNCH_CHECK(t->ctx);
     uint64_t btot = 0;
-    TR_HIP(t, hipMemcpyAsync(&btot, t->sp_blk + nblk, 8, hipMemcpyDeviceToHost, s));
+    if (t->lex) {
+        int rc = lx_expand<S>(t, dst, &btot);
+        if (rc != GBPE_OK) return rc;
+    } else {
+        hipLaunchKernelGGL(k_sp_counts, dim3((uint32_t)gbpe_div_up(nsec, 256)), dim3(256), 0, s, (const uint2*)t->sec, nsec,
+                           t->sp_loc);
+        const uint64_t nblk = gbpe_div_up(nsec, SCAN_BLK);
+        hipLaunchKernelGGL(k_chunk_scan1, dim3((uint32_t)nblk), dim3(SCAN_TPB), 0, s, (const uint32_t*)t->sp_loc,
+                           (uint64_t)nsec, t->sp_loc, t->sp_blk);
+        hipLaunchKernelGGL(k_chunk_scan2, dim3(1), dim3(SCAN_TPB), 0, s, t->sp_blk, nblk, t->sp_blk + nblk);
+        hipLaunchKernelGGL(k_sp_gather<S>, dim3((uint32_t)gbpe_div_up(nsec, TPB / 64)), dim3(TPB), 0, s, (const S*)body,
+                           (const uint2*)t->sec, nsec, (const uint32_t*)t->sp_loc, (const uint64_t*)t->sp_blk, dst);
+        GBPE_LAUNCH_CHECK(t->ctx);
+        TR_HIP(t, hipMemcpyAsync(&btot, t->sp_blk + nblk, 8, hipMemcpyDeviceToHost, s));
+    }
     TR_HIP(t, hipMemcpyAsync(dst + B, t->zbuf[t->zcur], (uint64_t)z * t->bps, hipMemcpyDeviceToDevice, s));
     // zero the rest of the dense buffer's padding the kernels may read (halo / look-ahead)
     TR_HIP(t, hipMemsetAsync(dst + n, 0, (t->cap_syms - n) * t->bps, s));
@@ -2564,6 +2911,7 @@ int sp_exit(gbpe_trainer* t) {
                                          (unsigned long long)btot, B);
     t->cur = t->bcur ^ 1;
     t->sp = false;
+    t->lex = false;
     ++t->sp_exits;
     return GBPE_OK;
 }
@@ -2599,6 +2947,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     t->body_cap = (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
     if (const char* e = getenv("GBPE_BODY_WG")) t->body_cap = std::max<uint32_t>(1, (uint32_t)atoi(e));
     if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_LEXICON")) t->lex_on = atoi(e) != 0;
     if (const char* e = getenv("GBPE_DELTA_MT")) t->delta_mt = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_DELTA_TPW")) {
         const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
@@ -2982,6 +3331,11 @@ extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
     o->ms_sparse = t->ms_sparse;
     o->ms_body = t->ms_body;
     o->zone_bytes = t->h_st->sp_bytes;
+    o->lexicon_builds = (uint32_t)t->lx_builds;
+    o->lexicon_fallbacks = (uint32_t)t->lx_fallbacks;
+    o->lexicon_words = t->lx_words;
+    o->lexicon_entries = t->lx_nuid;
+    o->lexicon_symbols = t->lx_len;
     if (t->wg_bytes && t->wg_cap) {   // the per-workgroup counters of k_body (and its zone workgroup)
         std::vector<uint64_t> h(t->wg_cap);
         if (hipMemcpy(h.data(), t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess)
@@ -3085,6 +3439,11 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->d_u32);
     hipFree(t->part);
     hipFree(t->wg_bytes);
+    hipFree(t->lx_store);
+    hipFree(t->lx_mul);
+    hipFree(t->lx_occ);
+    hipFree(t->lx_w0);
+    hipFree(t->lx_tmp);
     if (t->h_zst) hipHostFree(t->h_zst);
     if (t->graph_exec) hipGraphExecDestroy(t->graph_exec);
     hipFree(t->d_clog);
@@ -3888,13 +4247,13 @@ int shard_phase1_sp(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl)
     sh.rec = rec;
     const uint32_t gb = nbody + (zone ? 1u : 0u);
     if (exact)
-        launch_body<S, true>(bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, wpg, t->sig, t->tb, nbody,
+        launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, wpg, t->sig, t->tb, nbody,
                              (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc, zone ? 1u : 0u, (const uint64_t*)t->part,
-                             t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh);
+                             t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh, sp_mul(t));
     else
-        launch_body<S, false>(bt, gb, s, t->st, round, (S*)t->buf[t->bcur], t->sec, t->bits, t->W, wpg, t->sig, t->tb, nbody,
+        launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, wpg, t->sig, t->tb, nbody,
                               (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc, zone ? 1u : 0u, (const uint64_t*)t->part,
-                              t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh);
+                              t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh, sp_mul(t));
     const uint32_t nlb = grid_persistent(t->ctx, dt.nblk, 2);
     hipLaunchKernelGGL(k_shard_send_sp, dim3(nlb + 1), dim3(TPB), 0, s, t->st, t->zst, round, dt, rec, cl, nlb);
     GBPE_LAUNCH_CHECK(t->ctx);

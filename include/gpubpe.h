@@ -170,6 +170,11 @@ typedef struct gbpe_trainer_stats {
     double   ms_dense;            /* GBPE_TRAIN_TIMING: merge-pass device ms of the dense merges (k_delta + k_compact) */
     double   ms_sparse;           /* GBPE_TRAIN_TIMING: merge-pass device ms of the sparse merges (k_body + zone passes) */
     double   ms_body;             /* GBPE_TRAIN_TIMING: k_body alone */
+    uint32_t lexicon_builds;      /* sparse entries whose body became a word lexicon */
+    uint32_t lexicon_fallbacks;   /* ... that kept the in-place sectors (store not much smaller, collision) */
+    uint64_t lexicon_words;       /* body word occurrences the lexicon represents (all builds and shrinks) */
+    uint64_t lexicon_entries;     /* distinct-word entries of the current lexicon */
+    uint64_t lexicon_symbols;     /* symbols of the current lexicon store (separators included) */
 } gbpe_trainer_stats;
 int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* out);
 /* Current symbol stream in the reference u32 layout (bit16 = word start). */
