@@ -678,6 +678,26 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, 
     select_merge(st, tb, log, grpsum, nlog, rec, zst, exact);
 }
 
+// the next merge's count (the table maximum): the sparse entry decision before any merge ran
+__global__ __launch_bounds__(1024) void k_topcount(Table tb, uint32_t* __restrict__ out) {
+    __shared__ uint64_t red[16];
+    uint64_t best = 0;
+    for (uint32_t i = threadIdx.x; i < tb.nblk; i += 1024) {
+        const uint64_t v = tb.bmax[i];
+        best = v > best ? v : best;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) best = red[w] > best ? red[w] : best;
+        *out = (uint32_t)(best >> 32);
+    }
+}
+
 // A merge is "active" for the stream kernels iff k_select logged it this round.
 __device__ __forceinline__ bool merge_active(const DevState* st, uint32_t round) {
     return !st->stop && st->merges_done == round + 1u;
@@ -2134,6 +2154,9 @@ struct gbpe_trainer {
     uint32_t sp_enters = 0, sp_exits = 0;
     uint32_t sp_div = 64;        // enter when last_mc * sp_div <= n
     uint32_t sp_cooldown = 0;    // steps to stay dense after an abort
+    uint32_t lx_div = 16;        // with the lexicon: enter once next_mc * lx_div <= n, from the first step on (GBPE_LEXICON_DIV)
+    uint32_t sub_zone = 1u << 20;   // sparse steps run in sub-steps of sub_k merges while the zone exceeds this
+    uint32_t sub_k = 16;            // (the zone shrinks between them; GBPE_SUBSTEP_ZONE, GBPE_SUBSTEP)
     uint32_t sp_zt = 7;          // zone target = sp_zt * last_mc + 64 (>= 5: see sp_enter; 7 measured best, GBPE_SPARSE_ZT)
     bool fuse_sel = false;       // GBPE_FUSE_SELECT=1: select in k_refresh's last workgroup (measured slower: DESIGN §2b)
     uint32_t refresh_blocks = 0; // GBPE_REFRESH_BLOCKS: k_refresh grid (0 = 2 per CU)
@@ -2317,7 +2340,17 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
                              sp_mul(t));
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
     if (!g.zone1) {
-        if (exact)
+        // a zone of many tiles (the lexicon loop's first merges): TPW tiles per
+        // workgroup and one flush of their hot pairs, as in the dense loop
+        const bool mt = t->delta_mt && g.zdelta >= t->delta_mt;
+        const uint32_t g_mt = (uint32_t)gbpe_div_up(g.zdelta, 8);
+        if (exact && mt)
+            hipLaunchKernelGGL((k_delta_mt<S, true, 8>), dim3(g_mt), dim3(TPB), 0, s, t->zst, round, (const S*)zc, t->tb,
+                               t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt);
+        else if (mt)
+            hipLaunchKernelGGL((k_delta_mt<S, false, 8>), dim3(g_mt + g.ztail), dim3(TPB), 0, s, t->zst, round,
+                               (const S*)zc, t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt);
+        else if (exact)
             hipLaunchKernelGGL((k_delta<S, true, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc,
                                t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, 0xFFFFFFFFu);
         else   // + stale-tail slice blocks: the zone's tail (<= mc <= zone/5) in ~2K-symbol slices
@@ -2948,6 +2981,9 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     if (const char* e = getenv("GBPE_BODY_WG")) t->body_cap = std::max<uint32_t>(1, (uint32_t)atoi(e));
     if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_LEXICON")) t->lex_on = atoi(e) != 0;
+    if (const char* e = getenv("GBPE_LEXICON_DIV")) t->lx_div = std::max<uint32_t>(8, (uint32_t)strtoul(e, nullptr, 10));
+    if (const char* e = getenv("GBPE_SUBSTEP_ZONE")) t->sub_zone = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_SUBSTEP")) t->sub_k = std::max<uint32_t>(2, (uint32_t)strtoul(e, nullptr, 10)) & ~1u;
     if (const char* e = getenv("GBPE_DELTA_MT")) t->delta_mt = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_DELTA_TPW")) {
         const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
@@ -3079,9 +3115,8 @@ extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t
     return trainer_create_impl(ctx, bytes, n, word_starts, input_on_device, opts, 0, out);
 }
 
-extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out, uint32_t* n_done,
-                                 uint32_t* early_stop) {
-    if (!t) return GBPE_E_INVALID;
+namespace {
+int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out, uint32_t* n_done, uint32_t* early_stop) {
     if (n_done) *n_done = 0;
     if (early_stop) *early_stop = t->stop ? 1u : 0u;
     uint32_t k = max_merges ? max_merges : t->batch;
@@ -3099,10 +3134,27 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     // sector-sparse loop once merges touch a small fraction of the stream
     if (t->sp_cooldown) {
         --t->sp_cooldown;
-    } else if (!t->sp && !t->sharded && !(t->flags & GBPE_TRAIN_DENSE_ONLY) && t->last_mc &&
-        ((t->flags & GBPE_TRAIN_SPARSE_EARLY) || (uint64_t)t->last_mc * t->sp_div <= t->n)) {
-        int rc = t->u16 ? sp_enter<uint16_t>(t) : sp_enter<uint32_t>(t);
-        if (rc != GBPE_OK) return rc;
+    } else if (!t->sp && !t->sharded && !(t->flags & GBPE_TRAIN_DENSE_ONLY)) {
+        // with the word lexicon the body costs what its distinct words cost, so the
+        // loop can enter as soon as the zone (~7 x the next count) is a small part of
+        // the stream — before the first merge; without it, once counts
+        // are a 1/sp_div fraction
+        uint32_t mc = t->last_mc;
+        if (!mc && t->lex_on) {
+            if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
+            hipLaunchKernelGGL(k_topcount, dim3(1), dim3(1024), 0, s, t->tb, t->d_u32);
+            GBPE_LAUNCH_CHECK(t->ctx);
+            TR_HIP(t, hipMemcpyAsync(&mc, t->d_u32, 4, hipMemcpyDeviceToHost, s));
+            TR_HIP(t, hipStreamSynchronize(s));
+        }
+        const uint64_t div = t->lex_on ? t->lx_div : t->sp_div;
+        if (mc && ((t->flags & GBPE_TRAIN_SPARSE_EARLY) || (uint64_t)mc * div <= t->n)) {
+            const uint32_t keep = t->last_mc;
+            t->last_mc = mc;
+            int rc = t->u16 ? sp_enter<uint16_t>(t) : sp_enter<uint32_t>(t);
+            if (!t->sp) t->last_mc = keep;
+            if (rc != GBPE_OK) return rc;
+        }
     }
     // keep the zone near its minimum, then rebuild stale filters now and then
     if (t->sp) {
@@ -3114,6 +3166,8 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
         int rc = t->u16 ? sp_filters<uint16_t>(t, wb) : sp_filters<uint32_t>(t, wb);
         if (rc != GBPE_OK) return rc;
     }
+    // a large zone shrinks every sub_k merges instead of every step (early counts fall fast)
+    if (t->sp && t->n - t->h_st->B > t->sub_zone && k > t->sub_k) k = t->sub_k;
     // reset the per-step counter + budget (trainer.js:239)
     DevState* hs = t->h_st;
     hs->merges_done = 0;
@@ -3290,7 +3344,7 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
             int rc = sp_exit_any(t);
             if (rc != GBPE_OK) return rc;
             t->sp_cooldown = 1;
-            if (done == 0 && !hs->stop) return gbpe_trainer_step(t, max_merges, merges_out, n_done, early_stop);
+            if (done == 0 && !hs->stop) return trainer_step_once(t, max_merges, merges_out, n_done, early_stop);
         }
     } else {
         t->cur ^= (done & 1u);
@@ -3300,6 +3354,29 @@ extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t*
     if (n_done) *n_done = done;
     if (early_stop) *early_stop = t->stop ? 1u : 0u;
     return GBPE_OK;
+}
+}  // namespace
+
+// One host step of up to max_merges merges (trainer.js:225-335's 128-merge batch).
+// Internally a sparse step whose zone is still large runs as several sub-steps
+// (trainer_step_once), so the zone can shrink between them.
+extern "C" int gbpe_trainer_step(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out, uint32_t* n_done,
+                                 uint32_t* early_stop) {
+    if (!t) return GBPE_E_INVALID;
+    uint32_t want = max_merges ? max_merges : t->batch;
+    if (want > t->batch) want = t->batch;
+    uint32_t got = 0, es = 0;
+    int rc = GBPE_OK;
+    while (got < want) {
+        uint32_t nd = 0;
+        rc = trainer_step_once(t, want - got, merges_out ? merges_out + 4 * got : nullptr, &nd, &es);
+        if (rc != GBPE_OK) break;
+        got += nd;
+        if (nd == 0 || es) break;
+    }
+    if (n_done) *n_done = got;
+    if (early_stop) *early_stop = t->stop ? 1u : 0u;
+    return rc;
 }
 
 extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
