@@ -68,14 +68,12 @@ struct DevState {
     uint32_t used;         // occupied table slots
     uint32_t ndirty;       // dirty-block list length
     uint32_t err;          // error bits
-    uint32_t valid_total;  // (unused)
+    uint32_t valid_total;  // zone: survivors + 1 (zone_one → k_refresh's layout check)
     uint32_t budget;       // merges allowed in this step
     uint32_t live;         // distinct pairs with count > 0 at the last select
     uint64_t tail_total;   // sum of m
     uint32_t max_live;     // max of `live` over all selects
-    uint32_t ticket;       // (unused)
     uint32_t epoch;        // merge sequence number
-    uint32_t rw_count;     // (unused)
     // ── sharded training (gbpe_shard_*); n / new_n above are then LOCAL: the
     //    local stream length and the local keep limit ──
     uint32_t sharded, rank, world, stall;
@@ -98,7 +96,6 @@ struct DevState {
     uint32_t Bp;           // body length during the previous merge (stale-window source offset)
     uint32_t body_rm;      // B-sides removed from the body by this merge
     uint32_t sp_abort;     // a selected merge does not fit the zone: not run, host goes dense
-    uint32_t rticket;      // k_refresh workgroups done (fused selection)
     uint32_t sel_round;    // sector-sparse: round + 1 of the merge k_body selected
     uint64_t sp_bytes;     // sector-sparse: bytes moved by the multi-tile zone passes (k_refresh adds them)
     uint32_t zlast;        // sector-sparse: zone length of the rank that holds the zone (global knowledge)
@@ -129,7 +126,11 @@ __device__ __forceinline__ void kt_put(uint32_t round, uint32_t wg, int i, unsig
 #define KT(i) kt_put(round, blockIdx.x, (i), wall_clock64())
 #define KTV(i, v) kt_put(round, blockIdx.x, (i), (v))
 #define KTR(i) kt_put(round, KT_WG + blockIdx.x, (i), wall_clock64())
+#define TKT(i) kt_put(r, 1u, (i), wall_clock64())   // k_tail's own phases (workgroup slot 1)
+#define TKTV(i, v) kt_put(r, 1u, (i), (v))
 #else
+#define TKT(i) ((void)0)
+#define TKTV(i, v) ((void)0)
 #define KT(i) ((void)0)
 #define KTV(i, v) ((void)0)
 #define KTR(i) ((void)0)
@@ -207,11 +208,13 @@ template <int N>
 struct LdsTab {
     uint32_t key[N];
     uint32_t val[N];
+    uint32_t ovf;   // an add went straight to the global table (k_tail re-maxes every dirty block then)
 };
 
 template <int N>
 __device__ __forceinline__ void lds_clear(LdsTab<N>& t) {
     for (int i = threadIdx.x; i < N; i += blockDim.x) { t.key[i] = 0u; t.val[i] = 0u; }
+    if (threadIdx.x == 0) t.ovf = 0u;
 }
 
 template <int N>
@@ -226,6 +229,7 @@ __device__ __forceinline__ void lds_add(LdsTab<N>& t, const Table& tb, DevState*
             return;
         }
     }
+    t.ovf = 1u;
     table_add(tb, st, pid, d);   // LDS table crowded: go straight to the global table
 }
 
@@ -379,8 +383,7 @@ __global__ __launch_bounds__(TPB) void k_count_full(DevState* st, const S* __res
 __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log, uint32_t* __restrict__ grpsum,
                              uint32_t* __restrict__ nlog, uint32_t* __restrict__ rec, DevState* zst, uint32_t exact);
 
-// Selection fused into k_refresh (FusedSel::log != nullptr): the last workgroup
-// to finish re-maxing selects the NEXT merge, saving a launch per merge.
+// (unused launch argument: the selection fused into k_refresh was measured slower)
 struct FusedSel {
     uint32_t* log = nullptr;
     uint32_t* grpsum = nullptr;
@@ -539,19 +542,6 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             if (finish == 2) KTR(5);
         }
     }
-    if (fs.log) {   // last workgroup out selects the next merge
-        __shared__ uint32_t s_last;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();   // this block's maxima (and block 0's finish) before the ticket
-            s_last = atomicAdd(&st->rticket, 1u) == gridDim.x - 1 ? 1u : 0u;
-        }
-        __syncthreads();
-        if (!s_last) return;
-        __threadfence();       // acquire: every block's writes, L1 invalidated
-        if (threadIdx.x == 0) st->rticket = 0u;
-        select_merge(st, tb, fs.log, fs.grpsum, nullptr, nullptr, zst, fs.exact);
-    }
 }
 
 constexpr uint32_t GRP = 64;    // tiles per group sum (two-level tile prefix)
@@ -600,8 +590,6 @@ __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log,
     st->dused = 0u;
     st->dfull = 0u;
     st->valid_total = 0u;
-    st->ticket = 0u;
-    st->rw_count = 0u;
     const uint32_t mc = (uint32_t)(best >> 32);
     const uint32_t pid = ~(uint32_t)best;
     if (st->merges_done >= st->budget) {   // host asked for fewer merges this step
@@ -1314,9 +1302,9 @@ __device__ __forceinline__ void sector_first(const S* __restrict__ p, const uint
 // survivors compacted to the sector's front).  In the lexicon body (mp != null)
 // every symbol carries its word's multiplicity, which weights its count deltas
 // and moves with it.  Returns the B-sides removed (weighted: stream symbols).
-template <typename S>
+template <typename S, int NT = LTAB_T>
 __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, uint32_t cnt, uint32_t a, uint32_t b,
-                                uint32_t nw, LdsTab<LTAB_T>& lt, const Table& tb, DevState* st, uint32_t* __restrict__ sig,
+                                uint32_t nw, LdsTab<NT>& lt, const Table& tb, DevState* st, uint32_t* __restrict__ sig,
                                 uint32_t& out_cnt, const uint32_t (&first)[5], const uint32_t (&firstm)[4]) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     const int lane = threadIdx.x & 63;
@@ -1441,14 +1429,17 @@ __device__ __forceinline__ uint32_t lane_mask_n(uint64_t i0, uint64_t lim, int n
     return i0 >= lim ? 0u : (i0 + n <= lim ? full : ((1u << (uint32_t)(lim - i0)) - 1u));
 }
 
-template <typename S, bool EXACT, int BT>
+// zout (the persistent tail loop, k_tail): the delta table is shared with the body
+// pass (neither cleared nor flushed here) and m, the new zone length go to zout[0..1]
+template <typename S, bool EXACT, int BT, int NT = LTAB_T, int ZPT_ = ZoneDim<S, BT>::ZPT>
 __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
                          S* __restrict__ zo, ZoneLds<S, BT>& L,
-                         LdsTab<LTAB_T>& lt, const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
-                         uint64_t* __restrict__ bytes, uint32_t round) {
+                         LdsTab<NT>& lt, const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
+                         uint64_t* __restrict__ bytes, uint32_t round, uint32_t* zout = nullptr) {
     (void)round;   // phase stamps only (-DGBPE_KTRACE)
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
-    constexpr int ZPT = ZoneDim<S, BT>::ZPT;
+    constexpr int ZPT = ZPT_;                // zone positions per thread (<= ZoneDim's: the LDS is sized for that)
+    static_assert(ZPT <= ZoneDim<S, BT>::ZPT && ZPT * sizeof(S) % 16 == 0, "zone positions per thread");
     constexpr int V = ZPT * sizeof(S) / 16;  // 16-byte vectors per thread
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t z = zs.n;   // launch snapshots (LDS): no state round trip before the zone loads
@@ -1472,7 +1463,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
         const uint64_t src0 = (uint64_t)gs.n + gs.off - gs.poff - 2ull * mc - gs.Bp;
         for (uint32_t u = t; u < mc; u += BT) L.wb[u] = zo[src0 + u];
     }
-    lds_clear(lt);
+    if (!zout) lds_clear(lt);
     __syncthreads();
     if (t == 0) KT(2);
     const uint32_t xm2 = i0 >= 2 ? (uint32_t)xs[i0 - 2] : 0u, xm1 = i0 >= 1 ? (uint32_t)xs[i0 - 1] : 0u;
@@ -1587,10 +1578,15 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
         for (uint32_t j = nfull * PV + t; j < tot; j += BT) zo[j] = xs[swz(j)];
     }
     if (t == 0) KT(4);
-    lds_flush(lt, tb, st);
+    if (!zout) lds_flush(lt, tb, st);
     if (t == 0) {
-        zst->m = m;
-        zst->valid_total = Kz + m + 1u;   // survivors + 1 (k_refresh checks it against the new layout)
+        if (zout) {
+            zout[0] = m;
+            zout[1] = Kz + m;
+        } else {
+            zst->m = m;
+            zst->valid_total = Kz + m + 1u;   // survivors + 1 (k_refresh checks it against the new layout)
+        }
         // zone read, window source read, kept survivors + window written
         atomicAdd(bytes, (uint64_t)sizeof(S) * ((uint64_t)z + (EXACT ? 0u : mc) + Kz + m));
     }
@@ -1908,6 +1904,425 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     }
 }
 
+// ── persistent tail loop ──
+// Late merges (a few hundred sites in a handful of distinct words, a zone of a
+// few K symbols) cost launches and dependent round trips, not bytes: k_body +
+// k_refresh spend ~20 us per merge at 1 GiB on ~10 candidate sectors.  k_tail is
+// ONE 1024-thread workgroup that runs a whole step's merges back to back.  It is
+// the only writer of the pair table while it runs, so
+//   * selection reduces group maxima kept in LDS (64 argmax blocks per group)
+//     instead of a k_refresh pass and its partial maxima;
+//   * count deltas reach the table as plain read-modify-writes; each raises its
+//     block maximum (atomicMax) or, when it lowers the block's holder, has the
+//     block re-maxed from its 2048 slots by one wave;
+//   * the body pass (every bitmap word of rows a and b in one load, signatures,
+//     one wave per candidate sector) and the zone pass (zone_one) share one LDS
+//     delta table and one flush.
+// It leaves the step early — the host finishes it with k_body — when a merge's
+// candidate sectors or re-maxed blocks outgrow its LDS lists.
+#ifdef GBPE_TAIL_LOOP
+constexpr int TL_BT = 1024;
+constexpr int TL_LT = 4096;               // LDS delta table (body + zone deltas of one merge)
+constexpr uint32_t TL_GRP = 6;            // log2 argmax blocks per group
+constexpr uint32_t TL_MAXG = 256;         // groups: tables of up to 2^25 slots
+constexpr uint32_t TL_RS = 1024;          // re-maxed blocks per merge
+constexpr uint32_t TL_CAND = 8192;        // candidate sectors per merge (token bitmap)
+constexpr uint32_t TL_FILT = 3072;        // ... passing the signature filter
+enum : uint32_t { TL_EXIT_NONE = 0, TL_EXIT_CAND = 1, TL_EXIT_REMAX = 2, TL_EXIT_LDS = 3 };
+
+struct TailBody {   // the body pass's lists (the zone pass reuses this LDS)
+    uint32_t cand[TL_CAND];
+    uint32_t fsec[TL_FILT];
+    uint2 fext[TL_FILT];
+};
+template <typename S>
+union TailU {
+    ZoneLds<S, TL_BT> z;
+    TailBody c;
+};
+static_assert(sizeof(TailBody) <= sizeof(ZoneLds<uint32_t, TL_BT>), "the body lists share the zone's LDS");
+
+__device__ __forceinline__ uint64_t tl_key(uint32_t cnt, uint32_t pid) {
+    return (int32_t)cnt > 0 ? (((uint64_t)cnt << 32) | (uint32_t)~pid) : 0ull;
+}
+
+template <typename S, bool EXACT, int ZPT>
+__global__ __launch_bounds__(TL_BT) void k_tail(DevState* st, DevState* zst, S* __restrict__ body, uint32_t* __restrict__ lmul,
+                                                uint2* __restrict__ sec, uint32_t* __restrict__ bits, uint32_t W,
+                                                uint32_t wused, uint32_t* __restrict__ sig, Table tb, S* __restrict__ zb0,
+                                                S* __restrict__ zb1, uint32_t* __restrict__ log,
+                                                uint64_t* __restrict__ bytes, uint32_t* __restrict__ tstat) {
+    __shared__ TailU<S> u;
+    __shared__ LdsTab<TL_LT> lt;
+    __shared__ uint64_t gmax[TL_MAXG];
+    __shared__ uint32_t rs[TL_RS], rsmark[(TL_MAXG << TL_GRP) / 32], gmark[TL_MAXG / 32];
+    __shared__ uint32_t s_nrs, s_ntok, s_nf, s_rm, s_exit, s_used, s_idx, zout[2];
+    __shared__ uint64_t s_red[TL_BT / 64];
+    constexpr int NW = sizeof(DevState) / 4;
+    constexpr uint32_t NWAVE = TL_BT / 64;
+    __shared__ union {
+        DevState d;
+        uint32_t w[NW];
+    } s_g, s_z;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t ngrp = (tb.nblk + (1u << TL_GRP) - 1) >> TL_GRP;
+    if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
+    else if (t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
+    for (uint32_t g = wid; g < ngrp; g += NWAVE) {   // group maxima from the (exact) block maxima
+        const uint32_t blk = (g << TL_GRP) + (uint32_t)lane;
+        uint64_t v = blk < tb.nblk ? tb.bmax[blk] : 0ull;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(v, off);
+            v = o > v ? o : v;
+        }
+        if (lane == 0) gmax[g] = v;
+    }
+    for (uint32_t i = t; i < (TL_MAXG << TL_GRP) / 32; i += TL_BT) rsmark[i] = 0u;
+    if (t < (int)(TL_MAXG / 32)) gmark[t] = 0u;
+    if (t == 0) {
+        s_exit = TL_EXIT_NONE;
+        s_used = 0u;
+    }
+    __syncthreads();
+    DevState& g = s_g.d;
+    DevState& z = s_z.d;
+    const uint32_t K = g.budget;
+    uint64_t mybytes = 0;
+    auto remax_mark = [&](uint32_t blk) {   // queue a block for re-maxing (once per merge)
+        const uint32_t bit = 1u << (blk & 31u);
+        if (!(atomicOr(&rsmark[blk >> 5], bit) & bit)) {
+            const uint32_t q = atomicAdd(&s_nrs, 1u);
+            if (q < TL_RS) rs[q] = blk;
+            else tb.dirty[blk] = 1u;   // k_refresh after the kernel re-maxes it; the loop stops after this merge
+        }
+    };
+    uint32_t r = g.merges_done;
+    for (; r < K; ++r) {
+        if (g.stop || g.sp_abort || g.err) break;   // (uniform: LDS state, read after a barrier)
+        if (t == 0) TKT(0);
+        // ── selection: group maxima (LDS) ──
+        uint64_t best = 0;
+        for (uint32_t i = t; i < ngrp; i += TL_BT) best = gmax[i] > best ? gmax[i] : best;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(best, off);
+            best = o > best ? o : best;
+        }
+        if (lane == 0) s_red[wid] = best;
+        if (t == 0) {
+            s_ntok = 0u;
+            s_nf = 0u;
+            s_rm = 0u;
+            s_nrs = 0u;
+        }
+        lds_clear(lt);
+        __syncthreads();
+        best = s_red[0];
+#pragma unroll
+        for (uint32_t w2 = 1; w2 < NWAVE; ++w2) best = s_red[w2] > best ? s_red[w2] : best;
+        const uint32_t mc = (uint32_t)(best >> 32), pid = ~(uint32_t)best, a = pid >> 16, b = pid & 0xFFFFu;
+        const uint32_t nw = g.next_id;
+        if (mc < 2u || nw > 0xFFFFu) {   // train.wgsl:345-348
+            if (t == 0) g.stop = 1u;
+            break;
+        }
+        if (t == 0) TKT(1);
+        if (!EXACT) {
+            if ((uint64_t)g.n < 2ull * mc + g.Bp) {   // cannot happen (k_body's invariant)
+                if (t == 0) {
+                    g.err |= ERR_SPARSE_WINDOW;
+                    g.stop = 1u;
+                }
+                break;
+            }
+            if ((uint64_t)z.n < 5ull * mc + 2u) {   // zone misfit: the host goes dense
+                if (t == 0) g.sp_abort = 1u;
+                break;
+            }
+        }
+        // ── body candidates: every bitmap word of rows a and b at once (thread 0 finds (a,b)'s slot first) ──
+        if (t == 0) s_idx = table_find(tb, pid);
+        for (uint32_t w = t; w < wused; w += TL_BT) {
+            uint32_t c = bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w];
+            if (c) {
+                uint32_t pos = atomicAdd(&s_ntok, (uint32_t)__popc(c));
+                for (; c; c &= c - 1, ++pos)
+                    if (pos < TL_CAND) u.c.cand[pos] = w * 32u + (uint32_t)(__ffs(c) - 1);
+            }
+        }
+        __syncthreads();
+        const uint32_t ntok = s_ntok;
+        if (t == 0) {
+            TKT(2);
+            TKTV(10, ntok);
+        }
+        if (ntok > TL_CAND) {   // nothing of merge r is committed yet
+            if (t == 0) s_exit = TL_EXIT_CAND;
+            break;
+        }
+        for (uint32_t j = t; j < ntok; j += TL_BT) {   // signature filter (+ extents)
+            const uint32_t k = u.c.cand[j];
+            const uint2 e = sec[k];
+            if (sig_has(sig + (uint64_t)k * SP_SIGW, pid)) {
+                const uint32_t q = atomicAdd(&s_nf, 1u);
+                if (q < TL_FILT) {
+                    u.c.fsec[q] = k;
+                    u.c.fext[q] = e;
+                }
+            }
+        }
+        if (t == 0) mybytes += 16ull * ntok;
+        __syncthreads();
+        const uint32_t nf = s_nf;
+        if (t == 0) {
+            TKT(3);
+            TKTV(11, nf);
+        }
+        if (nf > TL_FILT) {
+            if (t == 0) s_exit = TL_EXIT_CAND;
+            break;
+        }
+        // ── commit: the log (thread 0); count(a,b) -= mc and the re-max of its block and
+        //    group by the last wave, while the others merge sectors ──
+        const uint32_t idx = s_idx;
+        if (t == 0) {
+            if (idx == 0xFFFFFFFFu) g.err |= ERR_PAIR_MISSING;
+            log[r * 4 + 0] = a;
+            log[r * 4 + 1] = b;
+            log[r * 4 + 2] = nw;
+            log[r * 4 + 3] = mc;
+        }
+        if (wid == (int)NWAVE - 1 && idx != 0xFFFFFFFFu) {
+            constexpr int NV = (1 << BLK_LOG2) / 2 / 64;   // 16-byte loads per lane
+            const uint32_t blk = idx >> BLK_LOG2, gq = blk >> TL_GRP, gb = (gq << TL_GRP) + (uint32_t)lane;
+            const uint32_t cnt_new = tb.slots[idx].y - mc;
+            const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)blk << BLK_LOG2));
+            uint4 e[NV];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) e[k] = sl[lane + k * 64];
+            const uint64_t gbm = gb < tb.nblk && gb != blk ? tb.bmax[gb] : 0ull;
+            if (lane == 0) tb.slots[idx].y = cnt_new;
+            uint64_t bst = 0;
+            uint32_t live = 0;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {   // (a,b)'s slot with its new count
+                const uint32_t s0 = ((uint32_t)(lane + k * 64) << 1) + ((blk << BLK_LOG2));
+                const uint32_t c1 = s0 == idx ? cnt_new : e[k].y, c2 = s0 + 1 == idx ? cnt_new : e[k].w;
+                const uint64_t k1 = e[k].x ? tl_key(c1, e[k].x) : 0ull, k2 = e[k].z ? tl_key(c2, e[k].z) : 0ull;
+                bst = k1 > bst ? k1 : bst;
+                bst = k2 > bst ? k2 : bst;
+                live += (k1 ? 1u : 0u) + (k2 ? 1u : 0u);
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint64_t o = __shfl_xor(bst, off);
+                bst = o > bst ? o : bst;
+                live += __shfl_xor(live, off);
+            }
+            uint64_t gv = gbm > bst ? gbm : bst;
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint64_t o = __shfl_xor(gv, off);
+                gv = o > gv ? o : gv;
+            }
+            if (lane == 0) {
+                tb.bmax[blk] = bst;
+                tb.blive[blk] = live;
+                gmax[gq] = gv;
+            }
+        }
+        // ── body sectors: one wave each, the next one's loads in flight ──
+        {
+            uint32_t removed = 0;
+            uint64_t moved = 0;
+            uint32_t nf5[5], nfm[4];
+            if ((uint32_t)wid < nf)
+                sector_first<S>(body + u.c.fext[wid].x, lmul ? lmul + u.c.fext[wid].x : nullptr, u.c.fext[wid].y, nf5, nfm);
+            for (uint32_t j = wid; j < nf; j += NWAVE) {
+                const uint32_t sct = u.c.fsec[j];
+                const uint2 e = u.c.fext[j];
+                uint32_t cf[5], cfm[4];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) cf[k] = nf5[k];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cfm[k] = nfm[k];
+                if (j + NWAVE < nf) {
+                    const uint2 en = u.c.fext[j + NWAVE];
+                    sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf5, nfm);
+                }
+                uint32_t out = 0;
+                const uint32_t rr = body_sector<S, TL_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, tb, st,
+                                                         sig + (uint64_t)sct * SP_SIGW, out, cf, cfm);
+                moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (rr ? out : 0u));
+                if (rr) {
+                    removed += rr;
+                    if (lane == 0) {
+                        sec[sct].y = out;
+                        atomicOr(&bits[(uint64_t)nw * W + (sct >> 5)], 1u << (sct & 31u));
+                    }
+                }
+            }
+            if (lane == 0) {
+                if (removed) atomicAdd(&s_rm, removed);
+                mybytes += moved;
+            }
+        }
+        __syncthreads();
+        if (t == 0) TKT(4);
+        // ── zone (the same delta table) ──
+        S* zc = (r & 1u) ? zb1 : zb0;
+        S* zo = (r & 1u) ? zb0 : zb1;
+        zone_one<S, EXACT, TL_BT, TL_LT, ZPT>(st, zst, g, z, zc, zo, u.z, lt, tb, a, b, nw, mc, bytes, r, zout);
+        __syncthreads();
+        if (t == 0) TKT(5);
+        // ── flush: plain read-modify-writes (the only writer), block maxima kept exact ──
+        {
+            uint32_t kk[TL_LT / TL_BT], vv[TL_LT / TL_BT];
+#pragma unroll
+            for (int j = 0; j < TL_LT / TL_BT; ++j) {
+                kk[j] = lt.key[t + j * TL_BT];
+                vv[j] = lt.val[t + j * TL_BT];
+            }
+#pragma unroll
+            for (int j = 0; j < TL_LT / TL_BT; ++j) {
+                const uint32_t p = kk[j], d = vv[j];
+                if (!p || !d) continue;
+                const uint32_t h = gbpe_fmix32(p) & tb.mask;
+                uint32_t idx = 0xFFFFFFFFu, old = 0;
+                for (uint32_t q = 0; q <= tb.mask; ++q) {
+                    const uint32_t i2 = (h + ((q * (q + 1)) >> 1)) & tb.mask;
+                    uint32_t k2 = tb.slots[i2].x;
+                    if (k2 == 0u) {
+                        k2 = atomicCAS(&tb.slots[i2].x, 0u, p);   // another new pair may race for the slot
+                        if (k2 == 0u) {
+                            atomicAdd(&s_used, 1u);
+                            idx = i2;
+                            old = 0u;
+                            break;
+                        }
+                    }
+                    if (k2 == p) {
+                        idx = i2;
+                        old = tb.slots[i2].y;
+                        break;
+                    }
+                }
+                if (idx == 0xFFFFFFFFu) {
+                    atomicOr(&g.err, ERR_TABLE_FULL);
+                    continue;
+                }
+                const uint32_t nv = old + d;
+                tb.slots[idx].y = nv;
+                const uint32_t blk = idx >> BLK_LOG2;
+                const uint64_t bm = __hip_atomic_load(&tb.bmax[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t ok = tl_key(old, p), nk = tl_key(nv, p);
+                if (nk > bm) {
+                    atomicMax(&tb.bmax[blk], nk);
+                    atomicMax(&gmax[blk >> TL_GRP], nk);
+                } else if (nk < ok && ok == bm) {
+                    remax_mark(blk);
+                }
+            }
+        }
+        __syncthreads();
+        if (t == 0) {
+            TKT(6);
+            TKTV(9, s_nrs);
+        }
+        // ── re-max queued blocks (one wave each), then their groups ──
+        if (s_nrs) {
+            const uint32_t nrs = s_nrs < TL_RS ? s_nrs : TL_RS;
+            constexpr int NV = (1 << BLK_LOG2) / 2 / 64;   // 16-byte loads per lane
+            for (uint32_t q = wid; q < nrs; q += NWAVE) {
+                const uint32_t blk = rs[q];
+                const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)blk << BLK_LOG2));
+                uint4 e[NV];
+#pragma unroll
+                for (int k = 0; k < NV; ++k) e[k] = sl[lane + k * 64];
+                uint64_t bst = 0;
+                uint32_t live = 0;
+#pragma unroll
+                for (int k = 0; k < NV; ++k) {
+                    const uint64_t k1 = e[k].x ? tl_key(e[k].y, e[k].x) : 0ull, k2 = e[k].z ? tl_key(e[k].w, e[k].z) : 0ull;
+                    bst = k1 > bst ? k1 : bst;
+                    bst = k2 > bst ? k2 : bst;
+                    live += (k1 ? 1u : 0u) + (k2 ? 1u : 0u);
+                }
+                for (int off = 32; off > 0; off >>= 1) {
+                    const uint64_t o = __shfl_xor(bst, off);
+                    bst = o > bst ? o : bst;
+                    live += __shfl_xor(live, off);
+                }
+                if (lane == 0) {
+                    tb.bmax[blk] = bst;
+                    tb.blive[blk] = live;
+                    atomicOr(&gmark[blk >> (TL_GRP + 5)], 1u << ((blk >> TL_GRP) & 31u));
+                }
+            }
+            __syncthreads();
+            for (uint32_t gq = wid; gq < ngrp; gq += NWAVE) {
+                if (!((gmark[gq >> 5] >> (gq & 31u)) & 1u)) continue;   // wave-uniform
+                const uint32_t blk = (gq << TL_GRP) + (uint32_t)lane;
+                uint64_t v = blk < tb.nblk ? __hip_atomic_load(&tb.bmax[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                for (int off = 32; off > 0; off >>= 1) {
+                    const uint64_t o = __shfl_xor(v, off);
+                    v = o > v ? o : v;
+                }
+                if (lane == 0) gmax[gq] = v;
+            }
+            __syncthreads();
+            if (t == 0) TKT(7);
+            for (uint32_t i = t; i < (TL_MAXG << TL_GRP) / 32; i += TL_BT) rsmark[i] = 0u;
+            if (t < (int)(TL_MAXG / 32)) gmark[t] = 0u;
+        }
+        // ── state (thread 0): the k_refresh (finish 2) bookkeeping ──
+        if (t == 0) {
+            const uint32_t m = zout[0], zkeep = zout[1];
+            const uint32_t n = g.n - mc, B = g.B - s_rm;
+            g.tail_total += m;
+            g.Bp = g.B;
+            g.B = B;
+            g.n = n;
+            g.new_n = n;
+            g.a = a;
+            g.b = b;
+            g.nw = nw;
+            g.mc = mc;
+            z.n = n - B;
+            g.zlast = z.n;
+            if (z.n != zkeep) {
+                g.err |= ERR_COUNT_MISMATCH;
+                g.stop = 1u;
+            }
+            g.next_id = nw + 1u;
+            g.epoch += 1u;
+            g.merges_done = r + 1u;
+            z.merges_done = r + 1u;
+            if (s_nrs > TL_RS) s_exit = TL_EXIT_REMAX;
+            if (lt.ovf) s_exit = TL_EXIT_LDS;
+        }
+        __syncthreads();
+        if (s_exit != TL_EXIT_NONE) {   // dirty blocks left for the host's k_refresh
+            ++r;
+            break;
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        g.body_rm = 0u;
+        tstat[0] = g.merges_done;
+        tstat[1] = s_exit;
+    }
+    if (mybytes) atomicAdd(bytes, mybytes);
+    __syncthreads();
+    // the states back (`used` by an add: an overflowing LDS table inserted through table_add)
+    constexpr int WUSED = (int)(offsetof(DevState, used) / 4);
+    if (t < NW) {
+        if (t != WUSED) reinterpret_cast<uint32_t*>(st)[t] = s_g.w[t];
+    } else if (t < 2 * NW) {
+        reinterpret_cast<uint32_t*>(zst)[t - NW] = s_z.w[t - NW];
+    }
+    if (t == 0 && s_used) atomicAdd(&st->used, s_used);
+}
+#endif  // GBPE_TAIL_LOOP
+
 // dense → sparse: the last word start at or before `lim` (one workgroup, backwards)
 template <typename S>
 __global__ __launch_bounds__(1024) void k_sp_zone_start(const S* __restrict__ cur, uint32_t lim, uint32_t* __restrict__ out) {
@@ -2066,17 +2481,6 @@ __global__ __launch_bounds__(TPB) void k_sp_gather(const S* __restrict__ body, c
 
 // ─── host side ──────────────────────────────────────────────────────────────
 
-// launch configuration of one captured step (gbpe_trainer_step)
-struct GraphKey {
-    bool sparse = false;
-    uint32_t k = 0;
-    int cur = 0, zcur = 0, bcur = 0;
-    uint32_t gd = 0, gc = 0, gr = 0, sb = 0, sc = 0, szd = 0, szc = 0;
-    bool z1 = false;
-    void *z0 = nullptr, *z1p = nullptr, *b0 = nullptr, *b1 = nullptr;
-    uint32_t W = 0;
-    bool operator==(const GraphKey& o) const { return memcmp(this, &o, sizeof(*this)) == 0; }
-};
 
 struct gbpe_trainer {
     gbpe_ctx* ctx = nullptr;
@@ -2157,14 +2561,16 @@ struct gbpe_trainer {
     uint32_t lx_div = 16;        // with the lexicon: enter once next_mc * lx_div <= n, from the first step on (GBPE_LEXICON_DIV)
     uint32_t sub_zone = 1u << 20;   // sparse steps run in sub-steps of sub_k merges while the zone exceeds this
     uint32_t sub_k = 16;            // (the zone shrinks between them; GBPE_SUBSTEP_ZONE, GBPE_SUBSTEP)
+    // persistent tail loop (k_tail)
+    bool tail_on = true;         // GBPE_TAIL=0: never (a -DGBPE_TAIL_LOOP build only; measured no faster)
+    uint32_t tail_mc = 4096;     // run a step in k_tail once the last count is at most this (GBPE_TAIL_MC)
+    bool tail_skip = false;      // k_tail left the last step early: the next one runs k_body
+    uint32_t* d_tstat = nullptr;
+    uint64_t tail_merges = 0, tail_steps = 0, tail_exits = 0;
+    double ms_tail = 0;
     uint32_t sp_zt = 7;          // zone target = sp_zt * last_mc + 64 (>= 5: see sp_enter; 7 measured best, GBPE_SPARSE_ZT)
-    bool fuse_sel = false;       // GBPE_FUSE_SELECT=1: select in k_refresh's last workgroup (measured slower: DESIGN §2b)
     uint32_t refresh_blocks = 0; // GBPE_REFRESH_BLOCKS: k_refresh grid (0 = 2 per CU)
     uint32_t body_cap = 256;     // GBPE_BODY_WG: most k_body workgroups (default one per CU)
-    bool use_graph = false;      // replay steps as HIP graphs (GBPE_GRAPH=1): measured slower on ROCm 7
-    hipGraphExec_t graph_exec = nullptr;
-    GraphKey graph_key;
-    uint32_t graph_builds = 0;
     uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
     uint32_t* h_clog = nullptr;
     FILE* trace = nullptr;
@@ -2236,8 +2642,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     S* oth = (S*)t->buf[t->cur ^ (round & 1) ^ 1];
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
-    if (round == 0 || !t->fuse_sel)   // with fuse_sel, later merges are selected by the previous k_refresh
-        hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
                            (uint32_t*)nullptr, (uint32_t*)nullptr, (DevState*)nullptr, exact ? 1u : 0u);
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
     // many tiles: TPW tiles per k_delta workgroup (fewer hot-pair flushes)
@@ -2274,7 +2679,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
     FusedSel fs;
-    fs.log = t->fuse_sel ? t->d_log : nullptr;
+    fs.log = nullptr;
     fs.grpsum = t->grpsum;
     fs.exact = exact ? 1u : 0u;
     hipLaunchKernelGGL(k_refresh<S>, dim3(g_refresh), dim3(TPB), 0, s, t->st, round, 1, t->tb, cur,
@@ -2974,13 +3379,13 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     t->u16 = max_id <= 0x8000ull;
     t->max_id = (uint32_t)(max_id < 0x10000ull ? max_id : 0x10000ull);
     if (const char* e = getenv("GBPE_SPARSE_DIV")) t->sp_div = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_GRAPH")) t->use_graph = atoi(e) != 0;
-    if (const char* e = getenv("GBPE_FUSE_SELECT")) t->fuse_sel = atoi(e) != 0;
     if (const char* e = getenv("GBPE_REFRESH_BLOCKS")) t->refresh_blocks = (uint32_t)atoi(e);
     t->body_cap = (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
     if (const char* e = getenv("GBPE_BODY_WG")) t->body_cap = std::max<uint32_t>(1, (uint32_t)atoi(e));
     if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_LEXICON")) t->lex_on = atoi(e) != 0;
+    if (const char* e = getenv("GBPE_TAIL")) t->tail_on = atoi(e) != 0;
+    if (const char* e = getenv("GBPE_TAIL_MC")) t->tail_mc = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_LEXICON_DIV")) t->lx_div = std::max<uint32_t>(8, (uint32_t)strtoul(e, nullptr, 10));
     if (const char* e = getenv("GBPE_SUBSTEP_ZONE")) t->sub_zone = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_SUBSTEP")) t->sub_k = std::max<uint32_t>(2, (uint32_t)strtoul(e, nullptr, 10)) & ~1u;
@@ -3217,7 +3622,49 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
                                       : grid_persistent(t->ctx, gbpe_div_up(zn / 2 + 1, TPB * 16), 1));
         sg.refresh = g_refresh;
     }
+    // the persistent tail loop: one workgroup, the whole step
+#ifdef GBPE_TAIL_LOOP
+    const uint32_t zn_now = sparse ? t->n - hs->B : 0u;
+    const bool tail = sparse && t->tail_on && !t->tail_skip && !t->sharded && t->last_mc <= t->tail_mc &&
+                      zn_now <= (t->u16 ? zone_max<uint16_t>(TL_BT) : zone_max<uint32_t>(TL_BT)) &&
+                      t->tb.nblk <= (TL_MAXG << TL_GRP);
+    t->tail_skip = false;
+    auto launch_tail = [&]() -> int {
+        if (!t->d_tstat) TR_HIP(t, hipMalloc(&t->d_tstat, 16));
+        if (timing) TR_HIP(t, hipEventRecord(t->evs[0], s));
+        const uint32_t wused = (uint32_t)gbpe_div_up(t->nsec, 32);
+        const bool ex = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
+#define GBPE_TAIL_LAUNCH(S_, E_)                                                                                     \
+        do {                                                                                                         \
+        if (zn_now <= (uint32_t)TL_BT * 8u)                                                                         \
+            hipLaunchKernelGGL((k_tail<S_, E_, 8>), dim3(1), dim3(TL_BT), 0, s, t->st, t->zst, (S_*)sp_body(t), sp_mul(t), \
+                               t->sec, t->bits, t->W, wused, t->sig, t->tb, (S_*)t->zbuf[t->zcur],                      \
+                               (S_*)t->zbuf[t->zcur ^ 1], t->d_log, t->wg_bytes, t->d_tstat);                          \
+        else                                                                                                         \
+        hipLaunchKernelGGL((k_tail<S_, E_, ZoneDim<S_, TL_BT>::ZPT>), dim3(1), dim3(TL_BT), 0, s, t->st, t->zst, (S_*)sp_body(t), sp_mul(t), t->sec, \
+                           t->bits, t->W, wused, t->sig, t->tb, (S_*)t->zbuf[t->zcur], (S_*)t->zbuf[t->zcur ^ 1], t->d_log,   \
+                           t->wg_bytes, t->d_tstat);                                                             \
+        hipLaunchKernelGGL(k_refresh<S_>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S_*)nullptr,    \
+                           (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part); \
+        } while (0)
+        if (t->u16) {
+            if (ex) GBPE_TAIL_LAUNCH(uint16_t, true);
+            else GBPE_TAIL_LAUNCH(uint16_t, false);
+        } else {
+            if (ex) GBPE_TAIL_LAUNCH(uint32_t, true);
+            else GBPE_TAIL_LAUNCH(uint32_t, false);
+        }
+#undef GBPE_TAIL_LAUNCH
+        GBPE_LAUNCH_CHECK(t->ctx);
+        if (timing) TR_HIP(t, hipEventRecord(t->evs[1], s));
+        return GBPE_OK;
+    };
+#else
+    const bool tail = false;   // (diagnostic build only: -DGBPE_TAIL_LOOP, tools/build_variant.sh)
+    auto launch_tail = [&]() -> int { return GBPE_OK; };
+#endif
     auto launch_all = [&]() -> int {
+        if (tail) return launch_tail();
         for (uint32_t r = 0; r < k; ++r) {
             hipEvent_t* ev = timing ? &t->evs[5 * r] : nullptr;
             int rc;
@@ -3231,55 +3678,9 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         }
         return GBPE_OK;
     };
-    // A step is the same few hundred launches step after step: replay it as a HIP
-    // graph (captured once per launch configuration) instead of paying the host
-    // launch path per kernel.  Event timing launches directly.
-    if (timing || !t->use_graph) {
+    {
         int rc = launch_all();
         if (rc != GBPE_OK) return rc;
-    } else {
-        GraphKey key;
-        memset(&key, 0, sizeof(key));   // padding too: keys compare bytewise
-        key.sparse = sparse;
-        key.k = k;
-        key.cur = t->cur;
-        key.zcur = t->zcur;
-        key.bcur = t->bcur;
-        key.gd = g_delta;
-        key.gc = g_compact;
-        key.gr = g_refresh;
-        key.sb = sg.body;
-        key.sc = sg.copy;
-        key.szd = sg.zdelta;
-        key.szc = sg.zcompact;
-        key.z1 = sg.zone1;
-        key.z0 = t->zbuf[0];
-        key.z1p = t->zbuf[1];
-        key.b0 = t->buf[0];
-        key.b1 = t->buf[1];
-        key.W = t->W;
-        if (!t->graph_exec || !(key == t->graph_key)) {
-            if (t->graph_exec) hipGraphExecDestroy(t->graph_exec);
-            t->graph_exec = nullptr;
-            hipGraph_t g = nullptr;
-            TR_HIP(t, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-            int rc = launch_all();
-            hipError_t e = hipStreamEndCapture(s, &g);
-            if (rc != GBPE_OK) {
-                if (g) hipGraphDestroy(g);
-                return rc;
-            }
-            if (e != hipSuccess) return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "step capture failed: %s", hipGetErrorString(e));
-            e = hipGraphInstantiate(&t->graph_exec, g, nullptr, nullptr, 0);
-            hipGraphDestroy(g);
-            if (e != hipSuccess) {
-                t->graph_exec = nullptr;
-                return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "step graph instantiate failed: %s", hipGetErrorString(e));
-            }
-            memcpy(&t->graph_key, &key, sizeof(key));
-            ++t->graph_builds;
-        }
-        TR_HIP(t, hipGraphLaunch(t->graph_exec, s));
     }
     TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipMemcpyAsync(t->h_log, t->d_log, (size_t)k * 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -3295,7 +3696,13 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
                               (err & ERR_PAIR_MISSING) ? "selected pair missing " : "",
                               (err & ERR_SPARSE_WINDOW) ? "sparse stale window outside the zone" : "");
     }
-    if (timing) {
+    if (timing && tail) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, t->evs[0], t->evs[1]);
+        t->ms_tail += ms;
+        t->ms_sparse += ms;
+        t->timed_merges += done;
+    } else if (timing) {
         for (uint32_t r = 0; r < done; ++r) {
             float a = 0, b = 0, c = 0, d1 = 0, d2 = 0;
             hipEvent_t* ev = &t->evs[5 * r];
@@ -3333,6 +3740,17 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
             fprintf(t->trace, "%u %u %llu %d %u %u\n", t->done + r, t->h_log[r * 4 + 3], (unsigned long long)nn,
                     sparse ? 1 : 0, sparse && t->h_clog ? t->h_clog[2 * r] : 0u, sparse && t->h_clog ? t->h_clog[2 * r + 1] : 0u);
             nn -= t->h_log[r * 4 + 3];
+        }
+    }
+    if (tail) {
+        t->tail_merges += done;
+        ++t->tail_steps;
+        if (done < k && !hs->stop && !hs->sp_abort) {   // left early (LDS lists): k_body finishes the step
+            t->tail_skip = true;
+            ++t->tail_exits;
+            if (done == 0) {   // (its first merge did not fit): run the step with k_body now
+                return trainer_step_once(t, max_merges, merges_out, n_done, early_stop);
+            }
         }
     }
     if (sparse) {
@@ -3413,6 +3831,10 @@ extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
     o->lexicon_words = t->lx_words;
     o->lexicon_entries = t->lx_nuid;
     o->lexicon_symbols = t->lx_len;
+    o->tail_merges = t->tail_merges;
+    o->tail_steps = t->tail_steps;
+    o->tail_exits = t->tail_exits;
+    o->ms_tail = t->ms_tail;
     if (t->wg_bytes && t->wg_cap) {   // the per-workgroup counters of k_body (and its zone workgroup)
         std::vector<uint64_t> h(t->wg_cap);
         if (hipMemcpy(h.data(), t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess)
@@ -3521,8 +3943,8 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->lx_occ);
     hipFree(t->lx_w0);
     hipFree(t->lx_tmp);
+    hipFree(t->d_tstat);
     if (t->h_zst) hipHostFree(t->h_zst);
-    if (t->graph_exec) hipGraphExecDestroy(t->graph_exec);
     hipFree(t->d_clog);
     if (t->h_clog) hipHostFree(t->h_clog);
     if (t->trace) fclose(t->trace);

@@ -55,7 +55,9 @@ class TrainerStats(C.Structure):
                 ("zone_bytes", C.c_uint64), ("dense_bytes", C.c_uint64), ("ms_dense", C.c_double),
                 ("ms_sparse", C.c_double), ("ms_body", C.c_double),
                 ("lexicon_builds", C.c_uint32), ("lexicon_fallbacks", C.c_uint32), ("lexicon_words", C.c_uint64),
-                ("lexicon_entries", C.c_uint64), ("lexicon_symbols", C.c_uint64)]
+                ("lexicon_entries", C.c_uint64), ("lexicon_symbols", C.c_uint64),
+                ("tail_merges", C.c_uint64), ("tail_steps", C.c_uint64), ("tail_exits", C.c_uint64),
+                ("ms_tail", C.c_double)]
 
 
 PROGRESS_CB = C.CFUNCTYPE(C.c_int, C.POINTER(Progress), u32p, C.c_void_p)

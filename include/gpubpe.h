@@ -175,6 +175,10 @@ typedef struct gbpe_trainer_stats {
     uint64_t lexicon_words;       /* body word occurrences the lexicon represents (all builds and shrinks) */
     uint64_t lexicon_entries;     /* distinct-word entries of the current lexicon */
     uint64_t lexicon_symbols;     /* symbols of the current lexicon store (separators included) */
+    uint64_t tail_merges;         /* merges run by the persistent one-workgroup tail loop */
+    uint64_t tail_steps;          /* its launches (one per step) */
+    uint64_t tail_exits;          /* ... that left their step early (LDS lists outgrown) */
+    double   ms_tail;             /* GBPE_TRAIN_TIMING: device ms of the tail loop (included in ms_sparse) */
 } gbpe_trainer_stats;
 int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* out);
 /* Current symbol stream in the reference u32 layout (bit16 = word start). */
