@@ -27,9 +27,9 @@ static const char* const kKernelNames[] = {
     "k_delta",           // bpe_merge_reduce_b (train.wgsl:433) + incremental pair-count deltas
     "k_compact",         // bpe_prefix_sum_scan_blocks_* + bpe_finalize_compact_b (train.wgsl:522-731) + stale-tail pairs
     "k_refresh",         // bpe_find_max_pair4 (train.wgsl:204) on touched blocks + symbol_count update
-    "k_trie_walk",       // trie_tokenizer_chunked (tokenize.wgsl:88): k_trie_walk_v3 (packed double array) / nested form
+    "k_trie_walk",       // trie_tokenizer_chunked (tokenize.wgsl:88): k_trie_walk_v5 (packed double array) / nested form
     "k_chunk_scan",      // trie_prefix_sum (tokenize.wgsl:199)
-    "k_chunk_compact",   // trie_tokenizer_compact (tokenize.wgsl:225)
+    "k_chunk_compact",   // trie_tokenizer_compact (tokenize.wgsl:225): k_chunk_compact4
     "k_shard_send",      // sharded training, phase 1: delta list + header + stale-window piece (no reference counterpart)
     "k_shard_recv",      // sharded training, phase 2: apply every rank's deltas + window pairs, owner appends the window
     "k_pretok",          // PreTokenizer GPT-4 word starts (pre_tokenizer.mjs:226-292): k_pt_scan1/2 + k_pt_mark

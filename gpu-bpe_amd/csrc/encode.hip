@@ -115,6 +115,31 @@ __device__ __forceinline__ uint4 load_win(const uint8_t* __restrict__ in, uint64
     return make_uint4(w0, w1, w2, w3);
 }
 
+// 64-byte input window (one cache line per refill): 4 x 16 bytes in registers
+struct Win64 {
+    uint4 q0, q1, q2, q3;
+};
+__device__ __forceinline__ Win64 load_win64(const uint8_t* __restrict__ in, uint64_t n, uint64_t ab) {
+    Win64 w;
+    if (ab + 64 <= n) {
+        const uint4* p = reinterpret_cast<const uint4*>(in + ab);
+        w.q0 = p[0];
+        w.q1 = p[1];
+        w.q2 = p[2];
+        w.q3 = p[3];
+    } else {
+        w.q0 = load_win(in, n, ab);
+        w.q1 = load_win(in, n, ab + 16);
+        w.q2 = load_win(in, n, ab + 32);
+        w.q3 = load_win(in, n, ab + 48);
+    }
+    return w;
+}
+__device__ __forceinline__ uint32_t win64_byte(const Win64& w, uint32_t o) {
+    const uint4 q = (o & 32u) ? ((o & 16u) ? w.q3 : w.q2) : ((o & 16u) ? w.q1 : w.q0);
+    return win_byte(q, o & 15u);
+}
+
 // token vector: slot j of a 16-byte register vector (8 x u16 or 4 x u32), stored whole
 template <typename T>
 __device__ __forceinline__ void vec_put(uint4& a, uint32_t j, uint32_t tok) {
@@ -134,19 +159,24 @@ __device__ __forceinline__ void vec_put(uint4& a, uint32_t j, uint32_t tok) {
     }
 }
 
-// Production walk.  One lane per chunk (as tokenize.wgsl:88), packed 8-byte
-// double-array records, and one L2 record load per loop iteration: token starts
-// resolve from the root transitions cached in LDS inside the same iteration
-// (runs of raw bytes and one-byte leaf tokens included), and a walk that
-// enters a leaf (base == 0: no children) ends its token without the extra
-// probe that would only discover the mismatch.
+// Production walk.  One lane per chunk (as tokenize.wgsl:88) over the packed
+// 8-byte double-array records, as a one-byte-per-trip state machine: every loop
+// trip a lane consumes exactly one byte — a token start resolved from the root
+// transitions cached in LDS, or one trie transition (the trip's single L2 load);
+// a start that leads into a multi-byte path does its first transition in the same
+// trip, and a walk that enters a leaf (base == 0) ends its token without the
+// probe that would only find the mismatch.  No lane waits on another lane's run
+// of raw / one-byte tokens (an inner start loop made the wave's walking lanes
+// wait: 4.84 vs 4.29 ms on C3).  Input arrives a 64-byte line per refill: with
+// ~65K lanes per XCD walking, 16-byte refills were evicted from the 4 MB L2
+// between uses (5.33 vs 4.84 ms).
 template <typename T>
-__global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v3(const uint8_t* __restrict__ in, uint64_t n, uint32_t cs,
+__global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v5(const uint8_t* __restrict__ in, uint64_t n, uint32_t cs,
                                                            const uint2* __restrict__ rec, uint32_t nrec,
                                                            uint32_t root_base, T* __restrict__ scratch,
                                                            uint32_t* __restrict__ counts, uint64_t nchunks) {
     constexpr uint32_t PER = 16 / sizeof(T);
-    __shared__ uint2 lut[256];   // root transitions: the packed record of child c, check == 0 when present
+    __shared__ uint2 lut[256];
     {
         const uint32_t t = root_base + threadIdx.x;
         lut[threadIdx.x] = t < nrec ? rec[t] : make_uint2(0x3FFFFFu, 0u);
@@ -158,16 +188,17 @@ __global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v3(const uint8_t* __rest
     const uint32_t ce = (uint32_t)(min(c0 + cs, n) - c0);
     T* out = scratch + c0;
     uint32_t cb = ~0u;
-    uint4 win = make_uint4(0, 0, 0, 0), acc = make_uint4(0, 0, 0, 0);
-    uint32_t cnt = 0, pos = 0, wp = 0, lmp = 0, st = 0, base = 0, lmt = TID_NONE, first = 0;
+    Win64 w64{};
+    uint4 acc = make_uint4(0, 0, 0, 0);
     auto byte_at = [&](uint32_t p) -> uint32_t {
-        const uint32_t b = p & ~15u;
+        const uint32_t b = p & ~63u;
         if (b != cb) {
             cb = b;
-            win = load_win(in, n, c0 + b);
+            w64 = load_win64(in, n, c0 + b);
         }
-        return win_byte(win, p & 15u);
+        return win64_byte(w64, p & 63u);
     };
+    uint32_t cnt = 0;
     auto emit = [&](uint32_t tok) {
         vec_put<T>(acc, cnt % PER, tok);
         if (++cnt % PER == 0) {
@@ -175,20 +206,17 @@ __global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v3(const uint8_t* __rest
             acc = make_uint4(0, 0, 0, 0);
         }
     };
-    bool need_start = true;
-    while (true) {
-        // token starts: LDS only
-        while (need_start && pos < ce) {
+    uint32_t pos = 0, wp = 0, lmp = 0, st = 0, base = 0, lmt = TID_NONE, first = 0;
+    bool walking = false;
+    while (pos < ce) {
+        if (!walking) {   // a token start: LDS only
             first = byte_at(pos);
             const uint2 e = lut[first];
-            if (rec_check(e) != 0u) {   // no token starts with this byte: emit it raw (tokenize.wgsl:169-171)
-                emit(first);
-                ++pos;
-                continue;
-            }
             const uint32_t tid = rec_tid(e);
-            if (rec_base(e) == 0u) {    // one-byte leaf token
-                emit(tid != TID_NONE ? tid : first);
+            if (rec_check(e) != 0u || rec_base(e) == 0u || pos + 1 >= ce) {
+                // no token starts with this byte (emit it raw, tokenize.wgsl:169-171), a
+                // one-byte leaf, or the chunk's last byte
+                emit(rec_check(e) == 0u && tid != TID_NONE ? tid : first);
                 ++pos;
                 continue;
             }
@@ -197,201 +225,80 @@ __global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v3(const uint8_t* __rest
             lmt = tid;
             lmp = pos + 1;
             wp = pos + 1;
-            need_start = false;
+            walking = true;
         }
-        if (need_start) break;   // chunk done
-        // one trie transition: the iteration's single L2 load
-        bool adv = false, leaf = false;
-        if (wp < ce) {
-            const uint32_t t = base + byte_at(wp);
-            const uint2 r = t < nrec ? rec[t] : make_uint2(0x3FFFFFu, 0u);
-            if (rec_check(r) == st) {
-                adv = true;
-                st = t;
-                base = rec_base(r);
-                ++wp;
-                const uint32_t tid = rec_tid(r);
-                if (tid != TID_NONE) {
-                    lmt = tid;
-                    lmp = wp;
-                }
-                leaf = base == 0u;
+        // one trie transition: the trip's L2 load
+        const uint32_t t = base + byte_at(wp);
+        const uint2 r = t < nrec ? rec[t] : make_uint2(0x3FFFFFu, 0u);
+        bool end = true;
+        if (rec_check(r) == st) {
+            st = t;
+            base = rec_base(r);
+            ++wp;
+            const uint32_t tid = rec_tid(r);
+            if (tid != TID_NONE) {
+                lmt = tid;
+                lmp = wp;
             }
+            end = base == 0u || wp >= ce;
         }
-        if (!adv || leaf) {   // the longest match ends: emit it (or the raw first byte), restart after it
+        if (end) {   // the longest match ends: emit it (or the raw first byte), restart after it
             const bool hit = lmt != TID_NONE;
             emit(hit ? lmt : first);
             pos = hit ? lmp : pos + 1;
-            need_start = true;
+            walking = false;
         }
     }
     if (cnt % PER) *reinterpret_cast<uint4*>(out + (cnt / PER) * PER) = acc;
     counts[chunk] = cnt;
 }
 
-// Interleaved walk: each lane walks ILP chunks in lock step, so every loop trip
-// has ILP independent record loads in flight instead of one.  Per chunk the
-// semantics and the output are exactly k_trie_walk_v3's.  Measured slower than
-// v3 on C3 (82 VGPRs: occupancy 5 instead of 8, and twice the divergent paths
-// per wave), so it is opt-in (GBPE_ENCODE_ILP=2).
+// Chunk tokens → final positions.  A wave moves CPW chunks at once (every
+// scratch load of the CPW chunks is issued before the first store: one chunk's
+// ~cs/4 tokens alone leave too few bytes in flight to cover the HBM latency);
+// token j + 64k of a chunk pass goes to lane j, so every u32 store instruction
+// writes 256 contiguous bytes.  Chunks of more than 256 tokens take more passes.
+constexpr int CPW = 4;   // chunks per wave
 template <typename T>
-struct WalkLane {
-    uint64_t c0;
-    uint32_t ce, cb, cnt, pos, wp, lmp, st, base, lmt, first;
-    uint4 win, acc;
-    bool need_start;
-    T* out;
-};
-
-template <typename T>
-__device__ __forceinline__ uint32_t wl_byte(WalkLane<T>& L, const uint8_t* __restrict__ in, uint64_t n, uint32_t p) {
-    const uint32_t b = p & ~15u;
-    if (b != L.cb) {
-        L.cb = b;
-        L.win = load_win(in, n, L.c0 + b);
-    }
-    return win_byte(L.win, p & 15u);
-}
-
-template <typename T>
-__device__ __forceinline__ void wl_emit(WalkLane<T>& L, uint32_t tok) {
-    constexpr uint32_t PER = 16 / sizeof(T);
-    vec_put<T>(L.acc, L.cnt % PER, tok);
-    if (++L.cnt % PER == 0) {
-        *reinterpret_cast<uint4*>(L.out + L.cnt - PER) = L.acc;
-        L.acc = make_uint4(0, 0, 0, 0);
-    }
-}
-
-// token starts (LDS only) until the walk needs a record: returns its index, or
-// INV when the chunk is done
-template <typename T>
-__device__ __forceinline__ uint32_t wl_prepare(WalkLane<T>& L, const uint8_t* __restrict__ in, uint64_t n,
-                                               const uint2* lut, uint32_t root_base) {
-    while (true) {
-        while (L.need_start && L.pos < L.ce) {
-            L.first = wl_byte(L, in, n, L.pos);
-            const uint2 e = lut[L.first];
-            if (rec_check(e) != 0u) {   // no token starts with this byte: emit it raw (tokenize.wgsl:169-171)
-                wl_emit(L, L.first);
-                ++L.pos;
-                continue;
-            }
-            const uint32_t tid = rec_tid(e);
-            if (rec_base(e) == 0u) {    // one-byte leaf token
-                wl_emit(L, tid != TID_NONE ? tid : L.first);
-                ++L.pos;
-                continue;
-            }
-            L.st = root_base + L.first;
-            L.base = rec_base(e);
-            L.lmt = tid;
-            L.lmp = L.pos + 1;
-            L.wp = L.pos + 1;
-            L.need_start = false;
-        }
-        if (L.need_start) return INV;   // chunk done
-        if (L.wp < L.ce) return L.base + wl_byte(L, in, n, L.wp);
-        const bool hit = L.lmt != TID_NONE;   // the chunk ends inside a match: emit it, restart
-        wl_emit(L, hit ? L.lmt : L.first);
-        L.pos = hit ? L.lmp : L.pos + 1;
-        L.need_start = true;
-    }
-}
-
-template <typename T>
-__device__ __forceinline__ void wl_consume(WalkLane<T>& L, uint2 r, uint32_t t) {
-    bool adv = false, leaf = false;
-    if (rec_check(r) == L.st) {
-        adv = true;
-        L.st = t;
-        L.base = rec_base(r);
-        ++L.wp;
-        const uint32_t tid = rec_tid(r);
-        if (tid != TID_NONE) {
-            L.lmt = tid;
-            L.lmp = L.wp;
-        }
-        leaf = L.base == 0u;
-    }
-    if (!adv || leaf) {   // the longest match ends: emit it (or the raw first byte), restart after it
-        const bool hit = L.lmt != TID_NONE;
-        wl_emit(L, hit ? L.lmt : L.first);
-        L.pos = hit ? L.lmp : L.pos + 1;
-        L.need_start = true;
-    }
-}
-
-template <typename T, int ILP>
-__global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v4(const uint8_t* __restrict__ in, uint64_t n, uint32_t cs,
-                                                           const uint2* __restrict__ rec, uint32_t nrec,
-                                                           uint32_t root_base, T* __restrict__ scratch,
-                                                           uint32_t* __restrict__ counts, uint64_t nchunks) {
-    constexpr uint32_t PER = 16 / sizeof(T);
-    __shared__ uint2 lut[256];
-    {
-        const uint32_t t = root_base + threadIdx.x;
-        lut[threadIdx.x] = t < nrec ? rec[t] : make_uint2(0x3FFFFFu, 0u);
+__global__ __launch_bounds__(256) void k_chunk_compact4(const T* __restrict__ scratch, const uint32_t* __restrict__ counts,
+                                                        const uint32_t* __restrict__ local,
+                                                        const uint64_t* __restrict__ blocksum, uint64_t nchunks,
+                                                        uint32_t cs, uint32_t* __restrict__ out, uint64_t out_cap) {
+    __shared__ uint64_t s_off[4 * CPW];
+    __shared__ uint32_t s_cnt[4 * CPW];
+    const uint64_t c0 = (uint64_t)blockIdx.x * (4 * CPW);
+    if (threadIdx.x < 4 * CPW) {
+        const uint64_t c = c0 + threadIdx.x;
+        s_cnt[threadIdx.x] = c < nchunks ? counts[c] : 0u;
+        s_off[threadIdx.x] = c < nchunks ? blocksum[c / SCAN_BLK] + local[c] : 0ull;
     }
     __syncthreads();
-    const uint64_t g = (uint64_t)blockIdx.x * WALK_TPB + threadIdx.x;
-    const uint64_t half = (nchunks + ILP - 1) / ILP;   // lane g walks chunks g, g + half, ...
-    if (g >= half) return;
-    WalkLane<T> L[ILP];
-    uint32_t tp[ILP];
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t most = 0;
 #pragma unroll
-    for (int j = 0; j < ILP; ++j) {
-        const uint64_t chunk = g + (uint64_t)j * half;
-        const bool live = chunk < nchunks;
-        L[j].c0 = chunk * cs;
-        L[j].ce = live ? (uint32_t)(min(L[j].c0 + cs, n) - L[j].c0) : 0u;
-        L[j].cb = ~0u;
-        L[j].cnt = L[j].pos = L[j].wp = L[j].lmp = L[j].st = L[j].base = L[j].first = 0;
-        L[j].lmt = TID_NONE;
-        L[j].win = L[j].acc = make_uint4(0, 0, 0, 0);
-        L[j].need_start = true;
-        L[j].out = scratch + (live ? L[j].c0 : 0);
-        tp[j] = wl_prepare(L[j], in, n, lut, root_base);
-    }
-    while (true) {
-        bool any = false;
-        uint2 r[ILP];
+    for (int q = 0; q < CPW; ++q) most = max(most, s_cnt[wid * CPW + q]);
+    for (uint32_t b0 = 0; b0 < most; b0 += 256) {
+        uint32_t v[CPW][4];
 #pragma unroll
-        for (int j = 0; j < ILP; ++j) {   // all of this trip's record loads first
-            any |= tp[j] != INV;
-            r[j] = (tp[j] != INV && tp[j] < nrec) ? rec[tp[j]] : make_uint2(0x3FFFFFu, 0u);
+        for (int q = 0; q < CPW; ++q) {
+            const uint32_t cnt = s_cnt[wid * CPW + q];
+            const T* src = scratch + (c0 + wid * CPW + q) * (uint64_t)cs;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t j = b0 + lane + 64u * k;
+                v[q][k] = j < cnt ? (uint32_t)src[j] : 0u;
+            }
         }
-        if (!any) break;
 #pragma unroll
-        for (int j = 0; j < ILP; ++j) {
-            if (tp[j] == INV) continue;
-            wl_consume(L[j], r[j], tp[j]);
-            tp[j] = wl_prepare(L[j], in, n, lut, root_base);
+        for (int q = 0; q < CPW; ++q) {
+            const uint32_t cnt = s_cnt[wid * CPW + q];
+            const uint64_t off = s_off[wid * CPW + q];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t j = b0 + lane + 64u * k;
+                if (j < cnt && off + j < out_cap) out[off + j] = v[q][k];
+            }
         }
-    }
-#pragma unroll
-    for (int j = 0; j < ILP; ++j) {
-        const uint64_t chunk = g + (uint64_t)j * half;
-        if (chunk >= nchunks) continue;
-        if (L[j].cnt % PER) *reinterpret_cast<uint4*>(L[j].out + (L[j].cnt / PER) * PER) = L[j].acc;
-        counts[chunk] = L[j].cnt;
-    }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void k_chunk_compact(const T* __restrict__ scratch, const uint32_t* __restrict__ counts,
-                                                       const uint32_t* __restrict__ local,
-                                                       const uint64_t* __restrict__ blocksum, uint64_t nchunks,
-                                                       uint32_t cs, uint32_t* __restrict__ out, uint64_t out_cap) {
-    const uint64_t chunk = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (chunk >= nchunks) return;
-    const int lane = threadIdx.x & 63;
-    const uint64_t off = blocksum[chunk / SCAN_BLK] + local[chunk];
-    const uint32_t cnt = counts[chunk];
-    const T* src = scratch + chunk * (uint64_t)cs;
-    for (uint32_t j = lane; j < cnt; j += 64) {
-        const uint64_t d = off + j;
-        if (d < out_cap) out[d] = (uint32_t)src[j];
     }
 }
 
@@ -573,36 +480,23 @@ int encode_device_impl(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* d_in, uint64
     uint64_t* d_total = blocksum + nblk + 1;
     const uint32_t gw = (uint32_t)gbpe_div_up(nchunks, WALK_TPB);
     GBPE_HIP(ctx, hipEventRecord(ctx->ev[0], s));
-    // packed-record walk when the trie packs and chunks are whole 16-byte token
-    // vectors; otherwise the plain per-token walk (GBPE_ENCODE_WALK=nested forces it)
-    static const bool force_nested = getenv("GBPE_ENCODE_WALK") && std::string(getenv("GBPE_ENCODE_WALK")) == "nested";
-    const bool v3 = !force_nested && (cs % 8u) == 0u && tr->rec2;
+    // the packed-record state-machine walk when the trie packs and chunks are whole
+    // 16-byte token vectors (cs % 8 == 0: every adaptive chunk size); otherwise the
+    // plain per-token walk over 16-byte records
+    const bool packed = (cs % 8u) == 0u && tr->rec2;
     const uint32_t nrec2 = tr->nrec + 256;
-    // GBPE_ENCODE_ILP=2: the interleaved walk (measured slower on C3: 7.0 vs 5.1 ms, occupancy 5 vs 8)
-    static const int ilp = getenv("GBPE_ENCODE_ILP") ? atoi(getenv("GBPE_ENCODE_ILP")) : 1;
-    if (v3 && ilp >= 2) {
-        const uint32_t g2 = (uint32_t)gbpe_div_up(gbpe_div_up(nchunks, 2), WALK_TPB);
-        if (narrow)
-            hipLaunchKernelGGL((k_trie_walk_v4<uint16_t, 2>), dim3(g2), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2,
-                               nrec2, tr->root_base, (uint16_t*)ctx->enc_scratch, counts, nchunks);
-        else
-            hipLaunchKernelGGL((k_trie_walk_v4<uint32_t, 2>), dim3(g2), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2,
-                               nrec2, tr->root_base, (uint32_t*)ctx->enc_scratch, counts, nchunks);
-    } else if (v3) {
-        if (narrow)
-            hipLaunchKernelGGL(k_trie_walk_v3<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
-                               tr->root_base, (uint16_t*)ctx->enc_scratch, counts, nchunks);
-        else
-            hipLaunchKernelGGL(k_trie_walk_v3<uint32_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
-                               tr->root_base, (uint32_t*)ctx->enc_scratch, counts, nchunks);
-    } else {
-        if (narrow)
-            hipLaunchKernelGGL(k_trie_walk<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec, tr->nrec,
-                               tr->root, (uint16_t*)ctx->enc_scratch, counts, nchunks);
-        else
-            hipLaunchKernelGGL(k_trie_walk<uint32_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec, tr->nrec,
-                               tr->root, (uint32_t*)ctx->enc_scratch, counts, nchunks);
-    }
+    if (packed && narrow)
+        hipLaunchKernelGGL(k_trie_walk_v5<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
+                           tr->root_base, (uint16_t*)ctx->enc_scratch, counts, nchunks);
+    else if (packed)
+        hipLaunchKernelGGL(k_trie_walk_v5<uint32_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
+                           tr->root_base, (uint32_t*)ctx->enc_scratch, counts, nchunks);
+    else if (narrow)
+        hipLaunchKernelGGL(k_trie_walk<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec, tr->nrec,
+                           tr->root, (uint16_t*)ctx->enc_scratch, counts, nchunks);
+    else
+        hipLaunchKernelGGL(k_trie_walk<uint32_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec, tr->nrec,
+                           tr->root, (uint32_t*)ctx->enc_scratch, counts, nchunks);
     GBPE_LAUNCH_CHECK(ctx);
     GBPE_HIP(ctx, hipEventRecord(ctx->ev[1], s));
     hipLaunchKernelGGL(k_chunk_scan1, dim3((uint32_t)nblk), dim3(SCAN_TPB), 0, s, (const uint32_t*)counts, nchunks, local,
@@ -610,13 +504,13 @@ int encode_device_impl(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* d_in, uint64
     hipLaunchKernelGGL(k_chunk_scan2, dim3(1), dim3(SCAN_TPB), 0, s, blocksum, nblk, d_total);
     GBPE_LAUNCH_CHECK(ctx);
     GBPE_HIP(ctx, hipEventRecord(ctx->ev[2], s));
-    const uint32_t gc = (uint32_t)gbpe_div_up(nchunks, 4);
+    const uint32_t gc4 = (uint32_t)gbpe_div_up(nchunks, 4 * CPW);
     if (narrow)
-        hipLaunchKernelGGL(k_chunk_compact<uint16_t>, dim3(gc), dim3(256), 0, s, (const uint16_t*)ctx->enc_scratch,
+        hipLaunchKernelGGL(k_chunk_compact4<uint16_t>, dim3(gc4), dim3(256), 0, s, (const uint16_t*)ctx->enc_scratch,
                            (const uint32_t*)counts, (const uint32_t*)local, (const uint64_t*)blocksum, nchunks, cs, d_out,
                            out_cap);
     else
-        hipLaunchKernelGGL(k_chunk_compact<uint32_t>, dim3(gc), dim3(256), 0, s, (const uint32_t*)ctx->enc_scratch,
+        hipLaunchKernelGGL(k_chunk_compact4<uint32_t>, dim3(gc4), dim3(256), 0, s, (const uint32_t*)ctx->enc_scratch,
                            (const uint32_t*)counts, (const uint32_t*)local, (const uint64_t*)blocksum, nchunks, cs, d_out,
                            out_cap);
     GBPE_LAUNCH_CHECK(ctx);

@@ -17,11 +17,22 @@
 //   trieUpload(ctx, nodes: Uint32Array, edges: Uint32Array) -> trie      trieFree(trie)
 //   encode(ctx, trie, bytes, chunkSize) -> Promise<Uint32Array>
 //   wordBoundary(ctx, bytes) -> Uint8Array
+//
+// Concurrency and lifetimes.  Every call that touches a context's device state
+// (its stream, pooled encode buffers, error string) holds that context's mutex,
+// so overlapping Promises (Promise.all over encode / trainerStep) run one after
+// the other on the device instead of racing (the reference serialises them on
+// one WebGPU queue).  Contexts are reference-counted by their trainers, tries,
+// BPE tables and in-flight work: destroyContext() closes a context for new
+// calls, and the device context is freed when the last of those is gone.
+// trainerDestroy() / trieFree() during a step / encode defer the free to its
+// completion.
 #include <node_api.h>
 
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -37,17 +48,58 @@
 
 namespace {
 
+// All reference counts below change on the JS thread only (calls, finalizers,
+// async-work completions); worker threads only take `mu`.
 struct Ctx {
     gbpe_ctx* ctx = nullptr;
+    std::mutex mu;          // serialises device work on this context
+    int refs = 1;           // the JS external + children + in-flight work
+    bool closed = false;    // destroyContext() was called
+    bool js_ref = true;     // the JS external's reference is still held
 };
+void ctx_release(Ctx* c) {
+    if (c && --c->refs == 0) {
+        if (c->ctx) gbpe_ctx_destroy(c->ctx);
+        delete c;
+    }
+}
+bool ctx_usable(const Ctx* c) { return c && c->ctx && !c->closed; }
+
 struct Trainer {
     gbpe_trainer* t = nullptr;
     Ctx* owner = nullptr;
     uint32_t batch = 128;
+    int inflight = 0;              // queued / running trainerStep works
+    bool destroy_pending = false;  // trainerDestroy() while a step ran
 };
+void trainer_free(Trainer* t) {   // the device trainer and its context reference
+    if (t->t) {
+        std::lock_guard<std::mutex> g(t->owner->mu);
+        gbpe_trainer_destroy(t->t);
+        t->t = nullptr;
+    }
+    if (t->owner) {
+        ctx_release(t->owner);
+        t->owner = nullptr;
+    }
+}
 struct Trie {
     gbpe_trie* trie = nullptr;
+    Ctx* owner = nullptr;
+    int inflight = 0;
+    bool destroy_pending = false;
 };
+void trie_free(Trie* t) {
+    if (t->trie) {
+        std::lock_guard<std::mutex> g(t->owner->mu);
+        gbpe_trie_free(t->trie);
+        t->trie = nullptr;
+    }
+    if (t->owner) {
+        ctx_release(t->owner);
+        t->owner = nullptr;
+    }
+}
 
 std::string last_error(gbpe_ctx* c, const char* what, int rc) {
     std::string m = what;
@@ -131,8 +183,10 @@ napi_value make_u32_array(napi_env env, const uint32_t* src, size_t n) {
 
 void ctx_finalize(napi_env, void* data, void*) {
     Ctx* c = static_cast<Ctx*>(data);
-    if (c->ctx) gbpe_ctx_destroy(c->ctx);
-    delete c;
+    if (c->js_ref) {
+        c->js_ref = false;
+        ctx_release(c);
+    }
 }
 
 napi_value CreateContext(napi_env env, napi_callback_info info) {
@@ -160,9 +214,12 @@ napi_value DestroyContext(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     Ctx* c = argc ? unwrap_external<Ctx>(env, argv[0]) : nullptr;
-    if (c && c->ctx) {
-        gbpe_ctx_destroy(c->ctx);
-        c->ctx = nullptr;
+    if (c && !c->closed) {   // freed once its trainers, tries and in-flight work are gone
+        c->closed = true;
+        if (c->js_ref) {
+            c->js_ref = false;
+            ctx_release(c);
+        }
     }
     return nullptr;
 }
@@ -172,12 +229,14 @@ napi_value Limits(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     Ctx* c = argc ? unwrap_external<Ctx>(env, argv[0]) : nullptr;
-    if (!c || !c->ctx) {
+    if (!ctx_usable(c)) {
         napi_throw_type_error(env, nullptr, "limits(ctx): invalid context");
         return nullptr;
     }
     uint64_t mb = 0;
+    std::unique_lock<std::mutex> g(c->mu);
     int rc = gbpe_ctx_limits(c->ctx, &mb);
+    g.unlock();
     if (rc != GBPE_OK) return throw_status(env, c->ctx, "limits", rc);
     napi_value obj, v;
     NAPI_CALL(env, napi_create_object(env, &obj));
@@ -205,14 +264,16 @@ napi_value WordBoundary(napi_env env, napi_callback_info info) {
     Ctx* c = argc >= 1 ? unwrap_external<Ctx>(env, argv[0]) : nullptr;
     const uint8_t* data = nullptr;
     size_t len = 0;
-    if (!c || !c->ctx || argc < 2 || !get_bytes(env, argv[1], &data, &len)) {
+    if (!ctx_usable(c) || argc < 2 || !get_bytes(env, argv[1], &data, &len)) {
         napi_throw_type_error(env, nullptr, "wordBoundary(ctx, Uint8Array)");
         return nullptr;
     }
     napi_value ab, ta;
     void* dst = nullptr;
     NAPI_CALL(env, napi_create_arraybuffer(env, len, &dst, &ab));
+    std::unique_lock<std::mutex> g(c->mu);
     int rc = gbpe_word_boundary(c->ctx, data, len, static_cast<uint8_t*>(dst));
+    g.unlock();
     if (rc != GBPE_OK) return throw_status(env, c->ctx, "wordBoundary", rc);
     NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, len, ab, 0, &ta));
     return ta;
@@ -226,14 +287,16 @@ napi_value PretokenizeGpt4(napi_env env, napi_callback_info info) {
     Ctx* c = argc >= 1 ? unwrap_external<Ctx>(env, argv[0]) : nullptr;
     const uint8_t* data = nullptr;
     size_t len = 0;
-    if (!c || !c->ctx || argc < 2 || !get_bytes(env, argv[1], &data, &len)) {
+    if (!ctx_usable(c) || argc < 2 || !get_bytes(env, argv[1], &data, &len)) {
         napi_throw_type_error(env, nullptr, "pretokenizeGpt4(ctx, Uint8Array)");
         return nullptr;
     }
     napi_value ab, ta;
     void* dst = nullptr;
     NAPI_CALL(env, napi_create_arraybuffer(env, len, &dst, &ab));
+    std::unique_lock<std::mutex> g(c->mu);
     int rc = gbpe_pretokenize_gpt4(c->ctx, data, len, static_cast<uint8_t*>(dst));
+    g.unlock();
     if (rc != GBPE_OK) return throw_status(env, c->ctx, "pretokenizeGpt4", rc);
     NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, len, ab, 0, &ta));
     return ta;
@@ -243,7 +306,7 @@ napi_value PretokenizeGpt4(napi_env env, napi_callback_info info) {
 
 void trainer_finalize(napi_env, void* data, void*) {
     Trainer* t = static_cast<Trainer*>(data);
-    if (t->t) gbpe_trainer_destroy(t->t);
+    trainer_free(t);   // (in-flight steps hold a reference to the external: none runs now)
     delete t;
 }
 
@@ -254,7 +317,7 @@ napi_value TrainerCreate(napi_env env, napi_callback_info info) {
     Ctx* c = argc >= 1 ? unwrap_external<Ctx>(env, argv[0]) : nullptr;
     const uint8_t* data = nullptr;
     size_t len = 0;
-    if (!c || !c->ctx || argc < 4 || !get_bytes(env, argv[1], &data, &len)) {
+    if (!ctx_usable(c) || argc < 4 || !get_bytes(env, argv[1], &data, &len)) {
         napi_throw_type_error(env, nullptr, "trainerCreate(ctx, Uint8Array, wordStarts|null, opts)");
         return nullptr;
     }
@@ -275,10 +338,14 @@ napi_value TrainerCreate(napi_env env, napi_callback_info info) {
     o.batch_size = get_u32_prop(env, argv[3], "batchSize", GBPE_BATCH_SIZE);
     o.flags = get_u32_prop(env, argv[3], "exact", 0) ? GBPE_TRAIN_EXACT_COMPACTION : 0u;
     auto* t = new Trainer();
-    t->owner = c;
     t->batch = o.batch_size ? o.batch_size : GBPE_BATCH_SIZE;
+    std::unique_lock<std::mutex> g(c->mu);
     int rc = gbpe_trainer_create(c->ctx, data, len, ws, 0, &o, &t->t);
-    if (rc != GBPE_OK) {
+    g.unlock();
+    if (rc == GBPE_OK) {
+        t->owner = c;
+        ++c->refs;
+    } else {
         delete t;
         if (rc == GBPE_E_EMPTY) {
             napi_throw_error(env, nullptr, "No symbols to train on — corpus is empty after pre-processing");
@@ -297,8 +364,8 @@ napi_value TrainerDestroy(napi_env env, napi_callback_info info) {
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     Trainer* t = argc ? unwrap_external<Trainer>(env, argv[0]) : nullptr;
     if (t && t->t) {
-        gbpe_trainer_destroy(t->t);
-        t->t = nullptr;
+        if (t->inflight) t->destroy_pending = true;   // step_complete frees it
+        else trainer_free(t);
     }
     return nullptr;
 }
@@ -319,6 +386,7 @@ struct StepWork {
 void step_execute(napi_env, void* data) {
     auto* w = static_cast<StepWork*>(data);
     w->merges.assign((size_t)w->tr->batch * 4, 0);
+    std::lock_guard<std::mutex> g(w->tr->owner->mu);
     w->rc = gbpe_trainer_step(w->tr->t, w->max_merges, w->merges.data(), &w->n_done, &w->early);
     if (w->rc != GBPE_OK) {
         w->err = last_error(w->tr->owner->ctx, "train step", w->rc);
@@ -345,6 +413,7 @@ void step_complete(napi_env env, napi_status, void* data) {
         napi_set_named_property(env, obj, "symbolCount", v);
         napi_resolve_deferred(env, w->deferred, obj);
     }
+    if (--w->tr->inflight == 0 && w->tr->destroy_pending) trainer_free(w->tr);
     napi_delete_reference(env, w->keep);
     napi_delete_async_work(env, w->work);
     delete w;
@@ -355,12 +424,13 @@ napi_value TrainerStep(napi_env env, napi_callback_info info) {
     napi_value argv[2];
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     Trainer* t = argc >= 1 ? unwrap_external<Trainer>(env, argv[0]) : nullptr;
-    if (!t || !t->t) {
+    if (!t || !t->t || t->destroy_pending) {
         napi_throw_type_error(env, nullptr, "trainerStep(trainer, maxMerges): invalid trainer");
         return nullptr;
     }
     auto* w = new StepWork();
     w->tr = t;
+    ++t->inflight;   // (the trainer holds its context: it outlives the work)
     if (argc >= 2) napi_get_value_uint32(env, argv[1], &w->max_merges);
     napi_value promise, name;
     NAPI_CALL(env, napi_create_promise(env, &w->deferred, &promise));
@@ -375,7 +445,7 @@ napi_value TrainerStep(napi_env env, napi_callback_info info) {
 
 void trie_finalize(napi_env, void* data, void*) {
     Trie* t = static_cast<Trie*>(data);
-    if (t->trie) gbpe_trie_free(t->trie);
+    trie_free(t);
     delete t;
 }
 
@@ -386,12 +456,18 @@ napi_value TrieUpload(napi_env env, napi_callback_info info) {
     Ctx* c = argc >= 1 ? unwrap_external<Ctx>(env, argv[0]) : nullptr;
     const uint32_t *nodes = nullptr, *edges = nullptr;
     size_t nn = 0, ne = 0;
-    if (!c || !c->ctx || argc < 3 || !get_u32s(env, argv[1], &nodes, &nn) || !get_u32s(env, argv[2], &edges, &ne)) {
+    if (!ctx_usable(c) || argc < 3 || !get_u32s(env, argv[1], &nodes, &nn) || !get_u32s(env, argv[2], &edges, &ne)) {
         napi_throw_type_error(env, nullptr, "trieUpload(ctx, nodes: Uint32Array, edges: Uint32Array)");
         return nullptr;
     }
     auto* t = new Trie();
+    std::unique_lock<std::mutex> g(c->mu);
     int rc = gbpe_trie_upload(c->ctx, nodes, (uint32_t)(nn / 3), edges, (uint32_t)(ne / 2), &t->trie);
+    g.unlock();
+    if (rc == GBPE_OK) {
+        t->owner = c;
+        ++c->refs;
+    }
     if (rc != GBPE_OK) {
         delete t;
         return throw_status(env, c->ctx, "trie upload", rc);
@@ -407,8 +483,8 @@ napi_value TrieFree(napi_env env, napi_callback_info info) {
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     Trie* t = argc ? unwrap_external<Trie>(env, argv[0]) : nullptr;
     if (t && t->trie) {
-        gbpe_trie_free(t->trie);
-        t->trie = nullptr;
+        if (t->inflight) t->destroy_pending = true;   // encode_complete frees it
+        else trie_free(t);
     }
     return nullptr;
 }
@@ -417,11 +493,16 @@ napi_value TrieFree(napi_env env, napi_callback_info info) {
 
 struct Bpe {
     gbpe_bpe* bpe = nullptr;
+    Ctx* owner = nullptr;
 };
 
 void bpe_finalize(napi_env, void* data, void*) {
     Bpe* b = static_cast<Bpe*>(data);
-    if (b->bpe) gbpe_bpe_free(b->bpe);
+    if (b->bpe) {
+        std::lock_guard<std::mutex> g(b->owner->mu);
+        gbpe_bpe_free(b->bpe);
+    }
+    ctx_release(b->owner);
     delete b;
 }
 
@@ -432,12 +513,18 @@ napi_value BpeUpload(napi_env env, napi_callback_info info) {
     Ctx* c = argc >= 1 ? unwrap_external<Ctx>(env, argv[0]) : nullptr;
     const uint32_t* m = nullptr;
     size_t nm = 0;
-    if (!c || !c->ctx || argc < 2 || !get_u32s(env, argv[1], &m, &nm)) {
+    if (!ctx_usable(c) || argc < 2 || !get_u32s(env, argv[1], &m, &nm)) {
         napi_throw_type_error(env, nullptr, "bpeUpload(ctx, merges: Uint32Array [a,b,id]*)");
         return nullptr;
     }
     auto* b = new Bpe();
+    std::unique_lock<std::mutex> g(c->mu);
     int rc = gbpe_bpe_upload(c->ctx, m, (uint32_t)(nm / 3), &b->bpe);
+    g.unlock();
+    if (rc == GBPE_OK) {
+        b->owner = c;
+        ++c->refs;
+    }
     if (rc != GBPE_OK) {
         delete b;
         return throw_status(env, c->ctx, "bpe upload", rc);
@@ -455,13 +542,15 @@ napi_value BpeEncode(napi_env env, napi_callback_info info) {
     Bpe* b = argc >= 2 ? unwrap_external<Bpe>(env, argv[1]) : nullptr;
     const uint8_t* data = nullptr;
     size_t len = 0;
-    if (!c || !c->ctx || !b || !b->bpe || argc < 3 || !get_bytes(env, argv[2], &data, &len)) {
+    if (!ctx_usable(c) || !b || !b->bpe || argc < 3 || !get_bytes(env, argv[2], &data, &len)) {
         napi_throw_type_error(env, nullptr, "bpeEncode(ctx, bpe, Uint8Array)");
         return nullptr;
     }
     std::vector<uint32_t> out(len ? len : 1);
     uint64_t n = 0;
+    std::unique_lock<std::mutex> g(c->mu);
     int rc = gbpe_bpe_encode(c->ctx, b->bpe, data, len, out.data(), out.size(), &n);
+    g.unlock();
     if (rc != GBPE_OK) return throw_status(env, c->ctx, "bpe encode", rc);
     return make_u32_array(env, out.data(), (size_t)n);
 }
@@ -484,6 +573,7 @@ struct EncodeWork {
 void encode_execute(napi_env, void* data) {
     auto* w = static_cast<EncodeWork*>(data);
     w->out.resize(w->len ? w->len : 1);
+    std::lock_guard<std::mutex> g(w->c->mu);
     w->rc = gbpe_encode(w->c->ctx, w->trie->trie, w->data, w->len, w->cs, w->out.data(), w->len, &w->n_out);
     if (w->rc != GBPE_OK) w->err = last_error(w->c->ctx, "encode", w->rc);
 }
@@ -498,6 +588,8 @@ void encode_complete(napi_env env, napi_status, void* data) {
     } else {
         napi_resolve_deferred(env, w->deferred, make_u32_array(env, w->out.data(), (size_t)w->n_out));
     }
+    if (--w->trie->inflight == 0 && w->trie->destroy_pending) trie_free(w->trie);
+    ctx_release(w->c);
     napi_delete_reference(env, w->keep_in);
     napi_delete_reference(env, w->keep_ctx);
     napi_delete_reference(env, w->keep_trie);
@@ -513,13 +605,15 @@ napi_value Encode(napi_env env, napi_callback_info info) {
     Trie* tr = argc >= 2 ? unwrap_external<Trie>(env, argv[1]) : nullptr;
     const uint8_t* data = nullptr;
     size_t len = 0;
-    if (!c || !c->ctx || !tr || !tr->trie || argc < 4 || !get_bytes(env, argv[2], &data, &len)) {
+    if (!ctx_usable(c) || !tr || !tr->trie || tr->destroy_pending || argc < 4 || !get_bytes(env, argv[2], &data, &len)) {
         napi_throw_type_error(env, nullptr, "encode(ctx, trie, Uint8Array, chunkSize)");
         return nullptr;
     }
     auto* w = new EncodeWork();
     w->c = c;
+    ++c->refs;        // released by encode_complete
     w->trie = tr;
+    ++tr->inflight;
     w->data = data;
     w->len = len;
     napi_get_value_uint32(env, argv[3], &w->cs);

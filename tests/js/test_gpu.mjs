@@ -49,6 +49,34 @@ async function main() {
     let threw = false;
     try { await new BPETrainer(engine).train(new Uint8Array(0)); } catch (e) { threw = /empty/.test(e.message); }
     if (!threw) fail('empty corpus must throw');
+    {   // concurrency + lifetimes on one engine (the addon serialises a context's device work)
+        const c = cases.train[0];
+        const r = await new BPETrainer(engine).train(new Uint8Array(Buffer.from(c.b64, 'base64')),
+                                                    { targetVocabSize: c.target });
+        const tok = TrieTokenizer.fromVocab(engine, r.vocab, c.chunkSize ? { chunkSize: c.chunkSize } : {});
+        const text = new Uint8Array(Buffer.from(c.text_b64, 'base64'));
+        const all = await Promise.all([tok.encodeBytes(text), tok.encodeBytes(text), tok.encodeBytes(text.subarray(7))]);
+        if (JSON.stringify(Array.from(all[0])) !== JSON.stringify(c.tokens)) fail('concurrent encode 0');
+        if (JSON.stringify(Array.from(all[1])) !== JSON.stringify(c.tokens)) fail('concurrent encode 1');
+        const solo = await tok.encodeBytes(text.subarray(7));
+        if (JSON.stringify(Array.from(all[2])) !== JSON.stringify(Array.from(solo))) fail('concurrent encode 2');
+        // free the trie while an encode is in flight, then destroy the engine while a
+        // training step is in flight: both complete, nothing is used after free
+        const n = (await import('../../gpu-bpe_amd/js/native.js')).native();
+        const pending = tok.encodeBytes(text);
+        tok.destroy();
+        const late = await pending;
+        if (JSON.stringify(Array.from(late)) !== JSON.stringify(c.tokens)) fail('encode across trie free');
+        const e2 = await new BPEEngine().init();
+        const tr = n.trainerCreate(e2.device, new Uint8Array(Buffer.from(c.b64, 'base64')), null,
+                                   { targetVocabSize: c.target });
+        const step = n.trainerStep(tr, 128);
+        e2.destroy();
+        n.trainerDestroy(tr);
+        const s = await step;
+        if (s.merges.length !== 4 * Math.min(128, c.merges.length)) fail('step across destroy');
+        checks += 4;
+    }
     engine.destroy();
     console.log('ok ' + checks + ' checks');
 }
