@@ -91,6 +91,10 @@ void gbpe_ctx_destroy(gbpe_ctx* ctx) {
     if (ctx->enc_host_total) hipHostFree(ctx->enc_host_total);
     for (auto& ev : ctx->ev)
         if (ev) hipEventDestroy(ev);
+    if (ctx->copy_stream) {
+        hipStreamSynchronize(ctx->copy_stream);
+        hipStreamDestroy(ctx->copy_stream);
+    }
     if (ctx->own_stream) {
         hipStreamSynchronize(ctx->own_stream);
         hipStreamDestroy(ctx->own_stream);

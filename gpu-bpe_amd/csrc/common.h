@@ -14,6 +14,7 @@ struct gbpe_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;   // created by gbpe_ctx_create; `stream` may be a caller's
+    hipStream_t copy_stream = nullptr;  // gbpe_encode's device-to-host copies of finished slices (created on first use)
     uint64_t total_mem = 0;
     int num_cu = 0;
     std::string err;

@@ -19,12 +19,17 @@
 #include "scan.h"
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
 
 namespace {
 
 constexpr int WALK_TPB = 256;
+constexpr uint64_t kEncSlice = 128ull << 20;   // gbpe_encode's pipeline slice (host buffers)
 constexpr uint32_t INV = 0xFFFFFFFFu;
 
 template <typename T>
@@ -543,6 +548,12 @@ extern "C" int gbpe_encode_device(gbpe_ctx* ctx, gbpe_trie* tr, const void* d_by
                               out_cap, n_out);
 }
 
+// Host buffers in and out (tokenizer.js:213-335 incl. the readback).  Inputs
+// larger than one slice run as a pipeline of chunk-aligned slices: while the
+// device encodes slice i+1 (after its upload), a second host thread copies slice
+// i's tokens back, so uploads, kernels and downloads overlap.  Slices start at
+// multiples of 64 * chunk size, so every chunk — and every token — is the one a
+// single pass produces.
 extern "C" int gbpe_encode(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* bytes, uint64_t n, uint32_t chunk_size,
                            uint32_t* out, uint64_t out_cap, uint64_t* n_out) {
     if (!ctx || !tr || !n_out || (n && !bytes)) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
@@ -552,16 +563,82 @@ extern "C" int gbpe_encode(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* bytes, u
     int rc = grow(ctx, &ctx->enc_in, &ctx->enc_in_bytes, gbpe_div_up(n, 4) * 4 + 16);
     if (rc == GBPE_OK) rc = grow(ctx, &ctx->enc_out, &ctx->enc_out_bytes, n * 4 + 16);   // <= 1 token per byte
     if (rc != GBPE_OK) return rc;
-    GBPE_HIP(ctx, hipMemcpyAsync(ctx->enc_in, bytes, n, hipMemcpyHostToDevice, ctx->stream));
+    const uint64_t unit = (uint64_t)cs * 64;
+    const char* se = getenv("GBPE_ENCODE_SLICE");   // (tests: many slices on small inputs)
+    const uint64_t want = se ? std::max<uint64_t>(1, strtoull(se, nullptr, 10)) : kEncSlice;
+    const uint64_t slice = std::max<uint64_t>(unit, (want / unit) * unit);
+    uint8_t* d_in = (uint8_t*)ctx->enc_in;
+    uint32_t* d_out = (uint32_t*)ctx->enc_out;
+    if (n <= slice) {
+        GBPE_HIP(ctx, hipMemcpyAsync(d_in, bytes, n, hipMemcpyHostToDevice, ctx->stream));
+        uint64_t total = 0;
+        rc = encode_device_impl(ctx, tr, d_in, n, cs, d_out, n, &total);
+        *n_out = total;
+        if (rc != GBPE_OK) return rc;
+        if (total > out_cap)
+            return gbpe_set_error(ctx, GBPE_E_CAPACITY, "encode: output needs %llu tokens", (unsigned long long)total);
+        if (total) {
+            GBPE_HIP(ctx, hipMemcpyAsync(out, d_out, total * 4, hipMemcpyDeviceToHost, ctx->stream));
+            GBPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        }
+        return GBPE_OK;
+    }
+    if (!ctx->copy_stream) GBPE_HIP(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    struct Part {
+        uint64_t off, cnt;
+    };
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Part> q;
+    bool finished = false;
+    hipError_t copy_err = hipSuccess;
+    hipStream_t so = ctx->copy_stream;
+    const int dev = ctx->device;
+    std::thread drain([&]() {
+        hipSetDevice(dev);
+        for (;;) {
+            Part p;
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return finished || !q.empty(); });
+                if (q.empty()) return;
+                p = q.front();
+                q.pop_front();
+            }
+            if (copy_err != hipSuccess) continue;
+            hipError_t e = hipMemcpyAsync(out + p.off, d_out + p.off, p.cnt * 4, hipMemcpyDeviceToHost, so);
+            if (e == hipSuccess) e = hipStreamSynchronize(so);
+            if (e != hipSuccess) copy_err = e;
+        }
+    });
     uint64_t total = 0;
-    rc = encode_device_impl(ctx, tr, (const uint8_t*)ctx->enc_in, n, cs, (uint32_t*)ctx->enc_out, n, &total);
+    for (uint64_t s0 = 0; s0 < n && rc == GBPE_OK; s0 += slice) {
+        const uint64_t len = std::min(slice, n - s0);
+        hipError_t e = hipMemcpyAsync(d_in + s0, bytes + s0, len, hipMemcpyHostToDevice, ctx->stream);
+        if (e != hipSuccess) {
+            rc = gbpe_set_error(ctx, GBPE_E_DEVICE, "encode upload failed: %s", hipGetErrorString(e));
+            break;
+        }
+        uint64_t t = 0;
+        rc = encode_device_impl(ctx, tr, d_in + s0, len, cs, d_out + total, n - total, &t);   // (synchronises)
+        if (rc != GBPE_OK) break;
+        if (t && total + t <= out_cap) {
+            std::lock_guard<std::mutex> g(mu);
+            q.push_back(Part{total, t});
+            cv.notify_one();
+        }
+        total += t;
+    }
+    {
+        std::lock_guard<std::mutex> g(mu);
+        finished = true;
+        cv.notify_one();
+    }
+    drain.join();
     *n_out = total;
     if (rc != GBPE_OK) return rc;
+    if (copy_err != hipSuccess) return gbpe_set_error(ctx, GBPE_E_DEVICE, "encode readback failed: %s", hipGetErrorString(copy_err));
     if (total > out_cap) return gbpe_set_error(ctx, GBPE_E_CAPACITY, "encode: output needs %llu tokens", (unsigned long long)total);
-    if (total) {
-        GBPE_HIP(ctx, hipMemcpyAsync(out, ctx->enc_out, total * 4, hipMemcpyDeviceToHost, ctx->stream));
-        GBPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    }
     return GBPE_OK;
 }
 

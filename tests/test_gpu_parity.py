@@ -253,6 +253,25 @@ def test_encode_matches_oracle(eng, cs):
     tok.destroy()
 
 
+@pytest.mark.parametrize("cs", [None, 7, 64])
+def test_encode_host_pipeline_slices(eng, cs, monkeypatch):
+    # gbpe_encode (host buffers) pipelines chunk-aligned slices with a second
+    # readback thread; a tiny slice makes a 150 KB input dozens of slices, and the
+    # tokens must equal one device pass (gbpe_encode_device) and the oracle
+    from gpubpe import TrieTokenizer, synth
+    train = synth.multilingual(80000, seed=31)
+    vocab = O.vocab_from_merges(O.train(train, 1200, compaction="exact")["merges"]).entries
+    text = synth.multilingual(150000, seed=33)
+    tok = TrieTokenizer.from_vocab(eng, vocab, chunk_size=cs)
+    want = _oracle_encode(vocab, text, tok.chunk_size)
+    monkeypatch.setenv("GBPE_ENCODE_SLICE", "4096")
+    got = tok.encode_bytes(text)
+    assert np.array_equal(got, want)
+    monkeypatch.delenv("GBPE_ENCODE_SLICE")
+    assert np.array_equal(tok.encode_bytes(text), want)
+    tok.destroy()
+
+
 def test_encode_edge_cases(eng):
     from gpubpe import TrieTokenizer
     vocab = O.vocab_from_merges([[116, 104], [256, 101], [32, 257]]).entries
