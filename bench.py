@@ -20,10 +20,17 @@ Secondary legs (same JSON line):
     (tests/golden/train_en1g.npz, all 32,512 merges), the encode tokens against
     the fixture and the CPU restatement.
 
-Multi-GPU (--gpus N under torch.distributed.run, one rank per GPU): the same
-1 GiB corpus cut at word starts into N shards (strong scaling, `value` =
-global merges / max wall over ranks), sharded training with one RCCL exchange
-per merge (gpubpe/sharded.py).
+Multi-GPU (--gpus N under torch.distributed.run, one rank per GPU):
+  * training: one 1 GiB corpus, one vocabulary (strong scaling: the total work
+    is fixed).  The merge chain is sequential — every merge's argmax needs the
+    previous merge's counts — and one merge costs less than an exchange between
+    GPUs, so every rank runs the complete training (replicated, no per-merge
+    collective); `value` = global merges / max wall over ranks.  The per-merge
+    sharded trainer (gpubpe/sharded.py, one RCCL all-gather per merge) runs with
+    --sharded;
+  * tokenize: the one 1 GiB C3 input cut into chunk-aligned slices, one per rank
+    (gpubpe/split_encode.py): GB/s = input bytes / max wall over ranks; the
+    tokens are gathered to rank 0 and checked against the fixture.
 """
 from __future__ import annotations
 
@@ -550,6 +557,114 @@ def sharded_line(args, lib, ctx, dist, rank, world):
     return line
 
 
+def c3_vocab_trie(args, lib, ctx):
+    """The C3 vocabulary (32K, trained on the GPU on the 100 MiB multilingual
+    sample, seed 4), compiled to the reference trie and uploaded."""
+    from gpubpe import _lib, compile_vocab_to_trie, parse_header, parse_trie_buffers
+    from gpubpe.vocab import Vocab
+    sample = make_corpus({"gen": "multilingual", "n": args.vocab_sample_bytes, "seed": 4})
+    d = device_buffer(lib, ctx, sample)
+    merges, _ = train_run(lib, ctx, d, len(sample), args.vocab)
+    lib.gbpe_device_free(ctx, d)
+    voc = Vocab()
+    for a, b in merges[:, :2].tolist():
+        voc.add_merge(a, b)
+    blob = compile_vocab_to_trie(voc.entries)
+    hdr = parse_header(blob)
+    nodes, edges = parse_trie_buffers(blob, hdr)
+    trie = C.c_void_p()
+    _lib.check(lib.gbpe_trie_upload(ctx, nodes.ctypes.data_as(_lib.u32p), hdr["nodeCount"],
+                                    edges.ctypes.data_as(_lib.u32p), hdr["edgeCount"], C.byref(trie)), ctx, "trie")
+    return trie, max(512, min(2048, hdr["maxTokenLen"] * 8))   # tokenizer.js:67-68
+
+
+def split_encode_leg(args, lib, ctx, dist, rank, world):
+    """C3 at N ranks: one 1 GiB input, chunk-aligned slice per rank."""
+    import torch
+    from gpubpe import _lib
+    from gpubpe.split_encode import slice_bounds
+    trie, cs = c3_vocab_trie(args, lib, ctx)
+    text = make_corpus({"gen": "multilingual", "n": args.encode_bytes, "seed": 3})
+    n = len(text)
+    s0, e0 = slice_bounds(n, cs, world)[rank]
+    part = text[s0:e0]
+    d_in = device_buffer(lib, ctx, part)
+    d_out = C.c_void_p()
+    _lib.check(lib.gbpe_device_alloc(ctx, 4 * len(part) + 64, C.byref(d_out)), ctx, "alloc out")
+    n_out = C.c_uint64()
+    _lib.check(lib.gbpe_encode_device(ctx, trie, d_in, len(part), cs, d_out, len(part), C.byref(n_out)), ctx, "warm")
+    reps = 5
+    lib.gbpe_synchronize(ctx)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _lib.check(lib.gbpe_encode_device(ctx, trie, d_in, len(part), cs, d_out, len(part), C.byref(n_out)), ctx, "enc")
+    lib.gbpe_synchronize(ctx)
+    wall = dist.max((time.perf_counter() - t0) / reps)
+    dist.barrier()
+    local = np.empty(int(n_out.value), dtype=np.uint32)
+    if local.shape[0]:
+        _lib.check(lib.gbpe_memcpy_d2h(ctx, local.ctypes.data_as(C.c_void_p), d_out, 4 * local.shape[0]), ctx, "d2h")
+    lib.gbpe_device_free(ctx, d_in)
+    lib.gbpe_device_free(ctx, d_out)
+    lib.gbpe_trie_free(trie)
+    # gather: slice totals (exclusive scan -> offsets), then the tokens to rank 0
+    dev = "cuda" if dist.transport == "nccl" else "cpu"
+    cnt = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.dist.all_gather(cnt, torch.tensor([local.shape[0]], dtype=torch.int64, device=dev))
+    counts = [int(c.item()) for c in cnt]
+    cap = max(counts)
+    buf = torch.zeros(cap, dtype=torch.int32, device=dev)
+    buf[: local.shape[0]] = torch.from_numpy(local.view(np.int32)).to(dev)
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.dist.all_gather(parts, buf)
+    res = {"workload": f"C3 split over {world} ranks: chunked greedy trie encode of one 1,073,741,824 B multilingual "
+                       f"UTF-8 input (seed 3), chunk-aligned slices (chunk {cs}), 32K vocab",
+           "bytes": n, "tokens": int(sum(counts)), "chunk_size": cs, "gbps_kernels_split": round(n / 1e9 / wall, 2),
+           "slice_tokens": counts}
+    if rank == 0:
+        toks = np.concatenate([p[:c].cpu().numpy().view(np.uint32) for p, c in zip(parts, counts)])
+        fx = os.path.join(GOLD, "encode_c3enc1g.json")
+        if os.path.exists(fx) and args.encode_bytes == 1 << 30 and args.vocab_sample_bytes == 104_857_600:
+            meta = json.load(open(fx))
+            res["fixture_tokens_equal"] = (toks.shape[0] == meta["n_tokens"] and
+                                           hashlib.sha256(np.ascontiguousarray(toks, "<u4").tobytes()).hexdigest()
+                                           == meta["tokens_sha256"])
+    return res
+
+
+def replicated_line(args, lib, ctx, dist, rank, world):
+    data, wall, total, last, det, parity = headline_leg(args, lib, ctx, dist)
+    line = {
+        "metric": METRIC,
+        "value": round(total / wall, 1),
+        "unit": "merges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * wall / max(1, args.steps), 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": f"u{8 * det['bytes_per_symbol']}",
+        "data": "synthetic (seeded Zipf English-like corpus, gpubpe.synth)",
+        "config": {"workload": "headline: 32K-vocab BPE train on one 1,073,741,824 B English-like UTF-8 corpus (seed 2); "
+                               f"{world} ranks each run the complete training (the merge chain is sequential: "
+                               "replicated, no per-merge exchange); step = one complete training run; value = global "
+                               "merges / max wall over ranks",
+                   "train_bytes": HEADLINE["n"], "target_vocab": args.vocab,
+                   "merges_per_step": det["merges_per_run"], "parallelism": f"replicated{world}"},
+        "roofline": train_roofline(det, wall / max(1, args.steps)),
+        "train_detail": det,
+        "parity": parity,
+    }
+    ok = 1.0 if parity.get("train_merges_equal_fixture", True) else 0.0
+    line["parity"]["all_ranks_merges_equal_fixture"] = -dist.max(-ok) == 1.0
+    if not args.no_encode:
+        line["tokenize"] = split_encode_leg(args, lib, ctx, dist, rank, world)
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -563,7 +678,8 @@ def main():
     ap.add_argument("--no-c2", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP-event roofline run")
     ap.add_argument("--cpu-merges", type=int, default=0, help="CPU baseline merges on the CPU share (0 = 24)")
-    ap.add_argument("--sharded", action="store_true", help="use the sharded trainer even at N=1 (RCCL rehearsal)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="the per-merge sharded trainer (one RCCL all-gather per merge; also at N=1 as a rehearsal)")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -574,8 +690,10 @@ def main():
     rc = lib.gbpe_ctx_create(int(os.environ.get("GBPE_BENCH_DEVICE", local)) if world > 1 else 0, C.byref(ctx))
     if rc != 0:
         raise SystemExit(f"gbpe_ctx_create failed ({rc}): no MI355X visible")
-    if world > 1 or args.sharded:
+    if args.sharded:
         line = sharded_line(args, lib, ctx, dist, rank, world)
+    elif world > 1:
+        line = replicated_line(args, lib, ctx, dist, rank, world)
     else:
         line = single_line(args, lib, ctx, dist, rank)
     if rank == 0:
