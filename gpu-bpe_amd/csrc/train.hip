@@ -1738,7 +1738,7 @@ union BodyLds {   // body workgroups use the candidate arrays, the zone workgrou
     BodyCand c;
 };
 
-template <typename S, bool EXACT, int BT>
+template <typename S, bool EXACT, int BT, int ZPT = ZoneDim<S, BT>::ZPT>
 __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
                                               uint32_t* __restrict__ bits, uint32_t W, uint32_t wpg,
                                               uint32_t* __restrict__ sig, Table tb, uint32_t nbody,
@@ -1763,7 +1763,8 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     const uint32_t bid = zone1 ? (blockIdx.x == 0 ? nbody : blockIdx.x - 1u) : blockIdx.x;
     // deltas go to the replica (single GPU) or to the per-merge delta table (sharded)
     if (zone1 && bid == nbody) {
-        zone_one<S, EXACT, BT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, dtb, a, b, nw, mc, wg_bytes + nbody, round);
+        zone_one<S, EXACT, BT, LTAB_T, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, dtb, a, b, nw, mc, wg_bytes + nbody,
+                                             round);
         if (t == 0) {
             KT(5);
             KTV(6, 2);
@@ -2561,6 +2562,7 @@ struct gbpe_trainer {
     uint32_t lx_div = 16;        // with the lexicon: enter once next_mc * lx_div <= n, from the first step on (GBPE_LEXICON_DIV)
     uint32_t sub_zone = 1u << 20;   // sparse steps run in sub-steps of sub_k merges while the zone exceeds this
     uint32_t sub_k = 16;            // (the zone shrinks between them; GBPE_SUBSTEP_ZONE, GBPE_SUBSTEP)
+    bool zone16 = true;             // u16 zones of 8K-16K symbols: the 16-per-thread zone pass (GBPE_ZONE16=0: off)
     // persistent tail loop (k_tail)
     bool tail_on = true;         // GBPE_TAIL=0: never (a -DGBPE_TAIL_LOOP build only; measured no faster)
     uint32_t tail_mc = 4096;     // run a step in k_tail once the last count is at most this (GBPE_TAIL_MC)
@@ -2700,7 +2702,9 @@ struct SpGrid {
 };
 
 template <typename S>
-uint32_t zone_max(int bt) { return bt == 1024 ? ZoneDim<S, 1024>::ZMAX : ZoneDim<S, 256>::ZMAX; }
+uint32_t zone_max(int bt) {
+    return bt == 1023 ? 1024u * 16u : bt == 1024 ? ZoneDim<S, 1024>::ZMAX : ZoneDim<S, 256>::ZMAX;
+}
 // k_body grid: bitmap words per workgroup (>= the measured best 16 / 32 at C2 size),
 // at most `cap` workgroups (GBPE_BODY_WG; default 4 per CU)
 inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* wpg) {
@@ -2716,9 +2720,15 @@ inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* 
 }
 
 // launch k_body<S, EXACT, bt> (one instantiation per workgroup size)
+// bt: 256, 1024, or 1023 = 1024 threads with 16 zone symbols each (u16 zones of
+// 8K-16K symbols: half the per-thread zone work of the 32K form; 1 GiB en1g
+// 1.017 -> 0.963 s.  1024 threads x 8 for zones <= 8K instead of 256 x 32 was
+// slower: C2 0.66 vs 0.61 s)
 template <typename S, bool EXACT, typename... A>
 void launch_body(int bt, uint32_t grid, hipStream_t s, A... args) {
-    if (bt == 1024)
+    if (bt == 1023 && sizeof(S) == 2)
+        hipLaunchKernelGGL((k_body<S, EXACT, 1024, 16>), dim3(grid), dim3(1024), 0, s, args...);
+    else if (bt >= 1023)
         hipLaunchKernelGGL((k_body<S, EXACT, 1024>), dim3(grid), dim3(1024), 0, s, args...);
     else
         hipLaunchKernelGGL((k_body<S, EXACT, 256>), dim3(grid), dim3(256), 0, s, args...);
@@ -3385,6 +3395,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_LEXICON")) t->lex_on = atoi(e) != 0;
     if (const char* e = getenv("GBPE_TAIL")) t->tail_on = atoi(e) != 0;
+    if (const char* e = getenv("GBPE_ZONE16")) t->zone16 = atoi(e) != 0;
     if (const char* e = getenv("GBPE_TAIL_MC")) t->tail_mc = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_LEXICON_DIV")) t->lx_div = std::max<uint32_t>(8, (uint32_t)strtoul(e, nullptr, 10));
     if (const char* e = getenv("GBPE_SUBSTEP_ZONE")) t->sub_zone = (uint32_t)strtoul(e, nullptr, 10);
@@ -3613,6 +3624,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         const uint32_t z256 = t->u16 ? zone_max<uint16_t>(256) : zone_max<uint32_t>(256);
         sg.bt = zn <= z256 ? 256 : 1024;   // small zone: the low-latency 256-thread workgroups
         body_grid(t, sg.bt, &sg.body, &sg.wpg);
+        if (sg.bt == 1024 && t->u16 && zn <= 16384u && t->zone16) sg.bt = 1023;
         sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt));
         sg.copy = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u : grid_persistent(t->ctx, gbpe_div_up(zn / 5 + 1, TPB * 8), 1);
         sg.zdelta = (uint32_t)(zt ? zt : 1);
