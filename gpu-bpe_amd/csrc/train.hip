@@ -48,7 +48,7 @@ constexpr int TILE = TPB * EPT;       // 8192 symbols per tile (16 KiB of u16 in
 constexpr int LTAB = 2048;            // LDS delta table slots (tail window)
 constexpr int LTAB_FULL = 8192;       // LDS table slots for the full recount
 constexpr int LPROBE = 24;            // LDS probes before spilling to the global table
-constexpr uint32_t BLK_LOG2 = 11;     // 2048 table slots per argmax block
+constexpr uint32_t BLK_LOG2 = 8;      // 256 table slots per argmax block: one wave re-maxes one (2 x 16 B per lane)
 constexpr int SEL_THREADS = 1024;
 
 template <typename S> struct Sym;
@@ -397,8 +397,6 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
                                                  const uint32_t* __restrict__ rwlist, DevState* zst,
                                                  uint32_t* __restrict__ clog = nullptr, FusedSel fs = FusedSel(),
                                                  uint64_t* __restrict__ part = nullptr) {
-    __shared__ uint64_t red[TPB / 64];
-    __shared__ uint32_t rlive[TPB / 64];
     (void)cur;
     (void)rwlist;
     if (part && finish == 2 && threadIdx.x == 0) KTR(0);
@@ -456,8 +454,10 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             }
         }
     }
-    // this WG's contiguous run of blocks: all flags (and, for `part`, the maxima
-    // kept from before) in one load, then only the dirty ones
+    // this WG's contiguous run of blocks (<= 64): all flags (and, for `part`, the
+    // maxima kept from before) in one load; then every wave re-maxes its share of
+    // the dirty ones, one 256-slot block at a time (no workgroup barrier per block:
+    // a merge dirties a few blocks per workgroup, each holding a few live pairs)
     __shared__ uint64_t s_dmask;
     __shared__ uint64_t s_bm[64];
     const uint32_t per = (tb.nblk + gridDim.x - 1) / gridDim.x;   // <= 64 (host-sized grid)
@@ -471,66 +471,48 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
         if (threadIdx.x == 0) s_dmask = m;
     }
     __syncthreads();
-    uint64_t dm = s_dmask;
-    // software-pipelined: the next dirty block's slots load while this one reduces
-    constexpr int NV = (1 << BLK_LOG2) / 2 / TPB;   // 16-byte loads per thread
-    uint4 en[NV];
-    uint32_t nblk = 0xFFFFFFFFu;
-    auto fetch = [&]() {
-        if (!dm) {
-            nblk = 0xFFFFFFFFu;
-            return;
-        }
-        nblk = b0 + (uint32_t)(__ffsll((long long)dm) - 1);
-        dm &= dm - 1;
-        const uint4* s = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)nblk << BLK_LOG2));
+    {
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        constexpr int NV = (1 << BLK_LOG2) / 2 / 64;   // 16-byte loads per lane
+        uint64_t dm = s_dmask;
+        for (int k = 0; dm; ++k) {   // (wave-uniform)
+            const uint32_t bit = (uint32_t)(__ffsll((long long)dm) - 1);
+            dm &= dm - 1;
+            if ((k & (TPB / 64 - 1)) != wid) continue;
+            const uint32_t blk = b0 + bit;
+            const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)blk << BLK_LOG2));
+            uint4 e[NV];
 #pragma unroll
-        for (int k = 0; k < NV; ++k) en[k] = s[threadIdx.x + k * TPB];
-    };
-    fetch();
-    while (nblk != 0xFFFFFFFFu) {
-        const uint32_t blk = nblk;
-        uint4 e[NV];
+            for (int q = 0; q < NV; ++q) e[q] = sl[lane + q * 64];
+            uint64_t best = 0;
+            uint32_t live = 0;
 #pragma unroll
-        for (int k = 0; k < NV; ++k) e[k] = en[k];
-        fetch();
-        uint64_t best = 0;
-        uint32_t live = 0;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-            if (e[k].x && (int32_t)e[k].y > 0) {
-                const uint64_t key = ((uint64_t)e[k].y << 32) | (uint32_t)(~e[k].x);
-                best = key > best ? key : best;
-                ++live;
+            for (int q = 0; q < NV; ++q) {
+                if (e[q].x && (int32_t)e[q].y > 0) {
+                    const uint64_t key = ((uint64_t)e[q].y << 32) | (uint32_t)(~e[q].x);
+                    best = key > best ? key : best;
+                    ++live;
+                }
+                if (e[q].z && (int32_t)e[q].w > 0) {
+                    const uint64_t key = ((uint64_t)e[q].w << 32) | (uint32_t)(~e[q].z);
+                    best = key > best ? key : best;
+                    ++live;
+                }
             }
-            if (e[k].z && (int32_t)e[k].w > 0) {
-                const uint64_t key = ((uint64_t)e[k].w << 32) | (uint32_t)(~e[k].z);
-                best = key > best ? key : best;
-                ++live;
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint64_t o = __shfl_xor(best, off);
+                best = o > best ? o : best;
+                live += __shfl_xor(live, off);
+            }
+            if (lane == 0) {
+                tb.bmax[blk] = best;
+                tb.blive[blk] = live;
+                tb.dirty[blk] = 0u;
+                s_bm[bit] = best;
             }
         }
-        for (int off = 32; off > 0; off >>= 1) {
-            uint64_t o = __shfl_xor(best, off);
-            best = o > best ? o : best;
-            live += __shfl_xor(live, off);
-        }
-        if ((threadIdx.x & 63) == 0) {
-            red[threadIdx.x >> 6] = best;
-            rlive[threadIdx.x >> 6] = live;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int w = 1; w < TPB / 64; ++w) {
-                best = red[w] > best ? red[w] : best;
-                live += rlive[w];
-            }
-            tb.bmax[blk] = best;
-            tb.blive[blk] = live;
-            tb.dirty[blk] = 0u;
-            s_bm[blk - b0] = best;
-        }
-        __syncthreads();
     }
+    __syncthreads();
     if (part && threadIdx.x < 64) {   // this workgroup's maximum, for sel_inline
         uint64_t best = s_bm[threadIdx.x];
         for (int off = 32; off > 0; off >>= 1) {
@@ -2608,6 +2590,10 @@ uint32_t grid_persistent(const gbpe_ctx* ctx, uint64_t work_tiles, uint32_t per_
     if (work_tiles < g) g = work_tiles;
     return (uint32_t)(g ? g : 1);
 }
+// a grid over argmax blocks: every workgroup owns at most 64 (one flag ballot)
+uint32_t grid_blocks(const gbpe_ctx* ctx, uint32_t nblk, uint32_t per_cu) {
+    return std::max<uint32_t>(grid_persistent(ctx, nblk, per_cu), (uint32_t)gbpe_div_up(nblk, 64));
+}
 
 int table_rebuild(gbpe_trainer* t) {
     hipStream_t s = t->ctx->stream;
@@ -2628,10 +2614,10 @@ int table_rebuild(gbpe_trainer* t) {
     hipLaunchKernelGGL(k_clear_dirty_all, dim3(gbpe_div_up(t->tb.nblk, 256)), dim3(256), 0, s, t->st, t->tb);
     GBPE_LAUNCH_CHECK(t->ctx);
     if (t->u16)
-        hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, 0u,
+        hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(grid_blocks(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, 0u,
                            0, t->tb, (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
     else
-        hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, 0u,
+        hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(grid_blocks(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, 0u,
                            0, t->tb, (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
@@ -3461,7 +3447,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         hipHostMalloc((void**)&t->h_log, (size_t)t->batch * 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipHostMalloc failed"));
     t->tb.used = &t->st->used;
-    t->g_refresh = grid_persistent(ctx, t->tb.nblk, 2);
+    t->g_refresh = grid_blocks(ctx, t->tb.nblk, 2);
     if (t->refresh_blocks) t->g_refresh = std::max<uint32_t>(t->refresh_blocks, (uint32_t)gbpe_div_up(t->tb.nblk, 64));
     if (hipMemsetAsync(t->tb.dirty, 0, t->tb.nblk * sizeof(uint32_t), s) != hipSuccess ||
         hipMemsetAsync(t->hitmask, 0, (ntiles0 + 1) * TPB * sizeof(uint32_t), s) != hipSuccess)
@@ -4079,14 +4065,16 @@ __device__ void shard_list_role(DevState* st, Table dt, uint32_t* __restrict__ r
     }
     __syncthreads();
     uint64_t dm = s_dmask;
-    constexpr int NV = (1 << BLK_LOG2) / 2 / TPB;
+    constexpr int NV = (1 << BLK_LOG2) / 2 >= TPB ? (1 << BLK_LOG2) / 2 / TPB : 1;
+    constexpr uint32_t NQ = (1u << BLK_LOG2) / 2;   // 16-byte quads per block
     while (dm) {
         const uint32_t blk = b0 + (uint32_t)(__ffsll((long long)dm) - 1);
         dm &= dm - 1;
         uint4* sl = reinterpret_cast<uint4*>(dt.slots + ((uint64_t)blk << BLK_LOG2));
         uint4 e[NV];
 #pragma unroll
-        for (int k = 0; k < NV; ++k) e[k] = sl[threadIdx.x + k * TPB];
+        for (int k = 0; k < NV; ++k)
+            e[k] = threadIdx.x + k * TPB < NQ ? sl[threadIdx.x + k * TPB] : make_uint4(0u, 0u, 0u, 0u);
         uint32_t c = 0;
 #pragma unroll
         for (int k = 0; k < NV; ++k) c += (e[k].x && e[k].y) + (e[k].z && e[k].w);
@@ -4119,7 +4107,7 @@ __device__ void shard_list_role(DevState* st, Table dt, uint32_t* __restrict__ r
                 if (o < cap_list) { rec[HDR + 2 * o] = e[k].z; rec[HDR + 2 * o + 1] = e[k].w; }
                 ++o;
             }
-            if (e[k].x || e[k].z) sl[threadIdx.x + k * TPB] = make_uint4(0u, 0u, 0u, 0u);
+            if ((e[k].x || e[k].z) && threadIdx.x + k * TPB < NQ) sl[threadIdx.x + k * TPB] = make_uint4(0u, 0u, 0u, 0u);
         }
         __syncthreads();
     }
@@ -4587,10 +4575,10 @@ extern "C" int gbpe_shard_import_counts(gbpe_trainer* t, const void* d_lists, co
     }
     hipLaunchKernelGGL(k_clear_dirty_all, dim3((uint32_t)gbpe_div_up(t->tb.nblk, 256)), dim3(256), 0, s, t->st, t->tb);
     if (t->u16)
-        hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st,
+        hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(grid_blocks(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st,
                            0u, 0, t->tb, (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
     else
-        hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(grid_persistent(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st,
+        hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(grid_blocks(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st,
                            0u, 0, t->tb, (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
@@ -4704,7 +4692,7 @@ int shard_phase1(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl, ui
     else
         hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, dt,
                            t->hitmask, t->tile_cnt, t->grpsum, eager);
-    const uint32_t nlb = grid_persistent(t->ctx, dt.nblk, 2);
+    const uint32_t nlb = grid_blocks(t->ctx, dt.nblk, 2);
     const uint32_t nwb = grid_persistent(t->ctx, gbpe_div_up(cw, TPB * 8) + 1, 1);
     hipLaunchKernelGGL(k_shard_send<S>, dim3(nlb + 1 + nwb), dim3(TPB), 0, s, t->st, round, dt, (const S*)cur,
                        (const S*)oth, (const uint32_t*)t->hitmask, (const uint32_t*)t->grpsum, rec, cl, cw, nlb);
@@ -4729,7 +4717,7 @@ int shard_phase2(gbpe_trainer* t, uint32_t round, const uint32_t* recv, uint32_t
     else
         hipLaunchKernelGGL((k_compact<S, false>), dim3(g_tiles), dim3(CTPB), 0, s, t->st, round, cur, oth,
                            (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
-    hipLaunchKernelGGL(k_refresh<S>, dim3(grid_persistent(t->ctx, t->tb.nblk, 2)), dim3(TPB), 0, s, t->st, round, 1,
+    hipLaunchKernelGGL(k_refresh<S>, dim3(grid_blocks(t->ctx, t->tb.nblk, 2)), dim3(TPB), 0, s, t->st, round, 1,
                        t->tb, cur, (const uint32_t*)nullptr, (DevState*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
@@ -4765,7 +4753,7 @@ int shard_phase1_sp(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl)
         launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, wpg, t->sig, t->tb, nbody,
                               (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc, zone ? 1u : 0u, (const uint64_t*)t->part,
                               t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh, sp_mul(t));
-    const uint32_t nlb = grid_persistent(t->ctx, dt.nblk, 2);
+    const uint32_t nlb = grid_blocks(t->ctx, dt.nblk, 2);
     hipLaunchKernelGGL(k_shard_send_sp, dim3(nlb + 1), dim3(TPB), 0, s, t->st, t->zst, round, dt, rec, cl, nlb);
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
