@@ -210,7 +210,8 @@ def train_roofline(det, wall_per_run):
                  "frac": round(a / HBM_PEAK_GBPS, 4), "algorithmic_bytes": ev["dense_bytes"],
                  "ms": round(ev["ms_dense"], 2)}
     equiv = det["stream_bytes"] / 1e9 / wall_per_run
-    roof = {"bound": "hbm", "kernel": "k_body (sector-sparse merge pass, one launch per merge)", "achieved": None,
+    roof = {"bound": "hbm", "kernel": "k_body (sector-sparse merge pass over the word lexicon, one launch per merge)",
+            "achieved": None,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None, "traffic": None}
     if ev and ev["ms_body"] > 0 and ev["sparse_merges"] > 0:
         a = ev["body_bytes"] / 1e9 / (ev["ms_body"] / 1e3)
@@ -220,8 +221,9 @@ def train_roofline(det, wall_per_run):
                      "launches": ev["sparse_merges"],
                      "timing": "HIP events around every k_body launch of one extra full run of the same workload "
                                "(events add inter-kernel gaps, so they stay out of the timed runs)",
-                     "note": "latency-bound by design: a late merge touches a few hundred sectors, so it moves "
-                             "kilobytes, not the stream; the loop avoids the bytes rather than streaming them"})
+                     "note": "latency-bound by design: the body is one copy of every distinct word (DESIGN §2c), "
+                             "so a merge moves the few sectors holding its pair, kilobytes, not the stream; the loop "
+                             "avoids the bytes rather than streaming them"})
     roof["dense_stream"] = dense
     roof["dense_equivalent"] = {"gbps": round(equiv, 1), "frac": round(equiv / HBM_PEAK_GBPS, 4),
                                 "bytes": det["stream_bytes"],
