@@ -668,6 +668,22 @@ __global__ __launch_bounds__(1024) void k_topcount(Table tb, uint32_t* __restric
     }
 }
 
+// live pairs (count > 0) from the per-block live counts k_refresh keeps, once per
+// sparse step (the dense loop's k_select counts them every merge)
+__global__ __launch_bounds__(1024) void k_live(DevState* st, Table tb) {
+    __shared__ uint32_t red[16];
+    uint32_t live = 0;
+    for (uint32_t i = threadIdx.x; i < tb.nblk; i += 1024) live += tb.blive[i];
+    for (int off = 32; off > 0; off >>= 1) live += __shfl_xor(live, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = live;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) live += red[w];
+        st->live = live;
+        if (live > st->max_live) st->max_live = live;
+    }
+}
+
 // A merge is "active" for the stream kernels iff k_select logged it this round.
 __device__ __forceinline__ bool merge_active(const DevState* st, uint32_t round) {
     return !st->stop && st->merges_done == round + 1u;
@@ -3679,6 +3695,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     {
         int rc = launch_all();
         if (rc != GBPE_OK) return rc;
+        if (sparse) hipLaunchKernelGGL(k_live, dim3(1), dim3(1024), 0, s, t->st, t->tb);
     }
     TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipMemcpyAsync(t->h_log, t->d_log, (size_t)k * 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
