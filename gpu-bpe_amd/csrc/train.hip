@@ -1411,7 +1411,7 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, ui
 template <typename S, int BT> struct ZoneDim {
     static constexpr int ZPT = (BT == 1024 && sizeof(S) == 4) ? 16 : 32;   // zone positions per thread
     static constexpr uint32_t ZMAX = (uint32_t)BT * ZPT;   // 8192 (256) / 32768 or 16384 (1024) symbols
-    static constexpr uint32_t ZWIN = ZMAX / 4;              // >= ZMAX / 5 >= mc (zone >= 5 mc)
+    static constexpr uint32_t ZWIN = ZMAX / 3 + 64;         // >= mc: the zone holds >= 3 mc (sel_inline's rule)
 };
 template <typename S, int BT>
 struct ZoneLds {
@@ -1600,6 +1600,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
 // merge whose count could overflow the exchange record stalls here, before any
 // sector is touched, on every rank alike (the count is global).
 struct SelShard {
+    uint32_t zf = 5;         // zone rule: z >= max(2 mc + mc_prev, zf mc) + 2 (single GPU: GBPE_ZONE_F, sharded 5)
     uint32_t cap_list = 0;   // 0 = single GPU
     uint32_t zmax = 0;       // the one-workgroup zone limit (sharded zones never run multi-tile)
     uint32_t* nlog = nullptr;
@@ -1649,8 +1650,11 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     const bool stop = mc < 2u || nw > 0xFFFFu;                                          // train.wgsl:345-348
     const bool bad = !stop && !exact && g.is_last &&
                      (uint64_t)g.n + g.off - g.poff < 2ull * mc + g.Bp;   // cannot happen
-    const bool abort = !stop && !bad && !exact &&
-                       ((uint64_t)g.zlast < 5ull * mc + 2u || (sh.zmax && g.zlast > sh.zmax));   // zone misfit
+    // zone misfit: this merge's window source must lie in the zone's stale buffer
+    // (n - 2mc >= Bp, where n - Bp >= z - mc_prev: the last merge removed <= mc_prev
+    // body symbols), and the zone keeps >= zf mc for the merges after it
+    const uint64_t zneed = std::max<uint64_t>(2ull * mc + g.mc, (uint64_t)sh.zf * mc) + 2u;
+    const bool abort = !stop && !bad && !exact && ((uint64_t)g.zlast < zneed || (sh.zmax && g.zlast > sh.zmax));
     const uint32_t need = 6u * mc + 64u;   // distinct deltas of one merge <= 4 per site + tail + window
     const bool stall = !stop && !bad && !abort && sh.cap_list && need > sh.cap_list;
     const bool go = !stop && !bad && !abort && !stall;
@@ -2568,7 +2572,10 @@ struct gbpe_trainer {
     uint32_t* d_tstat = nullptr;
     uint64_t tail_merges = 0, tail_steps = 0, tail_exits = 0;
     double ms_tail = 0;
-    uint32_t sp_zt = 7;          // zone target = sp_zt * last_mc + 64 (>= 5: see sp_enter; 7 measured best, GBPE_SPARSE_ZT)
+    uint32_t sp_zt = 5;          // zone target = sp_zt * last_mc + 64 (>= zone_f; GBPE_SPARSE_ZT; 4/5/6/7 measured
+                                 // 0.895/0.893/0.918/0.918 s at 1 GiB with zone_f 3)
+    uint32_t shrink_pct = 200;   // shrink once the zone exceeds shrink_pct % of the target + 4096 (GBPE_SHRINK_PCT)
+    uint32_t zone_f = 3;         // single-GPU zone rule factor (sel_inline; GBPE_ZONE_F, >= 3)
     uint32_t refresh_blocks = 0; // GBPE_REFRESH_BLOCKS: k_refresh grid (0 = 2 per CU)
     uint32_t body_cap = 256;     // GBPE_BODY_WG: most k_body workgroups (default one per CU)
     uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
@@ -2599,6 +2606,12 @@ int tr_err(gbpe_trainer* t, int code, const char* msg) { return gbpe_set_error(t
 // the symbols the sparse kernels merge: the lexicon store, or the body sectors in place
 inline void* sp_body(const gbpe_trainer* t) { return t->lex ? t->lx_store : t->buf[t->bcur]; }
 inline uint32_t* sp_mul(const gbpe_trainer* t) { return t->lex ? t->lx_mul : nullptr; }
+// the single-GPU selection's zone rule (sel_inline)
+inline SelShard sel_single(const gbpe_trainer* t) {
+    SelShard sh;
+    sh.zf = t->zone_f;
+    return sh;
+}
 
 
 uint32_t grid_persistent(const gbpe_ctx* ctx, uint64_t work_tiles, uint32_t per_cu) {
@@ -2748,12 +2761,12 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     if (exact)
         launch_body<S, true>(g.bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, g.zone1 ? 1u : 0u,
-                             (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, SelShard(),
+                             (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
                              sp_mul(t));
     else
         launch_body<S, false>(g.bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                               g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, g.zone1 ? 1u : 0u,
-                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, SelShard(),
+                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
                              sp_mul(t));
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
     if (!g.zone1) {
@@ -3278,7 +3291,7 @@ int sp_shrink(gbpe_trainer* t) {
     DevState* hs = t->h_st;
     const uint32_t z = t->n - hs->B;
     const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
-    if (t->sp_shrinks >= SP_SHRINKS || (uint64_t)z < 2 * zt + 4096) return GBPE_OK;
+    if (t->sp_shrinks >= SP_SHRINKS || (uint64_t)z < zt * t->shrink_pct / 100 + 4096) return GBPE_OK;
     S* zc = (S*)t->zbuf[t->zcur];
     S* zo = (S*)t->zbuf[t->zcur ^ 1];
     hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, (const S*)zc, (uint32_t)(z - zt), t->d_u32);
@@ -3407,7 +3420,9 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
         t->delta_tpw = v >= 32 ? 32 : v >= 16 ? 16 : 8;
     }
-    if (t->sp_zt < 5) t->sp_zt = 5;
+    if (const char* e = getenv("GBPE_SHRINK_PCT")) t->shrink_pct = std::max<uint32_t>(110, (uint32_t)strtoul(e, nullptr, 10));
+    if (const char* e = getenv("GBPE_ZONE_F")) t->zone_f = std::max<uint32_t>(3, (uint32_t)strtoul(e, nullptr, 10));
+    if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
         t->trace = fopen(e, "w");
         if (t->trace && (hipMalloc(&t->d_clog, (size_t)t->batch * 8) != hipSuccess ||
