@@ -470,7 +470,7 @@ def shard_of(data: bytes, rank: int, world: int) -> bytes:
 
 def run_sharded(args, lib, ctx, dist, rank, world, d, n, max_merges, table_log2):
     import torch
-    from gpubpe.sharded import GpuShardBackend, ShardedTrainer
+    from gpubpe.sharded import GpuShardBackend, GpuSingleBackend, ShardedTrainer
     be = GpuShardBackend(lib, ctx, d, None, rank, world, args.vocab, input_on_device=True, n=n,
                          table_log2=table_log2, cap_extra=max(TILE_SYMS, n // 4),
                          stream=torch.cuda.current_stream().cuda_stream)
@@ -490,11 +490,13 @@ def run_sharded(args, lib, ctx, dist, rank, world, d, n, max_merges, table_log2)
             tr.native = False
             be.comm = None
             _COMM["ok"] = False
-    merges, early = [], False
     needed = min(args.vocab - 256, max_merges)
-    while len(merges) < needed and not early:
-        got, early = tr.step(min(128, needed - len(merges)))
-        merges += got
+    below = args.consolidate_below if args.consolidate_below >= 0 else None
+    merges, early = tr.train(256 + needed, consolidate_below=below, root=0,
+                             make_single=lambda c, p, nid: GpuSingleBackend(lib, ctx, c, p, args.vocab, nid))
+    if tr.single is not None:
+        tr.single_stats = tr.single.stats()
+        tr.single.close()
     return be, tr, merges, early
 
 
@@ -546,6 +548,8 @@ def sharded_line(args, lib, ctx, dist, rank, world):
         "roofline": {"bound": "hbm", "kernel": "whole sharded loop (algorithmic stream bytes of all ranks / wall)",
                      "achieved": None, "peak": HBM_PEAK_GBPS * world, "unit": "GB/s", "frac": None, "traffic": None},
         "train_detail": {"stalls": tr.stalls if tr else 0, "record_caps": [tr.C, tr.Cw] if tr else None,
+                         "consolidate_below": args.consolidate_below if args.consolidate_below >= 0 else None,
+                         "consolidated_at_merge": tr.consolidated_at if tr else None,
                          "final_symbols_rank": int(st.symbol_count), "tail_dropped": int(st.tail_dropped),
                          "last_merge": merges[-1] if merges else []},
     }
@@ -680,6 +684,9 @@ def main():
     ap.add_argument("--no-c2", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP-event roofline run")
     ap.add_argument("--cpu-merges", type=int, default=0, help="CPU baseline merges on the CPU share (0 = 24)")
+    ap.add_argument("--consolidate-below", type=int, default=-1,
+                    help="--sharded: hand the run over to rank 0's GPU once the global stream is at most this many "
+                         "symbols (-1: never)")
     ap.add_argument("--sharded", action="store_true",
                     help="the per-merge sharded trainer (one RCCL all-gather per merge; also at N=1 as a rehearsal)")
     args = ap.parse_args()

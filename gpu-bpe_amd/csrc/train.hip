@@ -1234,6 +1234,15 @@ __global__ void k_export_symbols(const S* __restrict__ s, uint32_t* __restrict__
     out[i] = (x & Sym<S>::TM) | ((x & Sym<S>::WS) ? 0x10000u : 0u);
 }
 
+// the inverse: reference u32 layout (bit16 = word start) -> S (consolidation)
+template <typename S>
+__global__ void k_import_symbols(const uint32_t* __restrict__ in, S* __restrict__ s, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t x = in[i];
+    s[i] = (S)((x & Sym<S>::TM) | ((x & 0x10000u) ? Sym<S>::WS : 0u));
+}
+
 // ─── sector-sparse merge loop ──────────────────────────────────
 //
 // Late in training a merge's count is a tiny fraction of the stream, yet the
@@ -3384,8 +3393,16 @@ int sp_exit_any(gbpe_trainer* t) { return !t->sp ? GBPE_OK : (t->u16 ? sp_exit<u
 }  // namespace
 
 namespace {
+// a trainer continuing from an exported state (gbpe_trainer_create_from_state):
+// `bytes` is then the current u32 stream, `prev` the previous one
+struct StateInit {
+    const uint32_t* prev;
+    uint64_t n_prev;
+};
+
 int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
-                        int input_on_device, const gbpe_train_opts* opts, uint64_t cap_extra, gbpe_trainer** out) {
+                        int input_on_device, const gbpe_train_opts* opts, uint64_t cap_extra, gbpe_trainer** out,
+                        const StateInit* si = nullptr) {
     if (!ctx || !out || !opts) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
     *out = nullptr;
     if (n == 0) return gbpe_set_error(ctx, GBPE_E_EMPTY, "No symbols to train on — corpus is empty after pre-processing");
@@ -3486,9 +3503,56 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     DevState init{};
     init.n = (uint32_t)n;
     init.next_id = next_id;
+    if (si && si->n_prev > n) {   // the last merge's count (the zone rule's mc_prev)
+        init.mc = (uint32_t)(si->n_prev - n);
+        t->last_mc = init.mc;
+    }
     memcpy(t->h_st, &init, sizeof(init));
     if (hipMemcpyAsync(t->st, t->h_st, sizeof(DevState), hipMemcpyHostToDevice, s) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "state upload failed"));
+    auto finish = [&]() -> int {
+        if (t->flags & GBPE_TRAIN_TIMING) {
+            t->evs.resize(5 * t->batch);
+            for (auto& e : t->evs)
+                if (hipEventCreate(&e) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "hipEventCreate failed"));
+        }
+        if (hipStreamSynchronize(s) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "trainer init failed"));
+        *out = t;
+        return GBPE_OK;
+    };
+    if (si) {   // both ping-pong buffers from u32 streams (host or device resident)
+        const uint32_t* d_cur = (const uint32_t*)bytes;
+        const uint32_t* d_prev = si->prev;
+        void* tmp = nullptr;
+        if (!input_on_device) {
+            if (hipMalloc(&tmp, (n + si->n_prev) * 4 + 4) != hipSuccess)
+                return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(state) failed"));
+            uint32_t* h = (uint32_t*)tmp;
+            if (hipMemcpyAsync(h, bytes, n * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+                (si->n_prev && hipMemcpyAsync(h + n, si->prev, si->n_prev * 4, hipMemcpyHostToDevice, s) != hipSuccess)) {
+                hipFree(tmp);
+                return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "state upload failed"));
+            }
+            d_cur = h;
+            d_prev = h + n;
+        }
+        auto imp = [&](const uint32_t* src, void* dst, uint64_t cnt) {
+            if (!cnt) return;
+            const uint32_t g = (uint32_t)gbpe_div_up(cnt, TPB);
+            if (t->u16)
+                hipLaunchKernelGGL(k_import_symbols<uint16_t>, dim3(g), dim3(TPB), 0, s, src, (uint16_t*)dst, cnt);
+            else
+                hipLaunchKernelGGL(k_import_symbols<uint32_t>, dim3(g), dim3(TPB), 0, s, src, (uint32_t*)dst, cnt);
+        };
+        imp(d_cur, t->buf[0], n);
+        if (d_prev) imp(d_prev, t->buf[1], si->n_prev);
+        const bool launched = hipGetLastError() == hipSuccess;
+        int rc = launched ? table_rebuild(t) : gbpe_set_error(ctx, GBPE_E_DEVICE, "symbol import launch failed");
+        hipStreamSynchronize(s);
+        hipFree(tmp);
+        if (rc != GBPE_OK) return fail(rc);
+        return finish();
+    }
     // symbols: bytes (+ mask) → S with word-start bit; input may be host or device resident
     const uint8_t* d_bytes = bytes;
     const uint8_t* d_ws = word_starts;
@@ -3532,20 +3596,23 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         hipFree(d_gpt4);
     }
     if (rc != GBPE_OK) return fail(rc);
-    if (t->flags & GBPE_TRAIN_TIMING) {
-        t->evs.resize(5 * t->batch);
-        for (auto& e : t->evs)
-            if (hipEventCreate(&e) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "hipEventCreate failed"));
-    }
-    if (hipStreamSynchronize(s) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "trainer init failed"));
-    *out = t;
-    return GBPE_OK;
+    return finish();
 }
 }  // namespace
 
 extern "C" int gbpe_trainer_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
                                    int input_on_device, const gbpe_train_opts* opts, gbpe_trainer** out) {
     return trainer_create_impl(ctx, bytes, n, word_starts, input_on_device, opts, 0, out);
+}
+
+extern "C" int gbpe_trainer_create_from_state(gbpe_ctx* ctx, const uint32_t* cur, uint64_t n, const uint32_t* prev,
+                                              uint64_t n_prev, int input_on_device, const gbpe_train_opts* opts,
+                                              gbpe_trainer** out) {
+    if (n_prev < n) return gbpe_set_error(ctx, GBPE_E_INVALID, "create_from_state: n_prev (%llu) < n (%llu)",
+                                          (unsigned long long)n_prev, (unsigned long long)n);
+    if (n_prev > n && !prev) return gbpe_set_error(ctx, GBPE_E_INVALID, "create_from_state: prev is null");
+    const StateInit si{prev, n_prev};
+    return trainer_create_impl(ctx, (const uint8_t*)cur, n, nullptr, input_on_device, opts, n_prev - n, out, &si);
 }
 
 namespace {
@@ -3898,6 +3965,51 @@ extern "C" int gbpe_trainer_symbols(gbpe_trainer* t, uint32_t* out, uint64_t cap
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     hipFree(d);
     if (e != hipSuccess) return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "symbol export failed: %s", hipGetErrorString(e));
+    return GBPE_OK;
+}
+
+// current + previous stream (consolidation).  The previous stream
+// is the other ping-pong buffer over the previous length: a shard's pln, or
+// n + last count on one device (zeros before the first merge).
+extern "C" int gbpe_trainer_export_state(gbpe_trainer* t, uint32_t* cur, uint64_t cap_cur, uint64_t* n_cur,
+                                         uint32_t* prev, uint64_t cap_prev, uint64_t* n_prev, int on_device) {
+    if (!t || !n_cur || !n_prev) return GBPE_E_INVALID;
+    {
+        int rc = sp_exit_any(t);   // one dense stream (+ its stale buffer where the next window can read)
+        if (rc != GBPE_OK) return rc;
+    }
+    hipStream_t s = t->ctx->stream;
+    TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    const uint64_t n = t->n;
+    uint64_t np = t->sharded ? (uint64_t)t->h_st->pln : (t->done ? n + t->last_mc : n);
+    if (np > t->cap_syms) np = t->cap_syms;
+    *n_cur = n;
+    *n_prev = np;
+    if (!cur && !prev) return GBPE_OK;
+    if ((cur && cap_cur < n) || (prev && cap_prev < np))
+        return gbpe_set_error(t->ctx, GBPE_E_CAPACITY, "export_state: need %llu + %llu", (unsigned long long)n,
+                              (unsigned long long)np);
+    uint32_t* d = nullptr;
+    if (!on_device) TR_HIP(t, hipMalloc(&d, (n + np) * 4 + 4));
+    auto exp = [&](const void* src, uint32_t* dst, uint64_t cnt) {
+        if (!cnt || !dst) return;
+        const uint32_t g = (uint32_t)gbpe_div_up(cnt, 256);
+        if (t->u16)
+            hipLaunchKernelGGL(k_export_symbols<uint16_t>, dim3(g), dim3(256), 0, s, (const uint16_t*)src, dst, cnt);
+        else
+            hipLaunchKernelGGL(k_export_symbols<uint32_t>, dim3(g), dim3(256), 0, s, (const uint32_t*)src, dst, cnt);
+    };
+    exp(t->buf[t->cur], on_device ? cur : d, n);
+    exp(t->buf[t->cur ^ 1], on_device ? prev : d + n, np);
+    hipError_t e = hipGetLastError();
+    if (!on_device) {
+        if (e == hipSuccess && cur && n) e = hipMemcpyAsync(cur, d, n * 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && prev && np) e = hipMemcpyAsync(prev, d + n, np * 4, hipMemcpyDeviceToHost, s);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipFree(d);
+    if (e != hipSuccess) return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "state export failed: %s", hipGetErrorString(e));
     return GBPE_OK;
 }
 
@@ -4540,6 +4652,12 @@ extern "C" int gbpe_shard_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n
         *out = nullptr;
         return gbpe_set_error(ctx, GBPE_E_DEVICE, "shard init failed");
     }
+    return GBPE_OK;
+}
+
+extern "C" int gbpe_shard_global_len(gbpe_trainer* t, uint64_t* gn) {
+    if (!t || !gn || !t->sharded) return GBPE_E_INVALID;
+    *gn = t->h_st->gn;
     return GBPE_OK;
 }
 

@@ -121,6 +121,11 @@ _SIGS = [
     ("gbpe_comm_destroy", None, [C.c_void_p]),
     ("gbpe_shard_step_comm", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, u32p, u32p, u32p,
                                        u32p, u32p, u32p]),
+    ("gbpe_shard_global_len", C.c_int, [C.c_void_p, u64p]),
+    ("gbpe_trainer_export_state", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, u64p, C.c_void_p, C.c_uint64, u64p,
+                                            C.c_int]),
+    ("gbpe_trainer_create_from_state", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int,
+                                                 C.POINTER(TrainOpts), C.POINTER(C.c_void_p)]),
 ]
 
 EXPORTED = [s[0] for s in _SIGS]

@@ -27,6 +27,15 @@ rank (its selection is undone), the step ends early, and the host grows the
 capacity from the needs recorded in the gathered headers and continues — the
 merge list is unaffected.
 
+Consolidation (``train(..., consolidate_below=N)``): once the global stream is
+at most N symbols, merges are latency-bound and the per-merge exchange costs
+more than the merge.  The ranks then export their current and previous local
+streams, ``root`` gathers them (concatenated in rank order they ARE the global
+streams, the previous one included, so the compaction quirk's stale window
+reads the same symbols), continues on one device (``GpuSingleBackend``:
+gbpe_trainer_create_from_state, the single-GPU loop with its lexicon / sparse
+policy), and broadcasts the merge list at the end.
+
 The backend is the C-ABI trainer (``GpuShardBackend``); tests drive the same
 orchestration with a numpy model of one rank over gloo.
 """
@@ -172,11 +181,19 @@ class ShardedTrainer:
             self.Cw = min(self.Cw, _pow2_at_least(2 * res["need_win"], self.min_win))
         return res["merges"], res["early_stop"]
 
-    def train(self, target_vocab_size: int, vocab_size: int = 256, batch: int = BATCH_SIZE, on_progress=None):
+    def train(self, target_vocab_size: int, vocab_size: int = 256, batch: int = BATCH_SIZE, on_progress=None,
+              consolidate_below: int | None = None, make_single=None, root: int = 0):
+        """Merges until the target (every rank returns the same list).  With
+        ``consolidate_below`` the run moves to ``root`` once the global stream is
+        at most that many symbols: ``make_single(cur, prev, next_id)`` builds the
+        single-device backend there (``step(k) -> (merges, early_stop)``)."""
         needed = target_vocab_size - vocab_size
         merges = []
         early = False
+        self.consolidated_at = None
         while len(merges) < needed:
+            if consolidate_below is not None and self.b.global_len() <= consolidate_below:
+                return self._finish_on_one(merges, needed, vocab_size, batch, on_progress, make_single, root)
             got, early = self.step(min(batch, needed - len(merges)))
             merges += got
             if on_progress:
@@ -184,6 +201,81 @@ class ShardedTrainer:
             if early:
                 break
         return merges, early
+
+    # ── consolidation ──
+    def _bcast_ints(self, vals, root):
+        """int64 list from root to every rank (length first)."""
+        torch = self.torch
+        dev = "cpu" if self.staged else self.device
+        n = torch.tensor([len(vals) if self.rank == root else 0], dtype=torch.int64, device=dev)
+        self.dist.broadcast(n, src=root)
+        buf = torch.zeros(max(1, int(n.item())), dtype=torch.int64, device=dev)
+        if self.rank == root and vals:
+            buf[: len(vals)] = torch.tensor(vals, dtype=torch.int64)
+        self.dist.broadcast(buf, src=root)
+        return buf[: int(n.item())].cpu().tolist()
+
+    def consolidate(self, make_single, next_id: int, root: int = 0):
+        """Gather the global (current, previous) streams onto ``root`` and return
+        ``make_single(cur, prev, next_id)`` there, None on the other ranks."""
+        torch = self.torch
+        dev = "cpu" if self.staged else self.device
+        on_dev = getattr(self.b, "device_state", False) and dev != "cpu"
+        if on_dev:   # HBM to HBM: export into the send buffer, gather over RCCL, concatenate on the device
+            n, npv = self.b.state_lens()
+            lens = self._gather_ints([n, npv])
+            cap = max(1, int(lens.max()))
+            send = torch.zeros(2 * cap, dtype=torch.int32, device=dev)
+            self.b.export_state_device(send.data_ptr(), send.data_ptr() + 4 * cap, cap, cap)
+        else:
+            cur, prev = self.b.export_state()
+            lens = self._gather_ints([int(cur.shape[0]), int(prev.shape[0])])
+            cap = max(1, int(lens.max()))
+            send = torch.zeros(2 * cap, dtype=torch.int32, device=dev)
+            if cur.shape[0]:
+                send[: cur.shape[0]] = torch.from_numpy(cur.view(np.int32)).to(dev)
+            if prev.shape[0]:
+                send[cap: cap + prev.shape[0]] = torch.from_numpy(prev.view(np.int32)).to(dev)
+        if self.world == 1:
+            parts = [send]
+        else:
+            parts = [torch.empty_like(send) for _ in range(self.world)] if self.rank == root else None
+            self.dist.gather(send, parts, dst=root)
+        if self.rank != root:
+            return None
+        if on_dev:
+            gcur = torch.cat([parts[q][: lens[q, 0]] for q in range(self.world)])
+            gprev = torch.cat([parts[q][cap: cap + lens[q, 1]] for q in range(self.world)])
+            del parts, send
+            return make_single(gcur, gprev, next_id)
+        host = [p.cpu().numpy().view(np.uint32) for p in parts]
+        gcur = np.concatenate([host[q][: lens[q, 0]] for q in range(self.world)])
+        gprev = np.concatenate([host[q][cap: cap + lens[q, 1]] for q in range(self.world)])
+        return make_single(gcur, gprev, next_id)
+
+    def _finish_on_one(self, merges, needed, vocab_size, batch, on_progress, make_single, root):
+        self.consolidated_at = len(merges)
+        single = self.consolidate(make_single, vocab_size + len(merges), root)
+        early = False
+        flat = []
+        if self.rank == root:
+            try:
+                while len(merges) < needed:
+                    got, early = single.step(min(batch, needed - len(merges)))
+                    merges = merges + [list(m) for m in got]
+                    if on_progress:
+                        on_progress(len(merges), needed, got)
+                    if early or not got:
+                        break
+            finally:
+                self.single = single
+            flat = [1 if early else 0] + [int(x) for m in merges for x in m]
+        flat = self._bcast_ints(flat, root)
+        early = bool(flat[0])
+        merges = [flat[1 + 4 * i: 5 + 4 * i] for i in range((len(flat) - 1) // 4)]
+        return merges, early
+
+    single = None
 
 
 class GpuShardBackend:
@@ -221,6 +313,22 @@ class GpuShardBackend:
         n = C.c_uint64()
         self._lib.check(self.lib.gbpe_shard_local_len(self.t, C.byref(n)), self.ctx, "local_len")
         return int(n.value)
+
+    def global_len(self) -> int:
+        n = C.c_uint64()
+        self._lib.check(self.lib.gbpe_shard_global_len(self.t, C.byref(n)), self.ctx, "global_len")
+        return int(n.value)
+
+    def export_state(self):
+        return export_state(self.lib, self.ctx, self.t)
+
+    device_state = True   # the hand-over can stay in HBM (RCCL gather of device buffers)
+
+    def state_lens(self):
+        return state_lens(self.lib, self.ctx, self.t)
+
+    def export_state_device(self, cur_ptr, prev_ptr, cap_cur, cap_prev):
+        return export_state_device(self.lib, self.ctx, self.t, cur_ptr, prev_ptr, cap_cur, cap_prev)
 
     def set_layout(self, lens):
         arr = (C.c_uint64 * len(lens))(*lens)
@@ -305,3 +413,84 @@ class GpuShardBackend:
         if self.comm and self.owns_comm:
             self.lib.gbpe_comm_destroy(self.comm)
         self.comm = None
+
+
+def state_lens(lib, ctx, t):
+    """(current, previous) stream lengths of a trainer (gbpe_trainer_export_state, no copy)."""
+    from . import _lib
+    n, npv = C.c_uint64(), C.c_uint64()
+    _lib.check(lib.gbpe_trainer_export_state(t, None, 0, C.byref(n), None, 0, C.byref(npv), 0), ctx, "export_state")
+    return int(n.value), int(npv.value)
+
+
+def export_state(lib, ctx, t):
+    """(current, previous) stream of a trainer as host u32 arrays."""
+    from . import _lib
+    n, npv = state_lens(lib, ctx, t)
+    cur = np.zeros(max(1, n), np.uint32)
+    prev = np.zeros(max(1, npv), np.uint32)
+    a, b = C.c_uint64(), C.c_uint64()
+    _lib.check(lib.gbpe_trainer_export_state(t, cur.ctypes.data_as(C.c_void_p), n, C.byref(a),
+                                             prev.ctypes.data_as(C.c_void_p), npv, C.byref(b), 0),
+               ctx, "export_state")
+    return cur[:n], prev[:npv]
+
+
+def export_state_device(lib, ctx, t, cur_ptr: int, prev_ptr: int, cap_cur: int, cap_prev: int):
+    """The same into device buffers (HBM to HBM)."""
+    from . import _lib
+    a, b = C.c_uint64(), C.c_uint64()
+    _lib.check(lib.gbpe_trainer_export_state(t, C.c_void_p(cur_ptr), cap_cur, C.byref(a), C.c_void_p(prev_ptr),
+                                             cap_prev, C.byref(b), 1), ctx, "export_state")
+    return int(a.value), int(b.value)
+
+
+class GpuSingleBackend:
+    """The consolidated run: one device's trainer continuing from a gathered
+    state (gbpe_trainer_create_from_state) with the single-GPU policy."""
+
+    def __init__(self, lib, ctx, cur, prev, target_vocab: int, next_id: int, exact: bool = False, flags: int = 0,
+                 table_log2: int = 0, batch: int = BATCH_SIZE):
+        from . import _lib
+        self.lib, self.ctx, self._lib = lib, ctx, _lib
+        flags |= _lib.GBPE_TRAIN_EXACT_COMPACTION if exact else 0
+        self.opts = _lib.TrainOpts(target_vocab_size=target_vocab, vocab_size=next_id, next_token_id=next_id,
+                                   batch_size=batch, flags=flags, table_log2=table_log2)
+        t = C.c_void_p()
+        if hasattr(cur, "data_ptr"):   # torch tensors (int32 / uint32 view) already in HBM
+            cur, prev = cur.contiguous(), prev.contiguous()
+            assert cur.is_cuda and prev.is_cuda and cur.element_size() == 4 and prev.element_size() == 4
+            args = (C.c_void_p(cur.data_ptr()), cur.numel(), C.c_void_p(prev.data_ptr()), prev.numel(), 1)
+        else:
+            cur = np.ascontiguousarray(cur, dtype=np.uint32)
+            prev = np.ascontiguousarray(prev, dtype=np.uint32)
+            args = (cur.ctypes.data_as(C.c_void_p), cur.shape[0], prev.ctypes.data_as(C.c_void_p), prev.shape[0], 0)
+        _lib.check(lib.gbpe_trainer_create_from_state(ctx, *args, C.byref(self.opts), C.byref(t)), ctx,
+                   "create_from_state")
+        self.t = t
+        self.batch = batch
+        self._out = (C.c_uint32 * (4 * batch))()
+
+    def step(self, max_merges):
+        nd, es = C.c_uint32(), C.c_uint32()
+        self._lib.check(self.lib.gbpe_trainer_step(self.t, min(max_merges, self.batch), self._out, C.byref(nd),
+                                                   C.byref(es)), self.ctx, "single step")
+        return [list(self._out[4 * i: 4 * i + 4]) for i in range(nd.value)], bool(es.value)
+
+    def symbols(self):
+        n = C.c_uint64()
+        self._lib.check(self.lib.gbpe_trainer_symbols(self.t, None, 0, C.byref(n)), self.ctx, "symbols")
+        out = np.zeros(max(1, n.value), np.uint32)
+        self._lib.check(self.lib.gbpe_trainer_symbols(self.t, out.ctypes.data_as(C.POINTER(C.c_uint32)), n.value,
+                                                      C.byref(n)), self.ctx, "symbols")
+        return out[: n.value]
+
+    def stats(self):
+        st = self._lib.TrainerStats()
+        self.lib.gbpe_trainer_stats_get(self.t, C.byref(st))
+        return st
+
+    def close(self):
+        if self.t:
+            self.lib.gbpe_trainer_destroy(self.t)
+            self.t = None

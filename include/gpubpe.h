@@ -233,6 +233,28 @@ void gbpe_comm_destroy(gbpe_comm* comm);
 int  gbpe_shard_step_comm(gbpe_trainer* t, gbpe_comm* comm, uint32_t max_merges, uint32_t cap_list, uint32_t cap_win,
                           uint32_t* merges_out, uint32_t* n_done, uint32_t* early_stop, uint32_t* stalled,
                           uint32_t* need_list, uint32_t* need_win);
+/* Global stream length after the last step (every rank agrees). */
+int  gbpe_shard_global_len(gbpe_trainer* t, uint64_t* gn);
+
+/* ── consolidation: a run continues on another trainer ──────────────────────
+ * Late merges touch a few hundred symbols each; a per-merge exchange then costs
+ * more than the merge, so the sharded run hands its state to ONE device.  The
+ * state of a trainer is its current stream and its previous stream (the
+ * ping-pong buffer the compaction quirk reads stale symbols from,
+ * train.wgsl:605-607 + 698/727), both in the reference u32 layout (bit16 =
+ * word start).  For a sharded run the global streams are the rank pieces
+ * concatenated in rank order.  cur/prev NULL = lengths only; on_device != 0:
+ * cur/prev are device pointers (the hand-over then never leaves HBM). */
+int gbpe_trainer_export_state(gbpe_trainer* t, uint32_t* cur, uint64_t cap_cur, uint64_t* n_cur,
+                              uint32_t* prev, uint64_t cap_prev, uint64_t* n_prev, int on_device);
+/* A single-device trainer continuing from an exported state: opts as for
+ * gbpe_trainer_create with vocab_size / next_token_id of the run so far (the
+ * merges still to do are target_vocab_size - vocab_size); pair counts are
+ * recounted from `cur`.  n_prev >= n (n_prev - n is the last merge's count;
+ * n_prev == n for a run with no merges yet, whose prev is all zero). */
+int gbpe_trainer_create_from_state(gbpe_ctx* ctx, const uint32_t* cur, uint64_t n, const uint32_t* prev,
+                                   uint64_t n_prev, int input_on_device, const gbpe_train_opts* opts,
+                                   gbpe_trainer** out);
 
 /* ── trie encode (replaces tokenizer.js:54-335 TrieTokenizer over the
  *    tokenize.wgsl kernels) ─────────────────────────────────────────────── */

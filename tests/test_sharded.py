@@ -54,7 +54,7 @@ def cut_at_word_starts(data: bytes, fracs):
 def _worker(rank, world, port, case, outdir):
     import torch.distributed as dist
     from gpubpe.sharded import ShardedTrainer
-    from shard_model import ModelShardBackend
+    from shard_model import ModelShardBackend, OracleSingle
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -65,11 +65,21 @@ def _worker(rank, world, port, case, outdir):
         be = ModelShardBackend(d, ws, rank, world, case["vocab"], exact=case["exact"])
         tr = ShardedTrainer(be, dist, cap_list=case["cap"], cap_win=case["cap"])
         tr.setup()
-        merges, early = tr.train(case["vocab"], batch=case.get("batch", 128))
-        sym = be.symbols()
+        cb = case.get("consolidate")
+        below = None if cb is None else int(cb * len(data))
+        merges, early = tr.train(case["vocab"], batch=case.get("batch", 128), consolidate_below=below,
+                                 make_single=lambda c, p, nid: OracleSingle(c, p, nid, case["exact"]),
+                                 root=case.get("root", 0))
+        if tr.single is not None:   # the root holds the whole stream; the others none
+            sym = tr.single.symbols()
+        elif tr.consolidated_at is not None:
+            sym = np.zeros(0, np.uint32)
+        else:
+            sym = be.symbols()
         np.save(os.path.join(outdir, f"sym{rank}.npy"), sym)
         with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
-            json.dump({"merges": merges, "early": early, "stalls": tr.stalls, "events": be.events}, f)
+            json.dump({"merges": merges, "early": early, "stalls": tr.stalls, "events": be.events,
+                       "consolidated_at": tr.consolidated_at}, f)
     finally:
         dist.destroy_process_group()
 
@@ -96,6 +106,15 @@ CASES = [
     ("ref_w3_tiny_tail", 3, dict(bytes=20_000, seed=13, fracs=[0.945, 0.965], vocab=480, exact=False, cap=1 << 14)),
     # tiny capacities: every early merge stalls and the host grows C/Cw
     ("ref_w2_stalls", 2, dict(bytes=16_000, seed=14, fracs=[0.6], vocab=420, exact=False, cap=8, batch=32)),
+    # consolidation onto one rank once the global stream is <= a fraction of the
+    # corpus: the merge list and the final stream are unchanged
+    ("ref_w2_consolidate", 2, dict(bytes=24_000, seed=11, fracs=[0.5], vocab=520, exact=False, cap=1 << 14,
+                                   batch=32, consolidate=0.8)),
+    ("exact_w2_consolidate", 2, dict(bytes=24_000, seed=12, fracs=[0.5], vocab=520, exact=True, cap=1 << 14,
+                                     batch=32, consolidate=0.8)),
+    # windows spanning ranks right before the hand-over; root is the last rank
+    ("ref_w3_tiny_tail_consolidate", 3, dict(bytes=20_000, seed=13, fracs=[0.945, 0.965], vocab=480, exact=False,
+                                             cap=1 << 14, batch=16, consolidate=0.75, root=2)),
 ]
 
 
@@ -107,6 +126,9 @@ def test_sharded_matches_single_stream(name, world, case):
         assert res[r]["merges"] == exp["merges"], f"rank {r} merge list differs"
         assert res[r]["early"] == exp["early_stop"]
     np.testing.assert_array_equal(np.concatenate(syms), exp["symbols"])
+    if case.get("consolidate"):
+        at = res[0]["consolidated_at"]
+        assert at is not None and 0 < at < len(exp["merges"]), at
     if name.endswith("stalls"):
         assert res[0]["stalls"] > 0
     if name.endswith("tiny_tail"):
