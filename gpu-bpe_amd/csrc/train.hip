@@ -1600,7 +1600,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
 }
 
 // Selection inside k_body (sector-sparse loop): every workgroup reduces the
-// k_refresh partial maxima itself and gets the same merge; workgroup 0 commits
+// k_refresh partial maxima itself and gets the same merge; the last one commits
 // it (log, table slot zeroed, state for k_refresh and the zone kernels).  The
 // step counters move on in k_refresh (finish == 2), so nothing a workgroup reads
 // here changes under it.  Saves the k_select launch per merge.
@@ -1667,7 +1667,9 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     const uint32_t need = 6u * mc + 64u;   // distinct deltas of one merge <= 4 per site + tail + window
     const bool stall = !stop && !bad && !abort && sh.cap_list && need > sh.cap_list;
     const bool go = !stop && !bad && !abort && !stall;
-    if (blockIdx.x == 0) {
+    // the LAST workgroup commits: block 0 is the zone pass (the launch's longest
+    // chain), which then starts without the table probe and the state stores
+    if (blockIdx.x == gridDim.x - 1u) {
         if (t == 0) {
             if (stop) {
                 st->stop = 1u;
