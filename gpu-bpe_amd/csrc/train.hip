@@ -106,6 +106,16 @@ struct DevState {
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
+// the zone segments' per-merge hand-off (zone_seg; k_refresh zeroes it)
+constexpr uint32_t NSEG_MAX = 32;
+constexpr uint32_t ZSEG_SPIN = 1u << 22;
+struct ZSegState {
+    uint32_t ticket;
+    uint32_t pad[15];
+    unsigned long long gran[NSEG_MAX][4];   // {1, kept}, {1, tail survivors}, {1, last kept | has kept << 31}
+};
+constexpr uint32_t ZSEG_WORDS = 16 + NSEG_MAX * 8;   // u32 words k_refresh zeroes (ticket, granules)
+
 // Phase timestamps of the sector-sparse kernels (diagnostic builds only:
 // -DGBPE_KTRACE; tools/ktrace.sh).  Every KT_EVERY-th merge, each workgroup
 // stores its own wall-clock stamps (plain stores, no shared counters that
@@ -396,8 +406,11 @@ template <typename S>
 __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, int finish, Table tb, S* __restrict__ cur,
                                                  const uint32_t* __restrict__ rwlist, DevState* zst,
                                                  uint32_t* __restrict__ clog = nullptr, FusedSel fs = FusedSel(),
-                                                 uint64_t* __restrict__ part = nullptr) {
+                                                 uint64_t* __restrict__ part = nullptr, uint32_t* __restrict__ zseg = nullptr) {
     (void)cur;
+    if (zseg && blockIdx.x == 0)   // ZSegState: ticket + granules of the next merge's zone segments
+        for (uint32_t i = threadIdx.x; i < ZSEG_WORDS; i += TPB)
+            if (i == 0 || i >= 16) zseg[i] = 0u;
     (void)rwlist;
     if (part && finish == 2 && threadIdx.x == 0) KTR(0);
     // finish == 2: the sector-sparse loop, whose merge was selected inside k_body
@@ -1599,6 +1612,273 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
     }
 }
 
+// ── segmented zone pass (zones of 16K-512K symbols) ──
+// A zone too large for one workgroup but far smaller than the stream (merges
+// ~500-8000 at 1 GiB) is cut into segments of BT x ZPT = 16K symbols, one
+// 1024-thread workgroup each (blocks [0, nz) of k_body).  Two phases:
+//  A (no waiting): a segment runs zone_one's site deltas and local compaction
+//    on its range (neighbour symbols before / after it come from the current
+//    zone buffer, where their owners may already have rewritten them in place:
+//    token nw reads back as a, since nw exists nowhere else before this merge),
+//    and takes an even share of the two mc-long per-merge chores: the stale
+//    tail's destroyed pairs ([z - mc, z), read the same way) and the stale-window
+//    SOURCE ([n - 2mc - Bp, + mc) of the other buffer) copied into LDS.  It
+//    publishes (kept, tail survivors, last kept symbol) as three 8-byte
+//    {tag, value} granules (relaxed agent-scope stores: the data is the flag)
+//    after every wave drained its loads.
+//  B: one wave sweeps all nz segments' granules; then the segment stores its
+//    kept symbols at its prefix and the part of the window (the last m source
+//    symbols, m = all tail survivors) in its share after the Kz kept ones.  Every
+//    read of the other buffer (the window source) happened in phase A, before
+//    any segment passes phase B's sweep, so no store overwrites an unread source.
+//  Every zone workgroup waits only on zone workgroups, which never wait on body
+//  workgroups: with nz <= 32 workgroups they all become resident.
+// k_refresh zeroes the granules for the next merge (tag = 1).
+template <typename S, bool EXACT, int BT, int NT, int ZPT>
+__device__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
+                         S* __restrict__ zo, ZSegState* zg, uint32_t nz, ZoneLds<S, BT>& L, LdsTab<NT>& lt,
+                         const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
+                         uint64_t* __restrict__ bytes, uint32_t round) {
+    (void)round;
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    constexpr uint32_t SEG = (uint32_t)BT * ZPT;
+    constexpr int V = ZPT * sizeof(S) / 16;
+    static_assert(ZPT <= ZoneDim<S, BT>::ZPT && ZPT * sizeof(S) % 16 == 0, "segment positions per thread");
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    __shared__ uint32_t s_h[3], s_last, s_pre, s_kz, s_m, s_x0;
+    const uint32_t seg = blockIdx.x;
+    const uint32_t z = zs.n;
+    const uint32_t lim = EXACT ? z : z - mc;
+    const uint32_t g0 = seg * SEG;
+    const uint32_t nh = g0 < z ? (z - g0 < SEG ? z - g0 : SEG) : 0u;   // positions of this segment (0: past the end)
+    const uint32_t pid_ab = (a << 16) | b;
+    auto unrw = [&](uint32_t v) -> uint32_t { return (v & TM) == nw ? (a | (v & WS)) : v; };
+    auto zload = [&](uint32_t p) -> uint32_t { return unrw((uint32_t)((const volatile S*)zc)[p]); };   // old or rewritten
+    const uint32_t i0 = (uint32_t)t * ZPT;   // local
+    S* xs = reinterpret_cast<S*>(L.xv);
+    uint32_t x[ZPT];
+    {
+        uint4 v[V];
+        const uint4* src = reinterpret_cast<const uint4*>(zc + g0 + i0);
+        const bool any = i0 < nh;
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = any ? src[k] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int k = 0; k < V; ++k) L.xv[t * V + k] = v[k];
+        const S* e = reinterpret_cast<const S*>(v);
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < nh ? (uint32_t)e[k] : 0u;
+    }
+    if (t < 3) {   // neighbours g0 - 2, g0 - 1, g0 + nh
+        const uint32_t p = t < 2 ? g0 - 2u + (uint32_t)t : g0 + nh;
+        const bool ok = nh && (t < 2 ? g0 >= 2u - (uint32_t)t : g0 + nh < z);
+        s_h[t] = ok ? zload(p) : 0u;
+    }
+    // this segment's share of the window source (+ the symbol before it) into LDS
+    const uint32_t lw = (mc + nz - 1) / nz, q0 = seg * lw, q1 = q0 + lw < mc ? q0 + lw : mc;   // source [q0, q1)
+    const uint64_t src0 = (uint64_t)gs.n + gs.off - gs.poff - 2ull * mc - gs.Bp;
+    if (!EXACT && q0 < q1) {
+        const uint32_t f = q0 ? q0 - 1u : 0u;   // L.wb[j] = source[f + j]
+        for (uint32_t q = f + t; q < q1; q += BT) L.wb[q - f] = zo[src0 + q];
+    }
+    lds_clear(lt);
+    __syncthreads();
+    if (t == 0) KT(2);
+    auto X = [&](int j) -> uint32_t {   // local position j in [-2, SEG]
+        return j < 0 ? s_h[j + 2] : (uint32_t)j < nh ? (uint32_t)xs[j] : ((uint32_t)j == nh ? s_h[2] : 0u);
+    };
+    if (!EXACT) {   // this segment's share of the stale tail: old pairs destroyed
+        const uint32_t lo = lim > 1u ? lim : 1u;
+        const uint32_t nt_ = z > lo ? z - lo : 0u, lt_ = (nt_ + nz - 1) / nz;
+        const uint32_t p0 = lo + seg * lt_, p1 = p0 + lt_ < z ? p0 + lt_ : z;
+        for (uint32_t i = p0 + t; i < p1; i += BT) {
+            const uint32_t xi = zload(i);
+            if (xi & WS) continue;
+            const uint32_t tp = zload(i - 1) & TM, ti = xi & TM;
+            if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        }
+    }
+    const uint32_t xm2 = X((int)i0 - 2), xm1 = X((int)i0 - 1), nxr = X((int)(i0 + ZPT));
+    uint32_t eb = 0, ea = 0;
+#pragma unroll
+    for (int k = 0; k < ZPT; ++k) {
+        eb |= (x[k] == b ? 1u : 0u) << k;
+        ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
+    }
+    const uint32_t gi0 = g0 + i0;
+    const uint32_t inb = lane_mask_n(i0, nh, ZPT);
+    const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;
+    const uint32_t h_m1 = (gi0 >= 1 && i0 <= nh && xm1 == b && (xm2 & TM) == a) ? 1u : 0u;
+    const uint32_t h_32 = (nxr == b && (ea >> (ZPT - 1))) ? 1u : 0u;
+    const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (ZPT + 1));
+    const uint32_t below = lane_mask_n(gi0, lim, ZPT);
+    const uint32_t surv = inb & ~hitm, keep = surv & below;
+    const uint32_t rwm = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
+    uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+    while (rel) {
+        const int k = __ffs(rel) - 1;
+        rel &= rel - 1;
+        const uint32_t i = i0 + k;
+        if (g0 + i == 0) continue;
+        const uint32_t xi = X((int)i);
+        if (xi & WS) continue;
+        const uint32_t xp = X((int)i - 1);
+        const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+        const uint32_t tp = xp & TM, ti = xi & TM;
+        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        if (!h0) {
+            if (hm) {
+                const uint32_t t2 = hp ? nw : ti;
+                if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+            } else if (hp && tp) {
+                lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+            }
+        }
+    }
+    if (t == 0) KT(3);
+    // local exclusive scan of the kept counts; tail survivors; the last kept symbol
+    const uint32_t kc = __popc(keep);
+    uint32_t incl = kc, tl = __popc(surv & ~below);
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    for (int off = 32; off > 0; off >>= 1) tl += __shfl_xor(tl, off);
+    if (lane == 63) L.wsum[wid] = incl;
+    if (lane == 0) L.wtail[wid] = tl;
+    __syncthreads();
+    uint32_t pre = incl - kc, Ks = 0, Ts = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < BT / 64; ++w2) {
+        pre += w2 < wid ? L.wsum[w2] : 0u;
+        Ks += L.wsum[w2];
+        Ts += L.wtail[w2];
+    }
+    if (kc && pre + kc == Ks) {   // this thread holds the segment's last kept symbol
+        const int hk = 31 - __clz(keep);
+        uint32_t xv = x[0];
+#pragma unroll
+        for (int k = 1; k < ZPT; ++k) xv = k == hk ? x[k] : xv;
+        s_last = ((rwm >> hk) & 1u) ? (nw | (xv & WS)) : xv;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's reads of the other buffer are done
+    __syncthreads();
+    if (t == 0) {
+        constexpr unsigned long long TAG = 1ull << 32;
+        __hip_atomic_store(&zg->gran[seg][0], TAG | Ks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&zg->gran[seg][1], TAG | Ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&zg->gran[seg][2], TAG | (Ks ? (s_last | 0x80000000u) : 0u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        KT(7);
+    }
+    // the new segment assembled in LDS over the old copy (swizzled as in zone_one)
+    constexpr uint32_t PV = 16 / sizeof(S), PVL = sizeof(S) == 2 ? 3 : 2;
+    auto swz = [](uint32_t o) -> uint32_t {
+        const uint32_t c = o >> PVL;
+        return ((c ^ ((c >> 3) & 7u)) << PVL) | (o & (PV - 1u));
+    };
+    uint32_t wsm = 0;
+#pragma unroll
+    for (int k = 0; k < ZPT; ++k) {
+        const bool rw = (rwm >> k) & 1u;
+        const uint32_t v = rw ? (nw | (x[k] & WS)) : x[k];
+        wsm |= ((x[k] & WS) ? 1u : 0u) << k;
+        const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
+        S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
+        *dst = (S)v;
+    }
+    for (uint32_t r = rwm; r; r &= r - 1) {
+        const int k = __ffs(r) - 1;
+        zc[gi0 + k] = (S)(nw | (((wsm >> k) & 1u) ? WS : 0u));
+    }
+    // B: every segment's granules (one wave, relaxed sweeps, s_sleep between)
+    if (wid == 0) {
+        uint32_t gk = 0, gt = 0, gl = 0;
+        for (uint32_t it = 0;; ++it) {
+            bool ok = true;
+            if ((uint32_t)lane < nz) {
+                const unsigned long long x0 = __hip_atomic_load(&zg->gran[lane][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long x1 = __hip_atomic_load(&zg->gran[lane][1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long x2 = __hip_atomic_load(&zg->gran[lane][2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = (x0 >> 32) == 1u && (x1 >> 32) == 1u && (x2 >> 32) == 1u;
+                gk = (uint32_t)x0;
+                gt = (uint32_t)x1;
+                gl = (uint32_t)x2;
+            }
+            if (__all(ok)) break;
+            if (it > ZSEG_SPIN) {
+                if (lane == 0) atomicOr(&st->err, ERR_SPIN);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const bool in = (uint32_t)lane < nz;
+        uint32_t sp = in && (uint32_t)lane < seg ? gk : 0u, sk = in ? gk : 0u, stt = in ? gt : 0u;
+        for (int off = 32; off > 0; off >>= 1) {
+            sp += __shfl_xor(sp, off);
+            sk += __shfl_xor(sk, off);
+            stt += __shfl_xor(stt, off);
+        }
+        const unsigned long long hm = __ballot(in && (gl >> 31));
+        if (lane == 0) {
+            s_pre = sp;
+            s_kz = sk;
+            s_m = EXACT ? 0u : stt;
+            s_x0 = 0u;
+        }
+        if (hm && lane == 63 - __clzll(hm)) s_x0 = gl & 0x7FFFFFFFu;   // the last kept survivor overall
+    }
+    __syncthreads();
+    if (t == 0) KT(8);
+    const uint32_t P = s_pre, Kz = s_kz, m = s_m;
+    for (uint32_t j = t; j < Ks; j += BT) zo[P + j] = xs[swz(j)];
+    if (!EXACT && m) {   // the window = source [mc - m, mc) after the Kz kept symbols; this segment's share
+        const uint32_t w0 = mc - m, f = q0 ? q0 - 1u : 0u;
+        const uint32_t lo = q0 > w0 ? q0 : w0;
+        for (uint32_t q = lo + t; q < q1; q += BT) {
+            const uint32_t x1 = L.wb[q - f];
+            const uint32_t x0 = q == w0 ? s_x0 : (uint32_t)L.wb[q - 1u - f];
+            zo[Kz + (q - w0)] = (S)x1;
+            if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) lds_add(lt, tb, st, ((x0 & TM) << 16) | (x1 & TM), 1u);
+        }
+    }
+    if (t == 0) KT(9);
+    lds_flush(lt, tb, st);
+    if (t == 0) {
+        KT(4);
+        if (seg == 0) {
+            zst->m = m;
+            zst->valid_total = Kz + m + 1u;
+        }
+        const uint32_t ws = q1 > q0 ? q1 - q0 : 0u;
+        atomicAdd(bytes, (uint64_t)sizeof(S) * ((uint64_t)nh + Ks + 2u * ws + (EXACT ? 0u : mc / nz)));
+    }
+}
+
+// The segmented zone pass as its own launch after k_body (whose last workgroup
+// committed the merge): 1024 threads, nz workgroups.  (Inside k_body its
+// registers pushed every k_body form into scratch: 1 GiB 0.88 -> 0.98 s.)
+template <typename S, bool EXACT>
+__global__ __launch_bounds__(1024) void k_zseg(DevState* st, DevState* zst, uint32_t round, S* __restrict__ zc,
+                                               S* __restrict__ zo, ZSegState* __restrict__ zg, uint32_t nz, Table tb,
+                                               uint64_t* __restrict__ bytes) {
+    constexpr int NW = sizeof(DevState) / 4;
+    __shared__ union {
+        DevState d;
+        uint32_t w[NW];
+    } s_g, s_z;
+    __shared__ LdsTab<4096> lt;
+    __shared__ ZoneLds<S, 1024> L;
+    const int t = threadIdx.x;
+    if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
+    else if (t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
+    __syncthreads();
+    const DevState& g = s_g.d;
+    if (g.stop || g.sp_abort || g.sel_round != round + 1u) return;   // this round did not merge
+    zone_seg<S, EXACT, 1024, 4096, 16>(st, zst, g, s_z.d, zc, zo, zg, nz, L, lt, tb, g.a, g.b, g.nw, g.mc, bytes, round);
+    if (t == 0) KTV(6, 2);
+}
+
 // Selection inside k_body (sector-sparse loop): every workgroup reduces the
 // k_refresh partial maxima itself and gets the same merge; the last one commits
 // it (log, table slot zeroed, state for k_refresh and the zone kernels).  The
@@ -1760,7 +2040,8 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
                                               Table dtb, SelShard sh, uint32_t* __restrict__ lmul) {
-    __shared__ LdsTab<LTAB_T> lt;
+    constexpr int KB_LT = LTAB_T;
+    __shared__ LdsTab<KB_LT> lt;
     __shared__ BodyLds<S, BT> u;
     __shared__ uint32_t s_ntok, s_n, s_any, s_rm[BT / 64];
     __shared__ uint64_t s_mv[BT / 64];
@@ -1771,12 +2052,12 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     const DevState *gs, *zs;   // this workgroup's snapshots of the states at launch (LDS)
     if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh)) return;
     if (t == 0) KT(1);
-    // the zone workgroup is dispatched first (block 0): it is the longest single
-    // chain of the merge, and later blocks of a large grid start later
-    const uint32_t bid = zone1 ? (blockIdx.x == 0 ? nbody : blockIdx.x - 1u) : blockIdx.x;
+    // the zone workgroup is dispatched first (block 0 when zone1): it is the longest
+    // single chain of the merge, and later blocks of a large grid start later
+    const uint32_t bid = blockIdx.x - zone1;
     // deltas go to the replica (single GPU) or to the per-merge delta table (sharded)
-    if (zone1 && bid == nbody) {
-        zone_one<S, EXACT, BT, LTAB_T, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, dtb, a, b, nw, mc, wg_bytes + nbody,
+    if (zone1 == 1 && blockIdx.x == 0) {
+        zone_one<S, EXACT, BT, KB_LT, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, dtb, a, b, nw, mc, wg_bytes + nbody,
                                              round);
         if (t == 0) {
             KT(5);
@@ -1874,7 +2155,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                 sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
             }
             uint32_t out = 0;
-            const uint32_t r = body_sector<S>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, dtb, st,
+            const uint32_t r = body_sector<S, KB_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, dtb, st,
                                               sig + (uint64_t)sct * SP_SIGW, out, cf, cfm);
             moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (r ? out : 0u));
             if (r) {
@@ -2560,6 +2841,8 @@ struct gbpe_trainer {
     DevState* h_zst = nullptr;   // pinned
     uint32_t* d_u32 = nullptr;   // small device scratch
     uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
+    uint32_t* zseg = nullptr;    // ZSegState: the zone segments' per-merge hand-off (k_refresh zeroes it)
+    uint32_t zseg_mode = 1;      // GBPE_ZONE_SEG: 1 = segments for zones of 16K-512K, 2 = only above zone_one's 32K, 0 = off
     uint64_t* wg_bytes = nullptr;   // bytes moved per k_body workgroup (each its own counter)
     uint32_t delta_mt = 2048;       // dense k_delta: multi-tile workgroups from this many tiles (0 = never; GBPE_DELTA_MT)
     uint32_t delta_tpw = 8;         // ... of 8, 16 or 32 tiles (GBPE_DELTA_TPW)
@@ -2723,7 +3006,7 @@ struct SpGrid {
     uint32_t body, copy, zdelta, zcompact, refresh;
     uint32_t wpg = 16;    // bitmap words per k_body workgroup
     uint32_t ztail = 0;   // stale-tail slice blocks of the multi-tile zone k_delta
-    bool zone1;   // the zone fits one workgroup: it runs inside k_body
+    uint32_t zone1;   // zone workgroups inside k_body: 1 = zone_one, >= 2 = zone_seg segments, 0 = multi-tile passes
     int bt;       // k_body workgroup size (256 or 1024)
 };
 
@@ -2767,19 +3050,28 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));   // selection runs inside k_body (sel_inline)
-    const uint32_t gb = g.body + (g.zone1 ? 1u : g.copy);
+    const uint32_t gb = g.body + (g.zone1 == 1 ? 1u : g.zone1 >= 2 ? 0u : g.copy);
+    const uint32_t z1 = g.zone1 == 1 ? 1u : 0u;   // k_body's own zone workgroup
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
         launch_body<S, true>(g.bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
-                             g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, g.zone1 ? 1u : 0u,
+                             g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
                              sp_mul(t));
     else
         launch_body<S, false>(g.bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
-                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, g.zone1 ? 1u : 0u,
+                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
                               (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
                              sp_mul(t));
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
+    if (g.zone1 >= 2) {   // 16K-symbol zone segments (zone_seg)
+        if (exact)
+            hipLaunchKernelGGL((k_zseg<S, true>), dim3(g.zone1), dim3(1024), 0, s, t->st, t->zst, round, zc, zo,
+                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body);
+        else
+            hipLaunchKernelGGL((k_zseg<S, false>), dim3(g.zone1), dim3(1024), 0, s, t->st, t->zst, round, zc, zo,
+                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body);
+    }
     if (!g.zone1) {
         // a zone of many tiles (the lexicon loop's first merges): TPW tiles per
         // workgroup and one flush of their hot pairs, as in the dense loop
@@ -2810,7 +3102,7 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,
-                       (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part);
+                       (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part, t->zseg);
     if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
@@ -3280,6 +3572,10 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true) {
     }
     // per-k_refresh-workgroup maxima the sparse merges select from (sel_inline)
     if (!t->part) TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
+    if (!t->zseg && !t->sharded) {
+        TR_HIP(t, hipMalloc(&t->zseg, sizeof(ZSegState)));
+        TR_HIP(t, hipMemsetAsync(t->zseg, 0, sizeof(ZSegState), t->ctx->stream));
+    }
     hipLaunchKernelGGL(k_refresh<S>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
                        (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part);
     GBPE_LAUNCH_CHECK(t->ctx);
@@ -3440,6 +3736,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         t->delta_tpw = v >= 32 ? 32 : v >= 16 ? 16 : 8;
     }
     if (const char* e = getenv("GBPE_SHRINK_PCT")) t->shrink_pct = std::max<uint32_t>(110, (uint32_t)strtoul(e, nullptr, 10));
+    if (const char* e = getenv("GBPE_ZONE_SEG")) t->zseg_mode = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_ZONE_F")) t->zone_f = std::max<uint32_t>(3, (uint32_t)strtoul(e, nullptr, 10));
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
@@ -3711,7 +4008,11 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         sg.bt = zn <= z256 ? 256 : 1024;   // small zone: the low-latency 256-thread workgroups
         body_grid(t, sg.bt, &sg.body, &sg.wpg);
         if (sg.bt == 1024 && t->u16 && zn <= 16384u && t->zone16) sg.bt = 1023;
-        sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt));
+        sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt)) ? 1u : 0u;
+        // a zone of 16K-512K symbols: 16K-symbol segments inside k_body (zone_seg)
+        const uint32_t zs_lo = t->zseg_mode == 2 ? (t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024)) : 16384u;
+        if (t->zseg_mode && t->zseg && zn > zs_lo && zn <= NSEG_MAX * 16384u)
+            sg.zone1 = (uint32_t)gbpe_div_up(zn, 16384u);   // k_body keeps its size; k_zseg follows it
         sg.copy = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u : grid_persistent(t->ctx, gbpe_div_up(zn / 5 + 1, TPB * 8), 1);
         sg.zdelta = (uint32_t)(zt ? zt : 1);
         sg.ztail = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
@@ -3789,11 +4090,12 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     const uint32_t done = hs->merges_done;
     const uint32_t err = hs->err | (sparse ? t->h_zst->err : 0u);
     if (err) {
-        return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "training invariant violated (err=0x%x: %s%s%s%s)", err,
+        return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "training invariant violated (err=0x%x: %s%s%s%s%s)", err,
                               (err & ERR_TABLE_FULL) ? "pair table full " : "",
                               (err & ERR_COUNT_MISMATCH) ? "survivor count mismatch " : "",
                               (err & ERR_PAIR_MISSING) ? "selected pair missing " : "",
-                              (err & ERR_SPARSE_WINDOW) ? "sparse stale window outside the zone" : "");
+                              (err & ERR_SPARSE_WINDOW) ? "sparse stale window outside the zone " : "",
+                              (err & ERR_SPIN) ? "zone segment hand-off timed out" : "");
     }
     if (timing && tail) {
         float ms = 0;
@@ -4081,6 +4383,7 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->zst);
     hipFree(t->d_u32);
     hipFree(t->part);
+    hipFree(t->zseg);
     hipFree(t->wg_bytes);
     hipFree(t->lx_store);
     hipFree(t->lx_mul);
