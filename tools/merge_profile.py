@@ -16,7 +16,7 @@ import sys
 
 import numpy as np
 
-KS = ["k_select", "k_body", "k_delta", "k_compact", "k_refresh", "k_sp_"]
+KS = ["k_select", "k_body", "k_zseg", "k_delta", "k_compact", "k_refresh", "k_sp_"]
 
 
 def main():
