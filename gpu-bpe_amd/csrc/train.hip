@@ -107,7 +107,7 @@ struct DevState {
 static_assert(sizeof(DevState) <= 256, "state");
 
 // the zone segments' per-merge hand-off (zone_seg; k_refresh zeroes it)
-constexpr uint32_t NSEG_MAX = 32;
+constexpr uint32_t NSEG_MAX = 64;   // one sweeping wave: one lane per segment
 constexpr uint32_t ZSEG_SPIN = 1u << 22;
 struct ZSegState {
     uint32_t ticket;
@@ -1612,7 +1612,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
     }
 }
 
-// ── segmented zone pass (zones of 16K-512K symbols) ──
+// ── segmented zone pass (zones of 32K-1M symbols) ──
 // A zone too large for one workgroup but far smaller than the stream (merges
 // ~500-8000 at 1 GiB) is cut into segments of BT x ZPT = 16K symbols, one
 // 1024-thread workgroup each (blocks [0, nz) of k_body).  Two phases:
@@ -1632,7 +1632,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
 //    read of the other buffer (the window source) happened in phase A, before
 //    any segment passes phase B's sweep, so no store overwrites an unread source.
 //  Every zone workgroup waits only on zone workgroups, which never wait on body
-//  workgroups: with nz <= 32 workgroups they all become resident.
+//  workgroups: with nz <= 64 workgroups they all become resident.
 // k_refresh zeroes the granules for the next merge (tag = 1).
 template <typename S, bool EXACT, int BT, int NT, int ZPT>
 __device__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
@@ -2842,7 +2842,7 @@ struct gbpe_trainer {
     uint32_t* d_u32 = nullptr;   // small device scratch
     uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
     uint32_t* zseg = nullptr;    // ZSegState: the zone segments' per-merge hand-off (k_refresh zeroes it)
-    uint32_t zseg_mode = 1;      // GBPE_ZONE_SEG: 1 = segments for zones of 16K-512K, 2 = only above zone_one's 32K, 0 = off
+    uint32_t zseg_mode = 1;      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
     uint64_t* wg_bytes = nullptr;   // bytes moved per k_body workgroup (each its own counter)
     uint32_t delta_mt = 2048;       // dense k_delta: multi-tile workgroups from this many tiles (0 = never; GBPE_DELTA_MT)
     uint32_t delta_tpw = 8;         // ... of 8, 16 or 32 tiles (GBPE_DELTA_TPW)
@@ -4009,7 +4009,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         body_grid(t, sg.bt, &sg.body, &sg.wpg);
         if (sg.bt == 1024 && t->u16 && zn <= 16384u && t->zone16) sg.bt = 1023;
         sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt)) ? 1u : 0u;
-        // a zone of 16K-512K symbols: 16K-symbol segments inside k_body (zone_seg)
+        // a zone beyond zone_one, up to 1M symbols: 16K-symbol segments (k_zseg after k_body)
         const uint32_t zs_lo = t->zseg_mode == 2 ? (t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024)) : 16384u;
         if (t->zseg_mode && t->zseg && zn > zs_lo && zn <= NSEG_MAX * 16384u)
             sg.zone1 = (uint32_t)gbpe_div_up(zn, 16384u);   // k_body keeps its size; k_zseg follows it
