@@ -103,6 +103,8 @@ struct DevState {
     uint32_t is_last;      // sector-sparse: this rank holds the zone (single GPU: always)
     uint32_t cand;         // candidate sectors of this merge (trace)
     uint32_t hitsec;       // sectors with a site (trace)
+    uint32_t mc_prev;      // sector-sparse, single GPU: the last merge's count (k_refresh), for the zone rule;
+                           // unlike `mc` never written by a commit, so k_zseg beside k_body reads it safely
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
@@ -436,6 +438,7 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
                     st->merges_done = round + 1u;
                     st->next_id = g.next_id + 1u;
                     st->epoch = g.epoch + 1u;
+                    st->mc_prev = g.mc;
                 }
                 if (clog) {
                     clog[2 * round] = g.cand;
@@ -1855,30 +1858,6 @@ __device__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const 
     }
 }
 
-// The segmented zone pass as its own launch after k_body (whose last workgroup
-// committed the merge): 1024 threads, nz workgroups.  (Inside k_body its
-// registers pushed every k_body form into scratch: 1 GiB 0.88 -> 0.98 s.)
-template <typename S, bool EXACT>
-__global__ __launch_bounds__(1024) void k_zseg(DevState* st, DevState* zst, uint32_t round, S* __restrict__ zc,
-                                               S* __restrict__ zo, ZSegState* __restrict__ zg, uint32_t nz, Table tb,
-                                               uint64_t* __restrict__ bytes) {
-    constexpr int NW = sizeof(DevState) / 4;
-    __shared__ union {
-        DevState d;
-        uint32_t w[NW];
-    } s_g, s_z;
-    __shared__ LdsTab<4096> lt;
-    __shared__ ZoneLds<S, 1024> L;
-    const int t = threadIdx.x;
-    if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
-    else if (t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
-    __syncthreads();
-    const DevState& g = s_g.d;
-    if (g.stop || g.sp_abort || g.sel_round != round + 1u) return;   // this round did not merge
-    zone_seg<S, EXACT, 1024, 4096, 16>(st, zst, g, s_z.d, zc, zo, zg, nz, L, lt, tb, g.a, g.b, g.nw, g.mc, bytes, round);
-    if (t == 0) KTV(6, 2);
-}
-
 // Selection inside k_body (sector-sparse loop): every workgroup reduces the
 // k_refresh partial maxima itself and gets the same merge; the last one commits
 // it (log, table slot zeroed, state for k_refresh and the zone kernels).  The
@@ -1900,7 +1879,8 @@ template <int BT>
 __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
                            uint32_t round, bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
                            uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc,
-                           const DevState*& gsnap, const DevState*& zsnap, const SelShard sh = SelShard()) {
+                           const DevState*& gsnap, const DevState*& zsnap, const SelShard sh = SelShard(),
+                           bool commit = true) {
     __shared__ uint64_t s_red[BT / 64];
     constexpr int NW = sizeof(DevState) / 4;
     __shared__ union {
@@ -1942,14 +1922,15 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     // zone misfit: this merge's window source must lie in the zone's stale buffer
     // (n - 2mc >= Bp, where n - Bp >= z - mc_prev: the last merge removed <= mc_prev
     // body symbols), and the zone keeps >= zf mc for the merges after it
-    const uint64_t zneed = std::max<uint64_t>(2ull * mc + g.mc, (uint64_t)sh.zf * mc) + 2u;
+    const uint32_t mc_prev = sh.cap_list ? g.mc : g.mc_prev;
+    const uint64_t zneed = std::max<uint64_t>(2ull * mc + mc_prev, (uint64_t)sh.zf * mc) + 2u;
     const bool abort = !stop && !bad && !exact && ((uint64_t)g.zlast < zneed || (sh.zmax && g.zlast > sh.zmax));
     const uint32_t need = 6u * mc + 64u;   // distinct deltas of one merge <= 4 per site + tail + window
     const bool stall = !stop && !bad && !abort && sh.cap_list && need > sh.cap_list;
     const bool go = !stop && !bad && !abort && !stall;
     // the LAST workgroup commits: block 0 is the zone pass (the launch's longest
     // chain), which then starts without the table probe and the state stores
-    if (blockIdx.x == gridDim.x - 1u) {
+    if (commit && blockIdx.x == gridDim.x - 1u) {
         if (t == 0) {
             if (stop) {
                 st->stop = 1u;
@@ -2009,6 +1990,43 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     return go;
 }
 
+// The segmented zone pass as its own launch: after k_body (whose last workgroup
+// committed the merge), or beside it on the zone stream with the same selection
+// from the same snapshot and no commit.  1024 threads, nz workgroups.  (Inside k_body its
+// registers pushed every k_body form into scratch: 1 GiB 0.88 -> 0.98 s.)
+template <typename S, bool EXACT>
+__global__ __launch_bounds__(1024) void k_zseg(DevState* st, DevState* zst, uint32_t round, S* __restrict__ zc,
+                                               S* __restrict__ zo, ZSegState* __restrict__ zg, uint32_t nz, Table tb,
+                                               uint64_t* __restrict__ bytes, const uint64_t* __restrict__ part,
+                                               uint32_t npart, SelShard sh, uint32_t after) {
+    __shared__ LdsTab<4096> lt;
+    __shared__ ZoneLds<S, 1024> L;
+    uint32_t a, b, nw, mc;
+    const DevState *gs, *zs;
+    if (after) {   // after k_body: its commit is in the state
+        constexpr int NW = sizeof(DevState) / 4;
+        __shared__ union {
+            DevState d;
+            uint32_t w[NW];
+        } s_g, s_z;
+        const int t = threadIdx.x;
+        if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
+        else if (t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
+        __syncthreads();
+        const DevState& g = s_g.d;
+        if (g.stop || g.sp_abort || g.sel_round != round + 1u) return;   // this round did not merge
+        a = g.a, b = g.b, nw = g.nw, mc = g.mc;
+        gs = &s_g.d;
+        zs = &s_z.d;
+    } else {   // beside k_body (another stream): the same selection from the same snapshot, no commit
+        if (!sel_inline<1024>(st, zst, part, npart, round, EXACT, true, tb, nullptr, nullptr, a, b, nw, mc, gs, zs, sh,
+                              false))
+            return;
+    }
+    zone_seg<S, EXACT, 1024, 4096, 16>(st, zst, *gs, *zs, zc, zo, zg, nz, L, lt, tb, a, b, nw, mc, bytes, round);
+    if (threadIdx.x == 0) KTV(6, 2);
+}
+
 // Body pass: blocks [0, nbody) each own `wpg` consecutive bitmap words of
 // (a-row & b-row), tested PW words at a time: the candidate sectors whose pair
 // signature may hold (a, b) are merged (one wave per sector).  A fixed grid of
@@ -2039,7 +2057,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                                               uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
-                                              Table dtb, SelShard sh, uint32_t* __restrict__ lmul) {
+                                              Table dtb, SelShard sh, uint32_t* __restrict__ lmul, uint32_t zbeside) {
     constexpr int KB_LT = LTAB_T;
     __shared__ LdsTab<KB_LT> lt;
     __shared__ BodyLds<S, BT> u;
@@ -2050,7 +2068,9 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     uint32_t a, b, nw, mc;
     if (t == 0) KT(0);
     const DevState *gs, *zs;   // this workgroup's snapshots of the states at launch (LDS)
-    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh)) return;
+    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0 || zbeside, tb, log, grpsum, a, b, nw, mc, gs, zs,
+                        sh))
+        return;
     if (t == 0) KT(1);
     // the zone workgroup is dispatched first (block 0 when zone1): it is the longest
     // single chain of the merge, and later blocks of a large grid start later
@@ -2842,6 +2862,9 @@ struct gbpe_trainer {
     uint32_t* d_u32 = nullptr;   // small device scratch
     uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
     uint32_t* zseg = nullptr;    // ZSegState: the zone segments' per-merge hand-off (k_refresh zeroes it)
+    hipStream_t zstream = nullptr;   // zone segments beside k_body (GBPE_ZSEG_CONC)
+    hipEvent_t zev[2] = {nullptr, nullptr};
+    uint32_t zconc = 0;              // measured slower (cross-stream event waits per merge: 1 GiB 0.82 -> 0.87 s)
     uint32_t zseg_mode = 1;      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
     uint64_t* wg_bytes = nullptr;   // bytes moved per k_body workgroup (each its own counter)
     uint32_t delta_mt = 2048;       // dense k_delta: multi-tile workgroups from this many tiles (0 = never; GBPE_DELTA_MT)
@@ -3052,25 +3075,44 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));   // selection runs inside k_body (sel_inline)
     const uint32_t gb = g.body + (g.zone1 == 1 ? 1u : g.zone1 >= 2 ? 0u : g.copy);
     const uint32_t z1 = g.zone1 == 1 ? 1u : 0u;   // k_body's own zone workgroup
+    // zone segments on the zone stream beside k_body: after the last k_refresh, before the next
+    const bool conc = g.zone1 >= 2 && t->zconc && t->zstream;
+    if (conc) {
+        TR_HIP(t, hipEventRecord(t->zev[0], s));
+        TR_HIP(t, hipStreamWaitEvent(t->zstream, t->zev[0], 0));
+        if (exact)
+            hipLaunchKernelGGL((k_zseg<S, true>), dim3(g.zone1), dim3(1024), 0, t->zstream, t->st, t->zst, round, zc, zo,
+                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body, (const uint64_t*)t->part,
+                               g.refresh, sel_single(t), 0u);
+        else
+            hipLaunchKernelGGL((k_zseg<S, false>), dim3(g.zone1), dim3(1024), 0, t->zstream, t->st, t->zst, round, zc, zo,
+                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body, (const uint64_t*)t->part,
+                               g.refresh, sel_single(t), 0u);
+        TR_HIP(t, hipEventRecord(t->zev[1], t->zstream));
+    }
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
         launch_body<S, true>(g.bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
-                             sp_mul(t));
+                             sp_mul(t), conc ? 1u : 0u);
     else
         launch_body<S, false>(g.bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                               g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
                               (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
-                             sp_mul(t));
+                             sp_mul(t), conc ? 1u : 0u);
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
-    if (g.zone1 >= 2) {   // 16K-symbol zone segments (zone_seg)
+    if (conc) {
+        TR_HIP(t, hipStreamWaitEvent(s, t->zev[1], 0));
+    } else if (g.zone1 >= 2) {   // 16K-symbol zone segments (zone_seg) after k_body
         if (exact)
             hipLaunchKernelGGL((k_zseg<S, true>), dim3(g.zone1), dim3(1024), 0, s, t->st, t->zst, round, zc, zo,
-                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body);
+                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body, (const uint64_t*)t->part,
+                               g.refresh, sel_single(t), 1u);
         else
             hipLaunchKernelGGL((k_zseg<S, false>), dim3(g.zone1), dim3(1024), 0, s, t->st, t->zst, round, zc, zo,
-                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body);
+                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body, (const uint64_t*)t->part,
+                               g.refresh, sel_single(t), 1u);
     }
     if (!g.zone1) {
         // a zone of many tiles (the lexicon loop's first merges): TPW tiles per
@@ -3570,11 +3612,18 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true) {
             t->wg_cap = need;
         }
     }
+    // the zone rule's last count (sel_inline): the count of the merge before entry
+    TR_HIP(t, hipMemcpyAsync(&t->st->mc_prev, &t->st->mc, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     // per-k_refresh-workgroup maxima the sparse merges select from (sel_inline)
     if (!t->part) TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
     if (!t->zseg && !t->sharded) {
         TR_HIP(t, hipMalloc(&t->zseg, sizeof(ZSegState)));
         TR_HIP(t, hipMemsetAsync(t->zseg, 0, sizeof(ZSegState), t->ctx->stream));
+        if (t->zconc) {
+            TR_HIP(t, hipStreamCreateWithFlags(&t->zstream, hipStreamNonBlocking));
+            TR_HIP(t, hipEventCreateWithFlags(&t->zev[0], hipEventDisableTiming));
+            TR_HIP(t, hipEventCreateWithFlags(&t->zev[1], hipEventDisableTiming));
+        }
     }
     hipLaunchKernelGGL(k_refresh<S>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
                        (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part);
@@ -3737,6 +3786,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     }
     if (const char* e = getenv("GBPE_SHRINK_PCT")) t->shrink_pct = std::max<uint32_t>(110, (uint32_t)strtoul(e, nullptr, 10));
     if (const char* e = getenv("GBPE_ZONE_SEG")) t->zseg_mode = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_ZSEG_CONC")) t->zconc = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_ZONE_F")) t->zone_f = std::max<uint32_t>(3, (uint32_t)strtoul(e, nullptr, 10));
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
@@ -4384,6 +4434,12 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->d_u32);
     hipFree(t->part);
     hipFree(t->zseg);
+    if (t->zstream) {
+        hipStreamSynchronize(t->zstream);
+        hipStreamDestroy(t->zstream);
+    }
+    for (auto& e : t->zev)
+        if (e) hipEventDestroy(e);
     hipFree(t->wg_bytes);
     hipFree(t->lx_store);
     hipFree(t->lx_mul);
@@ -5203,11 +5259,11 @@ int shard_phase1_sp(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl)
     if (exact)
         launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, wpg, t->sig, t->tb, nbody,
                              (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc, zone ? 1u : 0u, (const uint64_t*)t->part,
-                             t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh, sp_mul(t));
+                             t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh, sp_mul(t), 0u);
     else
         launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, wpg, t->sig, t->tb, nbody,
                               (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc, zone ? 1u : 0u, (const uint64_t*)t->part,
-                              t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh, sp_mul(t));
+                              t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh, sp_mul(t), 0u);
     const uint32_t nlb = grid_blocks(t->ctx, dt.nblk, 2);
     hipLaunchKernelGGL(k_shard_send_sp, dim3(nlb + 1), dim3(TPB), 0, s, t->st, t->zst, round, dt, rec, cl, nlb);
     GBPE_LAUNCH_CHECK(t->ctx);
