@@ -2865,7 +2865,8 @@ struct gbpe_trainer {
     hipStream_t zstream = nullptr;   // zone segments beside k_body (GBPE_ZSEG_CONC)
     hipEvent_t zev[2] = {nullptr, nullptr};
     uint32_t zconc = 0;              // measured slower (cross-stream event waits per merge: 1 GiB 0.82 -> 0.87 s)
-    uint32_t zseg_mode = 1;      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
+    uint32_t zseg_mode = 1;
+    uint32_t table_grows = 0;    // crowded-table rebuilds (same size or larger)      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
     uint64_t* wg_bytes = nullptr;   // bytes moved per k_body workgroup (each its own counter)
     uint32_t delta_mt = 2048;       // dense k_delta: multi-tile workgroups from this many tiles (0 = never; GBPE_DELTA_MT)
     uint32_t delta_tpw = 8;         // ... of 8, 16 or 32 tiles (GBPE_DELTA_TPW)
@@ -2939,6 +2940,37 @@ uint32_t grid_persistent(const gbpe_ctx* ctx, uint64_t work_tiles, uint32_t per_
 // a grid over argmax blocks: every workgroup owns at most 64 (one flag ballot)
 uint32_t grid_blocks(const gbpe_ctx* ctx, uint32_t nblk, uint32_t per_cu) {
     return std::max<uint32_t>(grid_persistent(ctx, nblk, per_cu), (uint32_t)gbpe_div_up(nblk, 64));
+}
+
+// new (empty) table arrays of 2^lg slots; the caller recounts (table_rebuild)
+int table_resize(gbpe_trainer* t, uint32_t lg) {
+    hipStream_t s = t->ctx->stream;
+    TR_HIP(t, hipStreamSynchronize(s));
+    hipFree(t->tb.slots);
+    hipFree(t->tb.bmax);
+    hipFree(t->tb.dirty);
+    hipFree(t->tb.dlist);
+    hipFree(t->tb.blive);
+    t->tb.slots = nullptr, t->tb.bmax = nullptr, t->tb.dirty = nullptr, t->tb.dlist = nullptr, t->tb.blive = nullptr;
+    const uint64_t slots = 1ull << lg;
+    t->table_log2 = lg;
+    t->tb.mask = (uint32_t)(slots - 1);
+    t->tb.nblk = (uint32_t)(slots >> BLK_LOG2);
+    if (hipMalloc(&t->tb.slots, slots * sizeof(uint2)) != hipSuccess ||
+        hipMalloc(&t->tb.bmax, t->tb.nblk * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&t->tb.dirty, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->tb.dlist, (t->tb.nblk + 1) * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess)
+        return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(pair table, 2^%u slots) failed", lg);
+    TR_HIP(t, hipMemsetAsync(t->tb.dirty, 0, t->tb.nblk * sizeof(uint32_t), s));
+    t->g_refresh = grid_blocks(t->ctx, t->tb.nblk, 2);
+    if (t->refresh_blocks) t->g_refresh = std::max<uint32_t>(t->refresh_blocks, (uint32_t)gbpe_div_up(t->tb.nblk, 64));
+    if (t->part) {   // one partial maximum per k_refresh workgroup
+        hipFree(t->part);
+        t->part = nullptr;
+        TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
+    }
+    return GBPE_OK;
 }
 
 int table_rebuild(gbpe_trainer* t) {
@@ -3817,12 +3849,14 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
             return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "memset failed"));
     }
     // pair table
+    // distinct pairs start below 65536 (byte pairs) and grow by a few per merge
+    // (1 GiB English at 32K: 170K live, 243K slots used): start at 2^20 slots and
+    // grow when crowded (trainer_step_once).  An oversized table costs every merge:
+    // k_refresh scans one dirty flag per 256-slot block (2^24 slots: 65,536 flags,
+    // 1,024 workgroups) and sel_inline reduces one partial maximum per k_refresh
+    // workgroup.
     uint32_t lg = opts->table_log2;
-    if (lg == 0) {
-        lg = 22;
-        if (n > (64ull << 20)) lg = 23;
-        if (n > (512ull << 20)) lg = 24;
-    }
+    if (lg == 0) lg = 20;
     if (lg < BLK_LOG2 + 1) lg = BLK_LOG2 + 1;
     if (lg > 28) lg = 28;
     t->table_log2 = lg;
@@ -3973,12 +4007,18 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     if (t->done + k > t->needed) k = t->needed - t->done;
     if (t->stop || k == 0) return GBPE_OK;
     hipStream_t s = t->ctx->stream;
-    // rebuild the pair table when it gets crowded (dead pairs accumulate)
+    // rebuild the pair table when it gets crowded (dead pairs accumulate), twice as
+    // large (or more) while the live pairs would fill over a quarter of it
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
     if ((uint64_t)t->h_st->used * 2 > slots) {
         int rc = sp_exit_any(t);   // the full recount runs on the dense stream
+        const uint64_t live = std::max<uint64_t>(t->h_st->live, t->h_st->used / 2);
+        uint32_t lg = t->table_log2;
+        while (lg < 28 && live * 4 > (1ull << lg)) ++lg;
+        if (rc == GBPE_OK && lg != t->table_log2) rc = table_resize(t, lg);
         if (rc == GBPE_OK) rc = table_rebuild(t);
         if (rc != GBPE_OK) return rc;
+        ++t->table_grows;
     }
     // sector-sparse loop once merges touch a small fraction of the stream
     if (t->sp_cooldown) {
@@ -4982,7 +5022,14 @@ extern "C" int gbpe_shard_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n
                                  uint64_t cap_extra, gbpe_trainer** out) {
     if (!ctx || !out || !opts) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
     if (world == 0 || world > 64 || rank >= world) return gbpe_set_error(ctx, GBPE_E_INVALID, "rank/world out of range (world <= 64)");
-    int rc = trainer_create_impl(ctx, bytes, n, word_starts, input_on_device, opts, cap_extra, out);
+    // the replica holds GLOBAL counts and is only ever rehashed at its size: size
+    // it for the corpus as a whole (shard_rehash; no growth path)
+    gbpe_train_opts o = *opts;
+    if (o.table_log2 == 0) {
+        const uint64_t gn = n * world;
+        o.table_log2 = gn > (512ull << 20) ? 24u : gn > (64ull << 20) ? 23u : 22u;
+    }
+    int rc = trainer_create_impl(ctx, bytes, n, word_starts, input_on_device, &o, cap_extra, out);
     if (rc != GBPE_OK) return rc;
     gbpe_trainer* t = *out;
     t->sharded = true;
