@@ -166,16 +166,16 @@ def test_table_rebuild_small_table(eng):
 
 
 def test_table_grows_when_crowded(eng):
-    # a 2^10-slot table outgrown by the live pairs is rebuilt larger (more than once);
+    # a 2^13-slot table outgrown by the live pairs is rebuilt larger (more than once);
     # results must not change, dense or with the sector-sparse loop entering later
     from gpubpe import synth
     data = synth.english(300000, seed=41)
     ref = O.train(data, 1200)
     for sparse in (None, "dense"):
-        m, s, pairs, st = _train_native(eng, data, 1200, table_log2=10, batch=32, sparse=sparse)
+        m, s, pairs, st = _train_native(eng, data, 1200, table_log2=13, batch=16, sparse=sparse)
         assert m == ref["merges"] and np.array_equal(s, ref["symbols"])
         _assert_counts_match_stream(pairs, s)
-        assert st.table_slots >= 4096, st.table_slots
+        assert st.table_slots >= 1 << 15, st.table_slots
 
 
 def test_random_bytes_and_runs(eng):
