@@ -2049,7 +2049,10 @@ union BodyLds {   // body workgroups use the candidate arrays, the zone workgrou
     BodyCand c;
 };
 
-template <typename S, bool EXACT, int BT, int ZPT = ZoneDim<S, BT>::ZPT>
+// ZSEG: the form for zones of 32K-1M symbols: blocks [0, zone1) run the zone
+// segments (zone_seg) beside the body blocks, and zone_one is not compiled in
+// (with both, every form spilled to scratch)
+template <typename S, bool EXACT, int BT, int ZPT = ZoneDim<S, BT>::ZPT, bool ZSEG = false>
 __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
                                               uint32_t* __restrict__ bits, uint32_t W, uint32_t wpg,
                                               uint32_t* __restrict__ sig, Table tb, uint32_t nbody,
@@ -2057,8 +2060,9 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                                               uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
-                                              Table dtb, SelShard sh, uint32_t* __restrict__ lmul, uint32_t zbeside) {
-    constexpr int KB_LT = LTAB_T;
+                                              Table dtb, SelShard sh, uint32_t* __restrict__ lmul, uint32_t zbeside,
+                                              ZSegState* __restrict__ zg = nullptr) {
+    constexpr int KB_LT = ZSEG ? 4096 : LTAB_T;
     __shared__ LdsTab<KB_LT> lt;
     __shared__ BodyLds<S, BT> u;
     __shared__ uint32_t s_ntok, s_n, s_any, s_rm[BT / 64];
@@ -2076,14 +2080,26 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     // single chain of the merge, and later blocks of a large grid start later
     const uint32_t bid = blockIdx.x - zone1;
     // deltas go to the replica (single GPU) or to the per-merge delta table (sharded)
-    if (zone1 == 1 && blockIdx.x == 0) {
-        zone_one<S, EXACT, BT, KB_LT, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, dtb, a, b, nw, mc, wg_bytes + nbody,
-                                             round);
-        if (t == 0) {
-            KT(5);
-            KTV(6, 2);
+    if constexpr (ZSEG) {
+        if (blockIdx.x < zone1) {
+            zone_seg<S, EXACT, BT, KB_LT, 16>(st, zst, *gs, *zs, zcur, (S*)zoth, zg, zone1, u.z, lt, dtb, a, b, nw, mc,
+                                             wg_bytes + nbody, round);
+            if (t == 0) {
+                KT(5);
+                KTV(6, 2);
+            }
+            return;
         }
-        return;
+    } else {
+        if (zone1 == 1 && blockIdx.x == 0) {
+            zone_one<S, EXACT, BT, KB_LT, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, dtb, a, b, nw, mc,
+                                                 wg_bytes + nbody, round);
+            if (t == 0) {
+                KT(5);
+                KTV(6, 2);
+            }
+            return;
+        }
     }
     if (bid >= nbody) {
         const uint64_t src0 = (uint64_t)gs->n + gs->off - gs->poff - 2ull * mc - gs->Bp;
@@ -2864,6 +2880,7 @@ struct gbpe_trainer {
     uint32_t* zseg = nullptr;    // ZSegState: the zone segments' per-merge hand-off (k_refresh zeroes it)
     hipStream_t zstream = nullptr;   // zone segments beside k_body (GBPE_ZSEG_CONC)
     hipEvent_t zev[2] = {nullptr, nullptr};
+    uint32_t zseg_inbody = 1;        // GBPE_ZSEG_INBODY: segments in k_body's ZSEG form (0: k_zseg after k_body)
     uint32_t zconc = 0;              // measured slower (cross-stream event waits per merge: 1 GiB 0.82 -> 0.87 s)
     uint32_t zseg_mode = 1;
     uint32_t table_grows = 0;    // crowded-table rebuilds (same size or larger)      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
@@ -3090,7 +3107,9 @@ inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* 
 // slower: C2 0.66 vs 0.61 s)
 template <typename S, bool EXACT, typename... A>
 void launch_body(int bt, uint32_t grid, hipStream_t s, A... args) {
-    if (bt == 1023 && sizeof(S) == 2)
+    if (bt == 2048)   // zone segments inside k_body (the ZSEG form, 1024 threads)
+        hipLaunchKernelGGL((k_body<S, EXACT, 1024, 16, true>), dim3(grid), dim3(1024), 0, s, args...);
+    else if (bt == 1023 && sizeof(S) == 2)
         hipLaunchKernelGGL((k_body<S, EXACT, 1024, 16>), dim3(grid), dim3(1024), 0, s, args...);
     else if (bt >= 1023)
         hipLaunchKernelGGL((k_body<S, EXACT, 1024>), dim3(grid), dim3(1024), 0, s, args...);
@@ -3105,10 +3124,13 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));   // selection runs inside k_body (sel_inline)
-    const uint32_t gb = g.body + (g.zone1 == 1 ? 1u : g.zone1 >= 2 ? 0u : g.copy);
-    const uint32_t z1 = g.zone1 == 1 ? 1u : 0u;   // k_body's own zone workgroup
+    // zone segments inside k_body (the ZSEG form) unless GBPE_ZSEG_INBODY=0 (then k_zseg after it)
+    const bool inbody = g.zone1 >= 2 && t->zseg_inbody;
+    const uint32_t gb = g.body + (g.zone1 == 1 ? 1u : inbody ? g.zone1 : g.zone1 >= 2 ? 0u : g.copy);
+    const uint32_t z1 = g.zone1 == 1 ? 1u : inbody ? g.zone1 : 0u;   // k_body's own zone workgroups
+    const int bt = inbody ? 2048 : g.bt;
     // zone segments on the zone stream beside k_body: after the last k_refresh, before the next
-    const bool conc = g.zone1 >= 2 && t->zconc && t->zstream;
+    const bool conc = g.zone1 >= 2 && !inbody && t->zconc && t->zstream;
     if (conc) {
         TR_HIP(t, hipEventRecord(t->zev[0], s));
         TR_HIP(t, hipStreamWaitEvent(t->zstream, t->zev[0], 0));
@@ -3124,19 +3146,19 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     }
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
-        launch_body<S, true>(g.bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
+        launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
-                             sp_mul(t), conc ? 1u : 0u);
+                             sp_mul(t), conc ? 1u : 0u, (ZSegState*)t->zseg);
     else
-        launch_body<S, false>(g.bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
+        launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                               g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
                               (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
-                             sp_mul(t), conc ? 1u : 0u);
+                             sp_mul(t), conc ? 1u : 0u, (ZSegState*)t->zseg);
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
     if (conc) {
         TR_HIP(t, hipStreamWaitEvent(s, t->zev[1], 0));
-    } else if (g.zone1 >= 2) {   // 16K-symbol zone segments (zone_seg) after k_body
+    } else if (g.zone1 >= 2 && !inbody) {   // 16K-symbol zone segments (zone_seg) after k_body
         if (exact)
             hipLaunchKernelGGL((k_zseg<S, true>), dim3(g.zone1), dim3(1024), 0, s, t->st, t->zst, round, zc, zo,
                                (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body, (const uint64_t*)t->part,
@@ -3819,6 +3841,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     if (const char* e = getenv("GBPE_SHRINK_PCT")) t->shrink_pct = std::max<uint32_t>(110, (uint32_t)strtoul(e, nullptr, 10));
     if (const char* e = getenv("GBPE_ZONE_SEG")) t->zseg_mode = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_ZSEG_CONC")) t->zconc = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_ZSEG_INBODY")) t->zseg_inbody = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_ZONE_F")) t->zone_f = std::max<uint32_t>(3, (uint32_t)strtoul(e, nullptr, 10));
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
