@@ -103,8 +103,8 @@ struct DevState {
     uint32_t is_last;      // sector-sparse: this rank holds the zone (single GPU: always)
     uint32_t cand;         // candidate sectors of this merge (trace)
     uint32_t hitsec;       // sectors with a site (trace)
-    uint32_t mc_prev;      // sector-sparse, single GPU: the last merge's count (k_refresh), for the zone rule;
-                           // unlike `mc` never written by a commit, so k_zseg beside k_body reads it safely
+    uint32_t mc_prev;      // sector-sparse, single GPU: the last merge's count (k_refresh), for the zone rule
+                           // (never written by a commit: a reader beside k_body would see it unchanged)
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
@@ -1990,43 +1990,6 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     return go;
 }
 
-// The segmented zone pass as its own launch: after k_body (whose last workgroup
-// committed the merge), or beside it on the zone stream with the same selection
-// from the same snapshot and no commit.  1024 threads, nz workgroups.  (Inside k_body its
-// registers pushed every k_body form into scratch: 1 GiB 0.88 -> 0.98 s.)
-template <typename S, bool EXACT>
-__global__ __launch_bounds__(1024) void k_zseg(DevState* st, DevState* zst, uint32_t round, S* __restrict__ zc,
-                                               S* __restrict__ zo, ZSegState* __restrict__ zg, uint32_t nz, Table tb,
-                                               uint64_t* __restrict__ bytes, const uint64_t* __restrict__ part,
-                                               uint32_t npart, SelShard sh, uint32_t after) {
-    __shared__ LdsTab<4096> lt;
-    __shared__ ZoneLds<S, 1024> L;
-    uint32_t a, b, nw, mc;
-    const DevState *gs, *zs;
-    if (after) {   // after k_body: its commit is in the state
-        constexpr int NW = sizeof(DevState) / 4;
-        __shared__ union {
-            DevState d;
-            uint32_t w[NW];
-        } s_g, s_z;
-        const int t = threadIdx.x;
-        if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
-        else if (t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
-        __syncthreads();
-        const DevState& g = s_g.d;
-        if (g.stop || g.sp_abort || g.sel_round != round + 1u) return;   // this round did not merge
-        a = g.a, b = g.b, nw = g.nw, mc = g.mc;
-        gs = &s_g.d;
-        zs = &s_z.d;
-    } else {   // beside k_body (another stream): the same selection from the same snapshot, no commit
-        if (!sel_inline<1024>(st, zst, part, npart, round, EXACT, true, tb, nullptr, nullptr, a, b, nw, mc, gs, zs, sh,
-                              false))
-            return;
-    }
-    zone_seg<S, EXACT, 1024, 4096, 16>(st, zst, *gs, *zs, zc, zo, zg, nz, L, lt, tb, a, b, nw, mc, bytes, round);
-    if (threadIdx.x == 0) KTV(6, 2);
-}
-
 // Body pass: blocks [0, nbody) each own `wpg` consecutive bitmap words of
 // (a-row & b-row), tested PW words at a time: the candidate sectors whose pair
 // signature may hold (a, b) are merged (one wave per sector).  A fixed grid of
@@ -2060,7 +2023,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                                               uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
-                                              Table dtb, SelShard sh, uint32_t* __restrict__ lmul, uint32_t zbeside,
+                                              Table dtb, SelShard sh, uint32_t* __restrict__ lmul,
                                               ZSegState* __restrict__ zg = nullptr) {
     constexpr int KB_LT = ZSEG ? 4096 : LTAB_T;
     __shared__ LdsTab<KB_LT> lt;
@@ -2072,8 +2035,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     uint32_t a, b, nw, mc;
     if (t == 0) KT(0);
     const DevState *gs, *zs;   // this workgroup's snapshots of the states at launch (LDS)
-    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0 || zbeside, tb, log, grpsum, a, b, nw, mc, gs, zs,
-                        sh))
+    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh))
         return;
     if (t == 0) KT(1);
     // the zone workgroup is dispatched first (block 0 when zone1): it is the longest
@@ -2878,10 +2840,6 @@ struct gbpe_trainer {
     uint32_t* d_u32 = nullptr;   // small device scratch
     uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
     uint32_t* zseg = nullptr;    // ZSegState: the zone segments' per-merge hand-off (k_refresh zeroes it)
-    hipStream_t zstream = nullptr;   // zone segments beside k_body (GBPE_ZSEG_CONC)
-    hipEvent_t zev[2] = {nullptr, nullptr};
-    uint32_t zseg_inbody = 1;        // GBPE_ZSEG_INBODY: segments in k_body's ZSEG form (0: k_zseg after k_body)
-    uint32_t zconc = 0;              // measured slower (cross-stream event waits per merge: 1 GiB 0.82 -> 0.87 s)
     uint32_t zseg_mode = 1;
     uint32_t table_grows = 0;    // crowded-table rebuilds (same size or larger)      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
     uint64_t* wg_bytes = nullptr;   // bytes moved per k_body workgroup (each its own counter)
@@ -3124,50 +3082,23 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));   // selection runs inside k_body (sel_inline)
-    // zone segments inside k_body (the ZSEG form) unless GBPE_ZSEG_INBODY=0 (then k_zseg after it)
-    const bool inbody = g.zone1 >= 2 && t->zseg_inbody;
-    const uint32_t gb = g.body + (g.zone1 == 1 ? 1u : inbody ? g.zone1 : g.zone1 >= 2 ? 0u : g.copy);
-    const uint32_t z1 = g.zone1 == 1 ? 1u : inbody ? g.zone1 : 0u;   // k_body's own zone workgroups
+    // zone segments run inside k_body (its ZSEG form)
+    const bool inbody = g.zone1 >= 2;
+    const uint32_t gb = g.body + (g.zone1 ? g.zone1 : g.copy);
+    const uint32_t z1 = g.zone1;   // k_body's own zone workgroups
     const int bt = inbody ? 2048 : g.bt;
-    // zone segments on the zone stream beside k_body: after the last k_refresh, before the next
-    const bool conc = g.zone1 >= 2 && !inbody && t->zconc && t->zstream;
-    if (conc) {
-        TR_HIP(t, hipEventRecord(t->zev[0], s));
-        TR_HIP(t, hipStreamWaitEvent(t->zstream, t->zev[0], 0));
-        if (exact)
-            hipLaunchKernelGGL((k_zseg<S, true>), dim3(g.zone1), dim3(1024), 0, t->zstream, t->st, t->zst, round, zc, zo,
-                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body, (const uint64_t*)t->part,
-                               g.refresh, sel_single(t), 0u);
-        else
-            hipLaunchKernelGGL((k_zseg<S, false>), dim3(g.zone1), dim3(1024), 0, t->zstream, t->st, t->zst, round, zc, zo,
-                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body, (const uint64_t*)t->part,
-                               g.refresh, sel_single(t), 0u);
-        TR_HIP(t, hipEventRecord(t->zev[1], t->zstream));
-    }
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
         launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
-                             sp_mul(t), conc ? 1u : 0u, (ZSegState*)t->zseg);
+                             sp_mul(t), (ZSegState*)t->zseg);
     else
         launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                               g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
                               (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
-                             sp_mul(t), conc ? 1u : 0u, (ZSegState*)t->zseg);
+                             sp_mul(t), (ZSegState*)t->zseg);
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
-    if (conc) {
-        TR_HIP(t, hipStreamWaitEvent(s, t->zev[1], 0));
-    } else if (g.zone1 >= 2 && !inbody) {   // 16K-symbol zone segments (zone_seg) after k_body
-        if (exact)
-            hipLaunchKernelGGL((k_zseg<S, true>), dim3(g.zone1), dim3(1024), 0, s, t->st, t->zst, round, zc, zo,
-                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body, (const uint64_t*)t->part,
-                               g.refresh, sel_single(t), 1u);
-        else
-            hipLaunchKernelGGL((k_zseg<S, false>), dim3(g.zone1), dim3(1024), 0, s, t->st, t->zst, round, zc, zo,
-                               (ZSegState*)t->zseg, g.zone1, t->tb, t->wg_bytes + g.body, (const uint64_t*)t->part,
-                               g.refresh, sel_single(t), 1u);
-    }
     if (!g.zone1) {
         // a zone of many tiles (the lexicon loop's first merges): TPW tiles per
         // workgroup and one flush of their hot pairs, as in the dense loop
@@ -3673,11 +3604,6 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true) {
     if (!t->zseg && !t->sharded) {
         TR_HIP(t, hipMalloc(&t->zseg, sizeof(ZSegState)));
         TR_HIP(t, hipMemsetAsync(t->zseg, 0, sizeof(ZSegState), t->ctx->stream));
-        if (t->zconc) {
-            TR_HIP(t, hipStreamCreateWithFlags(&t->zstream, hipStreamNonBlocking));
-            TR_HIP(t, hipEventCreateWithFlags(&t->zev[0], hipEventDisableTiming));
-            TR_HIP(t, hipEventCreateWithFlags(&t->zev[1], hipEventDisableTiming));
-        }
     }
     hipLaunchKernelGGL(k_refresh<S>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
                        (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part);
@@ -3840,8 +3766,6 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     }
     if (const char* e = getenv("GBPE_SHRINK_PCT")) t->shrink_pct = std::max<uint32_t>(110, (uint32_t)strtoul(e, nullptr, 10));
     if (const char* e = getenv("GBPE_ZONE_SEG")) t->zseg_mode = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_ZSEG_CONC")) t->zconc = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_ZSEG_INBODY")) t->zseg_inbody = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_ZONE_F")) t->zone_f = std::max<uint32_t>(3, (uint32_t)strtoul(e, nullptr, 10));
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
@@ -4122,10 +4046,10 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         body_grid(t, sg.bt, &sg.body, &sg.wpg);
         if (sg.bt == 1024 && t->u16 && zn <= 16384u && t->zone16) sg.bt = 1023;
         sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt)) ? 1u : 0u;
-        // a zone beyond zone_one, up to 1M symbols: 16K-symbol segments (k_zseg after k_body)
+        // a zone of 16K-1M symbols: 16K-symbol segments inside k_body (its ZSEG form)
         const uint32_t zs_lo = t->zseg_mode == 2 ? (t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024)) : 16384u;
         if (t->zseg_mode && t->zseg && zn > zs_lo && zn <= NSEG_MAX * 16384u)
-            sg.zone1 = (uint32_t)gbpe_div_up(zn, 16384u);   // k_body keeps its size; k_zseg follows it
+            sg.zone1 = (uint32_t)gbpe_div_up(zn, 16384u);
         sg.copy = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u : grid_persistent(t->ctx, gbpe_div_up(zn / 5 + 1, TPB * 8), 1);
         sg.zdelta = (uint32_t)(zt ? zt : 1);
         sg.ztail = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
@@ -4497,12 +4421,6 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->d_u32);
     hipFree(t->part);
     hipFree(t->zseg);
-    if (t->zstream) {
-        hipStreamSynchronize(t->zstream);
-        hipStreamDestroy(t->zstream);
-    }
-    for (auto& e : t->zev)
-        if (e) hipEventDestroy(e);
     hipFree(t->wg_bytes);
     hipFree(t->lx_store);
     hipFree(t->lx_mul);
@@ -5329,11 +5247,11 @@ int shard_phase1_sp(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl)
     if (exact)
         launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, wpg, t->sig, t->tb, nbody,
                              (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc, zone ? 1u : 0u, (const uint64_t*)t->part,
-                             t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh, sp_mul(t), 0u);
+                             t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh, sp_mul(t));
     else
         launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, wpg, t->sig, t->tb, nbody,
                               (const S*)zo, (S*)t->wtmp, 0u, t->zst, zc, zone ? 1u : 0u, (const uint64_t*)t->part,
-                              t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh, sp_mul(t), 0u);
+                              t->g_refresh, t->d_log, t->grpsum, t->wg_bytes, dt, sh, sp_mul(t));
     const uint32_t nlb = grid_blocks(t->ctx, dt.nblk, 2);
     hipLaunchKernelGGL(k_shard_send_sp, dim3(nlb + 1), dim3(TPB), 0, s, t->st, t->zst, round, dt, rec, cl, nlb);
     GBPE_LAUNCH_CHECK(t->ctx);
