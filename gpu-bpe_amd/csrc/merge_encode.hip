@@ -16,6 +16,11 @@
 // k_me_walk: one lane per 4096-byte chunk; it owns the segments that START in
 // its chunk and BPE-encodes each in place (rank lookups in an L2-resident
 // open-addressing table).  Chunk counts → scan.h two-level scan → k_me_compact.
+// A segment longer than ME_LONG bytes (CJK paragraphs, base64, minified code:
+// no cut for a long stretch) would cost its lane one full pass per rank
+// applied; it is encoded with a rank-ordered heap over a linked list instead
+// (me_heap: O(len log len), same order: lowest rank first, leftmost first),
+// in an arena k_me_long sized and laid out beforehand.
 
 #include "common.h"
 #include "scan.h"
@@ -27,6 +32,17 @@ namespace {
 constexpr int ME_TPB = 64;
 constexpr uint32_t ME_CS = 4096;      // bytes per chunk (a lane's range of segment starts)
 constexpr uint32_t ME_NONE = 0xFFFFFFFFu;
+constexpr uint32_t ME_LONG = 1024;                  // longer segments take the heap path
+constexpr uint32_t ME_LSLOT = ME_CS / ME_LONG + 1;  // long segments that can start in one chunk
+constexpr uint32_t ME_DEAD = 0xFFFFFFFFu;
+
+struct MeArena {   // per long segment at offset `off` (bytes of all long segments before it)
+    uint32_t* tok;       // [off, off + len)
+    uint32_t* nxt;
+    uint32_t* prv;
+    uint64_t* heap;      // [3 off, 3 (off + len)): initial pairs + two per merge
+    const uint64_t* slot;   // per chunk: ME_LSLOT offsets of the long segments starting in it
+};
 
 struct MeTable {
     const uint4* slots;   // {pid, rank, new id, 0}; pid 0 = empty ((0,0) never merges: token 0 never pairs)
@@ -51,9 +67,98 @@ __device__ __forceinline__ bool me_cut(const uint8_t* __restrict__ in, const MeT
     return ((t.cross[k >> 5] >> (k & 31u)) & 1u) == 0u;
 }
 
+// the long segments (> ME_LONG bytes) starting in each chunk: arena offsets
+__global__ __launch_bounds__(ME_TPB) void k_me_long(const uint8_t* __restrict__ in, uint64_t n, MeTable t,
+                                                    unsigned long long* __restrict__ total, uint64_t* __restrict__ slot,
+                                                    uint64_t nchunks) {
+    const uint64_t c = (uint64_t)blockIdx.x * ME_TPB + threadIdx.x;
+    if (c >= nchunks) return;
+    const uint64_t lo = c * ME_CS, hi = min(lo + ME_CS, n);
+    uint64_t s = lo;
+    while (s < hi && !me_cut(in, t, s)) ++s;
+    uint32_t k = 0;
+    while (s < hi) {
+        uint64_t z = s + 1;
+        while (z < n && !me_cut(in, t, z)) ++z;
+        if (z - s > ME_LONG) slot[c * ME_LSLOT + k++] = atomicAdd(total, (unsigned long long)(z - s));
+        s = z;
+    }
+}
+
+// one long segment on one lane: a min-heap of (rank << 32 | position) over the
+// adjacent pairs of a doubly linked token list.  Popping the lowest rank, then
+// the leftmost position, applies every merge in rank order and each rank's
+// occurrences left to right, as the reference's one pass per merge does: a
+// merge's new pairs hold its new token, which only later ranks use.  Stale
+// entries (the pair at that position changed) are skipped on pop.
+__device__ uint32_t me_heap(const uint8_t* __restrict__ in, uint32_t len, const MeTable& t, uint32_t* __restrict__ tk,
+                            uint32_t* __restrict__ nx, uint32_t* __restrict__ pv, uint64_t* __restrict__ hp,
+                            uint32_t* __restrict__ out) {
+    for (uint32_t i = 0; i < len; ++i) {
+        tk[i] = in[i];
+        nx[i] = i + 1;
+        pv[i] = i ? i - 1 : ME_NONE;
+    }
+    uint32_t h = 0;
+    auto push = [&](uint64_t key) {
+        uint32_t i = h++;
+        while (i) {
+            const uint32_t p = (i - 1) >> 1;
+            if (hp[p] <= key) break;
+            hp[i] = hp[p];
+            i = p;
+        }
+        hp[i] = key;
+    };
+    auto rank_at = [&](uint32_t i, uint32_t j) -> uint4 { return me_find(t, (tk[i] << 16) | tk[j]); };
+    for (uint32_t i = 0; i + 1 < len; ++i) {
+        const uint4 e = rank_at(i, i + 1);
+        if (e.y != ME_NONE) push(((uint64_t)e.y << 32) | i);
+    }
+    while (h) {
+        const uint64_t key = hp[0];
+        const uint64_t last = hp[--h];
+        if (h) {   // sift the last entry down from the root
+            uint32_t i = 0;
+            for (;;) {
+                uint32_t c = 2 * i + 1;
+                if (c >= h) break;
+                if (c + 1 < h && hp[c + 1] < hp[c]) ++c;
+                if (last <= hp[c]) break;
+                hp[i] = hp[c];
+                i = c;
+            }
+            hp[i] = last;
+        }
+        const uint32_t r = (uint32_t)(key >> 32), i = (uint32_t)key;
+        if (tk[i] == ME_DEAD) continue;
+        const uint32_t j = nx[i];
+        if (j >= len) continue;
+        const uint4 e = rank_at(i, j);
+        if (e.y != r) continue;   // stale: the pair at i changed
+        tk[i] = e.z;
+        tk[j] = ME_DEAD;
+        const uint32_t q = nx[j];
+        nx[i] = q;
+        if (q < len) pv[q] = i;
+        const uint32_t p = pv[i];
+        if (p != ME_NONE) {
+            const uint4 ep = rank_at(p, i);
+            if (ep.y != ME_NONE) push(((uint64_t)ep.y << 32) | p);
+        }
+        if (q < len) {
+            const uint4 eq = rank_at(i, q);
+            if (eq.y != ME_NONE) push(((uint64_t)eq.y << 32) | i);
+        }
+    }
+    uint32_t cnt = 0;
+    for (uint32_t i = 0; i < len; i = nx[i]) out[cnt++] = tk[i];   // position 0 is never merged away
+    return cnt;
+}
+
 __global__ __launch_bounds__(ME_TPB) void k_me_walk(const uint8_t* __restrict__ in, uint64_t n, MeTable t,
                                                     uint32_t* __restrict__ scratch, uint32_t* __restrict__ counts,
-                                                    uint64_t* __restrict__ base, uint64_t nchunks) {
+                                                    uint64_t* __restrict__ base, uint64_t nchunks, MeArena ar) {
     const uint64_t c = (uint64_t)blockIdx.x * ME_TPB + threadIdx.x;
     if (c >= nchunks) return;
     const uint64_t lo = c * ME_CS, hi = min(lo + ME_CS, n);
@@ -61,12 +166,18 @@ __global__ __launch_bounds__(ME_TPB) void k_me_walk(const uint8_t* __restrict__ 
     while (s < hi && !me_cut(in, t, s)) ++s;   // first segment start in the chunk
     base[c] = s;
     const uint64_t b0 = s;   // this chunk's tokens go to scratch[b0 ...]: never past the bytes consumed
-    uint32_t written = 0;
+    uint32_t written = 0, nlong = 0;
     while (s < hi) {
         uint64_t z = s + 1;
         while (z < n && !me_cut(in, t, z)) ++z;   // the segment [s, z) may run past hi
         uint32_t* tok = scratch + b0 + written;
         uint32_t len = (uint32_t)(z - s);
+        if (len > ME_LONG) {
+            const uint64_t off = ar.slot[c * ME_LSLOT + nlong++];
+            written += me_heap(in + s, len, t, ar.tok + off, ar.nxt + off, ar.prv + off, ar.heap + 3 * off, tok);
+            s = z;
+            continue;
+        }
         for (uint32_t j = 0; j < len; ++j) tok[j] = in[s + j];
         while (len >= 2) {
             uint32_t best = ME_NONE, bpid = 0, bnew = 0;
@@ -211,8 +322,37 @@ extern "C" int gbpe_bpe_encode(gbpe_ctx* ctx, gbpe_bpe* bp, const uint8_t* bytes
     uint32_t* d_out = (uint32_t*)(((uintptr_t)(total + 1) + 15) & ~(uintptr_t)15);
     hipError_t e = hipMemcpyAsync(d_in, bytes, n, hipMemcpyHostToDevice, s);
     MeTable t{bp->slots, bp->mask, bp->cross};
-    hipLaunchKernelGGL(k_me_walk, dim3((uint32_t)gbpe_div_up(nchunks, ME_TPB)), dim3(ME_TPB), 0, s, d_in, n, t, scratch,
-                       counts, base, nchunks);
+    // long segments: their total length sizes the heap arena (none: no arena)
+    MeArena ar{};
+    uint8_t* da = nullptr;
+    uint64_t* slot = nullptr;
+    unsigned long long* d_long = nullptr;
+    unsigned long long long_total = 0;
+    if (e == hipSuccess) e = hipMalloc(&slot, nchunks * ME_LSLOT * sizeof(uint64_t) + 16);
+    if (e == hipSuccess) {
+        d_long = (unsigned long long*)(slot + nchunks * ME_LSLOT);
+        e = hipMemsetAsync(d_long, 0, 8, s);
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_me_long, dim3((uint32_t)gbpe_div_up(nchunks, ME_TPB)), dim3(ME_TPB), 0, s, d_in, n, t, d_long,
+                           slot, nchunks);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&long_total, d_long, 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess && long_total) {
+        e = hipMalloc(&da, long_total * (3 * sizeof(uint32_t) + 3 * sizeof(uint64_t)) + 64);
+        if (e == hipSuccess) {
+            ar.heap = (uint64_t*)da;
+            ar.tok = (uint32_t*)(ar.heap + 3 * long_total);
+            ar.nxt = ar.tok + long_total;
+            ar.prv = ar.nxt + long_total;
+        }
+    }
+    ar.slot = slot;
+    if (e == hipSuccess)
+        hipLaunchKernelGGL(k_me_walk, dim3((uint32_t)gbpe_div_up(nchunks, ME_TPB)), dim3(ME_TPB), 0, s, d_in, n, t,
+                           scratch, counts, base, nchunks, ar);
     hipLaunchKernelGGL(k_chunk_scan1, dim3((uint32_t)nblk), dim3(SCAN_TPB), 0, s, (const uint32_t*)counts, nchunks,
                        local, blocksum);
     hipLaunchKernelGGL(k_chunk_scan2, dim3(1), dim3(SCAN_TPB), 0, s, blocksum, nblk, total);
@@ -226,6 +366,8 @@ extern "C" int gbpe_bpe_encode(gbpe_ctx* ctx, gbpe_bpe* bp, const uint8_t* bytes
     if (e == hipSuccess && tot <= out_cap && out && tot)
         e = hipMemcpy(out, d_out, tot * 4, hipMemcpyDeviceToHost);
     hipFree(d);
+    hipFree(da);
+    hipFree(slot);
     if (e != hipSuccess) return gbpe_set_error(ctx, GBPE_E_DEVICE, "bpe encode failed: %s", hipGetErrorString(e));
     *n_out = tot;
     if (tot > out_cap) return gbpe_set_error(ctx, GBPE_E_CAPACITY, "bpe encode: output needs %llu tokens",

@@ -60,3 +60,53 @@ def test_merge_encode_edges(engine):
     for merges, text in cases:
         enc = MergeEncoder(engine, merges)
         assert enc.encode_bytes(text).tolist() == O.encode_merge_order(text, merges), (merges, text[:20])
+
+
+def _np_merge_order(data: bytes, merges) -> np.ndarray:
+    """numpy form of the oracle's encode_merge_order (one pass per merge, every
+    occurrence left to right; runs of a == b pair up from their left end)."""
+    tok = np.frombuffer(data, np.uint8).astype(np.int64)
+    for a, b, nid in (m[:3] for m in merges):
+        if tok.size < 2:
+            break
+        idx = np.flatnonzero((tok[:-1] == a) & (tok[1:] == b))
+        if idx.size == 0:
+            continue
+        if a == b:
+            k = np.arange(idx.size)
+            start = np.ones(idx.size, bool)
+            start[1:] = idx[1:] != idx[:-1] + 1
+            rs = np.maximum.accumulate(np.where(start, k, 0))
+            idx = idx[(k - rs) % 2 == 0]
+        tok[idx] = nid
+        rm = np.zeros(tok.size, bool)
+        rm[idx + 1] = True
+        tok = tok[~rm]
+    return tok
+
+
+def test_merge_encode_long_segment(engine):
+    # a text with no cut at all (every byte pair of its alphabet is joined by some
+    # merge): one segment of > 1 MB, encoded by the heap path on one lane; the
+    # numpy restatement is first checked against the oracle on a 40 KB piece
+    rng = np.random.default_rng(61)
+    alpha = np.frombuffer(b"abcd", np.uint8)
+    letters = alpha.tolist()
+    order = rng.permutation(16)   # every byte pair of the alphabet merges (in a random rank order) ...
+    merges = [[letters[k // 4], letters[k % 4], 256 + r] for r, k in enumerate(order.tolist())]
+    for r in range(40):           # ... and so do pairs of those tokens
+        i, j = rng.integers(0, 16, 2).tolist()
+        merges.append([256 + i, 256 + j, 272 + r])
+    small = bytes(alpha[rng.integers(0, 4, 40_000)])
+    assert _np_merge_order(small, merges).tolist() == O.encode_merge_order(small, merges)
+    big = bytes(alpha[rng.integers(0, 4, 1_300_000)])
+    enc = MergeEncoder(engine, merges)
+    got = enc.encode_bytes(big)
+    assert np.array_equal(np.asarray(got, dtype=np.int64), _np_merge_order(big, merges))
+    # a long run of one byte (a == b pairs) plus short segments around it
+    text = b"xy " + b"a" * 300_000 + b" yx"
+    m2 = [[97, 97, 256], [256, 97, 257], [256, 256, 258], [258, 258, 259]]
+    enc2 = MergeEncoder(engine, m2)
+    assert enc2.encode_bytes(text).tolist() == _np_merge_order(text, m2).tolist()
+    enc.destroy()
+    enc2.destroy()
