@@ -13,6 +13,10 @@ Secondary legs (same JSON line):
   * c2: BASELINE configs[1] (100 MiB English, seed 2, 32K vocab), full runs;
   * tokenize (configs[2], C3): chunked trie encode of 1 GiB multilingual text
     with a 32K vocab trained on a 100 MiB sample (seed 4);
+  * c4_shard: C4's per-rank shard (the C3 text: 1 GiB multilingual) at C4's
+    64K vocab, u32 symbols, run to the 0xFFFF id stop (configs[3] per rank);
+  * c5: configs[4], 1 GiB code at 50K vocab with GPT-4 rule word starts
+    computed on the device (u32 symbols); both against their oracle fixtures;
   * cpu_baseline: the reference algorithm restated on the CPU
     (oracle/bpe_oracle.c: full pair recount every merge), a bounded sample of
     the same workload on the box's CPU share and on 1 core;
@@ -157,17 +161,17 @@ def fixture(name: str):
     return z["merges"], json.loads(str(z["meta"]))
 
 
-def timed_runs(args, lib, ctx, dist, d, n, vocab, steps, warmup):
+def timed_runs(args, lib, ctx, dist, d, n, vocab, steps, warmup, flags=0):
     """W untimed + K timed full runs, barrier + sync on both sides of the timed ones."""
     for _ in range(warmup):
-        train_run(lib, ctx, d, n, vocab)
+        train_run(lib, ctx, d, n, vocab, flags=flags)
     lib.gbpe_synchronize(ctx)
     dist.barrier()
     lib.gbpe_synchronize(ctx)
     t0 = time.perf_counter()
     total, last, st = 0, None, None
     for _ in range(steps):
-        last, st = train_run(lib, ctx, d, n, vocab)
+        last, st = train_run(lib, ctx, d, n, vocab, flags=flags)
         total += last.shape[0]
     lib.gbpe_synchronize(ctx)
     t1 = time.perf_counter()
@@ -279,6 +283,23 @@ def c2_leg(args, lib, ctx, dist):
     if want is not None:
         res["merges_equal_fixture"] = bool(last.shape == want.shape and np.array_equal(last, want))
     return data, res
+
+
+def config_leg(args, lib, ctx, dist, name, data, vocab, flags, workload, runs=2):
+    """A secondary training configuration on its own fixture's corpus: 1 untimed +
+    `runs` timed full runs, every merge of the last one checked against the fixture."""
+    want, meta = fixture(name)
+    d = device_buffer(lib, ctx, data)
+    wall, total, last, st = timed_runs(args, lib, ctx, dist, d, len(data), vocab, runs, 1, flags)
+    lib.gbpe_device_free(ctx, d)
+    res = {"workload": workload, "value": round(total / wall, 1), "unit": "merges/s", "runs": runs,
+           "merges_per_run": int(last.shape[0]), "ms_per_run": round(1e3 * wall / runs, 2),
+           "bytes_per_symbol": int(st.bytes_per_symbol), "early_stop": bool(st.early_stop)}
+    if want is not None:
+        res["corpus_sha256_equal"] = hashlib.sha256(data).hexdigest() == meta["corpus_sha256"]
+        res["merges_equal_fixture"] = bool(last.shape == want.shape and np.array_equal(last, want))
+        res["fixture"] = f"tests/golden/train_{name}.npz"
+    return res
 
 
 def encode_leg(args, lib, ctx, dist, rank):
@@ -439,6 +460,21 @@ def single_line(args, lib, ctx, dist, rank):
     if not args.no_encode:
         enc = encode_leg(args, lib, ctx, dist, rank)
         line["tokenize"] = enc[-1]
+        if not args.no_c4 and args.encode_bytes == 1 << 30:
+            # C4's per-rank shard is the C3 text itself (1 GiB multilingual, seed 3)
+            line["c4_shard"] = config_leg(
+                args, lib, ctx, dist, "ml1g64k", enc[0], 65536, 0,
+                "C4 per-rank shard: 64K-vocab train on 1,073,741,824 B multilingual UTF-8 (seed 3; C4 = 8 such "
+                "shards), u32 symbols, run to the 0xFFFF id stop")
+    if not args.no_c5:
+        from gpubpe import _lib
+        t = time.time()
+        code = make_corpus({"gen": "code", "n": 1 << 30, "seed": 6})
+        log(f"[bench] C5 corpus {len(code)} B generated in {time.time() - t:.1f}s")
+        line["c5"] = config_leg(args, lib, ctx, dist, "code1g", code, 50000, _lib.GBPE_TRAIN_GPT4_BOUNDARIES,
+                                "C5: 50K-vocab train on 1,073,741,824 B code (seed 6), GPT-4 rule word starts "
+                                "computed on the device, u32 symbols")
+        del code
     if not args.no_cpu:
         base, cpu_merges, enc_base = cpu_baselines(args, data, enc)
         line["cpu_baseline"] = base
@@ -682,6 +718,8 @@ def main():
     ap.add_argument("--no-encode", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c2", action="store_true")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 per-rank shard leg (64K vocab)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 leg (1 GiB code, 50K vocab, GPT-4 rules)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP-event roofline run")
     ap.add_argument("--cpu-merges", type=int, default=0, help="CPU baseline merges on the CPU share (0 = 24)")
     ap.add_argument("--consolidate-below", type=int, default=-1,
