@@ -13,8 +13,8 @@ Secondary legs (same JSON line):
   * c2: BASELINE configs[1] (100 MiB English, seed 2, 32K vocab), full runs;
   * tokenize (configs[2], C3): chunked trie encode of 1 GiB multilingual text
     with a 32K vocab trained on a 100 MiB sample (seed 4);
-  * c4_shard: C4's per-rank shard (the C3 text: 1 GiB multilingual) at C4's
-    64K vocab, u32 symbols, run to the 0xFFFF id stop (configs[3] per rank);
+  * c4_shard: C4's rank-0 shard (1 GiB multilingual, seed 5) trained alone at
+    C4's 64K vocab, u32 symbols, run to the 0xFFFF id stop (configs[3] per rank);
   * c5: configs[4], 1 GiB code at 50K vocab with GPT-4 rule word starts
     computed on the device (u32 symbols); both against their oracle fixtures;
   * cpu_baseline: the reference algorithm restated on the CPU
@@ -460,12 +460,15 @@ def single_line(args, lib, ctx, dist, rank):
     if not args.no_encode:
         enc = encode_leg(args, lib, ctx, dist, rank)
         line["tokenize"] = enc[-1]
-        if not args.no_c4 and args.encode_bytes == 1 << 30:
-            # C4's per-rank shard is the C3 text itself (1 GiB multilingual, seed 3)
-            line["c4_shard"] = config_leg(
-                args, lib, ctx, dist, "ml1g64k", enc[0], 65536, 0,
-                "C4 per-rank shard: 64K-vocab train on 1,073,741,824 B multilingual UTF-8 (seed 3; C4 = 8 such "
-                "shards), u32 symbols, run to the 0xFFFF id stop")
+    if not args.no_c4:
+        t = time.time()
+        shard = make_corpus({"gen": "multilingual", "n": 1 << 30, "seed": 5})
+        log(f"[bench] C4 shard {len(shard)} B generated in {time.time() - t:.1f}s")
+        line["c4_shard"] = config_leg(
+            args, lib, ctx, dist, "ml1g64k", shard, 65536, 0,
+            "C4 rank-0 shard alone: 64K-vocab train on 1,073,741,824 B multilingual UTF-8 (seed 5; C4 = 8 such "
+            "shards, seed 5 + rank), u32 symbols, run to the 0xFFFF id stop")
+        del shard
     if not args.no_c5:
         from gpubpe import _lib
         t = time.time()

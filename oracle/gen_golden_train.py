@@ -46,9 +46,9 @@ TRAIN = {
     "c3vocab": ({"gen": "multilingual", "n": 104_857_600, "seed": 4}, 32768, "heuristic"),
     # 1 GiB multilingual @ 32K (the C3/C4 text model)
     "ml1g": ({"gen": "multilingual", "n": 1 << 30, "seed": 3}, 32768, "heuristic"),
-    # C4's per-rank shard: 1 GiB multilingual @ 64K vocab (u32 symbols: ids reach
-    # 0xFFFF, the stop of train.wgsl:345)
-    "ml1g64k": ({"gen": "multilingual", "n": 1 << 30, "seed": 3}, 65536, "heuristic"),
+    # C4's rank-0 shard (8 x 1 GiB multilingual, seed 5 + rank) trained
+    # alone at C4's 64K vocab (u32 symbols: ids reach 0xFFFF, the stop of train.wgsl:345)
+    "ml1g64k": ({"gen": "multilingual", "n": 1 << 30, "seed": 5}, 65536, "heuristic"),
 }
 # name -> (text spec, vocab fixture)
 ENCODE = {

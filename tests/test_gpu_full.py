@@ -10,7 +10,7 @@ stream must equal the CPU restatement's.  Configurations:
 * code1g  — C5: 1 GiB code, 50K vocab (u32 symbols), GPT-4 rule word starts
             computed on the device (pre_tokenizer.mjs:226-292), 49,744 merges
 * ml1g    — 1 GiB multilingual @ 32K
-* ml1g64k — C4's per-rank shard: the same 1 GiB multilingual @ 64K (u32 symbols)
+* ml1g64k — C4's rank-0 shard (1 GiB multilingual, seed 5) alone @ 64K (u32 symbols)
 * c3      — C3's 32K vocab (100 MiB multilingual sample) trained on the GPU,
             then the chunked trie encode of 64 MiB and of 1 GiB multilingual
             text with it (token count and token-stream sha256)
@@ -113,7 +113,7 @@ def test_full_ml1g(eng):
 
 
 def test_full_ml1g64k_c4_shard(eng):
-    # C4's per-rank shard (1 GiB multilingual) at C4's 64K vocab: ids past 0x7FFF
+    # C4's rank-0 shard (1 GiB multilingual, seed 5) at C4's 64K vocab: ids past 0x7FFF
     # need the u32 layout, and the run ends at the 0xFFFF stop (train.wgsl:345)
     st, _ = _check_train(eng, "ml1g64k")
     assert st.bytes_per_symbol == 4
