@@ -2870,6 +2870,7 @@ struct gbpe_trainer {
     uint32_t shrink_pct = 200;   // shrink once the zone exceeds shrink_pct % of the target + 4096 (GBPE_SHRINK_PCT)
     uint32_t zone_f = 3;         // single-GPU zone rule factor (sel_inline; GBPE_ZONE_F, >= 3)
     uint32_t refresh_blocks = 0; // GBPE_REFRESH_BLOCKS: k_refresh grid (0 = 2 per CU)
+    bool rehash_on = true;       // GBPE_REHASH: grow the table inside the sparse loop (0: exit, grow, recount)
     uint32_t body_cap = 256;     // GBPE_BODY_WG: most k_body workgroups (default one per CU)
     uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
     uint32_t* h_clog = nullptr;
@@ -2973,6 +2974,51 @@ int table_rebuild(gbpe_trainer* t) {
         hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(grid_blocks(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, 0u,
                            0, t->tb, (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+
+// Growing the table inside the sector-sparse loop: every count in the table is
+// exact between steps (the body's multiplicities included), so the live entries
+// move to the larger table as they are — no exit to one dense stream, no recount
+// and no lexicon rebuild on re-entry (C5 grew 2^20 -> 2^25 in five such exits).
+__global__ __launch_bounds__(TPB) void k_rehash(const uint2* __restrict__ old, uint64_t nold, DevState* st, Table tb) {
+    for (uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x; i < nold; i += (uint64_t)gridDim.x * TPB) {
+        const uint2 e = old[i];
+        if (e.x && (int32_t)e.y > 0) table_add(tb, st, e.x, e.y);
+    }
+}
+
+int table_rehash(gbpe_trainer* t, uint32_t lg) {
+    hipStream_t s = t->ctx->stream;
+    uint2* old = t->tb.slots;
+    const uint64_t nold = (uint64_t)t->tb.mask + 1;
+    t->tb.slots = nullptr;   // kept until the live entries have moved
+    int rc = table_resize(t, lg);
+    if (rc != GBPE_OK) {
+        hipFree(old);
+        return rc;
+    }
+    const uint64_t slots = (uint64_t)t->tb.mask + 1;
+    TR_HIP(t, hipMemsetAsync(t->tb.slots, 0, slots * sizeof(uint2), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.bmax, 0, (uint64_t)t->tb.nblk * sizeof(uint64_t), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.blive, 0, (uint64_t)t->tb.nblk * sizeof(uint32_t), s));
+    TR_HIP(t, hipMemsetAsync(&t->st->used, 0, sizeof(uint32_t), s));
+    hipLaunchKernelGGL(k_rehash, dim3(grid_persistent(t->ctx, gbpe_div_up(nold, TPB), 4)), dim3(TPB), 0, s,
+                       (const uint2*)old, nold, t->st, t->tb);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    hipLaunchKernelGGL(k_clear_dirty_all, dim3(gbpe_div_up(t->tb.nblk, 256)), dim3(256), 0, s, t->st, t->tb);
+    // block maxima and the per-workgroup partial maxima the next selection reads
+    if (t->u16)
+        hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
+                           (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr,
+                           FusedSel(), t->part, (uint32_t*)nullptr);
+    else
+        hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
+                           (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr,
+                           FusedSel(), t->part, (uint32_t*)nullptr);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    TR_HIP(t, hipStreamSynchronize(s));
+    hipFree(old);
     return GBPE_OK;
 }
 
@@ -3749,6 +3795,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     t->max_id = (uint32_t)(max_id < 0x10000ull ? max_id : 0x10000ull);
     if (const char* e = getenv("GBPE_SPARSE_DIV")) t->sp_div = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_REFRESH_BLOCKS")) t->refresh_blocks = (uint32_t)atoi(e);
+    if (const char* e = getenv("GBPE_REHASH")) t->rehash_on = atoi(e) != 0;
     t->body_cap = (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
     if (const char* e = getenv("GBPE_BODY_WG")) t->body_cap = std::max<uint32_t>(1, (uint32_t)atoi(e));
     if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
@@ -3958,12 +4005,17 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     // large (or more) while the live pairs would fill over a quarter of it
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
     if ((uint64_t)t->h_st->used * 2 > slots) {
-        int rc = sp_exit_any(t);   // the full recount runs on the dense stream
         const uint64_t live = std::max<uint64_t>(t->h_st->live, t->h_st->used / 2);
         uint32_t lg = t->table_log2;
         while (lg < 28 && live * 4 > (1ull << lg)) ++lg;
-        if (rc == GBPE_OK && lg != t->table_log2) rc = table_resize(t, lg);
-        if (rc == GBPE_OK) rc = table_rebuild(t);
+        int rc;
+        if (t->sp && !t->sharded && t->rehash_on) {   // the sparse loop goes on over the moved entries
+            rc = table_rehash(t, lg);
+        } else {
+            rc = sp_exit_any(t);   // the full recount runs on the dense stream
+            if (rc == GBPE_OK && lg != t->table_log2) rc = table_resize(t, lg);
+            if (rc == GBPE_OK) rc = table_rebuild(t);
+        }
         if (rc != GBPE_OK) return rc;
         ++t->table_grows;
     }

@@ -178,6 +178,24 @@ def test_table_grows_when_crowded(eng):
         assert st.table_slots >= 1 << 15, st.table_slots
 
 
+def test_table_grows_inside_sparse_loop(eng, monkeypatch):
+    # inside the sector-sparse loop a crowded table moves its live entries to a
+    # larger one (k_rehash) instead of leaving the loop for a dense recount: same
+    # merges and counts, fewer sparse -> dense exits than the recount path
+    from gpubpe import synth
+    data = synth.english(300000, seed=41)
+    ref = O.train(data, 1200)
+    exits = {}
+    for rehash in ("1", "0"):
+        monkeypatch.setenv("GBPE_REHASH", rehash)
+        m, s, pairs, st = _train_native(eng, data, 1200, table_log2=13, batch=16, sparse="early")
+        assert m == ref["merges"] and np.array_equal(s, ref["symbols"])
+        _assert_counts_match_stream(pairs, s)
+        assert st.table_slots >= 1 << 15, st.table_slots
+        exits[rehash] = st.sparse_exits
+    assert exits["1"] < exits["0"], exits
+
+
 def test_random_bytes_and_runs(eng):
     rng = np.random.default_rng(17)
     for trial in range(6):
