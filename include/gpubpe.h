@@ -159,7 +159,7 @@ typedef struct gbpe_trainer_stats {
     double   ms_compact;          /* k_compact alone (tiles + stale-tail blocks) */
     uint64_t sparse_merges;       /* merges run by the sector-sparse loop */
     uint32_t sparse_enters;       /* dense -> sparse re-layouts */
-    uint32_t sparse_exits;        /* sparse -> dense re-layouts (export, table rebuild, zone too small) */
+    uint32_t sparse_exits;        /* sparse -> dense re-layouts (export, zone too small; a crowded table grows in place) */
     uint64_t sparse_sectors;      /* sectors of the last sparse layout */
     uint64_t sparse_zone;         /* zone length at the last sparse entry */
     uint64_t body_bytes;          /* bytes k_body actually moved: candidate extents + signature words, sector
