@@ -128,9 +128,10 @@ def device_buffer(lib, ctx, data: bytes):
     return p
 
 
-def train_run(lib, ctx, d_bytes, n, vocab, flags=0, max_merges=0, batch=128):
+def train_run(lib, ctx, d_bytes, n, vocab, flags=0, max_merges=0, batch=128, pairs_out=None):
     """One training run on HBM-resident bytes: create + every step.  Returns
-    (merges [k, 4] uint32, stats)."""
+    (merges [k, 4] uint32, stats).  pairs_out (a list): the live pair ids at the
+    end are appended to it (the reference-table estimate; never in a timed run)."""
     from gpubpe import _lib
     opts = _lib.TrainOpts(target_vocab_size=vocab, vocab_size=256, next_token_id=256, batch_size=batch,
                           flags=flags, table_log2=0)
@@ -148,6 +149,14 @@ def train_run(lib, ctx, d_bytes, n, vocab, flags=0, max_merges=0, batch=128):
                 break
         st = _lib.TrainerStats()
         lib.gbpe_trainer_stats_get(tr, C.byref(st))
+        if pairs_out is not None:
+            cnt = C.c_uint64()
+            lib.gbpe_trainer_pair_counts(tr, None, None, 0, C.byref(cnt))
+            pids = np.zeros(max(1, cnt.value), np.uint32)
+            cts = np.zeros(max(1, cnt.value), np.uint32)
+            _lib.check(lib.gbpe_trainer_pair_counts(tr, pids.ctypes.data_as(_lib.u32p), cts.ctypes.data_as(_lib.u32p),
+                                                    cnt.value, C.byref(cnt)), ctx, "pair_counts")
+            pairs_out.append(pids[: cnt.value])
     finally:
         lib.gbpe_trainer_destroy(tr)
     return np.array(merges, dtype=np.uint32).reshape(-1, 4), st
@@ -161,10 +170,11 @@ def fixture(name: str):
     return z["merges"], json.loads(str(z["meta"]))
 
 
-def timed_runs(args, lib, ctx, dist, d, n, vocab, steps, warmup, flags=0):
-    """W untimed + K timed full runs, barrier + sync on both sides of the timed ones."""
-    for _ in range(warmup):
-        train_run(lib, ctx, d, n, vocab, flags=flags)
+def timed_runs(args, lib, ctx, dist, d, n, vocab, steps, warmup, flags=0, pairs_out=None):
+    """W untimed + K timed full runs, barrier + sync on both sides of the timed ones
+    (the last untimed run also hands its final live pairs to pairs_out)."""
+    for w in range(warmup):
+        train_run(lib, ctx, d, n, vocab, flags=flags, pairs_out=pairs_out if w == warmup - 1 else None)
     lib.gbpe_synchronize(ctx)
     dist.barrier()
     lib.gbpe_synchronize(ctx)
@@ -177,6 +187,12 @@ def timed_runs(args, lib, ctx, dist, d, n, vocab, steps, warmup, flags=0):
     t1 = time.perf_counter()
     dist.barrier()
     return dist.max(t1 - t0), total, last, st
+
+
+def ref_table(st, pairs):
+    """the reference's 2^21-slot table against this run's pair sets."""
+    from gpubpe import reftable
+    return reftable.report(int(st.max_live_pairs), pairs[0] if pairs else None)
 
 
 def train_detail(st, sk):
@@ -251,13 +267,16 @@ def headline_leg(args, lib, ctx, dist):
     log(f"[bench] headline corpus {len(data)} B generated in {time.time() - t:.1f}s")
     d = device_buffer(lib, ctx, data)
     n = len(data)
-    wall, total, last, st = timed_runs(args, lib, ctx, dist, d, n, args.vocab, args.steps, args.warmup)
+    pairs = []
+    wall, total, last, st = timed_runs(args, lib, ctx, dist, d, n, args.vocab, args.steps, args.warmup,
+                                       pairs_out=pairs)
     sk = None
     if not args.no_kernel_timing:
         from gpubpe import _lib
         _, sk = train_run(lib, ctx, d, n, args.vocab, flags=_lib.GBPE_TRAIN_TIMING)
     lib.gbpe_device_free(ctx, d)
     det = train_detail(st, sk)
+    det["reference_table"] = ref_table(st, pairs)
     det["merges_per_run"] = int(last.shape[0])
     det["last_merge"] = last[-1].tolist() if last.shape[0] else []
     parity = {}
@@ -274,12 +293,13 @@ def headline_leg(args, lib, ctx, dist):
 def c2_leg(args, lib, ctx, dist):
     data = make_corpus(C2)
     d = device_buffer(lib, ctx, data)
-    wall, total, last, st = timed_runs(args, lib, ctx, dist, d, len(data), args.vocab, 3, 1)
+    pairs = []
+    wall, total, last, st = timed_runs(args, lib, ctx, dist, d, len(data), args.vocab, 3, 1, pairs_out=pairs)
     lib.gbpe_device_free(ctx, d)
     want, _ = fixture("c2")
     res = {"workload": "C2 (BASELINE configs[1]): 32K-vocab train on 104,857,600 B English UTF-8 (seed 2), full runs",
            "value": round(total / wall, 1), "unit": "merges/s", "runs": 3, "merges_per_run": int(last.shape[0]),
-           "ms_per_run": round(1e3 * wall / 3, 2)}
+           "ms_per_run": round(1e3 * wall / 3, 2), "reference_table": ref_table(st, pairs)}
     if want is not None:
         res["merges_equal_fixture"] = bool(last.shape == want.shape and np.array_equal(last, want))
     return data, res
@@ -290,11 +310,16 @@ def config_leg(args, lib, ctx, dist, name, data, vocab, flags, workload, runs=2)
     `runs` timed full runs, every merge of the last one checked against the fixture."""
     want, meta = fixture(name)
     d = device_buffer(lib, ctx, data)
-    wall, total, last, st = timed_runs(args, lib, ctx, dist, d, len(data), vocab, runs, 1, flags)
+    pairs = []
+    wall, total, last, st = timed_runs(args, lib, ctx, dist, d, len(data), vocab, runs, 1, flags, pairs_out=pairs)
     lib.gbpe_device_free(ctx, d)
     res = {"workload": workload, "value": round(total / wall, 1), "unit": "merges/s", "runs": runs,
            "merges_per_run": int(last.shape[0]), "ms_per_run": round(1e3 * wall / runs, 2),
-           "bytes_per_symbol": int(st.bytes_per_symbol), "early_stop": bool(st.early_stop)}
+           "bytes_per_symbol": int(st.bytes_per_symbol), "early_stop": bool(st.early_stop),
+           "sparse": {"enters": int(st.sparse_enters), "exits": int(st.sparse_exits),
+                      "dense_merges": int(st.merges_done - st.sparse_merges),
+                      "lexicon_builds": int(st.lexicon_builds), "lexicon_fallbacks": int(st.lexicon_fallbacks)},
+           "reference_table": ref_table(st, pairs)}
     if want is not None:
         res["corpus_sha256_equal"] = hashlib.sha256(data).hexdigest() == meta["corpus_sha256"]
         res["merges_equal_fixture"] = bool(last.shape == want.shape and np.array_equal(last, want))

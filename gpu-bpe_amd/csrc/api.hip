@@ -39,7 +39,11 @@ static const char* const kKernelNames[] = {
 
 extern "C" {
 
-const char* gbpe_version(void) { return "gpubpe 0.1 (gfx950, abi 1)"; }
+const char* gbpe_version(void) { return "gpubpe 0.3 (gfx950, abi 2)"; }
+
+int gbpe_abi_version(void) { return GBPE_ABI_VERSION; }
+
+uint64_t gbpe_trainer_stats_size(void) { return sizeof(gbpe_trainer_stats); }
 
 int gbpe_kernel_count(void) { return (int)(sizeof(kKernelNames) / sizeof(kKernelNames[0])); }
 

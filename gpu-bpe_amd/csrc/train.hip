@@ -105,6 +105,8 @@ struct DevState {
     uint32_t hitsec;       // sectors with a site (trace)
     uint32_t mc_prev;      // sector-sparse, single GPU: the last merge's count (k_refresh), for the zone rule
                            // (never written by a commit: a reader beside k_body would see it unchanged)
+    uint32_t enter_lim;    // dense loop: end the step at the first merge whose count is <= this (the host
+                           // can then enter the sector-sparse loop; 0 = off)
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
@@ -591,6 +593,11 @@ __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log,
     const uint32_t mc = (uint32_t)(best >> 32);
     const uint32_t pid = ~(uint32_t)best;
     if (st->merges_done >= st->budget) {   // host asked for fewer merges this step
+        return;
+    }
+    if (!zst && st->enter_lim && mc <= st->enter_lim && st->merges_done > 0u) {
+        // counts fell far enough for the word-lexicon loop: end the step here so the
+        // host enters it (C5's first count is 17 % of the stream, its second 0.6 %)
         return;
     }
     if (mc < 2u || st->next_id > 0xFFFFu) {   // train.wgsl:345-348
@@ -2616,7 +2623,11 @@ __global__ __launch_bounds__(TL_BT) void k_tail(DevState* st, DevState* zst, S* 
 }
 #endif  // GBPE_TAIL_LOOP
 
-// dense → sparse: the last word start at or before `lim` (one workgroup, backwards)
+// dense → sparse: the last position at or before `lim` that no counted pair can
+// span — a word start, or a token-0 symbol on either side (one workgroup,
+// backwards).  The 0s count: the stale window of a huge merge is a 0 run of up
+// to ~mc symbols (C5's first merge: ~180M), which a word-start-only search
+// crossed at 1024 symbols per round (25 ms per entry / shrink).
 template <typename S>
 __global__ __launch_bounds__(1024) void k_sp_zone_start(const S* __restrict__ cur, uint32_t lim, uint32_t* __restrict__ out) {
     __shared__ uint32_t s_found;
@@ -2624,7 +2635,8 @@ __global__ __launch_bounds__(1024) void k_sp_zone_start(const S* __restrict__ cu
     __syncthreads();
     for (int64_t hi = lim; hi >= 1; hi -= 1024) {
         const int64_t i = hi - (int64_t)threadIdx.x;
-        if (i >= 1 && (cur[i] & Sym<S>::WS)) atomicMax(&s_found, (uint32_t)i);
+        const uint32_t x = i >= 1 ? (uint32_t)cur[i] : 0u, p = i >= 1 ? (uint32_t)cur[i - 1] : 0u;
+        if (i >= 1 && ((x & Sym<S>::WS) || !(x & Sym<S>::TM) || !(p & Sym<S>::TM))) atomicMax(&s_found, (uint32_t)i);
         __syncthreads();
         const uint32_t f = s_found;
         __syncthreads();
@@ -2780,6 +2792,7 @@ struct gbpe_trainer {
     bool u16 = true;
     uint32_t bps = 2;            // bytes per symbol
     uint64_t n0 = 0, cap_syms = 0;
+    uint64_t n_prev0 = 0;        // created from a state: its previous-stream length (export before any merge)
     void* buf[2] = {nullptr, nullptr};
     int cur = 0;                 // index of the buffer holding the stream
     uint32_t n = 0;              // host copy of the stream length
@@ -2840,8 +2853,8 @@ struct gbpe_trainer {
     uint32_t* d_u32 = nullptr;   // small device scratch
     uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
     uint32_t* zseg = nullptr;    // ZSegState: the zone segments' per-merge hand-off (k_refresh zeroes it)
-    uint32_t zseg_mode = 1;
-    uint32_t table_grows = 0;    // crowded-table rebuilds (same size or larger)      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
+    uint32_t zseg_mode = 1;      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
+    uint32_t table_grows = 0;    // crowded-table rebuilds (same size or larger)
     uint64_t* wg_bytes = nullptr;   // bytes moved per k_body workgroup (each its own counter)
     uint32_t delta_mt = 2048;       // dense k_delta: multi-tile workgroups from this many tiles (0 = never; GBPE_DELTA_MT)
     uint32_t delta_tpw = 8;         // ... of 8, 16 or 32 tiles (GBPE_DELTA_TPW)
@@ -3468,15 +3481,18 @@ int lx_expand(gbpe_trainer* t, S* dst, uint64_t* tot) {
 }
 
 // dense → sparse at a step boundary.  The zone is the stream from the last word
-// start at or before n - zt (zt = sp_zt * last_mc + 64: >= 5 x the next merge's
-// count while counts fall; a merge that would not fit is not run and the host
-// goes dense, sp_abort); the dense stale buffer's tail becomes the zone's stale
-// buffer.
+// start at or before n - zt (zt = max(sp_zt * next_mc, 2 next_mc + last_mc) + 64:
+// >= 5 x the next merge's count while counts fall, and room for the stale window
+// the last merge left (sel_inline's zone rule); a merge that would not fit is not
+// run and the host goes dense, sp_abort); the dense stale buffer's tail becomes the
+// zone's stale buffer.  next_mc = 0: the last merge's count stands in for it.
 template <typename S>
-int sp_enter(gbpe_trainer* t, bool with_zone = true) {
+int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
     hipStream_t s = t->ctx->stream;
     const uint32_t n = t->n;
-    const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
+    const uint64_t prev_mc = t->last_mc;   // the previous stream is n + prev_mc long
+    const uint64_t nmc = next_mc ? next_mc : prev_mc;
+    const uint64_t zt = std::max<uint64_t>((uint64_t)t->sp_zt * nmc, 2ull * nmc + prev_mc) + 64;
     const S* cur = (const S*)t->buf[t->cur];
     const S* stale = (const S*)t->buf[t->cur ^ 1];
     if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
@@ -3587,7 +3603,7 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true) {
     t->sp_shrinks = 0;
     // zone buffers: the zone, and the stale source (previous stream, n_prev - Zs <= z + last_mc symbols)
     // (>= the one-workgroup zone pass's full register window, which it loads unconditionally)
-    uint64_t zneed = (gbpe_div_up((uint64_t)z + t->last_mc + 1, TILE) + 2) * TILE;
+    uint64_t zneed = (gbpe_div_up((uint64_t)z + prev_mc + 1, TILE) + 2) * TILE;
     const uint64_t zmin = (uint64_t)(t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024)) + TILE;
     if (zneed < zmin) zneed = zmin;
     if (zneed > t->zcap) {
@@ -3606,7 +3622,7 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true) {
     for (int k = 0; k < 2; ++k) TR_HIP(t, hipMemsetAsync(t->zbuf[k], 0, t->zcap * t->bps, s));
     if (z) {
         TR_HIP(t, hipMemcpyAsync(t->zbuf[0], cur + Zs, (uint64_t)z * t->bps, hipMemcpyDeviceToDevice, s));
-        uint64_t sl = (uint64_t)z + t->last_mc;
+        uint64_t sl = (uint64_t)z + prev_mc;
         if (Zs + sl > t->cap_syms) sl = t->cap_syms - Zs;
         if (sl > t->zcap) sl = t->zcap;
         TR_HIP(t, hipMemcpyAsync(t->zbuf[1], stale + Zs, sl * t->bps, hipMemcpyDeviceToDevice, s));
@@ -3657,6 +3673,7 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true) {
     TR_HIP(t, hipStreamSynchronize(s));
     t->sp = true;
     t->zcur = 0;
+    if (t->last_mc < nmc) t->last_mc = (uint32_t)nmc;   // the zone-shrink target's count until a merge runs
     ++t->sp_enters;
     t->sp_sectors = t->nsec;
     t->sp_zone = z;
@@ -3883,6 +3900,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     if (si && si->n_prev > n) {   // the last merge's count (the zone rule's mc_prev)
         init.mc = (uint32_t)(si->n_prev - n);
         t->last_mc = init.mc;
+        t->n_prev0 = si->n_prev;
     }
     memcpy(t->h_st, &init, sizeof(init));
     if (hipMemcpyAsync(t->st, t->h_st, sizeof(DevState), hipMemcpyHostToDevice, s) != hipSuccess)
@@ -4027,21 +4045,30 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         // loop can enter as soon as the zone (~7 x the next count) is a small part of
         // the stream — before the first merge; without it, once counts
         // are a 1/sp_div fraction
-        uint32_t mc = t->last_mc;
-        if (!mc && t->lex_on) {
+        // with the lexicon the decision (and the zone) follow the NEXT merge's count,
+        // the table maximum: one huge first merge (C5's (32,32), 17 % of the stream)
+        // then ends only a one-merge dense step (enter_lim below)
+        uint32_t mc = t->last_mc, next = 0;
+        if (t->lex_on) {
             if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
             hipLaunchKernelGGL(k_topcount, dim3(1), dim3(1024), 0, s, t->tb, t->d_u32);
             GBPE_LAUNCH_CHECK(t->ctx);
-            TR_HIP(t, hipMemcpyAsync(&mc, t->d_u32, 4, hipMemcpyDeviceToHost, s));
+            TR_HIP(t, hipMemcpyAsync(&next, t->d_u32, 4, hipMemcpyDeviceToHost, s));
             TR_HIP(t, hipStreamSynchronize(s));
+            mc = next;
         }
         const uint64_t div = t->lex_on ? t->lx_div : t->sp_div;
-        if (mc && ((t->flags & GBPE_TRAIN_SPARSE_EARLY) || (uint64_t)mc * div <= t->n)) {
-            const uint32_t keep = t->last_mc;
-            t->last_mc = mc;
-            int rc = t->u16 ? sp_enter<uint16_t>(t) : sp_enter<uint32_t>(t);
-            if (!t->sp) t->last_mc = keep;
+        const bool count_ok = mc && ((t->flags & GBPE_TRAIN_SPARSE_EARLY) || (uint64_t)mc * div <= t->n);
+        if (count_ok) {
+            int rc = t->u16 ? sp_enter<uint16_t>(t, true, next) : sp_enter<uint32_t>(t, true, next);
             if (rc != GBPE_OK) return rc;
+        }
+        // still dense with the lexicon on: the device ends the step once a merge's count
+        // would pass the entry test, so the loop enters at the next step boundary
+        const uint32_t lim = (!t->sp && t->lex_on && mc && !count_ok) ? (uint32_t)(t->n / div) : 0u;
+        if (lim != t->h_st->enter_lim) {
+            t->h_st->enter_lim = lim;
+            TR_HIP(t, hipMemcpyAsync(&t->st->enter_lim, &t->h_st->enter_lim, sizeof(uint32_t), hipMemcpyHostToDevice, s));
         }
     }
     // keep the zone near its minimum, then rebuild stale filters now and then
@@ -4054,6 +4081,10 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         int rc = t->u16 ? sp_filters<uint16_t>(t, wb) : sp_filters<uint32_t>(t, wb);
         if (rc != GBPE_OK) return rc;
     }
+    // waiting for the lexicon entry on a long stream: one merge per step (a dense merge
+    // costs milliseconds there; every round the step enqueues after the entry point
+    // would still launch its full-grid kernels as no-ops)
+    if (!t->sp && t->h_st->enter_lim && t->n >= (1u << 24)) k = 1;
     // a large zone shrinks every sub_k merges instead of every step (early counts fall fast)
     if (t->sp && t->n - t->h_st->B > t->sub_zone && k > t->sub_k) k = t->sub_k;
     // reset the per-step counter + budget (trainer.js:239)
@@ -4375,7 +4406,8 @@ extern "C" int gbpe_trainer_export_state(gbpe_trainer* t, uint32_t* cur, uint64_
     TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipStreamSynchronize(s));
     const uint64_t n = t->n;
-    uint64_t np = t->sharded ? (uint64_t)t->h_st->pln : (t->done ? n + t->last_mc : n);
+    // (a trainer created from a state and not stepped since re-exports the imported length)
+    uint64_t np = t->sharded ? (uint64_t)t->h_st->pln : (t->done ? n + t->last_mc : (t->n_prev0 ? t->n_prev0 : n));
     if (np > t->cap_syms) np = t->cap_syms;
     *n_cur = n;
     *n_prev = np;

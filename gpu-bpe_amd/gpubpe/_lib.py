@@ -69,6 +69,8 @@ _SIGS = [
     ("gbpe_ctx_limits", C.c_int, [C.c_void_p, u64p]),
     ("gbpe_last_error", C.c_char_p, [C.c_void_p]),
     ("gbpe_version", C.c_char_p, []),
+    ("gbpe_abi_version", C.c_int, []),
+    ("gbpe_trainer_stats_size", C.c_uint64, []),
     ("gbpe_kernel_count", C.c_int, []),
     ("gbpe_kernel_name", C.c_char_p, [C.c_int]),
     ("gbpe_word_boundary", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),

@@ -226,7 +226,9 @@ class ShardedTrainer:
             lens = self._gather_ints([n, npv])
             cap = max(1, int(lens.max()))
             send = torch.zeros(2 * cap, dtype=torch.int32, device=dev)
-            self.b.export_state_device(send.data_ptr(), send.data_ptr() + 4 * cap, cap, cap)
+            # the zero fill runs on torch's stream, the export on the library's: order them
+            torch.cuda.current_stream().synchronize()
+            self.b.export_state_device(send.data_ptr(), send.data_ptr() + 4 * cap, cap, cap)   # (synchronous)
         else:
             cur, prev = self.b.export_state()
             lens = self._gather_ints([int(cur.shape[0]), int(prev.shape[0])])
@@ -238,15 +240,16 @@ class ShardedTrainer:
                 send[cap: cap + prev.shape[0]] = torch.from_numpy(prev.view(np.int32)).to(dev)
         if self.world == 1:
             parts = [send]
-        else:
-            parts = [torch.empty_like(send) for _ in range(self.world)] if self.rank == root else None
-            self.dist.gather(send, parts, dst=root)
+        else:   # all-gather (every backend offers it; gather is not exercised over RCCL)
+            allp = self._all_gather(send).view(self.world, 2 * cap)
+            parts = [allp[q] for q in range(self.world)]
         if self.rank != root:
             return None
         if on_dev:
             gcur = torch.cat([parts[q][: lens[q, 0]] for q in range(self.world)])
             gprev = torch.cat([parts[q][cap: cap + lens[q, 1]] for q in range(self.world)])
             del parts, send
+            torch.cuda.current_stream().synchronize()   # the import reads them on the library's stream
             return make_single(gcur, gprev, next_id)
         host = [p.cpu().numpy().view(np.uint32) for p in parts]
         gcur = np.concatenate([host[q][: lens[q, 0]] for q in range(self.world)])
@@ -254,12 +257,17 @@ class ShardedTrainer:
         return make_single(gcur, gprev, next_id)
 
     def _finish_on_one(self, merges, needed, vocab_size, batch, on_progress, make_single, root):
+        """Root continues alone; every rank then receives the merge list.  A failure
+        on root (make_single, a step) is broadcast as status -1, so the other ranks
+        raise instead of waiting in the broadcast forever; root re-raises it."""
         self.consolidated_at = len(merges)
-        single = self.consolidate(make_single, vocab_size + len(merges), root)
         early = False
         flat = []
-        if self.rank == root:
-            try:
+        err = None
+        try:
+            single = self.consolidate(make_single, vocab_size + len(merges), root)
+            if self.rank == root:
+                self.single = single
                 while len(merges) < needed:
                     got, early = single.step(min(batch, needed - len(merges)))
                     merges = merges + [list(m) for m in got]
@@ -267,10 +275,16 @@ class ShardedTrainer:
                         on_progress(len(merges), needed, got)
                     if early or not got:
                         break
-            finally:
-                self.single = single
-            flat = [1 if early else 0] + [int(x) for m in merges for x in m]
+                flat = [1 if early else 0] + [int(x) for m in merges for x in m]
+        except Exception as e:  # noqa: BLE001 — reported to every rank below
+            if self.rank != root:
+                raise
+            err, flat = e, [-1]
         flat = self._bcast_ints(flat, root)
+        if err is not None:
+            raise err
+        if flat[0] < 0:
+            raise RuntimeError(f"consolidated training failed on root rank {root}")
         early = bool(flat[0])
         merges = [flat[1 + 4 * i: 5 + 4 * i] for i in range((len(flat) - 1) // 4)]
         return merges, early

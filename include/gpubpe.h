@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GBPE_ABI_VERSION 1
+#define GBPE_ABI_VERSION 2   /* 2: gbpe_trainer_stats grew (round 2), shard/state entry points */
 
 /* status codes */
 #define GBPE_OK            0
@@ -60,6 +60,10 @@ void gbpe_ctx_destroy(gbpe_ctx* ctx);
 int  gbpe_ctx_limits(gbpe_ctx* ctx, uint64_t* max_buffer_size);
 const char* gbpe_last_error(const gbpe_ctx* ctx);
 const char* gbpe_version(void);
+/* GBPE_ABI_VERSION the library was built with, and sizeof(gbpe_trainer_stats) there:
+ * a caller built against another header checks both before gbpe_trainer_stats_get */
+int gbpe_abi_version(void);
+uint64_t gbpe_trainer_stats_size(void);
 /* number of compiled kernels (engine.js:234 logs Object.keys(pipelines).length) */
 int  gbpe_kernel_count(void);
 const char* gbpe_kernel_name(int i);
@@ -244,7 +248,11 @@ int  gbpe_shard_global_len(gbpe_trainer* t, uint64_t* gn);
  * train.wgsl:605-607 + 698/727), both in the reference u32 layout (bit16 =
  * word start).  For a sharded run the global streams are the rank pieces
  * concatenated in rank order.  cur/prev NULL = lengths only; on_device != 0:
- * cur/prev are device pointers (the hand-over then never leaves HBM). */
+ * cur/prev are device pointers (the hand-over then never leaves HBM).
+ * `prev` is defined only where the next merge's stale window can read it: after
+ * the sector-sparse loop, positions below the body length at its last merge hold
+ * the body as it was at entry, not the previous stream (the window always lies in
+ * the stream's tail, so a resumed run reads the same symbols). */
 int gbpe_trainer_export_state(gbpe_trainer* t, uint32_t* cur, uint64_t cap_cur, uint64_t* n_cur,
                               uint32_t* prev, uint64_t cap_prev, uint64_t* n_prev, int on_device);
 /* A single-device trainer continuing from an exported state: opts as for

@@ -59,6 +59,18 @@ def test_kernel_inventory(lib):
     assert lib.gbpe_version().startswith(b"gpubpe")
 
 
+def test_abi_version_and_stats_layout(lib):
+    """The header's ABI version is the library's, and the ctypes mirror of
+    gbpe_trainer_stats has the C struct's size (a stale caller struct would be
+    overrun by gbpe_trainer_stats_get)."""
+    from gpubpe import _lib
+    src = open(HEADER).read()
+    want = int(re.search(r"#define GBPE_ABI_VERSION (\d+)", src).group(1))
+    assert lib.gbpe_abi_version() == want
+    assert f"abi {want}".encode() in lib.gbpe_version()
+    assert lib.gbpe_trainer_stats_size() == C.sizeof(_lib.TrainerStats)
+
+
 def test_no_device_fails_loudly(lib):
     import torch
     if torch.cuda.is_available():

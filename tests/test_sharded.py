@@ -67,9 +67,24 @@ def _worker(rank, world, port, case, outdir):
         tr.setup()
         cb = case.get("consolidate")
         below = None if cb is None else int(cb * len(data))
+
+        def make_single(c, p, nid):
+            if case.get("fail_single"):
+                raise MemoryError("simulated failure building the consolidated trainer")
+            return OracleSingle(c, p, nid, case["exact"])
+        if case.get("fail_single"):   # every rank must raise (root: the error; others: the -1 status)
+            try:
+                tr.train(case["vocab"], batch=case.get("batch", 128), consolidate_below=below,
+                         make_single=make_single, root=case.get("root", 0))
+                raised = ""
+            except Exception as e:  # noqa: BLE001
+                raised = type(e).__name__
+            with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
+                json.dump({"raised": raised}, f)
+            np.save(os.path.join(outdir, f"sym{rank}.npy"), np.zeros(0, np.uint32))
+            return
         merges, early = tr.train(case["vocab"], batch=case.get("batch", 128), consolidate_below=below,
-                                 make_single=lambda c, p, nid: OracleSingle(c, p, nid, case["exact"]),
-                                 root=case.get("root", 0))
+                                 make_single=make_single, root=case.get("root", 0))
         if tr.single is not None:   # the root holds the whole stream; the others none
             sym = tr.single.symbols()
         elif tr.consolidated_at is not None:
@@ -134,3 +149,13 @@ def test_sharded_matches_single_stream(name, world, case):
     if name.endswith("tiny_tail"):
         ev = res[0]["events"]
         assert ev["window_multi_rank"] > 0 and ev["owner_not_last"] > 0, ev
+
+
+def test_consolidation_failure_on_root_reaches_every_rank():
+    """a failure on root during consolidation must not leave the other
+    ranks blocked in the merge-list broadcast."""
+    case = dict(bytes=24_000, seed=11, fracs=[0.5], vocab=520, exact=False, cap=1 << 14, batch=32, consolidate=0.8,
+                fail_single=True)
+    res, _ = run_case(2, case)
+    assert res[0]["raised"] == "MemoryError"
+    assert res[1]["raised"] == "RuntimeError"

@@ -33,6 +33,7 @@ def main():
     out_dir = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out_dir, exist_ok=True)
     reps = int(os.environ.get("EXPLORE_REPS", "1"))
+    max_steps = int(os.environ.get("EXPLORE_MAX_STEPS", "0"))   # 0 = the whole run
     for name in sys.argv[1:]:
         gen, vocab, flags = CONFIGS[name]
         t = time.time()
@@ -61,7 +62,7 @@ def main():
                 if len(steps) % 32 == 0:
                     print(f"[{name}] step {len(steps)} merges {len(merges) // 4} "
                           f"{time.perf_counter() - t1:.2f}s", flush=True)
-                if nd.value == 0 or es.value:
+                if nd.value == 0 or es.value or (max_steps and len(steps) >= max_steps):
                     break
             t2 = time.perf_counter()
             st = _lib.TrainerStats()
