@@ -1,0 +1,2757 @@
+// Device side of the training loop (kernels, loop state, pair table, LDS tables,
+// the sector-sparse loop and the word lexicon), shared by the translation units
+// train.hip (single-device trainer), train_shard.hip (sharded protocol) and
+// train_lexshard.hip (sharded first pass + lexicon hand-over).  Every kernel
+// lives in an anonymous namespace: each unit compiles the instances it launches.
+#pragma once
+
+#include "common.h"
+#include "scan.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+
+namespace {
+
+constexpr int TPB = 256;              // threads per block
+constexpr int EPT = 32;               // symbols per thread in a tile
+constexpr int TILE = TPB * EPT;       // 8192 symbols per tile (16 KiB of u16 in flight per workgroup)
+constexpr int LTAB = 2048;            // LDS delta table slots (tail window)
+constexpr int LTAB_FULL = 8192;       // LDS table slots for the full recount
+constexpr int LPROBE = 24;            // LDS probes before spilling to the global table
+constexpr uint32_t BLK_LOG2 = 8;      // 256 table slots per argmax block: one wave re-maxes one (2 x 16 B per lane)
+constexpr int SEL_THREADS = 1024;
+
+template <typename S> struct Sym;
+template <> struct Sym<uint16_t> { static constexpr uint32_t WS = 0x8000u, TM = 0x7FFFu; };
+template <> struct Sym<uint32_t> { static constexpr uint32_t WS = 0x10000u, TM = 0xFFFFu; };
+
+// device-side loop state (the reference's IterState, train.wgsl:45-58)
+struct DevState {
+    uint32_t n;            // current symbol count
+    uint32_t stop;         // early stop (mc < 2 or id > 0xFFFF)
+    uint32_t next_id;
+    uint32_t a, b, nw;     // merge pair and new id
+    uint32_t mc;           // its count
+    uint32_t new_n;        // n - mc
+    uint32_t m;            // survivors with old index >= new_n (tail window size)
+    uint32_t merges_done;  // in this step (reset by the host, trainer.js:239)
+    uint32_t used;         // occupied table slots
+    uint32_t ndirty;       // dirty-block list length
+    uint32_t err;          // error bits
+    uint32_t valid_total;  // zone: survivors + 1 (zone_one → k_refresh's layout check)
+    uint32_t budget;       // merges allowed in this step
+    uint32_t live;         // distinct pairs with count > 0 at the last select
+    uint64_t tail_total;   // sum of m
+    uint32_t max_live;     // max of `live` over all selects
+    uint32_t epoch;        // merge sequence number
+    // ── sharded training (gbpe_shard_*); n / new_n above are then LOCAL: the
+    //    local stream length and the local keep limit ──
+    uint32_t sharded, rank, world, stall;
+    uint32_t dused;        // occupied slots of the per-merge delta table
+    uint32_t dcount;       // delta entries of this merge (the record's list length)
+    uint32_t need_l, need_w;   // capacities a stalled merge asked for (max over ranks)
+    uint32_t owner;        // rank that appended this merge's stale window
+    uint32_t nl_next;      // local length after this merge
+    uint32_t m_glob;       // global stale-window length of this merge
+    uint32_t pln;          // local length of the previous input stream (stale-window source)
+    uint64_t gn;           // global stream length
+    uint64_t off;          // global offset of the local stream
+    uint64_t poff;         // global offset of the previous input stream
+    uint64_t off_next;
+    uint64_t gnew;         // gn - mc
+    uint32_t peak_l, peak_w;   // largest record list / window piece of this step (capacity sizing)
+    uint32_t dfull;            // the delta table overflowed this merge
+    // ── sector-sparse loop (n / new_n above stay GLOBAL; the zone has its own DevState) ──
+    uint32_t B;            // body length: symbols in the word-aligned sectors before the zone
+    uint32_t Bp;           // body length during the previous merge (stale-window source offset)
+    uint32_t body_rm;      // B-sides removed from the body by this merge
+    uint32_t sp_abort;     // a selected merge does not fit the zone: not run, host goes dense
+    uint32_t sel_round;    // sector-sparse: round + 1 of the merge k_body selected
+    uint64_t sp_bytes;     // sector-sparse: bytes moved by the multi-tile zone passes (k_refresh adds them)
+    uint32_t zlast;        // sector-sparse: zone length of the rank that holds the zone (global knowledge)
+    uint32_t ln_last;      // sharded: the last rank's local length after the last merge (from the records)
+    uint32_t is_last;      // sector-sparse: this rank holds the zone (single GPU: always)
+    uint32_t cand;         // candidate sectors of this merge (trace)
+    uint32_t hitsec;       // sectors with a site (trace)
+    uint32_t mc_prev;      // sector-sparse, single GPU: the last merge's count (k_refresh), for the zone rule
+                           // (never written by a commit: a reader beside k_body would see it unchanged)
+    uint32_t enter_lim;    // dense loop: end the step at the first merge whose count is <= this (the host
+                           // can then enter the sector-sparse loop; 0 = off)
+};
+static_assert(sizeof(DevState) <= 256, "state");
+
+// the zone segments' per-merge hand-off (zone_seg; k_refresh zeroes it)
+constexpr uint32_t NSEG_MAX = 64;   // one sweeping wave: one lane per segment
+constexpr uint32_t ZSEG_SPIN = 1u << 22;
+struct ZSegState {
+    uint32_t ticket;
+    uint32_t pad[15];
+    unsigned long long gran[NSEG_MAX][4];   // {1, kept}, {1, tail survivors}, {1, last kept | has kept << 31}
+};
+constexpr uint32_t ZSEG_WORDS = 16 + NSEG_MAX * 8;   // u32 words k_refresh zeroes (ticket, granules)
+
+// Phase timestamps of the sector-sparse kernels (diagnostic builds only:
+// -DGBPE_KTRACE; tools/ktrace.sh).  Every KT_EVERY-th merge, each workgroup
+// stores its own wall-clock stamps (plain stores, no shared counters that
+// would serialise the launch): k_body workgroups at [m][wg][slot], k_refresh
+// workgroups at [m][KT_WG + wg][slot].
+#ifdef GBPE_KTRACE
+constexpr uint32_t KT_MERGES = 40000, KT_EVERY = 16, KT_WG = 2048, KT_SLOTS = 12;
+// __constant__: scalar loads the compiler can hoist, so a stamp is a clock read
+// and a store (a __device__ global reloads with a vmcnt wait per stamp, which
+// drained the wave's outstanding stores and inflated every phase by ~1 µs)
+__constant__ unsigned long long* g_ktr;
+__constant__ uint32_t g_kt_base;
+__device__ __forceinline__ void kt_put(uint32_t round, uint32_t wg, int i, unsigned long long v) {
+    const uint32_t m = g_kt_base + round;
+    if (g_ktr && m < KT_MERGES && m % KT_EVERY == 0 && wg < 2 * KT_WG)
+        g_ktr[((uint64_t)(m / KT_EVERY) * 2 * KT_WG + wg) * KT_SLOTS + i] = v;
+}
+#define KT(i) kt_put(round, blockIdx.x, (i), wall_clock64())
+#define KTV(i, v) kt_put(round, blockIdx.x, (i), (v))
+#define KTR(i) kt_put(round, KT_WG + blockIdx.x, (i), wall_clock64())
+#define TKT(i) kt_put(r, 1u, (i), wall_clock64())   // k_tail's own phases (workgroup slot 1)
+#define TKTV(i, v) kt_put(r, 1u, (i), (v))
+#else
+#define TKT(i) ((void)0)
+#define TKTV(i, v) ((void)0)
+#define KT(i) ((void)0)
+#define KTV(i, v) ((void)0)
+#define KTR(i) ((void)0)
+#endif
+
+// exchange-record header words of sharded training (gpubpe/sharded.py mirrors them)
+enum : uint32_t {
+    H_ACTIVE = 0, H_L, H_KEPT, H_M, H_W, H_LASTSYM, H_HASLAST, H_SURV, H_LN, H_MC, H_A, H_B, H_ID, H_DFULL,
+    H_ZN = 14,             // sector-sparse records: the zone length after the merge (last rank), its window m
+    H_ZM = 15, HDR = 16
+};
+
+enum : uint32_t {
+    ERR_TABLE_FULL = 1, ERR_COUNT_MISMATCH = 2, ERR_PAIR_MISSING = 4, ERR_SPIN = 8,
+    ERR_SHARD_CAPACITY = 16,   // a rank's stream outgrew its buffers (stale window appended)
+    ERR_SHARD_RECORD = 32,     // exchange records disagree (ranks out of step)
+    ERR_SHARD_LAYOUT = 64,     // gathered survivor / length totals do not add up
+    ERR_SPARSE_WINDOW = 128    // sector-sparse: a stale window reaches past the zone's stale buffer
+};
+
+struct Table {
+    uint2* slots;      // .x = pid (0 = empty), .y = count (u32, wraps for transient negatives)
+    uint32_t mask;     // slots - 1
+    uint64_t* bmax;    // per block: (count << 32) | ~pid, 0 when empty
+    uint32_t* dirty;   // per block flag
+    uint32_t* dlist;   // dirty block list
+    uint32_t* blive;   // per block: entries with count > 0
+    uint32_t nblk;
+    uint32_t* used;    // occupied-slot counter (DevState::used or ::dused)
+    uint32_t* full;    // non-null: a full table sets *full instead of the fatal error (delta table)
+};
+
+// a touched block is re-maxed by the next k_refresh: a plain flag store, nothing waits on it
+__device__ __forceinline__ void mark_dirty(const Table& tb, DevState* st, uint32_t slot) {
+    (void)st;
+    tb.dirty[slot >> BLK_LOG2] = 1u;
+}
+
+// global insert-or-add (triangular probing visits every slot of a 2^k table)
+__device__ void table_add(const Table& tb, DevState* st, uint32_t pid, uint32_t delta) {
+    uint32_t h = gbpe_fmix32(pid) & tb.mask;
+    for (uint32_t p = 0; p <= tb.mask; ++p) {
+        uint32_t idx = (h + ((p * (p + 1)) >> 1)) & tb.mask;
+        uint32_t k = __hip_atomic_load(&tb.slots[idx].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == 0u) {
+            k = atomicCAS(&tb.slots[idx].x, 0u, pid);
+            if (k == 0u) {
+                if (tb.used) __hip_atomic_fetch_add(tb.used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                k = pid;
+            }
+        }
+        if (k == pid) {
+            atomicAdd(&tb.slots[idx].y, delta);
+            mark_dirty(tb, st, idx);
+            return;
+        }
+    }
+    if (tb.full) *tb.full = 1u;   // per-merge delta table sized too small: the merge stalls and retries bigger
+    else atomicOr(&st->err, ERR_TABLE_FULL);
+}
+
+__device__ uint32_t table_find(const Table& tb, uint32_t pid) {
+    uint32_t h = gbpe_fmix32(pid) & tb.mask;
+    for (uint32_t p = 0; p <= tb.mask; ++p) {
+        uint32_t idx = (h + ((p * (p + 1)) >> 1)) & tb.mask;
+        uint32_t k = tb.slots[idx].x;
+        if (k == pid) return idx;
+        if (k == 0u) return 0xFFFFFFFFu;
+    }
+    return 0xFFFFFFFFu;
+}
+
+// per-workgroup LDS aggregation of (pid, delta)
+template <int N>
+struct LdsTab {
+    uint32_t key[N];
+    uint32_t val[N];
+    uint32_t ovf;   // an add went straight to the global table (k_tail re-maxes every dirty block then)
+};
+
+template <int N>
+__device__ __forceinline__ void lds_clear(LdsTab<N>& t) {
+    for (int i = threadIdx.x; i < N; i += blockDim.x) { t.key[i] = 0u; t.val[i] = 0u; }
+    if (threadIdx.x == 0) t.ovf = 0u;
+}
+
+template <int N>
+__device__ __forceinline__ void lds_add(LdsTab<N>& t, const Table& tb, DevState* st, uint32_t pid, uint32_t d) {
+    uint32_t h = gbpe_fmix32(pid);
+#pragma unroll 1
+    for (int p = 0; p < LPROBE; ++p) {
+        uint32_t idx = (h + (uint32_t)((p * (p + 1)) >> 1)) & (N - 1);
+        uint32_t k = atomicCAS(&t.key[idx], 0u, pid);
+        if (k == 0u || k == pid) {
+            atomicAdd(&t.val[idx], d);
+            return;
+        }
+    }
+    t.ovf = 1u;
+    table_add(tb, st, pid, d);   // LDS table crowded: go straight to the global table
+}
+
+// Up to 8 (pid, delta) adds with their home-slot key loads issued together: at
+// the table's low load factor nearly every live pair sits in its home slot, so
+// a batch costs one round trip instead of one per entry; the rest (new keys,
+// collisions) take the full probe.  Entries with pid or delta 0 are skipped.
+__device__ __forceinline__ void table_add8(const Table& tb, DevState* st, const uint32_t (&kk)[8],
+                                           const uint32_t (&vv)[8]) {
+    uint32_t hs[8], hk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        hs[j] = (kk[j] && vv[j]) ? (gbpe_fmix32(kk[j]) & tb.mask) : 0u;
+        hk[j] = __hip_atomic_load(&tb.slots[hs[j]].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (!kk[j] || !vv[j]) continue;
+        if (hk[j] == kk[j]) {
+            atomicAdd(&tb.slots[hs[j]].y, vv[j]);
+            mark_dirty(tb, st, hs[j]);
+        } else {
+            table_add(tb, st, kk[j], vv[j]);
+        }
+    }
+}
+
+// Flush the workgroup's aggregated deltas into the global table.  Small tables
+// (<= 8 slots per thread) are first compacted to a list so every thread does at
+// most a few global adds instead of one per slot it owns: a merge's few live
+// entries then cost one global round trip, not a serial chain.  Large tables
+// (the multi-tile and zone k_delta, the full count) add in batches of 8 per
+// thread (table_add8).  The table's contents are consumed (callers clear it
+// before reuse).
+template <int N>
+__device__ __forceinline__ void lds_flush(LdsTab<N>& t, const Table& tb, DevState* st) {
+    __syncthreads();
+    const uint32_t nt = blockDim.x;
+    if (N > 8 * (int)nt) {
+        for (uint32_t i0 = threadIdx.x; i0 < (uint32_t)N; i0 += 8 * nt) {
+            uint32_t kk[8], vv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t i = i0 + j * nt;
+                kk[j] = i < (uint32_t)N ? t.key[i] : 0u;
+                vv[j] = i < (uint32_t)N ? t.val[i] : 0u;
+            }
+            table_add8(tb, st, kk, vv);
+        }
+        return;
+    }
+    __shared__ uint32_t s_cnt;
+    uint32_t kk[8], vv[8], live = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t i = threadIdx.x + j * nt;
+        kk[j] = i < (uint32_t)N ? t.key[i] : 0u;
+        vv[j] = i < (uint32_t)N ? t.val[i] : 0u;
+        if (kk[j] && vv[j]) live |= 1u << j;
+    }
+    if (threadIdx.x == 0) s_cnt = 0u;
+    __syncthreads();
+    uint32_t off = live ? atomicAdd(&s_cnt, (uint32_t)__popc(live)) : 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if ((live >> j) & 1u) {
+            t.key[off] = kk[j];
+            t.val[off] = vv[j];
+            ++off;
+        }
+    __syncthreads();
+    const uint32_t total = s_cnt;
+    for (uint32_t i = threadIdx.x; i < total; i += nt) table_add(tb, st, t.key[i], t.val[i]);
+}
+
+template <typename S>
+__device__ __forceinline__ void load_tile(const S* __restrict__ cur, uint64_t base, S* __restrict__ tile) {
+    // 16 symbols per thread, 16-byte vector loads (buffers are padded to whole tiles)
+    constexpr int V = EPT * sizeof(S) / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(cur + base) + threadIdx.x * V;
+    uint4* dst = reinterpret_cast<uint4*>(tile) + threadIdx.x * V;
+#pragma unroll
+    for (int v = 0; v < V; ++v) dst[v] = src[v];
+}
+
+// ─── kernels ────────────────────────────────────────────────────────────────
+
+// bpe_word_boundary (train.wgsl:111-186) fused with byte→symbol widening
+// (trainer.js:49-53) and external-mask tagging (trainer.js:115-121).
+__device__ __forceinline__ uint32_t byte_class(uint32_t t) {
+    if (t == 0x0Au) return 4u;
+    if (t == 0x20u) return 2u;
+    if (t - 0x30u <= 9u) return 1u;
+    if (t >= 0x80u) return 0u;
+    if ((t | 0x20u) - 0x61u <= 25u) return 0u;
+    return 3u;
+}
+
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_symbols(const uint8_t* __restrict__ bytes, const uint8_t* __restrict__ ws_ext,
+                                                 S* __restrict__ out, uint64_t n, uint8_t* __restrict__ ws_out) {
+    uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    uint32_t tok = bytes[i];
+    bool ws;
+    if (ws_ext) {
+        ws = ws_ext[i] != 0;
+    } else if (i == 0) {
+        ws = true;
+    } else {
+        uint32_t c = byte_class(tok), p = byte_class(bytes[i - 1]);
+        ws = c != p;
+        if (p == 2u && (c == 0u || c == 1u)) ws = false;
+        if (c == 2u && p != 2u) ws = true;
+        if (p == 4u || c == 4u) ws = true;
+    }
+    if (out) out[i] = (S)(tok | (ws ? Sym<S>::WS : 0u));
+    if (ws_out) ws_out[i] = ws ? 1 : 0;
+}
+
+// Full pair count of the current stream into the (cleared) table — once at
+// start and on table rebuilds.  Same counting rule as train.wgsl:393-399.
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_count_full(DevState* st, const S* __restrict__ cur, Table tb) {
+    __shared__ LdsTab<LTAB_FULL> lt;
+    __shared__ __attribute__((aligned(16))) S tile[TILE];
+    __shared__ S prev_last;
+    lds_clear(lt);
+    const uint32_t n = st->n;
+    const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
+    for (uint32_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+        const uint64_t base = (uint64_t)tl * TILE;
+        __syncthreads();
+        load_tile(cur, base, tile);
+        if (threadIdx.x == 0) prev_last = base ? cur[base - 1] : (S)0;
+        __syncthreads();
+#pragma unroll 1
+        for (int k = 0; k < EPT; ++k) {
+            int li = threadIdx.x * EPT + k;
+            uint64_t i = base + li;
+            if (i == 0 || i >= n) continue;
+            uint32_t x1 = tile[li];
+            uint32_t x0 = li ? (uint32_t)tile[li - 1] : (uint32_t)prev_last;
+            uint32_t t0 = x0 & Sym<S>::TM, t1 = x1 & Sym<S>::TM;
+            if (!(x1 & Sym<S>::WS) && t0 && t1) lds_add(lt, tb, st, (t0 << 16) | t1, 1u);
+        }
+    }
+    lds_flush(lt, tb, st);
+}
+
+__device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log, uint32_t* __restrict__ grpsum,
+                             uint32_t* __restrict__ nlog, uint32_t* __restrict__ rec, DevState* zst, uint32_t exact);
+
+// (unused launch argument: the selection fused into k_refresh was measured slower)
+struct FusedSel {
+    uint32_t* log = nullptr;
+    uint32_t* grpsum = nullptr;
+    uint32_t exact = 0;
+};
+
+// recompute block maxima for dirty blocks; with `finish`, also closes the
+// merge of `round` (state.symbol_count := new count, train.wgsl:605-607)
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, int finish, Table tb, S* __restrict__ cur,
+                                                 const uint32_t* __restrict__ rwlist, DevState* zst,
+                                                 uint32_t* __restrict__ clog = nullptr, FusedSel fs = FusedSel(),
+                                                 uint64_t* __restrict__ part = nullptr, uint32_t* __restrict__ zseg = nullptr) {
+    (void)cur;
+    if (zseg && blockIdx.x == 0)   // ZSegState: ticket + granules of the next merge's zone segments
+        for (uint32_t i = threadIdx.x; i < ZSEG_WORDS; i += TPB)
+            if (i == 0 || i >= 16) zseg[i] = 0u;
+    (void)rwlist;
+    if (part && finish == 2 && threadIdx.x == 0) KTR(0);
+    // finish == 2: the sector-sparse loop, whose merge was selected inside k_body
+    // (sel_inline): the step counters move on here
+    // block 0 closes the merge from one snapshot of both states: every field is
+    // read (one round trip) before any is written, not one round trip per field
+    if (finish && blockIdx.x == 0) {
+        constexpr int NW = sizeof(DevState) / 4;
+        __shared__ union {
+            DevState d;
+            uint32_t w[NW];
+        } s_g, s_z;
+        if (threadIdx.x < NW) s_g.w[threadIdx.x] = reinterpret_cast<const uint32_t*>(st)[threadIdx.x];
+        else if (zst && threadIdx.x < 2 * NW) s_z.w[threadIdx.x - NW] = reinterpret_cast<const uint32_t*>(zst)[threadIdx.x - NW];
+        __syncthreads();
+        const DevState& g = s_g.d;
+        const DevState& z = s_z.d;
+        const bool fin = finish == 2 ? (!g.stop && !g.sp_abort && g.sel_round == round + 1u)
+                                     : (!g.stop && !g.stall && g.merges_done == round + 1u);
+        if (fin && threadIdx.x == 0) {
+            if (zst) {   // sector-sparse: global length, body length, zone length
+                if (finish == 2) {
+                    st->merges_done = round + 1u;
+                    st->next_id = g.next_id + 1u;
+                    st->epoch = g.epoch + 1u;
+                    st->mc_prev = g.mc;
+                }
+                if (clog) {
+                    clog[2 * round] = g.cand;
+                    clog[2 * round + 1] = g.hitsec;
+                }
+                st->cand = 0u;
+                st->hitsec = 0u;
+                st->tail_total = g.tail_total + z.m;
+                const uint32_t n = g.new_n, B = g.B - g.body_rm, zn = n - B;
+                st->n = n;
+                st->Bp = g.B;
+                st->B = B;
+                st->body_rm = 0u;
+                zst->n = zn;
+                if (!g.sharded) st->zlast = zn;   // sharded: from the records (k_shard_apply)
+                if (!z.valid_total && g.is_last)   // multi-tile zone: k_delta + k_compact stream it twice, plus the window copy
+                    st->sp_bytes = g.sp_bytes + (uint64_t)sizeof(S) * (2ull * z.n + zn + 2ull * g.mc);
+                if (z.valid_total && z.valid_total != zn + 1u) atomicOr(&st->err, ERR_COUNT_MISMATCH);
+            } else if (g.sharded) {   // commit the new global layout computed by k_shard_recv
+                st->tail_total = g.tail_total + g.m_glob;
+                st->poff = g.off;
+                st->pln = g.n;
+                st->n = g.nl_next;
+                st->off = g.off_next;
+                st->gn = g.gnew;
+            } else {
+                st->tail_total = g.tail_total + g.m;
+                st->n = g.new_n;
+            }
+        }
+    }
+    // this WG's contiguous run of blocks (<= 64): all flags (and, for `part`, the
+    // maxima kept from before) in one load; then every wave re-maxes its share of
+    // the dirty ones, one 256-slot block at a time (no workgroup barrier per block:
+    // a merge dirties a few blocks per workgroup, each holding a few live pairs)
+    __shared__ uint64_t s_dmask;
+    __shared__ uint64_t s_bm[64];
+    const uint32_t per = (tb.nblk + gridDim.x - 1) / gridDim.x;   // <= 64 (host-sized grid)
+    const uint32_t b0 = blockIdx.x * per;
+    if (threadIdx.x < 64) {
+        const uint32_t blk = b0 + threadIdx.x;
+        const bool in = threadIdx.x < per && blk < tb.nblk;
+        if (part) s_bm[threadIdx.x] = in ? tb.bmax[blk] : 0ull;
+        const bool d = in && tb.dirty[blk];
+        const unsigned long long m = __ballot(d);
+        if (threadIdx.x == 0) s_dmask = m;
+    }
+    __syncthreads();
+    {
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        constexpr int NV = (1 << BLK_LOG2) / 2 / 64;   // 16-byte loads per lane
+        uint64_t dm = s_dmask;
+        for (int k = 0; dm; ++k) {   // (wave-uniform)
+            const uint32_t bit = (uint32_t)(__ffsll((long long)dm) - 1);
+            dm &= dm - 1;
+            if ((k & (TPB / 64 - 1)) != wid) continue;
+            const uint32_t blk = b0 + bit;
+            const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)blk << BLK_LOG2));
+            uint4 e[NV];
+#pragma unroll
+            for (int q = 0; q < NV; ++q) e[q] = sl[lane + q * 64];
+            uint64_t best = 0;
+            uint32_t live = 0;
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                if (e[q].x && (int32_t)e[q].y > 0) {
+                    const uint64_t key = ((uint64_t)e[q].y << 32) | (uint32_t)(~e[q].x);
+                    best = key > best ? key : best;
+                    ++live;
+                }
+                if (e[q].z && (int32_t)e[q].w > 0) {
+                    const uint64_t key = ((uint64_t)e[q].w << 32) | (uint32_t)(~e[q].z);
+                    best = key > best ? key : best;
+                    ++live;
+                }
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint64_t o = __shfl_xor(best, off);
+                best = o > best ? o : best;
+                live += __shfl_xor(live, off);
+            }
+            if (lane == 0) {
+                tb.bmax[blk] = best;
+                tb.blive[blk] = live;
+                tb.dirty[blk] = 0u;
+                s_bm[bit] = best;
+            }
+        }
+    }
+    __syncthreads();
+    if (part && threadIdx.x < 64) {   // this workgroup's maximum, for sel_inline
+        uint64_t best = s_bm[threadIdx.x];
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(best, off);
+            best = o > best ? o : best;
+        }
+        if (threadIdx.x == 0) {
+            part[blockIdx.x] = best;
+            if (finish == 2) KTR(5);
+        }
+    }
+}
+
+constexpr uint32_t GRP = 64;    // tiles per group sum (two-level tile prefix)
+constexpr uint32_t GSTR = 64;   // group sums 256 B apart: each is its own atomic serialisation point
+
+// argmax over block maxima + the reference's bpe_setup_merge (train.wgsl:340-364),
+// by one workgroup of any size <= SEL_THREADS
+__device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log, uint32_t* __restrict__ grpsum,
+                             uint32_t* __restrict__ nlog, uint32_t* __restrict__ rec, DevState* zst, uint32_t exact) {
+    __shared__ uint64_t red[SEL_THREADS / 64];
+    __shared__ uint32_t rlive[SEL_THREADS / 64];
+    const uint32_t nt = blockDim.x;
+    if (rec && threadIdx.x == 0) rec[H_L] = 0u;   // the send kernel's list blocks add their counts into it
+    if (st->stop || st->stall || st->sp_abort) return;
+    {   // group sums of the coming stream pass (the zone's, when sector-sparse) start at zero
+        const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(zst ? zst->n : st->n, TILE), GRP);
+        for (uint32_t g = threadIdx.x; g < ngrp; g += nt) grpsum[g * GSTR] = 0u;
+    }
+    uint64_t best = 0;
+    uint32_t live = 0;
+    for (uint32_t i = threadIdx.x; i < tb.nblk; i += nt) {
+        uint64_t v = tb.bmax[i];
+        best = v > best ? v : best;
+        live += tb.blive[i];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        uint64_t o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+        live += __shfl_xor(live, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = best;
+        rlive[threadIdx.x >> 6] = live;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (uint32_t w = 1; w < nt / 64; ++w) {
+        best = red[w] > best ? red[w] : best;
+        live += rlive[w];
+    }
+    st->live = live;
+    if (live > st->max_live) st->max_live = live;
+    st->ndirty = 0u;
+    st->m = 0u;
+    st->dcount = 0u;
+    st->dused = 0u;
+    st->dfull = 0u;
+    st->valid_total = 0u;
+    const uint32_t mc = (uint32_t)(best >> 32);
+    const uint32_t pid = ~(uint32_t)best;
+    if (st->merges_done >= st->budget) {   // host asked for fewer merges this step
+        return;
+    }
+    if (!zst && st->enter_lim && mc <= st->enter_lim && st->merges_done > 0u) {
+        // counts fell far enough for the word-lexicon loop: end the step here so the
+        // host enters it (C5's first count is 17 % of the stream, its second 0.6 %)
+        return;
+    }
+    if (mc < 2u || st->next_id > 0xFFFFu) {   // train.wgsl:345-348
+        st->stop = 1u;
+        return;
+    }
+    if (zst && !exact) {
+        // sector-sparse zone invariants: this merge's stale window
+        // [new_n - m, new_n) of the previous stream lies in the zone's stale buffer
+        // (n - 2mc >= Bp), and the zone stays >= 5 mc long so the next merge's window
+        // does too (its count is <= mc + m <= 2 mc).  Otherwise the merge is not run
+        // and the host returns to the dense loop.
+        if ((uint64_t)st->n < 2ull * mc + st->Bp) {   // cannot happen after the check below held
+            atomicOr(&st->err, ERR_SPARSE_WINDOW);
+            st->stop = 1u;
+            return;
+        }
+        if ((uint64_t)zst->n < 5ull * mc + 2u) {
+            st->sp_abort = 1u;
+            return;
+        }
+    }
+    const uint32_t idx = table_find(tb, pid);
+    if (idx == 0xFFFFFFFFu) {
+        atomicOr(&st->err, ERR_PAIR_MISSING);
+        st->stop = 1u;
+        return;
+    }
+    tb.slots[idx].y = 0u;                  // every (a,b) occurrence is a merge site
+    tb.dirty[idx >> BLK_LOG2] = 1u;
+    const uint32_t d = st->merges_done;
+    log[d * 4 + 0] = pid >> 16;
+    log[d * 4 + 1] = pid & 0xFFFFu;
+    log[d * 4 + 2] = st->next_id;
+    log[d * 4 + 3] = mc;
+    st->a = pid >> 16;
+    st->b = pid & 0xFFFFu;
+    st->nw = st->next_id;
+    st->mc = mc;
+    if (st->sharded) {   // global new length; the local keep limit (train.wgsl:727 on the global stream)
+        const uint64_t gnew = st->gn - mc;
+        st->gnew = gnew;
+        uint64_t lim = st->n;
+        if (!(st->sharded & 2u)) lim = gnew > st->off ? (gnew - st->off < st->n ? gnew - st->off : st->n) : 0u;
+        st->new_n = (uint32_t)lim;
+    } else {
+        st->new_n = st->n - mc;
+    }
+    if (nlog) nlog[d] = st->n;
+    if (zst) {   // the zone's view of the merge: k_delta / k_compact run on it unchanged
+        zst->a = st->a;
+        zst->b = st->b;
+        zst->nw = st->nw;
+        zst->mc = mc;
+        zst->new_n = exact ? zst->n : zst->n - mc;   // zone keep limit: global new_n - B
+        zst->m = 0u;
+        zst->valid_total = 0u;
+        zst->merges_done = d + 1u;
+        st->body_rm = 0u;
+        st->cand = 0u;
+        st->hitsec = 0u;
+    }
+    st->next_id += 1u;
+    st->epoch += 1u;
+    st->merges_done = d + 1u;
+}
+
+__global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, uint32_t* __restrict__ log,
+                                                        uint32_t* __restrict__ grpsum, uint32_t* __restrict__ nlog,
+                                                        uint32_t* __restrict__ rec, DevState* zst, uint32_t exact) {
+    select_merge(st, tb, log, grpsum, nlog, rec, zst, exact);
+}
+
+// the next merge's count (the table maximum): the sparse entry decision before any merge ran
+__global__ __launch_bounds__(1024) void k_topcount(Table tb, uint32_t* __restrict__ out) {
+    __shared__ uint64_t red[16];
+    uint64_t best = 0;
+    for (uint32_t i = threadIdx.x; i < tb.nblk; i += 1024) {
+        const uint64_t v = tb.bmax[i];
+        best = v > best ? v : best;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) best = red[w] > best ? red[w] : best;
+        *out = (uint32_t)(best >> 32);
+    }
+}
+
+// live pairs (count > 0) from the per-block live counts k_refresh keeps, once per
+// sparse step (the dense loop's k_select counts them every merge)
+__global__ __launch_bounds__(1024) void k_live(DevState* st, Table tb) {
+    __shared__ uint32_t red[16];
+    uint32_t live = 0;
+    for (uint32_t i = threadIdx.x; i < tb.nblk; i += 1024) live += tb.blive[i];
+    for (int off = 32; off > 0; off >>= 1) live += __shfl_xor(live, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = live;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) live += red[w];
+        st->live = live;
+        if (live > st->max_live) st->max_live = live;
+    }
+}
+
+// A merge is "active" for the stream kernels iff k_select logged it this round.
+__device__ __forceinline__ bool merge_active(const DevState* st, uint32_t round) {
+    return !st->stop && st->merges_done == round + 1u;
+}
+
+template <typename S>
+__device__ __forceinline__ void load_own(const S* cur, uint64_t i0, uint32_t* __restrict__ x) {
+    constexpr int V = EPT * sizeof(S) / 16;
+    uint4 v[V];
+    const uint4* src = reinterpret_cast<const uint4*>(cur + i0);
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = src[k];
+    const S* e = reinterpret_cast<const S*>(v);
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) x[k] = e[k];
+}
+
+constexpr int LTAB_T = 1024;          // per-workgroup LDS delta table of k_body / the zone pass
+constexpr int LTAB_Z = 4096;          // k_delta on a sparse zone: its stale tail holds many distinct pairs
+
+
+__device__ __forceinline__ uint32_t lane_mask32(uint64_t i0, uint64_t lim) {
+    // bits k with i0 + k < lim, k < 32
+    return i0 >= lim ? 0u : (i0 + 32 <= lim ? 0xFFFFFFFFu : ((1u << (uint32_t)(lim - i0)) - 1u));
+}
+
+// Pass 1 (one tile of TILE symbols per workgroup): merge-site mask, survivor
+// count per tile, count deltas.
+//   hit(i)  = (i >= 1) && !ws(i) && tok(i-1) == a && tok(i) == b     (B-side, train.wgsl:491-497)
+//   rw(i)   = hit(i+1)                                               (A-side, train.wgsl:482-485)
+//   survivor(i) = !hit(i)
+// Old pair at i is destroyed iff hit(i-1)|hit(i)|hit(i+1) or i >= limit (stale tail);
+// new pair at a survivor i < limit: hit(i-1) → (nw, tok'(i)); else hit(i+1) → (tok(i-1), nw).
+// The tile (32 symbols per lane + the 2 before + 1 after) is loaded before the
+// loop state is read, so the state's scalar load overlaps the HBM latency.  Lanes
+// with no site within reach and no tail element do no delta work; a tile with no
+// such lane passes a single barrier.
+// STAGE (the sector-sparse zone: few tiles, latency-bound): the work loop reads
+// the lane's symbols from an LDS copy instead of re-reading L2 per position.
+template <typename S, bool EXACT, bool STAGE = false>
+__global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, const S* cur, Table tb,
+                                               uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
+                                               uint32_t* __restrict__ grpsum, uint32_t eager_tiles,
+                                               uint32_t ngroups = 0xFFFFFFFFu) {
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    __shared__ LdsTab<STAGE ? LTAB_Z : LTAB_T> lt;
+    __shared__ uint32_t stg[STAGE ? EPT * TPB : 1];
+    __shared__ uint32_t red[TPB / 64], s_workw[TPB / 64];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t tl = blockIdx.x;
+    if (tl >= ngroups) {   // a stale-tail slice block (as in k_delta_mt); tiles skip their tail loop
+        const uint4 s0 = reinterpret_cast<const uint4*>(st)[0];
+        const uint4 s1 = reinterpret_cast<const uint4*>(st)[1];
+        const uint2 s2 = reinterpret_cast<const uint2*>(st)[4];
+        const uint32_t n = s0.x, lim = s1.w, pid_ab = (s0.w << 16) | s1.x;
+        if (EXACT || s0.y || s2.y != round + 1u || n <= lim) return;
+        const uint32_t nt2 = gridDim.x - ngroups, q = tl - ngroups;
+        const uint32_t len = n - lim, per = (len + nt2 - 1) / nt2;
+        const uint64_t a0 = (uint64_t)lim + (uint64_t)q * per;
+        const uint64_t a1 = a0 + per < (uint64_t)n ? a0 + per : (uint64_t)n;
+        if (a0 >= a1) return;
+        lds_clear(lt);
+        __syncthreads();
+        for (uint64_t i = a0 + t; i < a1; i += TPB) {
+            if (i == 0) continue;
+            const uint32_t xi = cur[i];
+            if (xi & WS) continue;
+            const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
+            if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        }
+        lds_flush(lt, tb, st);
+        return;
+    }
+    // tiles past the host's view of the stream (a shard that may have grown by an
+    // appended window) check the length before loading anything
+    if (tl >= eager_tiles && (uint64_t)tl * TILE >= st->n) return;
+    const uint64_t base = (uint64_t)tl * TILE;
+    const uint64_t i0 = base + (uint64_t)t * EPT;
+    // loads first, unconditionally (buffers are padded: every launched tile is in
+    // bounds); the compiler barrier keeps them ahead of the state's scalar loads
+    // so both round trips overlap
+    uint32_t x[EPT];
+    uint32_t lh = 0, rh = 0;
+    {
+        const uint64_t hi = i0 >= 2 ? i0 - 2 : 0;
+        if (sizeof(S) == 2) {
+            lh = *reinterpret_cast<const uint32_t*>(cur + hi);
+        } else {
+            const uint2 v2 = *reinterpret_cast<const uint2*>(cur + hi);
+            lh = v2.x;
+            rh = v2.y;
+        }
+    }
+    const uint32_t nxr = (uint32_t)cur[i0 + EPT];
+    load_own(cur, i0, x);
+    // the loop state, one snapshot: fields n .. merges_done (DevState offsets 0..39)
+    const uint4 s0 = reinterpret_cast<const uint4*>(st)[0];   // n, stop, next_id, a
+    const uint4 s1 = reinterpret_cast<const uint4*>(st)[1];   // b, nw, mc, new_n
+    const uint2 s2 = reinterpret_cast<const uint2*>(st)[4];   // m, merges_done
+    asm volatile("" ::: "memory");
+    const uint32_t n = s0.x, a = s0.w, b = s1.x, nw = s1.y, new_n = s1.w;
+    const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
+    if (s0.y || s2.y != round + 1u || tl >= ntiles) return;   // merge_active()
+    const uint32_t pid_ab = (a << 16) | b;
+    const uint32_t lim = EXACT ? 0xFFFFFFFFu : new_n;
+    uint32_t xm2 = sizeof(S) == 2 ? (lh & 0xFFFFu) : lh;   // symbol at i0 - 2
+    uint32_t xm1 = sizeof(S) == 2 ? (lh >> 16) : rh;       // symbol at i0 - 1
+    if (i0 < 2) xm2 = xm1 = 0;                              // tokens are never 0 = a, b
+    // branch-free site detection: eb bit j = (x_j == b) (a B-side symbol carries no
+    // word-start bit), ea bit j = (tok(x_j) == a)
+    uint32_t eb = 0, ea = 0;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        eb |= (x[k] == b ? 1u : 0u) << k;
+        ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
+    }
+    const uint32_t inb = lane_mask32(i0, n);
+    const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;   // hit(i0 + j)
+    const uint32_t h_m1 = (xm1 == b && (xm2 & TM) == a && i0 - 1 < n) ? 1u : 0u;  // hit(i0 - 1)
+    const uint32_t h_32 = (nxr == b && (ea >> (EPT - 1)) && i0 + EPT < n) ? 1u : 0u;  // hit(i0 + EPT)
+    const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (EPT + 1));
+    uint32_t cnt = __popc(inb & ~hitm);
+    uint32_t tail = 0;
+    const bool work = hbits != 0 || (i0 + EPT > lim && i0 < n);
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+    const bool wave_work = __any(work);
+    if (lane == 0) {
+        red[wid] = cnt;
+        s_workw[wid] = wave_work;
+    }
+    __syncthreads();
+    if (s_workw[0] | s_workw[1] | s_workw[2] | s_workw[3]) {   // block-uniform: only tiles with a site or a tail element touch the table
+        lds_clear(lt);
+        __syncthreads();
+        if (STAGE && work) {
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) stg[k * TPB + t] = x[k];
+        }
+        if (work) {
+            // only the positions where a pair can change: within one of a site, or in
+            // the stale tail; symbols re-read from the (L1/L2-hot) tile by index so the
+            // register window is never dynamically indexed
+            const uint32_t below = lane_mask32(i0, lim);
+            tail = __popc(inb & ~hitm & ~below);
+            // positions next to a site below the keep limit; the stale tail (old pairs
+            // destroyed, nothing new) is spread over the whole workgroup below
+            uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+            while (rel) {
+                const int k = __ffs(rel) - 1;
+                rel &= rel - 1;
+                const uint64_t i = i0 + k;
+                if (i == 0) continue;
+                uint32_t xi, xp;
+                if (STAGE) {   // the lane's own symbols, staged in LDS below
+                    xi = stg[k * TPB + t];
+                    xp = k ? stg[(k - 1) * TPB + t] : xm1;
+                } else {   // L1/L2-hot re-read (keeps the streaming kernel's LDS small)
+                    xi = cur[i];
+                    xp = cur[i - 1];
+                }
+                if (xi & WS) continue;   // no pair ends at i (old or new)
+                const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+                const uint32_t tp = xp & TM, ti = xi & TM;
+                if (tp && ti) {
+                    const uint32_t pid = (tp << 16) | ti;
+                    if (pid != pid_ab) lds_add(lt, tb, st, pid, 0xFFFFFFFFu);   // old pair destroyed
+                }
+                if (!h0 && i < lim) {
+                    if (hm) {
+                        const uint32_t t2 = hp ? nw : ti;
+                        if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+                    } else if (hp && tp) {
+                        lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+                    }
+                }
+            }
+        }
+        if (!EXACT && ngroups == 0xFFFFFFFFu && (uint64_t)base + TILE > lim && base < n) {
+            const uint64_t hi = (uint64_t)n < base + TILE ? (uint64_t)n : base + TILE;
+            for (uint64_t i = (lim > base ? (uint64_t)lim : base) + t; i < hi; i += TPB) {
+                if (i == 0) continue;
+                const uint32_t xi = cur[i];
+                if (xi & WS) continue;
+                const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
+                if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+            }
+        }
+        lds_flush(lt, tb, st);
+        for (int off = 32; off > 0; off >>= 1) tail += __shfl_xor(tail, off);
+        if (lane == 0 && tail) atomicAdd(&st->m, tail);
+    }
+    // stores last: nothing waits on them
+    if (i0 < n) hitmask[(uint64_t)tl * TPB + t] = hitm;
+    if (t == 0) {
+        const uint32_t tot = red[0] + red[1] + red[2] + red[3];
+        tile_cnt[tl] = tot;
+        atomicAdd(&grpsum[(tl / GRP) * GSTR], tot);
+    }
+}
+
+// k_delta over TPW consecutive tiles per workgroup, one LDS delta table for all
+// of them, flushed once: the dense loop's early merges (10^5-10^6 sites) add to
+// the same hot pairs from every tile, and same-address device atomics serialise
+// at the memory side, so TPW x fewer flushes is TPW x fewer of them.  Same
+// per-tile outputs and delta rule as k_delta.
+template <typename S, bool EXACT, int DELTA_TPW>
+__global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, const S* cur, Table tb,
+                                                  uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
+                                                  uint32_t* __restrict__ grpsum, uint32_t eager_tiles, uint32_t ngroups) {
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    __shared__ LdsTab<LTAB_Z> lt;
+    __shared__ uint32_t red[TPB / 64];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint4 s0 = reinterpret_cast<const uint4*>(st)[0];   // n, stop, next_id, a
+    const uint4 s1 = reinterpret_cast<const uint4*>(st)[1];   // b, nw, mc, new_n
+    const uint2 s2 = reinterpret_cast<const uint2*>(st)[4];   // m, merges_done
+    const uint32_t n = s0.x, a = s0.w, b = s1.x, nw = s1.y, new_n = s1.w;
+    const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
+    if (s0.y || s2.y != round + 1u) return;   // merge_active()
+    const uint32_t pid_ab = (a << 16) | b;
+    const uint32_t lim = EXACT ? 0xFFFFFFFFu : new_n;
+    lds_clear(lt);
+    __syncthreads();
+    if (blockIdx.x >= ngroups) {
+        // stale tail [new_n, n): every old pair there is destroyed.  Blocks past
+        // the tile groups take one contiguous slice each (up to ~2K symbols, so
+        // their LDS table holds every distinct pair), instead of the few tile
+        // workgroups the tail falls in walking all of it with an overflowing table.
+        if (EXACT || n <= lim) return;
+        const uint32_t nt2 = gridDim.x - ngroups, q = blockIdx.x - ngroups;
+        const uint32_t len = n - lim, per = (len + nt2 - 1) / nt2;
+        const uint64_t a0 = (uint64_t)lim + (uint64_t)q * per;
+        const uint64_t a1 = a0 + per < (uint64_t)n ? a0 + per : (uint64_t)n;
+        if (a0 >= a1) return;   // block-uniform
+        for (uint64_t i = a0 + t; i < a1; i += TPB) {
+            if (i == 0) continue;
+            const uint32_t xi = cur[i];
+            if (xi & WS) continue;
+            const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
+            if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        }
+        lds_flush(lt, tb, st);
+        return;
+    }
+    uint32_t tail = 0;
+    for (int q = 0; q < DELTA_TPW; ++q) {
+        const uint32_t tl = blockIdx.x * DELTA_TPW + q;
+        if (tl >= ntiles || (tl >= eager_tiles && (uint64_t)tl * TILE >= n)) break;   // block-uniform
+        const uint64_t base = (uint64_t)tl * TILE;
+        const uint64_t i0 = base + (uint64_t)t * EPT;
+        uint32_t x[EPT];
+        uint32_t lh = 0, rh = 0;
+        {
+            const uint64_t hi = i0 >= 2 ? i0 - 2 : 0;
+            if (sizeof(S) == 2) {
+                lh = *reinterpret_cast<const uint32_t*>(cur + hi);
+            } else {
+                const uint2 v2 = *reinterpret_cast<const uint2*>(cur + hi);
+                lh = v2.x;
+                rh = v2.y;
+            }
+        }
+        const uint32_t nxr = (uint32_t)cur[i0 + EPT];
+        load_own(cur, i0, x);
+        uint32_t xm2 = sizeof(S) == 2 ? (lh & 0xFFFFu) : lh;
+        uint32_t xm1 = sizeof(S) == 2 ? (lh >> 16) : rh;
+        if (i0 < 2) xm2 = xm1 = 0;
+        uint32_t eb = 0, ea = 0;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            eb |= (x[k] == b ? 1u : 0u) << k;
+            ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
+        }
+        const uint32_t inb = lane_mask32(i0, n);
+        const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;
+        const uint32_t h_m1 = (xm1 == b && (xm2 & TM) == a && i0 - 1 < n) ? 1u : 0u;
+        const uint32_t h_32 = (nxr == b && (ea >> (EPT - 1)) && i0 + EPT < n) ? 1u : 0u;
+        const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (EPT + 1));
+        uint32_t cnt = __popc(inb & ~hitm);
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+        if (hbits != 0 || (i0 + EPT > lim && i0 < n)) {
+            const uint32_t below = lane_mask32(i0, lim);
+            tail += __popc(inb & ~hitm & ~below);
+            uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+            while (rel) {
+                const int k = __ffs(rel) - 1;
+                rel &= rel - 1;
+                const uint64_t i = i0 + k;
+                if (i == 0) continue;
+                const uint32_t xi = cur[i], xp = cur[i - 1];
+                if (xi & WS) continue;
+                const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+                const uint32_t tp = xp & TM, ti = xi & TM;
+                if (tp && ti) {
+                    const uint32_t pid = (tp << 16) | ti;
+                    if (pid != pid_ab) lds_add(lt, tb, st, pid, 0xFFFFFFFFu);
+                }
+                if (!h0 && i < lim) {
+                    if (hm) {
+                        const uint32_t t2 = hp ? nw : ti;
+                        if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+                    } else if (hp && tp) {
+                        lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+                    }
+                }
+            }
+        }
+        // (the stale tail's destroyed pairs: the tail blocks above)
+        if (i0 < n) hitmask[(uint64_t)tl * TPB + t] = hitm;
+        if (lane == 0) red[wid] = cnt;
+        __syncthreads();
+        if (t == 0) {
+            const uint32_t tot = red[0] + red[1] + red[2] + red[3];
+            tile_cnt[tl] = tot;
+            atomicAdd(&grpsum[(tl / GRP) * GSTR], tot);
+        }
+        __syncthreads();   // red[] is rewritten by the next tile
+    }
+    lds_flush(lt, tb, st);
+    for (int off = 32; off > 0; off >>= 1) tail += __shfl_xor(tail, off);
+    if (lane == 0 && tail) atomicAdd(&st->m, tail);
+}
+
+// Pass 2.  Blocks [0, ntiles): in-place A-side rewrite (train.wgsl:486-487) +
+// scatter of the survivors with old index < new_n (the reference bound,
+// train.wgsl:727; all of them with EXACT) at tile prefix = group sums + the
+// tile counts of this group before the tile.  Blocks >= ntiles (reference
+// compaction only): the stale tail window [new_n - m, new_n) of the new
+// stream — add its pairs to the count table.
+constexpr int CTPB = 512;             // k_compact threads per tile
+constexpr int CEPT = TILE / CTPB;     // 16 symbols per k_compact thread
+
+template <typename S, int E>
+__device__ __forceinline__ void load_own_n(const S* __restrict__ cur, uint64_t i0, uint32_t* __restrict__ x) {
+    constexpr int V = E * sizeof(S) / 16;
+    uint4 v[V];
+    const uint4* src = reinterpret_cast<const uint4*>(cur + i0);
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = src[k];
+    const S* e = reinterpret_cast<const S*>(v);
+#pragma unroll
+    for (int k = 0; k < E; ++k) x[k] = e[k];
+}
+
+// ZONE (sector-sparse loop): st is the zone's view; the stale window is not in
+// place in `oth` (the zone's coordinates shift with the body) but copied to `win`
+// by k_body before this pass: window symbol j = win[mc - m + j], stored at zone
+// position (zone survivors - m) + j.  gst is the global state (count check).
+template <typename S, bool EXACT, bool ZONE = false>
+__global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, S* __restrict__ cur, S* __restrict__ oth,
+                                                 const uint32_t* __restrict__ hitmask,
+                                                 const uint32_t* __restrict__ tile_cnt,
+                                                 const uint32_t* __restrict__ grpsum, Table tb,
+                                                 const S* __restrict__ win = nullptr, const DevState* gst = nullptr) {
+    // one LDS arena: the compaction stage of tile blocks or the delta table of tail blocks
+    constexpr int STAGE = (TILE + 16) * sizeof(S);
+    constexpr int ARENA = (sizeof(LdsTab<LTAB>) > STAGE ? sizeof(LdsTab<LTAB>) : STAGE) / 16;
+    __shared__ uint4 arena[ARENA];
+    __shared__ uint32_t wsum[CTPB / 64], psum[CTPB / 64];
+    S* stage = reinterpret_cast<S*>(arena);
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t tl = blockIdx.x;
+    const uint64_t base = (uint64_t)tl * TILE;
+    if (!merge_active(st, round)) return;
+    const uint32_t n = st->n, new_n = st->new_n, nw = st->nw;
+    const uint32_t limit = EXACT ? n : new_n;
+    const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
+    if (tl >= ntiles) {
+        if (EXACT || st->sharded) return;   // sharded: the window is handled by k_shard_recv
+        // ── stale tail window ──
+        const uint32_t m = st->m;
+        if (m == 0) return;
+        LdsTab<LTAB>& lt = *reinterpret_cast<LdsTab<LTAB>*>(arena);
+        __shared__ uint32_t left_val;
+        lds_clear(lt);
+        uint32_t lo = new_n - m;
+        const uint32_t tb0 = tl - ntiles, ntb = gridDim.x - ntiles;
+        uint32_t woff = 0;
+        if (ZONE) {   // window start = zone survivors - m (the group sums hold the survivors)
+            __shared__ uint32_t s_surv[CTPB / 64];
+            const uint32_t ngrp = (uint32_t)gbpe_div_up(ntiles, GRP);
+            uint32_t sv = 0;
+            for (uint32_t g = t; g < ngrp; g += CTPB) sv += grpsum[g * GSTR];
+            for (int off = 32; off > 0; off >>= 1) sv += __shfl_xor(sv, off);
+            if (lane == 0) s_surv[wid] = sv;
+            __syncthreads();
+            sv = 0;
+            for (int w2 = 0; w2 < CTPB / 64; ++w2) sv += s_surv[w2];
+            lo = sv - m;
+            woff = st->mc - m;
+        }
+        const uint32_t hi = lo + m;
+        if (tb0 == 0 && wid == 0 && lo >= 1) {
+            // the survivor just before the window: last j < new_n with hit(j) == 0; its
+            // value is the A-side-rewritten symbol (the rewrite is idempotent, so racing
+            // with a tile block's in-place write is harmless)
+            int64_t wi = (int64_t)(new_n - 1) / 32;
+            uint32_t found = 0xFFFFFFFFu;
+            while (wi >= 0 && found == 0xFFFFFFFFu) {
+                const int64_t mywi = wi - lane;
+                uint32_t inv = 0;
+                if (mywi >= 0) {
+                    const uint64_t wbase = (uint64_t)mywi * 32;
+                    inv = ~hitmask[mywi] & lane_mask32(wbase, new_n);   // survivors below new_n
+                }
+                const unsigned long long has = __ballot(inv != 0u);
+                if (has) {
+                    const int l = __ffsll((long long)has) - 1;   // lowest lane = largest word index
+                    const uint32_t inv_l = __shfl(inv, l);
+                    found = (uint32_t)((wi - l) * 32 + (31 - __clz(inv_l)));
+                }
+                wi -= 64;
+            }
+            if (lane == 0) {
+                uint32_t v = 0;
+                if (found != 0xFFFFFFFFu) {
+                    v = cur[found];
+                    const uint32_t f1 = found + 1;
+                    const bool rw = (f1 < n) && ((hitmask[f1 / 32] >> (f1 % 32)) & 1u);
+                    if (rw) v = nw | (v & WS);
+                }
+                left_val = v;
+            }
+        }
+        __syncthreads();
+        for (uint32_t d = lo + tb0 * CTPB + t; d < hi; d += ntb * CTPB) {
+            if (d == 0) continue;
+            uint32_t x0, x1;
+            if (ZONE) {
+                x1 = win[woff + (d - lo)];
+                x0 = (d == lo) ? left_val : (uint32_t)win[woff + (d - lo) - 1];
+                oth[d] = (S)x1;
+            } else {
+                x0 = (d == lo) ? left_val : (uint32_t)oth[d - 1];
+                x1 = oth[d];
+            }
+            const uint32_t t0 = x0 & TM, t1 = x1 & TM;
+            if (!(x1 & WS) && t0 && t1) lds_add(lt, tb, st, (t0 << 16) | t1, 1u);
+        }
+        lds_flush(lt, tb, st);
+        return;
+    }
+    // 512 threads x 16 symbols cover the 8192-symbol tile; every independent load
+    // first: prefix terms, mask word, the tile
+    const uint64_t j0 = base + (uint64_t)t * CEPT;
+    const uint32_t G = tl / GRP;
+    uint32_t part = 0;
+    {
+        const uint32_t j = G * GRP + t;
+        const uint32_t v0 = (t < (int)GRP && j < tl) ? tile_cnt[j] : 0u;
+        const uint32_t g0 = ((uint32_t)t < G) ? grpsum[t * GSTR] : 0u;
+        const uint32_t g1 = ((uint32_t)t + CTPB < G) ? grpsum[(t + CTPB) * GSTR] : 0u;
+        part = v0 + g0 + g1;
+    }
+    const uint32_t hw = hitmask[(uint64_t)tl * TPB + (t >> 1)];
+    const uint32_t hn = (t & 1) ? hitmask[(uint64_t)tl * TPB + (t >> 1) + 1] : 0u;   // may be the next tile's first word
+    uint32_t x[CEPT];
+    load_own_n<S, CEPT>(cur, j0, x);
+    for (uint32_t g = t + 2 * CTPB; g < G; g += CTPB) part += grpsum[g * GSTR];   // only past 2*CTPB groups
+    const uint32_t hm = (t & 1) ? (hw >> 16) : (hw & 0xFFFFu);
+    const uint32_t nb = (t & 1) ? (hn & 1u) : ((hw >> 16) & 1u);
+    const uint32_t inb = lane_mask32(j0, n) & 0xFFFFu;
+    const uint32_t nextbit = (j0 + CEPT < n) ? nb : 0u;
+    const uint32_t rwm = ((hm >> 1) | (nextbit << (CEPT - 1))) & inb;
+    const uint32_t valid = inb & ~hm;
+    const uint32_t keep = EXACT ? valid : (valid & lane_mask32(j0, limit));
+    if (rwm) {   // in-place A-side rewrite (train.wgsl:486-487): the reference's ping buffer
+#pragma unroll
+        for (int k = 0; k < CEPT; ++k) {
+            if ((rwm >> k) & 1u) {
+                x[k] = nw | (x[k] & WS);
+                cur[j0 + k] = (S)x[k];
+            }
+        }
+    }
+    const uint32_t cnt = __popc(keep);
+    // block exclusive scan of cnt + block sum of part
+    uint32_t incl = cnt;
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+    if (lane == 63) wsum[wid] = incl;
+    if (lane == 0) psum[wid] = part;
+    __syncthreads();
+    uint32_t pre = incl - cnt, total = 0, prefix = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < CTPB / 64; ++w2) {
+        pre += w2 < wid ? wsum[w2] : 0u;
+        total += wsum[w2];
+        prefix += psum[w2];
+    }
+    if (tl == ntiles - 1 && t == 0 && !st->sharded &&
+        prefix + tile_cnt[tl] != (ZONE ? gst->new_n - (gst->B - gst->body_rm) : new_n))
+        atomicOr(ZONE ? (uint32_t*)&gst->err : &st->err, ERR_COUNT_MISMATCH);
+    // stage at the destination's alignment phase so both sides move whole 16-byte words
+    constexpr uint32_t VE = 16 / sizeof(S);           // symbols per 16-byte word
+    const uint32_t ph = prefix & (VE - 1);
+    pre += ph;
+#pragma unroll
+    for (int k = 0; k < CEPT; ++k)
+        if ((keep >> k) & 1u) stage[pre++] = (S)x[k];
+    __syncthreads();
+    S* dst = oth + (prefix - ph);                      // 16-byte aligned
+    const uint32_t end = ph + total;
+    const uint32_t nvec = end / VE;
+    uint4* dv = reinterpret_cast<uint4*>(dst);
+    const uint4* sv = reinterpret_cast<const uint4*>(stage);
+    for (uint32_t v = t; v < nvec; v += CTPB) {
+        if (v == 0 && ph) {
+            for (uint32_t j = ph; j < VE && j < end; ++j) dst[j] = stage[j];   // partial head word
+        } else {
+            dv[v] = sv[v];
+        }
+    }
+    if (t == 0 && nvec * VE < end) {
+        for (uint32_t j = (nvec * VE > ph ? nvec * VE : ph); j < end; ++j) dst[j] = stage[j];   // partial tail word
+    }
+}
+
+__global__ void k_clear_dirty_all(DevState* st, Table tb) {
+    (void)st;
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < tb.nblk) tb.dirty[i] = 1u;   // every block gets re-maxed
+}
+
+// dump live (count > 0) pairs
+__global__ void k_dump_pairs(Table tb, uint32_t* pids, uint32_t* counts, uint32_t* nout, uint32_t cap) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > tb.mask) return;
+    uint2 e = tb.slots[i];
+    if (e.x && (int32_t)e.y > 0) {
+        uint32_t k = atomicAdd(nout, 1u);
+        if (k < cap) {
+            pids[k] = e.x;
+            counts[k] = e.y;
+        }
+    }
+}
+
+template <typename S>
+__global__ void k_export_symbols(const S* __restrict__ s, uint32_t* __restrict__ out, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t x = s[i];
+    out[i] = (x & Sym<S>::TM) | ((x & Sym<S>::WS) ? 0x10000u : 0u);
+}
+
+// the inverse: reference u32 layout (bit16 = word start) -> S (consolidation)
+template <typename S>
+__global__ void k_import_symbols(const uint32_t* __restrict__ in, S* __restrict__ s, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t x = in[i];
+    s[i] = (S)((x & Sym<S>::TM) | ((x & 0x10000u) ? Sym<S>::WS : 0u));
+}
+
+// ─── sector-sparse merge loop ──────────────────────────────────
+//
+// Late in training a merge's count is a tiny fraction of the stream, yet the
+// dense pass above reads the whole stream twice per merge.  The sparse loop
+// re-lays the stream out as
+//   * a BODY of word-aligned sectors: sector k starts at the first word start at
+//     or after k*SEC and keeps its symbols compacted at its own start.  Pairs
+//     never cross a word start (train.wgsl:395, 483, 493), so sectors merge
+//     independently and their first symbol is never a B-side;
+//   * a token-presence bitmap (row = token id, bit = sector): a merge (a, b) can
+//     only have sites in sectors whose a-row and b-row bits are both set.  Bits
+//     are set when a token appears in a sector and never cleared (a superset);
+//   * a dense ZONE: the last >= 5*mc symbols, run by the dense kernels on their
+//     own ping-pong buffers.  It carries the reference's compaction quirk (the
+//     stale window always lands at the end of the stream).  Its coordinates are
+//     global position - B (body length), which shifts as the body loses
+//     symbols, so the stale window is copied out (k_body's copy blocks) instead
+//     of being left in place.
+// Per merge: k_select → k_body (candidate sectors + window copy) → k_delta (zone)
+// → k_compact<ZONE> → k_refresh.
+constexpr uint32_t SP_WPW_MIN = 16;  // fewest bitmap words per k_body workgroup (sizes its byte counters)
+constexpr uint32_t SP_CH = 256;      // symbols per wave pass over a sector (4 per lane)
+constexpr uint32_t SP_INV = 0xFFFFFFFFu;
+constexpr uint32_t SP_SHRINKS = 64;  // zone shrinks per sparse entry (sector capacity)
+
+// Per-sector pair signature: a 1024-bit Bloom filter (2 hash bits) of every pair
+// the sector has held since the filters were last rebuilt.  The token bitmap
+// gives candidate sectors; the signature drops most of those where a and b are
+// both present but never adjacent.
+constexpr uint32_t SP_SIGW = 32;     // u32 words per sector signature
+__device__ __forceinline__ uint32_t sig_hash(uint32_t pid) { return gbpe_fmix32(pid ^ 0x9E3779B9u); }
+__device__ __forceinline__ bool sig_has(const uint32_t* __restrict__ sig, uint32_t pid) {
+    const uint32_t h = sig_hash(pid), b1 = h & 1023u, b2 = (h >> 16) & 1023u;
+    return ((sig[b1 >> 5] >> (b1 & 31u)) & (sig[b2 >> 5] >> (b2 & 31u)) & 1u) != 0u;
+}
+// global signature (k_body): no-return atomics, no test load on the merge's critical path
+__device__ __forceinline__ void sig_or(uint32_t* __restrict__ sig, uint32_t pid) {
+    const uint32_t h = sig_hash(pid), b1 = h & 1023u, b2 = (h >> 16) & 1023u;
+    atomicOr(&sig[b1 >> 5], 1u << (b1 & 31u));
+    atomicOr(&sig[b2 >> 5], 1u << (b2 & 31u));
+}
+// LDS signature (k_sp_bits): test first, most bits are already set
+__device__ __forceinline__ void sig_set(uint32_t* __restrict__ sig, uint32_t pid) {
+    const uint32_t h = sig_hash(pid), b1 = h & 1023u, b2 = (h >> 16) & 1023u;
+    const uint32_t m1 = 1u << (b1 & 31u), m2 = 1u << (b2 & 31u);
+    if (!(sig[b1 >> 5] & m1)) atomicOr(&sig[b1 >> 5], m1);
+    if (!(sig[b2 >> 5] & m2)) atomicOr(&sig[b2 >> 5], m2);
+}
+
+// a sector's first wave pass: 4 symbols per lane and the one after the pass
+// (+ their word multiplicities in the lexicon body, else 1)
+template <typename S>
+__device__ __forceinline__ void sector_first(const S* __restrict__ p, const uint32_t* __restrict__ mp, uint32_t cnt,
+                                             uint32_t (&f)[5], uint32_t (&fm)[4]) {
+    const uint32_t i0 = 4u * (uint32_t)(threadIdx.x & 63);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] = (i0 + k < cnt) ? (uint32_t)p[i0 + k] : 0u;
+    f[4] = (SP_CH < cnt) ? (uint32_t)p[SP_CH] : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) fm[k] = mp ? ((i0 + k < cnt) ? mp[i0 + k] : 0u) : 1u;
+}
+
+// One wave merges one sector in place (snapshot semantics, k_delta's delta rule,
+// survivors compacted to the sector's front).  In the lexicon body (mp != null)
+// every symbol carries its word's multiplicity, which weights its count deltas
+// and moves with it.  Returns the B-sides removed (weighted: stream symbols).
+template <typename S, int NT = LTAB_T>
+__device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, uint32_t cnt, uint32_t a, uint32_t b,
+                                uint32_t nw, LdsTab<NT>& lt, const Table& tb, DevState* st, uint32_t* __restrict__ sig,
+                                uint32_t& out_cnt, const uint32_t (&first)[5], const uint32_t (&firstm)[4]) {
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    const int lane = threadIdx.x & 63;
+    const uint32_t pid_ab = (a << 16) | b;
+    uint32_t c1 = 0, c2 = 0, out = 0, removed = 0;
+    for (uint32_t c0 = 0; c0 < cnt; c0 += SP_CH) {
+        const uint32_t i0 = c0 + 4u * lane;
+        // X[0..1] = the two symbols before this lane's four, X[6] = the one after
+        uint32_t X[7], nx, M[4];
+        if (c0 == 0) {   // the first pass's symbols were loaded by the caller (sector_first)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                X[2 + k] = first[k];
+                M[k] = firstm[k];
+            }
+            nx = first[4];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) X[2 + k] = (i0 + k < cnt) ? (uint32_t)p[i0 + k] : 0u;
+            nx = (c0 + SP_CH < cnt) ? (uint32_t)p[c0 + SP_CH] : 0u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) M[k] = mp ? ((i0 + k < cnt) ? mp[i0 + k] : 0u) : 1u;
+        }
+        uint32_t pm1 = __shfl_up(X[5], 1), pm2 = __shfl_up(X[4], 1);
+        uint32_t np = __shfl_down(X[2], 1);
+        if (lane == 0) {
+            pm1 = c1;
+            pm2 = c2;
+        }
+        if (lane == 63) np = nx;
+        X[0] = pm2;
+        X[1] = pm1;
+        X[6] = np;
+        c1 = __shfl(X[5], 63);
+        c2 = __shfl(X[4], 63);
+        // h[j] = hit at the position of X[j]: a B-side (no word-start bit) after an a
+        bool h[7];
+        h[0] = false;
+#pragma unroll
+        for (int j = 1; j < 7; ++j) h[j] = X[j] == b && (X[j - 1] & TM) == a;
+        uint32_t keep = 0, vals[4];
+        bool touched = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = k + 2;
+            const bool valid = i0 + k < cnt;
+            const uint32_t w = M[k];   // a pair's occurrences = its right symbol's word multiplicity
+            if (valid && !h[j]) keep |= 1u << k;
+            if (valid && h[j]) removed += w;
+            vals[k] = h[j + 1] ? (nw | (X[j] & WS)) : X[j];
+            touched |= valid && (h[j] || h[j + 1]);
+            if (valid && !(X[j] & WS) && (h[j - 1] || h[j] || h[j + 1])) {
+                const uint32_t tp = X[j - 1] & TM, ti = X[j] & TM;
+                if (tp && ti) {
+                    const uint32_t pid = (tp << 16) | ti;
+                    if (pid != pid_ab) lds_add(lt, tb, st, pid, 0u - w);   // old pair destroyed
+                }
+                if (!h[j]) {
+                    if (h[j - 1]) {
+                        const uint32_t t2 = h[j + 1] ? nw : ti;
+                        if (t2) {
+                            lds_add(lt, tb, st, (nw << 16) | t2, w);
+                            sig_or(sig, (nw << 16) | t2);
+                        }
+                    } else if (h[j + 1] && tp) {
+                        lds_add(lt, tb, st, (tp << 16) | nw, w);
+                        sig_or(sig, (tp << 16) | nw);
+                    }
+                }
+            }
+        }
+        const uint32_t kc = __popc(keep);
+        uint32_t incl = kc;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off);
+            if (lane >= off) incl += o;
+        }
+        const uint32_t tot = __shfl(incl, 63);
+        // every read of this pass happened above; writes land at or before their source
+        if (out != c0 || __any(touched)) {
+            uint32_t w = out + incl - kc;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((keep >> k) & 1u) {
+                    if (mp) mp[w] = M[k];
+                    p[w++] = (S)vals[k];
+                }
+        }
+        out += tot;
+    }
+    out_cnt = out;
+    for (int off = 32; off > 0; off >>= 1) removed += __shfl_xor(removed, off);   // per lane → the wave's
+    return removed;
+}
+
+// Single-workgroup zone pass (zone <= ZMAX symbols): k_delta + k_compact<ZONE>
+// in one workgroup.  Each thread holds 32 consecutive zone symbols in registers
+// and builds k_delta's branch-free site masks; only positions next to a site or
+// in the stale tail touch the LDS copy and the delta table.  Kept survivors
+// (A-sides rewritten, also in place: the reference's ping buffer) are compacted
+// into the other zone buffer and the stale window follows them.  The window
+// source is read from the other buffer before anything is written to it.
+// k_body runs as 1024-thread workgroups (16 waves: more sectors in flight, a
+// zone up to 32K symbols in one workgroup) while the zone is large, and as
+// 256-thread ones late in training (small zone, lower latency per launch).
+template <typename S, int BT> struct ZoneDim {
+    static constexpr int ZPT = (BT == 1024 && sizeof(S) == 4) ? 16 : 32;   // zone positions per thread
+    static constexpr uint32_t ZMAX = (uint32_t)BT * ZPT;   // 8192 (256) / 32768 or 16384 (1024) symbols
+    static constexpr uint32_t ZWIN = ZMAX / 3 + 64;         // >= mc: the zone holds >= 3 mc (sel_inline's rule)
+};
+template <typename S, int BT>
+struct ZoneLds {
+    uint4 xv[ZoneDim<S, BT>::ZMAX * sizeof(S) / 16];   // the zone (symbol i = ((S*)xv)[i])
+    S wb[ZoneDim<S, BT>::ZWIN];
+    uint32_t wsum[BT / 64], wtail[BT / 64];
+    S trash[64];   // the zone pass's unconditional stores of dropped symbols
+};
+
+__device__ __forceinline__ uint32_t lane_mask_n(uint64_t i0, uint64_t lim, int n) {
+    // bits k with i0 + k < lim, k < n (n <= 32)
+    const uint32_t full = n == 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    return i0 >= lim ? 0u : (i0 + n <= lim ? full : ((1u << (uint32_t)(lim - i0)) - 1u));
+}
+
+// zout (the persistent tail loop, k_tail): the delta table is shared with the body
+// pass (neither cleared nor flushed here) and m, the new zone length go to zout[0..1]
+template <typename S, bool EXACT, int BT, int NT = LTAB_T, int ZPT_ = ZoneDim<S, BT>::ZPT>
+__device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
+                         S* __restrict__ zo, ZoneLds<S, BT>& L,
+                         LdsTab<NT>& lt, const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
+                         uint64_t* __restrict__ bytes, uint32_t round, uint32_t* zout = nullptr) {
+    (void)round;   // phase stamps only (-DGBPE_KTRACE)
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    constexpr int ZPT = ZPT_;                // zone positions per thread (<= ZoneDim's: the LDS is sized for that)
+    static_assert(ZPT <= ZoneDim<S, BT>::ZPT && ZPT * sizeof(S) % 16 == 0, "zone positions per thread");
+    constexpr int V = ZPT * sizeof(S) / 16;  // 16-byte vectors per thread
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t z = zs.n;   // launch snapshots (LDS): no state round trip before the zone loads
+    const uint32_t lim = EXACT ? z : z - mc;
+    const uint32_t pid_ab = (a << 16) | b;
+    const uint32_t i0 = (uint32_t)t * ZPT;
+    S* xs = reinterpret_cast<S*>(L.xv);
+    uint32_t x[ZPT];
+    {
+        uint4 v[V];
+        const uint4* src = reinterpret_cast<const uint4*>(zc + i0);   // zone buffers hold >= 2 tiles
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = src[k];
+#pragma unroll
+        for (int k = 0; k < V; ++k) L.xv[t * V + k] = v[k];
+        const S* e = reinterpret_cast<const S*>(v);
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
+    }
+    if (!EXACT) {   // window source: global n - 2mc in the previous stream (sharded: it began at poff, now off)
+        const uint64_t src0 = (uint64_t)gs.n + gs.off - gs.poff - 2ull * mc - gs.Bp;
+        for (uint32_t u = t; u < mc; u += BT) L.wb[u] = zo[src0 + u];
+    }
+    if (!zout) lds_clear(lt);
+    __syncthreads();
+    if (t == 0) KT(2);
+    const uint32_t xm2 = i0 >= 2 ? (uint32_t)xs[i0 - 2] : 0u, xm1 = i0 >= 1 ? (uint32_t)xs[i0 - 1] : 0u;
+    const uint32_t nxr = i0 + ZPT < z ? (uint32_t)xs[i0 + ZPT] : 0u;
+    uint32_t eb = 0, ea = 0;
+#pragma unroll
+    for (int k = 0; k < ZPT; ++k) {
+        eb |= (x[k] == b ? 1u : 0u) << k;
+        ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
+    }
+    const uint32_t inb = lane_mask_n(i0, z, ZPT);
+    const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;
+    const uint32_t h_m1 = (i0 >= 1 && i0 - 1 < z && xm1 == b && (xm2 & TM) == a) ? 1u : 0u;
+    const uint32_t h_32 = (nxr == b && (ea >> (ZPT - 1))) ? 1u : 0u;
+    const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (ZPT + 1));
+    const uint32_t below = lane_mask_n(i0, lim, ZPT);
+    const uint32_t surv = inb & ~hitm, keep = surv & below;
+    const uint32_t rwm = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
+    uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+    for (uint32_t i = (lim > 1u ? lim : 1u) + t; i < z; i += BT) {   // stale tail: old pairs destroyed
+        const uint32_t xi = xs[i];
+        if (xi & WS) continue;
+        const uint32_t tp = xs[i - 1] & TM, ti = xi & TM;
+        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+    }
+    while (rel) {
+        const int k = __ffs(rel) - 1;
+        rel &= rel - 1;
+        const uint32_t i = i0 + k;
+        if (i == 0) continue;
+        const uint32_t xi = xs[i];
+        if (xi & WS) continue;
+        const uint32_t xp = xs[i - 1];
+        const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+        const uint32_t tp = xp & TM, ti = xi & TM;
+        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        if (!h0) {
+            if (hm) {
+                const uint32_t t2 = hp ? nw : ti;
+                if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+            } else if (hp && tp) {
+                lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+            }
+        }
+    }
+    if (t == 0) KT(3);
+    // block exclusive scan of the kept counts; tail survivors sum to m
+    const uint32_t kc = __popc(keep);
+    uint32_t incl = kc, tl = __popc(surv & ~below);
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    for (int off = 32; off > 0; off >>= 1) tl += __shfl_xor(tl, off);
+    if (lane == 63) L.wsum[wid] = incl;
+    if (lane == 0) L.wtail[wid] = tl;
+    __syncthreads();
+    if (t == 0) KT(7);
+    uint32_t pre = incl - kc, Kz = 0, m = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < BT / 64; ++w2) {
+        pre += w2 < wid ? L.wsum[w2] : 0u;
+        Kz += L.wsum[w2];
+        m += L.wtail[w2];
+    }
+    // The new zone is assembled in LDS over the old copy (every read of it is
+    // done) and leaves in whole 16-byte stores: per-symbol global stores at a
+    // lane stride of ZPT symbols cost a cache line per lane and instruction.
+    // In LDS the 16-byte chunks are XOR-swizzled within groups of 8: lanes
+    // write ZPT symbols apart, which unswizzled lands every lane of a wave on
+    // the same two banks.
+    constexpr uint32_t PV = 16 / sizeof(S), PVL = sizeof(S) == 2 ? 3 : 2;
+    auto swz = [](uint32_t o) -> uint32_t {
+        const uint32_t c = o >> PVL;
+        return ((c ^ ((c >> 3) & 7u)) << PVL) | (o & (PV - 1u));
+    };
+    // branch-free: every position stores (dropped ones into a per-lane trash
+    // slot); the A-side rewrites of the reference's in-place ping buffer are
+    // the only global stores, one per rewritten position
+    uint32_t wsm = 0;
+#pragma unroll
+    for (int k = 0; k < ZPT; ++k) {
+        const bool rw = (rwm >> k) & 1u;
+        const uint32_t v = rw ? (nw | (x[k] & WS)) : x[k];
+        wsm |= ((x[k] & WS) ? 1u : 0u) << k;
+        const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
+        S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
+        *dst = (S)v;
+    }
+    for (uint32_t r = rwm; r; r &= r - 1) {
+        const int k = __ffs(r) - 1;
+        zc[i0 + k] = (S)(nw | (((wsm >> k) & 1u) ? WS : 0u));
+    }
+    if (t == 0) KT(8);
+    if (!EXACT && m) {
+        __syncthreads();
+        const uint32_t woff = mc - m;
+        for (uint32_t j = t; j < m; j += BT) {
+            const uint32_t x1 = L.wb[woff + j];
+            // left of the window: the last kept survivor (Kz > 0: the zone holds >= 5 mc)
+            const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : (Kz ? (uint32_t)xs[swz(Kz - 1)] : 0u);
+            xs[swz(Kz + j)] = (S)x1;
+            if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) lds_add(lt, tb, st, ((x0 & TM) << 16) | (x1 & TM), 1u);
+        }
+    }
+    __syncthreads();
+    if (t == 0) KT(9);
+    {
+        const uint32_t tot = Kz + m, nfull = tot / PV;
+        uint4* dst = reinterpret_cast<uint4*>(zo);
+        for (uint32_t q = t; q < nfull; q += BT) dst[q] = L.xv[q ^ ((q >> 3) & 7u)];
+        for (uint32_t j = nfull * PV + t; j < tot; j += BT) zo[j] = xs[swz(j)];
+    }
+    if (t == 0) KT(4);
+    if (!zout) lds_flush(lt, tb, st);
+    if (t == 0) {
+        if (zout) {
+            zout[0] = m;
+            zout[1] = Kz + m;
+        } else {
+            zst->m = m;
+            zst->valid_total = Kz + m + 1u;   // survivors + 1 (k_refresh checks it against the new layout)
+        }
+        // zone read, window source read, kept survivors + window written
+        atomicAdd(bytes, (uint64_t)sizeof(S) * ((uint64_t)z + (EXACT ? 0u : mc) + Kz + m));
+    }
+}
+
+// ── segmented zone pass (zones of 32K-1M symbols) ──
+// A zone too large for one workgroup but far smaller than the stream (merges
+// ~500-8000 at 1 GiB) is cut into segments of BT x ZPT = 16K symbols, one
+// 1024-thread workgroup each (blocks [0, nz) of k_body).  Two phases:
+//  A (no waiting): a segment runs zone_one's site deltas and local compaction
+//    on its range (neighbour symbols before / after it come from the current
+//    zone buffer, where their owners may already have rewritten them in place:
+//    token nw reads back as a, since nw exists nowhere else before this merge),
+//    and takes an even share of the two mc-long per-merge chores: the stale
+//    tail's destroyed pairs ([z - mc, z), read the same way) and the stale-window
+//    SOURCE ([n - 2mc - Bp, + mc) of the other buffer) copied into LDS.  It
+//    publishes (kept, tail survivors, last kept symbol) as three 8-byte
+//    {tag, value} granules (relaxed agent-scope stores: the data is the flag)
+//    after every wave drained its loads.
+//  B: one wave sweeps all nz segments' granules; then the segment stores its
+//    kept symbols at its prefix and the part of the window (the last m source
+//    symbols, m = all tail survivors) in its share after the Kz kept ones.  Every
+//    read of the other buffer (the window source) happened in phase A, before
+//    any segment passes phase B's sweep, so no store overwrites an unread source.
+//  Every zone workgroup waits only on zone workgroups, which never wait on body
+//  workgroups: with nz <= 64 workgroups they all become resident.
+// k_refresh zeroes the granules for the next merge (tag = 1).
+template <typename S, bool EXACT, int BT, int NT, int ZPT>
+__device__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
+                         S* __restrict__ zo, ZSegState* zg, uint32_t nz, ZoneLds<S, BT>& L, LdsTab<NT>& lt,
+                         const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
+                         uint64_t* __restrict__ bytes, uint32_t round) {
+    (void)round;
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    constexpr uint32_t SEG = (uint32_t)BT * ZPT;
+    constexpr int V = ZPT * sizeof(S) / 16;
+    static_assert(ZPT <= ZoneDim<S, BT>::ZPT && ZPT * sizeof(S) % 16 == 0, "segment positions per thread");
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    __shared__ uint32_t s_h[3], s_last, s_pre, s_kz, s_m, s_x0;
+    const uint32_t seg = blockIdx.x;
+    const uint32_t z = zs.n;
+    const uint32_t lim = EXACT ? z : z - mc;
+    const uint32_t g0 = seg * SEG;
+    const uint32_t nh = g0 < z ? (z - g0 < SEG ? z - g0 : SEG) : 0u;   // positions of this segment (0: past the end)
+    const uint32_t pid_ab = (a << 16) | b;
+    auto unrw = [&](uint32_t v) -> uint32_t { return (v & TM) == nw ? (a | (v & WS)) : v; };
+    auto zload = [&](uint32_t p) -> uint32_t { return unrw((uint32_t)((const volatile S*)zc)[p]); };   // old or rewritten
+    const uint32_t i0 = (uint32_t)t * ZPT;   // local
+    S* xs = reinterpret_cast<S*>(L.xv);
+    uint32_t x[ZPT];
+    {
+        uint4 v[V];
+        const uint4* src = reinterpret_cast<const uint4*>(zc + g0 + i0);
+        const bool any = i0 < nh;
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = any ? src[k] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int k = 0; k < V; ++k) L.xv[t * V + k] = v[k];
+        const S* e = reinterpret_cast<const S*>(v);
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < nh ? (uint32_t)e[k] : 0u;
+    }
+    if (t < 3) {   // neighbours g0 - 2, g0 - 1, g0 + nh
+        const uint32_t p = t < 2 ? g0 - 2u + (uint32_t)t : g0 + nh;
+        const bool ok = nh && (t < 2 ? g0 >= 2u - (uint32_t)t : g0 + nh < z);
+        s_h[t] = ok ? zload(p) : 0u;
+    }
+    // this segment's share of the window source (+ the symbol before it) into LDS
+    const uint32_t lw = (mc + nz - 1) / nz, q0 = seg * lw, q1 = q0 + lw < mc ? q0 + lw : mc;   // source [q0, q1)
+    const uint64_t src0 = (uint64_t)gs.n + gs.off - gs.poff - 2ull * mc - gs.Bp;
+    if (!EXACT && q0 < q1) {
+        const uint32_t f = q0 ? q0 - 1u : 0u;   // L.wb[j] = source[f + j]
+        for (uint32_t q = f + t; q < q1; q += BT) L.wb[q - f] = zo[src0 + q];
+    }
+    lds_clear(lt);
+    __syncthreads();
+    if (t == 0) KT(2);
+    auto X = [&](int j) -> uint32_t {   // local position j in [-2, SEG]
+        return j < 0 ? s_h[j + 2] : (uint32_t)j < nh ? (uint32_t)xs[j] : ((uint32_t)j == nh ? s_h[2] : 0u);
+    };
+    if (!EXACT) {   // this segment's share of the stale tail: old pairs destroyed
+        const uint32_t lo = lim > 1u ? lim : 1u;
+        const uint32_t nt_ = z > lo ? z - lo : 0u, lt_ = (nt_ + nz - 1) / nz;
+        const uint32_t p0 = lo + seg * lt_, p1 = p0 + lt_ < z ? p0 + lt_ : z;
+        for (uint32_t i = p0 + t; i < p1; i += BT) {
+            const uint32_t xi = zload(i);
+            if (xi & WS) continue;
+            const uint32_t tp = zload(i - 1) & TM, ti = xi & TM;
+            if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        }
+    }
+    const uint32_t xm2 = X((int)i0 - 2), xm1 = X((int)i0 - 1), nxr = X((int)(i0 + ZPT));
+    uint32_t eb = 0, ea = 0;
+#pragma unroll
+    for (int k = 0; k < ZPT; ++k) {
+        eb |= (x[k] == b ? 1u : 0u) << k;
+        ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
+    }
+    const uint32_t gi0 = g0 + i0;
+    const uint32_t inb = lane_mask_n(i0, nh, ZPT);
+    const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;
+    const uint32_t h_m1 = (gi0 >= 1 && i0 <= nh && xm1 == b && (xm2 & TM) == a) ? 1u : 0u;
+    const uint32_t h_32 = (nxr == b && (ea >> (ZPT - 1))) ? 1u : 0u;
+    const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (ZPT + 1));
+    const uint32_t below = lane_mask_n(gi0, lim, ZPT);
+    const uint32_t surv = inb & ~hitm, keep = surv & below;
+    const uint32_t rwm = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
+    uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+    while (rel) {
+        const int k = __ffs(rel) - 1;
+        rel &= rel - 1;
+        const uint32_t i = i0 + k;
+        if (g0 + i == 0) continue;
+        const uint32_t xi = X((int)i);
+        if (xi & WS) continue;
+        const uint32_t xp = X((int)i - 1);
+        const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+        const uint32_t tp = xp & TM, ti = xi & TM;
+        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        if (!h0) {
+            if (hm) {
+                const uint32_t t2 = hp ? nw : ti;
+                if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+            } else if (hp && tp) {
+                lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+            }
+        }
+    }
+    if (t == 0) KT(3);
+    // local exclusive scan of the kept counts; tail survivors; the last kept symbol
+    const uint32_t kc = __popc(keep);
+    uint32_t incl = kc, tl = __popc(surv & ~below);
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    for (int off = 32; off > 0; off >>= 1) tl += __shfl_xor(tl, off);
+    if (lane == 63) L.wsum[wid] = incl;
+    if (lane == 0) L.wtail[wid] = tl;
+    __syncthreads();
+    uint32_t pre = incl - kc, Ks = 0, Ts = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < BT / 64; ++w2) {
+        pre += w2 < wid ? L.wsum[w2] : 0u;
+        Ks += L.wsum[w2];
+        Ts += L.wtail[w2];
+    }
+    if (kc && pre + kc == Ks) {   // this thread holds the segment's last kept symbol
+        const int hk = 31 - __clz(keep);
+        uint32_t xv = x[0];
+#pragma unroll
+        for (int k = 1; k < ZPT; ++k) xv = k == hk ? x[k] : xv;
+        s_last = ((rwm >> hk) & 1u) ? (nw | (xv & WS)) : xv;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's reads of the other buffer are done
+    __syncthreads();
+    if (t == 0) {
+        constexpr unsigned long long TAG = 1ull << 32;
+        __hip_atomic_store(&zg->gran[seg][0], TAG | Ks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&zg->gran[seg][1], TAG | Ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&zg->gran[seg][2], TAG | (Ks ? (s_last | 0x80000000u) : 0u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        KT(7);
+    }
+    // the new segment assembled in LDS over the old copy (swizzled as in zone_one)
+    constexpr uint32_t PV = 16 / sizeof(S), PVL = sizeof(S) == 2 ? 3 : 2;
+    auto swz = [](uint32_t o) -> uint32_t {
+        const uint32_t c = o >> PVL;
+        return ((c ^ ((c >> 3) & 7u)) << PVL) | (o & (PV - 1u));
+    };
+    uint32_t wsm = 0;
+#pragma unroll
+    for (int k = 0; k < ZPT; ++k) {
+        const bool rw = (rwm >> k) & 1u;
+        const uint32_t v = rw ? (nw | (x[k] & WS)) : x[k];
+        wsm |= ((x[k] & WS) ? 1u : 0u) << k;
+        const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
+        S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
+        *dst = (S)v;
+    }
+    for (uint32_t r = rwm; r; r &= r - 1) {
+        const int k = __ffs(r) - 1;
+        zc[gi0 + k] = (S)(nw | (((wsm >> k) & 1u) ? WS : 0u));
+    }
+    // B: every segment's granules (one wave, relaxed sweeps, s_sleep between)
+    if (wid == 0) {
+        uint32_t gk = 0, gt = 0, gl = 0;
+        for (uint32_t it = 0;; ++it) {
+            bool ok = true;
+            if ((uint32_t)lane < nz) {
+                const unsigned long long x0 = __hip_atomic_load(&zg->gran[lane][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long x1 = __hip_atomic_load(&zg->gran[lane][1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long x2 = __hip_atomic_load(&zg->gran[lane][2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = (x0 >> 32) == 1u && (x1 >> 32) == 1u && (x2 >> 32) == 1u;
+                gk = (uint32_t)x0;
+                gt = (uint32_t)x1;
+                gl = (uint32_t)x2;
+            }
+            if (__all(ok)) break;
+            if (it > ZSEG_SPIN) {
+                if (lane == 0) atomicOr(&st->err, ERR_SPIN);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const bool in = (uint32_t)lane < nz;
+        uint32_t sp = in && (uint32_t)lane < seg ? gk : 0u, sk = in ? gk : 0u, stt = in ? gt : 0u;
+        for (int off = 32; off > 0; off >>= 1) {
+            sp += __shfl_xor(sp, off);
+            sk += __shfl_xor(sk, off);
+            stt += __shfl_xor(stt, off);
+        }
+        const unsigned long long hm = __ballot(in && (gl >> 31));
+        if (lane == 0) {
+            s_pre = sp;
+            s_kz = sk;
+            s_m = EXACT ? 0u : stt;
+            s_x0 = 0u;
+        }
+        if (hm && lane == 63 - __clzll(hm)) s_x0 = gl & 0x7FFFFFFFu;   // the last kept survivor overall
+    }
+    __syncthreads();
+    if (t == 0) KT(8);
+    const uint32_t P = s_pre, Kz = s_kz, m = s_m;
+    for (uint32_t j = t; j < Ks; j += BT) zo[P + j] = xs[swz(j)];
+    if (!EXACT && m) {   // the window = source [mc - m, mc) after the Kz kept symbols; this segment's share
+        const uint32_t w0 = mc - m, f = q0 ? q0 - 1u : 0u;
+        const uint32_t lo = q0 > w0 ? q0 : w0;
+        for (uint32_t q = lo + t; q < q1; q += BT) {
+            const uint32_t x1 = L.wb[q - f];
+            const uint32_t x0 = q == w0 ? s_x0 : (uint32_t)L.wb[q - 1u - f];
+            zo[Kz + (q - w0)] = (S)x1;
+            if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) lds_add(lt, tb, st, ((x0 & TM) << 16) | (x1 & TM), 1u);
+        }
+    }
+    if (t == 0) KT(9);
+    lds_flush(lt, tb, st);
+    if (t == 0) {
+        KT(4);
+        if (seg == 0) {
+            zst->m = m;
+            zst->valid_total = Kz + m + 1u;
+        }
+        const uint32_t ws = q1 > q0 ? q1 - q0 : 0u;
+        atomicAdd(bytes, (uint64_t)sizeof(S) * ((uint64_t)nh + Ks + 2u * ws + (EXACT ? 0u : mc / nz)));
+    }
+}
+
+// Selection inside k_body (sector-sparse loop): every workgroup reduces the
+// k_refresh partial maxima itself and gets the same merge; the last one commits
+// it (log, table slot zeroed, state for k_refresh and the zone kernels).  The
+// step counters move on in k_refresh (finish == 2), so nothing a workgroup reads
+// here changes under it.  Saves the k_select launch per merge.
+// Sharded (cap_list != 0): the zone sits on the last rank only, so the zone checks
+// use st->zlast, the zone length every rank learned from the last exchange; a
+// merge whose count could overflow the exchange record stalls here, before any
+// sector is touched, on every rank alike (the count is global).
+struct SelShard {
+    uint32_t zf = 5;         // zone rule: z >= max(2 mc + mc_prev, zf mc) + 2 (single GPU: GBPE_ZONE_F, sharded 5)
+    uint32_t cap_list = 0;   // 0 = single GPU
+    uint32_t zmax = 0;       // the one-workgroup zone limit (sharded zones never run multi-tile)
+    uint32_t* nlog = nullptr;
+    uint32_t* rec = nullptr; // this rank's exchange record (its list length restarts at 0)
+};
+
+template <int BT>
+__device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
+                           uint32_t round, bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
+                           uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc,
+                           const DevState*& gsnap, const DevState*& zsnap, const SelShard sh = SelShard(),
+                           bool commit = true) {
+    __shared__ uint64_t s_red[BT / 64];
+    constexpr int NW = sizeof(DevState) / 4;
+    __shared__ union {
+        DevState d;
+        uint32_t w[NW];
+    } s_g, s_z;
+    const int t = threadIdx.x;
+    // the partial maxima and snapshots of both states load together (one round
+    // trip, not one per field)
+    if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
+    else if (zst && t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
+    uint64_t best = 0;
+    for (uint32_t i = t; i < npart; i += BT) {
+        const uint64_t v = part[i];
+        best = v > best ? v : best;
+    }
+    __syncthreads();
+    const DevState& g = s_g.d;
+    gsnap = &s_g.d;
+    zsnap = &s_z.d;
+    if (!(round < g.budget && g.merges_done == round && !g.stop && !g.sp_abort && !g.stall)) return false;
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    if ((t & 63) == 0) s_red[t >> 6] = best;
+    __syncthreads();
+    best = s_red[0];
+#pragma unroll
+    for (int w = 1; w < BT / 64; ++w) best = s_red[w] > best ? s_red[w] : best;
+    mc = (uint32_t)(best >> 32);
+    const uint32_t pid = ~(uint32_t)best;
+    a = pid >> 16;
+    b = pid & 0xFFFFu;
+    nw = g.next_id;
+    const bool stop = mc < 2u || nw > 0xFFFFu;                                          // train.wgsl:345-348
+    const bool bad = !stop && !exact && g.is_last &&
+                     (uint64_t)g.n + g.off - g.poff < 2ull * mc + g.Bp;   // cannot happen
+    // zone misfit: this merge's window source must lie in the zone's stale buffer
+    // (n - 2mc >= Bp, where n - Bp >= z - mc_prev: the last merge removed <= mc_prev
+    // body symbols), and the zone keeps >= zf mc for the merges after it
+    const uint32_t mc_prev = sh.cap_list ? g.mc : g.mc_prev;
+    const uint64_t zneed = std::max<uint64_t>(2ull * mc + mc_prev, (uint64_t)sh.zf * mc) + 2u;
+    const bool abort = !stop && !bad && !exact && ((uint64_t)g.zlast < zneed || (sh.zmax && g.zlast > sh.zmax));
+    const uint32_t need = 6u * mc + 64u;   // distinct deltas of one merge <= 4 per site + tail + window
+    const bool stall = !stop && !bad && !abort && sh.cap_list && need > sh.cap_list;
+    const bool go = !stop && !bad && !abort && !stall;
+    // the LAST workgroup commits: block 0 is the zone pass (the launch's longest
+    // chain), which then starts without the table probe and the state stores
+    if (commit && blockIdx.x == gridDim.x - 1u) {
+        if (t == 0) {
+            if (stop) {
+                st->stop = 1u;
+            } else if (bad) {
+                atomicOr(&st->err, ERR_SPARSE_WINDOW);
+                st->stop = 1u;
+            } else if (abort) {
+                st->sp_abort = 1u;
+            } else if (stall) {   // the host grows the records and redoes this merge
+                st->stall = 1u;
+                st->need_l = need;
+                st->need_w = 0u;
+            } else {
+                if (sh.nlog) sh.nlog[round] = g.n;
+                if (sh.rec) {
+                    sh.rec[H_L] = 0u;
+                    st->dcount = 0u;
+                    st->dused = 0u;
+                    st->dfull = 0u;
+                }
+                const uint32_t idx = table_find(tb, pid);
+                if (idx == 0xFFFFFFFFu) {
+                    atomicOr(&st->err, ERR_PAIR_MISSING);
+                } else {
+                    // every (a,b) occurrence is a merge site: count -= mc, atomically, since
+                    // other workgroups may already add this merge's stale-window pairs
+                    atomicSub(&tb.slots[idx].y, mc);
+                    tb.dirty[idx >> BLK_LOG2] = 1u;
+                }
+                log[round * 4 + 0] = a;
+                log[round * 4 + 1] = b;
+                log[round * 4 + 2] = nw;
+                log[round * 4 + 3] = mc;
+                st->a = a;
+                st->b = b;
+                st->nw = nw;
+                st->mc = mc;
+                st->new_n = g.n - mc;
+                zst->a = a;
+                zst->b = b;
+                zst->nw = nw;
+                zst->mc = mc;
+                zst->new_n = exact ? s_z.d.n : s_z.d.n - mc;
+                if (!zone1) {   // zone_one (another workgroup of this launch) sets both itself
+                    zst->m = 0u;
+                    zst->valid_total = 0u;
+                }
+                zst->merges_done = round + 1u;
+                st->sel_round = round + 1u;
+            }
+        }
+        if (go) {   // group sums of a multi-tile zone pass start at zero
+            const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(s_z.d.n, TILE), GRP);
+            for (uint32_t q = t; q < ngrp; q += BT) grpsum[q * GSTR] = 0u;
+        }
+    }
+    return go;
+}
+
+// Body pass: blocks [0, nbody) each own `wpg` consecutive bitmap words of
+// (a-row & b-row), tested PW words at a time: the candidate sectors whose pair
+// signature may hold (a, b) are merged (one wave per sector).  A fixed grid of
+// wide workgroups (about 4 per CU at 1 GiB) instead of one workgroup per 16
+// words: the selection each workgroup repeats, and the rounds of workgroup
+// scheduling, cost more than the bitmap words themselves (75K words per row at
+// 1 GiB).  Blocks >= nbody copy the stale-window source [n - 2mc - Bp, + mc) of
+// the zone's other buffer to `wtmp`.
+// With `zst` (zone <= ZMAX), block nbody runs the whole zone pass (zone_one) and
+// there are no copy blocks: one launch merges body and zone.
+constexpr uint32_t SP_PW = 64;               // bitmap words tested per pass (one per lane of wave 0)
+constexpr uint32_t SP_CAP = SP_PW * 32;      // candidate sectors per pass
+struct BodyCand {
+    uint32_t sec[SP_CAP];
+    uint2 ext[SP_CAP];
+};
+template <typename S, int BT>
+union BodyLds {   // body workgroups use the candidate arrays, the zone workgroup the zone
+    ZoneLds<S, BT> z;
+    BodyCand c;
+};
+
+// ZSEG: the form for zones of 32K-1M symbols: blocks [0, zone1) run the zone
+// segments (zone_seg) beside the body blocks, and zone_one is not compiled in
+// (with both, every form spilled to scratch)
+template <typename S, bool EXACT, int BT, int ZPT = ZoneDim<S, BT>::ZPT, bool ZSEG = false>
+__global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
+                                              uint32_t* __restrict__ bits, uint32_t W, uint32_t wpg,
+                                              uint32_t* __restrict__ sig, Table tb, uint32_t nbody,
+                                              const S* __restrict__ zoth, S* __restrict__ wtmp,
+                                              uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
+                                              const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
+                                              uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
+                                              Table dtb, SelShard sh, uint32_t* __restrict__ lmul,
+                                              ZSegState* __restrict__ zg = nullptr) {
+    constexpr int KB_LT = ZSEG ? 4096 : LTAB_T;
+    __shared__ LdsTab<KB_LT> lt;
+    __shared__ BodyLds<S, BT> u;
+    __shared__ uint32_t s_ntok, s_n, s_any, s_rm[BT / 64];
+    __shared__ uint64_t s_mv[BT / 64];
+    constexpr int QPT = SP_CAP / BT;   // candidates per thread in the signature test
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    uint32_t a, b, nw, mc;
+    if (t == 0) KT(0);
+    const DevState *gs, *zs;   // this workgroup's snapshots of the states at launch (LDS)
+    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh))
+        return;
+    if (t == 0) KT(1);
+    // the zone workgroup is dispatched first (block 0 when zone1): it is the longest
+    // single chain of the merge, and later blocks of a large grid start later
+    const uint32_t bid = blockIdx.x - zone1;
+    // deltas go to the replica (single GPU) or to the per-merge delta table (sharded)
+    if constexpr (ZSEG) {
+        if (blockIdx.x < zone1) {
+            zone_seg<S, EXACT, BT, KB_LT, 16>(st, zst, *gs, *zs, zcur, (S*)zoth, zg, zone1, u.z, lt, dtb, a, b, nw, mc,
+                                             wg_bytes + nbody, round);
+            if (t == 0) {
+                KT(5);
+                KTV(6, 2);
+            }
+            return;
+        }
+    } else {
+        if (zone1 == 1 && blockIdx.x == 0) {
+            zone_one<S, EXACT, BT, KB_LT, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, dtb, a, b, nw, mc,
+                                                 wg_bytes + nbody, round);
+            if (t == 0) {
+                KT(5);
+                KTV(6, 2);
+            }
+            return;
+        }
+    }
+    if (bid >= nbody) {
+        const uint64_t src0 = (uint64_t)gs->n + gs->off - gs->poff - 2ull * mc - gs->Bp;
+        const uint64_t stride = (uint64_t)(gridDim.x - nbody) * BT;
+        for (uint64_t v = (uint64_t)(bid - nbody) * BT + t; v < mc; v += stride) wtmp[v] = zoth[src0 + v];
+        if (t == 0) {
+            KT(5);
+            KTV(6, 3);
+        }
+        return;
+    }
+    const uint32_t pid_ab = (a << 16) | b;
+    BodyCand& cb = u.c;
+    lds_clear(lt);
+    if (t == 0) s_any = 0u;
+    uint32_t removed = 0, ncand_all = 0;
+    uint64_t moved = 0, rd = 0;   // sector symbols read + rewritten (wave-uniform); extents + signature words read
+    const uint32_t w_beg = bid * wpg, w_end = w_beg + wpg < W ? w_beg + wpg : W;
+    for (uint32_t w0 = w_beg; w0 < w_end; w0 += SP_PW) {
+        __syncthreads();   // the previous pass is done with s_ntok / s_n / the candidate arrays
+        if (t == 0) {
+            s_ntok = 0u;
+            s_n = 0u;
+        }
+        __syncthreads();
+        if (t < (int)SP_PW && w0 + t < w_end) {   // token candidates
+            const uint32_t w = w0 + t;
+            uint32_t c = bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w];
+            if (c) {
+                uint32_t pos = atomicAdd(&s_ntok, (uint32_t)__popc(c));
+                while (c) {
+                    const int bit = __ffs(c) - 1;
+                    c &= c - 1;
+                    cb.sec[pos++] = w * 32u + (uint32_t)bit;
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t ntok = s_ntok;
+        if (t == 0) KT(2);
+        if (ntok == 0) continue;   // block-uniform
+        rd += 16ull * ntok;
+        // signature filter: this thread's candidates (their extents load alongside)
+        // into registers, then compacted in place
+        uint32_t cs[QPT];
+        uint2 ce[QPT];
+        bool ck[QPT];
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) {
+            const uint32_t j = (uint32_t)t + (uint32_t)q * BT;
+            cs[q] = j < ntok ? cb.sec[j] : SP_INV;
+        }
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) {
+            ck[q] = false;
+            if (cs[q] != SP_INV) {
+                ce[q] = sec[cs[q]];
+                ck[q] = sig_has(sig + (uint64_t)cs[q] * SP_SIGW, pid_ab);
+            }
+        }
+        __syncthreads();   // every candidate is read before the list is rewritten
+#pragma unroll
+        for (int q = 0; q < QPT; ++q)
+            if (ck[q]) {
+                const uint32_t qq = atomicAdd(&s_n, 1u);
+                cb.sec[qq] = cs[q];
+                cb.ext[qq] = ce[q];
+            }
+        __syncthreads();
+        const uint32_t ncand = s_n;
+        if (t == 0) KT(3);
+        if (ncand == 0) continue;   // block-uniform
+        ncand_all += ncand;
+        if (t == 0) s_any = 1u;
+        // software-pipelined: a wave's next sector loads while it merges this one
+        uint32_t nf[5], nfm[4];
+        if ((uint32_t)wid < ncand)
+            sector_first<S>(body + cb.ext[wid].x, lmul ? lmul + cb.ext[wid].x : nullptr, cb.ext[wid].y, nf, nfm);
+        for (uint32_t j = wid; j < ncand; j += BT / 64) {
+            const uint32_t sct = cb.sec[j];
+            const uint2 e = cb.ext[j];
+            uint32_t cf[5], cfm[4];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) cf[k] = nf[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cfm[k] = nfm[k];
+            if (j + BT / 64 < ncand) {
+                const uint2 en = cb.ext[j + BT / 64];
+                sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
+            }
+            uint32_t out = 0;
+            const uint32_t r = body_sector<S, KB_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, dtb, st,
+                                              sig + (uint64_t)sct * SP_SIGW, out, cf, cfm);
+            moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (r ? out : 0u));
+            if (r) {
+                removed += r;
+                if (lane == 0) {
+                    if (clog) atomicAdd(&st->hitsec, 1u);
+                    sec[sct].y = out;
+                    atomicOr(&bits[(uint64_t)nw * W + (sct >> 5)], 1u << (sct & 31u));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (t == 0) KT(4);
+    if (!s_any) {   // block-uniform: no candidate survived the filters
+        if (t == 0) {
+            if (rd) atomicAdd(&wg_bytes[bid], rd);
+            KT(5);
+            KTV(6, 0);
+        }
+        return;
+    }
+    if (t == 0 && clog) atomicAdd(&st->cand, ncand_all);
+    lds_flush(lt, dtb, st);
+    if (lane == 0) {
+        s_rm[wid] = removed;
+        s_mv[wid] = moved;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t r = 0;
+        uint64_t mv = rd;
+        for (int w2 = 0; w2 < BT / 64; ++w2) {
+            r += s_rm[w2];
+            mv += s_mv[w2];
+        }
+        if (r) atomicAdd(&st->body_rm, r);
+        atomicAdd(&wg_bytes[bid], mv);   // this workgroup's own counter
+        KT(5);
+        KTV(6, 1 | (ncand_all << 8));
+    }
+}
+
+// ── persistent tail loop ──
+// Late merges (a few hundred sites in a handful of distinct words, a zone of a
+// few K symbols) cost launches and dependent round trips, not bytes: k_body +
+// k_refresh spend ~20 us per merge at 1 GiB on ~10 candidate sectors.  k_tail is
+// ONE 1024-thread workgroup that runs a whole step's merges back to back.  It is
+// the only writer of the pair table while it runs, so
+//   * selection reduces group maxima kept in LDS (64 argmax blocks per group)
+//     instead of a k_refresh pass and its partial maxima;
+//   * count deltas reach the table as plain read-modify-writes; each raises its
+//     block maximum (atomicMax) or, when it lowers the block's holder, has the
+//     block re-maxed from its 2048 slots by one wave;
+//   * the body pass (every bitmap word of rows a and b in one load, signatures,
+//     one wave per candidate sector) and the zone pass (zone_one) share one LDS
+//     delta table and one flush.
+// It leaves the step early — the host finishes it with k_body — when a merge's
+// candidate sectors or re-maxed blocks outgrow its LDS lists.
+#ifdef GBPE_TAIL_LOOP
+constexpr int TL_BT = 1024;
+constexpr int TL_LT = 4096;               // LDS delta table (body + zone deltas of one merge)
+constexpr uint32_t TL_GRP = 6;            // log2 argmax blocks per group
+constexpr uint32_t TL_MAXG = 256;         // groups: tables of up to 2^25 slots
+constexpr uint32_t TL_RS = 1024;          // re-maxed blocks per merge
+constexpr uint32_t TL_CAND = 8192;        // candidate sectors per merge (token bitmap)
+constexpr uint32_t TL_FILT = 3072;        // ... passing the signature filter
+enum : uint32_t { TL_EXIT_NONE = 0, TL_EXIT_CAND = 1, TL_EXIT_REMAX = 2, TL_EXIT_LDS = 3 };
+
+struct TailBody {   // the body pass's lists (the zone pass reuses this LDS)
+    uint32_t cand[TL_CAND];
+    uint32_t fsec[TL_FILT];
+    uint2 fext[TL_FILT];
+};
+template <typename S>
+union TailU {
+    ZoneLds<S, TL_BT> z;
+    TailBody c;
+};
+static_assert(sizeof(TailBody) <= sizeof(ZoneLds<uint32_t, TL_BT>), "the body lists share the zone's LDS");
+
+__device__ __forceinline__ uint64_t tl_key(uint32_t cnt, uint32_t pid) {
+    return (int32_t)cnt > 0 ? (((uint64_t)cnt << 32) | (uint32_t)~pid) : 0ull;
+}
+
+template <typename S, bool EXACT, int ZPT>
+__global__ __launch_bounds__(TL_BT) void k_tail(DevState* st, DevState* zst, S* __restrict__ body, uint32_t* __restrict__ lmul,
+                                                uint2* __restrict__ sec, uint32_t* __restrict__ bits, uint32_t W,
+                                                uint32_t wused, uint32_t* __restrict__ sig, Table tb, S* __restrict__ zb0,
+                                                S* __restrict__ zb1, uint32_t* __restrict__ log,
+                                                uint64_t* __restrict__ bytes, uint32_t* __restrict__ tstat) {
+    __shared__ TailU<S> u;
+    __shared__ LdsTab<TL_LT> lt;
+    __shared__ uint64_t gmax[TL_MAXG];
+    __shared__ uint32_t rs[TL_RS], rsmark[(TL_MAXG << TL_GRP) / 32], gmark[TL_MAXG / 32];
+    __shared__ uint32_t s_nrs, s_ntok, s_nf, s_rm, s_exit, s_used, s_idx, zout[2];
+    __shared__ uint64_t s_red[TL_BT / 64];
+    constexpr int NW = sizeof(DevState) / 4;
+    constexpr uint32_t NWAVE = TL_BT / 64;
+    __shared__ union {
+        DevState d;
+        uint32_t w[NW];
+    } s_g, s_z;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t ngrp = (tb.nblk + (1u << TL_GRP) - 1) >> TL_GRP;
+    if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
+    else if (t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
+    for (uint32_t g = wid; g < ngrp; g += NWAVE) {   // group maxima from the (exact) block maxima
+        const uint32_t blk = (g << TL_GRP) + (uint32_t)lane;
+        uint64_t v = blk < tb.nblk ? tb.bmax[blk] : 0ull;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(v, off);
+            v = o > v ? o : v;
+        }
+        if (lane == 0) gmax[g] = v;
+    }
+    for (uint32_t i = t; i < (TL_MAXG << TL_GRP) / 32; i += TL_BT) rsmark[i] = 0u;
+    if (t < (int)(TL_MAXG / 32)) gmark[t] = 0u;
+    if (t == 0) {
+        s_exit = TL_EXIT_NONE;
+        s_used = 0u;
+    }
+    __syncthreads();
+    DevState& g = s_g.d;
+    DevState& z = s_z.d;
+    const uint32_t K = g.budget;
+    uint64_t mybytes = 0;
+    auto remax_mark = [&](uint32_t blk) {   // queue a block for re-maxing (once per merge)
+        const uint32_t bit = 1u << (blk & 31u);
+        if (!(atomicOr(&rsmark[blk >> 5], bit) & bit)) {
+            const uint32_t q = atomicAdd(&s_nrs, 1u);
+            if (q < TL_RS) rs[q] = blk;
+            else tb.dirty[blk] = 1u;   // k_refresh after the kernel re-maxes it; the loop stops after this merge
+        }
+    };
+    uint32_t r = g.merges_done;
+    for (; r < K; ++r) {
+        if (g.stop || g.sp_abort || g.err) break;   // (uniform: LDS state, read after a barrier)
+        if (t == 0) TKT(0);
+        // ── selection: group maxima (LDS) ──
+        uint64_t best = 0;
+        for (uint32_t i = t; i < ngrp; i += TL_BT) best = gmax[i] > best ? gmax[i] : best;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(best, off);
+            best = o > best ? o : best;
+        }
+        if (lane == 0) s_red[wid] = best;
+        if (t == 0) {
+            s_ntok = 0u;
+            s_nf = 0u;
+            s_rm = 0u;
+            s_nrs = 0u;
+        }
+        lds_clear(lt);
+        __syncthreads();
+        best = s_red[0];
+#pragma unroll
+        for (uint32_t w2 = 1; w2 < NWAVE; ++w2) best = s_red[w2] > best ? s_red[w2] : best;
+        const uint32_t mc = (uint32_t)(best >> 32), pid = ~(uint32_t)best, a = pid >> 16, b = pid & 0xFFFFu;
+        const uint32_t nw = g.next_id;
+        if (mc < 2u || nw > 0xFFFFu) {   // train.wgsl:345-348
+            if (t == 0) g.stop = 1u;
+            break;
+        }
+        if (t == 0) TKT(1);
+        if (!EXACT) {
+            if ((uint64_t)g.n < 2ull * mc + g.Bp) {   // cannot happen (k_body's invariant)
+                if (t == 0) {
+                    g.err |= ERR_SPARSE_WINDOW;
+                    g.stop = 1u;
+                }
+                break;
+            }
+            if ((uint64_t)z.n < 5ull * mc + 2u) {   // zone misfit: the host goes dense
+                if (t == 0) g.sp_abort = 1u;
+                break;
+            }
+        }
+        // ── body candidates: every bitmap word of rows a and b at once (thread 0 finds (a,b)'s slot first) ──
+        if (t == 0) s_idx = table_find(tb, pid);
+        for (uint32_t w = t; w < wused; w += TL_BT) {
+            uint32_t c = bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w];
+            if (c) {
+                uint32_t pos = atomicAdd(&s_ntok, (uint32_t)__popc(c));
+                for (; c; c &= c - 1, ++pos)
+                    if (pos < TL_CAND) u.c.cand[pos] = w * 32u + (uint32_t)(__ffs(c) - 1);
+            }
+        }
+        __syncthreads();
+        const uint32_t ntok = s_ntok;
+        if (t == 0) {
+            TKT(2);
+            TKTV(10, ntok);
+        }
+        if (ntok > TL_CAND) {   // nothing of merge r is committed yet
+            if (t == 0) s_exit = TL_EXIT_CAND;
+            break;
+        }
+        for (uint32_t j = t; j < ntok; j += TL_BT) {   // signature filter (+ extents)
+            const uint32_t k = u.c.cand[j];
+            const uint2 e = sec[k];
+            if (sig_has(sig + (uint64_t)k * SP_SIGW, pid)) {
+                const uint32_t q = atomicAdd(&s_nf, 1u);
+                if (q < TL_FILT) {
+                    u.c.fsec[q] = k;
+                    u.c.fext[q] = e;
+                }
+            }
+        }
+        if (t == 0) mybytes += 16ull * ntok;
+        __syncthreads();
+        const uint32_t nf = s_nf;
+        if (t == 0) {
+            TKT(3);
+            TKTV(11, nf);
+        }
+        if (nf > TL_FILT) {
+            if (t == 0) s_exit = TL_EXIT_CAND;
+            break;
+        }
+        // ── commit: the log (thread 0); count(a,b) -= mc and the re-max of its block and
+        //    group by the last wave, while the others merge sectors ──
+        const uint32_t idx = s_idx;
+        if (t == 0) {
+            if (idx == 0xFFFFFFFFu) g.err |= ERR_PAIR_MISSING;
+            log[r * 4 + 0] = a;
+            log[r * 4 + 1] = b;
+            log[r * 4 + 2] = nw;
+            log[r * 4 + 3] = mc;
+        }
+        if (wid == (int)NWAVE - 1 && idx != 0xFFFFFFFFu) {
+            constexpr int NV = (1 << BLK_LOG2) / 2 / 64;   // 16-byte loads per lane
+            const uint32_t blk = idx >> BLK_LOG2, gq = blk >> TL_GRP, gb = (gq << TL_GRP) + (uint32_t)lane;
+            const uint32_t cnt_new = tb.slots[idx].y - mc;
+            const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)blk << BLK_LOG2));
+            uint4 e[NV];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) e[k] = sl[lane + k * 64];
+            const uint64_t gbm = gb < tb.nblk && gb != blk ? tb.bmax[gb] : 0ull;
+            if (lane == 0) tb.slots[idx].y = cnt_new;
+            uint64_t bst = 0;
+            uint32_t live = 0;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {   // (a,b)'s slot with its new count
+                const uint32_t s0 = ((uint32_t)(lane + k * 64) << 1) + ((blk << BLK_LOG2));
+                const uint32_t c1 = s0 == idx ? cnt_new : e[k].y, c2 = s0 + 1 == idx ? cnt_new : e[k].w;
+                const uint64_t k1 = e[k].x ? tl_key(c1, e[k].x) : 0ull, k2 = e[k].z ? tl_key(c2, e[k].z) : 0ull;
+                bst = k1 > bst ? k1 : bst;
+                bst = k2 > bst ? k2 : bst;
+                live += (k1 ? 1u : 0u) + (k2 ? 1u : 0u);
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint64_t o = __shfl_xor(bst, off);
+                bst = o > bst ? o : bst;
+                live += __shfl_xor(live, off);
+            }
+            uint64_t gv = gbm > bst ? gbm : bst;
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint64_t o = __shfl_xor(gv, off);
+                gv = o > gv ? o : gv;
+            }
+            if (lane == 0) {
+                tb.bmax[blk] = bst;
+                tb.blive[blk] = live;
+                gmax[gq] = gv;
+            }
+        }
+        // ── body sectors: one wave each, the next one's loads in flight ──
+        {
+            uint32_t removed = 0;
+            uint64_t moved = 0;
+            uint32_t nf5[5], nfm[4];
+            if ((uint32_t)wid < nf)
+                sector_first<S>(body + u.c.fext[wid].x, lmul ? lmul + u.c.fext[wid].x : nullptr, u.c.fext[wid].y, nf5, nfm);
+            for (uint32_t j = wid; j < nf; j += NWAVE) {
+                const uint32_t sct = u.c.fsec[j];
+                const uint2 e = u.c.fext[j];
+                uint32_t cf[5], cfm[4];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) cf[k] = nf5[k];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cfm[k] = nfm[k];
+                if (j + NWAVE < nf) {
+                    const uint2 en = u.c.fext[j + NWAVE];
+                    sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf5, nfm);
+                }
+                uint32_t out = 0;
+                const uint32_t rr = body_sector<S, TL_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, tb, st,
+                                                         sig + (uint64_t)sct * SP_SIGW, out, cf, cfm);
+                moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (rr ? out : 0u));
+                if (rr) {
+                    removed += rr;
+                    if (lane == 0) {
+                        sec[sct].y = out;
+                        atomicOr(&bits[(uint64_t)nw * W + (sct >> 5)], 1u << (sct & 31u));
+                    }
+                }
+            }
+            if (lane == 0) {
+                if (removed) atomicAdd(&s_rm, removed);
+                mybytes += moved;
+            }
+        }
+        __syncthreads();
+        if (t == 0) TKT(4);
+        // ── zone (the same delta table) ──
+        S* zc = (r & 1u) ? zb1 : zb0;
+        S* zo = (r & 1u) ? zb0 : zb1;
+        zone_one<S, EXACT, TL_BT, TL_LT, ZPT>(st, zst, g, z, zc, zo, u.z, lt, tb, a, b, nw, mc, bytes, r, zout);
+        __syncthreads();
+        if (t == 0) TKT(5);
+        // ── flush: plain read-modify-writes (the only writer), block maxima kept exact ──
+        {
+            uint32_t kk[TL_LT / TL_BT], vv[TL_LT / TL_BT];
+#pragma unroll
+            for (int j = 0; j < TL_LT / TL_BT; ++j) {
+                kk[j] = lt.key[t + j * TL_BT];
+                vv[j] = lt.val[t + j * TL_BT];
+            }
+#pragma unroll
+            for (int j = 0; j < TL_LT / TL_BT; ++j) {
+                const uint32_t p = kk[j], d = vv[j];
+                if (!p || !d) continue;
+                const uint32_t h = gbpe_fmix32(p) & tb.mask;
+                uint32_t idx = 0xFFFFFFFFu, old = 0;
+                for (uint32_t q = 0; q <= tb.mask; ++q) {
+                    const uint32_t i2 = (h + ((q * (q + 1)) >> 1)) & tb.mask;
+                    uint32_t k2 = tb.slots[i2].x;
+                    if (k2 == 0u) {
+                        k2 = atomicCAS(&tb.slots[i2].x, 0u, p);   // another new pair may race for the slot
+                        if (k2 == 0u) {
+                            atomicAdd(&s_used, 1u);
+                            idx = i2;
+                            old = 0u;
+                            break;
+                        }
+                    }
+                    if (k2 == p) {
+                        idx = i2;
+                        old = tb.slots[i2].y;
+                        break;
+                    }
+                }
+                if (idx == 0xFFFFFFFFu) {
+                    atomicOr(&g.err, ERR_TABLE_FULL);
+                    continue;
+                }
+                const uint32_t nv = old + d;
+                tb.slots[idx].y = nv;
+                const uint32_t blk = idx >> BLK_LOG2;
+                const uint64_t bm = __hip_atomic_load(&tb.bmax[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t ok = tl_key(old, p), nk = tl_key(nv, p);
+                if (nk > bm) {
+                    atomicMax(&tb.bmax[blk], nk);
+                    atomicMax(&gmax[blk >> TL_GRP], nk);
+                } else if (nk < ok && ok == bm) {
+                    remax_mark(blk);
+                }
+            }
+        }
+        __syncthreads();
+        if (t == 0) {
+            TKT(6);
+            TKTV(9, s_nrs);
+        }
+        // ── re-max queued blocks (one wave each), then their groups ──
+        if (s_nrs) {
+            const uint32_t nrs = s_nrs < TL_RS ? s_nrs : TL_RS;
+            constexpr int NV = (1 << BLK_LOG2) / 2 / 64;   // 16-byte loads per lane
+            for (uint32_t q = wid; q < nrs; q += NWAVE) {
+                const uint32_t blk = rs[q];
+                const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)blk << BLK_LOG2));
+                uint4 e[NV];
+#pragma unroll
+                for (int k = 0; k < NV; ++k) e[k] = sl[lane + k * 64];
+                uint64_t bst = 0;
+                uint32_t live = 0;
+#pragma unroll
+                for (int k = 0; k < NV; ++k) {
+                    const uint64_t k1 = e[k].x ? tl_key(e[k].y, e[k].x) : 0ull, k2 = e[k].z ? tl_key(e[k].w, e[k].z) : 0ull;
+                    bst = k1 > bst ? k1 : bst;
+                    bst = k2 > bst ? k2 : bst;
+                    live += (k1 ? 1u : 0u) + (k2 ? 1u : 0u);
+                }
+                for (int off = 32; off > 0; off >>= 1) {
+                    const uint64_t o = __shfl_xor(bst, off);
+                    bst = o > bst ? o : bst;
+                    live += __shfl_xor(live, off);
+                }
+                if (lane == 0) {
+                    tb.bmax[blk] = bst;
+                    tb.blive[blk] = live;
+                    atomicOr(&gmark[blk >> (TL_GRP + 5)], 1u << ((blk >> TL_GRP) & 31u));
+                }
+            }
+            __syncthreads();
+            for (uint32_t gq = wid; gq < ngrp; gq += NWAVE) {
+                if (!((gmark[gq >> 5] >> (gq & 31u)) & 1u)) continue;   // wave-uniform
+                const uint32_t blk = (gq << TL_GRP) + (uint32_t)lane;
+                uint64_t v = blk < tb.nblk ? __hip_atomic_load(&tb.bmax[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                for (int off = 32; off > 0; off >>= 1) {
+                    const uint64_t o = __shfl_xor(v, off);
+                    v = o > v ? o : v;
+                }
+                if (lane == 0) gmax[gq] = v;
+            }
+            __syncthreads();
+            if (t == 0) TKT(7);
+            for (uint32_t i = t; i < (TL_MAXG << TL_GRP) / 32; i += TL_BT) rsmark[i] = 0u;
+            if (t < (int)(TL_MAXG / 32)) gmark[t] = 0u;
+        }
+        // ── state (thread 0): the k_refresh (finish 2) bookkeeping ──
+        if (t == 0) {
+            const uint32_t m = zout[0], zkeep = zout[1];
+            const uint32_t n = g.n - mc, B = g.B - s_rm;
+            g.tail_total += m;
+            g.Bp = g.B;
+            g.B = B;
+            g.n = n;
+            g.new_n = n;
+            g.a = a;
+            g.b = b;
+            g.nw = nw;
+            g.mc = mc;
+            z.n = n - B;
+            g.zlast = z.n;
+            if (z.n != zkeep) {
+                g.err |= ERR_COUNT_MISMATCH;
+                g.stop = 1u;
+            }
+            g.next_id = nw + 1u;
+            g.epoch += 1u;
+            g.merges_done = r + 1u;
+            z.merges_done = r + 1u;
+            if (s_nrs > TL_RS) s_exit = TL_EXIT_REMAX;
+            if (lt.ovf) s_exit = TL_EXIT_LDS;
+        }
+        __syncthreads();
+        if (s_exit != TL_EXIT_NONE) {   // dirty blocks left for the host's k_refresh
+            ++r;
+            break;
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        g.body_rm = 0u;
+        tstat[0] = g.merges_done;
+        tstat[1] = s_exit;
+    }
+    if (mybytes) atomicAdd(bytes, mybytes);
+    __syncthreads();
+    // the states back (`used` by an add: an overflowing LDS table inserted through table_add)
+    constexpr int WUSED = (int)(offsetof(DevState, used) / 4);
+    if (t < NW) {
+        if (t != WUSED) reinterpret_cast<uint32_t*>(st)[t] = s_g.w[t];
+    } else if (t < 2 * NW) {
+        reinterpret_cast<uint32_t*>(zst)[t - NW] = s_z.w[t - NW];
+    }
+    if (t == 0 && s_used) atomicAdd(&st->used, s_used);
+}
+#endif  // GBPE_TAIL_LOOP
+
+// dense → sparse: the last position at or before `lim` that no counted pair can
+// span — a word start, or a token-0 symbol on either side (one workgroup,
+// backwards).  The 0s count: the stale window of a huge merge is a 0 run of up
+// to ~mc symbols (C5's first merge: ~180M), which a word-start-only search
+// crossed at 1024 symbols per round (25 ms per entry / shrink).
+template <typename S>
+__global__ __launch_bounds__(1024) void k_sp_zone_start(const S* __restrict__ cur, uint32_t lim, uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_found;
+    if (threadIdx.x == 0) s_found = 0u;
+    __syncthreads();
+    for (int64_t hi = lim; hi >= 1; hi -= 1024) {
+        const int64_t i = hi - (int64_t)threadIdx.x;
+        const uint32_t x = i >= 1 ? (uint32_t)cur[i] : 0u, p = i >= 1 ? (uint32_t)cur[i - 1] : 0u;
+        if (i >= 1 && ((x & Sym<S>::WS) || !(x & Sym<S>::TM) || !(p & Sym<S>::TM))) atomicMax(&s_found, (uint32_t)i);
+        __syncthreads();
+        const uint32_t f = s_found;
+        __syncthreads();
+        if (f) break;
+    }
+    if (threadIdx.x == 0) *out = s_found;   // 0 = none
+}
+
+// window j of a body region [base, base + len) covers [base + j*SEC, +SEC); its
+// sector starts at the window's first word start or 0 symbol (window 0: at
+// `base`, which is a word start or the stream's first symbol).  No counted pair
+// spans either: pairs never cross a word start, and none holds token 0 — the
+// stale windows the reference compaction leaves are long 0 runs
+// that would otherwise make one sector of up to ~10^6 symbols.  One wave per
+// window.
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_sectors(const S* __restrict__ body, uint32_t base, uint32_t len, uint32_t SEC,
+                                                    uint32_t* __restrict__ starts, uint32_t nwin) {
+    const uint32_t j = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (j >= nwin) return;
+    const uint64_t end = (uint64_t)base + len;
+    const uint64_t lo = (uint64_t)base + (uint64_t)j * SEC, hi = lo + SEC < end ? lo + SEC : end;
+    uint32_t found = j == 0 ? base : SP_INV;
+    for (uint64_t b0 = lo; b0 < hi && found == SP_INV; b0 += 64) {
+        const uint64_t i = b0 + lane;
+        uint32_t x = i < hi ? (uint32_t)body[i] : 1u;
+        const bool ws = (x & Sym<S>::WS) || x == 0u;
+        const unsigned long long m = __ballot(ws);
+        if (m) found = (uint32_t)(b0 + (uint64_t)(__ffsll((long long)m) - 1));
+    }
+    if (lane == 0) starts[j] = found;
+}
+
+__global__ void k_sp_sector_len(const uint32_t* __restrict__ starts, uint32_t nwin, uint32_t end, uint2* __restrict__ sec) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nwin) return;
+    const uint32_t st = starts[k];
+    if (st == SP_INV) {
+        sec[k] = make_uint2(0u, 0u);
+        return;
+    }
+    uint32_t e = end;
+    for (uint32_t j = k + 1; j < nwin; ++j)   // windows inside one long word have no start
+        if (starts[j] != SP_INV) {
+            e = starts[j];
+            break;
+        }
+    sec[k] = make_uint2(st, e - st);
+}
+
+// presence bits of every token (with `bits`) and the pair signature of sectors
+// [k0, k0 + nk), one wave per sector.  The signature is built in LDS and stored
+// whole (one 128-B line per sector); bitmap words are tested before the atomic.
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_bits(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t k0,
+                                                 uint32_t nk, uint32_t* __restrict__ bits, uint32_t W,
+                                                 uint32_t* __restrict__ sig) {
+    __shared__ uint32_t ssig[TPB / 64][SP_SIGW];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t k = k0 + blockIdx.x * (TPB / 64) + wid;
+    const bool live = k < k0 + nk;
+    if (lane < (int)SP_SIGW) ssig[wid][lane] = 0u;
+    __syncthreads();
+    if (live) {
+        const uint2 e = sec[k];
+        const uint32_t bit = 1u << (k & 31u);
+        uint32_t* col = bits ? bits + (k >> 5) : nullptr;
+        for (uint32_t j = lane; j < e.y; j += 64) {
+            const uint32_t x = body[e.x + j];
+            const uint32_t tok = x & Sym<S>::TM;
+            if (col) {
+                uint32_t* wp = col + (uint64_t)tok * W;
+                if (!(*wp & bit)) atomicOr(wp, bit);
+            }
+            if (j && !(x & Sym<S>::WS)) {
+                const uint32_t tp = body[e.x + j - 1] & Sym<S>::TM;
+                if (tp && tok) sig_set(ssig[wid], (tp << 16) | tok);
+            }
+        }
+    }
+    __syncthreads();
+    if (live && lane < (int)SP_SIGW) sig[(uint64_t)k * SP_SIGW + lane] = ssig[wid][lane];
+}
+
+// token bitmap of whole columns (a full rebuild over a zeroed bitmap): one
+// workgroup per 32-sector column gathers token -> sector mask in LDS, then
+// writes each present token's word once (plain stores; the column is its own).
+// Tokens beyond the LDS table's reach take a global atomicOr instead.
+constexpr int COLT = 8192;
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_colbits(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t nsec,
+                                                    uint32_t* __restrict__ bits, uint32_t W) {
+    __shared__ uint32_t key[COLT], msk[COLT];
+    for (int i = threadIdx.x; i < COLT; i += TPB) {
+        key[i] = 0xFFFFFFFFu;
+        msk[i] = 0u;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t c = blockIdx.x;
+    for (uint32_t q = wid; q < 32; q += TPB / 64) {
+        const uint32_t k = c * 32 + q;
+        if (k >= nsec) break;
+        const uint2 e = sec[k];
+        for (uint32_t j = lane; j < e.y; j += 64) {
+            const uint32_t tok = body[e.x + j] & Sym<S>::TM;
+            uint32_t h = gbpe_fmix32(tok) & (COLT - 1);
+            bool done = false;
+            for (int p = 0; p < 32 && !done; ++p) {
+                const uint32_t o = atomicCAS(&key[h], 0xFFFFFFFFu, tok);
+                if (o == 0xFFFFFFFFu || o == tok) {
+                    atomicOr(&msk[h], 1u << q);
+                    done = true;
+                }
+                h = (h + 1) & (COLT - 1);
+            }
+            if (!done) atomicOr(&bits[(uint64_t)tok * W + c], 1u << q);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < COLT; i += TPB)
+        if (key[i] != 0xFFFFFFFFu) atomicOr(&bits[(uint64_t)key[i] * W + c], msk[i]);
+}
+
+// sparse → dense: sector counts, then a gather at the scanned offsets (one wave per sector)
+__global__ void k_sp_counts(const uint2* __restrict__ sec, uint32_t nsec, uint32_t* __restrict__ cnt) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nsec) cnt[k] = sec[k].y;
+}
+
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_gather(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t nsec,
+                                                   const uint32_t* __restrict__ loc, const uint64_t* __restrict__ blk,
+                                                   S* __restrict__ dst) {
+    const uint32_t k = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (k >= nsec) return;
+    const uint2 e = sec[k];
+    const uint64_t off = (uint64_t)loc[k] + blk[k / SCAN_BLK];
+    for (uint32_t j = lane; j < e.y; j += 64) dst[off + j] = body[e.x + j];
+}
+
+#include "lexicon.h"
+
+}  // namespace

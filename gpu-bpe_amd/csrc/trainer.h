@@ -1,0 +1,1016 @@
+// Host side of the trainer shared by the training translation units: the
+// gbpe_trainer object and the helpers that lay out and re-lay out its state
+// (pair table, sector-sparse layout, word lexicon, zone).  See train.hip.
+#pragma once
+
+#include "train_dev.h"
+
+
+// ─── host side ──────────────────────────────────────────────────────────────
+
+
+struct gbpe_trainer {
+    gbpe_ctx* ctx = nullptr;
+    bool u16 = true;
+    uint32_t bps = 2;            // bytes per symbol
+    uint64_t n0 = 0, cap_syms = 0;
+    uint64_t n_prev0 = 0;        // created from a state: its previous-stream length (export before any merge)
+    void* buf[2] = {nullptr, nullptr};
+    int cur = 0;                 // index of the buffer holding the stream
+    uint32_t n = 0;              // host copy of the stream length
+    uint32_t needed = 0, done = 0;
+    bool stop = false;
+    uint32_t flags = 0, batch = GBPE_BATCH_SIZE;
+    DevState* st = nullptr;
+    DevState* h_st = nullptr;    // pinned
+    uint32_t* d_log = nullptr;
+    uint32_t* h_log = nullptr;   // pinned
+    Table tb{};
+    uint32_t table_log2 = 22;
+    uint32_t* hitmask = nullptr;
+    uint32_t* tile_cnt = nullptr;
+    uint32_t* grpsum = nullptr;
+    // sharded training
+    bool sharded = false;
+    uint32_t rank = 0, world = 1;
+    Table dt{};                    // per-merge count-delta table (local deltas before the exchange)
+    uint32_t* d_nlog = nullptr;    // local length before each merge of a step
+    uint32_t* h_nlog = nullptr;    // pinned
+    uint32_t step_k = 0;
+    uint32_t* rec_send = nullptr;  // exchange records of gbpe_shard_step_comm
+    uint32_t* rec_recv = nullptr;
+    uint64_t rec_words = 0;
+    // stats
+    uint64_t bytes_moved = 0;
+    uint64_t max_live = 0;
+    double ms_merge = 0, ms_select = 0, ms_other = 0, ms_delta = 0, ms_compact = 0;
+    uint64_t timed_merges = 0;
+    std::vector<hipEvent_t> evs;
+    // sector-sparse loop
+    bool sp = false;             // the stream is in the sector layout
+    uint32_t sp_secw = 256;      // sector window (symbols)
+    uint32_t max_id = 0;         // exclusive bound of every token id of the run (bitmap rows)
+    uint32_t last_mc = 0;        // count of the last merge run
+    int bcur = 0;                // dense buffer holding the body sectors
+    uint32_t nsec = 0;
+    uint64_t nsec_cap = 0, loc_cap = 0;
+    uint32_t bend = 0;           // end of the body's sector windows in the body buffer
+    uint32_t sp_shrinks = 0;     // zone shrinks since the last entry
+    uint2* sec = nullptr;        // {start, count} per sector
+    uint32_t* sp_loc = nullptr;  // per-sector scratch (starts / scan)
+    uint64_t* sp_blk = nullptr;  // scan block totals
+    uint32_t* bits = nullptr;    // presence bitmap, rows = token ids, W words per row
+    uint32_t* sig = nullptr;     // per-sector pair signatures (SP_SIGW words each)
+    uint64_t sig_cap = 0;
+    uint64_t sp_age = 0;         // sparse merges since the signatures were built
+    uint64_t sp_bits_age = 0;    // ... since the token bitmap was built
+    uint64_t bits_cap = 0;       // words
+    uint32_t W = 0;
+    void* zbuf[2] = {nullptr, nullptr};
+    void* wtmp = nullptr;        // stale-window source copy
+    uint64_t zcap = 0;           // zone buffer capacity (symbols)
+    int zcur = 0;                // zone buffer holding the zone
+    DevState* zst = nullptr;     // the zone's loop state
+    DevState* h_zst = nullptr;   // pinned
+    uint32_t* d_u32 = nullptr;   // small device scratch
+    uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
+    uint32_t* zseg = nullptr;    // ZSegState: the zone segments' per-merge hand-off (k_refresh zeroes it)
+    uint32_t zseg_mode = 1;      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
+    uint32_t table_grows = 0;    // crowded-table rebuilds (same size or larger)
+    uint64_t* wg_bytes = nullptr;   // bytes moved per k_body workgroup (each its own counter)
+    uint32_t delta_mt = 2048;       // dense k_delta: multi-tile workgroups from this many tiles (0 = never; GBPE_DELTA_MT)
+    uint32_t delta_tpw = 8;         // ... of 8, 16 or 32 tiles (GBPE_DELTA_TPW)
+    uint64_t wg_cap = 0;
+    double ms_sparse = 0, ms_dense = 0;   // GBPE_TRAIN_TIMING: merge passes (without selection / refresh) by mode
+    double ms_body = 0;          // GBPE_TRAIN_TIMING: k_body alone
+    uint64_t dense_bytes = 0;    // algorithmic stream bytes of the dense merges
+    uint32_t g_refresh = 0;
+    uint64_t sp_merges = 0, sp_sectors = 0, sp_zone = 0;
+    uint32_t sp_enters = 0, sp_exits = 0;
+    uint32_t sp_div = 64;        // enter when last_mc * sp_div <= n
+    uint32_t sp_cooldown = 0;    // steps to stay dense after an abort
+    uint32_t lx_div = 16;        // with the lexicon: enter once next_mc * lx_div <= n, from the first step on (GBPE_LEXICON_DIV)
+    uint32_t sub_zone = 1u << 20;   // sparse steps run in sub-steps of sub_k merges while the zone exceeds this
+    uint32_t sub_k = 16;            // (the zone shrinks between them; GBPE_SUBSTEP_ZONE, GBPE_SUBSTEP)
+    bool zone16 = true;             // u16 zones of 8K-16K symbols: the 16-per-thread zone pass (GBPE_ZONE16=0: off)
+    // persistent tail loop (k_tail)
+    bool tail_on = true;         // GBPE_TAIL=0: never (a -DGBPE_TAIL_LOOP build only; measured no faster)
+    uint32_t tail_mc = 4096;     // run a step in k_tail once the last count is at most this (GBPE_TAIL_MC)
+    bool tail_skip = false;      // k_tail left the last step early: the next one runs k_body
+    uint32_t* d_tstat = nullptr;
+    uint64_t tail_merges = 0, tail_steps = 0, tail_exits = 0;
+    double ms_tail = 0;
+    uint32_t sp_zt = 5;          // zone target = sp_zt * last_mc + 64 (>= zone_f; GBPE_SPARSE_ZT; 4/5/6/7 measured
+                                 // 0.895/0.893/0.918/0.918 s at 1 GiB with zone_f 3)
+    uint32_t shrink_pct = 200;   // shrink once the zone exceeds shrink_pct % of the target + 4096 (GBPE_SHRINK_PCT)
+    uint32_t zone_f = 3;         // single-GPU zone rule factor (sel_inline; GBPE_ZONE_F, >= 3)
+    uint32_t refresh_blocks = 0; // GBPE_REFRESH_BLOCKS: k_refresh grid (0 = 2 per CU)
+    bool rehash_on = true;       // GBPE_REHASH: grow the table inside the sparse loop (0: exit, grow, recount)
+    uint32_t body_cap = 256;     // GBPE_BODY_WG: most k_body workgroups (default one per CU)
+    uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
+    uint32_t* h_clog = nullptr;
+    FILE* trace = nullptr;
+    // word-lexicon body (lexicon.h): the sectors hold one copy of every
+    // distinct body word instead of the body itself
+    bool lex = false;            // the current sparse entry uses it
+    bool lex_on = true;          // GBPE_LEXICON=0: never
+    void* lx_store = nullptr;    // distinct words, each followed by a 0 separator (S symbols)
+    uint32_t* lx_mul = nullptr;  // per store symbol: its word's occurrences (0 = separator / padding)
+    uint64_t lx_cap = 0, lx_len = 0;   // store symbols: capacity, used
+    uint32_t* lx_occ = nullptr;  // body words in stream order: uid, or LX_LIT | symbol
+    uint64_t lx_occ_cap = 0, lx_nocc = 0;
+    uint32_t* lx_w0 = nullptr;   // first uid of each sector window
+    uint32_t lx_nuid = 0, lx_uid_cap = 0;
+    void* lx_tmp = nullptr;      // build / expansion scratch (grown, kept)
+    uint64_t lx_tmp_bytes = 0;
+    uint64_t lx_words = 0, lx_builds = 0, lx_fallbacks = 0;   // stats
+};
+
+namespace {
+
+int tr_err(gbpe_trainer* t, int code, const char* msg) { return gbpe_set_error(t->ctx, code, "%s", msg); }
+
+#define TR_HIP(t, call) GBPE_HIP((t)->ctx, call)
+
+// the symbols the sparse kernels merge: the lexicon store, or the body sectors in place
+inline void* sp_body(const gbpe_trainer* t) { return t->lex ? t->lx_store : t->buf[t->bcur]; }
+inline uint32_t* sp_mul(const gbpe_trainer* t) { return t->lex ? t->lx_mul : nullptr; }
+// the single-GPU selection's zone rule (sel_inline)
+inline SelShard sel_single(const gbpe_trainer* t) {
+    SelShard sh;
+    sh.zf = t->zone_f;
+    return sh;
+}
+
+
+uint32_t grid_persistent(const gbpe_ctx* ctx, uint64_t work_tiles, uint32_t per_cu) {
+    uint64_t g = (uint64_t)(ctx->num_cu > 0 ? ctx->num_cu : 256) * per_cu;
+    if (work_tiles < g) g = work_tiles;
+    return (uint32_t)(g ? g : 1);
+}
+// a grid over argmax blocks: every workgroup owns at most 64 (one flag ballot)
+uint32_t grid_blocks(const gbpe_ctx* ctx, uint32_t nblk, uint32_t per_cu) {
+    return std::max<uint32_t>(grid_persistent(ctx, nblk, per_cu), (uint32_t)gbpe_div_up(nblk, 64));
+}
+
+// new (empty) table arrays of 2^lg slots; the caller recounts (table_rebuild)
+int table_resize(gbpe_trainer* t, uint32_t lg) {
+    hipStream_t s = t->ctx->stream;
+    TR_HIP(t, hipStreamSynchronize(s));
+    hipFree(t->tb.slots);
+    hipFree(t->tb.bmax);
+    hipFree(t->tb.dirty);
+    hipFree(t->tb.dlist);
+    hipFree(t->tb.blive);
+    t->tb.slots = nullptr, t->tb.bmax = nullptr, t->tb.dirty = nullptr, t->tb.dlist = nullptr, t->tb.blive = nullptr;
+    const uint64_t slots = 1ull << lg;
+    t->table_log2 = lg;
+    t->tb.mask = (uint32_t)(slots - 1);
+    t->tb.nblk = (uint32_t)(slots >> BLK_LOG2);
+    if (hipMalloc(&t->tb.slots, slots * sizeof(uint2)) != hipSuccess ||
+        hipMalloc(&t->tb.bmax, t->tb.nblk * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&t->tb.dirty, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->tb.dlist, (t->tb.nblk + 1) * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess)
+        return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(pair table, 2^%u slots) failed", lg);
+    TR_HIP(t, hipMemsetAsync(t->tb.dirty, 0, t->tb.nblk * sizeof(uint32_t), s));
+    t->g_refresh = grid_blocks(t->ctx, t->tb.nblk, 2);
+    if (t->refresh_blocks) t->g_refresh = std::max<uint32_t>(t->refresh_blocks, (uint32_t)gbpe_div_up(t->tb.nblk, 64));
+    if (t->part) {   // one partial maximum per k_refresh workgroup
+        hipFree(t->part);
+        t->part = nullptr;
+        TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
+    }
+    return GBPE_OK;
+}
+
+int table_rebuild(gbpe_trainer* t) {
+    hipStream_t s = t->ctx->stream;
+    const uint64_t slots = (uint64_t)t->tb.mask + 1;
+    TR_HIP(t, hipMemsetAsync(t->tb.slots, 0, slots * sizeof(uint2), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.bmax, 0, (uint64_t)t->tb.nblk * sizeof(uint64_t), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.blive, 0, (uint64_t)t->tb.nblk * sizeof(uint32_t), s));
+    TR_HIP(t, hipMemsetAsync(&t->st->used, 0, sizeof(uint32_t), s));
+    const uint64_t ntiles = gbpe_div_up(t->n, TILE);
+    const uint32_t g = grid_persistent(t->ctx, ntiles, 2);
+    if (t->u16)
+        hipLaunchKernelGGL(k_count_full<uint16_t>, dim3(g), dim3(TPB), 0, s, t->st,
+                           (const uint16_t*)t->buf[t->cur], t->tb);
+    else
+        hipLaunchKernelGGL(k_count_full<uint32_t>, dim3(g), dim3(TPB), 0, s, t->st,
+                           (const uint32_t*)t->buf[t->cur], t->tb);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    hipLaunchKernelGGL(k_clear_dirty_all, dim3(gbpe_div_up(t->tb.nblk, 256)), dim3(256), 0, s, t->st, t->tb);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    if (t->u16)
+        hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(grid_blocks(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, 0u,
+                           0, t->tb, (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
+    else
+        hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(grid_blocks(t->ctx, t->tb.nblk, 4)), dim3(TPB), 0, s, t->st, 0u,
+                           0, t->tb, (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+
+// Growing the table inside the sector-sparse loop: every count in the table is
+// exact between steps (the body's multiplicities included), so the live entries
+// move to the larger table as they are — no exit to one dense stream, no recount
+// and no lexicon rebuild on re-entry (C5 grew 2^20 -> 2^25 in five such exits).
+__global__ __launch_bounds__(TPB) void k_rehash(const uint2* __restrict__ old, uint64_t nold, DevState* st, Table tb) {
+    for (uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x; i < nold; i += (uint64_t)gridDim.x * TPB) {
+        const uint2 e = old[i];
+        if (e.x && (int32_t)e.y > 0) table_add(tb, st, e.x, e.y);
+    }
+}
+
+int table_rehash(gbpe_trainer* t, uint32_t lg) {
+    hipStream_t s = t->ctx->stream;
+    uint2* old = t->tb.slots;
+    const uint64_t nold = (uint64_t)t->tb.mask + 1;
+    t->tb.slots = nullptr;   // kept until the live entries have moved
+    int rc = table_resize(t, lg);
+    if (rc != GBPE_OK) {
+        hipFree(old);
+        return rc;
+    }
+    const uint64_t slots = (uint64_t)t->tb.mask + 1;
+    TR_HIP(t, hipMemsetAsync(t->tb.slots, 0, slots * sizeof(uint2), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.bmax, 0, (uint64_t)t->tb.nblk * sizeof(uint64_t), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.blive, 0, (uint64_t)t->tb.nblk * sizeof(uint32_t), s));
+    TR_HIP(t, hipMemsetAsync(&t->st->used, 0, sizeof(uint32_t), s));
+    hipLaunchKernelGGL(k_rehash, dim3(grid_persistent(t->ctx, gbpe_div_up(nold, TPB), 4)), dim3(TPB), 0, s,
+                       (const uint2*)old, nold, t->st, t->tb);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    hipLaunchKernelGGL(k_clear_dirty_all, dim3(gbpe_div_up(t->tb.nblk, 256)), dim3(256), 0, s, t->st, t->tb);
+    // block maxima and the per-workgroup partial maxima the next selection reads
+    if (t->u16)
+        hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
+                           (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr,
+                           FusedSel(), t->part, (uint32_t*)nullptr);
+    else
+        hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
+                           (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr,
+                           FusedSel(), t->part, (uint32_t*)nullptr);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    TR_HIP(t, hipStreamSynchronize(s));
+    hipFree(old);
+    return GBPE_OK;
+}
+
+template <typename S>
+int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delta, uint32_t g_compact,
+                 uint32_t g_refresh, bool timing, hipEvent_t* ev) {
+    S* cur = (S*)t->buf[t->cur ^ (round & 1)];
+    S* oth = (S*)t->buf[t->cur ^ (round & 1) ^ 1];
+    const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
+    if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
+                           (uint32_t*)nullptr, (uint32_t*)nullptr, (DevState*)nullptr, exact ? 1u : 0u);
+    if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
+    // many tiles: TPW tiles per k_delta workgroup (fewer hot-pair flushes)
+    const bool mt = t->delta_mt && g_delta >= t->delta_mt;
+    const uint32_t tpw = t->delta_tpw;
+    const uint32_t g_mt = (uint32_t)gbpe_div_up(g_delta, tpw);
+    // stale-tail blocks (reference compaction): ~2K symbols each of the largest
+    // possible tail (n/2), at most 1024
+    const uint32_t g_mtail = exact ? 0u : (uint32_t)std::min<uint64_t>(1024, gbpe_div_up((uint64_t)t->n / 2 + 1, 2048));
+    // the single-tile k_delta's tail blocks (1024-slot LDS table: ~1K-symbol slices)
+    const uint32_t g_dtail = exact ? 0u : (uint32_t)std::min<uint64_t>(1024, gbpe_div_up((uint64_t)t->n / 2 + 1, 1024));
+    if (exact) {
+        if (mt)
+            hipLaunchKernelGGL(tpw == 32 ? (k_delta_mt<S, true, 32>) : tpw == 16 ? (k_delta_mt<S, true, 16>) : (k_delta_mt<S, true, 8>),
+                               dim3(g_mt + g_mtail), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask,
+                               t->tile_cnt, t->grpsum, g_delta, g_mt);
+        else
+            hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
+                               t->hitmask, t->tile_cnt, t->grpsum, g_delta, 0xFFFFFFFFu);
+        if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
+        hipLaunchKernelGGL((k_compact<S, true>), dim3(g_compact), dim3(CTPB), 0, s, t->st, round, cur, oth,
+                           (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
+    } else {
+        if (mt)
+            hipLaunchKernelGGL(tpw == 32 ? (k_delta_mt<S, false, 32>) : tpw == 16 ? (k_delta_mt<S, false, 16>) : (k_delta_mt<S, false, 8>),
+                               dim3(g_mt + g_mtail), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask,
+                               t->tile_cnt, t->grpsum, g_delta, g_mt);
+        else
+            hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta + g_dtail), dim3(TPB), 0, s, t->st, round, (const S*)cur,
+                               t->tb, t->hitmask, t->tile_cnt, t->grpsum, g_delta, g_delta);
+        if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
+        hipLaunchKernelGGL((k_compact<S, false>), dim3(g_compact), dim3(CTPB), 0, s, t->st, round, cur, oth,
+                           (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb);
+    }
+    if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
+    FusedSel fs;
+    fs.log = nullptr;
+    fs.grpsum = t->grpsum;
+    fs.exact = exact ? 1u : 0u;
+    hipLaunchKernelGGL(k_refresh<S>, dim3(g_refresh), dim3(TPB), 0, s, t->st, round, 1, t->tb, cur,
+                       (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, fs);
+    if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
+    GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+
+// ── sector-sparse loop: launches and re-layouts ──
+
+struct SpGrid {
+    uint32_t body, copy, zdelta, zcompact, refresh;
+    uint32_t wpg = 16;    // bitmap words per k_body workgroup
+    uint32_t ztail = 0;   // stale-tail slice blocks of the multi-tile zone k_delta
+    uint32_t zone1;   // zone workgroups inside k_body: 1 = zone_one, >= 2 = zone_seg segments, 0 = multi-tile passes
+    int bt;       // k_body workgroup size (256 or 1024)
+};
+
+template <typename S>
+uint32_t zone_max(int bt) {
+    return bt == 1023 ? 1024u * 16u : bt == 1024 ? ZoneDim<S, 1024>::ZMAX : ZoneDim<S, 256>::ZMAX;
+}
+// k_body grid: bitmap words per workgroup (>= the measured best 16 / 32 at C2 size),
+// at most `cap` workgroups (GBPE_BODY_WG; default 4 per CU)
+inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* wpg) {
+    const uint32_t W = (uint32_t)gbpe_div_up(t->nsec, 32);
+    const uint32_t minw = bt == 1024 ? 32u : 16u;
+    uint32_t g = (uint32_t)gbpe_div_up(W, minw);
+    if (g > t->body_cap) g = t->body_cap;
+    if (g == 0) g = 1;
+    *wpg = (uint32_t)gbpe_div_up(W, g);
+    if (*wpg == 0) *wpg = 1;
+    *nbody = (uint32_t)gbpe_div_up(W, *wpg);
+    if (*nbody == 0) *nbody = 1;
+}
+
+// launch k_body<S, EXACT, bt> (one instantiation per workgroup size)
+// bt: 256, 1024, or 1023 = 1024 threads with 16 zone symbols each (u16 zones of
+// 8K-16K symbols: half the per-thread zone work of the 32K form; 1 GiB en1g
+// 1.017 -> 0.963 s.  1024 threads x 8 for zones <= 8K instead of 256 x 32 was
+// slower: C2 0.66 vs 0.61 s)
+template <typename S, bool EXACT, typename... A>
+void launch_body(int bt, uint32_t grid, hipStream_t s, A... args) {
+    if (bt == 2048)   // zone segments inside k_body (the ZSEG form, 1024 threads)
+        hipLaunchKernelGGL((k_body<S, EXACT, 1024, 16, true>), dim3(grid), dim3(1024), 0, s, args...);
+    else if (bt == 1023 && sizeof(S) == 2)
+        hipLaunchKernelGGL((k_body<S, EXACT, 1024, 16>), dim3(grid), dim3(1024), 0, s, args...);
+    else if (bt >= 1023)
+        hipLaunchKernelGGL((k_body<S, EXACT, 1024>), dim3(grid), dim3(1024), 0, s, args...);
+    else
+        hipLaunchKernelGGL((k_body<S, EXACT, 256>), dim3(grid), dim3(256), 0, s, args...);
+}
+
+template <typename S>
+int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const SpGrid& g, bool timing, hipEvent_t* ev) {
+    S* zc = (S*)t->zbuf[t->zcur ^ (round & 1)];
+    S* zo = (S*)t->zbuf[t->zcur ^ (round & 1) ^ 1];
+    const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
+    if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
+    if (timing) TR_HIP(t, hipEventRecord(ev[1], s));   // selection runs inside k_body (sel_inline)
+    // zone segments run inside k_body (its ZSEG form)
+    const bool inbody = g.zone1 >= 2;
+    const uint32_t gb = g.body + (g.zone1 ? g.zone1 : g.copy);
+    const uint32_t z1 = g.zone1;   // k_body's own zone workgroups
+    const int bt = inbody ? 2048 : g.bt;
+    // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
+    if (exact)
+        launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
+                             g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
+                             (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
+                             sp_mul(t), (ZSegState*)t->zseg);
+    else
+        launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
+                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
+                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
+                             sp_mul(t), (ZSegState*)t->zseg);
+    if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
+    if (!g.zone1) {
+        // a zone of many tiles (the lexicon loop's first merges): TPW tiles per
+        // workgroup and one flush of their hot pairs, as in the dense loop
+        const bool mt = t->delta_mt && g.zdelta >= t->delta_mt;
+        const uint32_t g_mt = (uint32_t)gbpe_div_up(g.zdelta, 8);
+        if (exact && mt)
+            hipLaunchKernelGGL((k_delta_mt<S, true, 8>), dim3(g_mt), dim3(TPB), 0, s, t->zst, round, (const S*)zc, t->tb,
+                               t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt);
+        else if (mt)
+            hipLaunchKernelGGL((k_delta_mt<S, false, 8>), dim3(g_mt + g.ztail), dim3(TPB), 0, s, t->zst, round,
+                               (const S*)zc, t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt);
+        else if (exact)
+            hipLaunchKernelGGL((k_delta<S, true, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc,
+                               t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, 0xFFFFFFFFu);
+        else   // + stale-tail slice blocks: the zone's tail (<= mc <= zone/5) in ~2K-symbol slices
+            hipLaunchKernelGGL((k_delta<S, false, true>), dim3(g.zdelta + g.ztail), dim3(TPB), 0, s, t->zst, round,
+                               (const S*)zc, t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g.zdelta);
+    }
+    if (!g.zone1) {
+        if (exact)
+            hipLaunchKernelGGL((k_compact<S, true, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
+                               (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
+                               t->tb, (const S*)t->wtmp, (const DevState*)t->st);
+        else
+            hipLaunchKernelGGL((k_compact<S, false, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
+                               (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
+                               t->tb, (const S*)t->wtmp, (const DevState*)t->st);
+    }
+    if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
+    hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,
+                       (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part, t->zseg);
+    if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
+    GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+
+template <typename T>
+int sp_grow(gbpe_trainer* t, T** p, uint64_t* cap, uint64_t need) {
+    if (*p && *cap >= need) return GBPE_OK;
+    hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc((void**)p, need * sizeof(T)) != hipSuccess) {
+        *p = nullptr;
+        return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sparse layout, %llu B) failed",
+                              (unsigned long long)(need * sizeof(T)));
+    }
+    *cap = need;
+    return GBPE_OK;
+}
+
+// sectors over body positions [base, base + len) appended after sector t->nsec
+// (their token bits and signatures too); base is a word start
+template <typename S>
+int sp_add_sectors(gbpe_trainer* t, uint32_t base, uint32_t len) {
+    hipStream_t s = t->ctx->stream;
+    const uint32_t nw = (uint32_t)gbpe_div_up(len, t->sp_secw);
+    if ((uint64_t)t->nsec + nw > t->nsec_cap || (uint64_t)t->nsec + nw > (uint64_t)t->W * 32 ||
+        ((uint64_t)t->nsec + nw) * SP_SIGW > t->sig_cap || nw > t->loc_cap)
+        return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "sector capacity exceeded");
+    const S* body = (const S*)t->buf[t->bcur];
+    hipLaunchKernelGGL(k_sp_sectors<S>, dim3((uint32_t)gbpe_div_up(nw, TPB / 64)), dim3(TPB), 0, s, body, base, len,
+                       t->sp_secw, t->sp_loc, nw);
+    hipLaunchKernelGGL(k_sp_sector_len, dim3((uint32_t)gbpe_div_up(nw, 256)), dim3(256), 0, s, (const uint32_t*)t->sp_loc,
+                       nw, base + len, t->sec + t->nsec);
+    if (t->nsec == 0) {   // a fresh build (sp_enter): whole columns
+        hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(nw, TPB / 64)), dim3(TPB), 0, s, body,
+                           (const uint2*)t->sec, 0u, nw, (uint32_t*)nullptr, t->W, t->sig);
+        hipLaunchKernelGGL(k_sp_colbits<S>, dim3((uint32_t)gbpe_div_up(nw, 32)), dim3(TPB), 0, s, body,
+                           (const uint2*)t->sec, nw, t->bits, t->W);
+    } else {
+        hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(nw, TPB / 64)), dim3(TPB), 0, s, body,
+                           (const uint2*)t->sec, t->nsec, nw, t->bits, t->W, t->sig);
+    }
+    GBPE_LAUNCH_CHECK(t->ctx);
+    t->nsec += nw;
+    t->bend = base + len;
+    return GBPE_OK;
+}
+
+// (re)build the pair signatures (and, with `with_bits`, the token bitmap) from the
+// body sectors: stale entries make the filters looser, never wrong
+template <typename S>
+int sp_filters(gbpe_trainer* t, bool with_bits) {
+    hipStream_t s = t->ctx->stream;
+    hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(t->nsec, TPB / 64)), dim3(TPB), 0, s,
+                       (const S*)sp_body(t), (const uint2*)t->sec, 0u, t->nsec, (uint32_t*)nullptr, t->W, t->sig);
+    if (with_bits) {
+        TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
+        hipLaunchKernelGGL(k_sp_colbits<S>, dim3((uint32_t)gbpe_div_up(t->nsec, 32)), dim3(TPB), 0, s,
+                           (const S*)sp_body(t), (const uint2*)t->sec, t->nsec, t->bits, t->W);
+    }
+    GBPE_LAUNCH_CHECK(t->ctx);
+    t->sp_age = 0;
+    if (with_bits) t->sp_bits_age = 0;
+    return GBPE_OK;
+}
+
+// ── word-lexicon body ──
+
+// bump allocation over the trainer's lexicon scratch
+struct LxCarve {
+    char* base;
+    uint64_t used = 0;
+    template <typename T>
+    T* take(uint64_t n) {
+        const uint64_t b = (used + 255) & ~255ull;
+        used = b + n * sizeof(T);
+        return reinterpret_cast<T*>(base + b);
+    }
+};
+
+int lx_scratch(gbpe_trainer* t, uint64_t bytes) {
+    if (t->lx_tmp && t->lx_tmp_bytes >= bytes) return GBPE_OK;
+    TR_HIP(t, hipStreamSynchronize(t->ctx->stream));
+    hipFree(t->lx_tmp);
+    t->lx_tmp = nullptr;
+    t->lx_tmp_bytes = 0;
+    if (hipMalloc(&t->lx_tmp, bytes) != hipSuccess) {
+        t->lx_tmp = nullptr;
+        return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(lexicon scratch, %llu B) failed", (unsigned long long)bytes);
+    }
+    t->lx_tmp_bytes = bytes;
+    return GBPE_OK;
+}
+
+// exclusive scan of n u32 counts in place (k_chunk_scan1/2); blk gets n/SCAN_BLK + 2
+// entries, the total at blk[nblk]
+inline void lx_scan(hipStream_t s, uint32_t* v, uint64_t n, uint64_t* blk) {
+    const uint64_t nb = gbpe_div_up(n ? n : 1, SCAN_BLK);
+    hipLaunchKernelGGL(k_chunk_scan1, dim3((uint32_t)nb), dim3(SCAN_TPB), 0, s, (const uint32_t*)v, n, v, blk);
+    hipLaunchKernelGGL(k_chunk_scan2, dim3(1), dim3(SCAN_TPB), 0, s, blk, nb, blk + nb);
+}
+
+// What a segment's words would add to the lexicon (nothing is committed yet)
+struct LxPlan {
+    bool ok = false;
+    uint32_t nw = 0, nshort = 0, nlong = 0, nu = 0, T = 0;   // words, distinct short / long, entries, store symbols
+    uint32_t *wpos = nullptr, *usz = nullptr, *umul = nullptr, *urep = nullptr, *occ = nullptr, *upre = nullptr;
+    uint64_t* ublk = nullptr;
+};
+
+// Dedup the words of seg[0, len) (a word starts at 0): word starts, the word
+// table, entries (uids from t->lx_nuid) and the segment's occurrence list, in
+// the scratch.  plan.ok = false when a hash collision or a full word table
+// makes the segment unusable, or (fresh) the store would not be much smaller
+// than the segment.
+template <typename S>
+int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& lp) {
+    hipStream_t s = t->ctx->stream;
+    lp = LxPlan();
+    if (len == 0) return GBPE_OK;
+    const uint64_t ntiles = gbpe_div_up(len, TILE);
+    // word count first (sizes the rest of the scratch)
+    int rc = lx_scratch(t, (ntiles + 64) * 4 + (ntiles / SCAN_BLK + 4) * 8 + 1024);
+    if (rc != GBPE_OK) return rc;
+    {
+        LxCarve c{(char*)t->lx_tmp};
+        uint32_t* tc = c.take<uint32_t>(ntiles);
+        uint64_t* tb = c.take<uint64_t>(ntiles / SCAN_BLK + 4);
+        hipLaunchKernelGGL(k_lx_count<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, tc);
+        lx_scan(s, tc, ntiles, tb);
+        GBPE_LAUNCH_CHECK(t->ctx);
+        uint64_t nw64 = 0;
+        TR_HIP(t, hipMemcpyAsync(&nw64, tb + gbpe_div_up(ntiles, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
+        TR_HIP(t, hipStreamSynchronize(s));
+        lp.nw = (uint32_t)nw64;
+    }
+    const uint32_t nw = lp.nw;
+    uint64_t P = 4096;
+    while (P < 2ull * nw && P < (1ull << 27)) P <<= 1;
+    const uint64_t nbb = gbpe_div_up(P, LX_TB);
+    const uint64_t need = (ntiles + 64) * 4 + (ntiles / SCAN_BLK + 4) * 8 + 9ull * (nw + 64) * 4 + P * 16 +
+                          (nbb + 64) * 4 + 2 * (nbb / SCAN_BLK + (uint64_t)nw / SCAN_BLK + 8) * 8 + 32 * 256;
+    rc = lx_scratch(t, need);
+    if (rc != GBPE_OK) return rc;
+    LxCarve c{(char*)t->lx_tmp};
+    uint32_t* tc = c.take<uint32_t>(ntiles);
+    uint64_t* tb = c.take<uint64_t>(ntiles / SCAN_BLK + 4);
+    lp.wpos = c.take<uint32_t>(nw + 1);
+    uint32_t* otmp = c.take<uint32_t>(nw + 1);
+    uint32_t* longs = c.take<uint32_t>(nw + 1);
+    lp.usz = c.take<uint32_t>(nw + 1);
+    lp.umul = c.take<uint32_t>(nw + 1);
+    lp.urep = c.take<uint32_t>(nw + 1);
+    lp.occ = c.take<uint32_t>(nw + 1);
+    auto* keys = c.take<unsigned long long>(P);
+    auto* vals = c.take<uint2>(P);
+    uint32_t* bc = c.take<uint32_t>(nbb);
+    uint64_t* bb = c.take<uint64_t>(nbb / SCAN_BLK + 4);
+    lp.ublk = c.take<uint64_t>((uint64_t)nw / SCAN_BLK + 4);
+    uint32_t* ctr = c.take<uint32_t>(8);
+    // (the tile counts are recomputed: the scratch may have moved)
+    hipLaunchKernelGGL(k_lx_count<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, tc);
+    lx_scan(s, tc, ntiles, tb);
+    hipLaunchKernelGGL(k_lx_wpos<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, (const uint32_t*)tc,
+                       (const uint64_t*)tb, lp.wpos);
+    TR_HIP(t, hipMemsetAsync(keys, 0, P * 8, s));
+    TR_HIP(t, hipMemsetAsync(vals, 0, P * 8, s));
+    TR_HIP(t, hipMemsetAsync(ctr, 0, 32, s));
+    if (nw)
+        hipLaunchKernelGGL(k_lx_hash<S>, dim3((uint32_t)gbpe_div_up(nw, TPB * LX_WPT)), dim3(TPB), 0, s, seg, len,
+                           (const uint32_t*)lp.wpos, nw, keys, vals, (uint32_t)P, otmp, longs, ctr);
+    hipLaunchKernelGGL(k_lx_tabcount, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const unsigned long long*)keys, (uint32_t)P, bc);
+    lx_scan(s, bc, nbb, bb);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    uint32_t h[4] = {0, 0, 0, 0};
+    uint64_t nshort = 0;
+    TR_HIP(t, hipMemcpyAsync(h, ctr, 8, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipMemcpyAsync(&nshort, bb + gbpe_div_up(nbb, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    if (h[1]) return GBPE_OK;   // word table overflow: not usable
+    lp.nshort = (uint32_t)nshort;
+    lp.nlong = h[0];
+    lp.nu = lp.nshort + lp.nlong;
+    if ((uint64_t)t->lx_nuid + lp.nu >= LX_LONG) return GBPE_OK;
+    hipLaunchKernelGGL(k_lx_tabuid, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const unsigned long long*)keys, vals, (uint32_t)P,
+                       (const uint32_t*)bc, (const uint64_t*)bb, (const uint32_t*)lp.wpos, nw, len, lp.usz, lp.umul, lp.urep);
+    if (lp.nlong)
+        hipLaunchKernelGGL(k_lx_longs, dim3((uint32_t)gbpe_div_up(lp.nlong, 256)), dim3(256), 0, s, (const uint32_t*)longs,
+                           (const uint32_t*)ctr, lp.nshort, (const uint32_t*)lp.wpos, nw, len, lp.usz, lp.umul, lp.urep);
+    if (nw)
+        hipLaunchKernelGGL(k_lx_occ<S>, dim3((uint32_t)gbpe_div_up(nw, 256)), dim3(256), 0, s, seg, (const uint32_t*)lp.wpos, nw,
+                           len, (const uint32_t*)otmp, (const unsigned long long*)keys, (const uint2*)vals, (uint32_t)P,
+                           (const uint32_t*)lp.urep, (const uint32_t*)lp.usz, lp.nshort, t->lx_nuid, lp.occ, ctr);
+    // store offsets: exclusive scan of the entry sizes, in otmp (k_lx_occ, queued
+    // before on the same stream, has consumed it)
+    uint32_t* upre = otmp;
+    TR_HIP(t, hipMemcpyAsync(upre, lp.usz, (uint64_t)lp.nu * 4, hipMemcpyDeviceToDevice, s));
+    lx_scan(s, upre, lp.nu, lp.ublk);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    uint64_t T = 0;
+    TR_HIP(t, hipMemcpyAsync(&T, lp.ublk + gbpe_div_up(lp.nu ? lp.nu : 1, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipMemcpyAsync(h, ctr, 8, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    if (h[1]) return GBPE_OK;   // a hash collision (or a word missing from the table)
+    lp.T = (uint32_t)T;
+    if (fresh && T * 2 > len) return GBPE_OK;   // not worth it: the store would be more than half the body
+    lp.upre = upre;
+    lp.ok = true;
+    return GBPE_OK;
+}
+
+// Append a planned segment to the lexicon: store entries (window-aligned), their
+// sector windows after t->nsec with token bits and signatures, occurrences after
+// t->lx_nocc.  plan.ok = false (nothing changed) when the capacities cannot take it.
+template <typename S>
+int lx_commit(gbpe_trainer* t, LxPlan& lp, const S* seg, bool fresh) {
+    hipStream_t s = t->ctx->stream;
+    const uint32_t SEC = t->sp_secw;
+    const uint64_t sbase = gbpe_div_up(t->lx_len, SEC) * SEC;
+    const uint64_t nwin = gbpe_div_up(lp.T ? lp.T : 1, SEC);
+    const uint64_t kb = sbase / SEC;
+    if (sbase + nwin * SEC > t->lx_cap || kb + nwin > t->nsec_cap || kb + nwin > (uint64_t)t->W * 32 ||
+        (kb + nwin) * SP_SIGW > t->sig_cap || nwin > t->loc_cap || t->lx_nocc + lp.nw > t->lx_occ_cap) {
+        lp.ok = false;
+        return GBPE_OK;
+    }
+    S* store = (S*)t->lx_store;
+    if (sbase > t->lx_len) {   // alignment padding: separators no sector covers
+        TR_HIP(t, hipMemsetAsync(store + t->lx_len, 0, (sbase - t->lx_len) * sizeof(S), s));
+        TR_HIP(t, hipMemsetAsync(t->lx_mul + t->lx_len, 0, (sbase - t->lx_len) * 4, s));
+    }
+    const uint32_t* upre = lp.upre;
+    if (lp.nu) {
+        hipLaunchKernelGGL(k_lx_fill<S>, dim3((uint32_t)gbpe_div_up(lp.nu, 256)), dim3(256), 0, s, seg,
+                           (const uint32_t*)lp.urep, (const uint32_t*)lp.usz, (const uint32_t*)lp.umul, upre,
+                           (const uint64_t*)lp.ublk, lp.nu, store + sbase, t->lx_mul + sbase);
+        TR_HIP(t, hipMemsetAsync(t->sp_loc, 0xFF, nwin * 4, s));
+        hipLaunchKernelGGL(k_lx_secstart, dim3((uint32_t)gbpe_div_up(lp.nu, 256)), dim3(256), 0, s, upre,
+                           (const uint64_t*)lp.ublk, lp.nu, SEC, (uint32_t)sbase, t->lx_nuid, t->sp_loc, t->lx_w0 + kb);
+        hipLaunchKernelGGL(k_sp_sector_len, dim3((uint32_t)gbpe_div_up(nwin, 256)), dim3(256), 0, s,
+                           (const uint32_t*)t->sp_loc, (uint32_t)nwin, (uint32_t)(sbase + lp.T), t->sec + kb);
+    } else {
+        TR_HIP(t, hipMemsetAsync(t->sec + kb, 0, nwin * sizeof(uint2), s));
+    }
+    if (lp.nw)
+        TR_HIP(t, hipMemcpyAsync(t->lx_occ + t->lx_nocc, lp.occ, (uint64_t)lp.nw * 4, hipMemcpyDeviceToDevice, s));
+    // token bits and signatures of the new sectors (a fresh build: whole columns)
+    hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(nwin, TPB / 64)), dim3(TPB), 0, s, (const S*)store,
+                       (const uint2*)t->sec, (uint32_t)kb, (uint32_t)nwin, fresh ? (uint32_t*)nullptr : t->bits, t->W, t->sig);
+    if (fresh)
+        hipLaunchKernelGGL(k_sp_colbits<S>, dim3((uint32_t)gbpe_div_up(nwin, 32)), dim3(TPB), 0, s, (const S*)store,
+                           (const uint2*)t->sec, (uint32_t)nwin, t->bits, t->W);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    t->nsec = (uint32_t)(kb + nwin);
+    t->lx_len = sbase + lp.T;
+    t->lx_nocc += lp.nw;
+    t->lx_nuid += lp.nu;
+    t->lx_words += lp.nw;
+    return GBPE_OK;
+}
+
+// lexicon → dense stream: every body word occurrence's current symbols, in
+// stream order, to dst[0, B); returns the symbol total through *tot
+template <typename S>
+int lx_expand(gbpe_trainer* t, S* dst, uint64_t* tot) {
+    hipStream_t s = t->ctx->stream;
+    const uint64_t nu = t->lx_nuid, no = t->lx_nocc;
+    int rc = lx_scratch(t, (2 * nu + no + 64) * 4 + (no / SCAN_BLK + 8) * 8 + 4096);
+    if (rc != GBPE_OK) return rc;
+    LxCarve c{(char*)t->lx_tmp};
+    uint32_t* coff = c.take<uint32_t>(nu + 1);
+    uint32_t* clen = c.take<uint32_t>(nu + 1);
+    uint32_t* olen = c.take<uint32_t>(no + 1);
+    uint64_t* oblk = c.take<uint64_t>(no / SCAN_BLK + 4);
+    if (t->nsec)
+        hipLaunchKernelGGL(k_lx_wordpos<S>, dim3((uint32_t)gbpe_div_up(t->nsec, TPB / 64)), dim3(TPB), 0, s,
+                           (const S*)t->lx_store, (const uint2*)t->sec, t->nsec, (const uint32_t*)t->lx_w0, coff, clen);
+    if (no)
+        hipLaunchKernelGGL(k_lx_olen, dim3((uint32_t)gbpe_div_up(no, 256)), dim3(256), 0, s, (const uint32_t*)t->lx_occ, no,
+                           (const uint32_t*)clen, olen);
+    lx_scan(s, olen, no, oblk);
+    if (no)
+        hipLaunchKernelGGL(k_lx_expand<S>, dim3((uint32_t)gbpe_div_up(no, 256)), dim3(256), 0, s, (const uint32_t*)t->lx_occ,
+                           no, (const uint32_t*)coff, (const uint32_t*)clen, (const S*)t->lx_store, (const uint32_t*)olen,
+                           (const uint64_t*)oblk, dst);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    TR_HIP(t, hipMemcpyAsync(tot, oblk + gbpe_div_up(no ? no : 1, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
+    return GBPE_OK;
+}
+
+// dense → sparse at a step boundary.  The zone is the stream from the last word
+// start at or before n - zt (zt = max(sp_zt * next_mc, 2 next_mc + last_mc) + 64:
+// >= 5 x the next merge's count while counts fall, and room for the stale window
+// the last merge left (sel_inline's zone rule); a merge that would not fit is not
+// run and the host goes dense, sp_abort); the dense stale buffer's tail becomes the
+// zone's stale buffer.  next_mc = 0: the last merge's count stands in for it.
+template <typename S>
+int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
+    hipStream_t s = t->ctx->stream;
+    const uint32_t n = t->n;
+    const uint64_t prev_mc = t->last_mc;   // the previous stream is n + prev_mc long
+    const uint64_t nmc = next_mc ? next_mc : prev_mc;
+    const uint64_t zt = std::max<uint64_t>((uint64_t)t->sp_zt * nmc, 2ull * nmc + prev_mc) + 64;
+    const S* cur = (const S*)t->buf[t->cur];
+    const S* stale = (const S*)t->buf[t->cur ^ 1];
+    if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
+    uint32_t Zs = n;   // sharded ranks before the last: all body, no zone
+    if (with_zone) {
+        if (zt + 2 >= n) return GBPE_OK;
+        hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, cur, (uint32_t)(n - zt), t->d_u32);
+        GBPE_LAUNCH_CHECK(t->ctx);
+        TR_HIP(t, hipMemcpyAsync(&Zs, t->d_u32, 4, hipMemcpyDeviceToHost, s));
+        TR_HIP(t, hipStreamSynchronize(s));
+        if (Zs < t->sp_secw) return GBPE_OK;   // the whole stream is one long word (or tiny): stay dense
+    }
+    const uint32_t z = n - Zs;
+    // word lexicon: plan the deduplicated body first; it sizes the sectors
+    t->lex = false;
+    t->lx_len = t->lx_nocc = 0;
+    t->lx_nuid = 0;
+    LxPlan lp;
+    if (t->lex_on && Zs) {
+        int rc0 = lx_analyze<S>(t, cur, Zs, true, lp);
+        if (rc0 != GBPE_OK) return rc0;
+        if (lp.ok) ++t->lx_builds;
+        else ++t->lx_fallbacks;
+    }
+    // capacities for every sector the body can ever hold: windows over [0, n) (the
+    // lexicon: over its store, and twice the zone for the words shrinks append) plus
+    // one partial window per zone shrink (at most SP_SHRINKS per entry)
+    const uint64_t cap = lp.ok ? gbpe_div_up((uint64_t)lp.T + 2ull * z, t->sp_secw) + 2 * (SP_SHRINKS + 1)
+                               : gbpe_div_up(n, t->sp_secw) + SP_SHRINKS + 1;
+    int rc = sp_grow(t, &t->sec, &t->nsec_cap, cap);
+    if (rc == GBPE_OK && (!t->sp_loc || t->loc_cap < cap)) {
+        hipFree(t->sp_loc);
+        hipFree(t->sp_blk);
+        t->sp_loc = nullptr;
+        t->sp_blk = nullptr;
+        t->loc_cap = 0;
+        if (hipMalloc(&t->sp_loc, cap * 4) != hipSuccess ||
+            hipMalloc(&t->sp_blk, (gbpe_div_up(cap, SCAN_BLK) + 1) * 8) != hipSuccess)
+            rc = gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sector scratch) failed");
+        else
+            t->loc_cap = cap;
+    }
+    if (rc != GBPE_OK) return rc;
+    t->W = (uint32_t)gbpe_div_up(cap, 32);
+    rc = sp_grow(t, &t->bits, &t->bits_cap, (uint64_t)t->max_id * t->W);
+    if (rc == GBPE_OK) rc = sp_grow(t, &t->sig, &t->sig_cap, cap * SP_SIGW);
+    if (rc != GBPE_OK) return rc;
+    t->bcur = t->cur;
+    t->nsec = 0;
+    TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
+    TR_HIP(t, hipMemsetAsync(t->sig, 0, cap * SP_SIGW * 4, s));
+    if (lp.ok) {
+        const uint64_t scap = cap * t->sp_secw, ocap = (uint64_t)lp.nw + z + 1;
+        if (!t->lx_store || t->lx_cap < scap) {
+            hipFree(t->lx_store);
+            hipFree(t->lx_mul);
+            hipFree(t->lx_w0);
+            t->lx_store = nullptr;
+            t->lx_mul = t->lx_w0 = nullptr;
+            t->lx_cap = 0;
+            if (hipMalloc(&t->lx_store, scap * t->bps) != hipSuccess || hipMalloc(&t->lx_mul, scap * 4) != hipSuccess ||
+                hipMalloc(&t->lx_w0, cap * 4) != hipSuccess)
+                return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(word lexicon) failed");
+            t->lx_cap = scap;
+        }
+        rc = sp_grow(t, &t->lx_occ, &t->lx_occ_cap, ocap);
+        if (rc != GBPE_OK) return rc;
+        t->lex = true;
+        rc = lx_commit<S>(t, lp, cur, true);
+        if (rc == GBPE_OK && !lp.ok) rc = gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "word lexicon capacity");
+        if (rc == GBPE_OK && getenv("GBPE_LEX_CHECK")) {   // diagnostic: the lexicon expands back to the body
+            S* chk = nullptr;
+            TR_HIP(t, hipMalloc(&chk, ((uint64_t)Zs + 64) * sizeof(S)));
+            uint64_t tot = 0;
+            rc = lx_expand<S>(t, chk, &tot);
+            std::vector<S> a(Zs), b(Zs);
+            TR_HIP(t, hipStreamSynchronize(s));
+            TR_HIP(t, hipMemcpy(a.data(), chk, (uint64_t)Zs * sizeof(S), hipMemcpyDeviceToHost));
+            TR_HIP(t, hipMemcpy(b.data(), cur, (uint64_t)Zs * sizeof(S), hipMemcpyDeviceToHost));
+            hipFree(chk);
+            uint64_t bad = Zs;
+            for (uint64_t i = 0; i < Zs; ++i)
+                if (a[i] != b[i]) {
+                    bad = i;
+                    break;
+                }
+            std::vector<uint32_t> mm(lp.T);
+            std::vector<S> ss(lp.T);
+            TR_HIP(t, hipMemcpy(mm.data(), t->lx_mul, (uint64_t)lp.T * 4, hipMemcpyDeviceToHost));
+            TR_HIP(t, hipMemcpy(ss.data(), t->lx_store, (uint64_t)lp.T * sizeof(S), hipMemcpyDeviceToHost));
+            uint64_t wsum = 0, nz = 0, badm = 0;
+            for (uint32_t i = 0; i < lp.T; ++i) {
+                wsum += mm[i];
+                if ((ss[i] == 0) != (mm[i] == 0)) ++badm;
+            }
+            for (uint32_t i = 0; i < Zs; ++i) nz += (b[i] & Sym<S>::TM) ? 1 : 0;
+            fprintf(stderr, "[lex-check] Zs=%u words=%u distinct=%u+%u store=%u expanded=%llu first_diff=%llu "
+                    "mult_sum=%llu nonzero_body=%llu sep_mismatch=%llu\n", Zs, lp.nw,
+                    lp.nshort, lp.nlong, lp.T, (unsigned long long)tot, (unsigned long long)bad,
+                    (unsigned long long)wsum, (unsigned long long)nz, (unsigned long long)badm);
+        }
+    } else {
+        rc = sp_add_sectors<S>(t, 0u, Zs);
+    }
+    if (rc != GBPE_OK) return rc;
+    t->sp_age = 0;
+    t->sp_bits_age = 0;
+    t->sp_shrinks = 0;
+    // zone buffers: the zone, and the stale source (previous stream, n_prev - Zs <= z + last_mc symbols)
+    // (>= the one-workgroup zone pass's full register window, which it loads unconditionally)
+    uint64_t zneed = (gbpe_div_up((uint64_t)z + prev_mc + 1, TILE) + 2) * TILE;
+    const uint64_t zmin = (uint64_t)(t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024)) + TILE;
+    if (zneed < zmin) zneed = zmin;
+    if (zneed > t->zcap) {
+        for (int k = 0; k < 2; ++k) {
+            hipFree(t->zbuf[k]);
+            t->zbuf[k] = nullptr;
+        }
+        hipFree(t->wtmp);
+        t->wtmp = nullptr;
+        t->zcap = 0;
+        if (hipMalloc(&t->zbuf[0], zneed * t->bps) != hipSuccess || hipMalloc(&t->zbuf[1], zneed * t->bps) != hipSuccess ||
+            hipMalloc(&t->wtmp, zneed * t->bps) != hipSuccess)
+            return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(zone) failed");
+        t->zcap = zneed;
+    }
+    for (int k = 0; k < 2; ++k) TR_HIP(t, hipMemsetAsync(t->zbuf[k], 0, t->zcap * t->bps, s));
+    if (z) {
+        TR_HIP(t, hipMemcpyAsync(t->zbuf[0], cur + Zs, (uint64_t)z * t->bps, hipMemcpyDeviceToDevice, s));
+        uint64_t sl = (uint64_t)z + prev_mc;
+        if (Zs + sl > t->cap_syms) sl = t->cap_syms - Zs;
+        if (sl > t->zcap) sl = t->zcap;
+        TR_HIP(t, hipMemcpyAsync(t->zbuf[1], stale + Zs, sl * t->bps, hipMemcpyDeviceToDevice, s));
+    }
+    // states
+    if (!t->zst) {
+        TR_HIP(t, hipMalloc(&t->zst, sizeof(DevState)));
+        TR_HIP(t, hipHostMalloc((void**)&t->h_zst, sizeof(DevState), hipHostMallocDefault));
+    }
+    memset(t->h_zst, 0, sizeof(DevState));
+    t->h_zst->n = z;
+    TR_HIP(t, hipMemcpyAsync(t->zst, t->h_zst, sizeof(DevState), hipMemcpyHostToDevice, s));
+    t->h_st->B = Zs;
+    t->h_st->Bp = Zs;
+    t->h_st->body_rm = 0;
+    t->h_st->sp_abort = 0;
+    TR_HIP(t, hipMemcpyAsync(&t->st->B, &t->h_st->B, 4 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    // every rank checks the zone against the same length: the zone rank's target
+    // until the first exchange reports the real one (single GPU: the real one)
+    t->h_st->zlast = t->sharded ? (uint32_t)zt : z;
+    t->h_st->is_last = z ? 1u : 0u;
+    TR_HIP(t, hipMemcpyAsync(&t->st->zlast, &t->h_st->zlast, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(&t->st->is_last, &t->h_st->is_last, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    {   // one byte counter per k_body workgroup, kept across entries (summed by gbpe_trainer_stats_get)
+        const uint64_t need = gbpe_div_up(gbpe_div_up(cap, 32), SP_WPW_MIN) + 2;
+        if (need > t->wg_cap) {
+            uint64_t* nb = nullptr;
+            TR_HIP(t, hipMalloc(&nb, need * sizeof(uint64_t)));
+            TR_HIP(t, hipMemsetAsync(nb, 0, need * sizeof(uint64_t), s));
+            if (t->wg_bytes) TR_HIP(t, hipMemcpyAsync(nb, t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+            TR_HIP(t, hipStreamSynchronize(s));
+            hipFree(t->wg_bytes);
+            t->wg_bytes = nb;
+            t->wg_cap = need;
+        }
+    }
+    // the zone rule's last count (sel_inline): the count of the merge before entry
+    TR_HIP(t, hipMemcpyAsync(&t->st->mc_prev, &t->st->mc, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    // per-k_refresh-workgroup maxima the sparse merges select from (sel_inline)
+    if (!t->part) TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
+    if (!t->zseg && !t->sharded) {
+        TR_HIP(t, hipMalloc(&t->zseg, sizeof(ZSegState)));
+        TR_HIP(t, hipMemsetAsync(t->zseg, 0, sizeof(ZSegState), t->ctx->stream));
+    }
+    hipLaunchKernelGGL(k_refresh<S>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
+                       (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    TR_HIP(t, hipStreamSynchronize(s));
+    t->sp = true;
+    t->zcur = 0;
+    if (t->last_mc < nmc) t->last_mc = (uint32_t)nmc;   // the zone-shrink target's count until a merge runs
+    ++t->sp_enters;
+    t->sp_sectors = t->nsec;
+    t->sp_zone = z;
+    return GBPE_OK;
+}
+
+// Zone shrink at a step boundary: the zone keeps >= zt = sp_zt * last_mc + 64
+// symbols (from a word start); its front moves into the body as new sectors and
+// both zone buffers shift down by the moved length (B and Bp with them, so the
+// stale buffer keeps its global coordinates).
+template <typename S>
+int sp_shrink(gbpe_trainer* t) {
+    hipStream_t s = t->ctx->stream;
+    DevState* hs = t->h_st;
+    const uint32_t z = t->n - hs->B;
+    const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
+    if (t->sp_shrinks >= SP_SHRINKS || (uint64_t)z < zt * t->shrink_pct / 100 + 4096) return GBPE_OK;
+    S* zc = (S*)t->zbuf[t->zcur];
+    S* zo = (S*)t->zbuf[t->zcur ^ 1];
+    hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, (const S*)zc, (uint32_t)(z - zt), t->d_u32);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    uint32_t L = 0;
+    TR_HIP(t, hipMemcpyAsync(&L, t->d_u32, 4, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    if (L < 4096) return GBPE_OK;
+    if (t->lex) {   // the front's words join the lexicon (deduplicated among themselves)
+        LxPlan lp;
+        int rc = lx_analyze<S>(t, (const S*)zc, L, false, lp);
+        if (rc == GBPE_OK && lp.ok) rc = lx_commit<S>(t, lp, (const S*)zc, false);
+        if (rc != GBPE_OK) return rc;
+        if (!lp.ok) return GBPE_OK;   // (a collision or no room): the zone keeps its front this time
+    } else {
+        if ((uint64_t)t->bend + L > t->cap_syms) return GBPE_OK;
+        S* body = (S*)t->buf[t->bcur];
+        TR_HIP(t, hipMemcpyAsync(body + t->bend, zc, (uint64_t)L * t->bps, hipMemcpyDeviceToDevice, s));
+        int rc = sp_add_sectors<S>(t, t->bend, L);
+        if (rc != GBPE_OK) return rc;
+    }
+    const uint64_t rest = t->zcap - L;
+    TR_HIP(t, hipMemcpyAsync(t->wtmp, zc + L, rest * t->bps, hipMemcpyDeviceToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(zc, t->wtmp, rest * t->bps, hipMemcpyDeviceToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(t->wtmp, zo + L, rest * t->bps, hipMemcpyDeviceToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(zo, t->wtmp, rest * t->bps, hipMemcpyDeviceToDevice, s));
+    TR_HIP(t, hipMemsetAsync(zc + rest, 0, (uint64_t)L * t->bps, s));
+    TR_HIP(t, hipMemsetAsync(zo + rest, 0, (uint64_t)L * t->bps, s));
+    hs->B += L;
+    hs->Bp += L;
+    t->h_zst->n = z - L;
+    TR_HIP(t, hipMemcpyAsync(&t->st->B, &hs->B, 2 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(&t->zst->n, &t->h_zst->n, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    ++t->sp_shrinks;
+    return GBPE_OK;
+}
+
+// sparse → dense: the body sectors gathered in order into the other dense
+// buffer, the zone appended; the old body buffer becomes the stale buffer, with
+// the zone's stale buffer at its global place (positions >= Bp: the only ones the
+// next merge's stale window can read).
+template <typename S>
+int sp_exit(gbpe_trainer* t) {
+    hipStream_t s = t->ctx->stream;
+    DevState* hs = t->h_st;
+    TR_HIP(t, hipMemcpyAsync(hs, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    const uint32_t B = hs->B, Bp = hs->Bp, n = hs->n;
+    const uint32_t z = n - B;
+    S* body = (S*)t->buf[t->bcur];
+    S* dst = (S*)t->buf[t->bcur ^ 1];
+    const uint32_t nsec = t->nsec;
+    uint64_t btot = 0;
+    if (t->lex) {
+        int rc = lx_expand<S>(t, dst, &btot);
+        if (rc != GBPE_OK) return rc;
+    } else {
+        hipLaunchKernelGGL(k_sp_counts, dim3((uint32_t)gbpe_div_up(nsec, 256)), dim3(256), 0, s, (const uint2*)t->sec, nsec,
+                           t->sp_loc);
+        const uint64_t nblk = gbpe_div_up(nsec, SCAN_BLK);
+        hipLaunchKernelGGL(k_chunk_scan1, dim3((uint32_t)nblk), dim3(SCAN_TPB), 0, s, (const uint32_t*)t->sp_loc,
+                           (uint64_t)nsec, t->sp_loc, t->sp_blk);
+        hipLaunchKernelGGL(k_chunk_scan2, dim3(1), dim3(SCAN_TPB), 0, s, t->sp_blk, nblk, t->sp_blk + nblk);
+        hipLaunchKernelGGL(k_sp_gather<S>, dim3((uint32_t)gbpe_div_up(nsec, TPB / 64)), dim3(TPB), 0, s, (const S*)body,
+                           (const uint2*)t->sec, nsec, (const uint32_t*)t->sp_loc, (const uint64_t*)t->sp_blk, dst);
+        GBPE_LAUNCH_CHECK(t->ctx);
+        TR_HIP(t, hipMemcpyAsync(&btot, t->sp_blk + nblk, 8, hipMemcpyDeviceToHost, s));
+    }
+    TR_HIP(t, hipMemcpyAsync(dst + B, t->zbuf[t->zcur], (uint64_t)z * t->bps, hipMemcpyDeviceToDevice, s));
+    // zero the rest of the dense buffer's padding the kernels may read (halo / look-ahead)
+    TR_HIP(t, hipMemsetAsync(dst + n, 0, (t->cap_syms - n) * t->bps, s));
+    uint64_t sl = t->zcap;
+    if (Bp + sl > t->cap_syms) sl = t->cap_syms - Bp;
+    TR_HIP(t, hipMemcpyAsync(body + Bp, t->zbuf[t->zcur ^ 1], sl * t->bps, hipMemcpyDeviceToDevice, s));
+    hs->sp_abort = 0;
+    TR_HIP(t, hipMemcpyAsync(&t->st->sp_abort, &hs->sp_abort, 4, hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    if (btot != B) return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "sparse exit: body sectors hold %llu symbols, expected %u",
+                                         (unsigned long long)btot, B);
+    t->cur = t->bcur ^ 1;
+    t->sp = false;
+    t->lex = false;
+    ++t->sp_exits;
+    return GBPE_OK;
+}
+
+int sp_exit_any(gbpe_trainer* t) { return !t->sp ? GBPE_OK : (t->u16 ? sp_exit<uint16_t>(t) : sp_exit<uint32_t>(t)); }
+
+}  // namespace
+
+// a trainer continuing from an exported state (gbpe_trainer_create_from_state):
+// `bytes` is then the current u32 stream, `prev` the previous one
+struct StateInit {
+    const uint32_t* prev;
+    uint64_t n_prev;
+};
+// the trainer constructor behind gbpe_trainer_create / _create_from_state / gbpe_shard_create
+int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
+                        int input_on_device, const gbpe_train_opts* opts, uint64_t cap_extra, gbpe_trainer** out,
+                        const StateInit* si = nullptr);
