@@ -1,7 +1,7 @@
 """numpy model of one rank of the sharded trainer — TEST INFRASTRUCTURE ONLY.
 
 Implements the backend interface of ``gpubpe.sharded.ShardedTrainer`` with
-plain numpy, record for record what csrc/train.hip's gbpe_shard_* kernels
+plain numpy, record for record what csrc/train_shard.hip's gbpe_shard_* kernels
 write, so the orchestration and the exchange protocol (window cut, owner
 rank, offsets, stall/undo) are tested over gloo on CPU against the
 single-stream oracle (oracle/bpe_oracle.py, the reference semantics).

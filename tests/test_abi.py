@@ -140,10 +140,10 @@ def test_model_json_round_trip():
 def test_shard_record_layout_matches_host_loop(lib):
     # the exchange record the native step loop (gbpe_shard_step_comm) all-gathers
     # is the one the Python host loop and the numpy rank model read: same header
-    # word positions (csrc/train.hip's enum vs gpubpe/sharded.py) and size
+    # word positions (csrc/train_dev.h enum vs gpubpe/sharded.py) and size
     import re
     from gpubpe import sharded
-    src = open(os.path.join(ROOT, "gpu-bpe_amd", "csrc", "train.hip")).read()
+    src = open(os.path.join(ROOT, "gpu-bpe_amd", "csrc", "train_dev.h")).read()
     body = re.search(r"enum : uint32_t \{\s*(H_ACTIVE = 0[^}]*)\}", src).group(1)
     body = re.sub(r"//[^\n]*", "", body)
     idx, names = 0, {}
