@@ -137,11 +137,14 @@ __device__ uint32_t lx_find(const unsigned long long* __restrict__ keys, uint32_
 // (hot words cost one global add per workgroup, not one per occurrence), then
 // adds them into the global table.  Token-0 words become literals, long words
 // entries of their own.  ctr[0] = long words, ctr[1] = failure flag.
+// wmul (weighted analysis, the lexicon hand-over of DESIGN §5): a word counts
+// wmul[its first position] occurrences instead of one — the segment is then a
+// concatenation of word stores, each word carrying its multiplicity.
 template <typename S>
 __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32_t len, const uint32_t* __restrict__ wpos,
                                                  uint32_t nw, unsigned long long* __restrict__ keys, uint2* __restrict__ vals,
                                                  uint32_t P, uint32_t* __restrict__ otmp, uint32_t* __restrict__ longs,
-                                                 uint32_t* __restrict__ ctr) {
+                                                 uint32_t* __restrict__ ctr, const uint32_t* __restrict__ wmul = nullptr) {
     __shared__ unsigned long long lk[LX_LT];
     __shared__ uint32_t lc[LX_LT], lr[LX_LT];
     for (int i = threadIdx.x; i < LX_LT; i += TPB) {
@@ -166,6 +169,7 @@ __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32
             continue;
         }
         otmp[j] = 0u;
+        const uint32_t wt = wmul ? wmul[s] : 1u;
         const unsigned long long h = lx_hash<S>(x, s, L);
         uint32_t slot = lx_home(h, LX_LT - 1);
         bool done = false;
@@ -173,14 +177,14 @@ __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32
             const unsigned long long o = atomicCAS(&lk[slot], 0ull, h);
             if (o == 0ull) {
                 lr[slot] = (uint32_t)j;
-                atomicAdd(&lc[slot], 1u);
+                atomicAdd(&lc[slot], wt);
                 done = true;
             } else if (o == h) {
-                atomicAdd(&lc[slot], 1u);
+                atomicAdd(&lc[slot], wt);
                 done = true;
             }
         }
-        if (!done && !lx_insert(keys, vals, P, h, (uint32_t)j, 1u)) ctr[1] = 1u;
+        if (!done && !lx_insert(keys, vals, P, h, (uint32_t)j, wt)) ctr[1] = 1u;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < LX_LT; i += TPB)
@@ -248,12 +252,13 @@ __global__ __launch_bounds__(TPB) void k_lx_tabuid(const unsigned long long* __r
 // long words: an entry each (uids after the deduplicated ones)
 __global__ void k_lx_longs(const uint32_t* __restrict__ longs, const uint32_t* __restrict__ ctr, uint32_t nshort,
                            const uint32_t* __restrict__ wpos, uint32_t nw, uint32_t len, uint32_t* __restrict__ usz,
-                           uint32_t* __restrict__ umul, uint32_t* __restrict__ urep) {
+                           uint32_t* __restrict__ umul, uint32_t* __restrict__ urep,
+                           const uint32_t* __restrict__ wmul = nullptr) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= ctr[0]) return;
     const uint32_t j = longs[i];
     usz[nshort + i] = lx_wlen(wpos, nw, len, j) + 1u;
-    umul[nshort + i] = 1u;
+    umul[nshort + i] = wmul ? wmul[wpos[j]] : 1u;
     urep[nshort + i] = wpos[j];
 }
 

@@ -46,44 +46,8 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     if (n >= 0xFFFFFFF0ull) return gbpe_set_error(ctx, GBPE_E_INVALID, "corpus too large for one device (%llu symbols)", (unsigned long long)n);
     auto* t = new (std::nothrow) gbpe_trainer();
     if (!t) return gbpe_set_error(ctx, GBPE_E_OOM, "host allocation failed");
-    t->ctx = ctx;
-    t->flags = opts->flags;
-    t->batch = opts->batch_size ? opts->batch_size : GBPE_BATCH_SIZE;
-    const uint32_t vocab_size = opts->vocab_size ? opts->vocab_size : 256u;
-    const uint32_t next_id = opts->next_token_id ? opts->next_token_id : 256u;
-    t->needed = opts->target_vocab_size > vocab_size ? opts->target_vocab_size - vocab_size : 0u;
-    // u16 symbols when every id the run can produce fits in 15 bits
-    const uint64_t max_id = (uint64_t)next_id + t->needed;    // exclusive
-    t->u16 = max_id <= 0x8000ull;
-    t->max_id = (uint32_t)(max_id < 0x10000ull ? max_id : 0x10000ull);
-    if (const char* e = getenv("GBPE_SPARSE_DIV")) t->sp_div = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_REFRESH_BLOCKS")) t->refresh_blocks = (uint32_t)atoi(e);
-    if (const char* e = getenv("GBPE_REHASH")) t->rehash_on = atoi(e) != 0;
-    t->body_cap = (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
-    if (const char* e = getenv("GBPE_BODY_WG")) t->body_cap = std::max<uint32_t>(1, (uint32_t)atoi(e));
-    if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_LEXICON")) t->lex_on = atoi(e) != 0;
-    if (const char* e = getenv("GBPE_TAIL")) t->tail_on = atoi(e) != 0;
-    if (const char* e = getenv("GBPE_ZONE16")) t->zone16 = atoi(e) != 0;
-    if (const char* e = getenv("GBPE_TAIL_MC")) t->tail_mc = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_LEXICON_DIV")) t->lx_div = std::max<uint32_t>(8, (uint32_t)strtoul(e, nullptr, 10));
-    if (const char* e = getenv("GBPE_SUBSTEP_ZONE")) t->sub_zone = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_SUBSTEP")) t->sub_k = std::max<uint32_t>(2, (uint32_t)strtoul(e, nullptr, 10)) & ~1u;
-    if (const char* e = getenv("GBPE_DELTA_MT")) t->delta_mt = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_DELTA_TPW")) {
-        const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
-        t->delta_tpw = v >= 32 ? 32 : v >= 16 ? 16 : 8;
-    }
-    if (const char* e = getenv("GBPE_SHRINK_PCT")) t->shrink_pct = std::max<uint32_t>(110, (uint32_t)strtoul(e, nullptr, 10));
-    if (const char* e = getenv("GBPE_ZONE_SEG")) t->zseg_mode = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_ZONE_F")) t->zone_f = std::max<uint32_t>(3, (uint32_t)strtoul(e, nullptr, 10));
-    if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
-    if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
-        t->trace = fopen(e, "w");
-        if (t->trace && (hipMalloc(&t->d_clog, (size_t)t->batch * 8) != hipSuccess ||
-                         hipHostMalloc((void**)&t->h_clog, (size_t)t->batch * 8, hipHostMallocDefault) != hipSuccess))
-            t->d_clog = nullptr, t->h_clog = nullptr;   // trace without candidate counts
-    }
+    trainer_config(t, ctx, opts);
+    const uint32_t next_id = t->next_id0;
     t->bps = t->u16 ? 2 : 4;
     t->n0 = n;
     t->n = (uint32_t)n;
@@ -331,7 +295,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     // would still launch its full-grid kernels as no-ops)
     if (!t->sp && t->h_st->enter_lim && t->n >= (1u << 24)) k = 1;
     // a large zone shrinks every sub_k merges instead of every step (early counts fall fast)
-    if (t->sp && t->n - t->h_st->B > t->sub_zone && k > t->sub_k) k = t->sub_k;
+    if (t->sp && (uint32_t)t->n - t->h_st->B > t->sub_zone && k > t->sub_k) k = t->sub_k;
     // reset the per-step counter + budget (trainer.js:239)
     DevState* hs = t->h_st;
     hs->merges_done = 0;
@@ -367,7 +331,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     const bool sparse = t->sp;
     SpGrid sg{};
     if (sparse) {
-        const uint32_t zn = t->n - hs->B;   // zone length (it only shrinks within a step)
+        const uint32_t zn = (uint32_t)t->n - hs->B;   // zone length (it only shrinks within a step)
         const uint64_t zt = gbpe_div_up(zn, TILE);
         const uint32_t z256 = t->u16 ? zone_max<uint16_t>(256) : zone_max<uint32_t>(256);
         sg.bt = zn <= z256 ? 256 : 1024;   // small zone: the low-latency 256-thread workgroups
@@ -388,7 +352,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     }
     // the persistent tail loop: one workgroup, the whole step
 #ifdef GBPE_TAIL_LOOP
-    const uint32_t zn_now = sparse ? t->n - hs->B : 0u;
+    const uint32_t zn_now = sparse ? (uint32_t)t->n - hs->B : 0u;
     const bool tail = sparse && t->tail_on && !t->tail_skip && !t->sharded && t->last_mc <= t->tail_mc &&
                       zn_now <= (t->u16 ? zone_max<uint16_t>(TL_BT) : zone_max<uint32_t>(TL_BT)) &&
                       t->tb.nblk <= (TL_MAXG << TL_GRP);
@@ -496,8 +460,8 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         N -= mc;
         if (merges_out) memcpy(merges_out + 4 * r, t->h_log + 4 * r, 4 * sizeof(uint32_t));
     }
-    t->n = hs->n;
-    if (N != t->n) return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "host/device symbol count disagree");
+    if ((uint32_t)N != hs->n) return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "host/device symbol count disagree");
+    t->n = N;
     if (done) t->last_mc = t->h_log[(done - 1) * 4 + 3];
     if (t->trace) {   // merge index, count, stream length before, sparse, candidate sectors, sectors with sites
         uint64_t nn = N;
@@ -613,7 +577,7 @@ extern "C" int gbpe_trainer_symbols(gbpe_trainer* t, uint32_t* out, uint64_t cap
     if (!t || !n) return GBPE_E_INVALID;
     *n = t->n;
     if (!out) return GBPE_OK;
-    if (cap < t->n) return gbpe_set_error(t->ctx, GBPE_E_CAPACITY, "symbols: need %u", t->n);
+    if (cap < t->n) return gbpe_set_error(t->ctx, GBPE_E_CAPACITY, "symbols: need %llu", (unsigned long long)t->n);
     {
         int rc = sp_exit_any(t);   // back to one dense stream (training may go on; it re-enters later)
         if (rc != GBPE_OK) return rc;

@@ -82,6 +82,15 @@ struct DevState {
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
+// Offset of a merge's stale-window source in the zone's other buffer: n - 2mc - Bp
+// (global positions).  On one device n and Bp are kept modulo 2^32 — a trainer
+// built from shards holds more than 2^32 symbols — and only their
+// difference, a zone-sized length, is used; sharded ranks add their offsets.
+__device__ __forceinline__ uint64_t win_src0(const DevState& g, uint32_t mc) {
+    return g.sharded ? (uint64_t)g.n + g.off - g.poff - 2ull * mc - g.Bp
+                     : (uint64_t)(uint32_t)(g.n - g.Bp) - 2ull * mc;
+}
+
 // the zone segments' per-merge hand-off (zone_seg; k_refresh zeroes it)
 constexpr uint32_t NSEG_MAX = 64;   // one sweeping wave: one lane per segment
 constexpr uint32_t ZSEG_SPIN = 1u << 22;
@@ -582,7 +591,8 @@ __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log,
         // (n - 2mc >= Bp), and the zone stays >= 5 mc long so the next merge's window
         // does too (its count is <= mc + m <= 2 mc).  Otherwise the merge is not run
         // and the host returns to the dense loop.
-        if ((uint64_t)st->n < 2ull * mc + st->Bp) {   // cannot happen after the check below held
+        if ((st->sharded ? (uint64_t)st->n < 2ull * mc + st->Bp : (uint64_t)(uint32_t)(st->n - st->Bp) < 2ull * mc)) {
+            // (cannot happen after the check below held)
             atomicOr(&st->err, ERR_SPARSE_WINDOW);
             st->stop = 1u;
             return;
@@ -1462,7 +1472,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
         for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
     }
     if (!EXACT) {   // window source: global n - 2mc in the previous stream (sharded: it began at poff, now off)
-        const uint64_t src0 = (uint64_t)gs.n + gs.off - gs.poff - 2ull * mc - gs.Bp;
+        const uint64_t src0 = win_src0(gs, mc);
         for (uint32_t u = t; u < mc; u += BT) L.wb[u] = zo[src0 + u];
     }
     if (!zout) lds_clear(lt);
@@ -1658,7 +1668,7 @@ __device__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const 
     }
     // this segment's share of the window source (+ the symbol before it) into LDS
     const uint32_t lw = (mc + nz - 1) / nz, q0 = seg * lw, q1 = q0 + lw < mc ? q0 + lw : mc;   // source [q0, q1)
-    const uint64_t src0 = (uint64_t)gs.n + gs.off - gs.poff - 2ull * mc - gs.Bp;
+    const uint64_t src0 = win_src0(gs, mc);
     if (!EXACT && q0 < q1) {
         const uint32_t f = q0 ? q0 - 1u : 0u;   // L.wb[j] = source[f + j]
         for (uint32_t q = f + t; q < q1; q += BT) L.wb[q - f] = zo[src0 + q];
@@ -1897,7 +1907,8 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     nw = g.next_id;
     const bool stop = mc < 2u || nw > 0xFFFFu;                                          // train.wgsl:345-348
     const bool bad = !stop && !exact && g.is_last &&
-                     (uint64_t)g.n + g.off - g.poff < 2ull * mc + g.Bp;   // cannot happen
+                     (g.sharded ? (uint64_t)g.n + g.off - g.poff < 2ull * mc + g.Bp
+                                : (uint64_t)(uint32_t)(g.n - g.Bp) < 2ull * mc);   // cannot happen
     // zone misfit: this merge's window source must lie in the zone's stale buffer
     // (n - 2mc >= Bp, where n - Bp >= z - mc_prev: the last merge removed <= mc_prev
     // body symbols), and the zone keeps >= zf mc for the merges after it
@@ -2043,7 +2054,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         }
     }
     if (bid >= nbody) {
-        const uint64_t src0 = (uint64_t)gs->n + gs->off - gs->poff - 2ull * mc - gs->Bp;
+        const uint64_t src0 = win_src0(*gs, mc);
         const uint64_t stride = (uint64_t)(gridDim.x - nbody) * BT;
         for (uint64_t v = (uint64_t)(bid - nbody) * BT + t; v < mc; v += stride) wtmp[v] = zoth[src0 + v];
         if (t == 0) {

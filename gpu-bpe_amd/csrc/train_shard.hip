@@ -731,7 +731,7 @@ int shard_phase1_sp(gbpe_trainer* t, uint32_t round, uint32_t* rec, uint32_t cl)
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     const Table dt = delta_view(t, cl);
     const bool zone = t->h_st->is_last != 0;
-    const uint32_t zn = zone ? t->n - t->h_st->B : 0u;   // the zone only shrinks within a step
+    const uint32_t zn = zone ? (uint32_t)t->n - t->h_st->B : 0u;   // the zone only shrinks within a step
     const int bt = zn <= (t->u16 ? zone_max<uint16_t>(256) : zone_max<uint32_t>(256)) ? 256 : 1024;
     uint32_t nbody = 0, wpg = 0;
     body_grid(t, bt, &nbody, &wpg);

@@ -15,9 +15,11 @@ struct gbpe_trainer {
     uint32_t bps = 2;            // bytes per symbol
     uint64_t n0 = 0, cap_syms = 0;
     uint64_t n_prev0 = 0;        // created from a state: its previous-stream length (export before any merge)
+    uint32_t next_id0 = 256;     // Vocab.nextTokenId at creation
     void* buf[2] = {nullptr, nullptr};
     int cur = 0;                 // index of the buffer holding the stream
-    uint32_t n = 0;              // host copy of the stream length
+    uint64_t n = 0;              // host copy of the stream length (the device state holds it modulo 2^32:
+                                 // a lexicon trainer built from shards may exceed 32 bits)
     uint32_t needed = 0, done = 0;
     bool stop = false;
     uint32_t flags = 0, batch = GBPE_BATCH_SIZE;
@@ -114,6 +116,8 @@ struct gbpe_trainer {
     // distinct body word instead of the body itself
     bool lex = false;            // the current sparse entry uses it
     bool lex_on = true;          // GBPE_LEXICON=0: never
+    bool lex_only = false;       // built from shard lexicons (gbpe_trainer_create_from_lexicon): no dense stream,
+                                 // the body's stream order lives on the ranks; never leaves the sparse loop
     void* lx_store = nullptr;    // distinct words, each followed by a 0 separator (S symbols)
     uint32_t* lx_mul = nullptr;  // per store symbol: its word's occurrences (0 = separator / padding)
     uint64_t lx_cap = 0, lx_len = 0;   // store symbols: capacity, used
@@ -528,7 +532,7 @@ struct LxPlan {
 // makes the segment unusable, or (fresh) the store would not be much smaller
 // than the segment.
 template <typename S>
-int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& lp) {
+int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& lp, const uint32_t* wmul = nullptr) {
     hipStream_t s = t->ctx->stream;
     lp = LxPlan();
     if (len == 0) return GBPE_OK;
@@ -582,7 +586,7 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
     TR_HIP(t, hipMemsetAsync(ctr, 0, 32, s));
     if (nw)
         hipLaunchKernelGGL(k_lx_hash<S>, dim3((uint32_t)gbpe_div_up(nw, TPB * LX_WPT)), dim3(TPB), 0, s, seg, len,
-                           (const uint32_t*)lp.wpos, nw, keys, vals, (uint32_t)P, otmp, longs, ctr);
+                           (const uint32_t*)lp.wpos, nw, keys, vals, (uint32_t)P, otmp, longs, ctr, wmul);
     hipLaunchKernelGGL(k_lx_tabcount, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const unsigned long long*)keys, (uint32_t)P, bc);
     lx_scan(s, bc, nbb, bb);
     GBPE_LAUNCH_CHECK(t->ctx);
@@ -600,7 +604,8 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
                        (const uint32_t*)bc, (const uint64_t*)bb, (const uint32_t*)lp.wpos, nw, len, lp.usz, lp.umul, lp.urep);
     if (lp.nlong)
         hipLaunchKernelGGL(k_lx_longs, dim3((uint32_t)gbpe_div_up(lp.nlong, 256)), dim3(256), 0, s, (const uint32_t*)longs,
-                           (const uint32_t*)ctr, lp.nshort, (const uint32_t*)lp.wpos, nw, len, lp.usz, lp.umul, lp.urep);
+                           (const uint32_t*)ctr, lp.nshort, (const uint32_t*)lp.wpos, nw, len, lp.usz, lp.umul, lp.urep,
+                           wmul);
     if (nw)
         hipLaunchKernelGGL(k_lx_occ<S>, dim3((uint32_t)gbpe_div_up(nw, 256)), dim3(256), 0, s, seg, (const uint32_t*)lp.wpos, nw,
                            len, (const uint32_t*)otmp, (const unsigned long long*)keys, (const uint2*)vals, (uint32_t)P,
@@ -627,14 +632,14 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
 // sector windows after t->nsec with token bits and signatures, occurrences after
 // t->lx_nocc.  plan.ok = false (nothing changed) when the capacities cannot take it.
 template <typename S>
-int lx_commit(gbpe_trainer* t, LxPlan& lp, const S* seg, bool fresh) {
+int lx_commit(gbpe_trainer* t, LxPlan& lp, const S* seg, bool fresh, bool keep_occ = true) {
     hipStream_t s = t->ctx->stream;
     const uint32_t SEC = t->sp_secw;
     const uint64_t sbase = gbpe_div_up(t->lx_len, SEC) * SEC;
     const uint64_t nwin = gbpe_div_up(lp.T ? lp.T : 1, SEC);
     const uint64_t kb = sbase / SEC;
     if (sbase + nwin * SEC > t->lx_cap || kb + nwin > t->nsec_cap || kb + nwin > (uint64_t)t->W * 32 ||
-        (kb + nwin) * SP_SIGW > t->sig_cap || nwin > t->loc_cap || t->lx_nocc + lp.nw > t->lx_occ_cap) {
+        (kb + nwin) * SP_SIGW > t->sig_cap || nwin > t->loc_cap || (keep_occ && t->lx_nocc + lp.nw > t->lx_occ_cap)) {
         lp.ok = false;
         return GBPE_OK;
     }
@@ -656,7 +661,7 @@ int lx_commit(gbpe_trainer* t, LxPlan& lp, const S* seg, bool fresh) {
     } else {
         TR_HIP(t, hipMemsetAsync(t->sec + kb, 0, nwin * sizeof(uint2), s));
     }
-    if (lp.nw)
+    if (lp.nw && keep_occ)
         TR_HIP(t, hipMemcpyAsync(t->lx_occ + t->lx_nocc, lp.occ, (uint64_t)lp.nw * 4, hipMemcpyDeviceToDevice, s));
     // token bits and signatures of the new sectors (a fresh build: whole columns)
     hipLaunchKernelGGL(k_sp_bits<S>, dim3((uint32_t)gbpe_div_up(nwin, TPB / 64)), dim3(TPB), 0, s, (const S*)store,
@@ -667,7 +672,7 @@ int lx_commit(gbpe_trainer* t, LxPlan& lp, const S* seg, bool fresh) {
     GBPE_LAUNCH_CHECK(t->ctx);
     t->nsec = (uint32_t)(kb + nwin);
     t->lx_len = sbase + lp.T;
-    t->lx_nocc += lp.nw;
+    if (keep_occ) t->lx_nocc += lp.nw;
     t->lx_nuid += lp.nu;
     t->lx_words += lp.nw;
     return GBPE_OK;
@@ -676,9 +681,11 @@ int lx_commit(gbpe_trainer* t, LxPlan& lp, const S* seg, bool fresh) {
 // lexicon → dense stream: every body word occurrence's current symbols, in
 // stream order, to dst[0, B); returns the symbol total through *tot
 template <typename S>
-int lx_expand(gbpe_trainer* t, S* dst, uint64_t* tot) {
+int lx_expand(gbpe_trainer* t, S* dst, uint64_t* tot, const uint32_t* occ = nullptr, uint64_t n_occ = 0) {
+    // occ: another occurrence list over this store (the lexicon hand-over's rank lists)
     hipStream_t s = t->ctx->stream;
-    const uint64_t nu = t->lx_nuid, no = t->lx_nocc;
+    if (!occ) occ = t->lx_occ, n_occ = t->lx_nocc;
+    const uint64_t nu = t->lx_nuid, no = n_occ;
     int rc = lx_scratch(t, (2 * nu + no + 64) * 4 + (no / SCAN_BLK + 8) * 8 + 4096);
     if (rc != GBPE_OK) return rc;
     LxCarve c{(char*)t->lx_tmp};
@@ -690,15 +697,175 @@ int lx_expand(gbpe_trainer* t, S* dst, uint64_t* tot) {
         hipLaunchKernelGGL(k_lx_wordpos<S>, dim3((uint32_t)gbpe_div_up(t->nsec, TPB / 64)), dim3(TPB), 0, s,
                            (const S*)t->lx_store, (const uint2*)t->sec, t->nsec, (const uint32_t*)t->lx_w0, coff, clen);
     if (no)
-        hipLaunchKernelGGL(k_lx_olen, dim3((uint32_t)gbpe_div_up(no, 256)), dim3(256), 0, s, (const uint32_t*)t->lx_occ, no,
+        hipLaunchKernelGGL(k_lx_olen, dim3((uint32_t)gbpe_div_up(no, 256)), dim3(256), 0, s, occ, no,
                            (const uint32_t*)clen, olen);
     lx_scan(s, olen, no, oblk);
     if (no)
-        hipLaunchKernelGGL(k_lx_expand<S>, dim3((uint32_t)gbpe_div_up(no, 256)), dim3(256), 0, s, (const uint32_t*)t->lx_occ,
-                           no, (const uint32_t*)coff, (const uint32_t*)clen, (const S*)t->lx_store, (const uint32_t*)olen,
+        hipLaunchKernelGGL(k_lx_expand<S>, dim3((uint32_t)gbpe_div_up(no, 256)), dim3(256), 0, s, occ, no,
+                           (const uint32_t*)coff, (const uint32_t*)clen, (const S*)t->lx_store, (const uint32_t*)olen,
                            (const uint64_t*)oblk, dst);
     GBPE_LAUNCH_CHECK(t->ctx);
     TR_HIP(t, hipMemcpyAsync(tot, oblk + gbpe_div_up(no ? no : 1, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
+    return GBPE_OK;
+}
+
+// diagnostic (GBPE_LEX_CHECK=1): the lexicon right after a build expands back to the body
+template <typename S>
+int lx_check(gbpe_trainer* t, const S* cur, uint32_t Zs, const LxPlan& lp) {
+    hipStream_t s = t->ctx->stream;
+    int rc = GBPE_OK;
+    S* chk = nullptr;
+    TR_HIP(t, hipMalloc(&chk, ((uint64_t)Zs + 64) * sizeof(S)));
+    uint64_t tot = 0;
+    rc = lx_expand<S>(t, chk, &tot);
+    std::vector<S> a(Zs), b(Zs);
+    TR_HIP(t, hipStreamSynchronize(s));
+    TR_HIP(t, hipMemcpy(a.data(), chk, (uint64_t)Zs * sizeof(S), hipMemcpyDeviceToHost));
+    TR_HIP(t, hipMemcpy(b.data(), cur, (uint64_t)Zs * sizeof(S), hipMemcpyDeviceToHost));
+    hipFree(chk);
+    uint64_t bad = Zs;
+    for (uint64_t i = 0; i < Zs; ++i)
+        if (a[i] != b[i]) {
+            bad = i;
+            break;
+        }
+    std::vector<uint32_t> mm(lp.T);
+    std::vector<S> ss(lp.T);
+    TR_HIP(t, hipMemcpy(mm.data(), t->lx_mul, (uint64_t)lp.T * 4, hipMemcpyDeviceToHost));
+    TR_HIP(t, hipMemcpy(ss.data(), t->lx_store, (uint64_t)lp.T * sizeof(S), hipMemcpyDeviceToHost));
+    uint64_t wsum = 0, nz = 0, badm = 0;
+    for (uint32_t i = 0; i < lp.T; ++i) {
+        wsum += mm[i];
+        if ((ss[i] == 0) != (mm[i] == 0)) ++badm;
+    }
+    for (uint32_t i = 0; i < Zs; ++i) nz += (b[i] & Sym<S>::TM) ? 1 : 0;
+    fprintf(stderr, "[lex-check] Zs=%u words=%u distinct=%u+%u store=%u expanded=%llu first_diff=%llu "
+            "mult_sum=%llu nonzero_body=%llu sep_mismatch=%llu\n", Zs, lp.nw,
+            lp.nshort, lp.nlong, lp.T, (unsigned long long)tot, (unsigned long long)bad,
+            (unsigned long long)wsum, (unsigned long long)nz, (unsigned long long)badm);
+    return rc;
+}
+
+// ── sector-sparse layout: allocations shared by sp_enter and the lexicon
+//    hand-over (gbpe_trainer_create_from_lexicon) ──
+
+// sector arrays for `cap` sectors: extents, scratch, token bitmap (W words per
+// row), pair signatures — bitmap and signatures zeroed
+int sp_alloc_layout(gbpe_trainer* t, uint64_t cap) {
+    hipStream_t s = t->ctx->stream;
+    int rc = sp_grow(t, &t->sec, &t->nsec_cap, cap);
+    if (rc == GBPE_OK && (!t->sp_loc || t->loc_cap < cap)) {
+        hipFree(t->sp_loc);
+        hipFree(t->sp_blk);
+        t->sp_loc = nullptr;
+        t->sp_blk = nullptr;
+        t->loc_cap = 0;
+        if (hipMalloc(&t->sp_loc, cap * 4) != hipSuccess ||
+            hipMalloc(&t->sp_blk, (gbpe_div_up(cap, SCAN_BLK) + 1) * 8) != hipSuccess)
+            rc = gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sector scratch) failed");
+        else
+            t->loc_cap = cap;
+    }
+    if (rc != GBPE_OK) return rc;
+    t->W = (uint32_t)gbpe_div_up(cap, 32);
+    rc = sp_grow(t, &t->bits, &t->bits_cap, (uint64_t)t->max_id * t->W);
+    if (rc == GBPE_OK) rc = sp_grow(t, &t->sig, &t->sig_cap, cap * SP_SIGW);
+    if (rc != GBPE_OK) return rc;
+    t->nsec = 0;
+    TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
+    TR_HIP(t, hipMemsetAsync(t->sig, 0, cap * SP_SIGW * 4, s));
+    return GBPE_OK;
+}
+
+// word-lexicon store for `cap` sectors of sp_secw symbols, occurrence list of `ocap`
+int sp_alloc_lexicon(gbpe_trainer* t, uint64_t cap, uint64_t ocap) {
+    const uint64_t scap = cap * t->sp_secw;
+    if (!t->lx_store || t->lx_cap < scap) {
+        hipFree(t->lx_store);
+        hipFree(t->lx_mul);
+        hipFree(t->lx_w0);
+        t->lx_store = nullptr;
+        t->lx_mul = t->lx_w0 = nullptr;
+        t->lx_cap = 0;
+        if (hipMalloc(&t->lx_store, scap * t->bps) != hipSuccess || hipMalloc(&t->lx_mul, scap * 4) != hipSuccess ||
+            hipMalloc(&t->lx_w0, cap * 4) != hipSuccess)
+            return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(word lexicon) failed");
+        t->lx_cap = scap;
+    }
+    return sp_grow(t, &t->lx_occ, &t->lx_occ_cap, ocap);
+}
+
+// zone buffers (zeroed): the zone, and the stale source (previous stream,
+// n_prev - Zs <= z + prev_mc symbols), at least the one-workgroup zone pass's full
+// register window, which it loads unconditionally
+int sp_alloc_zone(gbpe_trainer* t, uint64_t z, uint64_t prev_mc) {
+    hipStream_t s = t->ctx->stream;
+    uint64_t zneed = (gbpe_div_up(z + prev_mc + 1, TILE) + 2) * TILE;
+    const uint64_t zmin = (uint64_t)(t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024)) + TILE;
+    if (zneed < zmin) zneed = zmin;
+    if (zneed > t->zcap) {
+        for (int k = 0; k < 2; ++k) {
+            hipFree(t->zbuf[k]);
+            t->zbuf[k] = nullptr;
+        }
+        hipFree(t->wtmp);
+        t->wtmp = nullptr;
+        t->zcap = 0;
+        if (hipMalloc(&t->zbuf[0], zneed * t->bps) != hipSuccess || hipMalloc(&t->zbuf[1], zneed * t->bps) != hipSuccess ||
+            hipMalloc(&t->wtmp, zneed * t->bps) != hipSuccess)
+            return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(zone) failed");
+        t->zcap = zneed;
+    }
+    for (int k = 0; k < 2; ++k) TR_HIP(t, hipMemsetAsync(t->zbuf[k], 0, t->zcap * t->bps, s));
+    return GBPE_OK;
+}
+
+// the states of a sparse entry: zone state (length z), body length Zs in the
+// global state, the zone rule's fields; per-k_body-workgroup byte counters, the
+// k_refresh partial maxima, the zone-segment hand-off.  The caller then runs a
+// k_refresh (block maxima + partial maxima) before the first sparse merge.
+int sp_init_states(gbpe_trainer* t, uint64_t cap, uint32_t Zs, uint32_t z, uint32_t zlast) {
+    hipStream_t s = t->ctx->stream;
+    if (!t->zst) {
+        TR_HIP(t, hipMalloc(&t->zst, sizeof(DevState)));
+        TR_HIP(t, hipHostMalloc((void**)&t->h_zst, sizeof(DevState), hipHostMallocDefault));
+    }
+    memset(t->h_zst, 0, sizeof(DevState));
+    t->h_zst->n = z;
+    TR_HIP(t, hipMemcpyAsync(t->zst, t->h_zst, sizeof(DevState), hipMemcpyHostToDevice, s));
+    t->h_st->B = Zs;
+    t->h_st->Bp = Zs;
+    t->h_st->body_rm = 0;
+    t->h_st->sp_abort = 0;
+    TR_HIP(t, hipMemcpyAsync(&t->st->B, &t->h_st->B, 4 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    // every rank checks the zone against the same length: the zone rank's target
+    // until the first exchange reports the real one (single GPU: the real one)
+    t->h_st->zlast = zlast;
+    t->h_st->is_last = z ? 1u : 0u;
+    TR_HIP(t, hipMemcpyAsync(&t->st->zlast, &t->h_st->zlast, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    TR_HIP(t, hipMemcpyAsync(&t->st->is_last, &t->h_st->is_last, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    {   // one byte counter per k_body workgroup, kept across entries (summed by gbpe_trainer_stats_get)
+        const uint64_t need = gbpe_div_up(gbpe_div_up(cap, 32), SP_WPW_MIN) + 2;
+        if (need > t->wg_cap) {
+            uint64_t* nb = nullptr;
+            TR_HIP(t, hipMalloc(&nb, need * sizeof(uint64_t)));
+            TR_HIP(t, hipMemsetAsync(nb, 0, need * sizeof(uint64_t), s));
+            if (t->wg_bytes) TR_HIP(t, hipMemcpyAsync(nb, t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+            TR_HIP(t, hipStreamSynchronize(s));
+            hipFree(t->wg_bytes);
+            t->wg_bytes = nb;
+            t->wg_cap = need;
+        }
+    }
+    // the zone rule's last count (sel_inline): the count of the merge before entry
+    TR_HIP(t, hipMemcpyAsync(&t->st->mc_prev, &t->st->mc, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    // per-k_refresh-workgroup maxima the sparse merges select from (sel_inline)
+    if (!t->part) TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
+    if (!t->zseg && !t->sharded) {
+        TR_HIP(t, hipMalloc(&t->zseg, sizeof(ZSegState)));
+        TR_HIP(t, hipMemsetAsync(t->zseg, 0, sizeof(ZSegState), t->ctx->stream));
+    }
+    if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
     return GBPE_OK;
 }
 
@@ -711,7 +878,7 @@ int lx_expand(gbpe_trainer* t, S* dst, uint64_t* tot) {
 template <typename S>
 int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
     hipStream_t s = t->ctx->stream;
-    const uint32_t n = t->n;
+    const uint32_t n = (uint32_t)t->n;
     const uint64_t prev_mc = t->last_mc;   // the previous stream is n + prev_mc long
     const uint64_t nmc = next_mc ? next_mc : prev_mc;
     const uint64_t zt = std::max<uint64_t>((uint64_t)t->sp_zt * nmc, 2ull * nmc + prev_mc) + 64;
@@ -744,78 +911,16 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
     // one partial window per zone shrink (at most SP_SHRINKS per entry)
     const uint64_t cap = lp.ok ? gbpe_div_up((uint64_t)lp.T + 2ull * z, t->sp_secw) + 2 * (SP_SHRINKS + 1)
                                : gbpe_div_up(n, t->sp_secw) + SP_SHRINKS + 1;
-    int rc = sp_grow(t, &t->sec, &t->nsec_cap, cap);
-    if (rc == GBPE_OK && (!t->sp_loc || t->loc_cap < cap)) {
-        hipFree(t->sp_loc);
-        hipFree(t->sp_blk);
-        t->sp_loc = nullptr;
-        t->sp_blk = nullptr;
-        t->loc_cap = 0;
-        if (hipMalloc(&t->sp_loc, cap * 4) != hipSuccess ||
-            hipMalloc(&t->sp_blk, (gbpe_div_up(cap, SCAN_BLK) + 1) * 8) != hipSuccess)
-            rc = gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sector scratch) failed");
-        else
-            t->loc_cap = cap;
-    }
-    if (rc != GBPE_OK) return rc;
-    t->W = (uint32_t)gbpe_div_up(cap, 32);
-    rc = sp_grow(t, &t->bits, &t->bits_cap, (uint64_t)t->max_id * t->W);
-    if (rc == GBPE_OK) rc = sp_grow(t, &t->sig, &t->sig_cap, cap * SP_SIGW);
+    int rc = sp_alloc_layout(t, cap);
     if (rc != GBPE_OK) return rc;
     t->bcur = t->cur;
-    t->nsec = 0;
-    TR_HIP(t, hipMemsetAsync(t->bits, 0, (uint64_t)t->max_id * t->W * 4, s));
-    TR_HIP(t, hipMemsetAsync(t->sig, 0, cap * SP_SIGW * 4, s));
     if (lp.ok) {
-        const uint64_t scap = cap * t->sp_secw, ocap = (uint64_t)lp.nw + z + 1;
-        if (!t->lx_store || t->lx_cap < scap) {
-            hipFree(t->lx_store);
-            hipFree(t->lx_mul);
-            hipFree(t->lx_w0);
-            t->lx_store = nullptr;
-            t->lx_mul = t->lx_w0 = nullptr;
-            t->lx_cap = 0;
-            if (hipMalloc(&t->lx_store, scap * t->bps) != hipSuccess || hipMalloc(&t->lx_mul, scap * 4) != hipSuccess ||
-                hipMalloc(&t->lx_w0, cap * 4) != hipSuccess)
-                return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(word lexicon) failed");
-            t->lx_cap = scap;
-        }
-        rc = sp_grow(t, &t->lx_occ, &t->lx_occ_cap, ocap);
+        rc = sp_alloc_lexicon(t, cap, (uint64_t)lp.nw + z + 1);
         if (rc != GBPE_OK) return rc;
         t->lex = true;
         rc = lx_commit<S>(t, lp, cur, true);
         if (rc == GBPE_OK && !lp.ok) rc = gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "word lexicon capacity");
-        if (rc == GBPE_OK && getenv("GBPE_LEX_CHECK")) {   // diagnostic: the lexicon expands back to the body
-            S* chk = nullptr;
-            TR_HIP(t, hipMalloc(&chk, ((uint64_t)Zs + 64) * sizeof(S)));
-            uint64_t tot = 0;
-            rc = lx_expand<S>(t, chk, &tot);
-            std::vector<S> a(Zs), b(Zs);
-            TR_HIP(t, hipStreamSynchronize(s));
-            TR_HIP(t, hipMemcpy(a.data(), chk, (uint64_t)Zs * sizeof(S), hipMemcpyDeviceToHost));
-            TR_HIP(t, hipMemcpy(b.data(), cur, (uint64_t)Zs * sizeof(S), hipMemcpyDeviceToHost));
-            hipFree(chk);
-            uint64_t bad = Zs;
-            for (uint64_t i = 0; i < Zs; ++i)
-                if (a[i] != b[i]) {
-                    bad = i;
-                    break;
-                }
-            std::vector<uint32_t> mm(lp.T);
-            std::vector<S> ss(lp.T);
-            TR_HIP(t, hipMemcpy(mm.data(), t->lx_mul, (uint64_t)lp.T * 4, hipMemcpyDeviceToHost));
-            TR_HIP(t, hipMemcpy(ss.data(), t->lx_store, (uint64_t)lp.T * sizeof(S), hipMemcpyDeviceToHost));
-            uint64_t wsum = 0, nz = 0, badm = 0;
-            for (uint32_t i = 0; i < lp.T; ++i) {
-                wsum += mm[i];
-                if ((ss[i] == 0) != (mm[i] == 0)) ++badm;
-            }
-            for (uint32_t i = 0; i < Zs; ++i) nz += (b[i] & Sym<S>::TM) ? 1 : 0;
-            fprintf(stderr, "[lex-check] Zs=%u words=%u distinct=%u+%u store=%u expanded=%llu first_diff=%llu "
-                    "mult_sum=%llu nonzero_body=%llu sep_mismatch=%llu\n", Zs, lp.nw,
-                    lp.nshort, lp.nlong, lp.T, (unsigned long long)tot, (unsigned long long)bad,
-                    (unsigned long long)wsum, (unsigned long long)nz, (unsigned long long)badm);
-        }
+        if (rc == GBPE_OK && getenv("GBPE_LEX_CHECK")) rc = lx_check<S>(t, cur, Zs, lp);
     } else {
         rc = sp_add_sectors<S>(t, 0u, Zs);
     }
@@ -823,25 +928,8 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
     t->sp_age = 0;
     t->sp_bits_age = 0;
     t->sp_shrinks = 0;
-    // zone buffers: the zone, and the stale source (previous stream, n_prev - Zs <= z + last_mc symbols)
-    // (>= the one-workgroup zone pass's full register window, which it loads unconditionally)
-    uint64_t zneed = (gbpe_div_up((uint64_t)z + prev_mc + 1, TILE) + 2) * TILE;
-    const uint64_t zmin = (uint64_t)(t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024)) + TILE;
-    if (zneed < zmin) zneed = zmin;
-    if (zneed > t->zcap) {
-        for (int k = 0; k < 2; ++k) {
-            hipFree(t->zbuf[k]);
-            t->zbuf[k] = nullptr;
-        }
-        hipFree(t->wtmp);
-        t->wtmp = nullptr;
-        t->zcap = 0;
-        if (hipMalloc(&t->zbuf[0], zneed * t->bps) != hipSuccess || hipMalloc(&t->zbuf[1], zneed * t->bps) != hipSuccess ||
-            hipMalloc(&t->wtmp, zneed * t->bps) != hipSuccess)
-            return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(zone) failed");
-        t->zcap = zneed;
-    }
-    for (int k = 0; k < 2; ++k) TR_HIP(t, hipMemsetAsync(t->zbuf[k], 0, t->zcap * t->bps, s));
+    rc = sp_alloc_zone(t, z, prev_mc);
+    if (rc != GBPE_OK) return rc;
     if (z) {
         TR_HIP(t, hipMemcpyAsync(t->zbuf[0], cur + Zs, (uint64_t)z * t->bps, hipMemcpyDeviceToDevice, s));
         uint64_t sl = (uint64_t)z + prev_mc;
@@ -849,46 +937,8 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
         if (sl > t->zcap) sl = t->zcap;
         TR_HIP(t, hipMemcpyAsync(t->zbuf[1], stale + Zs, sl * t->bps, hipMemcpyDeviceToDevice, s));
     }
-    // states
-    if (!t->zst) {
-        TR_HIP(t, hipMalloc(&t->zst, sizeof(DevState)));
-        TR_HIP(t, hipHostMalloc((void**)&t->h_zst, sizeof(DevState), hipHostMallocDefault));
-    }
-    memset(t->h_zst, 0, sizeof(DevState));
-    t->h_zst->n = z;
-    TR_HIP(t, hipMemcpyAsync(t->zst, t->h_zst, sizeof(DevState), hipMemcpyHostToDevice, s));
-    t->h_st->B = Zs;
-    t->h_st->Bp = Zs;
-    t->h_st->body_rm = 0;
-    t->h_st->sp_abort = 0;
-    TR_HIP(t, hipMemcpyAsync(&t->st->B, &t->h_st->B, 4 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    // every rank checks the zone against the same length: the zone rank's target
-    // until the first exchange reports the real one (single GPU: the real one)
-    t->h_st->zlast = t->sharded ? (uint32_t)zt : z;
-    t->h_st->is_last = z ? 1u : 0u;
-    TR_HIP(t, hipMemcpyAsync(&t->st->zlast, &t->h_st->zlast, sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    TR_HIP(t, hipMemcpyAsync(&t->st->is_last, &t->h_st->is_last, sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    {   // one byte counter per k_body workgroup, kept across entries (summed by gbpe_trainer_stats_get)
-        const uint64_t need = gbpe_div_up(gbpe_div_up(cap, 32), SP_WPW_MIN) + 2;
-        if (need > t->wg_cap) {
-            uint64_t* nb = nullptr;
-            TR_HIP(t, hipMalloc(&nb, need * sizeof(uint64_t)));
-            TR_HIP(t, hipMemsetAsync(nb, 0, need * sizeof(uint64_t), s));
-            if (t->wg_bytes) TR_HIP(t, hipMemcpyAsync(nb, t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
-            TR_HIP(t, hipStreamSynchronize(s));
-            hipFree(t->wg_bytes);
-            t->wg_bytes = nb;
-            t->wg_cap = need;
-        }
-    }
-    // the zone rule's last count (sel_inline): the count of the merge before entry
-    TR_HIP(t, hipMemcpyAsync(&t->st->mc_prev, &t->st->mc, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-    // per-k_refresh-workgroup maxima the sparse merges select from (sel_inline)
-    if (!t->part) TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
-    if (!t->zseg && !t->sharded) {
-        TR_HIP(t, hipMalloc(&t->zseg, sizeof(ZSegState)));
-        TR_HIP(t, hipMemsetAsync(t->zseg, 0, sizeof(ZSegState), t->ctx->stream));
-    }
+    rc = sp_init_states(t, cap, Zs, z, t->sharded ? (uint32_t)zt : z);
+    if (rc != GBPE_OK) return rc;
     hipLaunchKernelGGL(k_refresh<S>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
                        (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part);
     GBPE_LAUNCH_CHECK(t->ctx);
@@ -910,7 +960,7 @@ template <typename S>
 int sp_shrink(gbpe_trainer* t) {
     hipStream_t s = t->ctx->stream;
     DevState* hs = t->h_st;
-    const uint32_t z = t->n - hs->B;
+    const uint32_t z = (uint32_t)t->n - hs->B;
     const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
     if (t->sp_shrinks >= SP_SHRINKS || (uint64_t)z < zt * t->shrink_pct / 100 + 4096) return GBPE_OK;
     S* zc = (S*)t->zbuf[t->zcur];
@@ -957,6 +1007,9 @@ int sp_shrink(gbpe_trainer* t) {
 // next merge's stale window can read).
 template <typename S>
 int sp_exit(gbpe_trainer* t) {
+    if (t->lex_only)
+        return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "a trainer built from shard lexicons cannot return to one dense "
+                              "stream (a merge outgrew the zone, or the stream was asked for: use gbpe_trainer_expand)");
     hipStream_t s = t->ctx->stream;
     DevState* hs = t->h_st;
     TR_HIP(t, hipMemcpyAsync(hs, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
@@ -998,6 +1051,50 @@ int sp_exit(gbpe_trainer* t) {
     t->lex = false;
     ++t->sp_exits;
     return GBPE_OK;
+}
+
+// options and environment knobs of a new trainer; symbol width from the ids the run can make
+void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts) {
+    t->ctx = ctx;
+    t->flags = opts->flags;
+    t->batch = opts->batch_size ? opts->batch_size : GBPE_BATCH_SIZE;
+    const uint32_t vocab_size = opts->vocab_size ? opts->vocab_size : 256u;
+    const uint32_t next_id = opts->next_token_id ? opts->next_token_id : 256u;
+    t->next_id0 = next_id;
+    t->needed = opts->target_vocab_size > vocab_size ? opts->target_vocab_size - vocab_size : 0u;
+    // u16 symbols when every id the run can produce fits in 15 bits
+    const uint64_t max_id = (uint64_t)next_id + t->needed;    // exclusive
+    t->u16 = max_id <= 0x8000ull;
+    t->max_id = (uint32_t)(max_id < 0x10000ull ? max_id : 0x10000ull);
+    if (const char* e = getenv("GBPE_SPARSE_DIV")) t->sp_div = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_REFRESH_BLOCKS")) t->refresh_blocks = (uint32_t)atoi(e);
+    if (const char* e = getenv("GBPE_REHASH")) t->rehash_on = atoi(e) != 0;
+    t->body_cap = (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
+    if (const char* e = getenv("GBPE_BODY_WG")) t->body_cap = std::max<uint32_t>(1, (uint32_t)atoi(e));
+    if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_LEXICON")) t->lex_on = atoi(e) != 0;
+    if (const char* e = getenv("GBPE_TAIL")) t->tail_on = atoi(e) != 0;
+    if (const char* e = getenv("GBPE_ZONE16")) t->zone16 = atoi(e) != 0;
+    if (const char* e = getenv("GBPE_TAIL_MC")) t->tail_mc = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_LEXICON_DIV")) t->lx_div = std::max<uint32_t>(8, (uint32_t)strtoul(e, nullptr, 10));
+    if (const char* e = getenv("GBPE_SUBSTEP_ZONE")) t->sub_zone = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_SUBSTEP")) t->sub_k = std::max<uint32_t>(2, (uint32_t)strtoul(e, nullptr, 10)) & ~1u;
+    if (const char* e = getenv("GBPE_DELTA_MT")) t->delta_mt = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_DELTA_TPW")) {
+        const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
+        t->delta_tpw = v >= 32 ? 32 : v >= 16 ? 16 : 8;
+    }
+    if (const char* e = getenv("GBPE_SHRINK_PCT")) t->shrink_pct = std::max<uint32_t>(110, (uint32_t)strtoul(e, nullptr, 10));
+    if (const char* e = getenv("GBPE_ZONE_SEG")) t->zseg_mode = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_ZONE_F")) t->zone_f = std::max<uint32_t>(3, (uint32_t)strtoul(e, nullptr, 10));
+    if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
+    if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
+        t->trace = fopen(e, "w");
+        if (t->trace && (hipMalloc(&t->d_clog, (size_t)t->batch * 8) != hipSuccess ||
+                         hipHostMalloc((void**)&t->h_clog, (size_t)t->batch * 8, hipHostMallocDefault) != hipSuccess))
+            t->d_clog = nullptr, t->h_clog = nullptr;   // trace without candidate counts
+    }
+    t->bps = t->u16 ? 2 : 4;
 }
 
 int sp_exit_any(gbpe_trainer* t) { return !t->sp ? GBPE_OK : (t->u16 ? sp_exit<uint16_t>(t) : sp_exit<uint32_t>(t)); }

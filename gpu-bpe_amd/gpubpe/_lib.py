@@ -60,6 +60,14 @@ class TrainerStats(C.Structure):
                 ("ms_tail", C.c_double)]
 
 
+class LexShardInfo(C.Structure):
+    _fields_ = [("symbols", C.c_uint64), ("body", C.c_uint64), ("zone", C.c_uint64), ("store_symbols", C.c_uint64),
+                ("entries", C.c_uint64), ("words", C.c_uint64), ("top_count", C.c_uint32),
+                ("bytes_per_symbol", C.c_uint32)]
+
+
+GBPE_LEXSHARD_STORE, GBPE_LEXSHARD_MUL, GBPE_LEXSHARD_OCC, GBPE_LEXSHARD_ZONE = 0, 1, 2, 3
+
 PROGRESS_CB = C.CFUNCTYPE(C.c_int, C.POINTER(Progress), u32p, C.c_void_p)
 
 # (name, restype, argtypes)
@@ -128,6 +136,19 @@ _SIGS = [
                                             C.c_int]),
     ("gbpe_trainer_create_from_state", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int,
                                                  C.POINTER(TrainOpts), C.POINTER(C.c_void_p)]),
+    ("gbpe_lexshard_create", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int, C.POINTER(TrainOpts),
+                                       C.POINTER(C.c_void_p)]),
+    ("gbpe_lexshard_build", C.c_int, [C.c_void_p, C.c_uint64]),
+    ("gbpe_lexshard_info_get", C.c_int, [C.c_void_p, C.POINTER(LexShardInfo)]),
+    ("gbpe_lexshard_copy", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64, C.c_int]),
+    ("gbpe_lexshard_release", C.c_int, [C.c_void_p]),
+    ("gbpe_lexshard_remap", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int]),
+    ("gbpe_lexshard_destroy", None, [C.c_void_p]),
+    ("gbpe_trainer_create_from_lexicon", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                                   C.c_uint64, C.c_uint64, C.c_int, C.POINTER(TrainOpts), C.c_void_p,
+                                                   C.c_uint64, u64p, C.c_int, C.POINTER(C.c_void_p)]),
+    ("gbpe_trainer_expand", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_uint64, u64p,
+                                      C.c_int]),
 ]
 
 EXPORTED = [s[0] for s in _SIGS]

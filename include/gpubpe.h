@@ -264,6 +264,64 @@ int gbpe_trainer_create_from_state(gbpe_ctx* ctx, const uint32_t* cur, uint64_t 
                                    uint64_t n_prev, int input_on_device, const gbpe_train_opts* opts,
                                    gbpe_trainer** out);
 
+/* ── sharded first pass + lexicon hand-over ─────────
+ * The reference trains on one device (training-pipeline.js:178-222) and its merge
+ * chain is sequential, so a multi-GPU run parallelises the first pass instead:
+ * every rank turns ITS piece of the corpus (cut at a word start of the global
+ * stream, the pieces concatenated in rank order are the corpus) into symbols, pair
+ * counts and a word lexicon — its distinct words with their multiplicities — and ONE
+ * root continues from all of them with the single-device sector-sparse loop
+ * (DESIGN §2b/§2c).  The last piece keeps its tail as the dense zone, where the
+ * reference compaction quirk acts (train.wgsl:605-607 + 698/727).  The stream order
+ * of the body stays on the ranks (their occurrence lists), so the stream may exceed
+ * one device's 32-bit positions (C4: 8.6*10^9 symbols).  Protocol:
+ *   rank:  lexshard_create → info_get: top_count → (sum over ranks: an upper bound of the
+ *          first merge's count; the last rank's zone target) lexshard_build(zt)
+ *          → copy STORE + MUL (and the last rank's ZONE) to the root → release
+ *   root:  trainer_create_from_lexicon(stores in rank order, zone, body symbols)
+ *          → map (a global word id per store entry, in rank order) → rank slices
+ *          → lexshard_remap; gbpe_trainer_step as for any trainer
+ *   check: gbpe_trainer_expand(root, every rank's OCC in rank order) = the stream. */
+typedef struct gbpe_lexshard gbpe_lexshard;
+typedef struct gbpe_lexshard_info {
+    uint64_t symbols;        /* the piece's symbols */
+    uint64_t body;           /* symbols before its zone (all of them on a rank without a zone) */
+    uint64_t zone;           /* zone symbols (the last rank) */
+    uint64_t store_symbols;  /* distinct words + one 0 separator each */
+    uint64_t entries;        /* distinct words (words over 64 symbols: one entry per occurrence) */
+    uint64_t words;          /* body words in stream order (the occurrence list) */
+    uint32_t top_count;      /* the piece's largest pair count */
+    uint32_t bytes_per_symbol;   /* STORE / ZONE layout: 2 = u16 (bit 15 word start), 4 = u32 (bit 16) */
+} gbpe_lexshard_info;
+#define GBPE_LEXSHARD_STORE 0   /* store_symbols x bytes_per_symbol */
+#define GBPE_LEXSHARD_MUL   1   /* store_symbols x u32: each symbol's word multiplicity (0 at separators) */
+#define GBPE_LEXSHARD_OCC   2   /* words x u32: word id (local; global after remap) or 0x80000000|symbol */
+#define GBPE_LEXSHARD_ZONE  3   /* zone x bytes_per_symbol */
+/* opts as for gbpe_trainer_create, identical on every rank and the root */
+int  gbpe_lexshard_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
+                          int input_on_device, const gbpe_train_opts* opts, gbpe_lexshard** out);
+int  gbpe_lexshard_build(gbpe_lexshard* ls, uint64_t zone_target /* 0: no zone */);
+int  gbpe_lexshard_info_get(const gbpe_lexshard* ls, gbpe_lexshard_info* out);
+int  gbpe_lexshard_copy(gbpe_lexshard* ls, int part, void* dst, uint64_t cap_bytes, int dst_on_device);
+int  gbpe_lexshard_release(gbpe_lexshard* ls);   /* frees the piece's stream and counts, keeps the lexicon */
+int  gbpe_lexshard_remap(gbpe_lexshard* ls, const uint32_t* map, uint64_t n_map, int map_on_device);
+void gbpe_lexshard_destroy(gbpe_lexshard* ls);
+/* The root trainer: store / mul = every rank's STORE and MUL concatenated in rank
+ * order (store_len symbols), zone = the last rank's ZONE, body_len = the symbols of
+ * every piece before the zone (the stream is body_len + zone_len symbols; may exceed
+ * 2^32).  map_out (map_cap entries) receives one global word id per store entry.
+ * The trainer never returns to one dense stream: gbpe_trainer_symbols /
+ * export_state fail, gbpe_trainer_expand rebuilds the stream. */
+int  gbpe_trainer_create_from_lexicon(gbpe_ctx* ctx, const void* store, const uint32_t* mul, uint64_t store_len,
+                                      const void* zone, uint64_t zone_len, uint64_t body_len, int input_on_device,
+                                      const gbpe_train_opts* opts, uint32_t* map_out, uint64_t map_cap,
+                                      uint64_t* n_map, int map_on_device, gbpe_trainer** out);
+/* The current stream (u32 reference layout) of a trainer in the word-lexicon loop:
+ * prefix_occ (every rank's remapped OCC in rank order; none for a single-device
+ * trainer) then the trainer's own occurrences, then its zone.  out NULL: length only. */
+int  gbpe_trainer_expand(gbpe_trainer* t, const uint32_t* prefix_occ, uint64_t n_prefix, int prefix_on_device,
+                         uint32_t* out, uint64_t cap, uint64_t* n_out, int out_on_device);
+
 /* ── trie encode (replaces tokenizer.js:54-335 TrieTokenizer over the
  *    tokenize.wgsl kernels) ─────────────────────────────────────────────── */
 

@@ -49,6 +49,9 @@ TRAIN = {
     # C4's rank-0 shard (8 x 1 GiB multilingual, seed 5 + rank) trained
     # alone at C4's 64K vocab (u32 symbols: ids reach 0xFFFF, the stop of train.wgsl:345)
     "ml1g64k": ({"gen": "multilingual", "n": 1 << 30, "seed": 5}, 65536, "heuristic"),
+    # C4-shaped at a size the oracle holds: 8 shards x 128 MiB multilingual, seeds 5..12,
+    # concatenated in rank order, 64K vocab, heuristic word starts of the concatenated stream
+    "c4s8x128m": ({"gen": "ml_shards", "shard": 128 << 20, "seeds": list(range(5, 13))}, 65536, "heuristic"),
 }
 # name -> (text spec, vocab fixture)
 ENCODE = {
@@ -65,6 +68,8 @@ def corpus(spec: dict) -> bytes:
         return synth.multilingual(spec["n"], seed=spec["seed"])
     if g == "code":
         return synth.code(spec["n"], seed=spec["seed"])
+    if g == "ml_shards":
+        return b"".join(synth.multilingual(spec["shard"], seed=sd) for sd in spec["seeds"])
     raise ValueError(g)
 
 
