@@ -77,6 +77,20 @@ def make_corpus(spec: dict) -> bytes:
     return synth.code(spec["n"], seed=spec["seed"])
 
 
+class _stdout_to_stderr:
+    """fd 1 -> fd 2 for the duration (native libraries' prints included)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 class Dist:
     """Process groups: the default group carries the sharded trainer's data path
     (RCCL = backend "nccl" over xGMI; GBPE_SHARD_TRANSPORT=gloo stages records
@@ -94,12 +108,14 @@ class Dist:
             import torch
             import torch.distributed as dist
             torch.cuda.set_device(local)
-            if self.transport == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-            else:
-                dist.init_process_group("gloo")
-            self.dist = dist
-            self.host = dist.new_group(backend="gloo")
+            with _stdout_to_stderr():   # gloo prints its connection banner on stdout: keep stdout the one JSON line
+                if self.transport == "nccl":
+                    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+                else:
+                    dist.init_process_group("gloo")
+                self.dist = dist
+                self.host = dist.new_group(backend="gloo")
+                self.dist.barrier(group=self.host)   # (the gloo pairs connect here)
 
     def barrier(self):
         if hasattr(self, "host"):
@@ -703,6 +719,162 @@ def split_encode_leg(args, lib, ctx, dist, rank, world):
     return res
 
 
+def lexshard_run(lib, ctx, dist, d, n, vocab, flags=0, want_final=False):
+    """One complete run of the sharded first pass + lexicon hand-over (DESIGN §5,
+    gpubpe/lexshard.py) on this rank's HBM-resident piece; every rank returns the
+    global merge list.  RCCL moves the stores point to point (device tensors);
+    GBPE_SHARD_TRANSPORT=gloo (ranks sharing one GPU) moves host copies."""
+    from gpubpe.lexshard import GpuLexBackend, LexShardTrainer
+    be = GpuLexBackend(lib, ctx, vocab, flags=flags)
+    staged = dist.transport != "nccl"
+    tr = LexShardTrainer(be, dist.dist, staged=staged, host_group=None if staged else dist.host)
+    try:
+        merges, early = tr.train(d, n, True, vocab)
+        fin = tr.final_stream() if want_final else None
+    finally:
+        be.close()
+    return np.array(merges, dtype=np.uint32).reshape(-1, 4), tr, fin
+
+
+LEX_PHASES = ("create_s", "build_s", "exchange_s", "root_create_s", "loop_s", "total_s")   # LexShardTrainer.timing
+
+
+def lex_timing(dist, tr):
+    """Phase times of the last run (seconds since its start), max over ranks (the
+    same keys on every rank: each is one collective)."""
+    return {k: round(dist.max(float(tr.timing.get(k, 0.0))), 4) for k in LEX_PHASES}
+
+
+def lexshard_line(args, lib, ctx, dist, rank, world):
+    """N > 1: the headline corpus cut at word starts into one piece per rank; the
+    first pass (symbols, counts, word lexicon) runs on every GPU, the merge chain
+    on the last rank (the reference's loop is sequential: training-pipeline.js:
+    178-222).  value = merges of the K timed runs / max wall over ranks."""
+    t = time.time()
+    full = make_corpus(HEADLINE)
+    piece = shard_of(full, rank, world)
+    log(f"[bench] rank {rank}: piece {len(piece)} B of {len(full)} in {time.time() - t:.1f}s")
+    d = device_buffer(lib, ctx, piece)
+    n = len(piece)
+    for _ in range(args.warmup):
+        lexshard_run(lib, ctx, dist, d, n, args.vocab)
+    lib.gbpe_synchronize(ctx)
+    dist.barrier()
+    lib.gbpe_synchronize(ctx)
+    t0 = time.perf_counter()
+    total, last, tr = 0, None, None
+    for _ in range(args.steps):
+        last, tr, _ = lexshard_run(lib, ctx, dist, d, n, args.vocab)
+        total += last.shape[0]
+    lib.gbpe_synchronize(ctx)
+    t1 = time.perf_counter()
+    dist.barrier()
+    wall = dist.max(t1 - t0)
+    timing = lex_timing(dist, tr)
+    lib.gbpe_device_free(ctx, d)
+    want, meta = fixture("en1g")
+    parity = {}
+    if want is not None and args.vocab == 32768:
+        ok = 1.0 if (last.shape == want.shape and np.array_equal(last, want)) else 0.0
+        parity = {"train_fixture": "tests/golden/train_en1g.npz", "merges_checked": int(want.shape[0]),
+                  "all_ranks_merges_equal_fixture": -dist.max(-ok) == 1.0}
+    # secondary: every rank trains the whole corpus on its own GPU (replicated)
+    dfull = device_buffer(lib, ctx, full)
+    rwall, rtotal, rlast, _ = timed_runs(args, lib, ctx, dist, dfull, len(full), args.vocab, 2, 1)
+    lib.gbpe_device_free(ctx, dfull)
+    rst = tr.root_stats if rank == world - 1 else None
+    sh = tr.shapes
+    line = {
+        "metric": METRIC,
+        "value": round(total / wall, 1),
+        "unit": "merges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * wall / max(1, args.steps), 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u16" if args.vocab <= 32768 else "u32",
+        "data": "synthetic (seeded Zipf English-like corpus, gpubpe.synth)",
+        "config": {"workload": f"headline: 32K-vocab BPE train on one 1,073,741,824 B English-like UTF-8 corpus "
+                               f"(seed 2) cut at word starts into {world} pieces; step = one complete training run: "
+                               "per-rank first pass (symbols, word boundaries, pair counts, word lexicon) on every "
+                               "GPU, stores to the last rank, one global lexicon, all 32,512 merges there (the merge "
+                               "chain is sequential), merge list broadcast",
+                   "train_bytes": HEADLINE["n"], "target_vocab": args.vocab,
+                   "merges_per_step": int(last.shape[0]), "parallelism": f"lexshard{world} ({dist.transport})"},
+        "roofline": {"bound": "hbm", "kernel": "see the N=1 line (the merge loop is the single-GPU one on the root)",
+                     "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None, "traffic": None},
+        "train_detail": {"timing_s_max_over_ranks": timing,
+                         "pieces": {"symbols": sh[:, 5].tolist(), "store_symbols": sh[:, 0].tolist(),
+                                    "entries": sh[:, 1].tolist(), "words": sh[:, 2].tolist(),
+                                    "zone": int(sh[-1, 4])},
+                         "amdahl": "only the first pass runs on every GPU; the merge loop (~90 % of a single-GPU "
+                                   "run at 1 GiB) stays on one: DESIGN §5"},
+        "replicated": {"value": round(rtotal / rwall, 1), "unit": "merges/s", "runs": 2,
+                       "meaning": "every rank trains the whole corpus on its own GPU (no exchange); max wall",
+                       "merges_equal_fixture": bool(want is not None and np.array_equal(rlast, want))},
+        "parity": parity,
+    }
+    if rst is not None:
+        line["train_detail"]["root"] = {"sparse_exits": int(rst.sparse_exits), "max_live_pairs": int(rst.max_live_pairs),
+                                        "lexicon_entries": int(rst.lexicon_entries)}
+    if not args.no_encode:
+        line["tokenize"] = split_encode_leg(args, lib, ctx, dist, rank, world)
+    return line
+
+
+C4_SHARD = 1 << 30   # SURVEY §8(d): 8 x 1 GiB multilingual, seed 5 + rank, 64K vocab
+
+
+def c4_line(args, lib, ctx, dist, rank, world):
+    """C4 (BASELINE configs[3]): one 64K vocabulary over the concatenation of
+    `world` multilingual shards of --c4-shard bytes (seed 5 + rank), one shard per
+    rank, re-cut at the concatenated stream's word starts (gpubpe.lexshard
+    .pieces_at_word_starts); the sharded first pass + lexicon hand-over.  No
+    oracle holds 8 GiB: the merge-list sha256 is reported, and the same code path
+    is pinned at 8 x 128 MiB by tests/test_gpu_lexshard.py's fixture test."""
+    from gpubpe.lexshard import device_word_boundary, pieces_at_word_starts
+    t = time.time()
+    shard = make_corpus({"gen": "multilingual", "n": args.c4_shard, "seed": 5 + rank})
+    piece = pieces_at_word_starts(dist.dist, shard, device_word_boundary(lib, ctx), host_group=dist.host)
+    del shard
+    log(f"[bench] rank {rank}: C4 piece {len(piece)} B in {time.time() - t:.1f}s")
+    d = device_buffer(lib, ctx, piece)
+    n = len(piece)
+    del piece
+    runs = max(1, args.c4_runs)
+    lib.gbpe_synchronize(ctx)
+    dist.barrier()
+    t0 = time.perf_counter()
+    last, tr = None, None
+    for _ in range(runs):
+        last, tr, _ = lexshard_run(lib, ctx, dist, d, n, 65536)
+    lib.gbpe_synchronize(ctx)
+    t1 = time.perf_counter()
+    dist.barrier()
+    wall = dist.max(t1 - t0) / runs
+    lib.gbpe_device_free(ctx, d)
+    timing = lex_timing(dist, tr)
+    sh = tr.shapes
+    rst = tr.root_stats if rank == world - 1 else None
+    res = {"workload": f"C4: 64K-vocab train on {world} x {args.c4_shard} B multilingual UTF-8 shards "
+                       f"(seeds 5..{4 + world}) concatenated ({int(sh[:, 5].sum())} symbols), sharded first pass + "
+                       "lexicon hand-over to the last rank",
+           "value": round(last.shape[0] / wall, 1), "unit": "merges/s", "runs": runs, "s_per_run": round(wall, 3),
+           "merges": int(last.shape[0]), "last_merge": last[-1].tolist() if last.shape[0] else [],
+           "merges_sha256": hashlib.sha256(np.ascontiguousarray(last, "<u4").tobytes()).hexdigest(),
+           "timing_s_max_over_ranks": timing, "transport": dist.transport,
+           "stream_symbols": int(sh[:, 5].sum()), "store_symbols": int(sh[:, 0].sum()), "zone": int(sh[-1, 4])}
+    if rst is not None:
+        from gpubpe import reftable
+        res["root"] = {"sparse_exits": int(rst.sparse_exits), "lexicon_entries": int(rst.lexicon_entries),
+                       "tail_dropped": int(rst.tail_dropped), "final_symbols": int(rst.symbol_count),
+                       "reference_table": reftable.report(int(rst.max_live_pairs))}
+    return res
+
+
 def replicated_line(args, lib, ctx, dist, rank, world):
     data, wall, total, last, det, parity = headline_leg(args, lib, ctx, dist)
     line = {
@@ -753,12 +925,18 @@ def main():
     ap.add_argument("--consolidate-below", type=int, default=-1,
                     help="--sharded: hand the run over to rank 0's GPU once the global stream is at most this many "
                          "symbols (-1: never)")
+    ap.add_argument("--replicated", action="store_true",
+                    help="N > 1: every rank trains the whole corpus (round-2 line) instead of the lexicon hand-over")
+    ap.add_argument("--c4-only", action="store_true",
+                    help="only the C4 leg: one multilingual shard per rank (seed 5 + rank), one 64K vocab")
+    ap.add_argument("--c4-shard", type=int, default=C4_SHARD, help="C4 shard bytes per rank")
+    ap.add_argument("--c4-runs", type=int, default=1)
     ap.add_argument("--sharded", action="store_true",
                     help="the per-merge sharded trainer (one RCCL all-gather per merge; also at N=1 as a rehearsal)")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
-    dist = Dist(world, local, force=args.sharded)
+    dist = Dist(world, local, force=args.sharded or args.c4_only)
     from gpubpe import _lib
     lib = _lib.load()
     ctx = C.c_void_p()
@@ -767,8 +945,17 @@ def main():
         raise SystemExit(f"gbpe_ctx_create failed ({rc}): no MI355X visible")
     if args.sharded:
         line = sharded_line(args, lib, ctx, dist, rank, world)
-    elif world > 1:
+    elif args.c4_only:
+        line = {"metric": METRIC, "c4": c4_line(args, lib, ctx, dist, rank, world)}
+    elif world > 1 and args.replicated:
         line = replicated_line(args, lib, ctx, dist, rank, world)
+    elif world > 1:
+        line = lexshard_line(args, lib, ctx, dist, rank, world)
+        if world == 8 and not args.no_c4:   # C4's configuration: one 1 GiB shard per GPU
+            try:
+                line["c4"] = c4_line(args, lib, ctx, dist, rank, world)
+            except Exception as e:  # noqa: BLE001
+                line["c4"] = {"error": f"{type(e).__name__}: {e}"}
     else:
         line = single_line(args, lib, ctx, dist, rank)
     if rank == 0:

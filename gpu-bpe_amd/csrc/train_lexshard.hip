@@ -149,9 +149,9 @@ int lex_root_build(gbpe_trainer* t, const S* store, const uint32_t* mul, uint64_
         GBPE_LAUNCH_CHECK(ctx);
     }
     // sectors, bitmap, signatures, store (the body is the deduplicated store)
-    const uint64_t cap = gbpe_div_up((uint64_t)lp.T + 2ull * z, t->sp_secw) + 2 * (SP_SHRINKS + 1);
+    const uint64_t cap = gbpe_div_up((uint64_t)lp.T + z / 16, t->sp_secw) + 2 * (SP_SHRINKS + 1);   // (sp_reserve grows it)
     rc = sp_alloc_layout(t, cap);
-    if (rc == GBPE_OK) rc = sp_alloc_lexicon(t, cap, z + 1);   // occurrences: the zone fronts shrinks move in
+    if (rc == GBPE_OK) rc = sp_alloc_lexicon(t, cap, z / 16 + 1024);   // occurrences: the zone fronts shrinks move in
     if (rc != GBPE_OK) return rc;
     t->lex = true;
     t->lx_len = t->lx_nocc = 0;

@@ -435,15 +435,127 @@ int sp_grow(gbpe_trainer* t, T** p, uint64_t* cap, uint64_t need) {
     return GBPE_OK;
 }
 
+// the token bitmap's rows at a new stride (bits of sectors past the old width: 0)
+__global__ void k_restride(const uint32_t* __restrict__ old, uint32_t w_old, uint32_t* __restrict__ nb, uint32_t w_new,
+                           uint64_t rows) {
+    const uint64_t tot = rows * w_new;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = i / w_new, w = i % w_new;
+        nb[i] = w < w_old ? old[r * w_old + w] : 0u;
+    }
+}
+
+// grow-and-copy a device array to `want` elements (the first `keep` kept)
+template <typename T>
+int sp_regrow(gbpe_trainer* t, T** p, uint64_t* cap, uint64_t want, uint64_t keep) {
+    if (*p && *cap >= want) return GBPE_OK;
+    T* nb = nullptr;
+    if (hipMalloc((void**)&nb, want * sizeof(T)) != hipSuccess)
+        return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sparse layout growth, %llu B) failed",
+                              (unsigned long long)(want * sizeof(T)));
+    hipStream_t s = t->ctx->stream;
+    if (*p && keep) TR_HIP(t, hipMemcpyAsync(nb, *p, keep * sizeof(T), hipMemcpyDeviceToDevice, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    hipFree(*p);
+    *p = nb;
+    *cap = want;
+    return GBPE_OK;
+}
+
+// Room for `need_sec` sectors, `need_store` lexicon store symbols and `need_occ`
+// occurrences, growing by >= 1.5x with the contents kept (the token bitmap
+// re-strided): the layout starts near its first build's size instead of the
+// worst case of every zone shrink (C4's hand-over root: 64 GB of bitmap)
+int sp_reserve(gbpe_trainer* t, uint64_t need_sec, uint64_t need_store, uint64_t need_occ) {
+    hipStream_t s = t->ctx->stream;
+    if (need_sec > t->nsec_cap || need_sec > (uint64_t)t->W * 32 || need_sec * SP_SIGW > t->sig_cap ||
+        need_sec > t->loc_cap) {
+        uint64_t cap = std::max<uint64_t>(need_sec, t->nsec_cap + t->nsec_cap / 2);
+        cap = (cap + 31) & ~31ull;
+        const uint64_t keep = t->nsec;
+        int rc = sp_regrow(t, &t->sec, &t->nsec_cap, cap, keep);
+        if (rc == GBPE_OK) rc = sp_regrow(t, &t->sig, &t->sig_cap, cap * SP_SIGW, keep * SP_SIGW);
+        if (rc == GBPE_OK && t->lx_w0) {
+            uint64_t wcap = 0;   // (allocated with the sector capacity)
+            rc = sp_regrow(t, &t->lx_w0, &wcap, cap, keep);
+        }
+        if (rc != GBPE_OK) return rc;
+        if (keep * SP_SIGW < cap * SP_SIGW)
+            TR_HIP(t, hipMemsetAsync(t->sig + keep * SP_SIGW, 0, (cap - keep) * SP_SIGW * 4, s));
+        hipFree(t->sp_loc);
+        hipFree(t->sp_blk);
+        t->sp_loc = nullptr;
+        t->sp_blk = nullptr;
+        t->loc_cap = 0;
+        if (hipMalloc(&t->sp_loc, cap * 4) != hipSuccess ||
+            hipMalloc(&t->sp_blk, (gbpe_div_up(cap, SCAN_BLK) + 1) * 8) != hipSuccess)
+            return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sector scratch) failed");
+        t->loc_cap = cap;
+        const uint32_t w_new = (uint32_t)gbpe_div_up(cap, 32);
+        if (w_new > t->W || !t->bits) {
+            uint32_t* nb = nullptr;
+            const uint64_t words = (uint64_t)t->max_id * w_new;
+            if (hipMalloc(&nb, words * 4) != hipSuccess)
+                return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(token bitmap, %llu B) failed",
+                                      (unsigned long long)(words * 4));
+            if (t->bits && t->W)
+                hipLaunchKernelGGL(k_restride, dim3(grid_persistent(t->ctx, gbpe_div_up(words, 256), 8)), dim3(256), 0, s,
+                                   (const uint32_t*)t->bits, t->W, nb, w_new, (uint64_t)t->max_id);
+            else
+                TR_HIP(t, hipMemsetAsync(nb, 0, words * 4, s));
+            GBPE_LAUNCH_CHECK(t->ctx);
+            TR_HIP(t, hipStreamSynchronize(s));
+            hipFree(t->bits);
+            t->bits = nb;
+            t->bits_cap = words;
+            t->W = w_new;
+        }
+        const uint64_t wneed = gbpe_div_up(w_new, SP_WPW_MIN) + 2;   // one byte counter per k_body workgroup
+        if (t->wg_bytes && wneed > t->wg_cap) {
+            uint64_t* nb = nullptr;
+            TR_HIP(t, hipMalloc(&nb, wneed * sizeof(uint64_t)));
+            TR_HIP(t, hipMemsetAsync(nb, 0, wneed * sizeof(uint64_t), s));
+            TR_HIP(t, hipMemcpyAsync(nb, t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+            TR_HIP(t, hipStreamSynchronize(s));
+            hipFree(t->wg_bytes);
+            t->wg_bytes = nb;
+            t->wg_cap = wneed;
+        }
+    }
+    if (t->lx_store && need_store > t->lx_cap) {
+        const uint64_t want = std::max<uint64_t>(need_store, t->lx_cap + t->lx_cap / 2);
+        uint64_t c1 = t->lx_cap, c2 = t->lx_cap;
+        void* st = t->lx_store;
+        if (hipMalloc(&t->lx_store, want * t->bps) != hipSuccess) {
+            t->lx_store = st;
+            return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(word lexicon growth) failed");
+        }
+        TR_HIP(t, hipMemcpyAsync(t->lx_store, st, t->lx_len * t->bps, hipMemcpyDeviceToDevice, s));
+        TR_HIP(t, hipStreamSynchronize(s));
+        hipFree(st);
+        int rc = sp_regrow(t, &t->lx_mul, &c1, want, t->lx_len);
+        if (rc != GBPE_OK) return rc;
+        (void)c2;
+        t->lx_cap = want;
+    }
+    if (t->lx_occ && need_occ > t->lx_occ_cap) {
+        const uint64_t want = std::max<uint64_t>(need_occ, t->lx_occ_cap + t->lx_occ_cap / 2);
+        int rc = sp_regrow(t, &t->lx_occ, &t->lx_occ_cap, want, t->lx_nocc);
+        if (rc != GBPE_OK) return rc;
+    }
+    return GBPE_OK;
+}
+
 // sectors over body positions [base, base + len) appended after sector t->nsec
 // (their token bits and signatures too); base is a word start
 template <typename S>
 int sp_add_sectors(gbpe_trainer* t, uint32_t base, uint32_t len) {
     hipStream_t s = t->ctx->stream;
     const uint32_t nw = (uint32_t)gbpe_div_up(len, t->sp_secw);
-    if ((uint64_t)t->nsec + nw > t->nsec_cap || (uint64_t)t->nsec + nw > (uint64_t)t->W * 32 ||
-        ((uint64_t)t->nsec + nw) * SP_SIGW > t->sig_cap || nw > t->loc_cap)
-        return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "sector capacity exceeded");
+    {
+        int rc = sp_reserve(t, (uint64_t)t->nsec + nw, 0, 0);
+        if (rc != GBPE_OK) return rc;
+    }
     const S* body = (const S*)t->buf[t->bcur];
     hipLaunchKernelGGL(k_sp_sectors<S>, dim3((uint32_t)gbpe_div_up(nw, TPB / 64)), dim3(TPB), 0, s, body, base, len,
                        t->sp_secw, t->sp_loc, nw);
@@ -638,10 +750,9 @@ int lx_commit(gbpe_trainer* t, LxPlan& lp, const S* seg, bool fresh, bool keep_o
     const uint64_t sbase = gbpe_div_up(t->lx_len, SEC) * SEC;
     const uint64_t nwin = gbpe_div_up(lp.T ? lp.T : 1, SEC);
     const uint64_t kb = sbase / SEC;
-    if (sbase + nwin * SEC > t->lx_cap || kb + nwin > t->nsec_cap || kb + nwin > (uint64_t)t->W * 32 ||
-        (kb + nwin) * SP_SIGW > t->sig_cap || nwin > t->loc_cap || (keep_occ && t->lx_nocc + lp.nw > t->lx_occ_cap)) {
-        lp.ok = false;
-        return GBPE_OK;
+    {
+        int rc = sp_reserve(t, kb + nwin, sbase + nwin * SEC, keep_occ ? t->lx_nocc + lp.nw : 0);
+        if (rc != GBPE_OK) return rc;
     }
     S* store = (S*)t->lx_store;
     if (sbase > t->lx_len) {   // alignment padding: separators no sector covers
@@ -906,16 +1017,16 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
         if (lp.ok) ++t->lx_builds;
         else ++t->lx_fallbacks;
     }
-    // capacities for every sector the body can ever hold: windows over [0, n) (the
-    // lexicon: over its store, and twice the zone for the words shrinks append) plus
-    // one partial window per zone shrink (at most SP_SHRINKS per entry)
-    const uint64_t cap = lp.ok ? gbpe_div_up((uint64_t)lp.T + 2ull * z, t->sp_secw) + 2 * (SP_SHRINKS + 1)
+    // sector capacity: windows over [0, n) (the lexicon: over its store, with room
+    // for a 16th of the zone's symbols as the words shrinks append; sp_reserve grows
+    // it) plus one partial window per zone shrink (at most SP_SHRINKS per entry)
+    const uint64_t cap = lp.ok ? gbpe_div_up((uint64_t)lp.T + z / 16, t->sp_secw) + 2 * (SP_SHRINKS + 1)
                                : gbpe_div_up(n, t->sp_secw) + SP_SHRINKS + 1;
     int rc = sp_alloc_layout(t, cap);
     if (rc != GBPE_OK) return rc;
     t->bcur = t->cur;
     if (lp.ok) {
-        rc = sp_alloc_lexicon(t, cap, (uint64_t)lp.nw + z + 1);
+        rc = sp_alloc_lexicon(t, cap, (uint64_t)lp.nw + z / 16 + 1024);
         if (rc != GBPE_OK) return rc;
         t->lex = true;
         rc = lx_commit<S>(t, lp, cur, true);

@@ -164,6 +164,9 @@ class GpuLexBackend:
         self._check(self.lib.gbpe_lexshard_release(self.ls), "lexshard_release")
 
     def remap(self, map_bytes, n_map: int):
+        if hasattr(map_bytes, "is_cuda") and map_bytes.is_cuda:
+            import torch
+            torch.cuda.current_stream().synchronize()   # received on torch's stream; read on the library's
         p, d = _ptr(map_bytes)
         self._check(self.lib.gbpe_lexshard_remap(self.ls, p, n_map, d), "lexshard_remap")
 
