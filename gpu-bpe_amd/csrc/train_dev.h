@@ -897,7 +897,9 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
 template <typename S, bool EXACT, int DELTA_TPW>
 __global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, const S* cur, Table tb,
                                                   uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
-                                                  uint32_t* __restrict__ grpsum, uint32_t eager_tiles, uint32_t ngroups) {
+                                                  uint32_t* __restrict__ grpsum, uint32_t eager_tiles, uint32_t ngroups,
+                                                  uint32_t first_block = 0) {
+    if (blockIdx.x < first_block) return;   // (GBPE_SPLIT_TAIL diagnostic launches: tiles and tail apart)
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     __shared__ LdsTab<LTAB_Z> lt;
     __shared__ uint32_t red[TPB / 64];
@@ -1042,7 +1044,9 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
                                                  const uint32_t* __restrict__ hitmask,
                                                  const uint32_t* __restrict__ tile_cnt,
                                                  const uint32_t* __restrict__ grpsum, Table tb,
-                                                 const S* __restrict__ win = nullptr, const DevState* gst = nullptr) {
+                                                 const S* __restrict__ win = nullptr, const DevState* gst = nullptr,
+                                                 uint32_t first_block = 0) {
+    if (blockIdx.x < first_block) return;   // (GBPE_SPLIT_TAIL diagnostic launches: tiles and window apart)
     // one LDS arena: the compaction stage of tile blocks or the delta table of tail blocks
     constexpr int STAGE = (TILE + 16) * sizeof(S);
     constexpr int ARENA = (sizeof(LdsTab<LTAB>) > STAGE ? sizeof(LdsTab<LTAB>) : STAGE) / 16;

@@ -284,7 +284,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
         if (mt)
             hipLaunchKernelGGL(tpw == 32 ? (k_delta_mt<S, true, 32>) : tpw == 16 ? (k_delta_mt<S, true, 16>) : (k_delta_mt<S, true, 8>),
                                dim3(g_mt + g_mtail), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask,
-                               t->tile_cnt, t->grpsum, g_delta, g_mt);
+                               t->tile_cnt, t->grpsum, g_delta, g_mt, 0u);
         else
             hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
                                t->hitmask, t->tile_cnt, t->grpsum, g_delta, 0xFFFFFFFFu);
@@ -295,7 +295,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
         if (mt)
             hipLaunchKernelGGL(tpw == 32 ? (k_delta_mt<S, false, 32>) : tpw == 16 ? (k_delta_mt<S, false, 16>) : (k_delta_mt<S, false, 8>),
                                dim3(g_mt + g_mtail), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask,
-                               t->tile_cnt, t->grpsum, g_delta, g_mt);
+                               t->tile_cnt, t->grpsum, g_delta, g_mt, 0u);
         else
             hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta + g_dtail), dim3(TPB), 0, s, t->st, round, (const S*)cur,
                                t->tb, t->hitmask, t->tile_cnt, t->grpsum, g_delta, g_delta);
@@ -392,6 +392,14 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
         if (exact && mt)
             hipLaunchKernelGGL((k_delta_mt<S, true, 8>), dim3(g_mt), dim3(TPB), 0, s, t->zst, round, (const S*)zc, t->tb,
                                t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt);
+#ifdef GBPE_SPLIT_TAIL   // diagnostic build: the stale-tail blocks as a launch of their own (rocprof splits them)
+        else if (mt) {
+            hipLaunchKernelGGL((k_delta_mt<S, false, 8>), dim3(g_mt), dim3(TPB), 0, s, t->zst, round,
+                               (const S*)zc, t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt, 0u);
+            hipLaunchKernelGGL((k_delta_mt<S, false, 8>), dim3(g_mt + g.ztail), dim3(TPB), 0, s, t->zst, round,
+                               (const S*)zc, t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt, g_mt);
+        }
+#endif
         else if (mt)
             hipLaunchKernelGGL((k_delta_mt<S, false, 8>), dim3(g_mt + g.ztail), dim3(TPB), 0, s, t->zst, round,
                                (const S*)zc, t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt);
@@ -407,10 +415,22 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
             hipLaunchKernelGGL((k_compact<S, true, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
                                (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
                                t->tb, (const S*)t->wtmp, (const DevState*)t->st);
+#ifdef GBPE_SPLIT_TAIL
+        else {
+            const uint32_t zt_ = g.zdelta;   // zone tiles (the window blocks follow them)
+            hipLaunchKernelGGL((k_compact<S, false, true>), dim3(zt_), dim3(CTPB), 0, s, t->zst, round, zc, zo,
+                               (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
+                               t->tb, (const S*)t->wtmp, (const DevState*)t->st, 0u);
+            hipLaunchKernelGGL((k_compact<S, false, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
+                               (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
+                               t->tb, (const S*)t->wtmp, (const DevState*)t->st, zt_);
+        }
+#else
         else
             hipLaunchKernelGGL((k_compact<S, false, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
                                (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
                                t->tb, (const S*)t->wtmp, (const DevState*)t->st);
+#endif
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,

@@ -1,11 +1,13 @@
-# Build libgpubpe.so from train.hip at git revision $1 (or "work" = the working
-# tree) into gpu-bpe_amd/lib/$2/, with extra compiler flags $3 (e.g. -DGBPE_KTRACE);
-# the other objects come from the working tree's build/.  For A/B runs via GBPE_LIB.
+# Build libgpubpe.so with extra compiler flags $2 (e.g. -DGBPE_KTRACE, -DGBPE_SPLIT_TAIL)
+# into gpu-bpe_amd/lib/$1/, from the working tree (the training units recompiled,
+# the other objects from build/).  For A/B runs via GBPE_LIB.
 set -e
 cd "$(dirname "$0")/../gpu-bpe_amd"
-mkdir -p build/$2 lib/$2
-if [ "$1" = work ]; then cp csrc/train.hip build/$2/train.hip; else git show "$1":gpu-bpe_amd/csrc/train.hip > build/$2/train.hip; fi
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $3 -Icsrc -I../include -c build/$2/train.hip -o build/$2/train.o
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 build/api.o build/$2/train.o build/encode.o build/pretok.o \
-  build/host_io.o build/merge_encode.o -o lib/$2/libgpubpe.so
-echo "lib/$2/libgpubpe.so"
+mkdir -p build/$1 lib/$1
+for u in train train_shard train_lexshard; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $2 -Icsrc -I../include -c csrc/$u.hip -o build/$1/$u.o &
+done
+wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 build/api.o build/$1/train.o build/$1/train_shard.o \
+  build/$1/train_lexshard.o build/encode.o build/pretok.o build/host_io.o build/merge_encode.o -o lib/$1/libgpubpe.so
+echo "lib/$1/libgpubpe.so"
