@@ -1045,8 +1045,8 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
                                                  const uint32_t* __restrict__ tile_cnt,
                                                  const uint32_t* __restrict__ grpsum, Table tb,
                                                  const S* __restrict__ win = nullptr, const DevState* gst = nullptr,
-                                                 uint32_t first_block = 0) {
-    if (blockIdx.x < first_block) return;   // (GBPE_SPLIT_TAIL diagnostic launches: tiles and window apart)
+                                                 uint32_t split = 0) {
+    // split (GBPE_SPLIT_TAIL diagnostic launches): 1 = tile blocks only, 2 = every block a window block
     // one LDS arena: the compaction stage of tile blocks or the delta table of tail blocks
     constexpr int STAGE = (TILE + 16) * sizeof(S);
     constexpr int ARENA = (sizeof(LdsTab<LTAB>) > STAGE ? sizeof(LdsTab<LTAB>) : STAGE) / 16;
@@ -1061,7 +1061,8 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
     const uint32_t n = st->n, new_n = st->new_n, nw = st->nw;
     const uint32_t limit = EXACT ? n : new_n;
     const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
-    if (tl >= ntiles) {
+    if (split == 1 && tl >= ntiles) return;
+    if (tl >= ntiles || split == 2) {
         if (EXACT || st->sharded) return;   // sharded: the window is handled by k_shard_recv
         // ── stale tail window ──
         const uint32_t m = st->m;
@@ -1070,7 +1071,7 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
         __shared__ uint32_t left_val;
         lds_clear(lt);
         uint32_t lo = new_n - m;
-        const uint32_t tb0 = tl - ntiles, ntb = gridDim.x - ntiles;
+        const uint32_t tb0 = split == 2 ? tl : tl - ntiles, ntb = split == 2 ? gridDim.x : gridDim.x - ntiles;
         uint32_t woff = 0;
         if (ZONE) {   // window start = zone survivors - m (the group sums hold the survivors)
             __shared__ uint32_t s_surv[CTPB / 64];

@@ -420,10 +420,10 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
             const uint32_t zt_ = g.zdelta;   // zone tiles (the window blocks follow them)
             hipLaunchKernelGGL((k_compact<S, false, true>), dim3(zt_), dim3(CTPB), 0, s, t->zst, round, zc, zo,
                                (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
-                               t->tb, (const S*)t->wtmp, (const DevState*)t->st, 0u);
-            hipLaunchKernelGGL((k_compact<S, false, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
-                               (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
-                               t->tb, (const S*)t->wtmp, (const DevState*)t->st, zt_);
+                               t->tb, (const S*)t->wtmp, (const DevState*)t->st, 1u);
+            hipLaunchKernelGGL((k_compact<S, false, true>), dim3(g.zcompact - zt_), dim3(CTPB), 0, s, t->zst, round, zc,
+                               zo, (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
+                               t->tb, (const S*)t->wtmp, (const DevState*)t->st, 2u);
         }
 #else
         else
