@@ -81,14 +81,18 @@ def test_known_answers(eng):
     import json, os
     ka = json.load(open(os.path.join(GOLDEN, "known_answers.json")))
     for c in ka["train"]:
+        nid = c.get("next_token_id", 256)
         for exact in (False, True):
-            m, s, pairs, _ = _train_native(eng, _text(c), c["target"], exact=exact)
-            want = c["merges_exact"] if exact and "merges_exact" in c else c["merges"]
-            assert m == want, (c["name"], exact)
-            key = "final_stream_exact" if exact else "final_stream"
-            if key in c:
-                assert s.tolist() == c[key], (c["name"], exact)
-            _assert_counts_match_stream(pairs, s)
+            for batch in [128] + c.get("batches", []):   # small batches: the odd-batch ping-pong swap
+                m, s, pairs, st = _train_native(eng, _text(c), c["target"], exact=exact, batch=batch, next_id=nid)
+                want = c["merges_exact"] if exact and "merges_exact" in c else c["merges"]
+                assert m == want, (c["name"], exact, batch)
+                if "early_stop" in c:
+                    assert bool(st.early_stop) == c["early_stop"], (c["name"], exact, batch)
+                key = "final_stream_exact" if exact else "final_stream"
+                if key in c:
+                    assert s.tolist() == c[key], (c["name"], exact, batch)
+                _assert_counts_match_stream(pairs, s)
 
 
 @pytest.mark.parametrize("kind,size,target", [("english", 65536, 1024), ("multilingual", 65536, 700),

@@ -75,13 +75,14 @@ def test_survey_trie_shape(ref):
 
 def test_train_known_answers(ka):
     for c in ka["train"]:
-        r = O.train(_text(c), c["target"])
+        nid = c.get("next_token_id", 256)
+        r = O.train(_text(c), c["target"], next_token_id=nid)
         assert [m for m in r["merges"]] == c["merges"], c["name"]
         if "early_stop" in c:
             assert r["early_stop"] == c["early_stop"], c["name"]
         if "final_stream" in c:
             assert r["symbols"].tolist() == c["final_stream"], c["name"]
-        rx = O.train(_text(c), c["target"], compaction="exact")
+        rx = O.train(_text(c), c["target"], compaction="exact", next_token_id=nid)
         if "merges_exact" in c:
             assert rx["merges"] == c["merges_exact"], c["name"]
         if "final_stream_exact" in c:
@@ -223,7 +224,8 @@ def test_c_oracle_matches_numpy_oracle():
 def test_c_oracle_known_answers(ka):
     import cpu_ref
     for c in ka["train"]:
-        r = cpu_ref.train(_text(c), c["target"], threads=2)
+        nid = c.get("next_token_id", 256)
+        r = cpu_ref.train(_text(c), c["target"], threads=2, next_token_id=nid)
         assert r["merges"] == c["merges"], c["name"]
         if "final_stream" in c:
             assert r["symbols"].tolist() == c["final_stream"], c["name"]
