@@ -714,6 +714,9 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->d_u32);
     hipFree(t->part);
     hipFree(t->zseg);
+    hipFree(t->zdr_out);
+    hipFree(t->zdr_offs);
+    hipFree(t->zdr_flag);
     hipFree(t->wg_bytes);
     hipFree(t->lx_store);
     hipFree(t->lx_mul);

@@ -715,6 +715,84 @@ __device__ __forceinline__ uint32_t lane_mask32(uint64_t i0, uint64_t lim) {
     return i0 >= lim ? 0u : (i0 + 32 <= lim ? 0xFFFFFFFFu : ((1u << (uint32_t)(lim - i0)) - 1u));
 }
 
+// ── two-stage delta reduction of the multi-tile zone passes ─────────────────
+// Early merges (zones of 10^6-10^8 symbols) produce their count deltas in
+// thousands of workgroups, each holding thousands of distinct pairs in its LDS
+// table; flushing every table into the global table was most of an early
+// merge's time (a diagnostic build without the stale-tail flush: 250 -> 33 us per
+// merge at merges 10-18, 1 GiB): the same hot pairs, one contended global atomic
+// per pair per workgroup.  Instead each workgroup DUMPS its table, partitioned
+// by pair hash into ZDR_P buckets (plain stores, no atomics), and k_zdr — one
+// workgroup per bucket — aggregates its bucket of every dump in LDS and adds each
+// distinct pair to the global table once.
+constexpr uint32_t ZDR_P = 256;          // hash buckets = k_zdr workgroups
+constexpr int ZDR_N_TILE = LTAB_Z;       // dump capacity of a zone tile workgroup (its LDS table)
+constexpr int ZDR_N_CHURN = 8192;        // ... of a k_churn workgroup
+constexpr int ZDR_R = 4096;              // k_zdr's LDS table
+__device__ __forceinline__ uint32_t zdr_part(uint32_t pid) { return gbpe_fmix32(pid ^ 0x85EBCA6Bu) >> 24; }
+
+struct ZdrView {                 // where stage-1 workgroup w writes (host-sized); out == null: flush instead
+    uint2* out = nullptr;        // entries: w < ntile ? w * ZDR_N_TILE : ntile * ZDR_N_TILE + (w - ntile) * ZDR_N_CHURN
+    uint32_t* offs = nullptr;    // (ZDR_P + 1) bucket offsets per workgroup
+    uint32_t* flag = nullptr;    // = tag when workgroup w dumped this merge
+    uint32_t ntile = 0;          // tile workgroups before the churn workgroups
+    uint32_t tag = 0;            // unique per merge
+};
+__device__ __forceinline__ uint64_t zdr_base(const ZdrView& z, uint32_t w) {
+    return w < z.ntile ? (uint64_t)w * ZDR_N_TILE
+                       : (uint64_t)z.ntile * ZDR_N_TILE + (uint64_t)(w - z.ntile) * ZDR_N_CHURN;
+}
+
+// stage 1: workgroup w's LDS table (its live entries) to its dump, bucket by bucket
+template <int N>
+__device__ void lds_dump(LdsTab<N>& t, const ZdrView& z, uint32_t w) {
+    __shared__ uint32_t s_cnt[ZDR_P];
+    __shared__ uint32_t s_tot;
+    const uint32_t nt = blockDim.x, tid = threadIdx.x;
+    __syncthreads();   // every lds_add of the table is done
+    for (uint32_t p = tid; p < ZDR_P; p += nt) s_cnt[p] = 0u;
+    __syncthreads();
+    for (uint32_t i = tid; i < (uint32_t)N; i += nt) {
+        const uint32_t k = t.key[i];
+        if (k && t.val[i]) atomicAdd(&s_cnt[zdr_part(k)], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {   // exclusive scan of the bucket counts by one wave (4 per lane)
+        uint32_t c[ZDR_P / 64], sum = 0;
+#pragma unroll
+        for (int q = 0; q < (int)(ZDR_P / 64); ++q) {
+            c[q] = s_cnt[tid * (ZDR_P / 64) + q];
+            sum += c[q];
+        }
+        uint32_t incl = sum;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off);
+            if ((int)tid >= off) incl += o;
+        }
+        uint32_t run = incl - sum;
+        uint32_t* offs = z.offs + (uint64_t)w * (ZDR_P + 1);
+#pragma unroll
+        for (int q = 0; q < (int)(ZDR_P / 64); ++q) {
+            const uint32_t p = tid * (ZDR_P / 64) + q;
+            s_cnt[p] = run;
+            offs[p] = run;
+            run += c[q];
+        }
+        if (tid == 63) {
+            offs[ZDR_P] = run;
+            s_tot = run;
+        }
+    }
+    __syncthreads();
+    if (s_tot == 0u) return;   // (block-uniform) nothing to dump: the flag stays stale
+    uint2* out = z.out + zdr_base(z, w);
+    for (uint32_t i = tid; i < (uint32_t)N; i += nt) {
+        const uint32_t k = t.key[i], v = t.val[i];
+        if (k && v) out[atomicAdd(&s_cnt[zdr_part(k)], 1u)] = make_uint2(k, v);
+    }
+    if (tid == 0) z.flag[w] = z.tag;   // (read by k_zdr, a later launch)
+}
+
 // Pass 1 (one tile of TILE symbols per workgroup): merge-site mask, survivor
 // count per tile, count deltas.
 //   hit(i)  = (i >= 1) && !ws(i) && tok(i-1) == a && tok(i) == b     (B-side, train.wgsl:491-497)
@@ -732,7 +810,7 @@ template <typename S, bool EXACT, bool STAGE = false>
 __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, const S* cur, Table tb,
                                                uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
                                                uint32_t* __restrict__ grpsum, uint32_t eager_tiles,
-                                               uint32_t ngroups = 0xFFFFFFFFu) {
+                                               uint32_t ngroups = 0xFFFFFFFFu, ZdrView zv = ZdrView()) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     __shared__ LdsTab<STAGE ? LTAB_Z : LTAB_T> lt;
     __shared__ uint32_t stg[STAGE ? EPT * TPB : 1];
@@ -757,9 +835,15 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
             const uint32_t xi = cur[i];
             if (xi & WS) continue;
             const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
+#if defined(GBPE_DIAG_TAIL) && GBPE_DIAG_TAIL >= 2   // diagnostic builds only (wrong counts): loads alone
+            if (tp && ti && ((tp << 16) | ti) == 0xFFFFFFFFu) lt.ovf = 1u;
+#else
             if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+#endif
         }
+#ifndef GBPE_DIAG_TAIL   // (GBPE_DIAG_TAIL=1: no flush)
         lds_flush(lt, tb, st);
+#endif
         return;
     }
     // tiles past the host's view of the stream (a shard that may have grown by an
@@ -876,7 +960,8 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
                 if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
             }
         }
-        lds_flush(lt, tb, st);
+        if (zv.out) lds_dump(lt, zv, tl);   // multi-tile zone pass: k_zdr adds the deltas
+        else lds_flush(lt, tb, st);
         for (int off = 32; off > 0; off >>= 1) tail += __shfl_xor(tail, off);
         if (lane == 0 && tail) atomicAdd(&st->m, tail);
     }
@@ -898,7 +983,7 @@ template <typename S, bool EXACT, int DELTA_TPW>
 __global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, const S* cur, Table tb,
                                                   uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
                                                   uint32_t* __restrict__ grpsum, uint32_t eager_tiles, uint32_t ngroups,
-                                                  uint32_t first_block = 0) {
+                                                  uint32_t first_block = 0, ZdrView zv = ZdrView()) {
     if (blockIdx.x < first_block) return;   // (GBPE_SPLIT_TAIL diagnostic launches: tiles and tail apart)
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     __shared__ LdsTab<LTAB_Z> lt;
@@ -930,9 +1015,15 @@ __global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, 
             const uint32_t xi = cur[i];
             if (xi & WS) continue;
             const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
+#if defined(GBPE_DIAG_TAIL) && GBPE_DIAG_TAIL >= 2   // diagnostic builds only (wrong counts): loads alone
+            if (tp && ti && ((tp << 16) | ti) == 0xFFFFFFFFu) lt.ovf = 1u;
+#else
             if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+#endif
         }
+#ifndef GBPE_DIAG_TAIL   // (GBPE_DIAG_TAIL=1: no flush)
         lds_flush(lt, tb, st);
+#endif
         return;
     }
     uint32_t tail = 0;
@@ -1009,7 +1100,8 @@ __global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, 
         }
         __syncthreads();   // red[] is rewritten by the next tile
     }
-    lds_flush(lt, tb, st);
+    if (zv.out) lds_dump(lt, zv, blockIdx.x);   // multi-tile zone pass: k_zdr adds the deltas
+    else lds_flush(lt, tb, st);
     for (int off = 32; off > 0; off >>= 1) tail += __shfl_xor(tail, off);
     if (lane == 0 && tail) atomicAdd(&st->m, tail);
 }
@@ -1214,6 +1306,116 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
     if (t == 0 && nvec * VE < end) {
         for (uint32_t j = (nvec * VE > ph ? nvec * VE : ph); j < end; ++j) dst[j] = stage[j];   // partial tail word
     }
+}
+
+// stage 2: bucket p of every dump of this merge, aggregated, into the global table
+__global__ __launch_bounds__(TPB) void k_zdr(ZdrView z, uint32_t nd, Table tb, DevState* st, uint32_t round) {
+    __shared__ LdsTab<ZDR_R> lt;
+    if (!merge_active(st, round)) return;
+    lds_clear(lt);
+    __syncthreads();
+    const uint32_t p = blockIdx.x;
+    for (uint32_t w = threadIdx.x; w < nd; w += TPB) {
+        if (z.flag[w] != z.tag) continue;
+        const uint32_t* offs = z.offs + (uint64_t)w * (ZDR_P + 1);
+        const uint32_t b = offs[p], e = offs[p + 1];
+        const uint2* in = z.out + zdr_base(z, w);
+        for (uint32_t j = b; j < e; ++j) {
+            const uint2 v = in[j];
+            lds_add(lt, tb, st, v.x, v.y);
+        }
+    }
+    lds_flush(lt, tb, st);
+}
+
+// The stale churn of a multi-tile zone pass, after k_compact's tiles (which
+// rewrote the zone's A-sides in place and placed the kept survivors):
+//   * the stale window [lo, lo + m): the window source (wtmp, copied by k_body)
+//     stored at its place and its pairs added — k_compact's window blocks;
+//   * the stale tail [new_n, n): every old pair there destroyed — k_delta's tail
+//     blocks — from the snapshot: a symbol rewritten as an A-side (hit at the
+//     next position, hitmask) held `a`.
+// Both in one workgroup's LDS table (a pair the tail drops and the window adds
+// is one entry), dumped for k_zdr.
+constexpr int CH_BT = 512;
+template <typename S>
+__global__ __launch_bounds__(CH_BT) void k_churn(DevState* zst, uint32_t round, S* __restrict__ cur,
+                                                 S* __restrict__ oth, const uint32_t* __restrict__ hitmask,
+                                                 const uint32_t* __restrict__ grpsum, const S* __restrict__ win,
+                                                 Table tb, ZdrView zv, uint32_t wbase) {
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    __shared__ LdsTab<ZDR_N_CHURN> lt;
+    __shared__ uint32_t s_surv[CH_BT / 64], s_left;
+    DevState* st = zst;
+    if (!merge_active(st, round)) return;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t n = st->n, new_n = st->new_n, m = st->m, mc = st->mc, a = st->a, b = st->b;
+    const uint32_t pid_ab = (a << 16) | b;
+    const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
+    lds_clear(lt);
+    // window start = zone survivors - m (the group sums hold the survivors)
+    {
+        const uint32_t ngrp = (uint32_t)gbpe_div_up(ntiles, GRP);
+        uint32_t sv = 0;
+        for (uint32_t g = t; g < ngrp; g += CH_BT) sv += grpsum[g * GSTR];
+        for (int off = 32; off > 0; off >>= 1) sv += __shfl_xor(sv, off);
+        if (lane == 0) s_surv[wid] = sv;
+    }
+    __syncthreads();
+    uint32_t sv = 0;
+    for (int w2 = 0; w2 < CH_BT / 64; ++w2) sv += s_surv[w2];
+    const uint32_t lo = sv - m, woff = mc - m;
+    const uint32_t G = gridDim.x, q = blockIdx.x;
+    // this workgroup's window slice [w0, w1) and tail slice [t0, t1)
+    const uint32_t wper = (m + G - 1) / G, w0 = lo + (q * wper < m ? q * wper : m),
+                   w1 = lo + ((q + 1) * wper < m ? (q + 1) * wper : m);
+    const uint32_t tlen = n > new_n ? n - new_n : 0u, tper = (tlen + G - 1) / G;
+    const uint32_t t0 = new_n + (q * tper < tlen ? q * tper : tlen), t1 = new_n + ((q + 1) * tper < tlen ? (q + 1) * tper : tlen);
+    if (w0 < w1 && wid == 0) {   // the symbol left of this slice: the survivor before the window, or the window itself
+        uint32_t v = 0;
+        if (w0 > lo) {
+            v = win[woff + (w0 - lo) - 1];
+        } else if (lo >= 1) {
+            // the last survivor below new_n (k_compact's rule): last j < new_n with hit(j) == 0, A-side rewritten
+            int64_t wi = (int64_t)(new_n - 1) / 32;
+            uint32_t found = 0xFFFFFFFFu;
+            while (wi >= 0 && found == 0xFFFFFFFFu) {
+                const int64_t mywi = wi - lane;
+                uint32_t inv = 0;
+                if (mywi >= 0) inv = ~hitmask[mywi] & lane_mask32((uint64_t)mywi * 32, new_n);
+                const unsigned long long has = __ballot(inv != 0u);
+                if (has) {
+                    const int l = __ffsll((long long)has) - 1;
+                    const uint32_t inv_l = __shfl(inv, l);
+                    found = (uint32_t)((wi - l) * 32 + (31 - __clz(inv_l)));
+                }
+                wi -= 64;
+            }
+            if (found != 0xFFFFFFFFu) v = cur[found];   // (its in-place A-side rewrite, if any, is done)
+        }
+        if (lane == 0) s_left = v;
+    }
+    __syncthreads();
+    for (uint32_t d = w0 + t; d < w1; d += CH_BT) {
+        if (d == 0) continue;
+        const uint32_t x1 = win[woff + (d - lo)];
+        const uint32_t x0 = d == w0 ? s_left : (uint32_t)win[woff + (d - lo) - 1];
+        oth[d] = (S)x1;
+        const uint32_t u0 = x0 & TM, u1 = x1 & TM;
+        if (!(x1 & WS) && u0 && u1) lds_add(lt, tb, st, (u0 << 16) | u1, 1u);
+    }
+    for (uint32_t i = t0 + t; i < t1; i += CH_BT) {
+        if (i == 0) continue;
+        // snapshot values: an A-side (hit at the next position) was rewritten to nw in place
+        const uint32_t j1 = i + 1, jp = i;
+        uint32_t xi = cur[i], xp = cur[i - 1];
+        if (j1 < n && ((hitmask[j1 / 32] >> (j1 % 32)) & 1u)) xi = a | (xi & WS);
+        if ((hitmask[jp / 32] >> (jp % 32)) & 1u) xp = a | (xp & WS);
+        if (xi & WS) continue;
+        const uint32_t tp = xp & TM, ti = xi & TM;
+        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+    }
+    lds_dump(lt, zv, wbase + q);
 }
 
 __global__ void k_clear_dirty_all(DevState* st, Table tb) {

@@ -76,6 +76,11 @@ struct gbpe_trainer {
     DevState* h_zst = nullptr;   // pinned
     uint32_t* d_u32 = nullptr;   // small device scratch
     uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
+    uint2* zdr_out = nullptr;    // the multi-tile zone passes' delta dumps (ZdrView, train_dev.h)
+    uint32_t* zdr_offs = nullptr;
+    uint32_t* zdr_flag = nullptr;
+    uint32_t zdr_ntile = 0;      // tile-workgroup dumps the buffers hold (+ ZDR_P churn workgroups)
+    bool zdr_on = true;          // GBPE_ZDR=0: flush every workgroup's deltas instead (round-2 path)
     uint32_t* zseg = nullptr;    // ZSegState: the zone segments' per-merge hand-off (k_refresh zeroes it)
     uint32_t zseg_mode = 1;      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
     uint32_t table_grows = 0;    // crowded-table rebuilds (same size or larger)
@@ -284,7 +289,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
         if (mt)
             hipLaunchKernelGGL(tpw == 32 ? (k_delta_mt<S, true, 32>) : tpw == 16 ? (k_delta_mt<S, true, 16>) : (k_delta_mt<S, true, 8>),
                                dim3(g_mt + g_mtail), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask,
-                               t->tile_cnt, t->grpsum, g_delta, g_mt, 0u);
+                               t->tile_cnt, t->grpsum, g_delta, g_mt, 0u, ZdrView());
         else
             hipLaunchKernelGGL((k_delta<S, true>), dim3(g_delta), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb,
                                t->hitmask, t->tile_cnt, t->grpsum, g_delta, 0xFFFFFFFFu);
@@ -295,7 +300,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
         if (mt)
             hipLaunchKernelGGL(tpw == 32 ? (k_delta_mt<S, false, 32>) : tpw == 16 ? (k_delta_mt<S, false, 16>) : (k_delta_mt<S, false, 8>),
                                dim3(g_mt + g_mtail), dim3(TPB), 0, s, t->st, round, (const S*)cur, t->tb, t->hitmask,
-                               t->tile_cnt, t->grpsum, g_delta, g_mt, 0u);
+                               t->tile_cnt, t->grpsum, g_delta, g_mt, 0u, ZdrView());
         else
             hipLaunchKernelGGL((k_delta<S, false>), dim3(g_delta + g_dtail), dim3(TPB), 0, s, t->st, round, (const S*)cur,
                                t->tb, t->hitmask, t->tile_cnt, t->grpsum, g_delta, g_delta);
@@ -384,7 +389,33 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
                               (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
                              sp_mul(t), (ZSegState*)t->zseg);
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
-    if (!g.zone1) {
+    if (!g.zone1 && !exact && t->zdr_on && t->zdr_out) {
+        // a zone of many tiles, reference compaction: tiles dump their deltas, k_churn
+        // runs the stale window and tail, k_zdr adds each distinct pair once (train_dev.h)
+        const bool mt = t->delta_mt && g.zdelta >= t->delta_mt;
+        const uint32_t g_mt = (uint32_t)gbpe_div_up(g.zdelta, 8);
+        const uint32_t ntw = mt ? g_mt : g.zdelta;
+        const uint32_t gch = (uint32_t)std::min<uint64_t>(ZDR_P, std::max<uint64_t>(1, gbpe_div_up(((uint32_t)t->n - t->h_st->B) / 5 + 1, 16384)));
+        ZdrView zv;
+        zv.out = t->zdr_out;
+        zv.offs = t->zdr_offs;
+        zv.flag = t->zdr_flag;
+        zv.ntile = ntw;
+        zv.tag = (uint32_t)(t->done + round + 1);
+        if (ntw > t->zdr_ntile) return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "zone delta dumps too small");
+        if (mt)
+            hipLaunchKernelGGL((k_delta_mt<S, false, 8>), dim3(g_mt), dim3(TPB), 0, s, t->zst, round, (const S*)zc, t->tb,
+                               t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt, 0u, zv);
+        else
+            hipLaunchKernelGGL((k_delta<S, false, true>), dim3(g.zdelta), dim3(TPB), 0, s, t->zst, round, (const S*)zc,
+                               t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g.zdelta, zv);
+        hipLaunchKernelGGL((k_compact<S, false, true>), dim3(g.zdelta), dim3(CTPB), 0, s, t->zst, round, zc, zo,
+                           (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum, t->tb,
+                           (const S*)t->wtmp, (const DevState*)t->st, 1u);
+        hipLaunchKernelGGL(k_churn<S>, dim3(gch), dim3(CH_BT), 0, s, t->zst, round, zc, zo, (const uint32_t*)t->hitmask,
+                           (const uint32_t*)t->grpsum, (const S*)t->wtmp, t->tb, zv, ntw);
+        hipLaunchKernelGGL(k_zdr, dim3(ZDR_P), dim3(TPB), 0, s, zv, ntw + gch, t->tb, t->zst, round);
+    } else if (!g.zone1) {
         // a zone of many tiles (the lexicon loop's first merges): TPW tiles per
         // workgroup and one flush of their hot pairs, as in the dense loop
         const bool mt = t->delta_mt && g.zdelta >= t->delta_mt;
@@ -410,7 +441,7 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
             hipLaunchKernelGGL((k_delta<S, false, true>), dim3(g.zdelta + g.ztail), dim3(TPB), 0, s, t->zst, round,
                                (const S*)zc, t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g.zdelta);
     }
-    if (!g.zone1) {
+    if (!g.zone1 && !(!exact && t->zdr_on && t->zdr_out)) {
         if (exact)
             hipLaunchKernelGGL((k_compact<S, true, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
                                (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
@@ -947,6 +978,25 @@ int sp_alloc_zone(gbpe_trainer* t, uint64_t z, uint64_t prev_mc) {
             return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(zone) failed");
         t->zcap = zneed;
     }
+    {   // delta dumps of the multi-tile zone passes: the most tile workgroups a pass can have
+        const uint64_t zt = gbpe_div_up(t->zcap, TILE);
+        const uint32_t need = (uint32_t)std::max<uint64_t>(std::min<uint64_t>(zt, t->delta_mt ? t->delta_mt : zt),
+                                                           gbpe_div_up(zt, 8)) + 1;
+        if (t->zdr_on && need > t->zdr_ntile) {
+            hipFree(t->zdr_out);
+            hipFree(t->zdr_offs);
+            hipFree(t->zdr_flag);
+            t->zdr_out = nullptr, t->zdr_offs = nullptr, t->zdr_flag = nullptr;
+            t->zdr_ntile = 0;
+            const uint64_t nd = (uint64_t)need + ZDR_P;
+            if (hipMalloc(&t->zdr_out, ((uint64_t)need * ZDR_N_TILE + (uint64_t)ZDR_P * ZDR_N_CHURN) * sizeof(uint2)) !=
+                    hipSuccess ||
+                hipMalloc(&t->zdr_offs, nd * (ZDR_P + 1) * 4) != hipSuccess || hipMalloc(&t->zdr_flag, nd * 4) != hipSuccess)
+                return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(zone delta dumps) failed");
+            TR_HIP(t, hipMemsetAsync(t->zdr_flag, 0, nd * 4, s));   // tags start at 1
+            t->zdr_ntile = need;
+        }
+    }
     for (int k = 0; k < 2; ++k) TR_HIP(t, hipMemsetAsync(t->zbuf[k], 0, t->zcap * t->bps, s));
     return GBPE_OK;
 }
@@ -1218,6 +1268,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     if (const char* e = getenv("GBPE_SHRINK_PCT")) t->shrink_pct = std::max<uint32_t>(110, (uint32_t)strtoul(e, nullptr, 10));
     if (const char* e = getenv("GBPE_ZONE_SEG")) t->zseg_mode = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_ZONE_F")) t->zone_f = std::max<uint32_t>(3, (uint32_t)strtoul(e, nullptr, 10));
+    if (const char* e = getenv("GBPE_ZDR")) t->zdr_on = atoi(e) != 0;
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
         t->trace = fopen(e, "w");

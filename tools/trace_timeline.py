@@ -31,3 +31,29 @@ for r in rows[:N]:
     name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-70:]
     print(f"{(s - t0) / 1e3:10.1f} {(e - s) / 1e3:9.1f} {(s - prev_end) / 1e3:8.1f} {g:>9} {name}")
     prev_end = max(prev_end, e)
+
+# per merge (a merge ends at its k_refresh): kernels numbered by repeat within the
+# merge (k_delta_mt#0 = tiles, #1 = stale tail under GBPE_SPLIT_TAIL), bucketed
+import os
+edges = [int(x) for x in os.environ.get("EDGES", "0,10,50,128,300,1000,4000,16000,1073741824").split(",")]
+merges, curm = [], []
+for r in rows:
+    k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].replace("void ", "")
+    curm.append((k, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    if k == "k_refresh":
+        merges.append(curm)
+        curm = []
+print(f"--- per merge ({len(merges)} k_refresh-terminated groups; group 0 holds the creation / entry kernels)")
+for a, b in zip(edges[:-1], edges[1:]):
+    sel = merges[a:b]
+    if not sel:
+        break
+    acc = defaultdict(float)
+    for m in sel:
+        seen = defaultdict(int)
+        for k, us in m:
+            acc[f"{k}#{seen[k]}"] += us
+            seen[k] += 1
+    tot = sum(acc.values())
+    print(f"merges {a}-{a + len(sel)}: {tot / len(sel):8.1f} us/merge  " +
+          "  ".join(f"{k} {v / len(sel):.1f}" for k, v in sorted(acc.items(), key=lambda kv: -kv[1])[:9]))
