@@ -232,6 +232,9 @@ __device__ __forceinline__ void lds_add(LdsTab<N>& t, const Table& tb, DevState*
 // the table's low load factor nearly every live pair sits in its home slot, so
 // a batch costs one round trip instead of one per entry; the rest (new keys,
 // collisions) take the full probe.  Entries with pid or delta 0 are skipped.
+// (Adding at the home slot blind — one returning 64-bit atomic on {pid, count},
+// taken back when another pid sits there — measured slower: late 1 GiB merges
+// k_body 10.7 -> 11.2 us, code1g 1.42 -> 1.52 s.)
 __device__ __forceinline__ void table_add8(const Table& tb, DevState* st, const uint32_t (&kk)[8],
                                            const uint32_t (&vv)[8]) {
     uint32_t hs[8], hk[8];
@@ -1480,28 +1483,43 @@ constexpr uint32_t SP_CH = 256;      // symbols per wave pass over a sector (4 p
 constexpr uint32_t SP_INV = 0xFFFFFFFFu;
 constexpr uint32_t SP_SHRINKS = 64;  // zone shrinks per sparse entry (sector capacity)
 
-// Per-sector pair signature: a 1024-bit Bloom filter (2 hash bits) of every pair
+// Per-sector pair signature: a 2048-bit Bloom filter (3 hash bits) of every pair
 // the sector has held since the filters were last rebuilt.  The token bitmap
 // gives candidate sectors; the signature drops most of those where a and b are
-// both present but never adjacent.
-constexpr uint32_t SP_SIGW = 32;     // u32 words per sector signature
+// both present but never adjacent.  (1024 bits / 2 hash bits let through 5 of
+// every 6 candidates without a site in the middle merges — a sector holds ~200
+// pairs plus those its merges add — and every false candidate costs a sector
+// pass: 2048 / 3 cuts that rate to a few percent.)
+constexpr uint32_t SP_SIGW = 64;     // u32 words per sector signature
+constexpr uint32_t SP_SIGB = SP_SIGW * 32 - 1;
 __device__ __forceinline__ uint32_t sig_hash(uint32_t pid) { return gbpe_fmix32(pid ^ 0x9E3779B9u); }
+__device__ __forceinline__ void sig_bits(uint32_t pid, uint32_t& b1, uint32_t& b2, uint32_t& b3) {
+    const uint32_t h = sig_hash(pid), h2 = h * 0x9E3779B1u;
+    b1 = h & SP_SIGB;
+    b2 = (h >> 16) & SP_SIGB;
+    b3 = (h2 >> 21) & SP_SIGB;
+}
 __device__ __forceinline__ bool sig_has(const uint32_t* __restrict__ sig, uint32_t pid) {
-    const uint32_t h = sig_hash(pid), b1 = h & 1023u, b2 = (h >> 16) & 1023u;
-    return ((sig[b1 >> 5] >> (b1 & 31u)) & (sig[b2 >> 5] >> (b2 & 31u)) & 1u) != 0u;
+    uint32_t b1, b2, b3;
+    sig_bits(pid, b1, b2, b3);
+    return ((sig[b1 >> 5] >> (b1 & 31u)) & (sig[b2 >> 5] >> (b2 & 31u)) & (sig[b3 >> 5] >> (b3 & 31u)) & 1u) != 0u;
 }
 // global signature (k_body): no-return atomics, no test load on the merge's critical path
 __device__ __forceinline__ void sig_or(uint32_t* __restrict__ sig, uint32_t pid) {
-    const uint32_t h = sig_hash(pid), b1 = h & 1023u, b2 = (h >> 16) & 1023u;
+    uint32_t b1, b2, b3;
+    sig_bits(pid, b1, b2, b3);
     atomicOr(&sig[b1 >> 5], 1u << (b1 & 31u));
     atomicOr(&sig[b2 >> 5], 1u << (b2 & 31u));
+    atomicOr(&sig[b3 >> 5], 1u << (b3 & 31u));
 }
 // LDS signature (k_sp_bits): test first, most bits are already set
 __device__ __forceinline__ void sig_set(uint32_t* __restrict__ sig, uint32_t pid) {
-    const uint32_t h = sig_hash(pid), b1 = h & 1023u, b2 = (h >> 16) & 1023u;
-    const uint32_t m1 = 1u << (b1 & 31u), m2 = 1u << (b2 & 31u);
+    uint32_t b1, b2, b3;
+    sig_bits(pid, b1, b2, b3);
+    const uint32_t m1 = 1u << (b1 & 31u), m2 = 1u << (b2 & 31u), m3 = 1u << (b3 & 31u);
     if (!(sig[b1 >> 5] & m1)) atomicOr(&sig[b1 >> 5], m1);
     if (!(sig[b2 >> 5] & m2)) atomicOr(&sig[b2 >> 5], m2);
+    if (!(sig[b3 >> 5] & m3)) atomicOr(&sig[b3 >> 5], m3);
 }
 
 // a sector's first wave pass: 4 symbols per lane and the one after the pass

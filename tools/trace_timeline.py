@@ -36,13 +36,18 @@ for r in rows[:N]:
 # merge (k_delta_mt#0 = tiles, #1 = stale tail under GBPE_SPLIT_TAIL), bucketed
 import os
 edges = [int(x) for x in os.environ.get("EDGES", "0,10,50,128,300,1000,4000,16000,1073741824").split(",")]
-merges, curm = [], []
+merges, curm, spans = [], [], []
+mstart = None
 for r in rows:
     k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].replace("void ", "")
-    curm.append((k, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    if mstart is None:
+        mstart = s0
+    curm.append((k, (e0 - s0) / 1e3))
     if k == "k_refresh":
         merges.append(curm)
-        curm = []
+        spans.append((e0 - mstart) / 1e3)
+        curm, mstart = [], e0
 print(f"--- per merge ({len(merges)} k_refresh-terminated groups; group 0 holds the creation / entry kernels)")
 for a, b in zip(edges[:-1], edges[1:]):
     sel = merges[a:b]
@@ -55,5 +60,6 @@ for a, b in zip(edges[:-1], edges[1:]):
             acc[f"{k}#{seen[k]}"] += us
             seen[k] += 1
     tot = sum(acc.values())
-    print(f"merges {a}-{a + len(sel)}: {tot / len(sel):8.1f} us/merge  " +
+    span = sum(spans[a:b]) / len(sel)
+    print(f"merges {a}-{a + len(sel)}: {tot / len(sel):8.1f} us busy, {span:8.1f} us span /merge  " +
           "  ".join(f"{k} {v / len(sel):.1f}" for k, v in sorted(acc.items(), key=lambda kv: -kv[1])[:9]))
