@@ -56,7 +56,12 @@ TILE_SYMS = 8192
 METRIC = "BPE merges/sec + tokenize GB/s, 1 GiB UTF-8 @ 32K vocab, 1/2/4/8 MI355X"
 HEADLINE = {"gen": "english", "n": 1 << 30, "seed": 2, "fancy_punct": 0.005}
 C2 = {"gen": "english", "n": 104_857_600, "seed": 2, "fancy_punct": 0.005}
-PMC_FILE = os.path.join(ROOT, "profiles", "r2_pmc_kbody.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r3_pmc_kbody.json")
+ROCPROF_EN1G = os.path.join(ROOT, "profiles", "r3_rocprof_en1g_kernel_stats.csv")
+CAL_NOTE = ("FETCH_SIZE x2: tools/micro/fetch_cal.hip measured 64 counter bytes per distinct 128-B line for "
+            "16-B streaming reads and 4-, 8- and 16-B one-per-line gathers alike (profiles/r3_fetch_calibration.json), "
+            "so every read line moves 128 B; WRITE_SIZE counts 32-B granules (4-B scattered stores and atomics: 32 B "
+            "per line, whole-line stores 128 B)")
 GOLD = os.path.join(ROOT, "tests", "golden")
 
 
@@ -260,6 +265,20 @@ def train_roofline(det, wall_per_run):
                      "note": "latency-bound by design: the body is one copy of every distinct word (DESIGN §2c), "
                              "so a merge moves the few sectors holding its pair, kilobytes, not the stream; the loop "
                              "avoids the bytes rather than streaming them"})
+    if os.path.exists(ROCPROF_EN1G) and roof.get("us_per_launch") is not None:
+        # the same kernel under rocprofv3 --kernel-trace --stats over one full run of this
+        # workload (tools/explore_1g.py en1g): its own durations, without the event gaps
+        import csv
+        calls, ns = 0, 0.0
+        for r in csv.DictReader(open(ROCPROF_EN1G)):
+            if "k_body<" in r["Name"]:
+                calls += int(r["Calls"])
+                ns += float(r["TotalDurationNs"])
+        if calls:
+            roof["rocprof_us_per_launch"] = round(ns / calls / 1e3, 2)
+            roof["rocprof_launches"] = calls
+            roof["rocprof_achieved_with_rocprof_time"] = round(roof["algorithmic_bytes_per_launch"] / (ns / calls), 1)
+            roof["rocprof_window"] = os.path.relpath(ROCPROF_EN1G, ROOT)
     roof["dense_stream"] = dense
     roof["dense_equivalent"] = {"gbps": round(equiv, 1), "frac": round(equiv / HBM_PEAK_GBPS, 4),
                                 "bytes": det["stream_bytes"],
@@ -274,6 +293,7 @@ def train_roofline(det, wall_per_run):
             roof["traffic_window"] = (f"{os.path.relpath(PMC_FILE, ROOT)}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and "
                                       f"WRITE_SIZE passes over one full run of this workload ({p['launches']} k_body "
                                       f"launches); algorithmic bytes from the same run")
+            roof["traffic_calibration"] = CAL_NOTE
     return roof
 
 
@@ -418,7 +438,7 @@ def encode_leg(args, lib, ctx, dist, rank):
                      "frac": round(alg / 1e9 / (k_all / 1e3) / HBM_PEAK_GBPS, 4), "algorithmic_bytes": alg,
                      "traffic": None},
     }
-    pmc = os.path.join(ROOT, "profiles", "r2_pmc_encode.json")
+    pmc = os.path.join(ROOT, "profiles", "r3_pmc_encode.json")
     if os.path.exists(pmc):
         p = json.load(open(pmc))
         if p.get("workload") == "c3-1g" and p.get("chunk_size") == cs:
@@ -426,6 +446,7 @@ def encode_leg(args, lib, ctx, dist, rank):
             res["roofline"]["traffic_unit"] = "bytes/encode (all encode kernels)"
             res["roofline"]["traffic_over_algorithmic"] = round(p["hbm_bytes_per_encode"] / alg, 4)
             res["roofline"]["traffic_window"] = f"{os.path.relpath(pmc, ROOT)}: FETCH_SIZE (x2) + WRITE_SIZE passes"
+            res["roofline"]["traffic_calibration"] = CAL_NOTE
     fx = os.path.join(GOLD, "encode_c3enc1g.json")
     if os.path.exists(fx) and args.encode_bytes == 1 << 30 and args.vocab_sample_bytes == 104_857_600:
         meta = json.load(open(fx))
