@@ -409,6 +409,18 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     {
         int rc = launch_all();
         if (rc != GBPE_OK) return rc;
+        if (sparse && !tail && hs_mode(t, sg)) {
+            // hand-off selection: close the step's last merge, every block maximum exact again
+            if (t->u16)
+                hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(g_refresh), dim3(TPB), 0, s, t->st, 0u, 3, t->tb,
+                                   (uint16_t*)nullptr, (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part,
+                                   t->zseg);
+            else
+                hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(g_refresh), dim3(TPB), 0, s, t->st, 0u, 3, t->tb,
+                                   (uint32_t*)nullptr, (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part,
+                                   t->zseg);
+            GBPE_LAUNCH_CHECK(t->ctx);
+        }
         if (sparse) hipLaunchKernelGGL(k_live, dim3(1), dim3(1024), 0, s, t->st, t->tb);
     }
     TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
@@ -674,6 +686,12 @@ extern "C" int gbpe_trainer_pair_counts(gbpe_trainer* t, uint32_t* pids, uint32_
 extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     if (!t) return;
     if (t->ctx && t->ctx->stream) hipStreamSynchronize(t->ctx->stream);
+    if (t->hs_stat && getenv("GBPE_HS_STATS")) {   // hand-off selections and their verification retries
+        uint32_t h[2] = {0, 0};
+        if (hipMemcpy(h, t->hs_stat, 8, hipMemcpyDeviceToHost) == hipSuccess)
+            fprintf(stderr, "[gpubpe] hand-off selections %u, verification retries %u (%u launches)\n", h[1], h[0],
+                    t->hs_seq);
+    }
 #ifdef GBPE_KTRACE
     if (const char* path = getenv("GBPE_KTRACE_OUT")) {   // one file per trainer: path.<done merges>
         std::vector<unsigned long long> h((size_t)(KT_MERGES / KT_EVERY) * 2 * KT_WG * KT_SLOTS);
@@ -714,6 +732,8 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->d_u32);
     hipFree(t->part);
     hipFree(t->zseg);
+    hipFree(t->hs_rec);
+    hipFree(t->hs_stat);
     hipFree(t->zdr_out);
     hipFree(t->zdr_offs);
     hipFree(t->zdr_flag);

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <type_traits>
 #include <cstdarg>
 
 namespace {
@@ -79,6 +80,8 @@ struct DevState {
                            // (never written by a commit: a reader beside k_body would see it unchanged)
     uint32_t enter_lim;    // dense loop: end the step at the first merge whose count is <= this (the host
                            // can then enter the sector-sparse loop; 0 = off)
+    uint32_t body_rm_base; // HS: body_rm at the last in-launch closing (body_rm itself is only reset by
+                           // k_refresh; this merge removed body_rm - body_rm_base)
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
@@ -149,19 +152,58 @@ enum : uint32_t {
 struct Table {
     uint2* slots;      // .x = pid (0 = empty), .y = count (u32, wraps for transient negatives)
     uint32_t mask;     // slots - 1
-    uint64_t* bmax;    // per block: (count << 32) | ~pid, 0 when empty
+    uint64_t* bmax;    // per block: (count << 32) | ~pid, KEY_NONE when no count is positive
     uint32_t* dirty;   // per block flag
     uint32_t* dlist;   // dirty block list
     uint32_t* blive;   // per block: entries with count > 0
     uint32_t nblk;
     uint32_t* used;    // occupied-slot counter (DevState::used or ::dused)
     uint32_t* full;    // non-null: a full table sets *full instead of the fatal error (delta table)
+    // hand-off selection (HS, k_body): bmax and the group maxima are upper BOUNDS between
+    // k_refresh passes, raised by positive deltas (slot_add; the selector verifies them)
+    uint64_t* bpart = nullptr;   // group bounds (k_refresh's partial maxima), null: exact maxima
+    uint32_t bper = 1;           // blocks per group
 };
+
+// the key of a block without a positive count (count 0, the weakest tie-break)
+constexpr uint64_t KEY_NONE = 0xFFFFFFFFull;
 
 // a touched block is re-maxed by the next k_refresh: a plain flag store, nothing waits on it
 __device__ __forceinline__ void mark_dirty(const Table& tb, DevState* st, uint32_t slot) {
     (void)st;
     tb.dirty[slot >> BLK_LOG2] = 1u;
+}
+
+// The HS view of the table (k_body's flushes in the hand-off selection mode):
+// its adds also raise the bounds.  A distinct type, so the exact-maxima paths
+// compile as before (overload resolution picks the add).
+struct TableB : Table {};
+template <bool B> struct TbSel { using type = Table; };
+template <> struct TbSel<true> { using type = TableB; };
+template <bool B>
+__device__ __forceinline__ typename TbSel<B>::type tb_view(const Table& t) {
+    typename TbSel<B>::type r;
+    static_cast<Table&>(r) = t;
+    return r;
+}
+
+// Count add at a found slot of the HS table: a positive delta returns the new
+// count and raises the block's and the group's bound to the pair's key
+// (atomicMax).  Whichever add to a pair lands last, a bound saw a count >= the
+// final one, so the bounds stay >= every key; negative deltas raise nothing.
+__device__ __forceinline__ void slot_add(const TableB& tb, DevState* st, uint32_t idx, uint32_t pid, uint32_t delta) {
+    if ((int32_t)delta > 0) {
+        const uint32_t nv = atomicAdd(&tb.slots[idx].y, delta) + delta;
+        if ((int32_t)nv > 0) {
+            const unsigned long long key = ((unsigned long long)nv << 32) | (uint32_t)~pid;
+            const uint32_t blk = idx >> BLK_LOG2;
+            atomicMax(reinterpret_cast<unsigned long long*>(&tb.bmax[blk]), key);
+            atomicMax(reinterpret_cast<unsigned long long*>(&tb.bpart[blk / tb.bper]), key);
+        }
+    } else {
+        atomicAdd(&tb.slots[idx].y, delta);
+    }
+    mark_dirty(tb, st, idx);
 }
 
 // global insert-or-add (triangular probing visits every slot of a 2^k table)
@@ -180,6 +222,28 @@ __device__ void table_add(const Table& tb, DevState* st, uint32_t pid, uint32_t 
         if (k == pid) {
             atomicAdd(&tb.slots[idx].y, delta);
             mark_dirty(tb, st, idx);
+            return;
+        }
+    }
+    if (tb.full) *tb.full = 1u;   // per-merge delta table sized too small: the merge stalls and retries bigger
+    else atomicOr(&st->err, ERR_TABLE_FULL);
+}
+
+// the HS table's insert-or-add
+__device__ void table_add(const TableB& tb, DevState* st, uint32_t pid, uint32_t delta) {
+    uint32_t h = gbpe_fmix32(pid) & tb.mask;
+    for (uint32_t p = 0; p <= tb.mask; ++p) {
+        uint32_t idx = (h + ((p * (p + 1)) >> 1)) & tb.mask;
+        uint32_t k = __hip_atomic_load(&tb.slots[idx].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == 0u) {
+            k = atomicCAS(&tb.slots[idx].x, 0u, pid);
+            if (k == 0u) {
+                if (tb.used) __hip_atomic_fetch_add(tb.used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                k = pid;
+            }
+        }
+        if (k == pid) {
+            slot_add(tb, st, idx, pid, delta);
             return;
         }
     }
@@ -212,8 +276,8 @@ __device__ __forceinline__ void lds_clear(LdsTab<N>& t) {
     if (threadIdx.x == 0) t.ovf = 0u;
 }
 
-template <int N>
-__device__ __forceinline__ void lds_add(LdsTab<N>& t, const Table& tb, DevState* st, uint32_t pid, uint32_t d) {
+template <int N, typename TB>
+__device__ __forceinline__ void lds_add(LdsTab<N>& t, const TB& tb, DevState* st, uint32_t pid, uint32_t d) {
     uint32_t h = gbpe_fmix32(pid);
 #pragma unroll 1
     for (int p = 0; p < LPROBE; ++p) {
@@ -247,7 +311,7 @@ __device__ __forceinline__ void table_add8(const Table& tb, DevState* st, const 
     for (int j = 0; j < 8; ++j) {
         if (!kk[j] || !vv[j]) continue;
         if (hk[j] == kk[j]) {
-            atomicAdd(&tb.slots[hs[j]].y, vv[j]);
+            atomicAdd(&tb.slots[hs[j]].y, vv[j]);   // (never a bounds table: HS flushes take table_add)
             mark_dirty(tb, st, hs[j]);
         } else {
             table_add(tb, st, kk[j], vv[j]);
@@ -262,11 +326,11 @@ __device__ __forceinline__ void table_add8(const Table& tb, DevState* st, const 
 // (the multi-tile and zone k_delta, the full count) add in batches of 8 per
 // thread (table_add8).  The table's contents are consumed (callers clear it
 // before reuse).
-template <int N>
-__device__ __forceinline__ void lds_flush(LdsTab<N>& t, const Table& tb, DevState* st) {
+template <int N, typename TB>
+__device__ __forceinline__ void lds_flush(LdsTab<N>& t, const TB& tb, DevState* st) {
     __syncthreads();
     const uint32_t nt = blockDim.x;
-    if (N > 8 * (int)nt) {
+    if (!std::is_same<TB, TableB>::value && N > 8 * (int)nt) {   // (the HS table takes the list path: table_add)
         for (uint32_t i0 = threadIdx.x; i0 < (uint32_t)N; i0 += 8 * nt) {
             uint32_t kk[8], vv[8];
 #pragma unroll
@@ -416,28 +480,35 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
         __syncthreads();
         const DevState& g = s_g.d;
         const DevState& z = s_z.d;
-        const bool fin = finish == 2 ? (!g.stop && !g.sp_abort && g.sel_round == round + 1u)
-                                     : (!g.stop && !g.stall && g.merges_done == round + 1u);
+        // finish == 3 (the HS steps' closing launch): whichever merge is still open
+        const uint32_t r = finish == 3 ? g.merges_done : round;
+        const bool fin = finish >= 2 ? (!g.stop && !g.sp_abort && g.sel_round == r + 1u)
+                                     : (!g.stop && !g.stall && g.merges_done == r + 1u);
+        if (finish == 3 && !fin && threadIdx.x == 0 && g.body_rm_base) {   // no open merge: body_rm relative to 0 again
+            st->body_rm = g.body_rm - g.body_rm_base;
+            st->body_rm_base = 0u;
+        }
         if (fin && threadIdx.x == 0) {
             if (zst) {   // sector-sparse: global length, body length, zone length
-                if (finish == 2) {
-                    st->merges_done = round + 1u;
+                if (finish >= 2) {
+                    st->merges_done = r + 1u;
                     st->next_id = g.next_id + 1u;
                     st->epoch = g.epoch + 1u;
                     st->mc_prev = g.mc;
                 }
                 if (clog) {
-                    clog[2 * round] = g.cand;
-                    clog[2 * round + 1] = g.hitsec;
+                    clog[2 * r] = g.cand;
+                    clog[2 * r + 1] = g.hitsec;
                 }
                 st->cand = 0u;
                 st->hitsec = 0u;
                 st->tail_total = g.tail_total + z.m;
-                const uint32_t n = g.new_n, B = g.B - g.body_rm, zn = n - B;
+                const uint32_t n = g.new_n, B = g.B - (g.body_rm - g.body_rm_base), zn = n - B;
                 st->n = n;
                 st->Bp = g.B;
                 st->B = B;
                 st->body_rm = 0u;
+                st->body_rm_base = 0u;
                 zst->n = zn;
                 if (!g.sharded) st->zlast = zn;   // sharded: from the records (k_shard_apply)
                 if (!z.valid_total && g.is_last)   // multi-tile zone: k_delta + k_compact stream it twice, plus the window copy
@@ -486,7 +557,7 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             uint4 e[NV];
 #pragma unroll
             for (int q = 0; q < NV; ++q) e[q] = sl[lane + q * 64];
-            uint64_t best = 0;
+            uint64_t best = KEY_NONE;
             uint32_t live = 0;
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
@@ -1539,9 +1610,9 @@ __device__ __forceinline__ void sector_first(const S* __restrict__ p, const uint
 // survivors compacted to the sector's front).  In the lexicon body (mp != null)
 // every symbol carries its word's multiplicity, which weights its count deltas
 // and moves with it.  Returns the B-sides removed (weighted: stream symbols).
-template <typename S, int NT = LTAB_T>
+template <typename S, int NT = LTAB_T, typename TB = Table>
 __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, uint32_t cnt, uint32_t a, uint32_t b,
-                                uint32_t nw, LdsTab<NT>& lt, const Table& tb, DevState* st, uint32_t* __restrict__ sig,
+                                uint32_t nw, LdsTab<NT>& lt, const TB& tb, DevState* st, uint32_t* __restrict__ sig,
                                 uint32_t& out_cnt, const uint32_t (&first)[5], const uint32_t (&firstm)[4]) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     const int lane = threadIdx.x & 63;
@@ -1668,10 +1739,10 @@ __device__ __forceinline__ uint32_t lane_mask_n(uint64_t i0, uint64_t lim, int n
 
 // zout (the persistent tail loop, k_tail): the delta table is shared with the body
 // pass (neither cleared nor flushed here) and m, the new zone length go to zout[0..1]
-template <typename S, bool EXACT, int BT, int NT = LTAB_T, int ZPT_ = ZoneDim<S, BT>::ZPT>
+template <typename S, bool EXACT, int BT, int NT = LTAB_T, int ZPT_ = ZoneDim<S, BT>::ZPT, typename TB = Table>
 __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
                          S* __restrict__ zo, ZoneLds<S, BT>& L,
-                         LdsTab<NT>& lt, const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
+                         LdsTab<NT>& lt, const TB& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
                          uint64_t* __restrict__ bytes, uint32_t round, uint32_t* zout = nullptr) {
     (void)round;   // phase stamps only (-DGBPE_KTRACE)
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
@@ -2205,6 +2276,337 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     return go;
 }
 
+// ── hand-off selection (HS, single GPU, zone in one workgroup) ──
+// k_refresh is no longer launched after every merge: block maxima and group
+// maxima are kept as upper BOUNDS (raised by each positive delta, mark_dirty),
+// and ONE workgroup of k_body — block 0, the zone workgroup — closes the last
+// merge (k_refresh's finish-2 bookkeeping), finds the exact maximum and hands
+// (a, b, new id, count) to the others through tagged 8-byte granules:
+//   1. group bounds + state snapshots (one round trip);
+//   2. the bounds of the best group's blocks;
+//   3. the best block's 256 slots: its exact maximum X and runner-up;
+//   4. X >= every other bound (groups and blocks): X is the table maximum.
+//      Otherwise the block's bound is tightened to X (and its group's), and
+//      steps 2-4 repeat.
+// The selected block's bound then drops to its runner-up, so the next selection
+// does not start at a stale holder.  Every bound change is an atomic add, which
+// commutes with the workgroups' own bound raises.  k_refresh (finish 3) closes
+// the last merge of the step and makes every maximum exact again.
+struct HsView {
+    unsigned long long* rec = nullptr;   // hand-off granules: value | tag << 32 (pid, count, new id | go)
+    const uint64_t* part = nullptr;      // group bounds (k_refresh's partial maxima)
+    uint32_t npart = 0, per = 1;         // groups; blocks per group
+    uint32_t tag = 0;                    // this launch's hand-off tag (a sequence number, never reused)
+    uint32_t* clog = nullptr;            // per-merge candidate / hit-sector log (GBPE_SPARSE_TRACE)
+    uint32_t* stat = nullptr;            // [0] verification retries, [1] selections
+};
+constexpr int HS_PPT = 8;          // group bounds per selector thread (the host checks npart <= 8 x threads)
+constexpr uint32_t HS_ITER = 256;  // verification rounds (each tightens one bound)
+
+// (k1, i1) the largest key and its index, k2 the runner-up, over the wave
+__device__ __forceinline__ void top2_wave(uint64_t& k1, uint32_t& i1, uint64_t& k2) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o1 = __shfl_xor(k1, off), o2 = __shfl_xor(k2, off);
+        const uint32_t oi = __shfl_xor(i1, off);
+        const bool take = o1 > k1 || (o1 == k1 && oi < i1);
+        const uint64_t lo = take ? k1 : o1;
+        k2 = lo > k2 ? lo : k2;
+        k2 = o2 > k2 ? o2 : k2;
+        if (take) {
+            k1 = o1;
+            i1 = oi;
+        }
+    }
+}
+
+template <int BT>
+__device__ __forceinline__ bool hs_select(DevState* st, DevState* zst, const HsView& hv, const Table& tb, uint32_t round, bool exact,
+                          uint32_t* __restrict__ log, uint32_t* __restrict__ grpsum, const SelShard& sh,
+                          uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc, const DevState*& gsnap,
+                          const DevState*& zsnap) {
+    constexpr int NWV = BT / 64;
+    constexpr int NW = sizeof(DevState) / 4;
+    __shared__ union {
+        DevState d;
+        uint32_t w[NW];
+    } s_g, s_z;
+    __shared__ uint64_t s_k1[NWV], s_k2[NWV];
+    __shared__ uint32_t s_i1[NWV];
+    __shared__ uint64_t s_sel, s_np;
+    __shared__ uint32_t s_state, s_sidx;   // 0 retry, 1 accepted
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t npart = hv.npart, per = hv.per;
+    // 1. snapshots and group bounds: one round trip
+    if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
+    else if (t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
+    uint64_t pv[HS_PPT];
+#pragma unroll
+    for (int j = 0; j < HS_PPT; ++j) {
+        const uint32_t i = (uint32_t)j * BT + t;
+        pv[j] = i < npart ? hv.part[i] : 0ull;
+    }
+    __syncthreads();
+    DevState& g = s_g.d;
+    DevState& z = s_z.d;
+    gsnap = &s_g.d;
+    zsnap = &s_z.d;
+    if (t == 0) {
+        // close the previous merge (k_refresh finish 2, mirrored): its deltas are all in
+        if (!g.stop && !g.sp_abort && g.sel_round == g.merges_done + 1u) {
+            const uint32_t r = g.merges_done;
+            if (hv.clog) {   // (trace only) counters the other workgroups add to: exchanged, waited for before the hand-off
+                hv.clog[2 * r] = atomicExch(&st->cand, 0u);
+                hv.clog[2 * r + 1] = atomicExch(&st->hitsec, 0u);
+            }
+            g.merges_done = r + 1u;
+            g.next_id += 1u;
+            g.epoch += 1u;
+            g.mc_prev = g.mc;
+            g.tail_total += z.m;
+            // body_rm is not reset here (the others add to it in this launch): its base moves
+            const uint32_t n = g.new_n, B = g.B - (g.body_rm - g.body_rm_base), zn = n - B;
+            if (z.valid_total && z.valid_total != zn + 1u) atomicOr(&st->err, ERR_COUNT_MISMATCH);
+            g.n = n;
+            g.Bp = g.B;
+            g.B = B;
+            g.body_rm_base = g.body_rm;
+            st->body_rm_base = g.body_rm;
+            g.zlast = zn;
+            g.cand = g.hitsec = 0u;
+            z.n = zn;
+            st->merges_done = g.merges_done;
+            st->next_id = g.next_id;
+            st->epoch = g.epoch;
+            st->mc_prev = g.mc_prev;
+            st->tail_total = g.tail_total;
+            st->n = n;
+            st->Bp = g.Bp;
+            st->B = B;
+            st->zlast = zn;
+            zst->n = zn;
+        }
+    }
+    __syncthreads();
+    bool go = round < g.budget && g.merges_done == round && !g.stop && !g.sp_abort && !g.stall;
+    if (go) {
+        // 2-4: the exact maximum
+        uint32_t it = 0;
+        for (;; ++it) {
+            uint64_t k1 = 0, k2 = 0;
+            uint32_t i1 = 0xFFFFFFFFu;
+#pragma unroll
+            for (int j = 0; j < HS_PPT; ++j) {
+                const uint32_t i = (uint32_t)j * BT + t;
+                const uint64_t v = pv[j];
+                if (v > k1) {
+                    k2 = k1;
+                    k1 = v;
+                    i1 = i;
+                } else if (v > k2) {
+                    k2 = v;
+                }
+            }
+            top2_wave(k1, i1, k2);
+            if (lane == 0) {
+                s_k1[wid] = k1;
+                s_k2[wid] = k2;
+                s_i1[wid] = i1;
+            }
+            __syncthreads();
+            if (wid == 0) {
+                k1 = lane < NWV ? s_k1[lane] : 0ull;
+                k2 = lane < NWV ? s_k2[lane] : 0ull;
+                i1 = lane < NWV ? s_i1[lane] : 0xFFFFFFFFu;
+                top2_wave(k1, i1, k2);
+                const uint32_t g1 = i1 < npart ? i1 : 0u;
+                const uint64_t pg = k1, pout = k2;   // the best group's bound, the best other group's
+                // 2+3 in one round trip when the group bound's pair sits in its home block
+                // (the common case: raised by atomicMax, the bound IS that pair's key): that
+                // block's slots load with the group's block bounds (atomic loads: this
+                // workgroup may have tightened them); otherwise the bounds first
+                const uint32_t hb = (gbpe_fmix32(~(uint32_t)pg) & tb.mask) >> BLK_LOG2;
+                const bool guess = hb / per == g1;
+                const uint32_t hl = hb - g1 * per;
+                const uint32_t blk = g1 * per + (uint32_t)lane;
+                const bool inb = (uint32_t)lane < per && blk < tb.nblk;
+                uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0;
+                if (guess) {
+                    const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)hb << BLK_LOG2));
+                    e0 = sl[lane];
+                    e1 = sl[lane + 64];
+                }
+                const uint64_t bb = inb ? __hip_atomic_load(&tb.bmax[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                uint32_t b1;
+                uint64_t c1, c2;   // the chosen block's bound, the best bound of the group's other blocks
+                if (guess) {
+                    b1 = hb;
+                    c1 = __shfl(bb, (int)hl);
+                    c2 = (uint32_t)lane == hl ? 0ull : bb;
+                    for (int off = 32; off > 0; off >>= 1) {
+                        const uint64_t o = __shfl_xor(c2, off);
+                        c2 = o > c2 ? o : c2;
+                    }
+                } else {
+                    uint32_t ci = inb ? (uint32_t)lane : 0xFFFFFFFFu;
+                    c1 = bb;
+                    c2 = 0;
+                    top2_wave(c1, ci, c2);
+                    b1 = g1 * per + (ci < 64u ? ci : 0u);
+                    const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)b1 << BLK_LOG2));
+                    e0 = sl[lane];
+                    e1 = sl[lane + 64];
+                }
+                // 3. the block's exact maximum and runner-up
+                uint64_t x1 = 0, x2 = 0;
+                uint32_t xi = 0xFFFFFFFFu;
+                {
+                    const uint32_t px[4] = {e0.x, e0.z, e1.x, e1.z}, py[4] = {e0.y, e0.w, e1.y, e1.w};
+                    const uint32_t pos[4] = {2u * lane, 2u * lane + 1u, 128u + 2u * lane, 129u + 2u * lane};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (px[q] && (int32_t)py[q] > 0) {
+                            const uint64_t key = ((uint64_t)py[q] << 32) | (uint32_t)(~px[q]);
+                            if (key > x1) {
+                                x2 = x1;
+                                x1 = key;
+                                xi = pos[q];
+                            } else if (key > x2) {
+                                x2 = key;
+                            }
+                        }
+                    }
+                }
+                top2_wave(x1, xi, x2);
+                if (x1 == 0) x1 = KEY_NONE;
+                if (x2 == 0) x2 = KEY_NONE;
+                // 4. X against every other bound
+                const uint64_t rest = pout > c2 ? pout : c2;
+                if (lane == 0) {
+                    if (x1 >= rest || it + 1u >= HS_ITER) {
+                        if (x1 < rest) atomicOr(&st->err, ERR_SPIN);   // (bounds that never settle: cannot happen)
+                        s_state = 1u;
+                        s_sel = x1;
+                        s_sidx = (b1 << BLK_LOG2) | (xi & 255u);
+                        // the block loses its holder: its bound drops to the runner-up, the
+                        // group's to its best remaining block
+                        const uint64_t np = x2 > c2 ? x2 : c2;
+                        s_np = np;
+                        if (x1 != KEY_NONE) {
+                            atomicAdd(reinterpret_cast<unsigned long long*>(&tb.bmax[b1]), (unsigned long long)(x2 - c1));
+                            atomicAdd(reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(&hv.part[g1])),
+                                      (unsigned long long)(np - pg));
+                        }
+                    } else {   // a stale bound: tighten it to X, and the group's
+                        s_state = 0u;
+                        const uint64_t np = x1 > c2 ? x1 : c2;
+                        s_np = np;
+                        atomicAdd(reinterpret_cast<unsigned long long*>(&tb.bmax[b1]), (unsigned long long)(x1 - c1));
+                        atomicAdd(reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(&hv.part[g1])),
+                                  (unsigned long long)(np - pg));
+                    }
+                    s_i1[0] = g1;
+                }
+            }
+            __syncthreads();
+            if (s_state) break;
+            {   // the owner of the tightened group updates its copy
+                const uint32_t g1 = s_i1[0];
+#pragma unroll
+                for (int j = 0; j < HS_PPT; ++j)
+                    if ((uint32_t)j * BT + t == g1) pv[j] = s_np;
+            }
+            __syncthreads();
+        }
+        if (t == 0 && hv.stat) {
+            atomicAdd(&hv.stat[0], it);
+            atomicAdd(&hv.stat[1], 1u);
+        }
+        const uint64_t best = s_sel;
+        mc = (uint32_t)(best >> 32);
+        const uint32_t pid = ~(uint32_t)best;
+        a = pid >> 16;
+        b = pid & 0xFFFFu;
+        nw = g.next_id;
+        // the reference's stop rule and the zone invariants, as sel_inline
+        const bool stop = mc < 2u || nw > 0xFFFFu;                                          // train.wgsl:345-348
+        const bool bad = !stop && !exact && (uint64_t)(uint32_t)(g.n - g.Bp) < 2ull * mc;   // cannot happen
+        const uint64_t zneed = std::max<uint64_t>(2ull * mc + g.mc_prev, (uint64_t)sh.zf * mc) + 2u;
+        const bool abort = !stop && !bad && !exact && ((uint64_t)g.zlast < zneed || (sh.zmax && g.zlast > sh.zmax));
+        go = !stop && !bad && !abort;
+        if (t == 0) {
+            if (stop) {
+                st->stop = 1u;
+            } else if (bad) {
+                atomicOr(&st->err, ERR_SPARSE_WINDOW);
+                st->stop = 1u;
+            } else if (abort) {
+                st->sp_abort = 1u;
+            } else {
+                const uint32_t idx = s_sidx;
+                atomicSub(&tb.slots[idx].y, mc);   // every (a,b) occurrence is a merge site
+                tb.dirty[idx >> BLK_LOG2] = 1u;
+                log[round * 4 + 0] = a;
+                log[round * 4 + 1] = b;
+                log[round * 4 + 2] = nw;
+                log[round * 4 + 3] = mc;
+                st->a = a;
+                st->b = b;
+                st->nw = nw;
+                st->mc = mc;
+                st->new_n = g.n - mc;
+                zst->a = a;
+                zst->b = b;
+                zst->nw = nw;
+                zst->mc = mc;
+                zst->new_n = exact ? z.n : z.n - mc;
+                zst->merges_done = round + 1u;
+                st->sel_round = round + 1u;
+            }
+        }
+        if (go) {   // group sums of a multi-tile zone pass start at zero
+            const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(z.n, TILE), GRP);
+            for (uint32_t q = t; q < ngrp; q += BT) grpsum[q * GSTR] = 0u;
+        }
+    }
+    // hand-off: three tagged granules (the commit's atomics commute with the other
+    // workgroups' adds; only the trace counters' exchange must land first)
+    if (t == 0) {
+        if (hv.clog) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long tg = (unsigned long long)hv.tag << 32;
+        __hip_atomic_store(&hv.rec[0], tg | (go ? ((a << 16) | b) : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&hv.rec[1], tg | (go ? mc : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&hv.rec[2], tg | (go ? (0x80000000u | nw) : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return go;
+}
+
+// the other workgroups: poll the three granules of this launch's tag
+__device__ __forceinline__ bool hs_wait(const HsView& hv, DevState* st, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc) {
+    __shared__ uint32_t s_v[3], s_to;
+    if (threadIdx.x == 0) s_to = 0u;
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        unsigned long long v = 0;
+        for (uint32_t spins = 0;; ++spins) {
+            v = __hip_atomic_load(&hv.rec[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(v >> 32) == hv.tag) break;
+            if (spins > ZSEG_SPIN) {   // the selector never published: give up (reported)
+                atomicOr(&st->err, ERR_SPIN);
+                s_to = 1u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        s_v[threadIdx.x] = (uint32_t)v;
+    }
+    __syncthreads();
+    a = s_v[0] >> 16;
+    b = s_v[0] & 0xFFFFu;
+    mc = s_v[1];
+    nw = s_v[2] & 0xFFFFu;
+    return !s_to && (s_v[2] >> 31) != 0u;
+}
+
 // Body pass: blocks [0, nbody) each own `wpg` consecutive bitmap words of
 // (a-row & b-row), tested PW words at a time: the candidate sectors whose pair
 // signature may hold (a, b) are merged (one wave per sector).  A fixed grid of
@@ -2230,7 +2632,7 @@ union BodyLds {   // body workgroups use the candidate arrays, the zone workgrou
 // ZSEG: the form for zones of 32K-1M symbols: blocks [0, zone1) run the zone
 // segments (zone_seg) beside the body blocks, and zone_one is not compiled in
 // (with both, every form spilled to scratch)
-template <typename S, bool EXACT, int BT, int ZPT = ZoneDim<S, BT>::ZPT, bool ZSEG = false>
+template <typename S, bool EXACT, int BT, int ZPT = ZoneDim<S, BT>::ZPT, bool ZSEG = false, bool HS = false>
 __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
                                               uint32_t* __restrict__ bits, uint32_t W, uint32_t wpg,
                                               uint32_t* __restrict__ sig, Table tb, uint32_t nbody,
@@ -2239,7 +2641,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
                                               Table dtb, SelShard sh, uint32_t* __restrict__ lmul,
-                                              ZSegState* __restrict__ zg = nullptr) {
+                                              ZSegState* __restrict__ zg = nullptr, HsView hv = HsView()) {
     constexpr int KB_LT = ZSEG ? 4096 : LTAB_T;
     __shared__ LdsTab<KB_LT> lt;
     __shared__ BodyLds<S, BT> u;
@@ -2249,9 +2651,17 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     uint32_t a, b, nw, mc;
     if (t == 0) KT(0);
-    const DevState *gs, *zs;   // this workgroup's snapshots of the states at launch (LDS)
-    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh))
+    const DevState *gs = nullptr, *zs = nullptr;   // this workgroup's snapshots of the states at launch (LDS)
+    const auto xtb = tb_view<HS>(dtb);   // the HS table view raises the bounds with its adds
+    if constexpr (HS) {   // hand-off selection: block 0 (the zone workgroup) selects, the others wait for it
+        if (blockIdx.x == 0) {
+            if (!hs_select<BT>(st, zst, hv, tb, round, EXACT, log, grpsum, sh, a, b, nw, mc, gs, zs)) return;
+        } else if (!hs_wait(hv, st, a, b, nw, mc)) {
+            return;
+        }
+    } else if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh)) {
         return;
+    }
     if (t == 0) KT(1);
     // the zone workgroup is dispatched first (block 0 when zone1): it is the longest
     // single chain of the merge, and later blocks of a large grid start later
@@ -2269,7 +2679,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         }
     } else {
         if (zone1 == 1 && blockIdx.x == 0) {
-            zone_one<S, EXACT, BT, KB_LT, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, dtb, a, b, nw, mc,
+            zone_one<S, EXACT, BT, KB_LT, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, xtb, a, b, nw, mc,
                                                  wg_bytes + nbody, round);
             if (t == 0) {
                 KT(5);
@@ -2368,7 +2778,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                 sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
             }
             uint32_t out = 0;
-            const uint32_t r = body_sector<S, KB_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, dtb, st,
+            const uint32_t r = body_sector<S, KB_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, xtb, st,
                                               sig + (uint64_t)sct * SP_SIGW, out, cf, cfm);
             moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (r ? out : 0u));
             if (r) {
@@ -2392,7 +2802,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         return;
     }
     if (t == 0 && clog) atomicAdd(&st->cand, ncand_all);
-    lds_flush(lt, dtb, st);
+    lds_flush(lt, xtb, st);
     if (lane == 0) {
         s_rm[wid] = removed;
         s_mv[wid] = moved;

@@ -81,6 +81,11 @@ struct gbpe_trainer {
     uint32_t* zdr_flag = nullptr;
     uint32_t zdr_ntile = 0;      // tile-workgroup dumps the buffers hold (+ ZDR_P churn workgroups)
     bool zdr_on = true;          // GBPE_ZDR=0: flush every workgroup's deltas instead (round-2 path)
+    // hand-off selection (k_body's block 0 selects from bounds, no k_refresh per merge)
+    bool hs_on = false;          // GBPE_HS=1: on (measured slower so far)
+    unsigned long long* hs_rec = nullptr;   // hand-off granules
+    uint32_t* hs_stat = nullptr; // [0] verification retries, [1] selections (device)
+    uint32_t hs_seq = 0;         // hand-off tags handed out
     uint32_t* zseg = nullptr;    // ZSegState: the zone segments' per-merge hand-off (k_refresh zeroes it)
     uint32_t zseg_mode = 1;      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
     uint32_t table_grows = 0;    // crowded-table rebuilds (same size or larger)
@@ -353,8 +358,17 @@ inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* 
 // 8K-16K symbols: half the per-thread zone work of the 32K form; 1 GiB en1g
 // 1.017 -> 0.963 s.  1024 threads x 8 for zones <= 8K instead of 256 x 32 was
 // slower: C2 0.66 vs 0.61 s)
-template <typename S, bool EXACT, typename... A>
+template <typename S, bool EXACT, bool HS = false, typename... A>
 void launch_body(int bt, uint32_t grid, hipStream_t s, A... args) {
+    if constexpr (HS) {   // hand-off selection: the zone_one forms only
+        if (bt == 1023 && sizeof(S) == 2)
+            hipLaunchKernelGGL((k_body<S, EXACT, 1024, 16, false, true>), dim3(grid), dim3(1024), 0, s, args...);
+        else if (bt >= 1023)
+            hipLaunchKernelGGL((k_body<S, EXACT, 1024, ZoneDim<S, 1024>::ZPT, false, true>), dim3(grid), dim3(1024), 0, s, args...);
+        else
+            hipLaunchKernelGGL((k_body<S, EXACT, 256, ZoneDim<S, 256>::ZPT, false, true>), dim3(grid), dim3(256), 0, s, args...);
+        return;
+    }
     if (bt == 2048)   // zone segments inside k_body (the ZSEG form, 1024 threads)
         hipLaunchKernelGGL((k_body<S, EXACT, 1024, 16, true>), dim3(grid), dim3(1024), 0, s, args...);
     else if (bt == 1023 && sizeof(S) == 2)
@@ -363,6 +377,12 @@ void launch_body(int bt, uint32_t grid, hipStream_t s, A... args) {
         hipLaunchKernelGGL((k_body<S, EXACT, 1024>), dim3(grid), dim3(1024), 0, s, args...);
     else
         hipLaunchKernelGGL((k_body<S, EXACT, 256>), dim3(grid), dim3(256), 0, s, args...);
+}
+
+// the hand-off selection serves single-GPU steps whose zone fits one workgroup
+inline bool hs_mode(const gbpe_trainer* t, const SpGrid& g) {
+    const uint32_t bt = g.bt >= 1023 ? 1024u : 256u;
+    return t->hs_on && t->hs_rec && t->part && !t->sharded && g.zone1 == 1u && g.refresh <= (uint32_t)HS_PPT * bt;
 }
 
 template <typename S>
@@ -378,6 +398,36 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const uint32_t z1 = g.zone1;   // k_body's own zone workgroups
     const int bt = inbody ? 2048 : g.bt;
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
+    if (hs_mode(t, g)) {   // block 0 selects and hands off; no k_refresh after the merge
+        HsView hv;
+        hv.rec = t->hs_rec;
+        hv.part = t->part;
+        hv.npart = g.refresh;
+        hv.per = (uint32_t)gbpe_div_up(t->tb.nblk, g.refresh);
+        hv.tag = ++t->hs_seq;
+        hv.clog = t->d_clog;
+        hv.stat = t->hs_stat;
+        Table tbh = t->tb;
+        tbh.bpart = t->part;
+        tbh.bper = hv.per;
+        if (exact)
+            launch_body<S, true, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, tbh,
+                                 g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
+                                 (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, tbh, sel_single(t),
+                                 sp_mul(t), (ZSegState*)t->zseg, hv);
+        else
+            launch_body<S, false, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, tbh,
+                                  g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
+                                  (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, tbh, sel_single(t),
+                                  sp_mul(t), (ZSegState*)t->zseg, hv);
+        if (timing) {
+            TR_HIP(t, hipEventRecord(ev[3], s));
+            TR_HIP(t, hipEventRecord(ev[2], s));
+            TR_HIP(t, hipEventRecord(ev[4], s));
+        }
+        GBPE_LAUNCH_CHECK(t->ctx);
+        return GBPE_OK;
+    }
     if (exact)
         launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
@@ -1046,6 +1096,12 @@ int sp_init_states(gbpe_trainer* t, uint64_t cap, uint32_t Zs, uint32_t z, uint3
         TR_HIP(t, hipMalloc(&t->zseg, sizeof(ZSegState)));
         TR_HIP(t, hipMemsetAsync(t->zseg, 0, sizeof(ZSegState), t->ctx->stream));
     }
+    if (!t->hs_rec && !t->sharded) {   // hand-off granules (tag 0 is never handed out) + counters
+        TR_HIP(t, hipMalloc(&t->hs_rec, 64));
+        TR_HIP(t, hipMemsetAsync(t->hs_rec, 0, 64, t->ctx->stream));
+        TR_HIP(t, hipMalloc(&t->hs_stat, 16));
+        TR_HIP(t, hipMemsetAsync(t->hs_stat, 0, 16, t->ctx->stream));
+    }
     if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
     return GBPE_OK;
 }
@@ -1269,6 +1325,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     if (const char* e = getenv("GBPE_ZONE_SEG")) t->zseg_mode = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_ZONE_F")) t->zone_f = std::max<uint32_t>(3, (uint32_t)strtoul(e, nullptr, 10));
     if (const char* e = getenv("GBPE_ZDR")) t->zdr_on = atoi(e) != 0;
+    if (const char* e = getenv("GBPE_HS")) t->hs_on = atoi(e) != 0;
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
         t->trace = fopen(e, "w");
