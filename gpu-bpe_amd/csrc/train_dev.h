@@ -2425,7 +2425,9 @@ __device__ __forceinline__ bool hs_select(DevState* st, DevState* zst, const HsV
                 // block's slots load with the group's block bounds (atomic loads: this
                 // workgroup may have tightened them); otherwise the bounds first
                 const uint32_t hb = (gbpe_fmix32(~(uint32_t)pg) & tb.mask) >> BLK_LOG2;
-                const bool guess = hb / per == g1;
+                // (first round only: a retry takes the bounds' order, which always tightens a
+                // stale bound; a guessed block need not be the stale one)
+                const bool guess = it == 0u && hb / per == g1;
                 const uint32_t hl = hb - g1 * per;
                 const uint32_t blk = g1 * per + (uint32_t)lane;
                 const bool inb = (uint32_t)lane < per && blk < tb.nblk;
