@@ -1,0 +1,12 @@
+# Round-3 closing run: every GPU test, smoke, the default bench line, and the
+# rocprof kernel stats of the bench (summaries only come back)
+set -e
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/r3_final_gt.log 2>&1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r3_final_smoke.log 2>&1
+timeout -k 10 600 python bench.py > gpurun_out/r3_final_bench.json 2> gpurun_out/r3_final_bench.err
+if [ -z "$SKIP_STATS" ]; then
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/final_prof -o run -- python3 bench.py --no-cpu --steps 2 > gpurun_out/r3_final_bench_rocprof.json 2> gpurun_out/r3_final_bench_rocprof.err
+mkdir -p gpurun_out/r3_final_prof && find /tmp/final_prof -name '*stats.csv' -exec cp {} gpurun_out/r3_final_prof/ \;
+fi
