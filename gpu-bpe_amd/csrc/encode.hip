@@ -258,223 +258,6 @@ __global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v5(const uint8_t* __rest
     counts[chunk] = cnt;
 }
 
-// ── segmented walk: K lanes per chunk (intra-chunk parallelism) ──
-// A lane's cost grows with the bytes it walks serially (the v5 walk at cs = 64
-// takes 2.94 ms on C3 against 4.0 ms at the reference's cs = 512), so each chunk
-// is cut into K segments of S = cs / K bytes, one lane each:
-//   1. every lane walks greedily from its segment's first byte (lane 0 from the
-//      chunk start: exact) and emits the tokens that start inside its segment
-//      into its own scratch region (2S entries), recording those token starts in
-//      an S-bit map; its exit is the first token boundary at or past the
-//      segment end;
-//   2. lane j continues the true path from its exit, one token at a time
-//      (appended to its region), until the boundary it stands on is one of lane
-//      j+1's recorded starts: greedy longest match from a boundary depends only
-//      on the bytes after it, so from there on lane j+1's tokens ARE the true
-//      ones (its tokens before that point are dropped);
-//   3. a chunk where some lane's continuation runs past the next segment without
-//      meeting a recorded start (periodic text out of phase with the segment
-//      length), or overflows its region, is walked again serially by its lane 0.
-// meta[lane] = (first kept token << 16) | kept tokens of the lane's region;
-// counts[chunk] = the chunk's token total (for the scan).
-template <typename T, int K, int NWB, int WPE>   // NWB = S / 32 bitmap words per lane
-__global__ __launch_bounds__(WALK_TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void k_trie_walk_seg(const uint8_t* __restrict__ in, uint64_t n, uint32_t cs,
-                                                            const uint2* __restrict__ rec, uint32_t nrec,
-                                                            uint32_t root_base, T* __restrict__ scratch,
-                                                            uint32_t* __restrict__ counts, uint32_t* __restrict__ meta,
-                                                            uint64_t nchunks) {
-    constexpr uint32_t PER = 16 / sizeof(T);
-    constexpr uint32_t S = 32u * NWB;   // segment bytes (the host launches this form for cs == K * S)
-    __shared__ uint2 lut[256];
-    __shared__ uint32_t sbits[WALK_TPB][NWB];
-    __shared__ uint32_t ssync[WALK_TPB];
-    __shared__ uint32_t sfail[WALK_TPB / K];
-    {
-        const uint32_t t = root_base + threadIdx.x;
-        lut[threadIdx.x] = t < nrec ? rec[t] : make_uint2(0x3FFFFFu, 0u);
-        ssync[threadIdx.x] = 0xFFFFFFFFu;
-        if (threadIdx.x < WALK_TPB / K) sfail[threadIdx.x] = 0u;
-    }
-    __syncthreads();
-    const uint64_t gt = (uint64_t)blockIdx.x * WALK_TPB + threadIdx.x;
-    const uint64_t chunk = gt / K;
-    const uint32_t j = (uint32_t)(gt % K), lc = threadIdx.x / K;
-    const bool live = chunk < nchunks;
-    const uint64_t c0 = chunk * cs;
-    const uint32_t ce = live ? (uint32_t)(min(c0 + cs, n) - c0) : 0u;
-    const uint32_t s0 = j * S, se = min(s0 + S, ce), s1 = s0 + S;
-    T* out = scratch + chunk * 2ull * cs + (uint64_t)j * 2u * S;   // this lane's region (2S entries)
-    uint32_t cb = ~0u;
-    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
-    uint4 acc = make_uint4(0, 0, 0, 0);
-    uint32_t cnt = 0, ns = 0, pos = s0, bits[NWB];
-#pragma unroll
-    for (int w = 0; w < NWB; ++w) bits[w] = 0u;
-    bool fail = false;
-    auto byte_at = [&](uint32_t p) -> uint32_t {
-        const uint32_t bb = p & ~63u;
-        if (bb != cb) {
-            cb = bb;
-            const Win64 w = load_win64(in, n, c0 + bb);
-            q0 = w.q0;
-            q1 = w.q1;
-            q2 = w.q2;
-            q3 = w.q3;
-        }
-        // (explicit selects over four named vectors: an indexed window spilled to scratch)
-        const uint32_t o = p & 63u;
-        const uint4 h0 = (o & 16u) ? q1 : q0, h1 = (o & 16u) ? q3 : q2;
-        const uint4 q = (o & 32u) ? h1 : h0;
-        const uint32_t d = (o & 8u) ? ((o & 4u) ? q.w : q.z) : ((o & 4u) ? q.y : q.x);
-        return (d >> ((o & 3u) * 8u)) & 0xFFu;
-    };
-    auto emit = [&](uint32_t tok) {
-        vec_put<T>(acc, cnt % PER, tok);
-        if (++cnt % PER == 0) {
-            *reinterpret_cast<uint4*>(out + cnt - PER) = acc;
-            acc = make_uint4(0, 0, 0, 0);
-        }
-    };
-#pragma unroll 1
-    for (int ph = 0; ph < 3; ++ph) {   // (wave-uniform) 0 segment, 1 continuation, 2 serial redo
-        bool act;
-        if (ph == 0) {
-            act = live;
-        } else if (ph == 1) {
-            act = live && j + 1 < K && s1 < ce;
-        } else {
-            act = live && sfail[lc] != 0u && j == 0;
-            if (act) {   // tokens contiguous from the chunk base (2 cs entries hold them)
-                cnt = 0;
-                acc = make_uint4(0, 0, 0, 0);
-                pos = 0;
-            }
-        }
-        // v5's one-byte-per-trip state machine; the phase's stop tests run at token starts
-        bool walking = false;
-        uint32_t st = 0, base = 0, lmt = TID_NONE, lmp = 0, wp = 0, first = 0;
-        while (act) {
-            if (!walking) {
-                if (ph == 0) {
-                    if (pos >= se) break;
-                    const uint32_t rel = pos - s0;
-#pragma unroll
-                    for (int w = 0; w < NWB; ++w)
-                        if ((rel >> 5) == (uint32_t)w) bits[w] |= 1u << (rel & 31u);
-                } else if (ph == 1) {
-                    if (pos >= ce) {   // the chunk ended: none of the next lane's tokens is kept
-                        ssync[threadIdx.x + 1] = ce;
-                        break;
-                    }
-                    const uint32_t rel = pos - s1;
-                    if (rel >= S || cnt >= 2u * S - 1u) {   // past the next segment (or the region is full)
-                        fail = true;
-                        break;
-                    }
-                    if ((sbits[threadIdx.x + 1][rel >> 5] >> (rel & 31u)) & 1u) {
-                        ssync[threadIdx.x + 1] = pos;
-                        break;
-                    }
-                } else if (pos >= ce) {
-                    break;
-                }
-                first = byte_at(pos);
-                const uint2 e = lut[first];
-                const uint32_t tid = rec_tid(e);
-                if (rec_check(e) != 0u || rec_base(e) == 0u || pos + 1 >= ce) {
-                    emit(rec_check(e) == 0u && tid != TID_NONE ? tid : first);
-                    ++pos;
-                    continue;
-                }
-                st = root_base + first;
-                base = rec_base(e);
-                lmt = tid;
-                lmp = pos + 1;
-                wp = pos + 1;
-                walking = true;
-            }
-            const uint32_t t = base + byte_at(wp);
-            const uint2 r = t < nrec ? rec[t] : make_uint2(0x3FFFFFu, 0u);
-            bool end = true;
-            if (rec_check(r) == st) {
-                st = t;
-                base = rec_base(r);
-                ++wp;
-                const uint32_t tid = rec_tid(r);
-                if (tid != TID_NONE) {
-                    lmt = tid;
-                    lmp = wp;
-                }
-                end = base == 0u || wp >= ce;
-            }
-            if (end) {
-                const bool hit = lmt != TID_NONE;
-                emit(hit ? lmt : first);
-                pos = hit ? lmp : pos + 1;
-                walking = false;
-            }
-        }
-        if (ph == 0) {   // publish the recorded starts
-            ns = cnt;
-#pragma unroll
-            for (int w = 0; w < NWB; ++w) sbits[threadIdx.x][w] = bits[w];
-        } else if (ph == 1) {   // a lane without a sync point (or a failed continuation): redo the chunk
-            if (fail || (live && j > 0 && s0 < ce && ssync[threadIdx.x] == 0xFFFFFFFFu)) sfail[lc] = 1u;
-        }
-        __syncthreads();
-        if (ph == 1) __syncthreads();   // (the failure flags are complete before phase 2 reads them)
-    }
-    uint32_t first_kept = 0, kept = 0;
-    const bool redo = live && sfail[lc] != 0u;
-    if (redo) {
-        kept = j == 0 ? cnt : 0u;
-    } else if (live && s0 < ce) {
-        if (j > 0) {   // drop the speculative tokens before the sync point
-            const uint32_t rel = ssync[threadIdx.x] - s0;
-            uint32_t sk = 0;
-#pragma unroll
-            for (int w = 0; w < NWB; ++w) {
-                const uint32_t lo = (uint32_t)w * 32u;
-                if (rel >= lo + 32u) sk += (uint32_t)__popc(bits[w]);
-                else if (rel > lo) sk += (uint32_t)__popc(bits[w] & ((1u << (rel - lo)) - 1u));
-            }
-            first_kept = sk < ns ? sk : ns;
-        }
-        kept = cnt - first_kept;
-    }
-    if (live && cnt % PER && (!redo || j == 0)) *reinterpret_cast<uint4*>(out + (cnt / PER) * PER) = acc;
-    if (live) meta[gt] = (first_kept << 16) | kept;
-    uint32_t tot = kept;   // the chunk total: its K lanes are consecutive lanes of one wave
-#pragma unroll
-    for (int off = 1; off < K; off <<= 1) tot += __shfl_xor(tot, off);
-    if (live && j == 0) counts[chunk] = tot;
-}
-
-// the segmented walk's tokens → final positions: one wave per chunk, its K
-// regions in order (each region's kept tokens are contiguous)
-template <typename T, int K>
-__global__ __launch_bounds__(256) void k_chunk_compact_seg(const T* __restrict__ scratch, const uint32_t* __restrict__ meta,
-                                                           const uint32_t* __restrict__ local,
-                                                           const uint64_t* __restrict__ blocksum, uint64_t nchunks,
-                                                           uint32_t cs, uint32_t* __restrict__ out, uint64_t out_cap) {
-    const uint64_t chunk = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-    const uint32_t lane = threadIdx.x & 63;
-    if (chunk >= nchunks) return;
-    uint32_t m = lane < (uint32_t)K ? meta[chunk * K + lane] : 0u;
-    const uint32_t S = cs / K;
-    uint64_t off = blocksum[chunk / SCAN_BLK] + local[chunk];
-    const T* base = scratch + chunk * 2ull * cs;
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        const uint32_t mj = __shfl(m, j);
-        const uint32_t st = mj >> 16, kp = mj & 0xFFFFu;
-        const T* src = base + (uint64_t)j * 2u * S + st;
-        for (uint32_t i = lane; i < kp; i += 64)
-            if (off + i < out_cap) out[off + i] = (uint32_t)src[i];
-        off += kp;
-    }
-}
-
 // Chunk tokens → final positions.  A wave moves CPW chunks at once (every
 // scratch load of the CPW chunks is issued before the first store: one chunk's
 // ~cs/4 tokens alone leave too few bytes in flight to cover the HBM latency);
@@ -692,21 +475,14 @@ int encode_device_impl(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* d_in, uint64
     const bool narrow = tr->max_token_id < 65536u;   // raw-byte fallbacks are < 256
     const uint64_t esz = narrow ? 2 : 4;
     const uint64_t nblk = gbpe_div_up(nchunks, SCAN_BLK);
-    // segmented walk (K lanes per chunk, GBPE_WALK_SEG = K): packed narrow tries, S = cs / K
-    // a multiple of 8 in [32, 256]
-    const char* segk_s = getenv("GBPE_WALK_SEG");   // (read per call: tests switch it)
-    const int segk_env = segk_s ? atoi(segk_s) : 0;
-    const uint32_t segk = (segk_env == 4 || segk_env == 8) ? (uint32_t)segk_env : 0u;
-    const bool seg = segk && tr->rec2 && narrow && (cs == segk * 64u || cs == segk * 128u);
-    int rc = grow(ctx, &ctx->enc_scratch, &ctx->enc_scratch_bytes, nchunks * cs * esz * (seg ? 2 : 1) + 16);
+    int rc = grow(ctx, &ctx->enc_scratch, &ctx->enc_scratch_bytes, nchunks * cs * esz + 16);
     if (rc == GBPE_OK)
-        rc = grow(ctx, &ctx->enc_counts, &ctx->enc_counts_bytes, nchunks * 8 + nblk * 8 + 64 + (seg ? nchunks * segk * 4 : 0));
+        rc = grow(ctx, &ctx->enc_counts, &ctx->enc_counts_bytes, nchunks * 8 + nblk * 8 + 64);
     if (rc != GBPE_OK) return rc;
     uint32_t* counts = (uint32_t*)ctx->enc_counts;
     uint32_t* local = counts + nchunks;
     uint64_t* blocksum = (uint64_t*)(((uintptr_t)(local + nchunks) + 15) & ~(uintptr_t)15);
     uint64_t* d_total = blocksum + nblk + 1;
-    uint32_t* meta = (uint32_t*)(d_total + 2);
     const uint32_t gw = (uint32_t)gbpe_div_up(nchunks, WALK_TPB);
     GBPE_HIP(ctx, hipEventRecord(ctx->ev[0], s));
     // the packed-record state-machine walk when the trie packs and chunks are whole
@@ -714,20 +490,7 @@ int encode_device_impl(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* d_in, uint64
     // plain per-token walk over 16-byte records
     const bool packed = (cs % 8u) == 0u && tr->rec2;
     const uint32_t nrec2 = tr->nrec + 256;
-    const uint32_t gseg = (uint32_t)gbpe_div_up(nchunks * (seg ? segk : 1u), WALK_TPB);
-    const char* wpe_s = getenv("GBPE_WALK_SEG_WPE");
-    const int wpe = wpe_s ? atoi(wpe_s) : 0;
-#define GBPE_SEG_WALK(K_, W_, E_)                                                                                \
-    hipLaunchKernelGGL((k_trie_walk_seg<uint16_t, K_, W_, E_>), dim3(gseg), dim3(WALK_TPB), 0, s, d_in, n, cs,        \
-                       tr->rec2, nrec2, tr->root_base, (uint16_t*)ctx->enc_scratch, counts, meta, nchunks)
-    if (seg && segk == 8 && cs == 512u) GBPE_SEG_WALK(8, 2, 1);
-    else if (seg && segk == 8) GBPE_SEG_WALK(8, 4, 1);
-    else if (seg && cs == 256u) GBPE_SEG_WALK(4, 2, 1);
-    else if (seg && wpe == 8) GBPE_SEG_WALK(4, 4, 8);
-    else if (seg && wpe == 6) GBPE_SEG_WALK(4, 4, 6);
-    else if (seg) GBPE_SEG_WALK(4, 4, 1);
-#undef GBPE_SEG_WALK
-    else if (packed && narrow)
+    if (packed && narrow)
         hipLaunchKernelGGL(k_trie_walk_v5<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
                            tr->root_base, (uint16_t*)ctx->enc_scratch, counts, nchunks);
     else if (packed)
@@ -747,15 +510,7 @@ int encode_device_impl(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* d_in, uint64
     GBPE_LAUNCH_CHECK(ctx);
     GBPE_HIP(ctx, hipEventRecord(ctx->ev[2], s));
     const uint32_t gc4 = (uint32_t)gbpe_div_up(nchunks, 4 * CPW);
-    if (seg && segk == 8)
-        hipLaunchKernelGGL((k_chunk_compact_seg<uint16_t, 8>), dim3((uint32_t)gbpe_div_up(nchunks, 4)), dim3(256), 0, s,
-                           (const uint16_t*)ctx->enc_scratch, (const uint32_t*)meta, (const uint32_t*)local,
-                           (const uint64_t*)blocksum, nchunks, cs, d_out, out_cap);
-    else if (seg)
-        hipLaunchKernelGGL((k_chunk_compact_seg<uint16_t, 4>), dim3((uint32_t)gbpe_div_up(nchunks, 4)), dim3(256), 0, s,
-                           (const uint16_t*)ctx->enc_scratch, (const uint32_t*)meta, (const uint32_t*)local,
-                           (const uint64_t*)blocksum, nchunks, cs, d_out, out_cap);
-    else if (narrow)
+    if (narrow)
         hipLaunchKernelGGL(k_chunk_compact4<uint16_t>, dim3(gc4), dim3(256), 0, s, (const uint16_t*)ctx->enc_scratch,
                            (const uint32_t*)counts, (const uint32_t*)local, (const uint64_t*)blocksum, nchunks, cs, d_out,
                            out_cap);

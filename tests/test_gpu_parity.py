@@ -307,31 +307,6 @@ def test_encode_host_pipeline_slices(eng, cs, monkeypatch):
     tok.destroy()
 
 
-@pytest.mark.parametrize("segk", ["8", "4"])
-def test_encode_segmented_walk(eng, segk, monkeypatch):
-    """The segmented walk (GBPE_WALK_SEG = K lanes per chunk): every chunk size it
-    serves (cs = 64K or 128K bytes: 256, 512, 1024), text where the lanes' guesses
-    meet the true path, periodic text whose token length never divides the
-    segment (each lane's guess stays out of phase: the serial redo), long runs of
-    one byte, random bytes and ragged last chunks — all equal the oracle."""
-    from gpubpe import TrieTokenizer, synth
-    monkeypatch.setenv("GBPE_WALK_SEG", segk)
-    train = synth.multilingual(80000, seed=31)
-    vocab = O.vocab_from_merges(O.train(train, 1200, compaction="exact")["merges"]).entries
-    per3 = O.vocab_from_merges([[97, 98], [256, 99]]).entries          # "abc" one token: period 3
-    rng = np.random.default_rng(5)
-    texts = [synth.multilingual(150000, seed=34), b"abc" * 20000, b"abcab" * 9000 + b"x",
-             b"a" * 70001, bytes(rng.integers(0, 256, size=65537, dtype=np.uint8)),
-             synth.english(4099, seed=35)]
-    for cs in (256, 512, 1024):
-        for voc in (vocab, per3):
-            tok = TrieTokenizer.from_vocab(eng, voc, chunk_size=cs)
-            for text in texts:
-                got = tok.encode_bytes(text)
-                assert np.array_equal(got, _oracle_encode(voc, text, cs)), (cs, len(text), text[:12])
-            tok.destroy()
-
-
 def test_encode_edge_cases(eng):
     from gpubpe import TrieTokenizer
     vocab = O.vocab_from_merges([[116, 104], [256, 101], [32, 257]]).entries
