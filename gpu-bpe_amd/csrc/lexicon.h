@@ -101,36 +101,46 @@ __device__ __forceinline__ unsigned long long lx_hash(const S* __restrict__ x, u
 
 __device__ __forceinline__ uint32_t lx_home(unsigned long long h, uint32_t mask) { return (uint32_t)(h ^ (h >> 32)) & mask; }
 
+// Word-table slot: the 64-bit key with its value in the same 16 bytes, so a
+// probe's one line fetch brings both (the table is far larger than the caches
+// at 1 GiB, and separate key / value arrays cost two random lines per word).
+struct alignas(16) LxSlot {
+    unsigned long long key;   // 0 = empty
+    uint32_t rep;             // a representative occurrence (word index)
+    uint32_t cnt;             // occurrences; the uid once k_lx_tabuid ran
+};
+
 // global word table (linear probing on 64-bit keys): insert-or-add `c` occurrences
-__device__ bool lx_insert(unsigned long long* __restrict__ keys, uint2* __restrict__ vals, uint32_t P,
-                          unsigned long long h, uint32_t rep, uint32_t c) {
+__device__ bool lx_insert(LxSlot* __restrict__ wt, uint32_t P, unsigned long long h, uint32_t rep, uint32_t c) {
     uint32_t slot = lx_home(h, P - 1);
     for (uint32_t p = 0; p < LX_PROBES; ++p, slot = (slot + 1) & (P - 1)) {
-        unsigned long long k = __hip_atomic_load(&keys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long k = __hip_atomic_load(&wt[slot].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k == 0ull) {
-            k = atomicCAS(&keys[slot], 0ull, h);
+            k = atomicCAS(&wt[slot].key, 0ull, h);
             if (k == 0ull) {
-                vals[slot].x = rep;   // any occurrence represents the word
-                atomicAdd(&vals[slot].y, c);
+                wt[slot].rep = rep;   // any occurrence represents the word
+                atomicAdd(&wt[slot].cnt, c);
                 return true;
             }
         }
         if (k == h) {
-            atomicAdd(&vals[slot].y, c);
+            atomicAdd(&wt[slot].cnt, c);
             return true;
         }
     }
     return false;
 }
 
-__device__ uint32_t lx_find(const unsigned long long* __restrict__ keys, uint32_t P, unsigned long long h) {
+// the slot of key h (its whole 16 bytes in one load), or SP_INV in .z
+__device__ uint4 lx_find(const LxSlot* __restrict__ wt, uint32_t P, unsigned long long h) {
     uint32_t slot = lx_home(h, P - 1);
     for (uint32_t p = 0; p < LX_PROBES; ++p, slot = (slot + 1) & (P - 1)) {
-        const unsigned long long k = keys[slot];
-        if (k == h) return slot;
-        if (k == 0ull) return SP_INV;
+        const uint4 v = *reinterpret_cast<const uint4*>(&wt[slot]);
+        const unsigned long long k = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+        if (k == h) return v;
+        if (k == 0ull) break;
     }
-    return SP_INV;
+    return make_uint4(0u, 0u, SP_INV, SP_INV);
 }
 
 // Word multiplicities: every workgroup aggregates 4096 words in an LDS table
@@ -142,7 +152,7 @@ __device__ uint32_t lx_find(const unsigned long long* __restrict__ keys, uint32_
 // concatenation of word stores, each word carrying its multiplicity.
 template <typename S>
 __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32_t len, const uint32_t* __restrict__ wpos,
-                                                 uint32_t nw, unsigned long long* __restrict__ keys, uint2* __restrict__ vals,
+                                                 uint32_t nw, LxSlot* __restrict__ wtab,
                                                  uint32_t P, uint32_t* __restrict__ otmp, uint32_t* __restrict__ longs,
                                                  uint32_t* __restrict__ ctr, const uint32_t* __restrict__ wmul = nullptr) {
     __shared__ unsigned long long lk[LX_LT];
@@ -184,22 +194,27 @@ __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32
                 done = true;
             }
         }
-        if (!done && !lx_insert(keys, vals, P, h, (uint32_t)j, wt)) ctr[1] = 1u;
+        if (!done && !lx_insert(wtab, P, h, (uint32_t)j, wt)) ctr[1] = 1u;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < LX_LT; i += TPB)
-        if (lk[i] && !lx_insert(keys, vals, P, lk[i], lr[i], lc[i])) ctr[1] = 1u;
+        if (lk[i] && !lx_insert(wtab, P, lk[i], lr[i], lc[i])) ctr[1] = 1u;
 }
 
 constexpr uint32_t LX_TB = TPB * 16;   // word-table slots per uid-assignment block
 
-__global__ __launch_bounds__(TPB) void k_lx_tabcount(const unsigned long long* __restrict__ keys, uint32_t P,
-                                                     uint32_t* __restrict__ cnt) {
+// slot k of thread t in block b: b * LX_TB + k * TPB + t (lane-contiguous, so every
+// load instruction of a wave reads 1 KB in one piece)
+__device__ __forceinline__ uint64_t lx_tslot(uint32_t k) { return (uint64_t)blockIdx.x * LX_TB + (uint64_t)k * TPB + threadIdx.x; }
+
+__global__ __launch_bounds__(TPB) void k_lx_tabcount(const LxSlot* __restrict__ wt, uint32_t P, uint32_t* __restrict__ cnt) {
     __shared__ uint32_t s[TPB / 64];
-    const uint64_t b0 = (uint64_t)blockIdx.x * LX_TB + (uint64_t)threadIdx.x * 16;
     uint32_t c = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) c += (b0 + k < P && keys[b0 + k]) ? 1u : 0u;
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t i = lx_tslot(k);
+        c += (i < P && wt[i].key) ? 1u : 0u;
+    }
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
     __syncthreads();
@@ -215,19 +230,24 @@ __device__ __forceinline__ uint32_t lx_wlen(const uint32_t* __restrict__ wpos, u
     return (j + 1 < nw ? wpos[j + 1] : len) - wpos[j];
 }
 
-// uids in slot order: usz = length + 1 (its separator), umul = occurrences,
-// urep = a representative's position; the slot's count becomes the uid
-__global__ __launch_bounds__(TPB) void k_lx_tabuid(const unsigned long long* __restrict__ keys, uint2* __restrict__ vals,
-                                                   uint32_t P, const uint32_t* __restrict__ bpre,
+// uids by block, then thread, then the thread's slots (lx_tslot): usz = length + 1
+// (its separator), umul = occurrences, urep = a representative's position; the
+// slot's count becomes the uid
+__global__ __launch_bounds__(TPB) void k_lx_tabuid(LxSlot* __restrict__ wt, uint32_t P, const uint32_t* __restrict__ bpre,
                                                    const uint64_t* __restrict__ bblk, const uint32_t* __restrict__ wpos,
                                                    uint32_t nw, uint32_t len, uint32_t* __restrict__ usz,
                                                    uint32_t* __restrict__ umul, uint32_t* __restrict__ urep) {
     __shared__ uint32_t s[TPB / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t b0 = (uint64_t)blockIdx.x * LX_TB + (uint64_t)threadIdx.x * 16;
     uint32_t occ = 0;
+    uint2 v[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) occ |= ((b0 + k < P && keys[b0 + k]) ? 1u : 0u) << k;
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t i = lx_tslot(k);
+        const uint4 e = i < P ? *reinterpret_cast<const uint4*>(&wt[i]) : make_uint4(0u, 0u, 0u, 0u);
+        v[k] = make_uint2(e.z, e.w);
+        occ |= ((e.x | e.y) ? 1u : 0u) << k;
+    }
     const uint32_t c = (uint32_t)__popc(occ);
     uint32_t incl = c;
     for (int off = 1; off < 64; off <<= 1) {
@@ -238,13 +258,13 @@ __global__ __launch_bounds__(TPB) void k_lx_tabuid(const unsigned long long* __r
     __syncthreads();
     uint32_t u = bpre[blockIdx.x] + (uint32_t)bblk[blockIdx.x / SCAN_BLK] + incl - c;
     for (int w = 0; w < wid; ++w) u += s[w];
-    for (uint32_t r = occ; r; r &= r - 1) {
-        const uint64_t slot = b0 + (uint64_t)(__ffs(r) - 1);
-        const uint2 v = vals[slot];
-        usz[u] = lx_wlen(wpos, nw, len, v.x) + 1u;
-        umul[u] = v.y;
-        urep[u] = wpos[v.x];
-        vals[slot].y = u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (!((occ >> k) & 1u)) continue;
+        usz[u] = lx_wlen(wpos, nw, len, v[k].x) + 1u;
+        umul[u] = v[k].y;
+        urep[u] = wpos[v[k].x];
+        wt[lx_tslot(k)].cnt = u;
         ++u;
     }
 }
@@ -299,8 +319,8 @@ __global__ void k_lx_secstart(const uint32_t* __restrict__ upre, const uint64_t*
 // fails the build instead of merging two different words)
 template <typename S>
 __global__ void k_lx_occ(const S* __restrict__ x, const uint32_t* __restrict__ wpos, uint32_t nw, uint32_t len,
-                         const uint32_t* __restrict__ otmp, const unsigned long long* __restrict__ keys,
-                         const uint2* __restrict__ vals, uint32_t P, const uint32_t* __restrict__ urep,
+                         const uint32_t* __restrict__ otmp, const LxSlot* __restrict__ wt,
+                         uint32_t P, const uint32_t* __restrict__ urep,
                          const uint32_t* __restrict__ usz, uint32_t nshort, uint32_t uid_base, uint32_t* __restrict__ occ,
                          uint32_t* __restrict__ ctr) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -315,11 +335,11 @@ __global__ void k_lx_occ(const S* __restrict__ x, const uint32_t* __restrict__ w
         return;
     }
     const uint32_t s = wpos[j], L = lx_wlen(wpos, nw, len, (uint32_t)j);
-    const uint32_t slot = lx_find(keys, P, lx_hash<S>(x, s, L));
-    bool ok = slot != SP_INV;
+    const uint4 e = lx_find(wt, P, lx_hash<S>(x, s, L));
+    bool ok = (e.x | e.y) != 0u;
     uint32_t u = 0;
     if (ok) {
-        u = vals[slot].y;
+        u = e.w;
         const uint32_t r = urep[u];
         ok = usz[u] == L + 1u;
         for (uint32_t i = 0; ok && i < L; ++i) ok = x[r + i] == x[s + i];

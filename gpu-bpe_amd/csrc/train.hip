@@ -184,7 +184,13 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         d_ws = d_gpt4;
     }
     const uint32_t gb = (uint32_t)gbpe_div_up(n, TPB);
-    if (t->u16)
+    const bool vec = ((uintptr_t)d_bytes & 15u) == 0 && ((uintptr_t)d_ws & 15u) == 0;   // (null is aligned)
+    const uint32_t gv = (uint32_t)gbpe_div_up(gbpe_div_up(n, 16), TPB);
+    if (t->u16 && vec)
+        hipLaunchKernelGGL(k_symbols_v<uint16_t>, dim3(gv), dim3(TPB), 0, s, d_bytes, d_ws, (uint16_t*)t->buf[0], n);
+    else if (vec)
+        hipLaunchKernelGGL(k_symbols_v<uint32_t>, dim3(gv), dim3(TPB), 0, s, d_bytes, d_ws, (uint32_t*)t->buf[0], n);
+    else if (t->u16)
         hipLaunchKernelGGL(k_symbols<uint16_t>, dim3(gb), dim3(TPB), 0, s, d_bytes, d_ws, (uint16_t*)t->buf[0], n,
                            (uint8_t*)nullptr);
     else
@@ -300,8 +306,8 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     DevState* hs = t->h_st;
     hs->merges_done = 0;
     hs->budget = k;
-    TR_HIP(t, hipMemcpyAsync(&t->st->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    TR_HIP(t, hipMemcpyAsync(&t->st->budget, &hs->budget, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    if (t->sp) hs->sel_round = 0;
+    hipLaunchKernelGGL(k_step_in, dim3(1), dim3(1), 0, s, t->st, t->sp ? t->zst : (DevState*)nullptr, k);
 #ifdef GBPE_KTRACE
     if (getenv("GBPE_KTRACE_OUT")) {
         static unsigned long long* kbuf = nullptr;
@@ -315,11 +321,6 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         TR_HIP(t, hipMemcpyToSymbolAsync(HIP_SYMBOL(g_kt_base), &kb, 4, 0, hipMemcpyHostToDevice, s));
     }
 #endif
-    if (t->sp) {
-        hs->sel_round = 0;
-        TR_HIP(t, hipMemcpyAsync(&t->zst->merges_done, &hs->merges_done, sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        TR_HIP(t, hipMemcpyAsync(&t->st->sel_round, &hs->sel_round, sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    }
     const uint64_t ntiles = gbpe_div_up(t->n, TILE);
     // tile blocks + stale-tail blocks (the window is at most mc <= n/2 symbols)
     const uint32_t g_tail = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
@@ -421,12 +422,13 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
                                    t->zseg);
             GBPE_LAUNCH_CHECK(t->ctx);
         }
-        if (sparse) hipLaunchKernelGGL(k_live, dim3(1), dim3(1024), 0, s, t->st, t->tb);
+        // the read-backs (and, sparse, k_live's count) in one launch: no copy blits
+        const bool cl = sparse && t->d_clog;
+        hipLaunchKernelGGL(k_step_out, dim3(1), dim3(1024), 0, s, t->st, sparse ? t->zst : (DevState*)nullptr, t->tb,
+                           sparse ? 1 : 0, (const uint32_t*)t->d_log, k * 4u, (const uint32_t*)(cl ? t->d_clog : nullptr),
+                           cl ? k * 2u : 0u, t->h_st, t->h_zst, t->h_log, cl ? t->h_clog : (uint32_t*)nullptr);
+        GBPE_LAUNCH_CHECK(t->ctx);
     }
-    TR_HIP(t, hipMemcpyAsync(t->h_st, t->st, sizeof(DevState), hipMemcpyDeviceToHost, s));
-    TR_HIP(t, hipMemcpyAsync(t->h_log, t->d_log, (size_t)k * 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    if (sparse) TR_HIP(t, hipMemcpyAsync(t->h_zst, t->zst, sizeof(DevState), hipMemcpyDeviceToHost, s));
-    if (sparse && t->d_clog) TR_HIP(t, hipMemcpyAsync(t->h_clog, t->d_clog, (size_t)k * 8, hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipStreamSynchronize(s));
     const uint32_t done = hs->merges_done;
     const uint32_t err = hs->err | (sparse ? t->h_zst->err : 0u);

@@ -412,6 +412,71 @@ __global__ __launch_bounds__(TPB) void k_symbols(const uint8_t* __restrict__ byt
     if (ws_out) ws_out[i] = ws ? 1 : 0;
 }
 
+// The same, 16 bytes per thread: one 16-byte load (+ the byte before it), the
+// symbols out as whole 16-byte vectors (the byte-per-thread form moved 1 GiB in
+// 3.5 ms, its 1- and 2-byte accesses bound by instruction issue).  Needs 16-byte
+// aligned bytes and word starts; the output buffer is padded to whole tiles.
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_symbols_v(const uint8_t* __restrict__ bytes, const uint8_t* __restrict__ ws_ext,
+                                                   S* __restrict__ out, uint64_t n) {
+    const uint64_t i0 = ((uint64_t)blockIdx.x * TPB + threadIdx.x) * 16u;
+    if (i0 >= n) return;
+    uint32_t by[16], we[16];
+    if (i0 + 16 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4*>(bytes + i0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) by[k] = (w[k >> 2] >> ((k & 3) * 8)) & 0xFFu;
+        if (ws_ext) {
+            const uint4 e = *reinterpret_cast<const uint4*>(ws_ext + i0);
+            const uint32_t f[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) we[k] = (f[k >> 2] >> ((k & 3) * 8)) & 0xFFu;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            by[k] = i0 + k < n ? bytes[i0 + k] : 0u;
+            we[k] = (ws_ext && i0 + k < n) ? ws_ext[i0 + k] : 0u;
+        }
+    }
+    uint32_t prev = i0 ? bytes[i0 - 1] : 0u;
+    uint32_t sym[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t tok = by[k];
+        bool ws;
+        if (ws_ext) {
+            ws = we[k] != 0u;
+        } else if (i0 + k == 0) {
+            ws = true;
+        } else {
+            const uint32_t c = byte_class(tok), p = byte_class(prev);
+            ws = c != p;
+            if (p == 2u && (c == 0u || c == 1u)) ws = false;
+            if (c == 2u && p != 2u) ws = true;
+            if (p == 4u || c == 4u) ws = true;
+        }
+        sym[k] = tok | (ws ? Sym<S>::WS : 0u);
+        prev = tok;
+    }
+    if (i0 + 16 <= n) {
+        if (sizeof(S) == 2) {
+            uint4* o = reinterpret_cast<uint4*>(out + i0);
+            o[0] = make_uint4(sym[0] | sym[1] << 16, sym[2] | sym[3] << 16, sym[4] | sym[5] << 16, sym[6] | sym[7] << 16);
+            o[1] = make_uint4(sym[8] | sym[9] << 16, sym[10] | sym[11] << 16, sym[12] | sym[13] << 16, sym[14] | sym[15] << 16);
+        } else {
+            uint4* o = reinterpret_cast<uint4*>(out + i0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = make_uint4(sym[4 * q], sym[4 * q + 1], sym[4 * q + 2], sym[4 * q + 3]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (i0 + k < n) out[i0 + k] = (S)sym[k];
+    }
+}
+
 // Full pair count of the current stream into the (cleared) table — once at
 // start and on table rebuilds.  Same counting rule as train.wgsl:393-399.
 template <typename S>
@@ -761,6 +826,55 @@ __global__ __launch_bounds__(1024) void k_live(DevState* st, Table tb) {
         st->live = live;
         if (live > st->max_live) st->max_live = live;
     }
+}
+
+// Step boundaries without copy engines: the host's four 4-byte resets and its
+// three read-backs (state, zone state, merge log) were each a blit on the
+// stream (~5 us apiece with their gaps, ~40 us per step); one thread sets the
+// counters, and one workgroup writes the read-backs straight into the pinned
+// host buffers (vector stores to host memory, a system-scope fence at the end).
+__global__ void k_step_in(DevState* st, DevState* zst, uint32_t k) {
+    st->merges_done = 0u;
+    st->budget = k;
+    if (zst) {
+        zst->merges_done = 0u;
+        st->sel_round = 0u;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_step_out(DevState* st, DevState* zst, Table tb, int live_too,
+                                                   const uint32_t* __restrict__ log, uint32_t nlog,
+                                                   const uint32_t* __restrict__ clog, uint32_t nclog,
+                                                   DevState* h_st, DevState* h_zst, uint32_t* h_log, uint32_t* h_clog) {
+    constexpr int NW = sizeof(DevState) / 4;
+    static_assert(NW <= 1024, "DevState fits one pass");
+    __shared__ uint32_t red[16];
+    __shared__ union {
+        DevState d;
+        uint32_t w[NW];
+    } g;
+    const uint32_t t = threadIdx.x;
+    uint32_t live = 0;
+    if (live_too) {   // k_live: live pairs from the per-block live counts
+        for (uint32_t i = t; i < tb.nblk; i += 1024) live += tb.blive[i];
+        for (int off = 32; off > 0; off >>= 1) live += __shfl_xor(live, off);
+        if ((t & 63) == 0) red[t >> 6] = live;
+    }
+    if (t < (uint32_t)NW) g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
+    __syncthreads();
+    if (live_too && t == 0) {
+        for (int w = 1; w < 16; ++w) live += red[w];
+        g.d.live = live;
+        if (live > g.d.max_live) g.d.max_live = live;
+        st->live = g.d.live;
+        st->max_live = g.d.max_live;
+    }
+    __syncthreads();
+    if (t < (uint32_t)NW) reinterpret_cast<uint32_t*>(h_st)[t] = g.w[t];
+    if (zst && t < (uint32_t)NW) reinterpret_cast<uint32_t*>(h_zst)[t] = reinterpret_cast<const uint32_t*>(zst)[t];
+    for (uint32_t i = t; i < nlog; i += 1024) h_log[i] = log[i];
+    for (uint32_t i = t; i < nclog; i += 1024) h_clog[i] = clog[i];
+    __threadfence_system();
 }
 
 // A merge is "active" for the stream kernels iff k_select logged it this round.

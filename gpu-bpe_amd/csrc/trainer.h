@@ -783,8 +783,7 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
     lp.umul = c.take<uint32_t>(nw + 1);
     lp.urep = c.take<uint32_t>(nw + 1);
     lp.occ = c.take<uint32_t>(nw + 1);
-    auto* keys = c.take<unsigned long long>(P);
-    auto* vals = c.take<uint2>(P);
+    auto* wtab = c.take<LxSlot>(P);
     uint32_t* bc = c.take<uint32_t>(nbb);
     uint64_t* bb = c.take<uint64_t>(nbb / SCAN_BLK + 4);
     lp.ublk = c.take<uint64_t>((uint64_t)nw / SCAN_BLK + 4);
@@ -794,13 +793,12 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
     lx_scan(s, tc, ntiles, tb);
     hipLaunchKernelGGL(k_lx_wpos<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, (const uint32_t*)tc,
                        (const uint64_t*)tb, lp.wpos);
-    TR_HIP(t, hipMemsetAsync(keys, 0, P * 8, s));
-    TR_HIP(t, hipMemsetAsync(vals, 0, P * 8, s));
+    TR_HIP(t, hipMemsetAsync(wtab, 0, P * sizeof(LxSlot), s));
     TR_HIP(t, hipMemsetAsync(ctr, 0, 32, s));
     if (nw)
         hipLaunchKernelGGL(k_lx_hash<S>, dim3((uint32_t)gbpe_div_up(nw, TPB * LX_WPT)), dim3(TPB), 0, s, seg, len,
-                           (const uint32_t*)lp.wpos, nw, keys, vals, (uint32_t)P, otmp, longs, ctr, wmul);
-    hipLaunchKernelGGL(k_lx_tabcount, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const unsigned long long*)keys, (uint32_t)P, bc);
+                           (const uint32_t*)lp.wpos, nw, wtab, (uint32_t)P, otmp, longs, ctr, wmul);
+    hipLaunchKernelGGL(k_lx_tabcount, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const LxSlot*)wtab, (uint32_t)P, bc);
     lx_scan(s, bc, nbb, bb);
     GBPE_LAUNCH_CHECK(t->ctx);
     uint32_t h[4] = {0, 0, 0, 0};
@@ -813,15 +811,14 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
     lp.nlong = h[0];
     lp.nu = lp.nshort + lp.nlong;
     if ((uint64_t)t->lx_nuid + lp.nu >= LX_LONG) return GBPE_OK;
-    hipLaunchKernelGGL(k_lx_tabuid, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const unsigned long long*)keys, vals, (uint32_t)P,
-                       (const uint32_t*)bc, (const uint64_t*)bb, (const uint32_t*)lp.wpos, nw, len, lp.usz, lp.umul, lp.urep);
+    hipLaunchKernelGGL(k_lx_tabuid, dim3((uint32_t)nbb), dim3(TPB), 0, s, wtab, (uint32_t)P, (const uint32_t*)bc, (const uint64_t*)bb, (const uint32_t*)lp.wpos, nw, len, lp.usz, lp.umul, lp.urep);
     if (lp.nlong)
         hipLaunchKernelGGL(k_lx_longs, dim3((uint32_t)gbpe_div_up(lp.nlong, 256)), dim3(256), 0, s, (const uint32_t*)longs,
                            (const uint32_t*)ctr, lp.nshort, (const uint32_t*)lp.wpos, nw, len, lp.usz, lp.umul, lp.urep,
                            wmul);
     if (nw)
         hipLaunchKernelGGL(k_lx_occ<S>, dim3((uint32_t)gbpe_div_up(nw, 256)), dim3(256), 0, s, seg, (const uint32_t*)lp.wpos, nw,
-                           len, (const uint32_t*)otmp, (const unsigned long long*)keys, (const uint2*)vals, (uint32_t)P,
+                           len, (const uint32_t*)otmp, (const LxSlot*)wtab, (uint32_t)P,
                            (const uint32_t*)lp.urep, (const uint32_t*)lp.usz, lp.nshort, t->lx_nuid, lp.occ, ctr);
     // store offsets: exclusive scan of the entry sizes, in otmp (k_lx_occ, queued
     // before on the same stream, has consumed it)

@@ -360,3 +360,45 @@ def test_train_large_vs_c_oracle(eng, exact):
     _assert_counts_match_stream(pairs, s)
     if not exact:
         assert st.tail_dropped == ref["tail_total"]
+
+
+@pytest.mark.parametrize("off", [0, 1, 7, 16])
+@pytest.mark.parametrize("n", [40_000, 40_013])
+def test_symbols_device_input_alignment(eng, off, n):
+    """Trainer creation from a device pointer at any byte offset and any length: the
+    16-byte symbol kernel (aligned input, whole vectors, a ragged last vector) and the
+    byte-per-thread one (unaligned input) give the reference's merges and stream."""
+    from gpubpe import _lib, synth
+    lib = _lib.load()
+    ctx = eng.device
+    data = synth.english(n, seed=11)
+    ref = O.train(data, 700)
+    want = [list(m[:4]) for m in ref["merges"]]
+    d = C.c_void_p()
+    _lib.check(lib.gbpe_device_alloc(ctx, n + 64, C.byref(d)), ctx, "alloc")
+    try:
+        pad = bytes([0x41]) * off
+        _lib.check(lib.gbpe_memcpy_h2d(ctx, d, pad + data, n + off), ctx, "h2d")
+        opts = _lib.TrainOpts(target_vocab_size=700, vocab_size=256, next_token_id=256, batch_size=128,
+                              flags=0, table_log2=0)
+        tr = C.c_void_p()
+        _lib.check(lib.gbpe_trainer_create(ctx, C.c_void_p(d.value + off), n, None, 1, C.byref(opts), C.byref(tr)),
+                   ctx, "create")
+        try:
+            merges, out = [], (C.c_uint32 * 512)()
+            while True:
+                nd, es = C.c_uint32(), C.c_uint32()
+                _lib.check(lib.gbpe_trainer_step(tr, 128, out, C.byref(nd), C.byref(es)), ctx, "step")
+                merges += [list(out[4 * i:4 * i + 4]) for i in range(nd.value)]
+                if nd.value == 0 or es.value:
+                    break
+            nn = C.c_uint64()
+            lib.gbpe_trainer_symbols(tr, None, 0, C.byref(nn))
+            syms = np.zeros(nn.value, np.uint32)
+            _lib.check(lib.gbpe_trainer_symbols(tr, syms.ctypes.data_as(_lib.u32p), nn.value, C.byref(nn)), ctx, "sym")
+        finally:
+            lib.gbpe_trainer_destroy(tr)
+    finally:
+        lib.gbpe_device_free(ctx, d)
+    assert [m[:4] for m in merges] == [m[:4] for m in want]
+    assert np.array_equal(syms, np.asarray(ref["symbols"], dtype=np.uint32))

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""A/B of library builds (diagnostic): alternating complete training runs of
+the named configurations with each libgpubpe.so, every run's merge list
+compared with its committed oracle fixture.
+
+    python tools/ab_libs.py gpu-bpe_amd/lib/A/libgpubpe.so gpu-bpe_amd/lib/B/libgpubpe.so -- en1g c2 code1g
+
+Each library runs in its own child process (one .so per process); the runs
+alternate A, B, A, B so drift on the box hits both alike.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import ctypes as C, json, os, sys, time
+sys.path.insert(0, os.path.join(sys.argv[1], "gpu-bpe_amd"))
+import numpy as np
+from gpubpe import _lib, synth
+CONF = {
+    "c2": (lambda: synth.english(104_857_600, seed=2, fancy_punct=0.005), 32768, 0),
+    "en1g": (lambda: synth.english(1 << 30, seed=2, fancy_punct=0.005), 32768, 0),
+    "ml1g": (lambda: synth.multilingual(1 << 30, seed=3), 32768, 0),
+    "code1g": (lambda: synth.code(1 << 30, seed=6), 50000, _lib.GBPE_TRAIN_GPT4_BOUNDARIES),
+}
+lib = _lib.load(sys.argv[2])
+ctx = C.c_void_p()
+_lib.check(lib.gbpe_ctx_create(0, C.byref(ctx)), None, "ctx")
+reps = int(sys.argv[3])
+for name in sys.argv[4:]:
+    gen, vocab, flags = CONF[name]
+    data = gen()
+    fx = np.load(os.path.join(sys.argv[1], "tests", "golden", "train_" + name + ".npz"))["merges"]
+    d = C.c_void_p()
+    _lib.check(lib.gbpe_device_alloc(ctx, len(data) + 64, C.byref(d)), ctx, "alloc")
+    _lib.check(lib.gbpe_memcpy_h2d(ctx, d, data, len(data)), ctx, "h2d")
+    for rep in range(reps + 1):   # the first run warms up
+        opts = _lib.TrainOpts(target_vocab_size=vocab, vocab_size=256, next_token_id=256, batch_size=128,
+                              flags=flags, table_log2=0)
+        tr = C.c_void_p()
+        lib.gbpe_synchronize(ctx)
+        t0 = time.perf_counter()
+        _lib.check(lib.gbpe_trainer_create(ctx, d, len(data), None, 1, C.byref(opts), C.byref(tr)), ctx, "create")
+        out = (C.c_uint32 * 512)()
+        merges = []
+        while True:
+            nd, es = C.c_uint32(), C.c_uint32()
+            _lib.check(lib.gbpe_trainer_step(tr, 128, out, C.byref(nd), C.byref(es)), ctx, "step")
+            merges += list(out[: 4 * nd.value])
+            if nd.value == 0 or es.value:
+                break
+        t1 = time.perf_counter()
+        lib.gbpe_trainer_destroy(tr)
+        m = np.array(merges, dtype=np.uint32).reshape(-1, 4)
+        eq = m.shape == fx.shape and bool((m == fx).all())
+        if rep:
+            print(json.dumps({"name": name, "s": round(t1 - t0, 4), "merges": int(m.shape[0]), "equal": eq}), flush=True)
+        if not eq:
+            print(json.dumps({"name": name, "error": "merges differ from the fixture"}), flush=True)
+            sys.exit(3)
+    lib.gbpe_device_free(ctx, d)
+lib.gbpe_ctx_destroy(ctx)
+"""
+
+
+def main():
+    i = sys.argv.index("--")
+    libs, names = sys.argv[1:i], sys.argv[i + 1:]
+    reps = int(os.environ.get("AB_REPS", "2"))
+    rounds = int(os.environ.get("AB_ROUNDS", "2"))
+    res = {}
+    for r in range(rounds):
+        for lp in libs:
+            p = subprocess.run([sys.executable, "-c", CHILD, ROOT, os.path.abspath(lp), str(reps)] + names,
+                               capture_output=True, text=True, timeout=600)
+            for line in p.stdout.splitlines():
+                j = json.loads(line)
+                if "error" in j:
+                    print(lp, j, flush=True)
+                    sys.exit(3)
+                res.setdefault((lp, j["name"]), []).append(j["s"])
+            if p.returncode:
+                print(lp, "rc", p.returncode, p.stderr[-2000:], flush=True)
+                sys.exit(p.returncode)
+            print(f"round {r} {lp} done", flush=True)
+    for (lp, name), v in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
+        print(f"{name:8s} {lp:50s} min {min(v):.4f} s  all {[round(x, 4) for x in v]}")
+
+
+if __name__ == "__main__":
+    main()
