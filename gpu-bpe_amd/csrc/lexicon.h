@@ -111,9 +111,10 @@ struct alignas(16) LxSlot {
 };
 
 // global word table (linear probing on 64-bit keys): insert-or-add `c` occurrences
-__device__ bool lx_insert(LxSlot* __restrict__ wt, uint32_t P, unsigned long long h, uint32_t rep, uint32_t c) {
+__device__ bool lx_insert(LxSlot* __restrict__ wt, uint32_t P, unsigned long long h, uint32_t rep, uint32_t c,
+                          uint32_t maxp = LX_PROBES) {
     uint32_t slot = lx_home(h, P - 1);
-    for (uint32_t p = 0; p < LX_PROBES; ++p, slot = (slot + 1) & (P - 1)) {
+    for (uint32_t p = 0; p < maxp; ++p, slot = (slot + 1) & (P - 1)) {
         unsigned long long k = __hip_atomic_load(&wt[slot].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k == 0ull) {
             k = atomicCAS(&wt[slot].key, 0ull, h);
@@ -154,7 +155,8 @@ template <typename S>
 __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32_t len, const uint32_t* __restrict__ wpos,
                                                  uint32_t nw, LxSlot* __restrict__ wtab,
                                                  uint32_t P, uint32_t* __restrict__ otmp, uint32_t* __restrict__ longs,
-                                                 uint32_t* __restrict__ ctr, const uint32_t* __restrict__ wmul = nullptr) {
+                                                 uint32_t* __restrict__ ctr, const uint32_t* __restrict__ wmul = nullptr,
+                                                 uint32_t maxp = LX_PROBES) {
     __shared__ unsigned long long lk[LX_LT];
     __shared__ uint32_t lc[LX_LT], lr[LX_LT];
     for (int i = threadIdx.x; i < LX_LT; i += TPB) {
@@ -194,11 +196,13 @@ __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32
                 done = true;
             }
         }
-        if (!done && !lx_insert(wtab, P, h, (uint32_t)j, wt)) ctr[1] = 1u;
+        if (!done && !lx_insert(wtab, P, h, (uint32_t)j, wt, maxp)) ctr[1] = 1u;
     }
     __syncthreads();
+    // a table already known to be too small (the build is redone or abandoned): no probing
+    if (__hip_atomic_load(&ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     for (int i = threadIdx.x; i < LX_LT; i += TPB)
-        if (lk[i] && !lx_insert(wtab, P, lk[i], lr[i], lc[i])) ctr[1] = 1u;
+        if (lk[i] && !lx_insert(wtab, P, lk[i], lr[i], lc[i], maxp)) ctr[1] = 1u;
 }
 
 constexpr uint32_t LX_TB = TPB * 16;   // word-table slots per uid-assignment block

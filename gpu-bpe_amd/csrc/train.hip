@@ -200,7 +200,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         if (tmp) hipFree(tmp);
         return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "symbol kernel launch failed"));
     }
-    int rc = table_rebuild(t);
+    int rc = table_rebuild(t, true);
     if (tmp || d_gpt4) {
         hipStreamSynchronize(s);
         hipFree(tmp);
@@ -733,6 +733,7 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->zst);
     hipFree(t->d_u32);
     hipFree(t->part);
+    hipFree(t->d_bhist);
     hipFree(t->zseg);
     hipFree(t->hs_rec);
     hipFree(t->hs_stat);

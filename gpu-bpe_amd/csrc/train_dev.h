@@ -507,6 +507,49 @@ __global__ __launch_bounds__(TPB) void k_count_full(DevState* st, const S* __res
     lds_flush(lt, tb, st);
 }
 
+// The first count, while every symbol is still a byte: only 256 x 256 pairs can
+// exist, so each workgroup counts one half of them (first byte < 128 or >= 128)
+// in a dense 32K-entry LDS histogram with plain LDS adds — no hashing, no probe —
+// over a share of the tiles, and adds its non-zero entries to a dense global
+// histogram; k_count_hist then inserts the (<= 65,536) pairs into the table.
+// (k_count_full's hashed LDS table took 6.4 ms for 1 GiB of u16 symbols.)
+constexpr int CB_T = 1024;
+template <typename S>
+__global__ __launch_bounds__(CB_T) void k_count_bytes(const S* __restrict__ cur, uint64_t n, uint32_t* __restrict__ gh) {
+    __shared__ uint32_t hist[32768];
+    for (int i = threadIdx.x; i < 32768; i += CB_T) hist[i] = 0u;
+    __syncthreads();
+    const uint32_t half = blockIdx.x & 1u, pair = blockIdx.x >> 1, npair = gridDim.x >> 1;
+    constexpr int PV = 16 / sizeof(S);   // symbols per 16-byte vector
+    const uint64_t nv = gbpe_div_up(n, PV);
+    for (uint64_t v = (uint64_t)pair * CB_T + threadIdx.x; v < nv; v += (uint64_t)npair * CB_T) {
+        const uint64_t i0 = v * PV;
+        uint4 q = *reinterpret_cast<const uint4*>(cur + i0);   // buffers are padded to whole tiles
+        const S* e = reinterpret_cast<const S*>(&q);
+        uint32_t prev = i0 ? (uint32_t)cur[i0 - 1] : 0u;
+#pragma unroll
+        for (int k = 0; k < PV; ++k) {
+            const uint32_t x = e[k];
+            const uint32_t t0 = prev & Sym<S>::TM, t1 = x & Sym<S>::TM;
+            if (i0 + k < n && i0 + k > 0 && !(x & Sym<S>::WS) && t0 && t1 && (t0 >> 7) == half)
+                atomicAdd(&hist[((t0 & 127u) << 8) | t1], 1u);
+            prev = x;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 32768; i += CB_T) {
+        const uint32_t c = hist[i];
+        if (c) atomicAdd(&gh[(half << 15) | (uint32_t)i], c);
+    }
+}
+
+__device__ void table_add(const Table& tb, DevState* st, uint32_t pid, uint32_t delta);
+__global__ __launch_bounds__(256) void k_count_hist(const uint32_t* __restrict__ gh, DevState* st, Table tb) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;   // (a << 8) | b
+    const uint32_t c = gh[i];
+    if (c) table_add(tb, st, ((i >> 8) << 16) | (i & 255u), c);
+}
+
 __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log, uint32_t* __restrict__ grpsum,
                              uint32_t* __restrict__ nlog, uint32_t* __restrict__ rec, DevState* zst, uint32_t exact);
 

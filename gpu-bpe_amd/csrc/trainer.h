@@ -3,6 +3,8 @@
 // (pair table, sector-sparse layout, word lexicon, zone).  See train.hip.
 #pragma once
 
+#include <cmath>
+
 #include "train_dev.h"
 
 
@@ -101,6 +103,10 @@ struct gbpe_trainer {
     uint32_t sp_enters = 0, sp_exits = 0;
     uint32_t sp_div = 64;        // enter when last_mc * sp_div <= n
     uint32_t sp_cooldown = 0;    // steps to stay dense after an abort
+    uint32_t* d_bhist = nullptr; // byte-pair histogram of the first count (65,536 u32)
+    uint32_t count_bytes_on = 1; // first count by the byte-pair histogram (GBPE_COUNT_BYTES=0: hashed k_count_full)
+    uint32_t lx_size_on = 1;     // word table sized from a sampled distinct count (GBPE_LEX_SIZE=0: from the word count)
+    uint32_t lx_resize = 0;      // builds whose sampled table was too small (rerun at full size)
     uint32_t lx_div = 16;        // with the lexicon: enter once next_mc * lx_div <= n, from the first step on (GBPE_LEXICON_DIV)
     uint32_t sub_zone = 1u << 20;   // sparse steps run in sub-steps of sub_k merges while the zone exceeds this
     uint32_t sub_k = 16;            // (the zone shrinks between them; GBPE_SUBSTEP_ZONE, GBPE_SUBSTEP)
@@ -198,7 +204,8 @@ int table_resize(gbpe_trainer* t, uint32_t lg) {
     return GBPE_OK;
 }
 
-int table_rebuild(gbpe_trainer* t) {
+// bytes_only: every symbol is a byte (the stream as trainer creation builds it)
+int table_rebuild(gbpe_trainer* t, bool bytes_only = false) {
     hipStream_t s = t->ctx->stream;
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
     TR_HIP(t, hipMemsetAsync(t->tb.slots, 0, slots * sizeof(uint2), s));
@@ -207,7 +214,24 @@ int table_rebuild(gbpe_trainer* t) {
     TR_HIP(t, hipMemsetAsync(&t->st->used, 0, sizeof(uint32_t), s));
     const uint64_t ntiles = gbpe_div_up(t->n, TILE);
     const uint32_t g = grid_persistent(t->ctx, ntiles, 2);
-    if (t->u16)
+    if (bytes_only && t->count_bytes_on) {
+        if (!t->d_bhist && hipMalloc((void**)&t->d_bhist, 65536 * sizeof(uint32_t)) != hipSuccess) {
+            t->d_bhist = nullptr;
+            return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(byte-pair histogram) failed");
+        }
+        uint32_t* gh = t->d_bhist;
+        TR_HIP(t, hipMemsetAsync(gh, 0, 65536 * sizeof(uint32_t), s));
+        const uint64_t ncu = t->ctx->num_cu > 0 ? (uint64_t)t->ctx->num_cu : 256u;
+        const uint32_t gb = 2u * (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ncu, gbpe_div_up(t->n, 16ull * CB_T)));
+        if (t->u16)
+            hipLaunchKernelGGL(k_count_bytes<uint16_t>, dim3(gb), dim3(CB_T), 0, s, (const uint16_t*)t->buf[t->cur],
+                               (uint64_t)t->n, gh);
+        else
+            hipLaunchKernelGGL(k_count_bytes<uint32_t>, dim3(gb), dim3(CB_T), 0, s, (const uint32_t*)t->buf[t->cur],
+                               (uint64_t)t->n, gh);
+        hipLaunchKernelGGL(k_count_hist, dim3(256), dim3(256), 0, s, (const uint32_t*)gh, t->st, t->tb);
+        GBPE_LAUNCH_CHECK(t->ctx);
+    } else if (t->u16)
         hipLaunchKernelGGL(k_count_full<uint16_t>, dim3(g), dim3(TPB), 0, s, t->st,
                            (const uint16_t*)t->buf[t->cur], t->tb);
     else
@@ -766,11 +790,14 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
         lp.nw = (uint32_t)nw64;
     }
     const uint32_t nw = lp.nw;
-    uint64_t P = 4096;
-    while (P < 2ull * nw && P < (1ull << 27)) P <<= 1;
-    const uint64_t nbb = gbpe_div_up(P, LX_TB);
-    const uint64_t need = (ntiles + 64) * 4 + (ntiles / SCAN_BLK + 4) * 8 + 9ull * (nw + 64) * 4 + P * 16 +
-                          (nbb + 64) * 4 + 2 * (nbb / SCAN_BLK + (uint64_t)nw / SCAN_BLK + 8) * 8 + 32 * 256;
+    // word table: room for every word at half load (Pfull), but sized from the
+    // distinct words of a sample when the segment is long — a table of the
+    // distinct words stays in the caches, one of all words (2 GB at 1 GiB) does not
+    uint64_t Pfull = 4096;
+    while (Pfull < 2ull * nw && Pfull < (1ull << 27)) Pfull <<= 1;
+    const uint64_t nbbf = gbpe_div_up(Pfull, LX_TB);
+    const uint64_t need = (ntiles + 64) * 4 + (ntiles / SCAN_BLK + 4) * 8 + 9ull * (nw + 64) * 4 + Pfull * 16 +
+                          (nbbf + 64) * 4 + 2 * (nbbf / SCAN_BLK + (uint64_t)nw / SCAN_BLK + 8) * 8 + 32 * 256;
     rc = lx_scratch(t, need);
     if (rc != GBPE_OK) return rc;
     LxCarve c{(char*)t->lx_tmp};
@@ -783,9 +810,9 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
     lp.umul = c.take<uint32_t>(nw + 1);
     lp.urep = c.take<uint32_t>(nw + 1);
     lp.occ = c.take<uint32_t>(nw + 1);
-    auto* wtab = c.take<LxSlot>(P);
-    uint32_t* bc = c.take<uint32_t>(nbb);
-    uint64_t* bb = c.take<uint64_t>(nbb / SCAN_BLK + 4);
+    auto* wtab = c.take<LxSlot>(Pfull);
+    uint32_t* bc = c.take<uint32_t>(nbbf);
+    uint64_t* bb = c.take<uint64_t>(nbbf / SCAN_BLK + 4);
     lp.ublk = c.take<uint64_t>((uint64_t)nw / SCAN_BLK + 4);
     uint32_t* ctr = c.take<uint32_t>(8);
     // (the tile counts are recomputed: the scratch may have moved)
@@ -793,19 +820,46 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
     lx_scan(s, tc, ntiles, tb);
     hipLaunchKernelGGL(k_lx_wpos<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, (const uint32_t*)tc,
                        (const uint64_t*)tb, lp.wpos);
-    TR_HIP(t, hipMemsetAsync(wtab, 0, P * sizeof(LxSlot), s));
-    TR_HIP(t, hipMemsetAsync(ctr, 0, 32, s));
-    if (nw)
-        hipLaunchKernelGGL(k_lx_hash<S>, dim3((uint32_t)gbpe_div_up(nw, TPB * LX_WPT)), dim3(TPB), 0, s, seg, len,
-                           (const uint32_t*)lp.wpos, nw, wtab, (uint32_t)P, otmp, longs, ctr, wmul);
-    hipLaunchKernelGGL(k_lx_tabcount, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const LxSlot*)wtab, (uint32_t)P, bc);
-    lx_scan(s, bc, nbb, bb);
-    GBPE_LAUNCH_CHECK(t->ctx);
     uint32_t h[4] = {0, 0, 0, 0};
     uint64_t nshort = 0;
-    TR_HIP(t, hipMemcpyAsync(h, ctr, 8, hipMemcpyDeviceToHost, s));
-    TR_HIP(t, hipMemcpyAsync(&nshort, bb + gbpe_div_up(nbb, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
-    TR_HIP(t, hipStreamSynchronize(s));
+    // hash the first `nh` words into a P-slot table; h = {long words, overflow}, nshort = distinct
+    auto hash_pass = [&](uint64_t P, uint32_t nh) -> int {
+        const uint64_t nbb = gbpe_div_up(P, LX_TB);
+        TR_HIP(t, hipMemsetAsync(wtab, 0, P * sizeof(LxSlot), s));
+        TR_HIP(t, hipMemsetAsync(ctr, 0, 32, s));
+        if (nh)
+            hipLaunchKernelGGL(k_lx_hash<S>, dim3((uint32_t)gbpe_div_up(nh, TPB * LX_WPT)), dim3(TPB), 0, s, seg, len,
+                               (const uint32_t*)lp.wpos, nh, wtab, (uint32_t)P, otmp, longs, ctr, wmul,
+                               P < Pfull ? 256u : LX_PROBES);   // an estimated table gives up early when short
+        hipLaunchKernelGGL(k_lx_tabcount, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const LxSlot*)wtab, (uint32_t)P, bc);
+        lx_scan(s, bc, nbb, bb);
+        GBPE_LAUNCH_CHECK(t->ctx);
+        TR_HIP(t, hipMemcpyAsync(h, ctr, 8, hipMemcpyDeviceToHost, s));
+        TR_HIP(t, hipMemcpyAsync(&nshort, bb + gbpe_div_up(nbb, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
+        TR_HIP(t, hipStreamSynchronize(s));
+        return GBPE_OK;
+    };
+    uint64_t P = Pfull;
+    constexpr uint32_t LX_SAMPLE = 1u << 22;   // words of the sample
+    if (nw > 4u * LX_SAMPLE && t->lx_size_on) {
+        rc = hash_pass(2ull * LX_SAMPLE, LX_SAMPLE);
+        if (rc != GBPE_OK) return rc;
+        if (!h[1]) {   // distinct words grow slower than words (Heaps): D ~ d (nw / sample)^0.8, at <= 1/3 load
+            const double D = (double)(nshort + h[0]) * pow((double)nw / LX_SAMPLE, 0.8);
+            uint64_t Pe = 1ull << 20;
+            while ((double)Pe < 3.0 * D && Pe < Pfull) Pe <<= 1;
+            P = Pe;
+        }
+    }
+    rc = hash_pass(P, nw);
+    if (rc != GBPE_OK) return rc;
+    if (h[1] && P < Pfull) {   // the estimate was short: the full-size table
+        P = Pfull;
+        ++t->lx_resize;
+        rc = hash_pass(P, nw);
+        if (rc != GBPE_OK) return rc;
+    }
+    const uint64_t nbb = gbpe_div_up(P, LX_TB);
     if (h[1]) return GBPE_OK;   // word table overflow: not usable
     lp.nshort = (uint32_t)nshort;
     lp.nlong = h[0];
@@ -1310,6 +1364,8 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     if (const char* e = getenv("GBPE_TAIL")) t->tail_on = atoi(e) != 0;
     if (const char* e = getenv("GBPE_ZONE16")) t->zone16 = atoi(e) != 0;
     if (const char* e = getenv("GBPE_TAIL_MC")) t->tail_mc = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_COUNT_BYTES")) t->count_bytes_on = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBPE_LEX_SIZE")) t->lx_size_on = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_LEXICON_DIV")) t->lx_div = std::max<uint32_t>(8, (uint32_t)strtoul(e, nullptr, 10));
     if (const char* e = getenv("GBPE_SUBSTEP_ZONE")) t->sub_zone = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_SUBSTEP")) t->sub_k = std::max<uint32_t>(2, (uint32_t)strtoul(e, nullptr, 10)) & ~1u;

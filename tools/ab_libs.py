@@ -3,7 +3,9 @@
 the named configurations with each libgpubpe.so, every run's merge list
 compared with its committed oracle fixture.
 
-    python tools/ab_libs.py gpu-bpe_amd/lib/A/libgpubpe.so gpu-bpe_amd/lib/B/libgpubpe.so -- en1g c2 code1g
+    python tools/ab_libs.py gpu-bpe_amd/lib/A/libgpubpe.so gpu-bpe_amd/lib/B/libgpubpe.so:GBPE_X=0 -- en1g c2 code1g
+
+(a library may carry environment settings after a colon)
 
 Each library runs in its own child process (one .so per process); the runs
 alternate A, B, A, B so drift on the box hits both alike.
@@ -73,9 +75,12 @@ def main():
     rounds = int(os.environ.get("AB_ROUNDS", "2"))
     res = {}
     for r in range(rounds):
-        for lp in libs:
-            p = subprocess.run([sys.executable, "-c", CHILD, ROOT, os.path.abspath(lp), str(reps)] + names,
-                               capture_output=True, text=True, timeout=600)
+        for lp in libs:   # "path" or "path:ENV=V,ENV2=V2"
+            path, _, envs = lp.partition(":")
+            env = dict(os.environ)
+            env.update(kv.split("=", 1) for kv in envs.split(",") if kv)
+            p = subprocess.run([sys.executable, "-c", CHILD, ROOT, os.path.abspath(path), str(reps)] + names,
+                               capture_output=True, text=True, timeout=600, env=env)
             for line in p.stdout.splitlines():
                 j = json.loads(line)
                 if "error" in j:
