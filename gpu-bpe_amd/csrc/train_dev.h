@@ -898,8 +898,17 @@ __global__ __launch_bounds__(1024) void k_step_out(DevState* st, DevState* zst, 
     } g;
     const uint32_t t = threadIdx.x;
     uint32_t live = 0;
-    if (live_too) {   // k_live: live pairs from the per-block live counts
-        for (uint32_t i = t; i < tb.nblk; i += 1024) live += tb.blive[i];
+    if (live_too) {   // k_live: live pairs from the per-block live counts (16-byte loads, 4 in flight)
+        const uint32_t nq = tb.nblk / 4u;
+        const uint4* bq = reinterpret_cast<const uint4*>(tb.blive);
+        if (4u * nq + t < tb.nblk) live += tb.blive[4u * nq + t];
+        for (uint32_t i = t; i < nq; i += 4096) {
+            uint4 q[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = i + k * 1024u < nq ? bq[i + k * 1024u] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) live += q[k].x + q[k].y + q[k].z + q[k].w;
+        }
         for (int off = 32; off > 0; off >>= 1) live += __shfl_xor(live, off);
         if ((t & 63) == 0) red[t >> 6] = live;
     }

@@ -1272,7 +1272,12 @@ int sp_shrink(gbpe_trainer* t) {
         int rc = sp_add_sectors<S>(t, t->bend, L);
         if (rc != GBPE_OK) return rc;
     }
-    const uint64_t rest = t->zcap - L;
+    // both buffers shift down by L.  Only their live extents move: the zone [0, z)
+    // and the stale buffer, which the next window reads below the previous zone
+    // length (<= z + last_mc); the buffers' capacity is the zone at entry (~200M
+    // symbols at 1 GiB), so moving all of it cost ~1 ms per late shrink.
+    const uint64_t live = std::min<uint64_t>(t->zcap, (uint64_t)z + 2ull * t->last_mc + 2ull * TILE);
+    const uint64_t rest = live - L;
     TR_HIP(t, hipMemcpyAsync(t->wtmp, zc + L, rest * t->bps, hipMemcpyDeviceToDevice, s));
     TR_HIP(t, hipMemcpyAsync(zc, t->wtmp, rest * t->bps, hipMemcpyDeviceToDevice, s));
     TR_HIP(t, hipMemcpyAsync(t->wtmp, zo + L, rest * t->bps, hipMemcpyDeviceToDevice, s));
