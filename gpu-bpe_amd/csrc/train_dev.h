@@ -573,6 +573,21 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             if (i == 0 || i >= 16) zseg[i] = 0u;
     (void)rwlist;
     if (part && finish == 2 && threadIdx.x == 0) KTR(0);
+    // this WG's contiguous run of blocks (<= 64): all flags (and, for `part`, the
+    // maxima kept from before) in one load — issued first, so block 0's state
+    // snapshot below travels in the same round trip instead of before it
+    __shared__ uint64_t s_dmask;
+    __shared__ uint64_t s_bm[64];
+    const uint32_t per = (tb.nblk + gridDim.x - 1) / gridDim.x;   // <= 64 (host-sized grid)
+    const uint32_t b0 = blockIdx.x * per;
+    uint64_t f_bm = 0ull;
+    bool f_d = false;
+    if (threadIdx.x < 64) {
+        const uint32_t blk = b0 + threadIdx.x;
+        const bool in = threadIdx.x < per && blk < tb.nblk;
+        if (part && in) f_bm = tb.bmax[blk];
+        f_d = in && tb.dirty[blk];
+    }
     // finish == 2: the sector-sparse loop, whose merge was selected inside k_body
     // (sel_inline): the step counters move on here
     // block 0 closes the merge from one snapshot of both states: every field is
@@ -583,8 +598,11 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             DevState d;
             uint32_t w[NW];
         } s_g, s_z;
-        if (threadIdx.x < NW) s_g.w[threadIdx.x] = reinterpret_cast<const uint32_t*>(st)[threadIdx.x];
-        else if (zst && threadIdx.x < 2 * NW) s_z.w[threadIdx.x - NW] = reinterpret_cast<const uint32_t*>(zst)[threadIdx.x - NW];
+        static_assert(64 + 2 * NW <= TPB, "state snapshot beside the flag loads");
+        if (threadIdx.x >= 64 && threadIdx.x < 64 + NW)
+            s_g.w[threadIdx.x - 64] = reinterpret_cast<const uint32_t*>(st)[threadIdx.x - 64];
+        else if (zst && threadIdx.x >= 64 + NW && threadIdx.x < 64 + 2 * NW)
+            s_z.w[threadIdx.x - 64 - NW] = reinterpret_cast<const uint32_t*>(zst)[threadIdx.x - 64 - NW];
         __syncthreads();
         const DevState& g = s_g.d;
         const DevState& z = s_z.d;
@@ -635,20 +653,12 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             }
         }
     }
-    // this WG's contiguous run of blocks (<= 64): all flags (and, for `part`, the
-    // maxima kept from before) in one load; then every wave re-maxes its share of
-    // the dirty ones, one 256-slot block at a time (no workgroup barrier per block:
-    // a merge dirties a few blocks per workgroup, each holding a few live pairs)
-    __shared__ uint64_t s_dmask;
-    __shared__ uint64_t s_bm[64];
-    const uint32_t per = (tb.nblk + gridDim.x - 1) / gridDim.x;   // <= 64 (host-sized grid)
-    const uint32_t b0 = blockIdx.x * per;
+    // then every wave re-maxes its share of the dirty ones, one 256-slot block at a
+    // time (no workgroup barrier per block: a merge dirties a few blocks per
+    // workgroup, each holding a few live pairs)
     if (threadIdx.x < 64) {
-        const uint32_t blk = b0 + threadIdx.x;
-        const bool in = threadIdx.x < per && blk < tb.nblk;
-        if (part) s_bm[threadIdx.x] = in ? tb.bmax[blk] : 0ull;
-        const bool d = in && tb.dirty[blk];
-        const unsigned long long m = __ballot(d);
+        if (part) s_bm[threadIdx.x] = f_bm;
+        const unsigned long long m = __ballot(f_d);
         if (threadIdx.x == 0) s_dmask = m;
     }
     __syncthreads();
