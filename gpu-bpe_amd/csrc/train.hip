@@ -327,7 +327,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
                             : grid_persistent(t->ctx, gbpe_div_up(t->n / 2 + 1, TPB * 16), 1);
     const uint32_t g_delta = (uint32_t)(ntiles ? ntiles : 1);
     const uint32_t g_compact = (uint32_t)ntiles + g_tail;
-    const uint32_t g_refresh = t->g_refresh;
+    uint32_t g_refresh = t->g_refresh;
     const bool timing = (t->flags & GBPE_TRAIN_TIMING) != 0;
     const bool sparse = t->sp;
     SpGrid sg{};
@@ -349,6 +349,25 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
                                                            : (uint32_t)std::min<uint64_t>(1024, gbpe_div_up(zn / 5 + 1, 2048));
         sg.zcompact = (uint32_t)zt + ((t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
                                       : grid_persistent(t->ctx, gbpe_div_up(zn / 2 + 1, TPB * 16), 1));
+        // late steps (the zone fits the 256-thread k_body): a smaller k_refresh grid —
+        // a late merge dirties a few blocks, and fewer workgroups dispatch and drain
+        // sooner.  The partial maxima the next k_body reads are laid out per k_refresh
+        // workgroup, so a grid change re-lays them out once (finish 0: no merge closed)
+        if (t->refresh_late && !t->sharded && sg.bt == 256 && sg.zone1 == 1u) {
+            const uint32_t want = std::max<uint32_t>(t->refresh_late, (uint32_t)gbpe_div_up(t->tb.nblk, 64));
+            if (want != t->g_refresh) {
+                t->g_refresh = g_refresh = want;
+                if (t->u16)
+                    hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(want), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
+                                       (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr,
+                                       (uint32_t*)nullptr, FusedSel(), t->part, (uint32_t*)nullptr);
+                else
+                    hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(want), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
+                                       (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr,
+                                       (uint32_t*)nullptr, FusedSel(), t->part, (uint32_t*)nullptr);
+                GBPE_LAUNCH_CHECK(t->ctx);
+            }
+        }
         sg.refresh = g_refresh;
     }
     // the persistent tail loop: one workgroup, the whole step
