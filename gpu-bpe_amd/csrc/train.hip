@@ -349,11 +349,11 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
                                                            : (uint32_t)std::min<uint64_t>(1024, gbpe_div_up(zn / 5 + 1, 2048));
         sg.zcompact = (uint32_t)zt + ((t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
                                       : grid_persistent(t->ctx, gbpe_div_up(zn / 2 + 1, TPB * 16), 1));
-        // late steps (the zone fits the 256-thread k_body): a smaller k_refresh grid —
+        // late steps (a zone of <= 16K symbols): a smaller k_refresh grid —
         // a late merge dirties a few blocks, and fewer workgroups dispatch and drain
         // sooner.  The partial maxima the next k_body reads are laid out per k_refresh
         // workgroup, so a grid change re-lays them out once (finish 0: no merge closed)
-        if (t->refresh_late && !t->sharded && sg.bt == 256 && sg.zone1 == 1u) {
+        if (t->refresh_late && !t->sharded && zn <= t->refresh_late_z) {
             const uint32_t want = std::max<uint32_t>(t->refresh_late, (uint32_t)gbpe_div_up(t->tb.nblk, 64));
             if (want != t->g_refresh) {
                 t->g_refresh = g_refresh = want;

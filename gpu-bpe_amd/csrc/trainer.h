@@ -123,7 +123,8 @@ struct gbpe_trainer {
     uint32_t shrink_pct = 200;   // shrink once the zone exceeds shrink_pct % of the target + 4096 (GBPE_SHRINK_PCT)
     uint32_t zone_f = 3;         // single-GPU zone rule factor (sel_inline; GBPE_ZONE_F, >= 3)
     uint32_t refresh_blocks = 0; // GBPE_REFRESH_BLOCKS: k_refresh grid (0 = 2 per CU)
-    uint32_t refresh_late = 64;  // GBPE_REFRESH_LATE: k_refresh grid of steps whose zone fits the 256-thread k_body (0 = unchanged)
+    uint32_t refresh_late_z = 16384; // GBPE_REFRESH_LATE_Z: ... for zones of at most this many symbols
+    uint32_t refresh_late = 64;  // GBPE_REFRESH_LATE: k_refresh grid of late steps (0 = unchanged)
     bool rehash_on = true;       // GBPE_REHASH: grow the table inside the sparse loop (0: exit, grow, recount)
     uint32_t body_cap = 256;     // GBPE_BODY_WG: most k_body workgroups (default one per CU)
     uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
@@ -1363,6 +1364,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     if (const char* e = getenv("GBPE_SPARSE_DIV")) t->sp_div = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_REFRESH_BLOCKS")) t->refresh_blocks = (uint32_t)atoi(e);
     if (const char* e = getenv("GBPE_REFRESH_LATE")) t->refresh_late = (uint32_t)atoi(e);
+    if (const char* e = getenv("GBPE_REFRESH_LATE_Z")) t->refresh_late_z = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("GBPE_REHASH")) t->rehash_on = atoi(e) != 0;
     t->body_cap = (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
     if (const char* e = getenv("GBPE_BODY_WG")) t->body_cap = std::max<uint32_t>(1, (uint32_t)atoi(e));
