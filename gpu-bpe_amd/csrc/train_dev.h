@@ -1588,6 +1588,7 @@ __global__ __launch_bounds__(TPB) void k_zdr(ZdrView z, uint32_t nd, Table tb, D
 // Both in one workgroup's LDS table (a pair the tail drops and the window adds
 // is one entry), dumped for k_zdr.
 constexpr int CH_BT = 512;
+constexpr int CH_U = 8;   // positions per thread per trip
 template <typename S>
 __global__ __launch_bounds__(CH_BT) void k_churn(DevState* zst, uint32_t round, S* __restrict__ cur,
                                                  S* __restrict__ oth, const uint32_t* __restrict__ hitmask,
@@ -1646,24 +1647,55 @@ __global__ __launch_bounds__(CH_BT) void k_churn(DevState* zst, uint32_t round, 
         if (lane == 0) s_left = v;
     }
     __syncthreads();
-    for (uint32_t d = w0 + t; d < w1; d += CH_BT) {
-        if (d == 0) continue;
-        const uint32_t x1 = win[woff + (d - lo)];
-        const uint32_t x0 = d == w0 ? s_left : (uint32_t)win[woff + (d - lo) - 1];
-        oth[d] = (S)x1;
-        const uint32_t u0 = x0 & TM, u1 = x1 & TM;
-        if (!(x1 & WS) && u0 && u1) lds_add(lt, tb, st, (u0 << 16) | u1, 1u);
+    // CH_U positions per thread per trip, all loaded before any LDS add: the slices
+    // are long early (~2 mc / 256 symbols per workgroup at one workgroup per CU), and
+    // one dependent load per position left every trip waiting on memory
+    for (uint32_t d0 = w0 + t; d0 < w1; d0 += CH_BT * CH_U) {
+        uint32_t x1[CH_U], x0[CH_U];
+#pragma unroll
+        for (int u = 0; u < CH_U; ++u) {
+            const uint32_t d = d0 + (uint32_t)u * CH_BT;
+            x1[u] = x0[u] = 0u;
+            if (d < w1) {
+                x1[u] = win[woff + (d - lo)];
+                x0[u] = d == w0 ? s_left : (uint32_t)win[woff + (d - lo) - 1];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < CH_U; ++u) {
+            const uint32_t d = d0 + (uint32_t)u * CH_BT;
+            if (d >= w1 || d == 0) continue;
+            oth[d] = (S)x1[u];
+            const uint32_t u0 = x0[u] & TM, u1 = x1[u] & TM;
+            if (!(x1[u] & WS) && u0 && u1) lds_add(lt, tb, st, (u0 << 16) | u1, 1u);
+        }
     }
-    for (uint32_t i = t0 + t; i < t1; i += CH_BT) {
-        if (i == 0) continue;
-        // snapshot values: an A-side (hit at the next position) was rewritten to nw in place
-        const uint32_t j1 = i + 1, jp = i;
-        uint32_t xi = cur[i], xp = cur[i - 1];
-        if (j1 < n && ((hitmask[j1 / 32] >> (j1 % 32)) & 1u)) xi = a | (xi & WS);
-        if ((hitmask[jp / 32] >> (jp % 32)) & 1u) xp = a | (xp & WS);
-        if (xi & WS) continue;
-        const uint32_t tp = xp & TM, ti = xi & TM;
-        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+    for (uint32_t i0 = t0 + t; i0 < t1; i0 += CH_BT * CH_U) {
+        uint32_t xi[CH_U], xp[CH_U], h1[CH_U], hp[CH_U];
+#pragma unroll
+        for (int u = 0; u < CH_U; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * CH_BT;
+            xi[u] = xp[u] = h1[u] = hp[u] = 0u;
+            if (i < t1 && i != 0) {
+                xi[u] = cur[i];
+                xp[u] = cur[i - 1];
+                if (i + 1 < n) h1[u] = hitmask[(i + 1) / 32];
+                hp[u] = hitmask[i / 32];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < CH_U; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * CH_BT;
+            if (i >= t1 || i == 0) continue;
+            // snapshot values: an A-side (hit at the next position) was rewritten to nw in place
+            const uint32_t j1 = i + 1, jp = i;
+            uint32_t x = xi[u], y = xp[u];
+            if ((h1[u] >> (j1 % 32)) & 1u) x = a | (x & WS);   // (h1 = 0 past the zone's end)
+            if ((hp[u] >> (jp % 32)) & 1u) y = a | (y & WS);
+            if (x & WS) continue;
+            const uint32_t tp = y & TM, ti = x & TM;
+            if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        }
     }
     lds_dump(lt, zv, wbase + q);
 }
