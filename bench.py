@@ -29,9 +29,7 @@ Multi-GPU (--gpus N under torch.distributed.run, one rank per GPU):
     is fixed).  The merge chain is sequential — every merge's argmax needs the
     previous merge's counts — and one merge costs less than an exchange between
     GPUs, so every rank runs the complete training (replicated, no per-merge
-    collective); `value` = global merges / max wall over ranks.  The per-merge
-    sharded trainer (gpubpe/sharded.py, one RCCL all-gather per merge) runs with
-    --sharded;
+    collective); `value` = global merges / max wall over ranks;
   * tokenize: the one 1 GiB C3 input cut into chunk-aligned slices, one per rank
     (gpubpe/split_encode.py): GB/s = input bytes / max wall over ranks; the
     tokens are gathered to rank 0 and checked against the fixture.
@@ -97,8 +95,8 @@ class _stdout_to_stderr:
 
 
 class Dist:
-    """Process groups: the default group carries the sharded trainer's data path
-    (RCCL = backend "nccl" over xGMI; GBPE_SHARD_TRANSPORT=gloo stages records
+    """Process groups: the default group carries the lexicon hand-over's data
+    path (RCCL = backend "nccl" over xGMI; GBPE_SHARD_TRANSPORT=gloo stages it
     through host memory instead); a gloo group carries the timing scalars."""
 
     def __init__(self, world, local, force=False):
@@ -551,9 +549,6 @@ def single_line(args, lib, ctx, dist, rank):
 
 # ── multi-GPU: strong scaling over one corpus ──────────────────────────────────
 
-_COMM = {}   # one RCCL communicator per process, created in the warmup (outside the timed region)
-
-
 def shard_of(data: bytes, rank: int, world: int) -> bytes:
     """Rank r's contiguous slice of the corpus, cut right after a newline (a word
     start under the reference heuristic: train.wgsl:166-170), so pair counts add
@@ -567,101 +562,6 @@ def shard_of(data: bytes, rank: int, world: int) -> bytes:
         cuts.append(max(cuts[-1], int(nl[k]) + 1 if k < nl.shape[0] else n))
     cuts.append(n)
     return data[cuts[rank]:cuts[rank + 1]]
-
-
-def run_sharded(args, lib, ctx, dist, rank, world, d, n, max_merges, table_log2):
-    import torch
-    from gpubpe.sharded import GpuShardBackend, GpuSingleBackend, ShardedTrainer
-    be = GpuShardBackend(lib, ctx, d, None, rank, world, args.vocab, input_on_device=True, n=n,
-                         table_log2=table_log2, cap_extra=max(TILE_SYMS, n // 4),
-                         stream=torch.cuda.current_stream().cuda_stream)
-    tr = ShardedTrainer(be, dist.dist, device="cuda", staged=dist.transport != "nccl")
-    tr.setup()
-    if dist.transport == "nccl" and os.environ.get("GBPE_SHARD_LOOP", "native") == "native" and _COMM.get("ok", True):
-        ok = 1.0
-        try:
-            _COMM["c"] = tr.attach_native_comm(_COMM.get("c"))
-            be.owns_comm = False
-        except Exception as e:  # noqa: BLE001
-            log(f"[bench] rank {rank}: native step loop unavailable ({e}); using the host loop")
-            ok = 0.0
-        if world > 1:
-            ok = -dist.max(-ok)   # min over ranks
-        if ok < 1.0:
-            tr.native = False
-            be.comm = None
-            _COMM["ok"] = False
-    needed = min(args.vocab - 256, max_merges)
-    below = args.consolidate_below if args.consolidate_below >= 0 else None
-    merges, early = tr.train(256 + needed, consolidate_below=below, root=0,
-                             make_single=lambda c, p, nid: GpuSingleBackend(lib, ctx, c, p, args.vocab, nid))
-    if tr.single is not None:
-        tr.single_stats = tr.single.stats()
-        tr.single.close()
-    return be, tr, merges, early
-
-
-def sharded_line(args, lib, ctx, dist, rank, world):
-    t = time.time()
-    full = make_corpus(HEADLINE)
-    data = shard_of(full, rank, world)
-    log(f"[bench] rank {rank}: shard {len(data)} B of {len(full)} in {time.time() - t:.1f}s")
-    d = device_buffer(lib, ctx, data)
-    n = len(data)
-    table_log2 = 24
-    for _ in range(args.warmup):   # RCCL communicators, code paths: W runs on an 8 MiB prefix of every shard
-        be, _, _, _ = run_sharded(args, lib, ctx, dist, rank, world, d, min(n, 8 << 20), 1 << 30, table_log2)
-        be.close()
-    lib.gbpe_synchronize(ctx)
-    dist.barrier()
-    lib.gbpe_synchronize(ctx)
-    t0 = time.perf_counter()
-    total, merges, early, st, tr = 0, [], False, None, None
-    for _ in range(args.steps):
-        be, tr, merges, early = run_sharded(args, lib, ctx, dist, rank, world, d, n, 1 << 30, table_log2)
-        total += len(merges)
-        st = be.stats()
-        be.close()
-    lib.gbpe_synchronize(ctx)
-    t1 = time.perf_counter()
-    dist.barrier()
-    lib.gbpe_device_free(ctx, d)
-    wall = dist.max(t1 - t0)
-    line = {
-        "metric": METRIC,
-        "value": round(total / wall, 1),
-        "unit": "merges/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1e3 * wall / max(1, args.steps), 3),
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": f"u{8 * int(st.bytes_per_symbol)}",
-        "data": "synthetic (seeded Zipf English-like corpus, gpubpe.synth)",
-        "config": {"workload": f"headline corpus (1,073,741,824 B English-like UTF-8, seed 2) cut at word starts "
-                               f"into {world} shards, one global 32K vocab, bit-exact to one stream; step = one "
-                               "complete training run",
-                   "train_bytes": HEADLINE["n"], "target_vocab": args.vocab, "merges_per_step": len(merges),
-                   "parallelism": f"shard{world} ({dist.transport} exchange per merge"
-                                  f"{', native step loop' if tr is not None and tr.native else ''})"},
-        "roofline": {"bound": "hbm", "kernel": "whole sharded loop (algorithmic stream bytes of all ranks / wall)",
-                     "achieved": None, "peak": HBM_PEAK_GBPS * world, "unit": "GB/s", "frac": None, "traffic": None},
-        "train_detail": {"stalls": tr.stalls if tr else 0, "record_caps": [tr.C, tr.Cw] if tr else None,
-                         "consolidate_below": args.consolidate_below if args.consolidate_below >= 0 else None,
-                         "consolidated_at_merge": tr.consolidated_at if tr else None,
-                         "final_symbols_rank": int(st.symbol_count), "tail_dropped": int(st.tail_dropped),
-                         "last_merge": merges[-1] if merges else []},
-    }
-    sb = dist.sum(float(st.stream_bytes_moved))
-    line["roofline"]["achieved"] = round(sb / 1e9 / (wall / max(1, args.steps)), 1)
-    line["roofline"]["frac"] = round(line["roofline"]["achieved"] / (HBM_PEAK_GBPS * world), 4)
-    want, _ = fixture("en1g")
-    if want is not None:
-        line["parity"] = {"merges_equal_fixture": bool(np.array_equal(np.array(merges, dtype=np.uint32), want)),
-                          "merges_checked": int(want.shape[0])}
-    return line
 
 
 def c3_vocab_trie(args, lib, ctx):
@@ -943,30 +843,23 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 leg (1 GiB code, 50K vocab, GPT-4 rules)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP-event roofline run")
     ap.add_argument("--cpu-merges", type=int, default=0, help="CPU baseline merges on the CPU share (0 = 24)")
-    ap.add_argument("--consolidate-below", type=int, default=-1,
-                    help="--sharded: hand the run over to rank 0's GPU once the global stream is at most this many "
-                         "symbols (-1: never)")
     ap.add_argument("--replicated", action="store_true",
                     help="N > 1: every rank trains the whole corpus (round-2 line) instead of the lexicon hand-over")
     ap.add_argument("--c4-only", action="store_true",
                     help="only the C4 leg: one multilingual shard per rank (seed 5 + rank), one 64K vocab")
     ap.add_argument("--c4-shard", type=int, default=C4_SHARD, help="C4 shard bytes per rank")
     ap.add_argument("--c4-runs", type=int, default=1)
-    ap.add_argument("--sharded", action="store_true",
-                    help="the per-merge sharded trainer (one RCCL all-gather per merge; also at N=1 as a rehearsal)")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
-    dist = Dist(world, local, force=args.sharded or args.c4_only)
+    dist = Dist(world, local, force=args.c4_only)
     from gpubpe import _lib
     lib = _lib.load()
     ctx = C.c_void_p()
     rc = lib.gbpe_ctx_create(int(os.environ.get("GBPE_BENCH_DEVICE", local)) if world > 1 else 0, C.byref(ctx))
     if rc != 0:
         raise SystemExit(f"gbpe_ctx_create failed ({rc}): no MI355X visible")
-    if args.sharded:
-        line = sharded_line(args, lib, ctx, dist, rank, world)
-    elif args.c4_only:
+    if args.c4_only:
         line = {"metric": METRIC, "c4": c4_line(args, lib, ctx, dist, rank, world)}
     elif world > 1 and args.replicated:
         line = replicated_line(args, lib, ctx, dist, rank, world)
@@ -981,8 +874,6 @@ def main():
         line = single_line(args, lib, ctx, dist, rank)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if _COMM.get("c"):
-        lib.gbpe_comm_destroy(_COMM["c"])
     lib.gbpe_ctx_destroy(ctx)
 
 

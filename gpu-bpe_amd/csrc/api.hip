@@ -30,8 +30,6 @@ static const char* const kKernelNames[] = {
     "k_trie_walk",       // trie_tokenizer_chunked (tokenize.wgsl:88): k_trie_walk_v5 (packed double array) / nested form
     "k_chunk_scan",      // trie_prefix_sum (tokenize.wgsl:199)
     "k_chunk_compact",   // trie_tokenizer_compact (tokenize.wgsl:225): k_chunk_compact4
-    "k_shard_send",      // sharded training, phase 1: delta list + header + stale-window piece (no reference counterpart)
-    "k_shard_recv",      // sharded training, phase 2: apply every rank's deltas + window pairs, owner appends the window
     "k_pretok",          // PreTokenizer GPT-4 word starts (pre_tokenizer.mjs:226-292): k_pt_scan1/2 + k_pt_mark
     "k_me_walk",         // TokenizerManager.encode (tokenizer-manager.js:13-61): per-segment rank-order BPE
     "k_me_compact",      // its token compaction

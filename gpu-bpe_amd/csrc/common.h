@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -53,6 +54,21 @@ __device__ __forceinline__ uint32_t gbpe_fmix32(uint32_t x) {
 }
 
 __host__ __device__ static inline uint64_t gbpe_div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+// Debug / test overrides: GBPE_DEBUG="key=value,key=value" (DESIGN §6 lists the
+// keys); every other tuning value is a compiled default
+inline long gbpe_debug_knob(const char* key, long def) {
+    const char* e = getenv("GBPE_DEBUG");
+    if (!e) return def;
+    const size_t kl = strlen(key);
+    for (const char* p = e; *p;) {
+        if (!strncmp(p, key, kl) && p[kl] == '=') return strtol(p + kl + 1, nullptr, 10);
+        const char* c = strchr(p, ',');
+        if (!c) break;
+        p = c + 1;
+    }
+    return def;
+}
 
 // GPT-4 rule word starts of device bytes on ctx->stream (pretok.hip)
 int gbpe_pretok_gpt4_launch(gbpe_ctx* ctx, const uint8_t* d_bytes, uint64_t n, uint8_t* d_ws);

@@ -564,8 +564,8 @@ extern "C" int gbpe_encode(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* bytes, u
     if (rc == GBPE_OK) rc = grow(ctx, &ctx->enc_out, &ctx->enc_out_bytes, n * 4 + 16);   // <= 1 token per byte
     if (rc != GBPE_OK) return rc;
     const uint64_t unit = (uint64_t)cs * 64;
-    const char* se = getenv("GBPE_ENCODE_SLICE");   // (tests: many slices on small inputs)
-    const uint64_t want = se ? std::max<uint64_t>(1, strtoull(se, nullptr, 10)) : kEncSlice;
+    // (test override: many slices on small inputs)
+    const uint64_t want = (uint64_t)std::max<long>(1, gbpe_debug_knob("encode_slice", (long)kEncSlice));
     const uint64_t slice = std::max<uint64_t>(unit, (want / unit) * unit);
     uint8_t* d_in = (uint8_t*)ctx->enc_in;
     uint32_t* d_out = (uint32_t*)ctx->enc_out;

@@ -242,7 +242,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         uint32_t lg = t->table_log2;
         while (lg < 28 && live * 4 > (1ull << lg)) ++lg;
         int rc;
-        if (t->sp && !t->sharded && t->rehash_on) {   // the sparse loop goes on over the moved entries
+        if (t->sp && t->rehash_on) {   // the sparse loop goes on over the moved entries
             rc = table_rehash(t, lg);
         } else {
             rc = sp_exit_any(t);   // the full recount runs on the dense stream
@@ -255,7 +255,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     // sector-sparse loop once merges touch a small fraction of the stream
     if (t->sp_cooldown) {
         --t->sp_cooldown;
-    } else if (!t->sp && !t->sharded && !(t->flags & GBPE_TRAIN_DENSE_ONLY)) {
+    } else if (!t->sp && !(t->flags & GBPE_TRAIN_DENSE_ONLY)) {
         // with the word lexicon the body costs what its distinct words cost, so the
         // loop can enter as soon as the zone (~7 x the next count) is a small part of
         // the stream — before the first merge; without it, once counts
@@ -353,7 +353,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         // a late merge dirties a few blocks, and fewer workgroups dispatch and drain
         // sooner.  The partial maxima the next k_body reads are laid out per k_refresh
         // workgroup, so a grid change re-lays them out once (finish 0: no merge closed)
-        if (t->refresh_late && !t->sharded && zn <= t->refresh_late_z) {
+        if (t->refresh_late && zn <= t->refresh_late_z) {
             const uint32_t want = std::max<uint32_t>(t->refresh_late, (uint32_t)gbpe_div_up(t->tb.nblk, 64));
             if (want != t->g_refresh) {
                 t->g_refresh = g_refresh = want;
@@ -370,49 +370,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         }
         sg.refresh = g_refresh;
     }
-    // the persistent tail loop: one workgroup, the whole step
-#ifdef GBPE_TAIL_LOOP
-    const uint32_t zn_now = sparse ? (uint32_t)t->n - hs->B : 0u;
-    const bool tail = sparse && t->tail_on && !t->tail_skip && !t->sharded && t->last_mc <= t->tail_mc &&
-                      zn_now <= (t->u16 ? zone_max<uint16_t>(TL_BT) : zone_max<uint32_t>(TL_BT)) &&
-                      t->tb.nblk <= (TL_MAXG << TL_GRP);
-    t->tail_skip = false;
-    auto launch_tail = [&]() -> int {
-        if (!t->d_tstat) TR_HIP(t, hipMalloc(&t->d_tstat, 16));
-        if (timing) TR_HIP(t, hipEventRecord(t->evs[0], s));
-        const uint32_t wused = (uint32_t)gbpe_div_up(t->nsec, 32);
-        const bool ex = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
-#define GBPE_TAIL_LAUNCH(S_, E_)                                                                                     \
-        do {                                                                                                         \
-        if (zn_now <= (uint32_t)TL_BT * 8u)                                                                         \
-            hipLaunchKernelGGL((k_tail<S_, E_, 8>), dim3(1), dim3(TL_BT), 0, s, t->st, t->zst, (S_*)sp_body(t), sp_mul(t), \
-                               t->sec, t->bits, t->W, wused, t->sig, t->tb, (S_*)t->zbuf[t->zcur],                      \
-                               (S_*)t->zbuf[t->zcur ^ 1], t->d_log, t->wg_bytes, t->d_tstat);                          \
-        else                                                                                                         \
-        hipLaunchKernelGGL((k_tail<S_, E_, ZoneDim<S_, TL_BT>::ZPT>), dim3(1), dim3(TL_BT), 0, s, t->st, t->zst, (S_*)sp_body(t), sp_mul(t), t->sec, \
-                           t->bits, t->W, wused, t->sig, t->tb, (S_*)t->zbuf[t->zcur], (S_*)t->zbuf[t->zcur ^ 1], t->d_log,   \
-                           t->wg_bytes, t->d_tstat);                                                             \
-        hipLaunchKernelGGL(k_refresh<S_>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S_*)nullptr,    \
-                           (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part); \
-        } while (0)
-        if (t->u16) {
-            if (ex) GBPE_TAIL_LAUNCH(uint16_t, true);
-            else GBPE_TAIL_LAUNCH(uint16_t, false);
-        } else {
-            if (ex) GBPE_TAIL_LAUNCH(uint32_t, true);
-            else GBPE_TAIL_LAUNCH(uint32_t, false);
-        }
-#undef GBPE_TAIL_LAUNCH
-        GBPE_LAUNCH_CHECK(t->ctx);
-        if (timing) TR_HIP(t, hipEventRecord(t->evs[1], s));
-        return GBPE_OK;
-    };
-#else
-    const bool tail = false;   // (diagnostic build only: -DGBPE_TAIL_LOOP, tools/build_variant.sh)
-    auto launch_tail = [&]() -> int { return GBPE_OK; };
-#endif
     auto launch_all = [&]() -> int {
-        if (tail) return launch_tail();
         for (uint32_t r = 0; r < k; ++r) {
             hipEvent_t* ev = timing ? &t->evs[5 * r] : nullptr;
             int rc;
@@ -429,18 +387,6 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     {
         int rc = launch_all();
         if (rc != GBPE_OK) return rc;
-        if (sparse && !tail && hs_mode(t, sg)) {
-            // hand-off selection: close the step's last merge, every block maximum exact again
-            if (t->u16)
-                hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(g_refresh), dim3(TPB), 0, s, t->st, 0u, 3, t->tb,
-                                   (uint16_t*)nullptr, (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part,
-                                   t->zseg);
-            else
-                hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(g_refresh), dim3(TPB), 0, s, t->st, 0u, 3, t->tb,
-                                   (uint32_t*)nullptr, (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part,
-                                   t->zseg);
-            GBPE_LAUNCH_CHECK(t->ctx);
-        }
         // the read-backs (and, sparse, k_live's count) in one launch: no copy blits
         const bool cl = sparse && t->d_clog;
         hipLaunchKernelGGL(k_step_out, dim3(1), dim3(1024), 0, s, t->st, sparse ? t->zst : (DevState*)nullptr, t->tb,
@@ -459,13 +405,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
                               (err & ERR_SPARSE_WINDOW) ? "sparse stale window outside the zone " : "",
                               (err & ERR_SPIN) ? "zone segment hand-off timed out" : "");
     }
-    if (timing && tail) {
-        float ms = 0;
-        hipEventElapsedTime(&ms, t->evs[0], t->evs[1]);
-        t->ms_tail += ms;
-        t->ms_sparse += ms;
-        t->timed_merges += done;
-    } else if (timing) {
+    if (timing) {
         for (uint32_t r = 0; r < done; ++r) {
             float a = 0, b = 0, c = 0, d1 = 0, d2 = 0;
             hipEvent_t* ev = &t->evs[5 * r];
@@ -503,17 +443,6 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
             fprintf(t->trace, "%u %u %llu %d %u %u\n", t->done + r, t->h_log[r * 4 + 3], (unsigned long long)nn,
                     sparse ? 1 : 0, sparse && t->h_clog ? t->h_clog[2 * r] : 0u, sparse && t->h_clog ? t->h_clog[2 * r + 1] : 0u);
             nn -= t->h_log[r * 4 + 3];
-        }
-    }
-    if (tail) {
-        t->tail_merges += done;
-        ++t->tail_steps;
-        if (done < k && !hs->stop && !hs->sp_abort) {   // left early (LDS lists): k_body finishes the step
-            t->tail_skip = true;
-            ++t->tail_exits;
-            if (done == 0) {   // (its first merge did not fit): run the step with k_body now
-                return trainer_step_once(t, max_merges, merges_out, n_done, early_stop);
-            }
         }
     }
     if (sparse) {
@@ -594,10 +523,6 @@ extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
     o->lexicon_words = t->lx_words;
     o->lexicon_entries = t->lx_nuid;
     o->lexicon_symbols = t->lx_len;
-    o->tail_merges = t->tail_merges;
-    o->tail_steps = t->tail_steps;
-    o->tail_exits = t->tail_exits;
-    o->ms_tail = t->ms_tail;
     if (t->wg_bytes && t->wg_cap) {   // the per-workgroup counters of k_body (and its zone workgroup)
         std::vector<uint64_t> h(t->wg_cap);
         if (hipMemcpy(h.data(), t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess)
@@ -635,7 +560,7 @@ extern "C" int gbpe_trainer_symbols(gbpe_trainer* t, uint32_t* out, uint64_t cap
 }
 
 // current + previous stream (consolidation).  The previous stream
-// is the other ping-pong buffer over the previous length: a shard's pln, or
+// is the other ping-pong buffer over the previous length:
 // n + last count on one device (zeros before the first merge).
 extern "C" int gbpe_trainer_export_state(gbpe_trainer* t, uint32_t* cur, uint64_t cap_cur, uint64_t* n_cur,
                                          uint32_t* prev, uint64_t cap_prev, uint64_t* n_prev, int on_device) {
@@ -649,7 +574,7 @@ extern "C" int gbpe_trainer_export_state(gbpe_trainer* t, uint32_t* cur, uint64_
     TR_HIP(t, hipStreamSynchronize(s));
     const uint64_t n = t->n;
     // (a trainer created from a state and not stepped since re-exports the imported length)
-    uint64_t np = t->sharded ? (uint64_t)t->h_st->pln : (t->done ? n + t->last_mc : (t->n_prev0 ? t->n_prev0 : n));
+    uint64_t np = t->done ? n + t->last_mc : (t->n_prev0 ? t->n_prev0 : n);
     if (np > t->cap_syms) np = t->cap_syms;
     *n_cur = n;
     *n_prev = np;
@@ -707,12 +632,6 @@ extern "C" int gbpe_trainer_pair_counts(gbpe_trainer* t, uint32_t* pids, uint32_
 extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     if (!t) return;
     if (t->ctx && t->ctx->stream) hipStreamSynchronize(t->ctx->stream);
-    if (t->hs_stat && getenv("GBPE_HS_STATS")) {   // hand-off selections and their verification retries
-        uint32_t h[2] = {0, 0};
-        if (hipMemcpy(h, t->hs_stat, 8, hipMemcpyDeviceToHost) == hipSuccess)
-            fprintf(stderr, "[gpubpe] hand-off selections %u, verification retries %u (%u launches)\n", h[1], h[0],
-                    t->hs_seq);
-    }
 #ifdef GBPE_KTRACE
     if (const char* path = getenv("GBPE_KTRACE_OUT")) {   // one file per trainer: path.<done merges>
         std::vector<unsigned long long> h((size_t)(KT_MERGES / KT_EVERY) * 2 * KT_WG * KT_SLOTS);
@@ -754,8 +673,6 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->part);
     hipFree(t->d_bhist);
     hipFree(t->zseg);
-    hipFree(t->hs_rec);
-    hipFree(t->hs_stat);
     hipFree(t->zdr_out);
     hipFree(t->zdr_offs);
     hipFree(t->zdr_flag);
@@ -765,17 +682,10 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->lx_occ);
     hipFree(t->lx_w0);
     hipFree(t->lx_tmp);
-    hipFree(t->d_tstat);
     if (t->h_zst) hipHostFree(t->h_zst);
     hipFree(t->d_clog);
     if (t->h_clog) hipHostFree(t->h_clog);
     if (t->trace) fclose(t->trace);
-    hipFree(t->dt.slots);
-    hipFree(t->dt.dirty);
-    hipFree(t->d_nlog);
-    hipFree(t->rec_send);
-    hipFree(t->rec_recv);
-    if (t->h_nlog) hipHostFree(t->h_nlog);
     hipFree(t->st);
     hipFree(t->d_log);
     if (t->h_st) hipHostFree(t->h_st);

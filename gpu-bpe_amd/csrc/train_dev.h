@@ -1,7 +1,7 @@
 // Device side of the training loop (kernels, loop state, pair table, LDS tables,
 // the sector-sparse loop and the word lexicon), shared by the translation units
-// train.hip (single-device trainer), train_shard.hip (sharded protocol) and
-// train_lexshard.hip (sharded first pass + lexicon hand-over).  Every kernel
+// train.hip (single-device trainer) and train_lexshard.hip (sharded first
+// pass + lexicon hand-over).  Every kernel
 // lives in an anonymous namespace: each unit compiles the instances it launches.
 #pragma once
 
@@ -47,23 +47,6 @@ struct DevState {
     uint64_t tail_total;   // sum of m
     uint32_t max_live;     // max of `live` over all selects
     uint32_t epoch;        // merge sequence number
-    // ── sharded training (gbpe_shard_*); n / new_n above are then LOCAL: the
-    //    local stream length and the local keep limit ──
-    uint32_t sharded, rank, world, stall;
-    uint32_t dused;        // occupied slots of the per-merge delta table
-    uint32_t dcount;       // delta entries of this merge (the record's list length)
-    uint32_t need_l, need_w;   // capacities a stalled merge asked for (max over ranks)
-    uint32_t owner;        // rank that appended this merge's stale window
-    uint32_t nl_next;      // local length after this merge
-    uint32_t m_glob;       // global stale-window length of this merge
-    uint32_t pln;          // local length of the previous input stream (stale-window source)
-    uint64_t gn;           // global stream length
-    uint64_t off;          // global offset of the local stream
-    uint64_t poff;         // global offset of the previous input stream
-    uint64_t off_next;
-    uint64_t gnew;         // gn - mc
-    uint32_t peak_l, peak_w;   // largest record list / window piece of this step (capacity sizing)
-    uint32_t dfull;            // the delta table overflowed this merge
     // ── sector-sparse loop (n / new_n above stay GLOBAL; the zone has its own DevState) ──
     uint32_t B;            // body length: symbols in the word-aligned sectors before the zone
     uint32_t Bp;           // body length during the previous merge (stale-window source offset)
@@ -72,7 +55,6 @@ struct DevState {
     uint32_t sel_round;    // sector-sparse: round + 1 of the merge k_body selected
     uint64_t sp_bytes;     // sector-sparse: bytes moved by the multi-tile zone passes (k_refresh adds them)
     uint32_t zlast;        // sector-sparse: zone length of the rank that holds the zone (global knowledge)
-    uint32_t ln_last;      // sharded: the last rank's local length after the last merge (from the records)
     uint32_t is_last;      // sector-sparse: this rank holds the zone (single GPU: always)
     uint32_t cand;         // candidate sectors of this merge (trace)
     uint32_t hitsec;       // sectors with a site (trace)
@@ -80,18 +62,15 @@ struct DevState {
                            // (never written by a commit: a reader beside k_body would see it unchanged)
     uint32_t enter_lim;    // dense loop: end the step at the first merge whose count is <= this (the host
                            // can then enter the sector-sparse loop; 0 = off)
-    uint32_t body_rm_base; // HS: body_rm at the last in-launch closing (body_rm itself is only reset by
-                           // k_refresh; this merge removed body_rm - body_rm_base)
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
 // Offset of a merge's stale-window source in the zone's other buffer: n - 2mc - Bp
 // (global positions).  On one device n and Bp are kept modulo 2^32 — a trainer
 // built from shards holds more than 2^32 symbols — and only their
-// difference, a zone-sized length, is used; sharded ranks add their offsets.
+// difference, a zone-sized length, is used.
 __device__ __forceinline__ uint64_t win_src0(const DevState& g, uint32_t mc) {
-    return g.sharded ? (uint64_t)g.n + g.off - g.poff - 2ull * mc - g.Bp
-                     : (uint64_t)(uint32_t)(g.n - g.Bp) - 2ull * mc;
+    return (uint64_t)(uint32_t)(g.n - g.Bp) - 2ull * mc;
 }
 
 // the zone segments' per-merge hand-off (zone_seg; k_refresh zeroes it)
@@ -124,28 +103,14 @@ __device__ __forceinline__ void kt_put(uint32_t round, uint32_t wg, int i, unsig
 #define KT(i) kt_put(round, blockIdx.x, (i), wall_clock64())
 #define KTV(i, v) kt_put(round, blockIdx.x, (i), (v))
 #define KTR(i) kt_put(round, KT_WG + blockIdx.x, (i), wall_clock64())
-#define TKT(i) kt_put(r, 1u, (i), wall_clock64())   // k_tail's own phases (workgroup slot 1)
-#define TKTV(i, v) kt_put(r, 1u, (i), (v))
 #else
-#define TKT(i) ((void)0)
-#define TKTV(i, v) ((void)0)
 #define KT(i) ((void)0)
 #define KTV(i, v) ((void)0)
 #define KTR(i) ((void)0)
 #endif
 
-// exchange-record header words of sharded training (gpubpe/sharded.py mirrors them)
-enum : uint32_t {
-    H_ACTIVE = 0, H_L, H_KEPT, H_M, H_W, H_LASTSYM, H_HASLAST, H_SURV, H_LN, H_MC, H_A, H_B, H_ID, H_DFULL,
-    H_ZN = 14,             // sector-sparse records: the zone length after the merge (last rank), its window m
-    H_ZM = 15, HDR = 16
-};
-
 enum : uint32_t {
     ERR_TABLE_FULL = 1, ERR_COUNT_MISMATCH = 2, ERR_PAIR_MISSING = 4, ERR_SPIN = 8,
-    ERR_SHARD_CAPACITY = 16,   // a rank's stream outgrew its buffers (stale window appended)
-    ERR_SHARD_RECORD = 32,     // exchange records disagree (ranks out of step)
-    ERR_SHARD_LAYOUT = 64,     // gathered survivor / length totals do not add up
     ERR_SPARSE_WINDOW = 128    // sector-sparse: a stale window reaches past the zone's stale buffer
 };
 
@@ -158,11 +123,6 @@ struct Table {
     uint32_t* blive;   // per block: entries with count > 0
     uint32_t nblk;
     uint32_t* used;    // occupied-slot counter (DevState::used or ::dused)
-    uint32_t* full;    // non-null: a full table sets *full instead of the fatal error (delta table)
-    // hand-off selection (HS, k_body): bmax and the group maxima are upper BOUNDS between
-    // k_refresh passes, raised by positive deltas (slot_add; the selector verifies them)
-    uint64_t* bpart = nullptr;   // group bounds (k_refresh's partial maxima), null: exact maxima
-    uint32_t bper = 1;           // blocks per group
 };
 
 // the key of a block without a positive count (count 0, the weakest tie-break)
@@ -172,38 +132,6 @@ constexpr uint64_t KEY_NONE = 0xFFFFFFFFull;
 __device__ __forceinline__ void mark_dirty(const Table& tb, DevState* st, uint32_t slot) {
     (void)st;
     tb.dirty[slot >> BLK_LOG2] = 1u;
-}
-
-// The HS view of the table (k_body's flushes in the hand-off selection mode):
-// its adds also raise the bounds.  A distinct type, so the exact-maxima paths
-// compile as before (overload resolution picks the add).
-struct TableB : Table {};
-template <bool B> struct TbSel { using type = Table; };
-template <> struct TbSel<true> { using type = TableB; };
-template <bool B>
-__device__ __forceinline__ typename TbSel<B>::type tb_view(const Table& t) {
-    typename TbSel<B>::type r;
-    static_cast<Table&>(r) = t;
-    return r;
-}
-
-// Count add at a found slot of the HS table: a positive delta returns the new
-// count and raises the block's and the group's bound to the pair's key
-// (atomicMax).  Whichever add to a pair lands last, a bound saw a count >= the
-// final one, so the bounds stay >= every key; negative deltas raise nothing.
-__device__ __forceinline__ void slot_add(const TableB& tb, DevState* st, uint32_t idx, uint32_t pid, uint32_t delta) {
-    if ((int32_t)delta > 0) {
-        const uint32_t nv = atomicAdd(&tb.slots[idx].y, delta) + delta;
-        if ((int32_t)nv > 0) {
-            const unsigned long long key = ((unsigned long long)nv << 32) | (uint32_t)~pid;
-            const uint32_t blk = idx >> BLK_LOG2;
-            atomicMax(reinterpret_cast<unsigned long long*>(&tb.bmax[blk]), key);
-            atomicMax(reinterpret_cast<unsigned long long*>(&tb.bpart[blk / tb.bper]), key);
-        }
-    } else {
-        atomicAdd(&tb.slots[idx].y, delta);
-    }
-    mark_dirty(tb, st, idx);
 }
 
 // global insert-or-add (triangular probing visits every slot of a 2^k table)
@@ -225,30 +153,7 @@ __device__ void table_add(const Table& tb, DevState* st, uint32_t pid, uint32_t 
             return;
         }
     }
-    if (tb.full) *tb.full = 1u;   // per-merge delta table sized too small: the merge stalls and retries bigger
-    else atomicOr(&st->err, ERR_TABLE_FULL);
-}
-
-// the HS table's insert-or-add
-__device__ void table_add(const TableB& tb, DevState* st, uint32_t pid, uint32_t delta) {
-    uint32_t h = gbpe_fmix32(pid) & tb.mask;
-    for (uint32_t p = 0; p <= tb.mask; ++p) {
-        uint32_t idx = (h + ((p * (p + 1)) >> 1)) & tb.mask;
-        uint32_t k = __hip_atomic_load(&tb.slots[idx].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k == 0u) {
-            k = atomicCAS(&tb.slots[idx].x, 0u, pid);
-            if (k == 0u) {
-                if (tb.used) __hip_atomic_fetch_add(tb.used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                k = pid;
-            }
-        }
-        if (k == pid) {
-            slot_add(tb, st, idx, pid, delta);
-            return;
-        }
-    }
-    if (tb.full) *tb.full = 1u;   // per-merge delta table sized too small: the merge stalls and retries bigger
-    else atomicOr(&st->err, ERR_TABLE_FULL);
+    atomicOr(&st->err, ERR_TABLE_FULL);
 }
 
 __device__ uint32_t table_find(const Table& tb, uint32_t pid) {
@@ -311,7 +216,7 @@ __device__ __forceinline__ void table_add8(const Table& tb, DevState* st, const 
     for (int j = 0; j < 8; ++j) {
         if (!kk[j] || !vv[j]) continue;
         if (hk[j] == kk[j]) {
-            atomicAdd(&tb.slots[hs[j]].y, vv[j]);   // (never a bounds table: HS flushes take table_add)
+            atomicAdd(&tb.slots[hs[j]].y, vv[j]);
             mark_dirty(tb, st, hs[j]);
         } else {
             table_add(tb, st, kk[j], vv[j]);
@@ -330,7 +235,7 @@ template <int N, typename TB>
 __device__ __forceinline__ void lds_flush(LdsTab<N>& t, const TB& tb, DevState* st) {
     __syncthreads();
     const uint32_t nt = blockDim.x;
-    if (!std::is_same<TB, TableB>::value && N > 8 * (int)nt) {   // (the HS table takes the list path: table_add)
+    if (N > 8 * (int)nt) {
         for (uint32_t i0 = threadIdx.x; i0 < (uint32_t)N; i0 += 8 * nt) {
             uint32_t kk[8], vv[8];
 #pragma unroll
@@ -551,7 +456,7 @@ __global__ __launch_bounds__(256) void k_count_hist(const uint32_t* __restrict__
 }
 
 __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log, uint32_t* __restrict__ grpsum,
-                             uint32_t* __restrict__ nlog, uint32_t* __restrict__ rec, DevState* zst, uint32_t exact);
+                             DevState* zst, uint32_t exact);
 
 // (unused launch argument: the selection fused into k_refresh was measured slower)
 struct FusedSel {
@@ -606,14 +511,9 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
         __syncthreads();
         const DevState& g = s_g.d;
         const DevState& z = s_z.d;
-        // finish == 3 (the HS steps' closing launch): whichever merge is still open
-        const uint32_t r = finish == 3 ? g.merges_done : round;
+        const uint32_t r = round;
         const bool fin = finish >= 2 ? (!g.stop && !g.sp_abort && g.sel_round == r + 1u)
-                                     : (!g.stop && !g.stall && g.merges_done == r + 1u);
-        if (finish == 3 && !fin && threadIdx.x == 0 && g.body_rm_base) {   // no open merge: body_rm relative to 0 again
-            st->body_rm = g.body_rm - g.body_rm_base;
-            st->body_rm_base = 0u;
-        }
+                                     : (!g.stop && g.merges_done == r + 1u);
         if (fin && threadIdx.x == 0) {
             if (zst) {   // sector-sparse: global length, body length, zone length
                 if (finish >= 2) {
@@ -629,24 +529,16 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
                 st->cand = 0u;
                 st->hitsec = 0u;
                 st->tail_total = g.tail_total + z.m;
-                const uint32_t n = g.new_n, B = g.B - (g.body_rm - g.body_rm_base), zn = n - B;
+                const uint32_t n = g.new_n, B = g.B - g.body_rm, zn = n - B;
                 st->n = n;
                 st->Bp = g.B;
                 st->B = B;
                 st->body_rm = 0u;
-                st->body_rm_base = 0u;
                 zst->n = zn;
-                if (!g.sharded) st->zlast = zn;   // sharded: from the records (k_shard_apply)
+                st->zlast = zn;
                 if (!z.valid_total && g.is_last)   // multi-tile zone: k_delta + k_compact stream it twice, plus the window copy
                     st->sp_bytes = g.sp_bytes + (uint64_t)sizeof(S) * (2ull * z.n + zn + 2ull * g.mc);
                 if (z.valid_total && z.valid_total != zn + 1u) atomicOr(&st->err, ERR_COUNT_MISMATCH);
-            } else if (g.sharded) {   // commit the new global layout computed by k_shard_recv
-                st->tail_total = g.tail_total + g.m_glob;
-                st->poff = g.off;
-                st->pln = g.n;
-                st->n = g.nl_next;
-                st->off = g.off_next;
-                st->gn = g.gnew;
             } else {
                 st->tail_total = g.tail_total + g.m;
                 st->n = g.new_n;
@@ -723,12 +615,11 @@ constexpr uint32_t GSTR = 64;   // group sums 256 B apart: each is its own atomi
 // argmax over block maxima + the reference's bpe_setup_merge (train.wgsl:340-364),
 // by one workgroup of any size <= SEL_THREADS
 __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log, uint32_t* __restrict__ grpsum,
-                             uint32_t* __restrict__ nlog, uint32_t* __restrict__ rec, DevState* zst, uint32_t exact) {
+                             DevState* zst, uint32_t exact) {
     __shared__ uint64_t red[SEL_THREADS / 64];
     __shared__ uint32_t rlive[SEL_THREADS / 64];
     const uint32_t nt = blockDim.x;
-    if (rec && threadIdx.x == 0) rec[H_L] = 0u;   // the send kernel's list blocks add their counts into it
-    if (st->stop || st->stall || st->sp_abort) return;
+    if (st->stop || st->sp_abort) return;
     {   // group sums of the coming stream pass (the zone's, when sector-sparse) start at zero
         const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(zst ? zst->n : st->n, TILE), GRP);
         for (uint32_t g = threadIdx.x; g < ngrp; g += nt) grpsum[g * GSTR] = 0u;
@@ -759,9 +650,6 @@ __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log,
     if (live > st->max_live) st->max_live = live;
     st->ndirty = 0u;
     st->m = 0u;
-    st->dcount = 0u;
-    st->dused = 0u;
-    st->dfull = 0u;
     st->valid_total = 0u;
     const uint32_t mc = (uint32_t)(best >> 32);
     const uint32_t pid = ~(uint32_t)best;
@@ -783,7 +671,7 @@ __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log,
         // (n - 2mc >= Bp), and the zone stays >= 5 mc long so the next merge's window
         // does too (its count is <= mc + m <= 2 mc).  Otherwise the merge is not run
         // and the host returns to the dense loop.
-        if ((st->sharded ? (uint64_t)st->n < 2ull * mc + st->Bp : (uint64_t)(uint32_t)(st->n - st->Bp) < 2ull * mc)) {
+        if ((uint64_t)(uint32_t)(st->n - st->Bp) < 2ull * mc) {
             // (cannot happen after the check below held)
             atomicOr(&st->err, ERR_SPARSE_WINDOW);
             st->stop = 1u;
@@ -811,16 +699,7 @@ __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log,
     st->b = pid & 0xFFFFu;
     st->nw = st->next_id;
     st->mc = mc;
-    if (st->sharded) {   // global new length; the local keep limit (train.wgsl:727 on the global stream)
-        const uint64_t gnew = st->gn - mc;
-        st->gnew = gnew;
-        uint64_t lim = st->n;
-        if (!(st->sharded & 2u)) lim = gnew > st->off ? (gnew - st->off < st->n ? gnew - st->off : st->n) : 0u;
-        st->new_n = (uint32_t)lim;
-    } else {
-        st->new_n = st->n - mc;
-    }
-    if (nlog) nlog[d] = st->n;
+    st->new_n = st->n - mc;
     if (zst) {   // the zone's view of the merge: k_delta / k_compact run on it unchanged
         zst->a = st->a;
         zst->b = st->b;
@@ -840,9 +719,8 @@ __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log,
 }
 
 __global__ __launch_bounds__(SEL_THREADS) void k_select(DevState* st, Table tb, uint32_t* __restrict__ log,
-                                                        uint32_t* __restrict__ grpsum, uint32_t* __restrict__ nlog,
-                                                        uint32_t* __restrict__ rec, DevState* zst, uint32_t exact) {
-    select_merge(st, tb, log, grpsum, nlog, rec, zst, exact);
+                                                        uint32_t* __restrict__ grpsum, DevState* zst, uint32_t exact) {
+    select_merge(st, tb, log, grpsum, zst, exact);
 }
 
 // the next merge's count (the table maximum): the sparse entry decision before any merge ran
@@ -1085,15 +963,9 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
             const uint32_t xi = cur[i];
             if (xi & WS) continue;
             const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
-#if defined(GBPE_DIAG_TAIL) && GBPE_DIAG_TAIL >= 2   // diagnostic builds only (wrong counts): loads alone
-            if (tp && ti && ((tp << 16) | ti) == 0xFFFFFFFFu) lt.ovf = 1u;
-#else
             if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
-#endif
         }
-#ifndef GBPE_DIAG_TAIL   // (GBPE_DIAG_TAIL=1: no flush)
         lds_flush(lt, tb, st);
-#endif
         return;
     }
     // tiles past the host's view of the stream (a shard that may have grown by an
@@ -1265,15 +1137,9 @@ __global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, 
             const uint32_t xi = cur[i];
             if (xi & WS) continue;
             const uint32_t tp = cur[i - 1] & TM, ti = xi & TM;
-#if defined(GBPE_DIAG_TAIL) && GBPE_DIAG_TAIL >= 2   // diagnostic builds only (wrong counts): loads alone
-            if (tp && ti && ((tp << 16) | ti) == 0xFFFFFFFFu) lt.ovf = 1u;
-#else
             if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
-#endif
         }
-#ifndef GBPE_DIAG_TAIL   // (GBPE_DIAG_TAIL=1: no flush)
         lds_flush(lt, tb, st);
-#endif
         return;
     }
     uint32_t tail = 0;
@@ -1405,7 +1271,7 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
     const uint32_t ntiles = (uint32_t)gbpe_div_up(n, TILE);
     if (split == 1 && tl >= ntiles) return;
     if (tl >= ntiles || split == 2) {
-        if (EXACT || st->sharded) return;   // sharded: the window is handled by k_shard_recv
+        if (EXACT) return;
         // ── stale tail window ──
         const uint32_t m = st->m;
         if (m == 0) return;
@@ -1530,7 +1396,7 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
         total += wsum[w2];
         prefix += psum[w2];
     }
-    if (tl == ntiles - 1 && t == 0 && !st->sharded &&
+    if (tl == ntiles - 1 && t == 0 &&
         prefix + tile_cnt[tl] != (ZONE ? gst->new_n - (gst->B - gst->body_rm) : new_n))
         atomicOr(ZONE ? (uint32_t*)&gst->err : &st->err, ERR_COUNT_MISMATCH);
     // stage at the destination's alignment phase so both sides move whole 16-byte words
@@ -1975,7 +1841,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
 #pragma unroll
         for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
     }
-    if (!EXACT) {   // window source: global n - 2mc in the previous stream (sharded: it began at poff, now off)
+    if (!EXACT) {   // window source: global n - 2mc in the previous stream
         const uint64_t src0 = win_src0(gs, mc);
         for (uint32_t u = t; u < mc; u += BT) L.wb[u] = zo[src0 + u];
     }
@@ -2356,16 +2222,8 @@ __device__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const 
 // it (log, table slot zeroed, state for k_refresh and the zone kernels).  The
 // step counters move on in k_refresh (finish == 2), so nothing a workgroup reads
 // here changes under it.  Saves the k_select launch per merge.
-// Sharded (cap_list != 0): the zone sits on the last rank only, so the zone checks
-// use st->zlast, the zone length every rank learned from the last exchange; a
-// merge whose count could overflow the exchange record stalls here, before any
-// sector is touched, on every rank alike (the count is global).
 struct SelShard {
-    uint32_t zf = 5;         // zone rule: z >= max(2 mc + mc_prev, zf mc) + 2 (single GPU: GBPE_ZONE_F, sharded 5)
-    uint32_t cap_list = 0;   // 0 = single GPU
-    uint32_t zmax = 0;       // the one-workgroup zone limit (sharded zones never run multi-tile)
-    uint32_t* nlog = nullptr;
-    uint32_t* rec = nullptr; // this rank's exchange record (its list length restarts at 0)
+    uint32_t zf = 3;         // zone rule: z >= max(2 mc + mc_prev, zf mc) + 2 (GBPE_ZONE_F)
 };
 
 template <int BT>
@@ -2394,7 +2252,7 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     const DevState& g = s_g.d;
     gsnap = &s_g.d;
     zsnap = &s_z.d;
-    if (!(round < g.budget && g.merges_done == round && !g.stop && !g.sp_abort && !g.stall)) return false;
+    if (!(round < g.budget && g.merges_done == round && !g.stop && !g.sp_abort)) return false;
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t o = __shfl_xor(best, off);
         best = o > best ? o : best;
@@ -2410,18 +2268,14 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     b = pid & 0xFFFFu;
     nw = g.next_id;
     const bool stop = mc < 2u || nw > 0xFFFFu;                                          // train.wgsl:345-348
-    const bool bad = !stop && !exact && g.is_last &&
-                     (g.sharded ? (uint64_t)g.n + g.off - g.poff < 2ull * mc + g.Bp
-                                : (uint64_t)(uint32_t)(g.n - g.Bp) < 2ull * mc);   // cannot happen
+    const bool bad = !stop && !exact && g.is_last && (uint64_t)(uint32_t)(g.n - g.Bp) < 2ull * mc;   // cannot happen
     // zone misfit: this merge's window source must lie in the zone's stale buffer
     // (n - 2mc >= Bp, where n - Bp >= z - mc_prev: the last merge removed <= mc_prev
     // body symbols), and the zone keeps >= zf mc for the merges after it
-    const uint32_t mc_prev = sh.cap_list ? g.mc : g.mc_prev;
+    const uint32_t mc_prev = g.mc_prev;
     const uint64_t zneed = std::max<uint64_t>(2ull * mc + mc_prev, (uint64_t)sh.zf * mc) + 2u;
-    const bool abort = !stop && !bad && !exact && ((uint64_t)g.zlast < zneed || (sh.zmax && g.zlast > sh.zmax));
-    const uint32_t need = 6u * mc + 64u;   // distinct deltas of one merge <= 4 per site + tail + window
-    const bool stall = !stop && !bad && !abort && sh.cap_list && need > sh.cap_list;
-    const bool go = !stop && !bad && !abort && !stall;
+    const bool abort = !stop && !bad && !exact && (uint64_t)g.zlast < zneed;
+    const bool go = !stop && !bad && !abort;
     // the LAST workgroup commits: block 0 is the zone pass (the launch's longest
     // chain), which then starts without the table probe and the state stores
     if (commit && blockIdx.x == gridDim.x - 1u) {
@@ -2433,18 +2287,7 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
                 st->stop = 1u;
             } else if (abort) {
                 st->sp_abort = 1u;
-            } else if (stall) {   // the host grows the records and redoes this merge
-                st->stall = 1u;
-                st->need_l = need;
-                st->need_w = 0u;
             } else {
-                if (sh.nlog) sh.nlog[round] = g.n;
-                if (sh.rec) {
-                    sh.rec[H_L] = 0u;
-                    st->dcount = 0u;
-                    st->dused = 0u;
-                    st->dfull = 0u;
-                }
                 const uint32_t idx = table_find(tb, pid);
                 if (idx == 0xFFFFFFFFu) {
                     atomicOr(&st->err, ERR_PAIR_MISSING);
@@ -2484,339 +2327,6 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     return go;
 }
 
-// ── hand-off selection (HS, single GPU, zone in one workgroup) ──
-// k_refresh is no longer launched after every merge: block maxima and group
-// maxima are kept as upper BOUNDS (raised by each positive delta, mark_dirty),
-// and ONE workgroup of k_body — block 0, the zone workgroup — closes the last
-// merge (k_refresh's finish-2 bookkeeping), finds the exact maximum and hands
-// (a, b, new id, count) to the others through tagged 8-byte granules:
-//   1. group bounds + state snapshots (one round trip);
-//   2. the bounds of the best group's blocks;
-//   3. the best block's 256 slots: its exact maximum X and runner-up;
-//   4. X >= every other bound (groups and blocks): X is the table maximum.
-//      Otherwise the block's bound is tightened to X (and its group's), and
-//      steps 2-4 repeat.
-// The selected block's bound then drops to its runner-up, so the next selection
-// does not start at a stale holder.  Every bound change is an atomic add, which
-// commutes with the workgroups' own bound raises.  k_refresh (finish 3) closes
-// the last merge of the step and makes every maximum exact again.
-struct HsView {
-    unsigned long long* rec = nullptr;   // hand-off granules: value | tag << 32 (pid, count, new id | go)
-    const uint64_t* part = nullptr;      // group bounds (k_refresh's partial maxima)
-    uint32_t npart = 0, per = 1;         // groups; blocks per group
-    uint32_t tag = 0;                    // this launch's hand-off tag (a sequence number, never reused)
-    uint32_t* clog = nullptr;            // per-merge candidate / hit-sector log (GBPE_SPARSE_TRACE)
-    uint32_t* stat = nullptr;            // [0] verification retries, [1] selections
-};
-constexpr int HS_PPT = 8;          // group bounds per selector thread (the host checks npart <= 8 x threads)
-constexpr uint32_t HS_ITER = 256;  // verification rounds (each tightens one bound)
-
-// (k1, i1) the largest key and its index, k2 the runner-up, over the wave
-__device__ __forceinline__ void top2_wave(uint64_t& k1, uint32_t& i1, uint64_t& k2) {
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o1 = __shfl_xor(k1, off), o2 = __shfl_xor(k2, off);
-        const uint32_t oi = __shfl_xor(i1, off);
-        const bool take = o1 > k1 || (o1 == k1 && oi < i1);
-        const uint64_t lo = take ? k1 : o1;
-        k2 = lo > k2 ? lo : k2;
-        k2 = o2 > k2 ? o2 : k2;
-        if (take) {
-            k1 = o1;
-            i1 = oi;
-        }
-    }
-}
-
-template <int BT>
-__device__ __forceinline__ bool hs_select(DevState* st, DevState* zst, const HsView& hv, const Table& tb, uint32_t round, bool exact,
-                          uint32_t* __restrict__ log, uint32_t* __restrict__ grpsum, const SelShard& sh,
-                          uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc, const DevState*& gsnap,
-                          const DevState*& zsnap) {
-    constexpr int NWV = BT / 64;
-    constexpr int NW = sizeof(DevState) / 4;
-    __shared__ union {
-        DevState d;
-        uint32_t w[NW];
-    } s_g, s_z;
-    __shared__ uint64_t s_k1[NWV], s_k2[NWV];
-    __shared__ uint32_t s_i1[NWV];
-    __shared__ uint64_t s_sel, s_np;
-    __shared__ uint32_t s_state, s_sidx;   // 0 retry, 1 accepted
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const uint32_t npart = hv.npart, per = hv.per;
-    // 1. snapshots and group bounds: one round trip
-    if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
-    else if (t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
-    uint64_t pv[HS_PPT];
-#pragma unroll
-    for (int j = 0; j < HS_PPT; ++j) {
-        const uint32_t i = (uint32_t)j * BT + t;
-        pv[j] = i < npart ? hv.part[i] : 0ull;
-    }
-    __syncthreads();
-    DevState& g = s_g.d;
-    DevState& z = s_z.d;
-    gsnap = &s_g.d;
-    zsnap = &s_z.d;
-    if (t == 0) {
-        // close the previous merge (k_refresh finish 2, mirrored): its deltas are all in
-        if (!g.stop && !g.sp_abort && g.sel_round == g.merges_done + 1u) {
-            const uint32_t r = g.merges_done;
-            if (hv.clog) {   // (trace only) counters the other workgroups add to: exchanged, waited for before the hand-off
-                hv.clog[2 * r] = atomicExch(&st->cand, 0u);
-                hv.clog[2 * r + 1] = atomicExch(&st->hitsec, 0u);
-            }
-            g.merges_done = r + 1u;
-            g.next_id += 1u;
-            g.epoch += 1u;
-            g.mc_prev = g.mc;
-            g.tail_total += z.m;
-            // body_rm is not reset here (the others add to it in this launch): its base moves
-            const uint32_t n = g.new_n, B = g.B - (g.body_rm - g.body_rm_base), zn = n - B;
-            if (z.valid_total && z.valid_total != zn + 1u) atomicOr(&st->err, ERR_COUNT_MISMATCH);
-            g.n = n;
-            g.Bp = g.B;
-            g.B = B;
-            g.body_rm_base = g.body_rm;
-            st->body_rm_base = g.body_rm;
-            g.zlast = zn;
-            g.cand = g.hitsec = 0u;
-            z.n = zn;
-            st->merges_done = g.merges_done;
-            st->next_id = g.next_id;
-            st->epoch = g.epoch;
-            st->mc_prev = g.mc_prev;
-            st->tail_total = g.tail_total;
-            st->n = n;
-            st->Bp = g.Bp;
-            st->B = B;
-            st->zlast = zn;
-            zst->n = zn;
-        }
-    }
-    __syncthreads();
-    bool go = round < g.budget && g.merges_done == round && !g.stop && !g.sp_abort && !g.stall;
-    if (go) {
-        // 2-4: the exact maximum
-        uint32_t it = 0;
-        for (;; ++it) {
-            uint64_t k1 = 0, k2 = 0;
-            uint32_t i1 = 0xFFFFFFFFu;
-#pragma unroll
-            for (int j = 0; j < HS_PPT; ++j) {
-                const uint32_t i = (uint32_t)j * BT + t;
-                const uint64_t v = pv[j];
-                if (v > k1) {
-                    k2 = k1;
-                    k1 = v;
-                    i1 = i;
-                } else if (v > k2) {
-                    k2 = v;
-                }
-            }
-            top2_wave(k1, i1, k2);
-            if (lane == 0) {
-                s_k1[wid] = k1;
-                s_k2[wid] = k2;
-                s_i1[wid] = i1;
-            }
-            __syncthreads();
-            if (wid == 0) {
-                k1 = lane < NWV ? s_k1[lane] : 0ull;
-                k2 = lane < NWV ? s_k2[lane] : 0ull;
-                i1 = lane < NWV ? s_i1[lane] : 0xFFFFFFFFu;
-                top2_wave(k1, i1, k2);
-                const uint32_t g1 = i1 < npart ? i1 : 0u;
-                const uint64_t pg = k1, pout = k2;   // the best group's bound, the best other group's
-                // 2+3 in one round trip when the group bound's pair sits in its home block
-                // (the common case: raised by atomicMax, the bound IS that pair's key): that
-                // block's slots load with the group's block bounds (atomic loads: this
-                // workgroup may have tightened them); otherwise the bounds first
-                const uint32_t hb = (gbpe_fmix32(~(uint32_t)pg) & tb.mask) >> BLK_LOG2;
-                // (first round only: a retry takes the bounds' order, which always tightens a
-                // stale bound; a guessed block need not be the stale one)
-                const bool guess = it == 0u && hb / per == g1;
-                const uint32_t hl = hb - g1 * per;
-                const uint32_t blk = g1 * per + (uint32_t)lane;
-                const bool inb = (uint32_t)lane < per && blk < tb.nblk;
-                uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0;
-                if (guess) {
-                    const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)hb << BLK_LOG2));
-                    e0 = sl[lane];
-                    e1 = sl[lane + 64];
-                }
-                const uint64_t bb = inb ? __hip_atomic_load(&tb.bmax[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-                uint32_t b1;
-                uint64_t c1, c2;   // the chosen block's bound, the best bound of the group's other blocks
-                if (guess) {
-                    b1 = hb;
-                    c1 = __shfl(bb, (int)hl);
-                    c2 = (uint32_t)lane == hl ? 0ull : bb;
-                    for (int off = 32; off > 0; off >>= 1) {
-                        const uint64_t o = __shfl_xor(c2, off);
-                        c2 = o > c2 ? o : c2;
-                    }
-                } else {
-                    uint32_t ci = inb ? (uint32_t)lane : 0xFFFFFFFFu;
-                    c1 = bb;
-                    c2 = 0;
-                    top2_wave(c1, ci, c2);
-                    b1 = g1 * per + (ci < 64u ? ci : 0u);
-                    const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)b1 << BLK_LOG2));
-                    e0 = sl[lane];
-                    e1 = sl[lane + 64];
-                }
-                // 3. the block's exact maximum and runner-up
-                uint64_t x1 = 0, x2 = 0;
-                uint32_t xi = 0xFFFFFFFFu;
-                {
-                    const uint32_t px[4] = {e0.x, e0.z, e1.x, e1.z}, py[4] = {e0.y, e0.w, e1.y, e1.w};
-                    const uint32_t pos[4] = {2u * lane, 2u * lane + 1u, 128u + 2u * lane, 129u + 2u * lane};
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        if (px[q] && (int32_t)py[q] > 0) {
-                            const uint64_t key = ((uint64_t)py[q] << 32) | (uint32_t)(~px[q]);
-                            if (key > x1) {
-                                x2 = x1;
-                                x1 = key;
-                                xi = pos[q];
-                            } else if (key > x2) {
-                                x2 = key;
-                            }
-                        }
-                    }
-                }
-                top2_wave(x1, xi, x2);
-                if (x1 == 0) x1 = KEY_NONE;
-                if (x2 == 0) x2 = KEY_NONE;
-                // 4. X against every other bound
-                const uint64_t rest = pout > c2 ? pout : c2;
-                if (lane == 0) {
-                    if (x1 >= rest || it + 1u >= HS_ITER) {
-                        if (x1 < rest) atomicOr(&st->err, ERR_SPIN);   // (bounds that never settle: cannot happen)
-                        s_state = 1u;
-                        s_sel = x1;
-                        s_sidx = (b1 << BLK_LOG2) | (xi & 255u);
-                        // the block loses its holder: its bound drops to the runner-up, the
-                        // group's to its best remaining block
-                        const uint64_t np = x2 > c2 ? x2 : c2;
-                        s_np = np;
-                        if (x1 != KEY_NONE) {
-                            atomicAdd(reinterpret_cast<unsigned long long*>(&tb.bmax[b1]), (unsigned long long)(x2 - c1));
-                            atomicAdd(reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(&hv.part[g1])),
-                                      (unsigned long long)(np - pg));
-                        }
-                    } else {   // a stale bound: tighten it to X, and the group's
-                        s_state = 0u;
-                        const uint64_t np = x1 > c2 ? x1 : c2;
-                        s_np = np;
-                        atomicAdd(reinterpret_cast<unsigned long long*>(&tb.bmax[b1]), (unsigned long long)(x1 - c1));
-                        atomicAdd(reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(&hv.part[g1])),
-                                  (unsigned long long)(np - pg));
-                    }
-                    s_i1[0] = g1;
-                }
-            }
-            __syncthreads();
-            if (s_state) break;
-            {   // the owner of the tightened group updates its copy
-                const uint32_t g1 = s_i1[0];
-#pragma unroll
-                for (int j = 0; j < HS_PPT; ++j)
-                    if ((uint32_t)j * BT + t == g1) pv[j] = s_np;
-            }
-            __syncthreads();
-        }
-        if (t == 0 && hv.stat) {
-            atomicAdd(&hv.stat[0], it);
-            atomicAdd(&hv.stat[1], 1u);
-        }
-        const uint64_t best = s_sel;
-        mc = (uint32_t)(best >> 32);
-        const uint32_t pid = ~(uint32_t)best;
-        a = pid >> 16;
-        b = pid & 0xFFFFu;
-        nw = g.next_id;
-        // the reference's stop rule and the zone invariants, as sel_inline
-        const bool stop = mc < 2u || nw > 0xFFFFu;                                          // train.wgsl:345-348
-        const bool bad = !stop && !exact && (uint64_t)(uint32_t)(g.n - g.Bp) < 2ull * mc;   // cannot happen
-        const uint64_t zneed = std::max<uint64_t>(2ull * mc + g.mc_prev, (uint64_t)sh.zf * mc) + 2u;
-        const bool abort = !stop && !bad && !exact && ((uint64_t)g.zlast < zneed || (sh.zmax && g.zlast > sh.zmax));
-        go = !stop && !bad && !abort;
-        if (t == 0) {
-            if (stop) {
-                st->stop = 1u;
-            } else if (bad) {
-                atomicOr(&st->err, ERR_SPARSE_WINDOW);
-                st->stop = 1u;
-            } else if (abort) {
-                st->sp_abort = 1u;
-            } else {
-                const uint32_t idx = s_sidx;
-                atomicSub(&tb.slots[idx].y, mc);   // every (a,b) occurrence is a merge site
-                tb.dirty[idx >> BLK_LOG2] = 1u;
-                log[round * 4 + 0] = a;
-                log[round * 4 + 1] = b;
-                log[round * 4 + 2] = nw;
-                log[round * 4 + 3] = mc;
-                st->a = a;
-                st->b = b;
-                st->nw = nw;
-                st->mc = mc;
-                st->new_n = g.n - mc;
-                zst->a = a;
-                zst->b = b;
-                zst->nw = nw;
-                zst->mc = mc;
-                zst->new_n = exact ? z.n : z.n - mc;
-                zst->merges_done = round + 1u;
-                st->sel_round = round + 1u;
-            }
-        }
-        if (go) {   // group sums of a multi-tile zone pass start at zero
-            const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(z.n, TILE), GRP);
-            for (uint32_t q = t; q < ngrp; q += BT) grpsum[q * GSTR] = 0u;
-        }
-    }
-    // hand-off: three tagged granules (the commit's atomics commute with the other
-    // workgroups' adds; only the trace counters' exchange must land first)
-    if (t == 0) {
-        if (hv.clog) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned long long tg = (unsigned long long)hv.tag << 32;
-        __hip_atomic_store(&hv.rec[0], tg | (go ? ((a << 16) | b) : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&hv.rec[1], tg | (go ? mc : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&hv.rec[2], tg | (go ? (0x80000000u | nw) : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return go;
-}
-
-// the other workgroups: poll the three granules of this launch's tag
-__device__ __forceinline__ bool hs_wait(const HsView& hv, DevState* st, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc) {
-    __shared__ uint32_t s_v[3], s_to;
-    if (threadIdx.x == 0) s_to = 0u;
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        unsigned long long v = 0;
-        for (uint32_t spins = 0;; ++spins) {
-            v = __hip_atomic_load(&hv.rec[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)(v >> 32) == hv.tag) break;
-            if (spins > ZSEG_SPIN) {   // the selector never published: give up (reported)
-                atomicOr(&st->err, ERR_SPIN);
-                s_to = 1u;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        s_v[threadIdx.x] = (uint32_t)v;
-    }
-    __syncthreads();
-    a = s_v[0] >> 16;
-    b = s_v[0] & 0xFFFFu;
-    mc = s_v[1];
-    nw = s_v[2] & 0xFFFFu;
-    return !s_to && (s_v[2] >> 31) != 0u;
-}
-
 // Body pass: blocks [0, nbody) each own `wpg` consecutive bitmap words of
 // (a-row & b-row), tested PW words at a time: the candidate sectors whose pair
 // signature may hold (a, b) are merged (one wave per sector).  A fixed grid of
@@ -2842,7 +2352,7 @@ union BodyLds {   // body workgroups use the candidate arrays, the zone workgrou
 // ZSEG: the form for zones of 32K-1M symbols: blocks [0, zone1) run the zone
 // segments (zone_seg) beside the body blocks, and zone_one is not compiled in
 // (with both, every form spilled to scratch)
-template <typename S, bool EXACT, int BT, int ZPT = ZoneDim<S, BT>::ZPT, bool ZSEG = false, bool HS = false>
+template <typename S, bool EXACT, int BT, int ZPT = ZoneDim<S, BT>::ZPT, bool ZSEG = false>
 __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
                                               uint32_t* __restrict__ bits, uint32_t W, uint32_t wpg,
                                               uint32_t* __restrict__ sig, Table tb, uint32_t nbody,
@@ -2851,7 +2361,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
                                               Table dtb, SelShard sh, uint32_t* __restrict__ lmul,
-                                              ZSegState* __restrict__ zg = nullptr, HsView hv = HsView()) {
+                                              ZSegState* __restrict__ zg = nullptr) {
     constexpr int KB_LT = ZSEG ? 4096 : LTAB_T;
     __shared__ LdsTab<KB_LT> lt;
     __shared__ BodyLds<S, BT> u;
@@ -2862,21 +2372,14 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     uint32_t a, b, nw, mc;
     if (t == 0) KT(0);
     const DevState *gs = nullptr, *zs = nullptr;   // this workgroup's snapshots of the states at launch (LDS)
-    const auto xtb = tb_view<HS>(dtb);   // the HS table view raises the bounds with its adds
-    if constexpr (HS) {   // hand-off selection: block 0 (the zone workgroup) selects, the others wait for it
-        if (blockIdx.x == 0) {
-            if (!hs_select<BT>(st, zst, hv, tb, round, EXACT, log, grpsum, sh, a, b, nw, mc, gs, zs)) return;
-        } else if (!hs_wait(hv, st, a, b, nw, mc)) {
-            return;
-        }
-    } else if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh)) {
+    const Table& xtb = dtb;
+    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh)) {
         return;
     }
     if (t == 0) KT(1);
     // the zone workgroup is dispatched first (block 0 when zone1): it is the longest
     // single chain of the merge, and later blocks of a large grid start later
     const uint32_t bid = blockIdx.x - zone1;
-    // deltas go to the replica (single GPU) or to the per-merge delta table (sharded)
     if constexpr (ZSEG) {
         if (blockIdx.x < zone1) {
             zone_seg<S, EXACT, BT, KB_LT, 16>(st, zst, *gs, *zs, zcur, (S*)zoth, zg, zone1, u.z, lt, dtb, a, b, nw, mc,
@@ -3031,425 +2534,6 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         KTV(6, 1 | (ncand_all << 8));
     }
 }
-
-// ── persistent tail loop ──
-// Late merges (a few hundred sites in a handful of distinct words, a zone of a
-// few K symbols) cost launches and dependent round trips, not bytes: k_body +
-// k_refresh spend ~20 us per merge at 1 GiB on ~10 candidate sectors.  k_tail is
-// ONE 1024-thread workgroup that runs a whole step's merges back to back.  It is
-// the only writer of the pair table while it runs, so
-//   * selection reduces group maxima kept in LDS (64 argmax blocks per group)
-//     instead of a k_refresh pass and its partial maxima;
-//   * count deltas reach the table as plain read-modify-writes; each raises its
-//     block maximum (atomicMax) or, when it lowers the block's holder, has the
-//     block re-maxed from its 2048 slots by one wave;
-//   * the body pass (every bitmap word of rows a and b in one load, signatures,
-//     one wave per candidate sector) and the zone pass (zone_one) share one LDS
-//     delta table and one flush.
-// It leaves the step early — the host finishes it with k_body — when a merge's
-// candidate sectors or re-maxed blocks outgrow its LDS lists.
-#ifdef GBPE_TAIL_LOOP
-constexpr int TL_BT = 1024;
-constexpr int TL_LT = 4096;               // LDS delta table (body + zone deltas of one merge)
-constexpr uint32_t TL_GRP = 6;            // log2 argmax blocks per group
-constexpr uint32_t TL_MAXG = 256;         // groups: tables of up to 2^25 slots
-constexpr uint32_t TL_RS = 1024;          // re-maxed blocks per merge
-constexpr uint32_t TL_CAND = 8192;        // candidate sectors per merge (token bitmap)
-constexpr uint32_t TL_FILT = 3072;        // ... passing the signature filter
-enum : uint32_t { TL_EXIT_NONE = 0, TL_EXIT_CAND = 1, TL_EXIT_REMAX = 2, TL_EXIT_LDS = 3 };
-
-struct TailBody {   // the body pass's lists (the zone pass reuses this LDS)
-    uint32_t cand[TL_CAND];
-    uint32_t fsec[TL_FILT];
-    uint2 fext[TL_FILT];
-};
-template <typename S>
-union TailU {
-    ZoneLds<S, TL_BT> z;
-    TailBody c;
-};
-static_assert(sizeof(TailBody) <= sizeof(ZoneLds<uint32_t, TL_BT>), "the body lists share the zone's LDS");
-
-__device__ __forceinline__ uint64_t tl_key(uint32_t cnt, uint32_t pid) {
-    return (int32_t)cnt > 0 ? (((uint64_t)cnt << 32) | (uint32_t)~pid) : 0ull;
-}
-
-template <typename S, bool EXACT, int ZPT>
-__global__ __launch_bounds__(TL_BT) void k_tail(DevState* st, DevState* zst, S* __restrict__ body, uint32_t* __restrict__ lmul,
-                                                uint2* __restrict__ sec, uint32_t* __restrict__ bits, uint32_t W,
-                                                uint32_t wused, uint32_t* __restrict__ sig, Table tb, S* __restrict__ zb0,
-                                                S* __restrict__ zb1, uint32_t* __restrict__ log,
-                                                uint64_t* __restrict__ bytes, uint32_t* __restrict__ tstat) {
-    __shared__ TailU<S> u;
-    __shared__ LdsTab<TL_LT> lt;
-    __shared__ uint64_t gmax[TL_MAXG];
-    __shared__ uint32_t rs[TL_RS], rsmark[(TL_MAXG << TL_GRP) / 32], gmark[TL_MAXG / 32];
-    __shared__ uint32_t s_nrs, s_ntok, s_nf, s_rm, s_exit, s_used, s_idx, zout[2];
-    __shared__ uint64_t s_red[TL_BT / 64];
-    constexpr int NW = sizeof(DevState) / 4;
-    constexpr uint32_t NWAVE = TL_BT / 64;
-    __shared__ union {
-        DevState d;
-        uint32_t w[NW];
-    } s_g, s_z;
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const uint32_t ngrp = (tb.nblk + (1u << TL_GRP) - 1) >> TL_GRP;
-    if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
-    else if (t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
-    for (uint32_t g = wid; g < ngrp; g += NWAVE) {   // group maxima from the (exact) block maxima
-        const uint32_t blk = (g << TL_GRP) + (uint32_t)lane;
-        uint64_t v = blk < tb.nblk ? tb.bmax[blk] : 0ull;
-        for (int off = 32; off > 0; off >>= 1) {
-            const uint64_t o = __shfl_xor(v, off);
-            v = o > v ? o : v;
-        }
-        if (lane == 0) gmax[g] = v;
-    }
-    for (uint32_t i = t; i < (TL_MAXG << TL_GRP) / 32; i += TL_BT) rsmark[i] = 0u;
-    if (t < (int)(TL_MAXG / 32)) gmark[t] = 0u;
-    if (t == 0) {
-        s_exit = TL_EXIT_NONE;
-        s_used = 0u;
-    }
-    __syncthreads();
-    DevState& g = s_g.d;
-    DevState& z = s_z.d;
-    const uint32_t K = g.budget;
-    uint64_t mybytes = 0;
-    auto remax_mark = [&](uint32_t blk) {   // queue a block for re-maxing (once per merge)
-        const uint32_t bit = 1u << (blk & 31u);
-        if (!(atomicOr(&rsmark[blk >> 5], bit) & bit)) {
-            const uint32_t q = atomicAdd(&s_nrs, 1u);
-            if (q < TL_RS) rs[q] = blk;
-            else tb.dirty[blk] = 1u;   // k_refresh after the kernel re-maxes it; the loop stops after this merge
-        }
-    };
-    uint32_t r = g.merges_done;
-    for (; r < K; ++r) {
-        if (g.stop || g.sp_abort || g.err) break;   // (uniform: LDS state, read after a barrier)
-        if (t == 0) TKT(0);
-        // ── selection: group maxima (LDS) ──
-        uint64_t best = 0;
-        for (uint32_t i = t; i < ngrp; i += TL_BT) best = gmax[i] > best ? gmax[i] : best;
-        for (int off = 32; off > 0; off >>= 1) {
-            const uint64_t o = __shfl_xor(best, off);
-            best = o > best ? o : best;
-        }
-        if (lane == 0) s_red[wid] = best;
-        if (t == 0) {
-            s_ntok = 0u;
-            s_nf = 0u;
-            s_rm = 0u;
-            s_nrs = 0u;
-        }
-        lds_clear(lt);
-        __syncthreads();
-        best = s_red[0];
-#pragma unroll
-        for (uint32_t w2 = 1; w2 < NWAVE; ++w2) best = s_red[w2] > best ? s_red[w2] : best;
-        const uint32_t mc = (uint32_t)(best >> 32), pid = ~(uint32_t)best, a = pid >> 16, b = pid & 0xFFFFu;
-        const uint32_t nw = g.next_id;
-        if (mc < 2u || nw > 0xFFFFu) {   // train.wgsl:345-348
-            if (t == 0) g.stop = 1u;
-            break;
-        }
-        if (t == 0) TKT(1);
-        if (!EXACT) {
-            if ((uint64_t)g.n < 2ull * mc + g.Bp) {   // cannot happen (k_body's invariant)
-                if (t == 0) {
-                    g.err |= ERR_SPARSE_WINDOW;
-                    g.stop = 1u;
-                }
-                break;
-            }
-            if ((uint64_t)z.n < 5ull * mc + 2u) {   // zone misfit: the host goes dense
-                if (t == 0) g.sp_abort = 1u;
-                break;
-            }
-        }
-        // ── body candidates: every bitmap word of rows a and b at once (thread 0 finds (a,b)'s slot first) ──
-        if (t == 0) s_idx = table_find(tb, pid);
-        for (uint32_t w = t; w < wused; w += TL_BT) {
-            uint32_t c = bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w];
-            if (c) {
-                uint32_t pos = atomicAdd(&s_ntok, (uint32_t)__popc(c));
-                for (; c; c &= c - 1, ++pos)
-                    if (pos < TL_CAND) u.c.cand[pos] = w * 32u + (uint32_t)(__ffs(c) - 1);
-            }
-        }
-        __syncthreads();
-        const uint32_t ntok = s_ntok;
-        if (t == 0) {
-            TKT(2);
-            TKTV(10, ntok);
-        }
-        if (ntok > TL_CAND) {   // nothing of merge r is committed yet
-            if (t == 0) s_exit = TL_EXIT_CAND;
-            break;
-        }
-        for (uint32_t j = t; j < ntok; j += TL_BT) {   // signature filter (+ extents)
-            const uint32_t k = u.c.cand[j];
-            const uint2 e = sec[k];
-            if (sig_has(sig + (uint64_t)k * SP_SIGW, pid)) {
-                const uint32_t q = atomicAdd(&s_nf, 1u);
-                if (q < TL_FILT) {
-                    u.c.fsec[q] = k;
-                    u.c.fext[q] = e;
-                }
-            }
-        }
-        if (t == 0) mybytes += 16ull * ntok;
-        __syncthreads();
-        const uint32_t nf = s_nf;
-        if (t == 0) {
-            TKT(3);
-            TKTV(11, nf);
-        }
-        if (nf > TL_FILT) {
-            if (t == 0) s_exit = TL_EXIT_CAND;
-            break;
-        }
-        // ── commit: the log (thread 0); count(a,b) -= mc and the re-max of its block and
-        //    group by the last wave, while the others merge sectors ──
-        const uint32_t idx = s_idx;
-        if (t == 0) {
-            if (idx == 0xFFFFFFFFu) g.err |= ERR_PAIR_MISSING;
-            log[r * 4 + 0] = a;
-            log[r * 4 + 1] = b;
-            log[r * 4 + 2] = nw;
-            log[r * 4 + 3] = mc;
-        }
-        if (wid == (int)NWAVE - 1 && idx != 0xFFFFFFFFu) {
-            constexpr int NV = (1 << BLK_LOG2) / 2 / 64;   // 16-byte loads per lane
-            const uint32_t blk = idx >> BLK_LOG2, gq = blk >> TL_GRP, gb = (gq << TL_GRP) + (uint32_t)lane;
-            const uint32_t cnt_new = tb.slots[idx].y - mc;
-            const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)blk << BLK_LOG2));
-            uint4 e[NV];
-#pragma unroll
-            for (int k = 0; k < NV; ++k) e[k] = sl[lane + k * 64];
-            const uint64_t gbm = gb < tb.nblk && gb != blk ? tb.bmax[gb] : 0ull;
-            if (lane == 0) tb.slots[idx].y = cnt_new;
-            uint64_t bst = 0;
-            uint32_t live = 0;
-#pragma unroll
-            for (int k = 0; k < NV; ++k) {   // (a,b)'s slot with its new count
-                const uint32_t s0 = ((uint32_t)(lane + k * 64) << 1) + ((blk << BLK_LOG2));
-                const uint32_t c1 = s0 == idx ? cnt_new : e[k].y, c2 = s0 + 1 == idx ? cnt_new : e[k].w;
-                const uint64_t k1 = e[k].x ? tl_key(c1, e[k].x) : 0ull, k2 = e[k].z ? tl_key(c2, e[k].z) : 0ull;
-                bst = k1 > bst ? k1 : bst;
-                bst = k2 > bst ? k2 : bst;
-                live += (k1 ? 1u : 0u) + (k2 ? 1u : 0u);
-            }
-            for (int off = 32; off > 0; off >>= 1) {
-                const uint64_t o = __shfl_xor(bst, off);
-                bst = o > bst ? o : bst;
-                live += __shfl_xor(live, off);
-            }
-            uint64_t gv = gbm > bst ? gbm : bst;
-            for (int off = 32; off > 0; off >>= 1) {
-                const uint64_t o = __shfl_xor(gv, off);
-                gv = o > gv ? o : gv;
-            }
-            if (lane == 0) {
-                tb.bmax[blk] = bst;
-                tb.blive[blk] = live;
-                gmax[gq] = gv;
-            }
-        }
-        // ── body sectors: one wave each, the next one's loads in flight ──
-        {
-            uint32_t removed = 0;
-            uint64_t moved = 0;
-            uint32_t nf5[5], nfm[4];
-            if ((uint32_t)wid < nf)
-                sector_first<S>(body + u.c.fext[wid].x, lmul ? lmul + u.c.fext[wid].x : nullptr, u.c.fext[wid].y, nf5, nfm);
-            for (uint32_t j = wid; j < nf; j += NWAVE) {
-                const uint32_t sct = u.c.fsec[j];
-                const uint2 e = u.c.fext[j];
-                uint32_t cf[5], cfm[4];
-#pragma unroll
-                for (int k = 0; k < 5; ++k) cf[k] = nf5[k];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) cfm[k] = nfm[k];
-                if (j + NWAVE < nf) {
-                    const uint2 en = u.c.fext[j + NWAVE];
-                    sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf5, nfm);
-                }
-                uint32_t out = 0;
-                const uint32_t rr = body_sector<S, TL_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, tb, st,
-                                                         sig + (uint64_t)sct * SP_SIGW, out, cf, cfm);
-                moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (rr ? out : 0u));
-                if (rr) {
-                    removed += rr;
-                    if (lane == 0) {
-                        sec[sct].y = out;
-                        atomicOr(&bits[(uint64_t)nw * W + (sct >> 5)], 1u << (sct & 31u));
-                    }
-                }
-            }
-            if (lane == 0) {
-                if (removed) atomicAdd(&s_rm, removed);
-                mybytes += moved;
-            }
-        }
-        __syncthreads();
-        if (t == 0) TKT(4);
-        // ── zone (the same delta table) ──
-        S* zc = (r & 1u) ? zb1 : zb0;
-        S* zo = (r & 1u) ? zb0 : zb1;
-        zone_one<S, EXACT, TL_BT, TL_LT, ZPT>(st, zst, g, z, zc, zo, u.z, lt, tb, a, b, nw, mc, bytes, r, zout);
-        __syncthreads();
-        if (t == 0) TKT(5);
-        // ── flush: plain read-modify-writes (the only writer), block maxima kept exact ──
-        {
-            uint32_t kk[TL_LT / TL_BT], vv[TL_LT / TL_BT];
-#pragma unroll
-            for (int j = 0; j < TL_LT / TL_BT; ++j) {
-                kk[j] = lt.key[t + j * TL_BT];
-                vv[j] = lt.val[t + j * TL_BT];
-            }
-#pragma unroll
-            for (int j = 0; j < TL_LT / TL_BT; ++j) {
-                const uint32_t p = kk[j], d = vv[j];
-                if (!p || !d) continue;
-                const uint32_t h = gbpe_fmix32(p) & tb.mask;
-                uint32_t idx = 0xFFFFFFFFu, old = 0;
-                for (uint32_t q = 0; q <= tb.mask; ++q) {
-                    const uint32_t i2 = (h + ((q * (q + 1)) >> 1)) & tb.mask;
-                    uint32_t k2 = tb.slots[i2].x;
-                    if (k2 == 0u) {
-                        k2 = atomicCAS(&tb.slots[i2].x, 0u, p);   // another new pair may race for the slot
-                        if (k2 == 0u) {
-                            atomicAdd(&s_used, 1u);
-                            idx = i2;
-                            old = 0u;
-                            break;
-                        }
-                    }
-                    if (k2 == p) {
-                        idx = i2;
-                        old = tb.slots[i2].y;
-                        break;
-                    }
-                }
-                if (idx == 0xFFFFFFFFu) {
-                    atomicOr(&g.err, ERR_TABLE_FULL);
-                    continue;
-                }
-                const uint32_t nv = old + d;
-                tb.slots[idx].y = nv;
-                const uint32_t blk = idx >> BLK_LOG2;
-                const uint64_t bm = __hip_atomic_load(&tb.bmax[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t ok = tl_key(old, p), nk = tl_key(nv, p);
-                if (nk > bm) {
-                    atomicMax(&tb.bmax[blk], nk);
-                    atomicMax(&gmax[blk >> TL_GRP], nk);
-                } else if (nk < ok && ok == bm) {
-                    remax_mark(blk);
-                }
-            }
-        }
-        __syncthreads();
-        if (t == 0) {
-            TKT(6);
-            TKTV(9, s_nrs);
-        }
-        // ── re-max queued blocks (one wave each), then their groups ──
-        if (s_nrs) {
-            const uint32_t nrs = s_nrs < TL_RS ? s_nrs : TL_RS;
-            constexpr int NV = (1 << BLK_LOG2) / 2 / 64;   // 16-byte loads per lane
-            for (uint32_t q = wid; q < nrs; q += NWAVE) {
-                const uint32_t blk = rs[q];
-                const uint4* sl = reinterpret_cast<const uint4*>(tb.slots + ((uint64_t)blk << BLK_LOG2));
-                uint4 e[NV];
-#pragma unroll
-                for (int k = 0; k < NV; ++k) e[k] = sl[lane + k * 64];
-                uint64_t bst = 0;
-                uint32_t live = 0;
-#pragma unroll
-                for (int k = 0; k < NV; ++k) {
-                    const uint64_t k1 = e[k].x ? tl_key(e[k].y, e[k].x) : 0ull, k2 = e[k].z ? tl_key(e[k].w, e[k].z) : 0ull;
-                    bst = k1 > bst ? k1 : bst;
-                    bst = k2 > bst ? k2 : bst;
-                    live += (k1 ? 1u : 0u) + (k2 ? 1u : 0u);
-                }
-                for (int off = 32; off > 0; off >>= 1) {
-                    const uint64_t o = __shfl_xor(bst, off);
-                    bst = o > bst ? o : bst;
-                    live += __shfl_xor(live, off);
-                }
-                if (lane == 0) {
-                    tb.bmax[blk] = bst;
-                    tb.blive[blk] = live;
-                    atomicOr(&gmark[blk >> (TL_GRP + 5)], 1u << ((blk >> TL_GRP) & 31u));
-                }
-            }
-            __syncthreads();
-            for (uint32_t gq = wid; gq < ngrp; gq += NWAVE) {
-                if (!((gmark[gq >> 5] >> (gq & 31u)) & 1u)) continue;   // wave-uniform
-                const uint32_t blk = (gq << TL_GRP) + (uint32_t)lane;
-                uint64_t v = blk < tb.nblk ? __hip_atomic_load(&tb.bmax[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-                for (int off = 32; off > 0; off >>= 1) {
-                    const uint64_t o = __shfl_xor(v, off);
-                    v = o > v ? o : v;
-                }
-                if (lane == 0) gmax[gq] = v;
-            }
-            __syncthreads();
-            if (t == 0) TKT(7);
-            for (uint32_t i = t; i < (TL_MAXG << TL_GRP) / 32; i += TL_BT) rsmark[i] = 0u;
-            if (t < (int)(TL_MAXG / 32)) gmark[t] = 0u;
-        }
-        // ── state (thread 0): the k_refresh (finish 2) bookkeeping ──
-        if (t == 0) {
-            const uint32_t m = zout[0], zkeep = zout[1];
-            const uint32_t n = g.n - mc, B = g.B - s_rm;
-            g.tail_total += m;
-            g.Bp = g.B;
-            g.B = B;
-            g.n = n;
-            g.new_n = n;
-            g.a = a;
-            g.b = b;
-            g.nw = nw;
-            g.mc = mc;
-            z.n = n - B;
-            g.zlast = z.n;
-            if (z.n != zkeep) {
-                g.err |= ERR_COUNT_MISMATCH;
-                g.stop = 1u;
-            }
-            g.next_id = nw + 1u;
-            g.epoch += 1u;
-            g.merges_done = r + 1u;
-            z.merges_done = r + 1u;
-            if (s_nrs > TL_RS) s_exit = TL_EXIT_REMAX;
-            if (lt.ovf) s_exit = TL_EXIT_LDS;
-        }
-        __syncthreads();
-        if (s_exit != TL_EXIT_NONE) {   // dirty blocks left for the host's k_refresh
-            ++r;
-            break;
-        }
-    }
-    __syncthreads();
-    if (t == 0) {
-        g.body_rm = 0u;
-        tstat[0] = g.merges_done;
-        tstat[1] = s_exit;
-    }
-    if (mybytes) atomicAdd(bytes, mybytes);
-    __syncthreads();
-    // the states back (`used` by an add: an overflowing LDS table inserted through table_add)
-    constexpr int WUSED = (int)(offsetof(DevState, used) / 4);
-    if (t < NW) {
-        if (t != WUSED) reinterpret_cast<uint32_t*>(st)[t] = s_g.w[t];
-    } else if (t < 2 * NW) {
-        reinterpret_cast<uint32_t*>(zst)[t - NW] = s_z.w[t - NW];
-    }
-    if (t == 0 && s_used) atomicAdd(&st->used, s_used);
-}
-#endif  // GBPE_TAIL_LOOP
 
 // dense → sparse: the last position at or before `lim` that no counted pair can
 // span — a word start, or a token-0 symbol on either side (one workgroup,

@@ -34,16 +34,6 @@ struct gbpe_trainer {
     uint32_t* hitmask = nullptr;
     uint32_t* tile_cnt = nullptr;
     uint32_t* grpsum = nullptr;
-    // sharded training
-    bool sharded = false;
-    uint32_t rank = 0, world = 1;
-    Table dt{};                    // per-merge count-delta table (local deltas before the exchange)
-    uint32_t* d_nlog = nullptr;    // local length before each merge of a step
-    uint32_t* h_nlog = nullptr;    // pinned
-    uint32_t step_k = 0;
-    uint32_t* rec_send = nullptr;  // exchange records of gbpe_shard_step_comm
-    uint32_t* rec_recv = nullptr;
-    uint64_t rec_words = 0;
     // stats
     uint64_t bytes_moved = 0;
     uint64_t max_live = 0;
@@ -82,18 +72,13 @@ struct gbpe_trainer {
     uint32_t* zdr_offs = nullptr;
     uint32_t* zdr_flag = nullptr;
     uint32_t zdr_ntile = 0;      // tile-workgroup dumps the buffers hold (+ ZDR_P churn workgroups)
-    bool zdr_on = true;          // GBPE_ZDR=0: flush every workgroup's deltas instead (round-2 path)
-    // hand-off selection (k_body's block 0 selects from bounds, no k_refresh per merge)
-    bool hs_on = false;          // GBPE_HS=1: on (measured slower so far)
-    unsigned long long* hs_rec = nullptr;   // hand-off granules
-    uint32_t* hs_stat = nullptr; // [0] verification retries, [1] selections (device)
-    uint32_t hs_seq = 0;         // hand-off tags handed out
+    bool zdr_on = true;          // two-stage zone delta reduction (false: every workgroup flushes, the round-2 path)
     uint32_t* zseg = nullptr;    // ZSegState: the zone segments' per-merge hand-off (k_refresh zeroes it)
-    uint32_t zseg_mode = 1;      // GBPE_ZONE_SEG: 1 = segments for zones beyond zone_one (up to 1M), 0 = off
+    uint32_t zseg_mode = 1;      // 1 = zone segments for zones beyond zone_one (up to 1M), 0 = off
     uint32_t table_grows = 0;    // crowded-table rebuilds (same size or larger)
     uint64_t* wg_bytes = nullptr;   // bytes moved per k_body workgroup (each its own counter)
     uint32_t delta_mt = 2048;       // dense k_delta: multi-tile workgroups from this many tiles (0 = never; GBPE_DELTA_MT)
-    uint32_t delta_tpw = 8;         // ... of 8, 16 or 32 tiles (GBPE_DELTA_TPW)
+    uint32_t delta_tpw = 8;         // ... of 8, 16 or 32 tiles
     uint64_t wg_cap = 0;
     double ms_sparse = 0, ms_dense = 0;   // GBPE_TRAIN_TIMING: merge passes (without selection / refresh) by mode
     double ms_body = 0;          // GBPE_TRAIN_TIMING: k_body alone
@@ -104,27 +89,20 @@ struct gbpe_trainer {
     uint32_t sp_div = 64;        // enter when last_mc * sp_div <= n
     uint32_t sp_cooldown = 0;    // steps to stay dense after an abort
     uint32_t* d_bhist = nullptr; // byte-pair histogram of the first count (65,536 u32)
-    uint32_t count_bytes_on = 1; // first count by the byte-pair histogram (GBPE_COUNT_BYTES=0: hashed k_count_full)
-    uint32_t lx_size_on = 1;     // word table sized from a sampled distinct count (GBPE_LEX_SIZE=0: from the word count)
+    uint32_t count_bytes_on = 1; // first count by the byte-pair histogram (0: hashed k_count_full)
+    uint32_t lx_size_on = 1;     // word table sized from a sampled distinct count (0: from the word count)
     uint32_t lx_resize = 0;      // builds whose sampled table was too small (rerun at full size)
     uint32_t lx_div = 16;        // with the lexicon: enter once next_mc * lx_div <= n, from the first step on (GBPE_LEXICON_DIV)
     uint32_t sub_zone = 1u << 20;   // sparse steps run in sub-steps of sub_k merges while the zone exceeds this
     uint32_t sub_k = 16;            // (the zone shrinks between them; GBPE_SUBSTEP_ZONE, GBPE_SUBSTEP)
-    bool zone16 = true;             // u16 zones of 8K-16K symbols: the 16-per-thread zone pass (GBPE_ZONE16=0: off)
-    // persistent tail loop (k_tail)
-    bool tail_on = true;         // GBPE_TAIL=0: never (a -DGBPE_TAIL_LOOP build only; measured no faster)
-    uint32_t tail_mc = 4096;     // run a step in k_tail once the last count is at most this (GBPE_TAIL_MC)
-    bool tail_skip = false;      // k_tail left the last step early: the next one runs k_body
-    uint32_t* d_tstat = nullptr;
-    uint64_t tail_merges = 0, tail_steps = 0, tail_exits = 0;
-    double ms_tail = 0;
-    uint32_t sp_zt = 5;          // zone target = sp_zt * last_mc + 64 (>= zone_f; GBPE_SPARSE_ZT; 4/5/6/7 measured
+    bool zone16 = true;             // u16 zones of 8K-16K symbols: the 16-per-thread zone pass 
+    uint32_t sp_zt = 5;          // zone target = sp_zt * last_mc + 64 (>= zone_f; GBPE_DEBUG zt; 4/5/6/7 measured
                                  // 0.895/0.893/0.918/0.918 s at 1 GiB with zone_f 3)
-    uint32_t shrink_pct = 200;   // shrink once the zone exceeds shrink_pct % of the target + 4096 (GBPE_SHRINK_PCT)
-    uint32_t zone_f = 3;         // single-GPU zone rule factor (sel_inline; GBPE_ZONE_F, >= 3)
-    uint32_t refresh_blocks = 0; // GBPE_REFRESH_BLOCKS: k_refresh grid (0 = 2 per CU)
-    uint32_t refresh_late_z = 16384; // GBPE_REFRESH_LATE_Z: ... for zones of at most this many symbols
-    uint32_t refresh_late = 64;  // GBPE_REFRESH_LATE: k_refresh grid of late steps (0 = unchanged)
+    uint32_t shrink_pct = 200;   // shrink once the zone exceeds shrink_pct % of the target + 4096 
+    uint32_t zone_f = 3;         // single-GPU zone rule factor (sel_inline, >= 3)
+    uint32_t refresh_blocks = 0; // k_refresh grid (0 = 2 per CU)
+    uint32_t refresh_late_z = 16384; // ... for zones of at most this many symbols
+    uint32_t refresh_late = 64;  // k_refresh grid of late steps (0 = unchanged)
     bool rehash_on = true;       // GBPE_REHASH: grow the table inside the sparse loop (0: exit, grow, recount)
     uint32_t body_cap = 256;     // GBPE_BODY_WG: most k_body workgroups (default one per CU)
     uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
@@ -305,7 +283,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
     hipLaunchKernelGGL(k_select, dim3(1), dim3(SEL_THREADS), 0, s, t->st, t->tb, t->d_log, t->grpsum,
-                           (uint32_t*)nullptr, (uint32_t*)nullptr, (DevState*)nullptr, exact ? 1u : 0u);
+                       (DevState*)nullptr, exact ? 1u : 0u);
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));
     // many tiles: TPW tiles per k_delta workgroup (fewer hot-pair flushes)
     const bool mt = t->delta_mt && g_delta >= t->delta_mt;
@@ -384,17 +362,8 @@ inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* 
 // 8K-16K symbols: half the per-thread zone work of the 32K form; 1 GiB en1g
 // 1.017 -> 0.963 s.  1024 threads x 8 for zones <= 8K instead of 256 x 32 was
 // slower: C2 0.66 vs 0.61 s)
-template <typename S, bool EXACT, bool HS = false, typename... A>
+template <typename S, bool EXACT, typename... A>
 void launch_body(int bt, uint32_t grid, hipStream_t s, A... args) {
-    if constexpr (HS) {   // hand-off selection: the zone_one forms only
-        if (bt == 1023 && sizeof(S) == 2)
-            hipLaunchKernelGGL((k_body<S, EXACT, 1024, 16, false, true>), dim3(grid), dim3(1024), 0, s, args...);
-        else if (bt >= 1023)
-            hipLaunchKernelGGL((k_body<S, EXACT, 1024, ZoneDim<S, 1024>::ZPT, false, true>), dim3(grid), dim3(1024), 0, s, args...);
-        else
-            hipLaunchKernelGGL((k_body<S, EXACT, 256, ZoneDim<S, 256>::ZPT, false, true>), dim3(grid), dim3(256), 0, s, args...);
-        return;
-    }
     if (bt == 2048)   // zone segments inside k_body (the ZSEG form, 1024 threads)
         hipLaunchKernelGGL((k_body<S, EXACT, 1024, 16, true>), dim3(grid), dim3(1024), 0, s, args...);
     else if (bt == 1023 && sizeof(S) == 2)
@@ -403,12 +372,6 @@ void launch_body(int bt, uint32_t grid, hipStream_t s, A... args) {
         hipLaunchKernelGGL((k_body<S, EXACT, 1024>), dim3(grid), dim3(1024), 0, s, args...);
     else
         hipLaunchKernelGGL((k_body<S, EXACT, 256>), dim3(grid), dim3(256), 0, s, args...);
-}
-
-// the hand-off selection serves single-GPU steps whose zone fits one workgroup
-inline bool hs_mode(const gbpe_trainer* t, const SpGrid& g) {
-    const uint32_t bt = g.bt >= 1023 ? 1024u : 256u;
-    return t->hs_on && t->hs_rec && t->part && !t->sharded && g.zone1 == 1u && g.refresh <= (uint32_t)HS_PPT * bt;
 }
 
 template <typename S>
@@ -424,36 +387,6 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const uint32_t z1 = g.zone1;   // k_body's own zone workgroups
     const int bt = inbody ? 2048 : g.bt;
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
-    if (hs_mode(t, g)) {   // block 0 selects and hands off; no k_refresh after the merge
-        HsView hv;
-        hv.rec = t->hs_rec;
-        hv.part = t->part;
-        hv.npart = g.refresh;
-        hv.per = (uint32_t)gbpe_div_up(t->tb.nblk, g.refresh);
-        hv.tag = ++t->hs_seq;
-        hv.clog = t->d_clog;
-        hv.stat = t->hs_stat;
-        Table tbh = t->tb;
-        tbh.bpart = t->part;
-        tbh.bper = hv.per;
-        if (exact)
-            launch_body<S, true, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, tbh,
-                                 g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
-                                 (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, tbh, sel_single(t),
-                                 sp_mul(t), (ZSegState*)t->zseg, hv);
-        else
-            launch_body<S, false, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, tbh,
-                                  g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
-                                  (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, tbh, sel_single(t),
-                                  sp_mul(t), (ZSegState*)t->zseg, hv);
-        if (timing) {
-            TR_HIP(t, hipEventRecord(ev[3], s));
-            TR_HIP(t, hipEventRecord(ev[2], s));
-            TR_HIP(t, hipEventRecord(ev[4], s));
-        }
-        GBPE_LAUNCH_CHECK(t->ctx);
-        return GBPE_OK;
-    }
     if (exact)
         launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
@@ -499,14 +432,6 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
         if (exact && mt)
             hipLaunchKernelGGL((k_delta_mt<S, true, 8>), dim3(g_mt), dim3(TPB), 0, s, t->zst, round, (const S*)zc, t->tb,
                                t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt);
-#ifdef GBPE_SPLIT_TAIL   // diagnostic build: the stale-tail blocks as a launch of their own (rocprof splits them)
-        else if (mt) {
-            hipLaunchKernelGGL((k_delta_mt<S, false, 8>), dim3(g_mt), dim3(TPB), 0, s, t->zst, round,
-                               (const S*)zc, t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt, 0u);
-            hipLaunchKernelGGL((k_delta_mt<S, false, 8>), dim3(g_mt + g.ztail), dim3(TPB), 0, s, t->zst, round,
-                               (const S*)zc, t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt, g_mt);
-        }
-#endif
         else if (mt)
             hipLaunchKernelGGL((k_delta_mt<S, false, 8>), dim3(g_mt + g.ztail), dim3(TPB), 0, s, t->zst, round,
                                (const S*)zc, t->tb, t->hitmask, t->tile_cnt, t->grpsum, g.zdelta, g_mt);
@@ -522,22 +447,10 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
             hipLaunchKernelGGL((k_compact<S, true, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
                                (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
                                t->tb, (const S*)t->wtmp, (const DevState*)t->st);
-#ifdef GBPE_SPLIT_TAIL
-        else {
-            const uint32_t zt_ = g.zdelta;   // zone tiles (the window blocks follow them)
-            hipLaunchKernelGGL((k_compact<S, false, true>), dim3(zt_), dim3(CTPB), 0, s, t->zst, round, zc, zo,
-                               (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
-                               t->tb, (const S*)t->wtmp, (const DevState*)t->st, 1u);
-            hipLaunchKernelGGL((k_compact<S, false, true>), dim3(g.zcompact - zt_), dim3(CTPB), 0, s, t->zst, round, zc,
-                               zo, (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
-                               t->tb, (const S*)t->wtmp, (const DevState*)t->st, 2u);
-        }
-#else
         else
             hipLaunchKernelGGL((k_compact<S, false, true>), dim3(g.zcompact), dim3(CTPB), 0, s, t->zst, round, zc, zo,
                                (const uint32_t*)t->hitmask, (const uint32_t*)t->tile_cnt, (const uint32_t*)t->grpsum,
                                t->tb, (const S*)t->wtmp, (const DevState*)t->st);
-#endif
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,
@@ -1145,15 +1058,9 @@ int sp_init_states(gbpe_trainer* t, uint64_t cap, uint32_t Zs, uint32_t z, uint3
     TR_HIP(t, hipMemcpyAsync(&t->st->mc_prev, &t->st->mc, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     // per-k_refresh-workgroup maxima the sparse merges select from (sel_inline)
     if (!t->part) TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
-    if (!t->zseg && !t->sharded) {
+    if (!t->zseg) {
         TR_HIP(t, hipMalloc(&t->zseg, sizeof(ZSegState)));
         TR_HIP(t, hipMemsetAsync(t->zseg, 0, sizeof(ZSegState), t->ctx->stream));
-    }
-    if (!t->hs_rec && !t->sharded) {   // hand-off granules (tag 0 is never handed out) + counters
-        TR_HIP(t, hipMalloc(&t->hs_rec, 64));
-        TR_HIP(t, hipMemsetAsync(t->hs_rec, 0, 64, t->ctx->stream));
-        TR_HIP(t, hipMalloc(&t->hs_stat, 16));
-        TR_HIP(t, hipMemsetAsync(t->hs_stat, 0, 16, t->ctx->stream));
     }
     if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
     return GBPE_OK;
@@ -1175,7 +1082,7 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
     const S* cur = (const S*)t->buf[t->cur];
     const S* stale = (const S*)t->buf[t->cur ^ 1];
     if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
-    uint32_t Zs = n;   // sharded ranks before the last: all body, no zone
+    uint32_t Zs = n;
     if (with_zone) {
         if (zt + 2 >= n) return GBPE_OK;
         hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, cur, (uint32_t)(n - zt), t->d_u32);
@@ -1210,7 +1117,7 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
         t->lex = true;
         rc = lx_commit<S>(t, lp, cur, true);
         if (rc == GBPE_OK && !lp.ok) rc = gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "word lexicon capacity");
-        if (rc == GBPE_OK && getenv("GBPE_LEX_CHECK")) rc = lx_check<S>(t, cur, Zs, lp);
+        if (rc == GBPE_OK && gbpe_debug_knob("lex_check", 0)) rc = lx_check<S>(t, cur, Zs, lp);
     } else {
         rc = sp_add_sectors<S>(t, 0u, Zs);
     }
@@ -1227,7 +1134,7 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
         if (sl > t->zcap) sl = t->zcap;
         TR_HIP(t, hipMemcpyAsync(t->zbuf[1], stale + Zs, sl * t->bps, hipMemcpyDeviceToDevice, s));
     }
-    rc = sp_init_states(t, cap, Zs, z, t->sharded ? (uint32_t)zt : z);
+    rc = sp_init_states(t, cap, Zs, z, z);
     if (rc != GBPE_OK) return rc;
     hipLaunchKernelGGL(k_refresh<S>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
                        (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part);
@@ -1361,33 +1268,13 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     const uint64_t max_id = (uint64_t)next_id + t->needed;    // exclusive
     t->u16 = max_id <= 0x8000ull;
     t->max_id = (uint32_t)(max_id < 0x10000ull ? max_id : 0x10000ull);
-    if (const char* e = getenv("GBPE_SPARSE_DIV")) t->sp_div = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_REFRESH_BLOCKS")) t->refresh_blocks = (uint32_t)atoi(e);
-    if (const char* e = getenv("GBPE_REFRESH_LATE")) t->refresh_late = (uint32_t)atoi(e);
-    if (const char* e = getenv("GBPE_REFRESH_LATE_Z")) t->refresh_late_z = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_REHASH")) t->rehash_on = atoi(e) != 0;
     t->body_cap = (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
-    if (const char* e = getenv("GBPE_BODY_WG")) t->body_cap = std::max<uint32_t>(1, (uint32_t)atoi(e));
-    if (const char* e = getenv("GBPE_SPARSE_ZT")) t->sp_zt = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_LEXICON")) t->lex_on = atoi(e) != 0;
-    if (const char* e = getenv("GBPE_TAIL")) t->tail_on = atoi(e) != 0;
-    if (const char* e = getenv("GBPE_ZONE16")) t->zone16 = atoi(e) != 0;
-    if (const char* e = getenv("GBPE_TAIL_MC")) t->tail_mc = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_COUNT_BYTES")) t->count_bytes_on = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_LEX_SIZE")) t->lx_size_on = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_LEXICON_DIV")) t->lx_div = std::max<uint32_t>(8, (uint32_t)strtoul(e, nullptr, 10));
-    if (const char* e = getenv("GBPE_SUBSTEP_ZONE")) t->sub_zone = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_SUBSTEP")) t->sub_k = std::max<uint32_t>(2, (uint32_t)strtoul(e, nullptr, 10)) & ~1u;
-    if (const char* e = getenv("GBPE_DELTA_MT")) t->delta_mt = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_DELTA_TPW")) {
-        const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
-        t->delta_tpw = v >= 32 ? 32 : v >= 16 ? 16 : 8;
-    }
-    if (const char* e = getenv("GBPE_SHRINK_PCT")) t->shrink_pct = std::max<uint32_t>(110, (uint32_t)strtoul(e, nullptr, 10));
-    if (const char* e = getenv("GBPE_ZONE_SEG")) t->zseg_mode = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("GBPE_ZONE_F")) t->zone_f = std::max<uint32_t>(3, (uint32_t)strtoul(e, nullptr, 10));
-    if (const char* e = getenv("GBPE_ZDR")) t->zdr_on = atoi(e) != 0;
-    if (const char* e = getenv("GBPE_HS")) t->hs_on = atoi(e) != 0;
+    // test overrides (GBPE_DEBUG): the lexicon off / its build check, the
+    // in-loop table growth off, the multi-tile k_delta threshold, the zone target
+    t->lex_on = gbpe_debug_knob("lexicon", 1) != 0;
+    t->rehash_on = gbpe_debug_knob("rehash", 1) != 0;
+    t->delta_mt = (uint32_t)gbpe_debug_knob("delta_mt", t->delta_mt);
+    t->sp_zt = (uint32_t)gbpe_debug_knob("zt", t->sp_zt);
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
         t->trace = fopen(e, "w");

@@ -114,24 +114,6 @@ _SIGS = [
     ("gbpe_pretokenize_gpt4_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     ("gbpe_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("gbpe_ctx_get_stream", C.c_void_p, [C.c_void_p]),
-    ("gbpe_shard_create", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int, C.POINTER(TrainOpts),
-                                    C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_void_p)]),
-    ("gbpe_shard_local_len", C.c_int, [C.c_void_p, u64p]),
-    ("gbpe_shard_set_layout", C.c_int, [C.c_void_p, u64p, C.c_uint32]),
-    ("gbpe_shard_export_counts", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, u64p]),
-    ("gbpe_shard_import_counts", C.c_int, [C.c_void_p, C.c_void_p, u64p, C.c_uint32, C.c_uint64]),
-    ("gbpe_shard_record_words", C.c_int, [C.c_uint32, C.c_uint32]),
-    ("gbpe_shard_step_begin", C.c_int, [C.c_void_p, C.c_uint32]),
-    ("gbpe_shard_phase1", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]),
-    ("gbpe_shard_phase2", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]),
-    ("gbpe_shard_step_end", C.c_int, [C.c_void_p, u32p, u32p, u32p, u32p, u32p, u32p]),
-    ("gbpe_comm_unique_id", C.c_int, [C.c_void_p, C.c_uint32]),
-    ("gbpe_comm_create", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
-                                   C.POINTER(C.c_void_p)]),
-    ("gbpe_comm_destroy", None, [C.c_void_p]),
-    ("gbpe_shard_step_comm", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, u32p, u32p, u32p,
-                                       u32p, u32p, u32p]),
-    ("gbpe_shard_global_len", C.c_int, [C.c_void_p, u64p]),
     ("gbpe_trainer_export_state", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, u64p, C.c_void_p, C.c_uint64, u64p,
                                             C.c_int]),
     ("gbpe_trainer_create_from_state", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int,

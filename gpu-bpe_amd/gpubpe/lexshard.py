@@ -112,6 +112,15 @@ class _Xfer:
         return buf[: int(sizes[self.rank])]
 
 
+def _debug_knob(key: str, default: int) -> int:
+    """GBPE_DEBUG="key=value,..." (the library's test overrides, csrc/common.h)."""
+    for kv in os.environ.get("GBPE_DEBUG", "").split(","):
+        k, _, v = kv.partition("=")
+        if k == key and v:
+            return int(v)
+    return default
+
+
 def _ptr(x):
     """(pointer, on_device) of a torch tensor or numpy array."""
     if hasattr(x, "data_ptr"):
@@ -234,7 +243,7 @@ class LexShardTrainer:
         self.rank, self.world = self.x.rank, self.x.world
         self.root = self.world - 1
         self.staged = staged
-        self.sp_zt = max(3, sp_zt if sp_zt is not None else int(os.environ.get("GBPE_SPARSE_ZT", "5")))
+        self.sp_zt = max(3, sp_zt if sp_zt is not None else _debug_knob("zt", 5))
         self.timing = {}
         self.shapes = None
         self.map = None

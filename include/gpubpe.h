@@ -191,64 +191,16 @@ int gbpe_trainer_symbols(gbpe_trainer* t, uint32_t* out, uint64_t cap, uint64_t*
 int gbpe_trainer_pair_counts(gbpe_trainer* t, uint32_t* pids, uint32_t* counts, uint64_t cap, uint64_t* n);
 void gbpe_trainer_destroy(gbpe_trainer* t);
 
-/* ── sharded training: one rank per GPU ──────────────────────
- * The reference trains on one WebGPU device (training-pipeline.js:178-222);
- * these entry points run the same merge loop over a corpus cut at word starts
- * into one shard per rank, bit-exact to the single-stream run.  Each rank keeps
- * a replica of the global pair-count table; every merge exchanges one
- * fixed-size record per rank (gbpe_shard_record_words(C, Cw) u32 words) with
- * an all-gather the CALLER performs between phase 1 and phase 2 (RCCL via
- * torch.distributed on the stream set with gbpe_ctx_set_stream; gloo in tests).
- * Protocol and host loop: gpu-bpe_amd/gpubpe/sharded.py.
- *   create → local_len → (all-gather lengths) set_layout → export_counts →
- *   (all-gather lists) import_counts → per step: step_begin, per merge k
- *   {phase1(k, send) ; all_gather(recv, send) ; phase2(k, recv)}, step_end.
- * A merge whose record needs more than (C, Cw) stalls on every rank; step_end
- * reports it with the capacities needed, and the next step redoes it.  A step
- * without a stall reports the largest list / window piece it exchanged, so
- * the host can shrink (C, Cw) as merges get rarer. */
+/* The library's HIP stream (the lexicon hand-over runs RCCL transfers on it). */
 int gbpe_ctx_set_stream(gbpe_ctx* ctx, void* hip_stream);   /* taken literally (NULL = the null stream) */
 void* gbpe_ctx_get_stream(gbpe_ctx* ctx);                    /* current stream (save / restore) */
-int gbpe_shard_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
-                      int input_on_device, const gbpe_train_opts* opts, uint32_t rank, uint32_t world,
-                      uint64_t cap_extra /* symbols of room for appended stale windows */, gbpe_trainer** out);
-int gbpe_shard_local_len(gbpe_trainer* t, uint64_t* n);
-int gbpe_shard_set_layout(gbpe_trainer* t, const uint64_t* lens, uint32_t world);
-/* device list of {pid, count} u32 pairs of the local stream; d_out NULL = count only */
-int gbpe_shard_export_counts(gbpe_trainer* t, void* d_out, uint64_t cap, uint64_t* n_pairs);
-/* d_lists: world lists of {pid, count}, list q at d_lists + q*stride pairs, counts[q] entries */
-int gbpe_shard_import_counts(gbpe_trainer* t, const void* d_lists, const uint64_t* counts, uint32_t world,
-                             uint64_t stride);
-int gbpe_shard_record_words(uint32_t cap_list, uint32_t cap_win);
-int gbpe_shard_step_begin(gbpe_trainer* t, uint32_t max_merges);
-int gbpe_shard_phase1(gbpe_trainer* t, uint32_t round, void* d_send, uint32_t cap_list, uint32_t cap_win);
-int gbpe_shard_phase2(gbpe_trainer* t, uint32_t round, const void* d_recv, uint32_t cap_list, uint32_t cap_win);
-int gbpe_shard_step_end(gbpe_trainer* t, uint32_t* merges_out, uint32_t* n_done, uint32_t* early_stop,
-                        uint32_t* stalled, uint32_t* need_list, uint32_t* need_win);
-
-/* Native exchange: the library runs a whole step (phase 1, ncclAllGather,
- * phase 2 per merge) on its stream over an RCCL communicator (RCCL is opened
- * at run time).  Rank 0 makes the id, the caller broadcasts it (any channel),
- * every rank creates its communicator on its own device. */
-typedef struct gbpe_comm gbpe_comm;
-int  gbpe_comm_unique_id(uint8_t* out, uint32_t len /* >= 128 */);
-int  gbpe_comm_create(gbpe_ctx* ctx, const uint8_t* id, uint32_t len, uint32_t rank, uint32_t world, gbpe_comm** out);
-void gbpe_comm_destroy(gbpe_comm* comm);
-int  gbpe_shard_step_comm(gbpe_trainer* t, gbpe_comm* comm, uint32_t max_merges, uint32_t cap_list, uint32_t cap_win,
-                          uint32_t* merges_out, uint32_t* n_done, uint32_t* early_stop, uint32_t* stalled,
-                          uint32_t* need_list, uint32_t* need_win);
-/* Global stream length after the last step (every rank agrees). */
-int  gbpe_shard_global_len(gbpe_trainer* t, uint64_t* gn);
-
-/* ── consolidation: a run continues on another trainer ──────────────────────
- * Late merges touch a few hundred symbols each; a per-merge exchange then costs
- * more than the merge, so the sharded run hands its state to ONE device.  The
+/* ── checkpoint / resume: a run continues on another trainer ─────────────────
+ * (The reference keeps no mid-run checkpoint)  The
  * state of a trainer is its current stream and its previous stream (the
  * ping-pong buffer the compaction quirk reads stale symbols from,
  * train.wgsl:605-607 + 698/727), both in the reference u32 layout (bit16 =
- * word start).  For a sharded run the global streams are the rank pieces
- * concatenated in rank order.  cur/prev NULL = lengths only; on_device != 0:
- * cur/prev are device pointers (the hand-over then never leaves HBM).
+ * word start).  cur/prev NULL = lengths only; on_device != 0: cur/prev are
+ * device pointers.
  * `prev` is defined only where the next merge's stale window can read it: after
  * the sector-sparse loop, positions below the body length at its last merge hold
  * the body as it was at entry, not the previous stream (the window always lies in

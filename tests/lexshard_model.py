@@ -28,7 +28,6 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
 
 import bpe_oracle as O  # noqa: E402
-from shard_model import OracleSingle  # noqa: E402
 
 WS, TM = O.WORD_START_BIT, O.TOKEN_MASK
 LIT = 0x80000000
@@ -174,3 +173,36 @@ class ModelLexBackend:
 
     def close(self):
         pass
+
+
+class OracleSingle:
+    """The consolidated run on the CPU: the oracle's merge loop (bpe_oracle.train's
+    body) continued from a gathered (current, previous) global state."""
+
+    def __init__(self, cur, prev, next_id: int, exact: bool = False):
+        n, npv = int(cur.shape[0]), int(prev.shape[0])
+        cap = max(n, npv) + 16
+        self.cur = np.zeros(cap, np.uint32)
+        self.oth = np.zeros(cap, np.uint32)
+        self.cur[:n] = cur
+        self.oth[:npv] = prev
+        self.n = n
+        self.nxt = next_id
+        self.compaction = "exact" if exact else "reference"
+
+    def step(self, k):
+        out = []
+        for _ in range(k):
+            uniq, counts = O.count_pairs(self.cur[: self.n])
+            mc, pid = O.select_best(uniq, counts)
+            if mc < 2 or self.nxt > TM:
+                return out, True
+            a, b = pid >> 16, pid & TM
+            self.n, _ = O.merge_step(self.cur, self.oth, self.n, a, b, self.nxt, self.compaction)
+            out.append([a, b, self.nxt, mc])
+            self.nxt += 1
+            self.cur, self.oth = self.oth, self.cur
+        return out, False
+
+    def symbols(self):
+        return self.cur[: self.n].copy()

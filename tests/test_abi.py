@@ -135,29 +135,3 @@ def test_model_json_round_trip():
     assert m["vocabStrings"][256] == "hi" and m["vocabStrings"][257] == "�"   # non-fatal UTF-8 decode
     with pytest.raises(ValueError, match="missing vocab or merges"):
         load_model_json({"vocab": [[1]]})
-
-
-def test_shard_record_layout_matches_host_loop(lib):
-    # the exchange record the native step loop (gbpe_shard_step_comm) all-gathers
-    # is the one the Python host loop and the numpy rank model read: same header
-    # word positions (csrc/train_dev.h enum vs gpubpe/sharded.py) and size
-    import re
-    from gpubpe import sharded
-    src = open(os.path.join(ROOT, "gpu-bpe_amd", "csrc", "train_dev.h")).read()
-    body = re.search(r"enum : uint32_t \{\s*(H_ACTIVE = 0[^}]*)\}", src).group(1)
-    body = re.sub(r"//[^\n]*", "", body)
-    idx, names = 0, {}
-    for item in [x.strip() for x in body.split(",") if x.strip()]:
-        if "=" in item:
-            k, v = [y.strip() for y in item.split("=")]
-            idx = int(v)
-        else:
-            k = item
-        names[k] = idx
-        idx += 1
-    for k in ("H_ACTIVE", "H_L", "H_KEPT", "H_M", "H_W", "H_LASTSYM", "H_HASLAST", "H_SURV", "H_LN", "H_MC", "H_A",
-              "H_B", "H_ID", "H_DFULL"):
-        assert names[k] == getattr(sharded, k), k
-    assert names["HDR"] == sharded.HDR
-    for cl, cw in ((8, 8), (1 << 14, 1 << 12), (4096, 1024)):
-        assert lib.gbpe_shard_record_words(cl, cw) == sharded.record_words(cl, cw)

@@ -27,7 +27,7 @@ def _train(eng, d, n, merges, env):
     lib = _lib.load()
     ctx = eng.device
     old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)   # read at trainer creation (GBPE_LEX_CHECK at every build)
+    os.environ.update(env)   # read at trainer creation (GBPE_DEBUG lex_check at every build)
     tr = C.c_void_p()
     try:
         opts = _lib.TrainOpts(target_vocab_size=256 + merges, vocab_size=256, next_token_id=256, batch_size=128,
@@ -68,8 +68,8 @@ def test_word_table_estimate_short(eng):
     _lib.check(lib.gbpe_device_alloc(ctx, n + 64, C.byref(d)), ctx, "alloc")
     try:
         _lib.check(lib.gbpe_memcpy_h2d(ctx, d, data, n), ctx, "h2d")
-        lex, st = _train(eng, d, n, 300, {"GBPE_LEXICON": "1", "GBPE_LEX_CHECK": "1"})
-        ref, _ = _train(eng, d, n, 300, {"GBPE_LEXICON": "0"})
+        lex, st = _train(eng, d, n, 300, {"GBPE_DEBUG": "lexicon=1,lex_check=1"})
+        ref, _ = _train(eng, d, n, 300, {"GBPE_DEBUG": "lexicon=0"})
     finally:
         lib.gbpe_device_free(ctx, d)
     assert st.lexicon_builds >= 1 and st.lexicon_fallbacks == 0

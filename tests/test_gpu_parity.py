@@ -112,10 +112,10 @@ def test_train_matches_oracle(eng, kind, size, target, exact):
 
 @pytest.mark.parametrize("exact", [False, True])
 def test_train_multitile_delta(eng, monkeypatch, exact):
-    # GBPE_DELTA_MT=1: every dense merge runs k_delta_mt (8 tiles per workgroup,
+    # GBPE_DEBUG=delta_mt=1: every dense merge runs k_delta_mt (8 tiles per workgroup,
     # the last workgroup partial), which the library otherwise keeps for >= 2048 tiles
     from gpubpe import synth
-    monkeypatch.setenv("GBPE_DELTA_MT", "1")
+    monkeypatch.setenv("GBPE_DEBUG", "delta_mt=1")
     data = synth.english(300000, seed=41)
     ref = O.train(data, 1500, compaction="exact" if exact else "reference")
     m, s, pairs, st = _train_native(eng, data, 1500, exact=exact, sparse="dense")
@@ -191,7 +191,7 @@ def test_table_grows_inside_sparse_loop(eng, monkeypatch):
     ref = O.train(data, 1200)
     exits = {}
     for rehash in ("1", "0"):
-        monkeypatch.setenv("GBPE_REHASH", rehash)
+        monkeypatch.setenv("GBPE_DEBUG", f"rehash={rehash}")
         m, s, pairs, st = _train_native(eng, data, 1200, table_log2=13, batch=16, sparse="early")
         assert m == ref["merges"] and np.array_equal(s, ref["symbols"])
         _assert_counts_match_stream(pairs, s)
@@ -299,10 +299,10 @@ def test_encode_host_pipeline_slices(eng, cs, monkeypatch):
     text = synth.multilingual(150000, seed=33)
     tok = TrieTokenizer.from_vocab(eng, vocab, chunk_size=cs)
     want = _oracle_encode(vocab, text, tok.chunk_size)
-    monkeypatch.setenv("GBPE_ENCODE_SLICE", "4096")
+    monkeypatch.setenv("GBPE_DEBUG", "encode_slice=4096")
     got = tok.encode_bytes(text)
     assert np.array_equal(got, want)
-    monkeypatch.delenv("GBPE_ENCODE_SLICE")
+    monkeypatch.delenv("GBPE_DEBUG")
     assert np.array_equal(tok.encode_bytes(text), want)
     tok.destroy()
 

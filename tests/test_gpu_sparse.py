@@ -60,7 +60,7 @@ def test_sparse_zone_aborts_and_reentry(eng, monkeypatch):
     # the smallest zone the invariant allows (5 mc): merges outgrow it, the loop
     # returns to dense mid-step and re-enters later; results must not change
     from gpubpe import synth
-    monkeypatch.setenv("GBPE_SPARSE_ZT", "5")
+    monkeypatch.setenv("GBPE_DEBUG", "zt=5")
     data = synth.multilingual(120000, seed=13)
     ref = O.train(data, 1500)
     m, s, pairs, st = _train_native(eng, data, 1500, batch=16, sparse="early", table_log2=15)

@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(HERE), "gpu-bpe_amd"))
 
 import bpe_oracle as O  # noqa: E402
 from gpubpe import synth  # noqa: E402
-from test_sharded import _free_port  # noqa: E402
+from dist_util import free_port as _free_port  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
