@@ -382,18 +382,25 @@ __global__ __launch_bounds__(TPB) void k_lx_wordpos(const S* __restrict__ store,
     }
 }
 
+// bad (optional): set when an occurrence names no entry (o >= nu); it then counts 0 symbols
 __global__ void k_lx_olen(const uint32_t* __restrict__ occ, uint64_t nocc, const uint32_t* __restrict__ clen,
-                          uint32_t* __restrict__ olen) {
+                          uint32_t* __restrict__ olen, uint32_t nu = 0xFFFFFFFFu, uint32_t* __restrict__ bad = nullptr) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nocc) return;
     const uint32_t o = occ[j];
+    if (!(o & LX_LIT) && o >= nu) {
+        if (bad) *bad = 1u;
+        olen[j] = 0u;
+        return;
+    }
     olen[j] = (o & LX_LIT) ? 1u : clen[o];
 }
 
 template <typename S>
 __global__ void k_lx_expand(const uint32_t* __restrict__ occ, uint64_t nocc, const uint32_t* __restrict__ coff,
                             const uint32_t* __restrict__ clen, const S* __restrict__ store,
-                            const uint32_t* __restrict__ opre, const uint64_t* __restrict__ oblk, S* __restrict__ dst) {
+                            const uint32_t* __restrict__ opre, const uint64_t* __restrict__ oblk, S* __restrict__ dst,
+                            uint32_t nu) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nocc) return;
     const uint64_t off = (uint64_t)opre[j] + oblk[j / SCAN_BLK];
@@ -402,6 +409,7 @@ __global__ void k_lx_expand(const uint32_t* __restrict__ occ, uint64_t nocc, con
         dst[off] = (S)(o & ((Sym<S>::WS << 1) - 1u));
         return;
     }
+    if (o >= nu) return;   // (k_lx_olen reported it; the host stops before this kernel)
     const uint32_t c = coff[o], L = clen[o];
     for (uint32_t i = 0; i < L; ++i) dst[off + i] = store[c + i];
 }

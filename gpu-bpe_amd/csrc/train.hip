@@ -370,7 +370,9 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         }
         sg.refresh = g_refresh;
     }
+    const bool late = sparse && late_eligible(t);
     auto launch_all = [&]() -> int {
+        if (late) return t->u16 ? launch_late<uint16_t>(t, s, g_refresh, timing) : launch_late<uint32_t>(t, s, g_refresh, timing);
         for (uint32_t r = 0; r < k; ++r) {
             hipEvent_t* ev = timing ? &t->evs[5 * r] : nullptr;
             int rc;
@@ -405,7 +407,18 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
                               (err & ERR_SPARSE_WINDOW) ? "sparse stale window outside the zone " : "",
                               (err & ERR_SPIN) ? "zone segment hand-off timed out" : "");
     }
-    if (timing) {
+    if (late) {
+        ++t->late_launches;
+        t->late_merges += done;
+        if (done < k && !hs->stop && !hs->sp_abort) ++t->late_exits;
+        if (timing) {
+            float ms = 0;
+            hipEventElapsedTime(&ms, t->late_ev[0], t->late_ev[1]);
+            t->ms_late += ms;
+            t->ms_sparse += ms;
+            t->timed_merges += done;
+        }
+    } else if (timing) {
         for (uint32_t r = 0; r < done; ++r) {
             float a = 0, b = 0, c = 0, d1 = 0, d2 = 0;
             hipEvent_t* ev = &t->evs[5 * r];
@@ -423,6 +436,12 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
             if (sparse) t->ms_body += d1;
         }
         t->timed_merges += done;
+    }
+    if (late && done == 0 && !hs->stop && !hs->sp_abort) {   // the hot set could not select: k_body runs this step
+        t->late_skip = true;
+        int rc = trainer_step_once(t, max_merges, merges_out, n_done, early_stop);
+        t->late_skip = false;
+        return rc;
     }
     // algorithmic stream bytes: s * (2 N_i + N_{i+1})
     uint64_t N = t->n;
@@ -523,6 +542,17 @@ extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
     o->lexicon_words = t->lx_words;
     o->lexicon_entries = t->lx_nuid;
     o->lexicon_symbols = t->lx_len;
+    o->late_merges = t->late_merges;
+    o->late_launches = t->late_launches;
+    o->late_exits = t->late_exits;
+    o->ms_late = t->ms_late;
+    if (t->late_u32) {
+        uint32_t h[8] = {};
+        if (hipMemcpy(h, t->late_u32, 32, hipMemcpyDeviceToHost) == hipSuccess) {
+            o->late_bytes = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
+            o->late_bound_exits = h[1];
+        }
+    }
     if (t->wg_bytes && t->wg_cap) {   // the per-workgroup counters of k_body (and its zone workgroup)
         std::vector<uint64_t> h(t->wg_cap);
         if (hipMemcpy(h.data(), t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess)
@@ -674,6 +704,11 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     hipFree(t->d_bhist);
     hipFree(t->zseg);
     hipFree(t->zdr_out);
+    hipFree(t->late_hot);
+    hipFree(t->late_log);
+    hipFree(t->late_u32);
+    for (auto& e : t->late_ev)
+        if (e) hipEventDestroy(e);
     hipFree(t->zdr_offs);
     hipFree(t->zdr_flag);
     hipFree(t->wg_bytes);

@@ -1626,7 +1626,8 @@ __global__ void k_import_symbols(const uint32_t* __restrict__ in, S* __restrict_
 constexpr uint32_t SP_WPW_MIN = 16;  // fewest bitmap words per k_body workgroup (sizes its byte counters)
 constexpr uint32_t SP_CH = 256;      // symbols per wave pass over a sector (4 per lane)
 constexpr uint32_t SP_INV = 0xFFFFFFFFu;
-constexpr uint32_t SP_SHRINKS = 64;  // zone shrinks per sparse entry (sector capacity)
+constexpr uint32_t SP_SHRINKS = 64;  // zone shrinks per sparse entry the first sector capacity allows for (sp_reserve grows it)
+constexpr uint32_t SP_SHRINKS_MAX = 1024;   // zone shrinks per sparse entry
 
 // Per-sector pair signature: a 2048-bit Bloom filter (3 hash bits) of every pair
 // the sector has held since the filters were last rebuilt.  The token bitmap

@@ -88,16 +88,13 @@ int ls_build(gbpe_lexshard* ls, uint64_t zone_target) {
     const S* cur = (const S*)t->buf[t->cur];
     const uint64_t n = t->n;
     uint32_t Zs = (uint32_t)n;
-    if (zone_target) {   // the last piece keeps its tail as the dense zone
-        if (zone_target + 2 >= n)
-            return gbpe_set_error(ls->ctx, GBPE_E_INVALID,
-                                  "lexshard: zone of %llu symbols does not fit the last piece (%llu symbols)",
-                                  (unsigned long long)zone_target, (unsigned long long)n);
+    if (zone_target >= n) {   // the whole piece lies inside the zone (a zone spanning several pieces)
+        Zs = 0;
+    } else if (zone_target) {   // the piece's tail from the last word start at or before n - zone_target
         hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, cur, (uint32_t)(n - zone_target), t->d_u32);
         GBPE_LAUNCH_CHECK(ls->ctx);
         TR_HIP(t, hipMemcpyAsync(&Zs, t->d_u32, 4, hipMemcpyDeviceToHost, s));
         TR_HIP(t, hipStreamSynchronize(s));
-        if (Zs == 0) return gbpe_set_error(ls->ctx, GBPE_E_INVALID, "lexshard: no word start before the zone");
     }
     LxPlan lp;
     int rc = lx_analyze<S>(t, cur, Zs, false, lp);
@@ -357,7 +354,7 @@ extern "C" int gbpe_trainer_create_from_lexicon(gbpe_ctx* ctx, const void* store
     if (zone_len >= (1ull << 31))   // the device keeps n - Bp, a zone-sized length, in 32 bits
         return gbpe_set_error(ctx, GBPE_E_INVALID, "lexicon hand-over: zone of %llu symbols (at most 2^31)",
                               (unsigned long long)zone_len);
-    if (zone_len == 0) return gbpe_set_error(ctx, GBPE_E_INVALID, "lexicon hand-over: the last piece keeps a zone");
+    if (zone_len == 0) return gbpe_set_error(ctx, GBPE_E_INVALID, "lexicon hand-over: the stream's tail must be a zone");
     auto* t = new (std::nothrow) gbpe_trainer();
     if (!t) return gbpe_set_error(ctx, GBPE_E_OOM, "host allocation failed");
     trainer_config(t, ctx, opts);
@@ -450,7 +447,7 @@ int trainer_expand(gbpe_trainer* t, const uint32_t* d_prefix, uint64_t n_prefix,
         hipFree(occ);
         return gbpe_set_error(t->ctx, GBPE_E_OOM, "expand: hipMalloc(%llu symbols) failed", (unsigned long long)t->n);
     }
-    int rc = lx_expand<S>(t, tmp, &tot, occ, no);
+    int rc = lx_expand<S>(t, tmp, t->n - z, &tot, occ, no);   // (checks the total before writing)
     TR_HIP(t, hipStreamSynchronize(s));
     if (rc == GBPE_OK && tot + z != t->n)
         rc = gbpe_set_error(t->ctx, GBPE_E_INVALID, "expand: the occurrence lists hold %llu body symbols, the trainer %llu",

@@ -6,6 +6,7 @@
 #include <cmath>
 
 #include "train_dev.h"
+#include "late.h"
 
 
 // ─── host side ──────────────────────────────────────────────────────────────
@@ -96,6 +97,16 @@ struct gbpe_trainer {
     uint32_t sub_zone = 1u << 20;   // sparse steps run in sub-steps of sub_k merges while the zone exceeds this
     uint32_t sub_k = 16;            // (the zone shrinks between them; GBPE_SUBSTEP_ZONE, GBPE_SUBSTEP)
     bool zone16 = true;             // u16 zones of 8K-16K symbols: the 16-per-thread zone pass 
+    // the late-merge loop (k_late): one workgroup runs a step's merges
+    bool late_on = true;         // GBPE_DEBUG late=0: off
+    bool late_skip = false;      // its last launch could not run a merge: this step runs k_body
+    LateHot* late_hot = nullptr; // hot-set refresh state
+    uint2* late_log = nullptr;   // the launch's count deltas (k_late_apply)
+    uint32_t late_logcap = 0;
+    uint32_t* late_u32 = nullptr;   // [0] log entries, [1..2] launch-end causes, [4..5] bytes (u64)
+    uint64_t late_merges = 0, late_launches = 0, late_exits = 0;
+    double ms_late = 0;
+    hipEvent_t late_ev[2] = {nullptr, nullptr};
     uint32_t sp_zt = 5;          // zone target = sp_zt * last_mc + 64 (>= zone_f; GBPE_DEBUG zt; 4/5/6/7 measured
                                  // 0.895/0.893/0.918/0.918 s at 1 GiB with zone_f 3)
     uint32_t shrink_pct = 200;   // shrink once the zone exceeds shrink_pct % of the target + 4096 
@@ -456,6 +467,83 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,
                        (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part, t->zseg);
     if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
+    GBPE_LAUNCH_CHECK(t->ctx);
+    return GBPE_OK;
+}
+
+// ── the late-merge loop ──
+
+// symbols the LDS zone buffers hold
+inline uint32_t late_zcap(const gbpe_trainer* t) {
+    return t->u16 ? LateDim<uint16_t>::ZCAP : LateDim<uint32_t>::ZCAP;
+}
+
+// a sparse step the late loop can run: the zone and the stale source it reads
+// fit the LDS buffers (the zone only shrinks within a step)
+inline bool late_eligible(const gbpe_trainer* t) {
+    const uint32_t zc = late_zcap(t);
+    const uint32_t z = (uint32_t)t->n - t->h_st->B;
+    return t->late_on && !t->late_skip && t->sp && !t->d_clog && z <= zc &&
+           (uint32_t)((uint32_t)t->n - t->h_st->Bp) <= zc && t->zcap >= zc;
+}
+
+int late_alloc(gbpe_trainer* t) {
+    hipStream_t s = t->ctx->stream;
+    if (!t->late_hot) {
+        TR_HIP(t, hipMalloc(&t->late_hot, sizeof(LateHot)));
+        TR_HIP(t, hipMemsetAsync(t->late_hot, 0, sizeof(LateHot), s));
+        TR_HIP(t, hipMalloc(&t->late_u32, 64));
+        TR_HIP(t, hipMemsetAsync(t->late_u32, 0, 64, s));
+    }
+    const uint32_t need = t->batch * (uint32_t)(LATE_LT + 1) + 4096;
+    if (t->late_logcap < need) {
+        hipFree(t->late_log);
+        t->late_log = nullptr;
+        t->late_logcap = 0;
+        TR_HIP(t, hipMalloc(&t->late_log, (uint64_t)need * sizeof(uint2)));
+        t->late_logcap = need;
+    }
+    if (!t->late_ev[0] && (t->flags & GBPE_TRAIN_TIMING)) {
+        TR_HIP(t, hipEventCreate(&t->late_ev[0]));
+        TR_HIP(t, hipEventCreate(&t->late_ev[1]));
+    }
+    return GBPE_OK;
+}
+
+// One step of the late loop: hot-set refresh (k_hot_hist, k_hot_gather), the
+// merges (k_late, one workgroup), their count deltas into the table
+// (k_late_apply) and the block maxima / partial maxima k_body selects from
+// (k_refresh): the table is exact again at the step boundary.
+template <typename S>
+int launch_late(gbpe_trainer* t, hipStream_t s, uint32_t g_refresh, bool timing) {
+    int rc = late_alloc(t);
+    if (rc != GBPE_OK) return rc;
+    const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
+    const uint32_t gh = grid_persistent(t->ctx, gbpe_div_up(((uint64_t)t->tb.mask + 1) / 2, 256), 1);
+    hipLaunchKernelGGL(k_hot_hist, dim3(gh), dim3(256), 0, s, t->tb, t->late_hot);
+    hipLaunchKernelGGL(k_hot_gather, dim3(gh), dim3(256), 0, s, t->tb, t->late_hot);
+    LateOut lo;
+    lo.dlog = t->late_log;
+    lo.dcap = t->late_logcap;
+    lo.dlog_n = t->late_u32;
+    lo.mlog = t->d_log;
+    lo.bytes = reinterpret_cast<uint64_t*>(t->late_u32 + 4);
+    lo.stat = t->late_u32 + 1;
+    S* z0 = (S*)t->zbuf[t->zcur];
+    S* z1 = (S*)t->zbuf[t->zcur ^ 1];
+    if (timing) TR_HIP(t, hipEventRecord(t->late_ev[0], s));
+    if (exact)
+        hipLaunchKernelGGL((k_late<S, true>), dim3(1), dim3(LATE_BT), 0, s, t->st, t->zst, (S*)sp_body(t), sp_mul(t),
+                           t->sec, t->bits, t->W, t->sig, z0, z1, t->late_hot, t->zone_f, lo);
+    else
+        hipLaunchKernelGGL((k_late<S, false>), dim3(1), dim3(LATE_BT), 0, s, t->st, t->zst, (S*)sp_body(t), sp_mul(t),
+                           t->sec, t->bits, t->W, t->sig, z0, z1, t->late_hot, t->zone_f, lo);
+    if (timing) TR_HIP(t, hipEventRecord(t->late_ev[1], s));
+    hipLaunchKernelGGL(k_late_apply, dim3(grid_persistent(t->ctx, 256, 1)), dim3(256), 0, s,
+                       (const uint2*)t->late_log, (const uint32_t*)t->late_u32, t->st, t->tb);
+    hipLaunchKernelGGL(k_refresh<S>, dim3(g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
+                       (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part,
+                       (uint32_t*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
 }
@@ -857,9 +945,11 @@ int lx_commit(gbpe_trainer* t, LxPlan& lp, const S* seg, bool fresh, bool keep_o
 }
 
 // lexicon → dense stream: every body word occurrence's current symbols, in
-// stream order, to dst[0, B); returns the symbol total through *tot
+// stream order, to dst[0, B); returns the symbol total through *tot.  The sizes
+// are checked before anything is written: an occurrence naming no entry, or a
+// total above dst_cap symbols, fails (GBPE_E_INVALID) with dst untouched.
 template <typename S>
-int lx_expand(gbpe_trainer* t, S* dst, uint64_t* tot, const uint32_t* occ = nullptr, uint64_t n_occ = 0) {
+int lx_expand(gbpe_trainer* t, S* dst, uint64_t dst_cap, uint64_t* tot, const uint32_t* occ = nullptr, uint64_t n_occ = 0) {
     // occ: another occurrence list over this store (the lexicon hand-over's rank lists)
     hipStream_t s = t->ctx->stream;
     if (!occ) occ = t->lx_occ, n_occ = t->lx_nocc;
@@ -871,19 +961,31 @@ int lx_expand(gbpe_trainer* t, S* dst, uint64_t* tot, const uint32_t* occ = null
     uint32_t* clen = c.take<uint32_t>(nu + 1);
     uint32_t* olen = c.take<uint32_t>(no + 1);
     uint64_t* oblk = c.take<uint64_t>(no / SCAN_BLK + 4);
+    uint32_t* bad = c.take<uint32_t>(4);
+    TR_HIP(t, hipMemsetAsync(bad, 0, 4, s));
     if (t->nsec)
         hipLaunchKernelGGL(k_lx_wordpos<S>, dim3((uint32_t)gbpe_div_up(t->nsec, TPB / 64)), dim3(TPB), 0, s,
                            (const S*)t->lx_store, (const uint2*)t->sec, t->nsec, (const uint32_t*)t->lx_w0, coff, clen);
     if (no)
         hipLaunchKernelGGL(k_lx_olen, dim3((uint32_t)gbpe_div_up(no, 256)), dim3(256), 0, s, occ, no,
-                           (const uint32_t*)clen, olen);
+                           (const uint32_t*)clen, olen, (uint32_t)nu, bad);
     lx_scan(s, olen, no, oblk);
+    GBPE_LAUNCH_CHECK(t->ctx);
+    uint64_t total = 0;
+    uint32_t hbad = 0;
+    TR_HIP(t, hipMemcpyAsync(&total, oblk + gbpe_div_up(no ? no : 1, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
+    TR_HIP(t, hipStreamSynchronize(s));
+    *tot = total;
+    if (hbad) return gbpe_set_error(t->ctx, GBPE_E_INVALID, "lexicon expand: an occurrence names no word entry");
+    if (total > dst_cap)
+        return gbpe_set_error(t->ctx, GBPE_E_INVALID, "lexicon expand: the occurrences hold %llu symbols, room for %llu",
+                              (unsigned long long)total, (unsigned long long)dst_cap);
     if (no)
         hipLaunchKernelGGL(k_lx_expand<S>, dim3((uint32_t)gbpe_div_up(no, 256)), dim3(256), 0, s, occ, no,
                            (const uint32_t*)coff, (const uint32_t*)clen, (const S*)t->lx_store, (const uint32_t*)olen,
-                           (const uint64_t*)oblk, dst);
+                           (const uint64_t*)oblk, dst, (uint32_t)nu);
     GBPE_LAUNCH_CHECK(t->ctx);
-    TR_HIP(t, hipMemcpyAsync(tot, oblk + gbpe_div_up(no ? no : 1, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
     return GBPE_OK;
 }
 
@@ -895,7 +997,7 @@ int lx_check(gbpe_trainer* t, const S* cur, uint32_t Zs, const LxPlan& lp) {
     S* chk = nullptr;
     TR_HIP(t, hipMalloc(&chk, ((uint64_t)Zs + 64) * sizeof(S)));
     uint64_t tot = 0;
-    rc = lx_expand<S>(t, chk, &tot);
+    rc = lx_expand<S>(t, chk, (uint64_t)Zs + 64, &tot);
     std::vector<S> a(Zs), b(Zs);
     TR_HIP(t, hipStreamSynchronize(s));
     TR_HIP(t, hipMemcpy(a.data(), chk, (uint64_t)Zs * sizeof(S), hipMemcpyDeviceToHost));
@@ -1159,7 +1261,9 @@ int sp_shrink(gbpe_trainer* t) {
     DevState* hs = t->h_st;
     const uint32_t z = (uint32_t)t->n - hs->B;
     const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
-    if (t->sp_shrinks >= SP_SHRINKS || (uint64_t)z < zt * t->shrink_pct / 100 + 4096) return GBPE_OK;
+    // a zone just above the late loop's LDS buffers shrinks to its target at once
+    const bool to_late = t->late_on && z > late_zcap(t) && zt + 1024 <= late_zcap(t);
+    if (t->sp_shrinks >= SP_SHRINKS_MAX || (!to_late && (uint64_t)z < zt * t->shrink_pct / 100 + 4096)) return GBPE_OK;
     S* zc = (S*)t->zbuf[t->zcur];
     S* zo = (S*)t->zbuf[t->zcur ^ 1];
     hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, (const S*)zc, (uint32_t)(z - zt), t->d_u32);
@@ -1167,7 +1271,7 @@ int sp_shrink(gbpe_trainer* t) {
     uint32_t L = 0;
     TR_HIP(t, hipMemcpyAsync(&L, t->d_u32, 4, hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipStreamSynchronize(s));
-    if (L < 4096) return GBPE_OK;
+    if (L < (to_late ? 1024u : 4096u)) return GBPE_OK;
     if (t->lex) {   // the front's words join the lexicon (deduplicated among themselves)
         LxPlan lp;
         int rc = lx_analyze<S>(t, (const S*)zc, L, false, lp);
@@ -1223,7 +1327,7 @@ int sp_exit(gbpe_trainer* t) {
     const uint32_t nsec = t->nsec;
     uint64_t btot = 0;
     if (t->lex) {
-        int rc = lx_expand<S>(t, dst, &btot);
+        int rc = lx_expand<S>(t, dst, (uint64_t)B, &btot);
         if (rc != GBPE_OK) return rc;
     } else {
         hipLaunchKernelGGL(k_sp_counts, dim3((uint32_t)gbpe_div_up(nsec, 256)), dim3(256), 0, s, (const uint2*)t->sec, nsec,
@@ -1275,6 +1379,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->rehash_on = gbpe_debug_knob("rehash", 1) != 0;
     t->delta_mt = (uint32_t)gbpe_debug_knob("delta_mt", t->delta_mt);
     t->sp_zt = (uint32_t)gbpe_debug_knob("zt", t->sp_zt);
+    t->late_on = gbpe_debug_knob("late", 1) != 0;
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
         t->trace = fopen(e, "w");

@@ -11,9 +11,10 @@ share the part that is not a chain, the first pass over the corpus:
   lexicon (``gbpe_lexshard_build``): its distinct words, each with its
   multiplicity, plus the occurrence list that keeps its stream order;
 * the sum of the ranks' largest counts bounds the first merge's global count,
-  which sizes the dense zone the last rank keeps (the stream's tail, where the
-  reference compaction quirk acts, train.wgsl:605-607 + 698/727);
-* the stores (and the zone) go to ONE root, the last rank, which deduplicates
+  which sizes the dense zone (the stream's tail, where the reference compaction
+  quirk acts, train.wgsl:605-607 + 698/727): the last ranks keep their part of
+  it dense — the tail of one piece and every piece after it;
+* the stores and the zone parts go to ONE root, the last rank, which deduplicates
   them into one lexicon, counts the pairs and continues with the single-device
   sector-sparse loop (``gbpe_trainer_create_from_lexicon``) from the first merge;
 * the root broadcasts the merge list; on request it sends each rank its slice of
@@ -249,29 +250,79 @@ class LexShardTrainer:
         self.map = None
         self.root_stats = None
 
+    def _agree(self, failed: bool, err, what: str):
+        """Every rank learns whether any rank failed since the last exchange and
+        raises alike (a rank that left early would leave its peers blocked in the
+        next collective)."""
+        bad = self.x.ints([1 if failed else 0])[:, 0]
+        if bad.any():
+            if err is not None:
+                raise err
+            raise RuntimeError(f"lexicon hand-over: rank(s) {np.flatnonzero(bad).tolist()} failed in {what}")
+
+    def zone_targets(self, lens, ub: int):
+        """Per-rank zone targets: the zone is the stream's last zt symbols (the zone
+        rule's target for a first count <= ub, trainer.h sp_enter), which may span
+        the tails of several pieces; a rank whose piece lies wholly inside it keeps
+        the whole piece dense (target = its length), the rank where it begins keeps
+        its tail from the last word start at or before the zone's start."""
+        zt = max(self.sp_zt * ub, 2 * ub) + 64
+        N = int(np.sum(lens))
+        if zt + 2 >= N:
+            raise RuntimeError(f"lexicon hand-over: a zone of {zt} symbols does not fit the {N}-symbol stream")
+        G = N - zt
+        offs = np.concatenate([[0], np.cumsum(lens)])
+        out = []
+        for q in range(len(lens)):
+            a, b = int(offs[q]), int(offs[q + 1])
+            out.append(0 if b <= G else (b - a if a >= G else b - G))
+        return out
+
     def first_pass(self, piece, n: int, on_device: bool, word_starts=None):
-        """Symbols, counts and the word lexicon of this rank's piece; stores (and
-        the zone) to the root.  Returns the root's inputs there, None elsewhere."""
+        """Symbols, counts and the word lexicon of this rank's piece; stores and
+        zone parts to the root.  Returns the root's inputs there, None elsewhere."""
         t0 = time.perf_counter()
-        info = self.b.create(piece, n, on_device, word_starts)
-        ub = int(self.x.ints([info["top_count"]])[:, 0].sum())   # >= the first merge's global count
-        zt = max(self.sp_zt * ub, 2 * ub) + 64                    # the zone rule's target (trainer.h sp_enter)
+        info, err = None, None
+        try:
+            info = self.b.create(piece, n, on_device, word_starts)
+        except Exception as e:  # noqa: BLE001 — every rank raises below
+            err = e
+        g = self.x.ints([info["top_count"], info["symbols"], 0] if info else [0, 0, 1])
+        if g[:, 2].any():
+            if err is not None:
+                raise err
+            raise RuntimeError(f"lexicon hand-over: rank(s) {np.flatnonzero(g[:, 2]).tolist()} failed in create")
+        ub = int(g[:, 0].sum())   # >= the first merge's global count
+        zts = self.zone_targets(g[:, 1], ub)
         self.timing["create_s"] = time.perf_counter() - t0
-        info = self.b.build(zt if self.rank == self.root else 0)
-        bps = info["bytes_per_symbol"]
+        try:
+            info = self.b.build(zts[self.rank])
+        except Exception as e:  # noqa: BLE001
+            err, info = e, None
         sh = self.x.ints([info["store_symbols"], info["entries"], info["words"], info["body"], info["zone"],
-                          info["symbols"]])
-        self.shapes = sh
+                          info["symbols"], 0] if info else [0] * 6 + [1])
+        if sh[:, 6].any():
+            if err is not None:
+                raise err
+            raise RuntimeError(f"lexicon hand-over: rank(s) {np.flatnonzero(sh[:, 6]).tolist()} failed in build")
+        self.shapes = sh[:, :6]
         self.timing["build_s"] = time.perf_counter() - t0
-        T = info["store_symbols"]
-        store = self.b.export(STORE, T * bps, self.x.dev)
-        mul = self.b.export(MUL, T * 4, self.x.dev)
-        zone = self.b.export(ZONE, info["zone"] * bps, self.x.dev) if self.rank == self.root else None
-        self.b.release()   # the piece's stream and counts are no longer needed
+        bps = info["bytes_per_symbol"]
+        store = mul = zone = None
+        try:
+            T = info["store_symbols"]
+            store = self.b.export(STORE, T * bps, self.x.dev)
+            mul = self.b.export(MUL, T * 4, self.x.dev)
+            zone = self.b.export(ZONE, info["zone"] * bps, self.x.dev)
+            self.b.release()   # the piece's stream and counts are no longer needed
+        except Exception as e:  # noqa: BLE001
+            err = e
+        self._agree(err is not None, err, "export")
         stores = self.x.to_root(store, [int(v) * bps for v in sh[:, 0]], self.root)
         muls = self.x.to_root(mul, [int(v) * 4 for v in sh[:, 0]], self.root)
+        zones = self.x.to_root(zone, [int(v) * bps for v in sh[:, 4]], self.root)   # in rank order: the stream's tail
         self.timing["exchange_s"] = time.perf_counter() - t0
-        return (stores, muls, zone) if self.rank == self.root else None
+        return (stores, muls, zones) if self.rank == self.root else None
 
     def train(self, piece, n: int, on_device: bool, target_vocab: int, word_starts=None, batch: int = BATCH_SIZE,
               on_progress=None):
@@ -283,7 +334,7 @@ class LexShardTrainer:
             try:
                 sh = self.shapes
                 t1 = time.perf_counter()
-                self.map = self.b.root_create(*got, int(sh[:, 0].sum()), int(sh[self.root, 4]), int(sh[:, 3].sum()),
+                self.map = self.b.root_create(*got, int(sh[:, 0].sum()), int(sh[:, 4].sum()), int(sh[:, 3].sum()),
                                               int(sh[:, 1].sum()))
                 del got
                 t2 = time.perf_counter()
@@ -320,8 +371,13 @@ class LexShardTrainer:
             offs = np.concatenate([[0], np.cumsum(sizes)])
             parts = [self.map[int(offs[q]): int(offs[q + 1])] for q in range(self.world)]
         mine = self.x.from_root(parts, sizes, self.root)
-        self.b.remap(mine, int(sh[self.rank, 1]))
-        occ = self.b.export(OCC, int(sh[self.rank, 2]) * 4, self.x.dev)
+        occ, err = None, None
+        try:
+            self.b.remap(mine, int(sh[self.rank, 1]))
+            occ = self.b.export(OCC, int(sh[self.rank, 2]) * 4, self.x.dev)
+        except Exception as e:  # noqa: BLE001
+            err = e
+        self._agree(err is not None, err, "remap / occurrence export")
         allocc = self.x.to_root(occ, [int(v) * 4 for v in sh[:, 2]], self.root)
         if self.rank != self.root:
             return None

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GBPE_ABI_VERSION 2   /* 2: gbpe_trainer_stats grew (round 2), shard/state entry points */
+#define GBPE_ABI_VERSION 3   /* 3: late-loop stats, the per-merge sharded entry points removed (round 4) */
 
 /* status codes */
 #define GBPE_OK            0
@@ -179,10 +179,13 @@ typedef struct gbpe_trainer_stats {
     uint64_t lexicon_words;       /* body word occurrences the lexicon represents (all builds and shrinks) */
     uint64_t lexicon_entries;     /* distinct-word entries of the current lexicon */
     uint64_t lexicon_symbols;     /* symbols of the current lexicon store (separators included) */
-    uint64_t tail_merges;         /* merges run by the persistent one-workgroup tail loop */
-    uint64_t tail_steps;          /* its launches (one per step) */
-    uint64_t tail_exits;          /* ... that left their step early (LDS lists outgrown) */
-    double   ms_tail;             /* GBPE_TRAIN_TIMING: device ms of the tail loop (included in ms_sparse) */
+    uint64_t late_merges;         /* merges run by the one-workgroup late-merge loop k_late */
+    uint64_t late_launches;       /* its launches (one per step) */
+    uint64_t late_exits;          /* ... that ended before their step's budget (the hot-set bound; host refreshes) */
+    double   ms_late;             /* GBPE_TRAIN_TIMING: device ms of k_late (included in ms_sparse) */
+    uint64_t late_bytes;          /* bytes k_late moved: body sectors read + rewritten, extents + signatures,
+                                     the LDS-resident zone pass (pair-table traffic excluded) */
+    uint64_t late_bound_exits;    /* k_late launches ended by the hot-set bound */
 } gbpe_trainer_stats;
 int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* out);
 /* Current symbol stream in the reference u32 layout (bit16 = word start). */
@@ -223,14 +226,17 @@ int gbpe_trainer_create_from_state(gbpe_ctx* ctx, const uint32_t* cur, uint64_t 
  * stream, the pieces concatenated in rank order are the corpus) into symbols, pair
  * counts and a word lexicon — its distinct words with their multiplicities — and ONE
  * root continues from all of them with the single-device sector-sparse loop
- * (DESIGN §2b/§2c).  The last piece keeps its tail as the dense zone, where the
- * reference compaction quirk acts (train.wgsl:605-607 + 698/727).  The stream order
+ * (DESIGN §2b/§2c).  The stream's tail — the last zt symbols, cut at a word start;
+ * it may span several pieces — stays dense as the zone, where the reference
+ * compaction quirk acts (train.wgsl:605-607 + 698/727).  The stream order
  * of the body stays on the ranks (their occurrence lists), so the stream may exceed
  * one device's 32-bit positions (C4: 8.6*10^9 symbols).  Protocol:
- *   rank:  lexshard_create → info_get: top_count → (sum over ranks: an upper bound of the
- *          first merge's count; the last rank's zone target) lexshard_build(zt)
- *          → copy STORE + MUL (and the last rank's ZONE) to the root → release
- *   root:  trainer_create_from_lexicon(stores in rank order, zone, body symbols)
+ *   rank:  lexshard_create → info_get: top_count, symbols → (sum of top counts: an upper
+ *          bound of the first merge's count → zt; this piece's part of the last zt
+ *          stream symbols) lexshard_build(part) → copy STORE + MUL + ZONE to the root
+ *          → release
+ *   root:  trainer_create_from_lexicon(stores in rank order, zones in rank order,
+ *          body symbols)
  *          → map (a global word id per store entry, in rank order) → rank slices
  *          → lexshard_remap; gbpe_trainer_step as for any trainer
  *   check: gbpe_trainer_expand(root, every rank's OCC in rank order) = the stream. */
@@ -238,7 +244,7 @@ typedef struct gbpe_lexshard gbpe_lexshard;
 typedef struct gbpe_lexshard_info {
     uint64_t symbols;        /* the piece's symbols */
     uint64_t body;           /* symbols before its zone (all of them on a rank without a zone) */
-    uint64_t zone;           /* zone symbols (the last rank) */
+    uint64_t zone;           /* zone symbols (the ranks holding the stream's tail) */
     uint64_t store_symbols;  /* distinct words + one 0 separator each */
     uint64_t entries;        /* distinct words (words over 64 symbols: one entry per occurrence) */
     uint64_t words;          /* body words in stream order (the occurrence list) */
@@ -252,14 +258,14 @@ typedef struct gbpe_lexshard_info {
 /* opts as for gbpe_trainer_create, identical on every rank and the root */
 int  gbpe_lexshard_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
                           int input_on_device, const gbpe_train_opts* opts, gbpe_lexshard** out);
-int  gbpe_lexshard_build(gbpe_lexshard* ls, uint64_t zone_target /* 0: no zone */);
+int  gbpe_lexshard_build(gbpe_lexshard* ls, uint64_t zone_target /* 0: no zone; >= symbols: all zone */);
 int  gbpe_lexshard_info_get(const gbpe_lexshard* ls, gbpe_lexshard_info* out);
 int  gbpe_lexshard_copy(gbpe_lexshard* ls, int part, void* dst, uint64_t cap_bytes, int dst_on_device);
 int  gbpe_lexshard_release(gbpe_lexshard* ls);   /* frees the piece's stream and counts, keeps the lexicon */
 int  gbpe_lexshard_remap(gbpe_lexshard* ls, const uint32_t* map, uint64_t n_map, int map_on_device);
 void gbpe_lexshard_destroy(gbpe_lexshard* ls);
 /* The root trainer: store / mul = every rank's STORE and MUL concatenated in rank
- * order (store_len symbols), zone = the last rank's ZONE, body_len = the symbols of
+ * order (store_len symbols), zone = every rank's ZONE in rank order, body_len = the symbols of
  * every piece before the zone (the stream is body_len + zone_len symbols; may exceed
  * 2^32).  map_out (map_cap entries) receives one global word id per store entry.
  * The trainer never returns to one dense stream: gbpe_trainer_symbols /

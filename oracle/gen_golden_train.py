@@ -34,8 +34,12 @@ from gpubpe import synth  # noqa: E402
 
 GOLD = os.path.join(ROOT, "tests", "golden")
 
-# name -> (corpus spec, target vocab, boundary source)
+# name -> (corpus spec, target vocab, boundary source[, compaction]); compaction "reference"
+# (default: the quirk of train.wgsl:605-607 + 698/727) or "exact"
 TRAIN = {
+    # C1 (BASELINE configs[0]): 256 KiB ASCII English, seed 1, 1K vocab (768 merges)
+    "c1": ({"gen": "english", "n": 262_144, "seed": 1}, 1024, "heuristic"),
+    "c1x": ({"gen": "english", "n": 262_144, "seed": 1}, 1024, "heuristic", "exact"),
     # C2, exactly the bench's secondary leg (bench.py train_leg)
     "c2": ({"gen": "english", "n": 104_857_600, "seed": 2, "fancy_punct": 0.005}, 32768, "heuristic"),
     # headline: 1 GiB English-like UTF-8 @ 32K (BASELINE.json metric)
@@ -78,13 +82,15 @@ def sha(b) -> str:
 
 
 def gen_train(name: str):
-    spec, vocab, bnd = TRAIN[name]
+    spec, vocab, bnd = TRAIN[name][:3]
+    compaction = TRAIN[name][3] if len(TRAIN[name]) > 3 else "reference"
     t = time.time()
     data = corpus(spec)
     ws = cpu_ref.gpt4_word_starts_ascii(data) if bnd == "gpt4" else None
-    r = cpu_ref.train_inc(data, vocab, word_starts=ws, want_symbols=True)
+    r = cpu_ref.train_inc(data, vocab, word_starts=ws, want_symbols=True, exact=compaction == "exact")
     syms = np.ascontiguousarray(r["symbols"], dtype="<u4")
     meta = {"name": name, "corpus": spec, "corpus_sha256": sha(data), "target_vocab": vocab, "boundaries": bnd,
+            "compaction": compaction,
             "final_n": r["final_n"], "tail_total": r["tail_total"], "early_stop": r["early_stop"],
             "final_stream_sha256": sha(syms.tobytes()), "n_merges": len(r["merges"]),
             "generator": "oracle/bpe_oracle_inc.c (oracle/gen_golden_train.py)"}

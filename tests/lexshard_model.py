@@ -69,11 +69,11 @@ class ModelLexBackend:
     def build(self, zone_target):
         s, n = self.s, int(self.s.shape[0])
         Zs = n
-        if zone_target:
-            assert zone_target + 2 < n, "zone does not fit the last piece"
+        if zone_target >= n:   # the whole piece lies inside the zone
+            Zs = 0
+        elif zone_target:
             st = np.flatnonzero(_starts(s)[: n - zone_target + 1])
             Zs = int(st[-1])
-            assert Zs > 0
         self.Zs = Zs
         self.uids, mult, self.occ = {}, [], []
         for w in _words(s[:Zs]):

@@ -5,6 +5,8 @@ Every merge [a, b, id, count] of a whole training run, the final stream length,
 the reference compaction's stale-tail total and the sha256 of the final symbol
 stream must equal the CPU restatement's.  Configurations:
 
+* c1, c1x — C1 (BASELINE configs[0]): 256 KiB ASCII English, seed 1, 1K vocab,
+            768 merges, reference and exact compaction
 * c2      — 100 MiB English (the bench's C2 leg), 32K vocab, 32,512 merges
 * en1g    — 1 GiB English @ 32K: the bench's headline workload
 * code1g  — C5: 1 GiB code, 50K vocab (u32 symbols), GPT-4 rule word starts
@@ -82,6 +84,8 @@ def _check_train(eng, name: str):
     data = G.corpus(meta["corpus"])
     assert _sha(data) == meta["corpus_sha256"], "corpus generator drift (numpy version?): not the fixture's input"
     flags = _lib.GBPE_TRAIN_GPT4_BOUNDARIES if meta["boundaries"] == "gpt4" else 0
+    if meta.get("compaction") == "exact":
+        flags |= _lib.GBPE_TRAIN_EXACT_COMPACTION
     got, st, syms = _train_full(eng, data, meta["target_vocab"], flags)
     assert got.shape == want.shape, (got.shape, want.shape)
     bad = np.flatnonzero((got != want).any(axis=1))
@@ -91,6 +95,13 @@ def _check_train(eng, name: str):
     assert bool(st.early_stop) == meta["early_stop"]
     assert _sha(syms.tobytes()) == meta["final_stream_sha256"]
     return st, syms
+
+
+@pytest.mark.parametrize("name", ["c1", "c1x"])
+def test_full_c1(eng, name):
+    # C1 on the HIP path: every merge, the final stream and the stale-tail total
+    st, _ = _check_train(eng, name)
+    assert st.merges_done == 768 and st.bytes_per_symbol == 2
 
 
 def test_full_c2_bench_corpus(eng):

@@ -13,7 +13,6 @@ from __future__ import annotations
 
 import json
 import os
-import socket
 import sys
 import tempfile
 
@@ -29,12 +28,7 @@ import bpe_oracle as O  # noqa: E402
 from gpubpe import synth  # noqa: E402
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+from dist_util import free_port as _free_port  # noqa: E402
 
 
 def _corpus(case):
@@ -61,13 +55,22 @@ def _worker(rank, world, port, case, outdir):
         piece = pieces_at_word_starts(dist, shard, lambda b: O.heuristic_word_starts(np.frombuffer(b, np.uint8)),
                                       halo=case.get("halo", 1 << 16))
         be = ModelLexBackend(exact=case["exact"])
+        if case.get("fail_build") == rank:   # a rank whose build fails: every rank must raise, none may hang
+            def boom(zt):
+                raise RuntimeError("injected build failure")
+            be.build = boom
         tr = LexShardTrainer(be, dist, staged=True)
-        merges, early = tr.train(piece, len(piece), False, case["vocab"], batch=case.get("batch", 128))
+        try:
+            merges, early = tr.train(piece, len(piece), False, case["vocab"], batch=case.get("batch", 128))
+        except RuntimeError as e:
+            with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
+                json.dump({"error": str(e)}, f)
+            return
         fin = tr.final_stream()
         if fin is not None:
             np.save(os.path.join(outdir, "final.npy"), fin)
         with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
-            json.dump({"merges": merges, "early": early, "piece": len(piece), "zone": int(tr.shapes[-1, 4])}, f)
+            json.dump({"merges": merges, "early": early, "piece": len(piece), "zones": tr.shapes[:, 4].tolist()}, f)
     finally:
         dist.destroy_process_group()
 
@@ -78,7 +81,7 @@ def run_case(world, case):
         mp.start_processes(_worker, args=(world, _free_port(), case, td), nprocs=world, start_method="spawn",
                            join=True)
         res = [json.load(open(os.path.join(td, f"r{r}.json"))) for r in range(world)]
-        fin = np.load(os.path.join(td, "final.npy"))
+        fin = np.load(os.path.join(td, "final.npy")) if os.path.exists(os.path.join(td, "final.npy")) else None
     return res, fin
 
 
@@ -91,6 +94,11 @@ CASES = [
     # (UTF-8 sequences and words cut at the shard seams), 3 shards at 64K-style ids
     ("c4_shaped_w3", 3, dict(gen="multilingual", shard=12_000, seeds=[5, 6, 7], fracs=[1 / 3, 2 / 3], vocab=600,
                              exact=False)),
+    # the zone (5 x the first count) is longer than the last piece: it spans the
+    # tail of one piece and the whole of the next ones (the N=8 headline shape)
+    ("zone_spans_w3", 3, dict(bytes=30_000, seed=25, fracs=[0.6, 0.93], vocab=560, exact=False, spans=2)),
+    ("zone_spans_w4_exact", 4, dict(bytes=30_000, seed=26, fracs=[0.5, 0.9, 0.95], vocab=560, exact=True, batch=32,
+                                    spans=3)),
 ]
 
 
@@ -104,3 +112,13 @@ def test_lexshard_matches_single_stream(name, world, case):
         assert res[r]["early"] == exp["early_stop"]
     assert sum(r["piece"] for r in res) == len(data)       # the pieces tile the corpus
     np.testing.assert_array_equal(fin, exp["symbols"])
+    if "spans" in case:
+        assert sum(1 for z in res[0]["zones"] if z) >= case["spans"], res[0]["zones"]
+
+
+def test_lexshard_failure_reaches_every_rank():
+    # a rank failing in its build must not leave the others blocked in
+    # the next collective — every rank raises
+    res, _ = run_case(3, dict(bytes=24_000, seed=22, fracs=[0.4, 0.7], vocab=520, exact=False, fail_build=1))
+    assert all("error" in r for r in res), res
+    assert "injected" in res[1]["error"] and "rank(s) [1]" in res[0]["error"]

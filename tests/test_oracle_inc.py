@@ -28,6 +28,22 @@ def test_inc_english_c1(exact):
     assert len(r["merges"]) == 768
 
 
+@pytest.mark.parametrize("name", ["c1", "c1x"])
+def test_c1_fixture_is_the_full_recount(name):
+    # the committed C1 fixtures (GPU test + bench leg) equal the reference algorithm
+    # restated as a full recount per merge (oracle/bpe_oracle.c)
+    import hashlib
+    import gen_golden_train as G
+    want, meta = G.load_train(name)
+    data = G.corpus(meta["corpus"])
+    assert hashlib.sha256(data).hexdigest() == meta["corpus_sha256"]
+    r = cpu_ref.train(data, meta["target_vocab"], exact=meta["compaction"] == "exact")
+    assert np.array_equal(np.array(r["merges"], dtype=np.uint32), want)
+    assert r["tail_total"] == meta["tail_total"] and int(r["symbols"].shape[0]) == meta["final_n"]
+    syms = np.ascontiguousarray(r["symbols"], dtype="<u4")
+    assert hashlib.sha256(syms.tobytes()).hexdigest() == meta["final_stream_sha256"]
+
+
 def test_inc_multilingual_and_code_gpt4():
     from gpubpe import synth
     _same(synth.multilingual(1 << 19, seed=4), 2000)

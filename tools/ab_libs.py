@@ -55,11 +55,15 @@ for name in sys.argv[4:]:
             if nd.value == 0 or es.value:
                 break
         t1 = time.perf_counter()
+        st = _lib.TrainerStats()
+        lib.gbpe_trainer_stats_get(tr, C.byref(st))
         lib.gbpe_trainer_destroy(tr)
         m = np.array(merges, dtype=np.uint32).reshape(-1, 4)
         eq = m.shape == fx.shape and bool((m == fx).all())
         if rep:
-            print(json.dumps({"name": name, "s": round(t1 - t0, 4), "merges": int(m.shape[0]), "equal": eq}), flush=True)
+            print(json.dumps({"name": name, "s": round(t1 - t0, 4), "merges": int(m.shape[0]), "equal": eq,
+                              "late": [int(st.late_merges), int(st.late_launches), int(st.late_exits),
+                                       int(st.late_bound_exits)], "sparse_exits": int(st.sparse_exits)}), flush=True)
         if not eq:
             print(json.dumps({"name": name, "error": "merges differ from the fixture"}), flush=True)
             sys.exit(3)
@@ -85,8 +89,10 @@ def main():
                 j = json.loads(line)
                 if "error" in j:
                     print(lp, j, flush=True)
+                    print(p.stderr[-3000:], flush=True)
                     sys.exit(3)
                 res.setdefault((lp, j["name"]), []).append(j["s"])
+                print(lp, line, flush=True)
             if p.returncode:
                 print(lp, "rc", p.returncode, p.stderr[-2000:], flush=True)
                 sys.exit(p.returncode)
