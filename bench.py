@@ -10,6 +10,8 @@ initial pair count) plus all 32,512 merges (every 128-merge host round trip of
 trainer.js:225-335).  `value` = merges of the K timed runs / their wall time.
 
 Secondary legs (same JSON line):
+  * c1: BASELINE configs[0] (1K vocab on 256 KiB ASCII, seed 1), full runs, with
+    the full 768-merge CPU run on 1 core and on the CPU share beside it;
   * c2: BASELINE configs[1] (100 MiB English, seed 2, 32K vocab), full runs;
   * tokenize (configs[2], C3): chunked trie encode of 1 GiB multilingual text
     with a 32K vocab trained on a 100 MiB sample (seed 4);
@@ -361,6 +363,47 @@ def config_leg(args, lib, ctx, dist, name, data, vocab, flags, workload, runs=2)
     return res
 
 
+def c1_leg(args, lib, ctx, dist):
+    """C1 (BASELINE configs[0]): 1K vocab on 256 KiB ASCII English (seed 1), 768
+    merges, heuristic word boundaries.  GPU: full runs on HBM-resident input,
+    every merge checked against tests/golden/train_c1.npz.  CPU (BASELINE.md's
+    plan): the same full run by the reference algorithm restated on the host
+    (oracle/bpe_oracle.c, full recount per merge) on 1 core and on the CPU share.
+    The reference itself needs a WebGPU adapter; none exists on the box
+    (profiles/r3_webgpu_probe.txt: no Vulkan ICD, Dawn, wgpu or browser)."""
+    want, meta = fixture("c1")
+    data = make_corpus({"gen": "english", "n": 262_144, "seed": 1})
+    d = device_buffer(lib, ctx, data)
+    runs = 20
+    wall, total, last, st = timed_runs(args, lib, ctx, dist, d, len(data), 1024, runs, 2)
+    lib.gbpe_device_free(ctx, d)
+    res = {"workload": "C1 (BASELINE configs[0]): 1K-vocab train on 262,144 B ASCII English (seed 1), 768 merges, "
+                       "heuristic word boundaries, reference compaction; full runs on the HBM-resident corpus",
+           "value": round(total / wall, 1), "unit": "merges/s", "runs": runs, "merges_per_run": int(last.shape[0]),
+           "ms_per_run": round(1e3 * wall / runs, 3),
+           "webgpu_reference": "not runnable: no WebGPU implementation on the box (profiles/r3_webgpu_probe.txt)"}
+    if want is not None:
+        res["corpus_sha256_equal"] = hashlib.sha256(data).hexdigest() == meta["corpus_sha256"]
+        res["merges_equal_fixture"] = bool(last.shape == want.shape and np.array_equal(last, want))
+        res["fixture"] = "tests/golden/train_c1.npz"
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import cpu_ref
+        share = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        cpu = {}
+        for cores in (1, share):
+            t0 = time.perf_counter()
+            r = cpu_ref.train(data, 1024, threads=cores, want_symbols=False)
+            dt = time.perf_counter() - t0
+            cpu[str(cores)] = {"merges_per_s": round(len(r["merges"]) / dt, 1), "seconds": round(dt, 3),
+                               "merges_equal_fixture": bool(want is not None and np.array_equal(
+                                   np.array(r["merges"], dtype=np.uint32), want))}
+        res["cpu_baseline"] = {"kind": "port", "sample": "the full 768-merge run, full pair recount per merge "
+                                                         "(oracle/bpe_oracle.c, OpenMP)", "cores": cpu,
+                               "nproc": os.cpu_count()}
+    return res
+
+
 def encode_leg(args, lib, ctx, dist, rank):
     """C3: train a 32K vocab on a 100 MiB multilingual sample (seed 4), then
     encode 1 GiB multilingual text (seed 3) with the chunked trie walk."""
@@ -514,6 +557,8 @@ def single_line(args, lib, ctx, dist, rank):
         "train_detail": det,
         "parity": parity,
     }
+    if not args.no_c1:
+        line["c1"] = c1_leg(args, lib, ctx, dist)
     if not args.no_c2:
         _, line["c2"] = c2_leg(args, lib, ctx, dist)
     enc = None
@@ -838,6 +883,7 @@ def main():
     ap.add_argument("--vocab-sample-bytes", type=int, default=104_857_600)
     ap.add_argument("--no-encode", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 leg (1K vocab on 256 KiB ASCII)")
     ap.add_argument("--no-c2", action="store_true")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 per-rank shard leg (64K vocab)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 leg (1 GiB code, 50K vocab, GPT-4 rules)")

@@ -238,6 +238,19 @@ def test_trainer_api_and_persistent_vocab(eng):
     assert t.export_vocab() == v.export()
 
 
+def test_word_boundary_known_answers_gpu(eng):
+    # the hand-traced byte-class cases (train.wgsl:111-185) through the device kernel
+    import json, os
+    from gpubpe import _lib
+    lib = _lib.load()
+    ka = json.load(open(os.path.join(GOLDEN, "known_answers.json")))
+    for c in ka["word_boundary"]:
+        data = bytes.fromhex(c["text_hex"]) if "text_hex" in c else c["text"].encode("utf-8")
+        out = np.zeros(len(data), np.uint8)
+        _lib.check(lib.gbpe_word_boundary(eng.device, data, len(data), out.ctypes.data_as(C.c_void_p)), eng.device, "wb")
+        assert out.astype(int).tolist() == c["ws"], c["name"]
+
+
 def test_word_boundary_kernel(eng):
     from gpubpe import _lib
     lib = _lib.load()
