@@ -185,6 +185,17 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
     return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
 }
 
+// phase stamps of a -DGBPE_KTRACE build (tools/ktrace_late.py): every KT_EVERY-th
+// merge, slots 0-5 = merge start, selection done, zone reads done, zone written,
+// body done, merge closed; 6 = candidates << 16 | filtered candidates
+#ifdef GBPE_KTRACE
+#define LKT(i) do { if (t == 0) kt_put(r, KT_WG - 1u, (i), wall_clock64()); } while (0)
+#define LKTV(i, v) do { if (t == 0) kt_put(r, KT_WG - 1u, (i), (v)); } while (0)
+#else
+#define LKT(i) ((void)0)
+#define LKTV(i, v) ((void)0)
+#endif
+
 struct LateOut {
     uint2* dlog;            // count deltas of the launch (k_late_apply)
     uint32_t dcap;
@@ -259,6 +270,7 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
     const LateSpill spill{out.dlog, out.dcap, &s_logpos, &s_inval};
     uint64_t bytes = 0;
     for (uint32_t r = 0; ended_by == 0 && r < budget; ++r) {
+        LKT(0);
         // ── selection over the hot set ──
         uint64_t best = 0;
         for (uint32_t i = t; i < LATE_HS; i += BT) {
@@ -278,6 +290,7 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
 #pragma unroll
         for (int w2 = 1; w2 < NWAVE; ++w2) best = s_red[w2] > best ? s_red[w2] : best;
         best = uni64(best);
+        LKT(1);
         const uint32_t mc = (uint32_t)(best >> 32);
         const uint32_t pid = ~(uint32_t)best;
         const uint32_t a = pid >> 16, b = pid & 0xFFFFu, nw = nid;
@@ -401,6 +414,7 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
         if (lane == 63) s_sum[wid] = incl;
         if (lane == 0) s_tl[wid] = tl;
         __syncthreads();   // every read of C and P is done
+        LKT(2);
         uint32_t pre = incl - kc, Kz = 0, m = 0;
 #pragma unroll
         for (int w2 = 0; w2 < NWAVE; ++w2) {
@@ -453,6 +467,8 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
             ncand += s_sum[w2];
         }
         ncand = uni(ncand);
+        LKT(3);
+        [[maybe_unused]] uint32_t nfilt = 0;
         // ── body passes: candidates in batches of LATE_CAP (bitmap words beyond the
         //    first 4 x 1024 in further passes) ──
         uint32_t removed = 0;
@@ -494,6 +510,7 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
                 }
                 __syncthreads();
                 const uint32_t nc = uni(s_n);
+                nfilt += nc;
                 // one wave per sector; the next one's first pass loads while this one merges
                 uint32_t nf[5], nfm[4];
                 if ((uint32_t)wid < nc)
@@ -552,6 +569,8 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
             __syncthreads();
         }
         if (lane == 0) s_rm[wid] = removed;   // (per lane: body_sector returns the wave's total)
+        LKT(4);
+        LKTV(6, ((uint64_t)ncand << 16) | nfilt);
         // ── the merge's deltas: log, hot set, bound ──
         uint32_t wmax = 0;
         for (uint32_t i = t; i < (uint32_t)LATE_LT; i += BT) {
@@ -602,6 +621,7 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
         done = r + 1;
         const bool inval = uni(s_inval) != 0u;
         __syncthreads();   // s_wmax, s_rm, s_inval read by all
+        LKT(5);
         if (t == 0) s_wmax = 0u;
         if (inval) {
             ended_by = 2;
@@ -663,5 +683,8 @@ __global__ __launch_bounds__(256) void k_late_apply(const uint2* __restrict__ dl
     }
     lds_flush(lt, tb, st);
 }
+
+#undef LKT
+#undef LKTV
 
 }  // namespace
