@@ -66,10 +66,24 @@ def recount(fin_host: np.ndarray):
     return u.cpu().numpy().astype(np.uint32), tot.cpu().numpy()
 
 
+def heartbeat(rank):
+    # gpurun takes 3 minutes without output for a hang: one line per 30 s
+    import threading
+
+    def beat():
+        t0 = time.time()
+        while True:
+            time.sleep(30)
+            log(f"[c4check] rank {rank} alive {time.time() - t0:.0f}s")
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     from gpubpe import _lib, synth
     from gpubpe.lexshard import GpuLexBackend, LexShardTrainer, device_word_boundary, pieces_at_word_starts
     rank, world, local = B.dist_env()
+    if rank == 0:
+        heartbeat(rank)
     dist = B.Dist(world, local, force=True)
     lib = _lib.load()
     ctx = C.c_void_p()
