@@ -224,25 +224,43 @@ def train_detail(st, sk):
         "max_live_pairs": int(st.max_live_pairs), "table_slots": int(st.table_slots),
         "sparse": {"merges": int(st.sparse_merges), "enters": int(st.sparse_enters), "exits": int(st.sparse_exits),
                    "sectors": int(st.sparse_sectors), "zone_at_entry": int(st.sparse_zone)},
+        "late": {"merges": int(st.late_merges), "launches": int(st.late_launches), "early_ends": int(st.late_exits),
+                 "bound_ends": int(st.late_bound_exits)},
         "events": None if sk is None else {
             "merges": int(sk.timed_merges), "dense_merges": int(sk.timed_merges - sk.sparse_merges),
             "dense_bytes": int(sk.dense_bytes), "ms_dense": sk.ms_dense,
             "sparse_merges": int(sk.sparse_merges), "body_bytes": int(sk.body_bytes), "zone_bytes": int(sk.zone_bytes),
             "ms_body": sk.ms_body, "ms_sparse": sk.ms_sparse, "ms_select": sk.ms_select, "ms_refresh": sk.ms_other,
-            "ms_delta": sk.ms_delta, "ms_compact": sk.ms_compact},
+            "ms_delta": sk.ms_delta, "ms_compact": sk.ms_compact,
+            "late_merges": int(sk.late_merges), "late_launches": int(sk.late_launches), "late_bytes": int(sk.late_bytes),
+            "ms_late": sk.ms_late},
     }
+
+
+def _rocprof_kernel(prefix: str):
+    """(calls, total ns) of the kernels whose name starts with `prefix` in the
+    committed rocprofv3 --stats summary of one full headline run."""
+    import csv
+    calls, ns = 0, 0.0
+    if os.path.exists(ROCPROF_EN1G):
+        for r in csv.DictReader(open(ROCPROF_EN1G)):
+            if r["Name"].startswith(prefix):
+                calls += int(r["Calls"])
+                ns += float(r["TotalDurationNs"])
+    return calls, ns
 
 
 def train_roofline(det, wall_per_run):
     """Roofline of the dominant training kernel from the HIP-event run.
 
-    Sector-sparse merges (32,384 of 32,512) spend their time in k_body; its bytes
-    are the ones it moves (candidate extents and signatures, sector symbols read
-    and rewritten, the one-workgroup zone pass) — pair-table traffic excluded as
-    in SURVEY §8(d).  The dense merges' stream kernels are reported beside it with
-    the SURVEY bytes s*(2N_i + N_{i+1}); the SURVEY formula over the whole run and
-    its wall time is given as the bandwidth a stream-per-merge loop would need to
-    match this merge rate (not credited as moved)."""
+    The late merges (~3/4 of them at 1 GiB) run in k_late, one launch per step
+    (DESIGN §2d); the earlier sparse merges in k_body, one launch per merge.
+    Each kernel's bytes are the ones it moves (candidate extents and signatures,
+    sector symbols read and rewritten, the zone pass) — pair-table traffic
+    excluded as in SURVEY §8(d).  The kernel with the larger share of the run's
+    device time is the roofline kernel; the other is reported beside it.  The
+    SURVEY formula over the whole run and its wall time is given as the bandwidth
+    a stream-per-merge loop would need to match this merge rate (not credited)."""
     ev = det["events"]
     dense = None
     if ev and ev["ms_dense"] > 0:
@@ -251,34 +269,42 @@ def train_roofline(det, wall_per_run):
                  "frac": round(a / HBM_PEAK_GBPS, 4), "algorithmic_bytes": ev["dense_bytes"],
                  "ms": round(ev["ms_dense"], 2)}
     equiv = det["stream_bytes"] / 1e9 / wall_per_run
-    roof = {"bound": "hbm", "kernel": "k_body (sector-sparse merge pass over the word lexicon, one launch per merge)",
-            "achieved": None,
-            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None, "traffic": None}
-    if ev and ev["ms_body"] > 0 and ev["sparse_merges"] > 0:
-        a = ev["body_bytes"] / 1e9 / (ev["ms_body"] / 1e3)
-        roof.update({"achieved": round(a, 1), "frac": round(a / HBM_PEAK_GBPS, 4),
-                     "algorithmic_bytes_per_launch": round(ev["body_bytes"] / ev["sparse_merges"]),
-                     "us_per_launch": round(1e3 * ev["ms_body"] / ev["sparse_merges"], 2),
-                     "launches": ev["sparse_merges"],
-                     "timing": "HIP events around every k_body launch of one extra full run of the same workload "
-                               "(events add inter-kernel gaps, so they stay out of the timed runs)",
-                     "note": "latency-bound by design: the body is one copy of every distinct word (DESIGN §2c), "
-                             "so a merge moves the few sectors holding its pair, kilobytes, not the stream; the loop "
-                             "avoids the bytes rather than streaming them"})
-    if os.path.exists(ROCPROF_EN1G) and roof.get("us_per_launch") is not None:
-        # the same kernel under rocprofv3 --kernel-trace --stats over one full run of this
-        # workload (tools/explore_1g.py en1g): its own durations, without the event gaps
-        import csv
-        calls, ns = 0, 0.0
-        for r in csv.DictReader(open(ROCPROF_EN1G)):
-            if "k_body<" in r["Name"]:
-                calls += int(r["Calls"])
-                ns += float(r["TotalDurationNs"])
+
+    def kern(name, byts, ms, launches, merges, prefix, desc):
+        if not ev or ms <= 0 or launches <= 0:
+            return None
+        a = byts / 1e9 / (ms / 1e3)
+        k = {"bound": "hbm", "kernel": desc, "achieved": round(a, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+             "frac": round(a / HBM_PEAK_GBPS, 4), "traffic": None,
+             "algorithmic_bytes_per_launch": round(byts / launches), "us_per_launch": round(1e3 * ms / launches, 2),
+             "launches": launches, "merges": merges, "ms_per_run": round(ms, 2),
+             "timing": "HIP events around every launch of one extra full run of the same workload (events add "
+                       "inter-kernel gaps, so they stay out of the timed runs)"}
+        calls, ns = _rocprof_kernel(prefix)
         if calls:
-            roof["rocprof_us_per_launch"] = round(ns / calls / 1e3, 2)
-            roof["rocprof_launches"] = calls
-            roof["rocprof_achieved_with_rocprof_time"] = round(roof["algorithmic_bytes_per_launch"] / (ns / calls), 1)
-            roof["rocprof_window"] = os.path.relpath(ROCPROF_EN1G, ROOT)
+            k["rocprof_us_per_launch"] = round(ns / calls / 1e3, 2)
+            k["rocprof_launches"] = calls
+            k["rocprof_achieved_with_rocprof_time"] = round(k["algorithmic_bytes_per_launch"] / (ns / calls), 1)
+            k["rocprof_window"] = os.path.relpath(ROCPROF_EN1G, ROOT)
+        return k
+
+    late = kern("late", ev["late_bytes"], ev["ms_late"], ev["late_launches"], ev["late_merges"], "k_late<",
+                "k_late (the late-merge loop: one 1024-thread workgroup runs a step's merges, zone in LDS, "
+                "hot-set selection; DESIGN §2d)") if ev else None
+    body = kern("body", ev["body_bytes"], ev["ms_body"], ev["sparse_merges"] - ev["late_merges"],
+                ev["sparse_merges"] - ev["late_merges"], "k_body<",
+                "k_body (sector-sparse merge pass over the word lexicon, one launch per merge)") if ev else None
+    cand = [k for k in (late, body) if k]
+    roof = max(cand, key=lambda k: k["ms_per_run"]) if cand else {
+        "bound": "hbm", "kernel": None, "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None,
+        "traffic": None}
+    roof = dict(roof)
+    roof["note"] = ("latency-bound by design: the body is one copy of every distinct word (DESIGN §2c), so a merge "
+                    "moves the few sectors holding its pair, kilobytes, not the stream; the loop avoids the bytes "
+                    "rather than streaming them")
+    other = [k for k in cand if k["kernel"] != roof.get("kernel")]
+    if other:
+        roof["other_kernel"] = other[0]
     roof["dense_stream"] = dense
     roof["dense_equivalent"] = {"gbps": round(equiv, 1), "frac": round(equiv / HBM_PEAK_GBPS, 4),
                                 "bytes": det["stream_bytes"],
@@ -286,12 +312,13 @@ def train_roofline(det, wall_per_run):
                                            "full-stream-per-merge loop would need for this merge rate"}
     if os.path.exists(PMC_FILE):
         p = json.load(open(PMC_FILE))
-        if p.get("workload") == "en1g-full-run":
+        kn = (roof.get("kernel") or "").split(" ")[0]
+        if p.get("workload") == "en1g-full-run" and p.get("kernel", "k_body") == kn:
             roof["traffic"] = round(p["hbm_bytes_per_launch"])
-            roof["traffic_unit"] = "bytes/launch (k_body)"
+            roof["traffic_unit"] = f"bytes/launch ({kn})"
             roof["traffic_over_algorithmic"] = round(p["traffic_over_algorithmic"], 4)
             roof["traffic_window"] = (f"{os.path.relpath(PMC_FILE, ROOT)}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and "
-                                      f"WRITE_SIZE passes over one full run of this workload ({p['launches']} k_body "
+                                      f"WRITE_SIZE passes over one full run of this workload ({p['launches']} {kn} "
                                       f"launches); algorithmic bytes from the same run")
             roof["traffic_calibration"] = CAL_NOTE
     return roof
