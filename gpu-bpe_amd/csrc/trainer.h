@@ -1379,7 +1379,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->rehash_on = gbpe_debug_knob("rehash", 1) != 0;
     t->delta_mt = (uint32_t)gbpe_debug_knob("delta_mt", t->delta_mt);
     t->sp_zt = (uint32_t)gbpe_debug_knob("zt", t->sp_zt);
-    t->late_on = gbpe_debug_knob("late", 1) != 0;
+    t->late_on = gbpe_debug_knob("late", 0) != 0;   // (off until it beats k_body: DESIGN §2d)
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
         t->trace = fopen(e, "w");
