@@ -37,7 +37,7 @@ static const char* const kKernelNames[] = {
 
 extern "C" {
 
-const char* gbpe_version(void) { return "gpubpe 0.3 (gfx950, abi 2)"; }
+const char* gbpe_version(void) { return "gpubpe 0.4 (gfx950, abi 3)"; }
 
 int gbpe_abi_version(void) { return GBPE_ABI_VERSION; }
 

@@ -29,20 +29,22 @@
 
 namespace {
 
-constexpr int LATE_BT = 1024;
-constexpr uint32_t LATE_HS = 4096;     // hot-set slots (LDS hash: pid -> exact count)
-constexpr uint32_t LATE_K = 1536;      // most pairs a refresh puts in the hot set
-constexpr uint32_t LATE_HP = 64;       // hot-set probes
+constexpr int LATE_BT = 1024;          // 16 waves (512 threads: no spills, but slower per merge: DESIGN §2d)
+constexpr uint32_t LATE_HS = 2048;     // hot-set slots (LDS hash: pid -> exact count), two per thread
+constexpr uint32_t LATE_K = 512;       // most pairs a refresh puts in the hot set
+constexpr uint32_t LATE_HP = 32;       // hot-set probes
 constexpr int LATE_LT = 4096;          // per-merge LDS delta table
-constexpr uint32_t LATE_CAP = 1024;    // candidate sectors per pass
+constexpr uint32_t LATE_CAP = LATE_BT; // candidate sectors per pass (one per thread)
 constexpr uint32_t LATE_NB = 8192;     // count histogram bins of the refresh
-constexpr int LATE_WJ = 6;             // window-source symbols per thread: mc <= z/3 <= 5461
 constexpr uint32_t LATE_WW = 4;        // bitmap words per thread and pass
+constexpr uint32_t LATE_FC = 2;        // candidates per thread the fast body path filters during the zone pass
 template <typename S>
 struct LateDim {
-    static constexpr int ZPT = sizeof(S) == 2 ? 16 : 8;          // zone positions per thread
+    static constexpr int ZPT = (sizeof(S) == 2 ? 16 : 8) * 1024 / LATE_BT;   // zone positions per thread
     static constexpr uint32_t ZCAP = (uint32_t)LATE_BT * ZPT;    // 16K u16 / 8K u32 symbols (32 KB)
+    static_assert(ZPT <= 32, "thread masks are 32 bits");
     static constexpr uint32_t ZV = ZCAP * sizeof(S) / 16;        // 16-byte vectors per buffer
+    static constexpr uint32_t WB = ZCAP / 8 * 3;                 // window staging: mc <= z / 3 < 3/8 ZCAP
 };
 
 // the hot-set refresh between launches (k_hot_hist, k_hot_gather)
@@ -143,12 +145,35 @@ struct LateSpill {
     uint32_t cap;
     uint32_t* pos;    // LDS: next log entry
     uint32_t* inval;  // LDS: the hot set is no longer complete
+    uint32_t* ltn;    // LDS: slots of the delta table this merge touched
 };
 __device__ void table_add(const LateSpill& sp, DevState* st, uint32_t pid, uint32_t d) {
     const uint32_t i = atomicAdd(sp.pos, 1u);
     if (i < sp.cap) sp.log[i] = make_uint2(pid, d);
     else atomicOr(&st->err, ERR_TABLE_FULL);
     *sp.inval = 1u;
+}
+
+// the per-merge delta table: LdsTab's probing, plus the list of slots a merge
+// filled, so the walk reads those instead of scanning every slot
+struct LateTab {
+    uint32_t key[LATE_LT];
+    uint32_t val[LATE_LT];
+    uint16_t list[LATE_LT];
+};
+__device__ __forceinline__ void lds_add(LateTab& t, const LateSpill& sp, DevState* st, uint32_t pid, uint32_t d) {
+    const uint32_t h = gbpe_fmix32(pid);
+#pragma unroll 1
+    for (int p = 0; p < LPROBE; ++p) {
+        const uint32_t idx = (h + (uint32_t)((p * (p + 1)) >> 1)) & (LATE_LT - 1);
+        const uint32_t k = atomicCAS(&t.key[idx], 0u, pid);
+        if (k == 0u) t.list[atomicAdd(sp.ltn, 1u)] = (uint16_t)idx;
+        if (k == 0u || k == pid) {
+            atomicAdd(&t.val[idx], d);
+            return;
+        }
+    }
+    table_add(sp, st, pid, d);
 }
 
 __device__ __forceinline__ uint32_t hot_find(const uint32_t* hk, uint32_t pid) {
@@ -186,8 +211,9 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 }
 
 // phase stamps of a -DGBPE_KTRACE build (tools/ktrace_late.py): every KT_EVERY-th
-// merge, slots 0-5 = merge start, selection done, zone reads done, zone written,
-// body done, merge closed; 6 = candidates << 16 | filtered candidates
+// merge, slots 0-5 = merge start, selection done, zone reads + candidate filter
+// done, zone written + sectors merged, deltas walked, merge closed;
+// 6 = candidates << 16 | filtered candidates
 #ifdef GBPE_KTRACE
 #define LKT(i) do { if (t == 0) kt_put(r, KT_WG - 1u, (i), wall_clock64()); } while (0)
 #define LKTV(i, v) do { if (t == 0) kt_put(r, KT_WG - 1u, (i), (v)); } while (0)
@@ -205,6 +231,21 @@ struct LateOut {
     uint32_t* stat;         // [0] launches ended by the hot-set bound, [1] ... by a spill / full hot set
 };
 
+// per-merge LDS counters, double-buffered by merge parity: merge r's are read
+// after its last barrier and zeroed during merge r + 1, so no barrier of their own
+enum : int { LC_NPASS = 0, LC_BIG, LC_LTN, LC_WMAX, LC_NCAND, LC_N };
+
+// Per merge, four workgroup barriers:
+//   selection  argmax over the hot set                                  | barrier
+//   phase 1    zone reads, masks, destroyed pairs (LDS) while the bitmap rows
+//              load; then each thread's candidates (<= LATE_FC) load their
+//              extents and signatures and the survivors join the sector list | barrier
+//   phase 2    zone writes (only where the new zone differs from what the
+//              stale buffer already holds: the agreement prefix `eq`), window
+//              pairs; one wave per listed sector                      | barrier
+//   walk       the merge's touched delta slots -> log, hot set, bound | barrier
+// A merge with more candidates (or a bitmap wider than one pass) takes the
+// batched body path after its zone writes.
 template <typename S, bool EXACT>
 __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S* __restrict__ body,
                                                    uint32_t* __restrict__ lmul, uint2* __restrict__ sec,
@@ -214,12 +255,14 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     constexpr int BT = LATE_BT;
     constexpr int ZPT = LateDim<S>::ZPT;
-    constexpr uint32_t ZV = LateDim<S>::ZV;
+    constexpr uint32_t ZV = LateDim<S>::ZV, WBN = LateDim<S>::WB;
     constexpr int NWAVE = BT / 64;
     constexpr int NW = sizeof(DevState) / 4;
+    static_assert(2 * NW <= BT && LC_N * 2 <= BT, "the prologue loads both states in one pass");
     __shared__ uint4 zb[2][ZV];                  // zone and stale buffer (ping-pong)
+    __shared__ S wb[WBN];                        // the merge's window source (stale symbols)
     __shared__ uint32_t hk[LATE_HS], hc[LATE_HS];   // hot set
-    __shared__ LdsTab<LATE_LT> lt;
+    __shared__ LateTab lt;
     __shared__ uint32_t cs[LATE_CAP];
     __shared__ uint2 ce[LATE_CAP];
     __shared__ union {
@@ -227,9 +270,11 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
         uint32_t w[NW];
     } g0, z0;
     __shared__ uint64_t s_red[NWAVE];
-    __shared__ uint32_t s_sum[NWAVE], s_tl[NWAVE], s_rm[NWAVE];
-    __shared__ uint32_t s_logpos, s_inval, s_wmax, s_n, s_err;
-    __shared__ uint64_t s_bytes;
+    __shared__ uint32_t s_sum[NWAVE], s_tl[NWAVE], s_fh[NWAVE], s_rm[NWAVE], s_cs[NWAVE];
+    __shared__ uint32_t s_pc[2][LC_N];
+    __shared__ uint32_t s_logpos, s_inval, s_gn, s_err;
+    __shared__ uint64_t s_bytes, s_tail;
+    __shared__ uint32_t s_last[5];   // the last merge's a, b, id, count, window (epilogue only: off the registers)
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
 
     // ── prologue: states, zone buffers, hot set ──
@@ -240,14 +285,23 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
         zb[1][q] = reinterpret_cast<const uint4*>(zg1)[q];
     }
     for (uint32_t i = t; i < LATE_HS; i += BT) hk[i] = 0u;
-    lds_clear(lt);
+    for (uint32_t i = t; i < (uint32_t)LATE_LT; i += BT) {
+        lt.key[i] = 0u;
+        lt.val[i] = 0u;
+    }
     const uint32_t hok = uni(hot->ok), nhot = uni(hot->nhot), tau = uni(hot->tau);
+    if (t < 2 * LC_N) s_pc[t / LC_N][t % LC_N] = 0u;
     if (t == 0) {
         s_logpos = 0u;
         s_inval = 0u;
         s_err = 0u;
-        s_wmax = 0u;
         s_bytes = 0ull;
+        s_tail = g0.d.tail_total;
+        s_last[0] = g0.d.a;
+        s_last[1] = g0.d.b;
+        s_last[2] = g0.d.nw;
+        s_last[3] = g0.d.mc;
+        s_last[4] = z0.d.m;
     }
     __syncthreads();
     if (t == 0) hot->nhot = 0u;   // (read above by every thread; the next gather appends from 0)
@@ -261,24 +315,25 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
     // loop state (every thread keeps its own copy: all updates are uniform)
     uint32_t n = uni(g0.d.n), B = uni(g0.d.B), Bp = uni(g0.d.Bp), z = uni(z0.d.n), mc_prev = uni(g0.d.mc_prev);
     uint32_t nid = uni(g0.d.next_id);
-    uint64_t tail_total = uni64(g0.d.tail_total), Wb = 0;
-    uint32_t done = 0, cur = 0, stop = 0, abrt = 0, err = 0, m_last = uni(z0.d.m);
-    uint32_t la = uni(g0.d.a), lb = uni(g0.d.b), lnw = uni(g0.d.nw), lmc = uni(g0.d.mc);
+    uint64_t Wb = 0;
+    uint32_t done = 0, cur = 0, stop = 0, abrt = 0, err = 0;
+    uint32_t eq = 0;   // the stale buffer equals the zone on [0, eq)
     const uint32_t budget = uni(g0.d.budget);
     uint32_t ended_by = 0;   // 1: hot-set bound, 2: hot set incomplete
     if (!usable || uni(s_inval) || uni(g0.d.stop) || uni(g0.d.sp_abort) || z > LateDim<S>::ZCAP) ended_by = 2;
-    const LateSpill spill{out.dlog, out.dcap, &s_logpos, &s_inval};
     uint64_t bytes = 0;
     for (uint32_t r = 0; ended_by == 0 && r < budget; ++r) {
+        const uint32_t par = r & 1u;
+        uint32_t* const pc = s_pc[par];
         LKT(0);
         // ── selection over the hot set ──
         uint64_t best = 0;
-        for (uint32_t i = t; i < LATE_HS; i += BT) {
+#pragma unroll
+        for (uint32_t j = 0; j < LATE_HS / BT; ++j) {
+            const uint32_t i = (uint32_t)t + j * BT;
             const uint32_t k = hk[i], c = hc[i];
-            if (k && (int32_t)c > 0) {
-                const uint64_t key = ((uint64_t)c << 32) | (uint32_t)~k;
-                best = key > best ? key : best;
-            }
+            const uint64_t key = ((uint64_t)c << 32) | (uint32_t)~k;
+            best = (k && (int32_t)c > 0 && key > best) ? key : best;
         }
         for (int off = 32; off > 0; off >>= 1) {
             const uint64_t o = __shfl_xor(best, off);
@@ -313,10 +368,11 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
             abrt = 1;
             break;
         }
-        if (!EXACT && (mc > (uint32_t)(LATE_WJ * BT) || (uint32_t)(n - Bp) - mc > LateDim<S>::ZCAP)) {
+        if (!EXACT && (mc > WBN || (uint32_t)(n - Bp) - mc > LateDim<S>::ZCAP)) {
             ended_by = 2;   // (the zone rule keeps both inside the LDS buffers)
             break;
         }
+        const LateSpill spill{out.dlog, out.dcap, &s_logpos, &s_inval, &pc[LC_LTN]};
         // ── commit: log, the merged pair's count to 0 (every occurrence is a site) ──
         if (t == 0) {
             out.mlog[r * 4 + 0] = a;
@@ -329,44 +385,37 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
             if (lp < out.dcap) out.dlog[lp] = make_uint2(pid, 0u - mc);
             else atomicOr(&s_err, ERR_TABLE_FULL);
         }
-        // ── body: the two bitmap rows of the first pass load during the zone pass ──
+        if (t < LC_N) s_pc[par ^ 1u][t] = 0u;   // the other parity's counters (read before this merge's first barrier)
+        // ── phase 1: the two bitmap rows load while the zone is read ──
         uint32_t bw[LATE_WW];
 #pragma unroll
         for (uint32_t q = 0; q < LATE_WW; ++q) {
             const uint32_t w = (uint32_t)t + q * BT;
             bw[q] = w < W ? bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w] : 0u;
         }
-        // ── zone pass, in LDS (zone_one's rules) ──
         S* const C = reinterpret_cast<S*>(zb[cur]);
         S* const P = reinterpret_cast<S*>(zb[cur ^ 1u]);
         const uint32_t lim = EXACT ? z : z - mc;
         const uint32_t i0 = (uint32_t)t * ZPT;
-        uint32_t wsrc[LATE_WJ];
-        if (!EXACT) {   // window source: global n - 2mc of the previous stream, read before P is rewritten
-            const uint32_t src0 = (uint32_t)(n - Bp) - 2u * mc;
+        // this thread's ZPT zone symbols, packed as loaded (positions past z are
+        // garbage: every mask below is cut to inb)
+        constexpr int XD = ZPT * (int)sizeof(S) / 4;
+        uint32_t xq[XD];
 #pragma unroll
-            for (int j = 0; j < LATE_WJ; ++j) {
-                const uint32_t u = (uint32_t)t + (uint32_t)j * BT;
-                wsrc[j] = u < mc ? (uint32_t)P[src0 + u] : 0u;
-            }
+        for (int q = 0; q < XD / 4; ++q) {
+            const uint4 v = zb[cur][t * (XD / 4) + q];
+            xq[4 * q] = v.x, xq[4 * q + 1] = v.y, xq[4 * q + 2] = v.z, xq[4 * q + 3] = v.w;
         }
-        uint32_t x[ZPT];
-        {
-            constexpr int V = ZPT * sizeof(S) / 16;
-            uint4 v[V];
-#pragma unroll
-            for (int q = 0; q < V; ++q) v[q] = zb[cur][t * V + q];
-            const S* e = reinterpret_cast<const S*>(v);
-#pragma unroll
-            for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
-        }
+        auto xat = [&](int k) -> uint32_t {
+            return sizeof(S) == 2 ? (xq[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : xq[k];
+        };
         const uint32_t xm2 = i0 >= 2 ? (uint32_t)C[i0 - 2] : 0u, xm1 = i0 >= 1 ? (uint32_t)C[i0 - 1] : 0u;
         const uint32_t nxr = i0 + ZPT < z ? (uint32_t)C[i0 + ZPT] : 0u;
         uint32_t eb = 0, ea = 0;
 #pragma unroll
         for (int k = 0; k < ZPT; ++k) {
-            eb |= (x[k] == b ? 1u : 0u) << k;
-            ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
+            eb |= (xat(k) == b ? 1u : 0u) << k;
+            ea |= ((xat(k) & TM) == a ? 1u : 0u) << k;
         }
         const uint32_t inb = lane_mask_n(i0, z, ZPT);
         const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;
@@ -403,180 +452,235 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
                 }
             }
         }
-        // block scan of the kept counts; tail survivors sum to m
+        // block scan of the kept counts; tail survivors sum to m; the first removed symbol below lim
         const uint32_t kc = __popc(keep);
         uint32_t incl = kc, tl = __popc(surv & ~below);
+        uint32_t fh = (hitm & below) ? i0 + (uint32_t)(__ffs(hitm & below) - 1) : 0xFFFFFFFFu;
         for (int off = 1; off < 64; off <<= 1) {
             const uint32_t o = __shfl_up(incl, off);
             if (lane >= off) incl += o;
         }
-        for (int off = 32; off > 0; off >>= 1) tl += __shfl_xor(tl, off);
+        for (int off = 32; off > 0; off >>= 1) {
+            tl += __shfl_xor(tl, off);
+            fh = min(fh, (uint32_t)__shfl_xor(fh, off));
+        }
         if (lane == 63) s_sum[wid] = incl;
-        if (lane == 0) s_tl[wid] = tl;
-        __syncthreads();   // every read of C and P is done
+        if (lane == 0) {
+            s_tl[wid] = tl;
+            s_fh[wid] = fh;
+        }
+        // this thread's candidates (a thread with more, or a wider bitmap: the batched path)
+        uint32_t ncnd = 0, c0 = SP_INV, c1 = SP_INV;
+#pragma unroll
+        for (uint32_t q = 0; q < LATE_WW; ++q) {
+            uint32_t c = bw[q];
+            const uint32_t w = (uint32_t)t + q * BT;
+            while (c) {
+                const uint32_t sid = w * 32u + (uint32_t)(__ffs(c) - 1);
+                c &= c - 1;
+                c0 = ncnd == 0 ? sid : c0;
+                c1 = ncnd == 1 ? sid : c1;
+                ++ncnd;
+            }
+        }
+        const bool fast = ncnd <= LATE_FC && W <= LATE_WW * (uint32_t)BT;
+        uint2 e0 = make_uint2(0u, 0u), e1 = make_uint2(0u, 0u);
+        bool k0 = false, k1 = false;
+        if (fast && ncnd) {
+            e0 = sec[c0];
+            k0 = sig_has(sig + (uint64_t)c0 * SP_SIGW, pid);
+            if (ncnd > 1) {
+                e1 = sec[c1];
+                k1 = sig_has(sig + (uint64_t)c1 * SP_SIGW, pid);
+            }
+            bytes += 16ull * ncnd;
+        }
+        // the window source (the stale buffer: global n - 2mc of the previous
+        // stream), staged before phase 2 rewrites P, while the extents load
+        if (!EXACT) {
+            const uint32_t src0 = (uint32_t)(n - Bp) - 2u * mc;
+            for (uint32_t u = t; u < mc; u += BT) wb[u] = P[src0 + u];
+        }
+        if (!fast) pc[LC_BIG] = 1u;
+        if (ncnd) atomicAdd(&pc[LC_NCAND], ncnd);
+        if (k0 || k1) {
+            uint32_t q = atomicAdd(&pc[LC_NPASS], (k0 ? 1u : 0u) + (k1 ? 1u : 0u));
+            if (k0) {
+                if (q < LATE_CAP) {
+                    cs[q] = c0;
+                    ce[q] = e0;
+                }
+                ++q;
+            }
+            if (k1 && q < LATE_CAP) {
+                cs[q] = c1;
+                ce[q] = e1;
+            }
+        }
+        __syncthreads();   // every read of C and P is done; the sector list is built
         LKT(2);
-        uint32_t pre = incl - kc, Kz = 0, m = 0;
+        uint32_t pre = incl - kc, Kz = 0, m = 0, fhb = 0xFFFFFFFFu;
 #pragma unroll
         for (int w2 = 0; w2 < NWAVE; ++w2) {
             pre += w2 < wid ? s_sum[w2] : 0u;
             Kz += s_sum[w2];
             m += s_tl[w2];
+            fhb = min(fhb, s_fh[w2]);
         }
         Kz = uni(Kz);
         m = EXACT ? 0u : uni(m);
-        // the new zone into P: kept survivors (A-sides rewritten), then the window;
-        // the A-side rewrites also land in C in place (the reference's ping buffer,
-        // the next merge's stale source)
+        const uint32_t npass = uni(pc[LC_NPASS]);
+        const bool big = uni(pc[LC_BIG]) != 0u || npass > LATE_CAP;
+        // ── phase 2: the new zone into P — kept survivors (A-sides rewritten), then
+        //    the window — writing only what P does not already hold; the A-side
+        //    rewrites also land in C in place (the next merge's stale source) ──
+        uint32_t lastv = 0;
 #pragma unroll
         for (int k = 0; k < ZPT; ++k) {
             const bool rw = (rwm >> k) & 1u;
-            const uint32_t v = rw ? (nw | (x[k] & WS)) : x[k];
-            if ((keep >> k) & 1u) P[pre + (uint32_t)__popc(keep & ((1u << k) - 1u))] = (S)v;
+            const uint32_t v = rw ? (nw | (xat(k) & WS)) : xat(k);
+            if ((keep >> k) & 1u) {
+                const uint32_t d = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
+                if (rw || d >= eq || d != i0 + (uint32_t)k) P[d] = (S)v;
+                lastv = v;
+            }
             if (rw) C[i0 + k] = (S)v;
         }
-        if (!EXACT) {
-#pragma unroll
-            for (int j = 0; j < LATE_WJ; ++j) {
-                const uint32_t u = (uint32_t)t + (uint32_t)j * BT;
-                if (u < mc && u >= mc - m) P[Kz + (u - (mc - m))] = (S)wsrc[j];
+        if (!EXACT && m) {
+            const uint32_t w0 = mc - m;
+            for (uint32_t j = t; j < m; j += BT) {   // the window and its re-added pairs
+                const uint32_t x1 = wb[w0 + j];
+                P[Kz + j] = (S)x1;
+                const uint32_t x0 = j ? (uint32_t)wb[w0 + j - 1] : 0u;
+                if (j && !(x1 & WS) && (x0 & TM) && (x1 & TM)) lds_add(lt, spill, st, ((x0 & TM) << 16) | (x1 & TM), 1u);
+            }
+            if (kc && pre + kc == Kz) {   // the last kept symbol and the window's first
+                const uint32_t x1 = wb[w0];
+                if (!(x1 & WS) && (lastv & TM) && (x1 & TM)) lds_add(lt, spill, st, ((lastv & TM) << 16) | (x1 & TM), 1u);
             }
         }
-        // the candidate list of the first body pass: a block scan of the word popcounts
-        uint32_t pc = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < LATE_WW; ++q) pc += __popc(bw[q]);
-        uint32_t cincl = pc;
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t o = __shfl_up(cincl, off);
-            if (lane >= off) cincl += o;
-        }
-        __syncthreads();   // P written (window pairs read it), s_sum free
-        if (lane == 63) s_sum[wid] = cincl;
-        if (!EXACT)
-            for (uint32_t j = t; j < m; j += BT) {   // the window's re-added pairs
-                const uint32_t x1 = P[Kz + j];
-                const uint32_t x0 = j ? (uint32_t)P[Kz + j - 1] : (Kz ? (uint32_t)P[Kz - 1] : 0u);
-                if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) lds_add(lt, spill, st, ((x0 & TM) << 16) | (x1 & TM), 1u);
-            }
         bytes += (t == 0) ? (uint64_t)sizeof(S) * ((uint64_t)z + (EXACT ? 0u : mc) + Kz + m) : 0ull;
-        __syncthreads();
-        uint32_t cpre = cincl - pc, ncand = 0;
-#pragma unroll
-        for (int w2 = 0; w2 < NWAVE; ++w2) {
-            cpre += w2 < wid ? s_sum[w2] : 0u;
-            ncand += s_sum[w2];
-        }
-        ncand = uni(ncand);
-        LKT(3);
-        [[maybe_unused]] uint32_t nfilt = 0;
-        // ── body passes: candidates in batches of LATE_CAP (bitmap words beyond the
-        //    first 4 x 1024 in further passes) ──
+        // ── body: one wave per listed sector; the next one's first pass loads
+        //    while this one merges ──
         uint32_t removed = 0;
-        uint32_t wbase = 0;
-        for (;;) {
-            for (uint32_t base = 0; base < ncand; base += LATE_CAP) {
-                {   // this thread's candidates with list positions in [base, base + CAP)
-                    uint32_t pos = cpre;
+        auto sectors = [&](uint32_t nc) {
+            uint32_t nf[5], nfm[4];
+            if ((uint32_t)wid < nc)
+                sector_first<S>(body + ce[wid].x, lmul ? lmul + ce[wid].x : nullptr, ce[wid].y, nf, nfm);
+            for (uint32_t j = wid; j < nc; j += NWAVE) {
+                const uint32_t sct = cs[j];
+                const uint2 e = ce[j];
+                uint32_t cf[5], cfm[4];
 #pragma unroll
-                    for (uint32_t q = 0; q < LATE_WW; ++q) {
-                        uint32_t c = bw[q];
-                        const uint32_t w = wbase + (uint32_t)t + q * BT;
-                        while (c) {
-                            const int bit = __ffs(c) - 1;
-                            c &= c - 1;
-                            if (pos >= base && pos < base + LATE_CAP) cs[pos - base] = w * 32u + (uint32_t)bit;
-                            ++pos;
+                for (int k = 0; k < 5; ++k) cf[k] = nf[k];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cfm[k] = nfm[k];
+                if (j + NWAVE < nc) {
+                    const uint2 en = ce[j + NWAVE];
+                    sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
+                }
+                uint32_t outc = 0;
+                const uint32_t rr = body_sector<S, LATE_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt,
+                                                             spill, st, sig + (uint64_t)sct * SP_SIGW, outc, cf, cfm);
+                if (lane == 0) bytes += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (rr ? outc : 0u));
+                if (rr) {
+                    removed += rr;
+                    if (lane == 0) {
+                        sec[sct].y = outc;
+                        atomicOr(&bits[(uint64_t)nw * W + (sct >> 5)], 1u << (sct & 31u));
+                    }
+                }
+            }
+        };
+        [[maybe_unused]] uint32_t nfilt = npass;
+        if (!big) {
+            sectors(npass);
+        } else {
+            // batched: every candidate of the bitmap, LATE_CAP at a time, LATE_WW x BT words per pass
+            nfilt = 0;
+            for (uint32_t wbase = 0;;) {
+                uint32_t pcn = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < LATE_WW; ++q) pcn += __popc(bw[q]);
+                uint32_t cincl = pcn;
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t o = __shfl_up(cincl, off);
+                    if (lane >= off) cincl += o;
+                }
+                if (lane == 63) s_cs[wid] = cincl;
+                __syncthreads();   // (also: the fast list is no longer read)
+                uint32_t cpre = cincl - pcn, ncand = 0;
+#pragma unroll
+                for (int w2 = 0; w2 < NWAVE; ++w2) {
+                    cpre += w2 < wid ? s_cs[w2] : 0u;
+                    ncand += s_cs[w2];
+                }
+                ncand = uni(ncand);
+                for (uint32_t base = 0; base < ncand; base += LATE_CAP) {
+                    {   // this thread's candidates with list positions in [base, base + CAP)
+                        uint32_t pos = cpre;
+#pragma unroll
+                        for (uint32_t q = 0; q < LATE_WW; ++q) {
+                            uint32_t c = bw[q];
+                            const uint32_t w = wbase + (uint32_t)t + q * BT;
+                            while (c) {
+                                const int bit = __ffs(c) - 1;
+                                c &= c - 1;
+                                if (pos >= base && pos < base + LATE_CAP) cs[pos - base] = w * 32u + (uint32_t)bit;
+                                ++pos;
+                            }
                         }
                     }
-                }
-                if (t == 0) s_n = 0u;
-                __syncthreads();
-                const uint32_t nb = ncand - base < LATE_CAP ? ncand - base : LATE_CAP;
-                // signature filter (extents load alongside)
-                uint32_t fs = SP_INV;
-                uint2 fe = make_uint2(0u, 0u);
-                bool fk = false;
-                if ((uint32_t)t < nb) {
-                    fs = cs[t];
-                    fe = sec[fs];
-                    fk = sig_has(sig + (uint64_t)fs * SP_SIGW, pid);
-                    bytes += 16ull;
-                }
-                __syncthreads();   // the list is read before it is rewritten
-                if (fk) {
-                    const uint32_t qq = atomicAdd(&s_n, 1u);
-                    cs[qq] = fs;
-                    ce[qq] = fe;
-                }
-                __syncthreads();
-                const uint32_t nc = uni(s_n);
-                nfilt += nc;
-                // one wave per sector; the next one's first pass loads while this one merges
-                uint32_t nf[5], nfm[4];
-                if ((uint32_t)wid < nc)
-                    sector_first<S>(body + ce[wid].x, lmul ? lmul + ce[wid].x : nullptr, ce[wid].y, nf, nfm);
-                for (uint32_t j = wid; j < nc; j += NWAVE) {
-                    const uint32_t sct = cs[j];
-                    const uint2 e = ce[j];
-                    uint32_t cf[5], cfm[4];
-#pragma unroll
-                    for (int k = 0; k < 5; ++k) cf[k] = nf[k];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) cfm[k] = nfm[k];
-                    if (j + NWAVE < nc) {
-                        const uint2 en = ce[j + NWAVE];
-                        sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
+                    if (t == 0) s_gn = 0u;
+                    __syncthreads();
+                    const uint32_t nb = ncand - base < LATE_CAP ? ncand - base : LATE_CAP;
+                    uint32_t fs = SP_INV;
+                    uint2 fe = make_uint2(0u, 0u);
+                    bool fk = false;
+                    if ((uint32_t)t < nb) {
+                        fs = cs[t];
+                        fe = sec[fs];
+                        fk = sig_has(sig + (uint64_t)fs * SP_SIGW, pid);
+                        bytes += 16ull;
                     }
-                    uint32_t outc = 0;
-                    const uint32_t rr = body_sector<S, LATE_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt,
-                                                                 spill, st, sig + (uint64_t)sct * SP_SIGW, outc, cf, cfm);
-                    if (lane == 0) bytes += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (rr ? outc : 0u));
-                    if (rr) {
-                        removed += rr;
-                        if (lane == 0) {
-                            sec[sct].y = outc;
-                            atomicOr(&bits[(uint64_t)nw * W + (sct >> 5)], 1u << (sct & 31u));
-                        }
+                    __syncthreads();   // the list is read before it is rewritten
+                    if (fk) {
+                        const uint32_t qq = atomicAdd(&s_gn, 1u);
+                        cs[qq] = fs;
+                        ce[qq] = fe;
                     }
+                    __syncthreads();
+                    const uint32_t nc = uni(s_gn);
+                    nfilt += nc;
+                    sectors(nc);
+                    __syncthreads();   // the list is free for the next batch
                 }
-                __syncthreads();   // the list is free for the next batch
-            }
-            wbase += LATE_WW * BT;
-            if (wbase >= W) break;   // (block-uniform)
-            // further bitmap words (stores of more than 128K sectors)
-            pc = 0;
+                wbase += LATE_WW * BT;
+                if (wbase >= W) break;   // (block-uniform)
 #pragma unroll
-            for (uint32_t q = 0; q < LATE_WW; ++q) {
-                const uint32_t w = wbase + (uint32_t)t + q * BT;
-                bw[q] = w < W ? bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w] : 0u;
-                pc += __popc(bw[q]);
+                for (uint32_t q = 0; q < LATE_WW; ++q) {
+                    const uint32_t w = wbase + (uint32_t)t + q * BT;
+                    bw[q] = w < W ? bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w] : 0u;
+                }
             }
-            cincl = pc;
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t o = __shfl_up(cincl, off);
-                if (lane >= off) cincl += o;
-            }
-            if (lane == 63) s_sum[wid] = cincl;
-            __syncthreads();
-            cpre = cincl - pc;
-            ncand = 0;
-#pragma unroll
-            for (int w2 = 0; w2 < NWAVE; ++w2) {
-                cpre += w2 < wid ? s_sum[w2] : 0u;
-                ncand += s_sum[w2];
-            }
-            ncand = uni(ncand);
-            __syncthreads();
         }
         if (lane == 0) s_rm[wid] = removed;   // (per lane: body_sector returns the wave's total)
-        LKT(4);
-        LKTV(6, ((uint64_t)ncand << 16) | nfilt);
+        __syncthreads();   // every delta of the merge is in the table
+        LKT(3);
+        LKTV(6, ((uint64_t)pc[LC_NCAND] << 16) | nfilt);
         // ── the merge's deltas: log, hot set, bound ──
+        const uint32_t nl = uni(pc[LC_LTN]);
         uint32_t wmax = 0;
-        for (uint32_t i = t; i < (uint32_t)LATE_LT; i += BT) {
-            const uint32_t k = lt.key[i], d = lt.val[i];
-            lt.key[i] = 0u;
-            lt.val[i] = 0u;
+        for (uint32_t i1 = 0; i1 < nl; i1 += BT) {   // (a uniform trip count: the ballot below)
+            const uint32_t i = i1 + (uint32_t)t;
+            uint32_t k = 0, d = 0;
+            if (i < nl) {
+                const uint32_t s = lt.list[i];
+                k = lt.key[s];
+                d = lt.val[s];
+                lt.key[s] = 0u;
+                lt.val[s] = 0u;
+            }
             const bool live = k && d;
             const unsigned long long bal = __ballot(live);
             uint32_t base = 0;
@@ -597,9 +701,9 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
             }
         }
         for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor(wmax, off));
-        if (lane == 0 && wmax) atomicMax(&s_wmax, wmax);
-        if (t == 0) lt.ovf = 0u;
-        __syncthreads();
+        if (lane == 0 && wmax) atomicMax(&pc[LC_WMAX], wmax);
+        __syncthreads();   // hot set updated; s_wmax, s_rm, s_inval final
+        LKT(4);
         uint32_t body_rm = 0;
 #pragma unroll
         for (int w2 = 0; w2 < NWAVE; ++w2) body_rm += s_rm[w2];
@@ -607,23 +711,26 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
         // ── close the merge (k_refresh's finish-2 bookkeeping) ──
         const uint32_t n1 = n - mc, B1 = B - body_rm, z1 = Kz + m;
         if (z1 != n1 - B1) err |= ERR_COUNT_MISMATCH;
-        Wb += uni(s_wmax);
+        Wb += uni(pc[LC_WMAX]);
+        eq = min(uni(fhb), lim);   // the zone just read (now the stale buffer) equals the new one below its first removed symbol
         Bp = B;
         B = B1;
         n = n1;
         z = z1;
         mc_prev = mc;
-        tail_total += m;
-        m_last = m;
+        if (t == 0) {
+            s_tail += m;
+            s_last[0] = a;
+            s_last[1] = b;
+            s_last[2] = nw;
+            s_last[3] = mc;
+            s_last[4] = m;
+        }
         ++nid;
-        la = a, lb = b, lnw = nw, lmc = mc;
         cur ^= 1u;
         done = r + 1;
-        const bool inval = uni(s_inval) != 0u;
-        __syncthreads();   // s_wmax, s_rm, s_inval read by all
         LKT(5);
-        if (t == 0) s_wmax = 0u;
-        if (inval) {
+        if (uni(s_inval)) {
             ended_by = 2;
             break;
         }
@@ -646,19 +753,19 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
         st->mc_prev = mc_prev;
         st->next_id = nid;
         st->epoch = g0.d.epoch + done;
-        st->tail_total = tail_total;
+        st->tail_total = s_tail;
         st->merges_done = done;
         st->sel_round = done;
         st->zlast = z;
-        st->a = la;
-        st->b = lb;
-        st->nw = lnw;
-        st->mc = lmc;
+        st->a = s_last[0];
+        st->b = s_last[1];
+        st->nw = s_last[2];
+        st->mc = s_last[3];
         st->new_n = n;
         if (stop) st->stop = 1u;
         if (abrt) st->sp_abort = 1u;
         zst->n = z;
-        zst->m = m_last;
+        zst->m = s_last[4];
         zst->merges_done = done;
         zst->valid_total = 0u;
         *out.dlog_n = s_logpos < out.dcap ? s_logpos : out.dcap;

@@ -1685,9 +1685,9 @@ __device__ __forceinline__ void sector_first(const S* __restrict__ p, const uint
 // survivors compacted to the sector's front).  In the lexicon body (mp != null)
 // every symbol carries its word's multiplicity, which weights its count deltas
 // and moves with it.  Returns the B-sides removed (weighted: stream symbols).
-template <typename S, int NT = LTAB_T, typename TB = Table>
+template <typename S, int NT = LTAB_T, typename TB = Table, typename LT = LdsTab<NT>>
 __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, uint32_t cnt, uint32_t a, uint32_t b,
-                                uint32_t nw, LdsTab<NT>& lt, const TB& tb, DevState* st, uint32_t* __restrict__ sig,
+                                uint32_t nw, LT& lt, const TB& tb, DevState* st, uint32_t* __restrict__ sig,
                                 uint32_t& out_cnt, const uint32_t (&first)[5], const uint32_t (&firstm)[4]) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     const int lane = threadIdx.x & 63;

@@ -125,15 +125,31 @@ int ls_build(gbpe_lexshard* ls, uint64_t zone_target) {
 }
 
 // the hand-over's trainer (gbpe_trainer_create_from_lexicon), from device buffers
+// GBPE_DEBUG=rtime=1: the hand-over root's phases to stderr (stream-synchronised wall times)
+struct RootTimer {
+    bool on;
+    hipStream_t s;
+    std::chrono::steady_clock::time_point t0;
+    RootTimer(hipStream_t s_) : on(gbpe_debug_knob("rtime", 0) != 0), s(s_), t0(std::chrono::steady_clock::now()) {}
+    void mark(const char* what) {
+        if (!on) return;
+        (void)hipStreamSynchronize(s);
+        const auto t1 = std::chrono::steady_clock::now();
+        fprintf(stderr, "[gbpe root] %-10s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+        t0 = t1;
+    }
+};
+
 template <typename S>
 int lex_root_build(gbpe_trainer* t, const S* store, const uint32_t* mul, uint64_t T, const S* zone, uint64_t z,
-                   uint64_t body_len, uint32_t* d_map, uint64_t* n_map) {
+                   uint64_t body_len, uint32_t* d_map, uint64_t* n_map, RootTimer& rt) {
     gbpe_ctx* ctx = t->ctx;
     hipStream_t s = ctx->stream;
     // weighted analysis of the concatenated stores: one global uid per distinct word
     LxPlan lp;
     int rc = lx_analyze<S>(t, store, (uint32_t)T, false, lp, mul);
     if (rc != GBPE_OK) return rc;
+    rt.mark("analyze");
     if (T && !lp.ok)
         return gbpe_set_error(ctx, GBPE_E_INTERNAL, "lexicon hand-over: global word table full or a 64-bit word-hash "
                                                     "collision");
@@ -157,6 +173,7 @@ int lex_root_build(gbpe_trainer* t, const S* store, const uint32_t* mul, uint64_
     if (rc == GBPE_OK && !lp.ok) rc = gbpe_set_error(ctx, GBPE_E_INTERNAL, "lexicon hand-over: store capacity");
     if (rc != GBPE_OK) return rc;
     ++t->lx_builds;
+    rt.mark("commit");
     // the zone; its stale source is all 0 (no merge has run: both ping-pong buffers
     // start zeroed, as WebGPU zero-initialises buffers)
     rc = sp_alloc_zone(t, z, 0);
@@ -186,6 +203,7 @@ int lex_root_build(gbpe_trainer* t, const S* store, const uint32_t* mul, uint64_
                        (S*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr);
     hipLaunchKernelGGL(k_topcount, dim3(1), dim3(1024), 0, s, t->tb, t->d_u32);
     GBPE_LAUNCH_CHECK(ctx);
+    rt.mark("zone+count");
     uint32_t hs[2] = {0, 0};
     TR_HIP(t, hipMemcpyAsync(hs, t->d_u32, 8, hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipStreamSynchronize(s));
@@ -198,6 +216,7 @@ int lex_root_build(gbpe_trainer* t, const S* store, const uint32_t* mul, uint64_
                        (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part);
     GBPE_LAUNCH_CHECK(ctx);
     TR_HIP(t, hipStreamSynchronize(s));
+    rt.mark("states");
     t->sp = true;
     t->zcur = 0;
     t->sp_age = t->sp_bits_age = 0;
@@ -361,6 +380,7 @@ extern "C" int gbpe_trainer_create_from_lexicon(gbpe_ctx* ctx, const void* store
     t->lex_only = true;
     t->n0 = t->n = body_len + zone_len;
     hipStream_t s = ctx->stream;
+    RootTimer rt(s);
     auto fail = [&](int code) {
         gbpe_trainer_destroy(t);
         return code;
@@ -404,6 +424,7 @@ extern "C" int gbpe_trainer_create_from_lexicon(gbpe_ctx* ctx, const void* store
         d_mul = (const uint32_t*)(p + store_len * bps);
         d_zone = p + store_len * (bps + 4);
     }
+    rt.mark("upload");
     uint32_t* d_map = nullptr;
     if (hipMalloc(&d_map, (store_len / 2 + 2) * 4) != hipSuccess) {
         hipFree(tmp);
@@ -411,9 +432,9 @@ extern "C" int gbpe_trainer_create_from_lexicon(gbpe_ctx* ctx, const void* store
     }
     uint64_t nm = 0;
     rc = t->u16 ? lex_root_build<uint16_t>(t, (const uint16_t*)d_store, d_mul, store_len, (const uint16_t*)d_zone,
-                                           zone_len, body_len, d_map, &nm)
+                                           zone_len, body_len, d_map, &nm, rt)
                 : lex_root_build<uint32_t>(t, (const uint32_t*)d_store, d_mul, store_len, (const uint32_t*)d_zone,
-                                           zone_len, body_len, d_map, &nm);
+                                           zone_len, body_len, d_map, &nm, rt);
     if (rc == GBPE_OK && map_out) {
         if (map_cap < nm) rc = gbpe_set_error(ctx, GBPE_E_CAPACITY, "lexicon hand-over: map needs %llu entries",
                                               (unsigned long long)nm);
@@ -422,6 +443,7 @@ extern "C" int gbpe_trainer_create_from_lexicon(gbpe_ctx* ctx, const void* store
             rc = gbpe_set_error(ctx, GBPE_E_DEVICE, "lexicon hand-over: map copy failed");
     }
     hipStreamSynchronize(s);
+    rt.mark("map");
     hipFree(d_map);
     hipFree(tmp);
     *n_map = nm;

@@ -3,10 +3,11 @@
 medians over merge buckets.
 
   sel     selection over the hot set (merge start -> selection done)
-  zone    selection -> every zone read done (bitmap rows in flight meanwhile)
-  zwrite  zone writes + window pairs + candidate scan
-  body    candidates, signature filter, sector merges
-  walk    deltas -> log, hot set, bound; merge closed
+  p1      zone reads and destroyed pairs; bitmap rows, candidates' extents and
+          signatures in flight meanwhile; the sector list
+  p2      zone writes, window pairs, sector merges
+  walk    touched delta slots -> log, hot set, bound
+  close   merge bookkeeping
   total   merge start -> merge closed;  ncand / nfilt  candidates, after the filter
 
 usage: python tools/ktrace_late.py <dump file>
@@ -34,7 +35,7 @@ def main():
         print("no k_late stamps")
         return
     a = np.array(rows)
-    names = ["sel", "zone", "zwrite", "body", "walk", "total", "ncand", "nfilt"]
+    names = ["sel", "p1", "p2", "walk", "close", "total", "ncand", "nfilt"]
     edges = [int(e) for e in os.environ.get("EDGES", "0,2000,4000,8000,12000,16000,24000,32000,50000,66000").split(",")]
     print(f"{'merges':<13}{'n':>5}" + "".join(f"{k:>9}" for k in names))
     for lo, hi in zip(edges[:-1], edges[1:]):
