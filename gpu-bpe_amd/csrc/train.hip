@@ -349,6 +349,13 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
                                                            : (uint32_t)std::min<uint64_t>(1024, gbpe_div_up(zn / 5 + 1, 2048));
         sg.zcompact = (uint32_t)zt + ((t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u
                                       : grid_persistent(t->ctx, gbpe_div_up(zn / 2 + 1, TPB * 16), 1));
+        // the 1024-thread forms hold one workgroup per CU (their LDS): the zone's (or
+        // the window copy's) workgroups beside the body's, past the CU count, wait for
+        // a CU to drain (C5 merges 512-8K: the last one started 14-19 us late) — so
+        // the body takes the CUs the others leave
+        const uint32_t extra = sg.zone1 ? sg.zone1 : sg.copy;
+        if (sg.bt >= 1023 && t->body_fit && extra && sg.body + extra > t->body_cap && 2 * extra <= t->body_cap)
+            body_grid(t, sg.bt, &sg.body, &sg.wpg, t->body_cap - extra);
         // late steps (a zone of <= 16K symbols): a smaller k_refresh grid —
         // a late merge dirties a few blocks, and fewer workgroups dispatch and drain
         // sooner.  The partial maxima the next k_body reads are laid out per k_refresh

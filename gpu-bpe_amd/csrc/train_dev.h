@@ -2363,7 +2363,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
                                               Table dtb, SelShard sh, uint32_t* __restrict__ lmul,
                                               ZSegState* __restrict__ zg = nullptr) {
-    constexpr int KB_LT = ZSEG ? 4096 : LTAB_T;
+    constexpr int KB_LT = ZSEG ? 4096 : LTAB_T;   // (4096 for every 1024-thread form: no change on C5 / 1 GiB / C2, r4)
     __shared__ LdsTab<KB_LT> lt;
     __shared__ BodyLds<S, BT> u;
     __shared__ uint32_t s_ntok, s_n, s_any, s_rm[BT / 64];

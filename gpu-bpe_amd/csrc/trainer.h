@@ -116,6 +116,7 @@ struct gbpe_trainer {
     uint32_t refresh_late = 64;  // k_refresh grid of late steps (0 = unchanged)
     bool rehash_on = true;       // GBPE_REHASH: grow the table inside the sparse loop (0: exit, grow, recount)
     uint32_t body_cap = 256;     // GBPE_BODY_WG: most k_body workgroups (default one per CU)
+    bool body_fit = true;        // the body's workgroups leave the zone's their CUs (GBPE_DEBUG bodyfit=0: off)
     uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
     uint32_t* h_clog = nullptr;
     FILE* trace = nullptr;
@@ -356,11 +357,11 @@ uint32_t zone_max(int bt) {
 }
 // k_body grid: bitmap words per workgroup (>= the measured best 16 / 32 at C2 size),
 // at most `cap` workgroups (GBPE_BODY_WG; default 4 per CU)
-inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* wpg) {
+inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* wpg, uint32_t cap = 0) {
     const uint32_t W = (uint32_t)gbpe_div_up(t->nsec, 32);
     const uint32_t minw = bt == 1024 ? 32u : 16u;
     uint32_t g = (uint32_t)gbpe_div_up(W, minw);
-    if (g > t->body_cap) g = t->body_cap;
+    if (g > (cap ? cap : t->body_cap)) g = cap ? cap : t->body_cap;
     if (g == 0) g = 1;
     *wpg = (uint32_t)gbpe_div_up(W, g);
     if (*wpg == 0) *wpg = 1;
@@ -1376,6 +1377,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     // test overrides (GBPE_DEBUG): the lexicon off / its build check, the
     // in-loop table growth off, the multi-tile k_delta threshold, the zone target
     t->lex_on = gbpe_debug_knob("lexicon", 1) != 0;
+    t->body_fit = gbpe_debug_knob("bodyfit", 1) != 0;
     t->rehash_on = gbpe_debug_knob("rehash", 1) != 0;
     t->delta_mt = (uint32_t)gbpe_debug_knob("delta_mt", t->delta_mt);
     t->sp_zt = (uint32_t)gbpe_debug_knob("zt", t->sp_zt);

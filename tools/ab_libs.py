@@ -48,10 +48,13 @@ for name in sys.argv[4:]:
         _lib.check(lib.gbpe_trainer_create(ctx, d, len(data), None, 1, C.byref(opts), C.byref(tr)), ctx, "create")
         out = (C.c_uint32 * 512)()
         merges = []
+        t4k = None
         while True:
             nd, es = C.c_uint32(), C.c_uint32()
             _lib.check(lib.gbpe_trainer_step(tr, 128, out, C.byref(nd), C.byref(es)), ctx, "step")
             merges += list(out[: 4 * nd.value])
+            if t4k is None and len(merges) >= 4 * 4096:
+                t4k = time.perf_counter()
             if nd.value == 0 or es.value:
                 break
         t1 = time.perf_counter()
@@ -61,7 +64,8 @@ for name in sys.argv[4:]:
         m = np.array(merges, dtype=np.uint32).reshape(-1, 4)
         eq = m.shape == fx.shape and bool((m == fx).all())
         if rep:
-            print(json.dumps({"name": name, "s": round(t1 - t0, 4), "merges": int(m.shape[0]), "equal": eq,
+            print(json.dumps({"name": name, "s": round(t1 - t0, 4), "s_first4k": round((t4k or t1) - t0, 4),
+                              "merges": int(m.shape[0]), "equal": eq,
                               "late": [int(st.late_merges), int(st.late_launches), int(st.late_exits),
                                        int(st.late_bound_exits)], "sparse_exits": int(st.sparse_exits)}), flush=True)
         if not eq:

@@ -35,7 +35,7 @@ import numpy as np  # noqa: E402
 import bench as B  # noqa: E402
 
 SHARD = int(os.environ.get("C4_SHARD", str(1 << 30)))
-K = int(os.environ.get("C4_K", "3"))
+K = int(os.environ.get("C4_K", "6"))
 WS = 0x10000
 
 
@@ -109,7 +109,8 @@ def main():
     res = {"shards": world, "shard_bytes": SHARD, "merges": len(merges), "seconds_train": round(t2 - t1, 2),
            "stream_symbols": int(tr.shapes[:, 5].sum()), "zones": tr.shapes[:, 4].tolist(),
            "merges_sha256": hashlib.sha256(np.ascontiguousarray(np.array(merges, np.uint32), "<u4").tobytes()).hexdigest(),
-           "timing": {k: round(float(v), 3) for k, v in tr.timing.items()}}
+           "store_symbols": int(tr.shapes[:, 0].sum()), "store_entries": int(tr.shapes[:, 1].sum()),
+           "timing_rank%d" % rank: {k: round(float(v), 3) for k, v in tr.timing.items()}}
     fin = tr.final_stream()   # root: the final stream (host u32), rebuilt from every rank's occurrence list
     lib.gbpe_device_free(ctx, d)
     if rank == tr.root:
@@ -157,6 +158,8 @@ def main():
     if rank == 0:
         merged = dict(out[0])
         merged.update({k: v for k, v in out[world - 1].items() if k not in merged})
+        merged["timing_max_over_ranks"] = {k: max(o["timing_rank%d" % q].get(k, 0.0) for q, o in enumerate(out))
+                                           for k in out[world - 1]["timing_rank%d" % (world - 1)]}
         print(json.dumps(merged), flush=True)
     lib.gbpe_ctx_destroy(ctx)
 
