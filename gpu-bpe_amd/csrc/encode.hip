@@ -175,17 +175,11 @@ __device__ __forceinline__ void vec_put(uint4& a, uint32_t j, uint32_t tok) {
 // wait: 4.84 vs 4.29 ms on C3).  Input arrives a 64-byte line per refill: with
 // ~65K lanes per XCD walking, 16-byte refills were evicted from the 4 MB L2
 // between uses (5.33 vs 4.84 ms).
-//
-// T2 (GBPE_DEBUG walk=6, round 4): a token start reads the record of its first
-// two bytes' state from a 65,536-entry table (t2[b0 << 8 | b1], the packed
-// record of the double-array state base(root child b0) + b1, or empty) — one L2
-// load that does not wait for the LDS root lookup.
-template <typename T, bool T2>
+template <typename T>
 __global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v5(const uint8_t* __restrict__ in, uint64_t n, uint32_t cs,
                                                            const uint2* __restrict__ rec, uint32_t nrec,
                                                            uint32_t root_base, T* __restrict__ scratch,
-                                                           uint32_t* __restrict__ counts, uint64_t nchunks,
-                                                           const uint2* __restrict__ t2) {
+                                                           uint32_t* __restrict__ counts, uint64_t nchunks) {
     constexpr uint32_t PER = 16 / sizeof(T);
     __shared__ uint2 lut[256];
     {
@@ -222,12 +216,6 @@ __global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v5(const uint8_t* __rest
     while (pos < ce) {
         if (!walking) {   // a token start: LDS only
             first = byte_at(pos);
-            uint32_t b1 = 0;
-            uint2 r2 = make_uint2(0x3FFFFFu, 0u);
-            if (T2 && pos + 1 < ce) {
-                b1 = byte_at(pos + 1);
-                r2 = t2[(first << 8) | b1];
-            }
             const uint2 e = lut[first];
             const uint32_t tid = rec_tid(e);
             if (rec_check(e) != 0u || rec_base(e) == 0u || pos + 1 >= ce) {
@@ -242,28 +230,6 @@ __global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v5(const uint8_t* __rest
             lmt = tid;
             lmp = pos + 1;
             wp = pos + 1;
-            if (T2) {   // the second byte's transition, from the table
-                bool end = true;
-                if (rec_check(r2) != 0x3FFFFFu) {
-                    st = base + b1;
-                    base = rec_base(r2);
-                    wp = pos + 2;
-                    const uint32_t tid2 = rec_tid(r2);
-                    if (tid2 != TID_NONE) {
-                        lmt = tid2;
-                        lmp = wp;
-                    }
-                    end = base == 0u || wp >= ce;
-                }
-                if (end) {
-                    const bool hit = lmt != TID_NONE;
-                    emit(hit ? lmt : first);
-                    pos = hit ? lmp : pos + 1;
-                } else {
-                    walking = true;
-                }
-                continue;
-            }
             walking = true;
         }
         // one trie transition: the trip's L2 load
@@ -347,7 +313,6 @@ struct gbpe_trie {
     gbpe_ctx* ctx = nullptr;
     uint4* rec = nullptr;      // double-array records {check, base, tokenId, 0}
     uint2* rec2 = nullptr;     // packed 8-byte records (pack_rec); null when ids / states do not fit
-    uint2* t2 = nullptr;       // two-byte start table (k_trie_walk_v5<T, true>), with rec2
     uint32_t root_base = 0;    // base of the root state
     uint32_t nrec = 0;
     uint4* root = nullptr;     // 256 root transitions {state, base, tokenId, present}
@@ -454,19 +419,6 @@ extern "C" int gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n
         }
         e = hipMalloc(&tr->rec2, r2.size() * sizeof(uint2));
         if (e == hipSuccess) e = hipMemcpy(tr->rec2, r2.data(), r2.size() * sizeof(uint2), hipMemcpyHostToDevice);
-        // the two-byte start table: the packed record of every depth-2 state
-        std::vector<uint2> t2(65536, make_uint2(0x3FFFFFu, 0u));
-        for (uint32_t c0 = 0; c0 < 256; ++c0) {
-            if (!root[c0].w) continue;
-            const uint32_t s1 = root[c0].x, b1 = rec[s1].y;
-            if (!b1) continue;
-            for (uint32_t c1 = 0; c1 < 256; ++c1) {
-                const uint64_t s2 = (uint64_t)b1 + c1;
-                if (s2 < rec.size() && rec[s2].x == s1) t2[(c0 << 8) | c1] = r2[s2];
-            }
-        }
-        if (e == hipSuccess) e = hipMalloc(&tr->t2, t2.size() * sizeof(uint2));
-        if (e == hipSuccess) e = hipMemcpy(tr->t2, t2.data(), t2.size() * sizeof(uint2), hipMemcpyHostToDevice);
     }
     if (e != hipSuccess) {
         gbpe_trie_free(tr);
@@ -488,7 +440,6 @@ extern "C" void gbpe_trie_free(gbpe_trie* tr) {
     if (!tr) return;
     hipFree(tr->rec);
     hipFree(tr->rec2);
-    hipFree(tr->t2);
     hipFree(tr->root);
     delete tr;
 }
@@ -539,19 +490,12 @@ int encode_device_impl(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* d_in, uint64
     // plain per-token walk over 16-byte records
     const bool packed = (cs % 8u) == 0u && tr->rec2;
     const uint32_t nrec2 = tr->nrec + 256;
-    const bool t2 = packed && tr->t2 && gbpe_debug_knob("walk", 5) == 6;
-    if (packed && narrow && t2)
-        hipLaunchKernelGGL((k_trie_walk_v5<uint16_t, true>), dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
-                           tr->root_base, (uint16_t*)ctx->enc_scratch, counts, nchunks, (const uint2*)tr->t2);
-    else if (packed && narrow)
-        hipLaunchKernelGGL((k_trie_walk_v5<uint16_t, false>), dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
-                           tr->root_base, (uint16_t*)ctx->enc_scratch, counts, nchunks, (const uint2*)nullptr);
-    else if (packed && t2)
-        hipLaunchKernelGGL((k_trie_walk_v5<uint32_t, true>), dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
-                           tr->root_base, (uint32_t*)ctx->enc_scratch, counts, nchunks, (const uint2*)tr->t2);
+    if (packed && narrow)
+        hipLaunchKernelGGL(k_trie_walk_v5<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
+                           tr->root_base, (uint16_t*)ctx->enc_scratch, counts, nchunks);
     else if (packed)
-        hipLaunchKernelGGL((k_trie_walk_v5<uint32_t, false>), dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
-                           tr->root_base, (uint32_t*)ctx->enc_scratch, counts, nchunks, (const uint2*)nullptr);
+        hipLaunchKernelGGL(k_trie_walk_v5<uint32_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec2, nrec2,
+                           tr->root_base, (uint32_t*)ctx->enc_scratch, counts, nchunks);
     else if (narrow)
         hipLaunchKernelGGL(k_trie_walk<uint16_t>, dim3(gw), dim3(WALK_TPB), 0, s, d_in, n, cs, tr->rec, tr->nrec,
                            tr->root, (uint16_t*)ctx->enc_scratch, counts, nchunks);
