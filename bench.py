@@ -253,9 +253,9 @@ def _rocprof_kernel(prefix: str):
 def train_roofline(det, wall_per_run):
     """Roofline of the dominant training kernel from the HIP-event run.
 
-    The late merges (~3/4 of them at 1 GiB) run in k_late, one launch per step
-    (DESIGN §2d); the earlier sparse merges in k_body, one launch per merge.
-    Each kernel's bytes are the ones it moves (candidate extents and signatures,
+    The sparse merges run in k_body, one launch per merge (the one-workgroup
+    late loop k_late runs them only under GBPE_DEBUG=late=1: measured slower,
+    DESIGN §2d).  Each kernel's bytes are the ones it moves (candidate extents and signatures,
     sector symbols read and rewritten, the zone pass) — pair-table traffic
     excluded as in SURVEY §8(d).  The kernel with the larger share of the run's
     device time is the roofline kernel; the other is reported beside it.  The
@@ -286,6 +286,9 @@ def train_roofline(det, wall_per_run):
             k["rocprof_launches"] = calls
             k["rocprof_achieved_with_rocprof_time"] = round(k["algorithmic_bytes_per_launch"] / (ns / calls), 1)
             k["rocprof_window"] = os.path.relpath(ROCPROF_EN1G, ROOT)
+            k["rocprof_note"] = ("from a run under rocprofv3 --kernel-trace, which runs a few percent slower than the "
+                                 "untraced timed runs (kernel-busy time above the untraced wall), so these per-launch "
+                                 "times are slightly inflated")
         return k
 
     late = kern("late", ev["late_bytes"], ev["ms_late"], ev["late_launches"], ev["late_merges"], "k_late<",
@@ -365,6 +368,22 @@ def c2_leg(args, lib, ctx, dist):
            "ms_per_run": round(1e3 * wall / 3, 2), "reference_table": ref_table(st, pairs)}
     if want is not None:
         res["merges_equal_fixture"] = bool(last.shape == want.shape and np.array_equal(last, want))
+    if not args.no_cpu:
+        # the stronger CPU comparator: the whole C2 run by the
+        # incremental restatement of the reference algorithm (the fixtures' generator)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import cpu_ref
+        t0 = time.perf_counter()
+        r = cpu_ref.train_inc(data, args.vocab, want_symbols=False)
+        dt = time.perf_counter() - t0
+        m = np.array(r["merges"], dtype=np.uint32).reshape(-1, 4)
+        res["cpu_incremental"] = {
+            "value": round(m.shape[0] / dt, 1), "unit": "merges/s", "seconds": round(dt, 2), "cores": 1,
+            "kind": "port", "merges": int(m.shape[0]),
+            "sample": "the whole C2 run (32,512 merges), incremental restatement (oracle/bpe_oracle_inc.c: linked-list "
+                      "stream, per-pair occurrence lists, lazy max-heap), one thread",
+            "merges_equal_fixture": bool(want is not None and m.shape == want.shape and np.array_equal(m, want)),
+            "gpu_over_cpu": round((total / wall) / (m.shape[0] / dt), 1)}
     return data, res
 
 
