@@ -1637,6 +1637,11 @@ constexpr uint32_t SP_SHRINKS_MAX = 1024;   // zone shrinks per sparse entry
 // pairs plus those its merges add — and every false candidate costs a sector
 // pass: 2048 / 3 cuts that rate to a few percent.)
 constexpr uint32_t SP_SIGW = 64;     // u32 words per sector signature
+#ifdef GBPE_SIG_GLOBAL
+constexpr bool SIG_LDS = false;      // (A/B build: every created pair's bits straight to the global signature)
+#else
+constexpr bool SIG_LDS = true;       // k_body gathers a sector's new signature bits in LDS (body_sector's lsig)
+#endif
 constexpr uint32_t SP_SIGB = SP_SIGW * 32 - 1;
 __device__ __forceinline__ uint32_t sig_hash(uint32_t pid) { return gbpe_fmix32(pid ^ 0x9E3779B9u); }
 __device__ __forceinline__ void sig_bits(uint32_t pid, uint32_t& b1, uint32_t& b2, uint32_t& b3) {
@@ -1652,6 +1657,14 @@ __device__ __forceinline__ bool sig_has(const uint32_t* __restrict__ sig, uint32
 }
 // global signature (k_body): no-return atomics, no test load on the merge's critical path
 __device__ __forceinline__ void sig_or(uint32_t* __restrict__ sig, uint32_t pid) {
+    uint32_t b1, b2, b3;
+    sig_bits(pid, b1, b2, b3);
+    atomicOr(&sig[b1 >> 5], 1u << (b1 & 31u));
+    atomicOr(&sig[b2 >> 5], 1u << (b2 & 31u));
+    atomicOr(&sig[b3 >> 5], 1u << (b3 & 31u));
+}
+// a sector's new signature bits gathered in LDS (body_sector's lsig)
+__device__ __forceinline__ void sig_lds(uint32_t* sig, uint32_t pid) {
     uint32_t b1, b2, b3;
     sig_bits(pid, b1, b2, b3);
     atomicOr(&sig[b1 >> 5], 1u << (b1 & 31u));
@@ -1685,10 +1698,15 @@ __device__ __forceinline__ void sector_first(const S* __restrict__ p, const uint
 // survivors compacted to the sector's front).  In the lexicon body (mp != null)
 // every symbol carries its word's multiplicity, which weights its count deltas
 // and moves with it.  Returns the B-sides removed (weighted: stream symbols).
-template <typename S, int NT = LTAB_T, typename TB = Table, typename LT = LdsTab<NT>>
+// lsig (optional): this wave's 64-word LDS copy of the sector signature's new
+// bits — a created pair sets its 3 bits there (LDS atomics), and the sector's end
+// ORs each word into the global signature once (one atomic per non-zero word
+// instead of three per created pair: early merges create thousands per sector)
+template <typename S, int NT = LTAB_T, typename TB = Table, typename LT = LdsTab<NT>, bool LSIG = false>
 __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, uint32_t cnt, uint32_t a, uint32_t b,
                                 uint32_t nw, LT& lt, const TB& tb, DevState* st, uint32_t* __restrict__ sig,
-                                uint32_t& out_cnt, const uint32_t (&first)[5], const uint32_t (&firstm)[4]) {
+                                uint32_t& out_cnt, const uint32_t (&first)[5], const uint32_t (&firstm)[4],
+                                uint32_t* lsig = nullptr) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     const int lane = threadIdx.x & 63;
     const uint32_t pid_ab = (a << 16) | b;
@@ -1750,11 +1768,13 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, ui
                         const uint32_t t2 = h[j + 1] ? nw : ti;
                         if (t2) {
                             lds_add(lt, tb, st, (nw << 16) | t2, w);
-                            sig_or(sig, (nw << 16) | t2);
+                            if (LSIG) sig_lds(lsig, (nw << 16) | t2);
+                            else sig_or(sig, (nw << 16) | t2);
                         }
                     } else if (h[j + 1] && tp) {
                         lds_add(lt, tb, st, (tp << 16) | nw, w);
-                        sig_or(sig, (tp << 16) | nw);
+                        if (LSIG) sig_lds(lsig, (tp << 16) | nw);
+                        else sig_or(sig, (tp << 16) | nw);
                     }
                 }
             }
@@ -1779,6 +1799,10 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, ui
         out += tot;
     }
     out_cnt = out;
+    if (LSIG) {   // (SP_SIGW == 64: a word per lane; the exchange also clears it for the next sector)
+        const uint32_t v = atomicExch(&lsig[lane], 0u);
+        if (v) atomicOr(&sig[lane], v);
+    }
     for (int off = 32; off > 0; off >>= 1) removed += __shfl_xor(removed, off);   // per lane → the wave's
     return removed;
 }
@@ -2366,10 +2390,15 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     constexpr int KB_LT = ZSEG ? 4096 : LTAB_T;   // (4096 for every 1024-thread form: no change on C5 / 1 GiB / C2, r4)
     __shared__ LdsTab<KB_LT> lt;
     __shared__ BodyLds<S, BT> u;
+    // per wave: its sector's new signature bits (the 1024-thread forms: the early,
+    // site-heavy merges; the 256-thread late form keeps 4 waves per SIMD without it)
+    constexpr bool SIGL = SIG_LDS && BT == 1024;
+    __shared__ uint32_t s_sig[SIGL ? BT / 64 : 1][SP_SIGW];
     __shared__ uint32_t s_ntok, s_n, s_any, s_rm[BT / 64];
     __shared__ uint64_t s_mv[BT / 64];
     constexpr int QPT = SP_CAP / BT;   // candidates per thread in the signature test
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    if (SIGL) s_sig[wid][lane] = 0u;   // (a wave's own words: no barrier needed before its first sector)
     uint32_t a, b, nw, mc;
     if (t == 0) KT(0);
     const DevState *gs = nullptr, *zs = nullptr;   // this workgroup's snapshots of the states at launch (LDS)
@@ -2492,8 +2521,9 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                 sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
             }
             uint32_t out = 0;
-            const uint32_t r = body_sector<S, KB_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, xtb, st,
-                                              sig + (uint64_t)sct * SP_SIGW, out, cf, cfm);
+            const uint32_t r = body_sector<S, KB_LT, Table, LdsTab<KB_LT>, SIGL>(
+                body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, xtb, st, sig + (uint64_t)sct * SP_SIGW, out, cf,
+                cfm, s_sig[SIGL ? wid : 0]);
             moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (r ? out : 0u));
             if (r) {
                 removed += r;
