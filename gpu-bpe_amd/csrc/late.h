@@ -580,8 +580,12 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
                     sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
                 }
                 uint32_t outc = 0;
+#ifdef GBPE_BSPROF
+                unsigned long long bsp[6] = {0, 0, 0, 0, 0, 0};
+#endif
                 const uint32_t rr = body_sector<S, LATE_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt,
-                                                             spill, st, sig + (uint64_t)sct * SP_SIGW, outc, cf, cfm);
+                                                             spill, st, sig + (uint64_t)sct * SP_SIGW, outc, cf, cfm,
+                                                             nullptr BSP_PASS);
                 if (lane == 0) bytes += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (rr ? outc : 0u));
                 if (rr) {
                     removed += rr;

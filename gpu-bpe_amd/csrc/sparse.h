@@ -1,0 +1,1168 @@
+// Sector-sparse merge loop: the word-lexicon body's sectors,
+// token bitmap and pair signatures, the one-workgroup zone pass, and k_body — the
+// per-merge pass over the candidate sectors.  Shares train_dev.h's state, pair
+// table and LDS delta tables.
+#pragma once
+
+#include "train_dev.h"
+
+namespace {
+
+// ─── sector-sparse merge loop ──────────────────────────────────
+//
+// Late in training a merge's count is a tiny fraction of the stream, yet the
+// dense pass above reads the whole stream twice per merge.  The sparse loop
+// re-lays the stream out as
+//   * a BODY of word-aligned sectors: sector k starts at the first word start at
+//     or after k*SEC and keeps its symbols compacted at its own start.  Pairs
+//     never cross a word start (train.wgsl:395, 483, 493), so sectors merge
+//     independently and their first symbol is never a B-side;
+//   * a token-presence bitmap (row = token id, bit = sector): a merge (a, b) can
+//     only have sites in sectors whose a-row and b-row bits are both set.  Bits
+//     are set when a token appears in a sector and never cleared (a superset);
+//   * a dense ZONE: the last >= 5*mc symbols, run by the dense kernels on their
+//     own ping-pong buffers.  It carries the reference's compaction quirk (the
+//     stale window always lands at the end of the stream).  Its coordinates are
+//     global position - B (body length), which shifts as the body loses
+//     symbols, so the stale window is copied out (k_body's copy blocks) instead
+//     of being left in place.
+// Per merge: k_select → k_body (candidate sectors + window copy) → k_delta (zone)
+// → k_compact<ZONE> → k_refresh.
+constexpr uint32_t SP_WPW_MIN = 16;  // fewest bitmap words per k_body workgroup (sizes its byte counters)
+constexpr uint32_t SP_CH = 256;      // symbols per wave pass over a sector (4 per lane)
+constexpr uint32_t SP_INV = 0xFFFFFFFFu;
+constexpr uint32_t SP_SHRINKS = 64;  // zone shrinks per sparse entry the first sector capacity allows for (sp_reserve grows it)
+constexpr uint32_t SP_SHRINKS_MAX = 1024;   // zone shrinks per sparse entry
+
+// Per-sector pair signature: a 2048-bit Bloom filter (3 hash bits) of every pair
+// the sector has held since the filters were last rebuilt.  The token bitmap
+// gives candidate sectors; the signature drops most of those where a and b are
+// both present but never adjacent.  (1024 bits / 2 hash bits let through 5 of
+// every 6 candidates without a site in the middle merges — a sector holds ~200
+// pairs plus those its merges add — and every false candidate costs a sector
+// pass: 2048 / 3 cuts that rate to a few percent.)
+constexpr uint32_t SP_SIGW = 64;     // u32 words per sector signature
+#ifdef GBPE_SIG_GLOBAL
+constexpr bool SIG_LDS = false;      // (A/B build: every created pair's bits straight to the global signature)
+#else
+constexpr bool SIG_LDS = true;       // k_body gathers a sector's new signature bits in LDS (body_sector's lsig)
+#endif
+constexpr uint32_t SP_SIGB = SP_SIGW * 32 - 1;
+__device__ __forceinline__ uint32_t sig_hash(uint32_t pid) { return gbpe_fmix32(pid ^ 0x9E3779B9u); }
+__device__ __forceinline__ void sig_bits(uint32_t pid, uint32_t& b1, uint32_t& b2, uint32_t& b3) {
+    const uint32_t h = sig_hash(pid), h2 = h * 0x9E3779B1u;
+    b1 = h & SP_SIGB;
+    b2 = (h >> 16) & SP_SIGB;
+    b3 = (h2 >> 21) & SP_SIGB;
+}
+__device__ __forceinline__ bool sig_has(const uint32_t* __restrict__ sig, uint32_t pid) {
+    uint32_t b1, b2, b3;
+    sig_bits(pid, b1, b2, b3);
+    return ((sig[b1 >> 5] >> (b1 & 31u)) & (sig[b2 >> 5] >> (b2 & 31u)) & (sig[b3 >> 5] >> (b3 & 31u)) & 1u) != 0u;
+}
+// global signature (k_body): no-return atomics, no test load on the merge's critical path
+__device__ __forceinline__ void sig_or(uint32_t* __restrict__ sig, uint32_t pid) {
+    uint32_t b1, b2, b3;
+    sig_bits(pid, b1, b2, b3);
+    atomicOr(&sig[b1 >> 5], 1u << (b1 & 31u));
+    atomicOr(&sig[b2 >> 5], 1u << (b2 & 31u));
+    atomicOr(&sig[b3 >> 5], 1u << (b3 & 31u));
+}
+// a sector's new signature bits gathered in LDS (body_sector's lsig)
+__device__ __forceinline__ void sig_lds(uint32_t* sig, uint32_t pid) {
+    uint32_t b1, b2, b3;
+    sig_bits(pid, b1, b2, b3);
+    atomicOr(&sig[b1 >> 5], 1u << (b1 & 31u));
+    atomicOr(&sig[b2 >> 5], 1u << (b2 & 31u));
+    atomicOr(&sig[b3 >> 5], 1u << (b3 & 31u));
+}
+// LDS signature (k_sp_bits): test first, most bits are already set
+__device__ __forceinline__ void sig_set(uint32_t* __restrict__ sig, uint32_t pid) {
+    uint32_t b1, b2, b3;
+    sig_bits(pid, b1, b2, b3);
+    const uint32_t m1 = 1u << (b1 & 31u), m2 = 1u << (b2 & 31u), m3 = 1u << (b3 & 31u);
+    if (!(sig[b1 >> 5] & m1)) atomicOr(&sig[b1 >> 5], m1);
+    if (!(sig[b2 >> 5] & m2)) atomicOr(&sig[b2 >> 5], m2);
+    if (!(sig[b3 >> 5] & m3)) atomicOr(&sig[b3 >> 5], m3);
+}
+
+// a sector's first wave pass: 4 symbols per lane and the one after the pass
+// (+ their word multiplicities in the lexicon body, else 1)
+template <typename S>
+__device__ __forceinline__ void sector_first(const S* __restrict__ p, const uint32_t* __restrict__ mp, uint32_t cnt,
+                                             uint32_t (&f)[5], uint32_t (&fm)[4]) {
+    const uint32_t i0 = 4u * (uint32_t)(threadIdx.x & 63);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] = (i0 + k < cnt) ? (uint32_t)p[i0 + k] : 0u;
+    f[4] = (SP_CH < cnt) ? (uint32_t)p[SP_CH] : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) fm[k] = mp ? ((i0 + k < cnt) ? mp[i0 + k] : 0u) : 1u;
+}
+
+// One wave merges one sector in place (snapshot semantics, k_delta's delta rule,
+// survivors compacted to the sector's front).  In the lexicon body (mp != null)
+// every symbol carries its word's multiplicity, which weights its count deltas
+// and moves with it.  Returns the B-sides removed (weighted: stream symbols).
+// lsig (optional): this wave's 64-word LDS copy of the sector signature's new
+// bits — a created pair sets its 3 bits there (LDS atomics), and the sector's end
+// ORs each word into the global signature once (one atomic per non-zero word
+// instead of three per created pair: early merges create thousands per sector)
+template <typename S, int NT = LTAB_T, typename TB = Table, typename LT = LdsTab<NT>, bool LSIG = false>
+__device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, uint32_t cnt, uint32_t a, uint32_t b,
+                                uint32_t nw, LT& lt, const TB& tb, DevState* st, uint32_t* __restrict__ sig,
+                                uint32_t& out_cnt, const uint32_t (&first)[5], const uint32_t (&firstm)[4],
+                                uint32_t* lsig BSP_ARG) {
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    const int lane = threadIdx.x & 63;
+    const uint32_t pid_ab = (a << 16) | b;
+    uint32_t c1 = 0, c2 = 0, out = 0, removed = 0;
+    for (uint32_t c0 = 0; c0 < cnt; c0 += SP_CH) {
+        BSP_CLK(q0);
+        const uint32_t i0 = c0 + 4u * lane;
+        // X[0..1] = the two symbols before this lane's four, X[6] = the one after
+        uint32_t X[7], nx, M[4];
+        if (c0 == 0) {   // the first pass's symbols were loaded by the caller (sector_first)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                X[2 + k] = first[k];
+                M[k] = firstm[k];
+            }
+            nx = first[4];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) X[2 + k] = (i0 + k < cnt) ? (uint32_t)p[i0 + k] : 0u;
+            nx = (c0 + SP_CH < cnt) ? (uint32_t)p[c0 + SP_CH] : 0u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) M[k] = mp ? ((i0 + k < cnt) ? mp[i0 + k] : 0u) : 1u;
+        }
+        uint32_t pm1 = __shfl_up(X[5], 1), pm2 = __shfl_up(X[4], 1);
+        uint32_t np = __shfl_down(X[2], 1);
+        if (lane == 0) {
+            pm1 = c1;
+            pm2 = c2;
+        }
+        if (lane == 63) np = nx;
+        X[0] = pm2;
+        X[1] = pm1;
+        X[6] = np;
+        c1 = __shfl(X[5], 63);
+        c2 = __shfl(X[4], 63);
+        // h[j] = hit at the position of X[j]: a B-side (no word-start bit) after an a
+        bool h[7];
+        h[0] = false;
+#pragma unroll
+        for (int j = 1; j < 7; ++j) h[j] = X[j] == b && (X[j - 1] & TM) == a;
+#ifdef GBPE_BSPROF
+        const unsigned long long q1 = clock64() + (h[2] && h[3] && h[4] && h[5] && !M[0] ? 1ull : 0ull);   // (after the loads)
+        BSP_ADD(0, q1 - q0);
+#endif
+        uint32_t keep = 0, vals[4];
+        bool touched = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = k + 2;
+            const bool valid = i0 + k < cnt;
+            const uint32_t w = M[k];   // a pair's occurrences = its right symbol's word multiplicity
+            if (valid && !h[j]) keep |= 1u << k;
+            if (valid && h[j]) removed += w;
+            vals[k] = h[j + 1] ? (nw | (X[j] & WS)) : X[j];
+            touched |= valid && (h[j] || h[j + 1]);
+            if (valid && !(X[j] & WS) && (h[j - 1] || h[j] || h[j + 1])) {
+                const uint32_t tp = X[j - 1] & TM, ti = X[j] & TM;
+                if (tp && ti) {
+                    const uint32_t pid = (tp << 16) | ti;
+                    if (pid != pid_ab) lds_add(lt, tb, st, pid, 0u - w);   // old pair destroyed
+                }
+                if (!h[j]) {
+                    if (h[j - 1]) {
+                        const uint32_t t2 = h[j + 1] ? nw : ti;
+                        if (t2) {
+                            lds_add(lt, tb, st, (nw << 16) | t2, w);
+                            if (LSIG) sig_lds(lsig, (nw << 16) | t2);
+                            else sig_or(sig, (nw << 16) | t2);
+                        }
+                    } else if (h[j + 1] && tp) {
+                        lds_add(lt, tb, st, (tp << 16) | nw, w);
+                        if (LSIG) sig_lds(lsig, (tp << 16) | nw);
+                        else sig_or(sig, (tp << 16) | nw);
+                    }
+                }
+            }
+        }
+#ifdef GBPE_BSPROF
+        BSP_CLK(q2);
+        BSP_ADD(1, q2 - q1);
+#endif
+        const uint32_t kc = __popc(keep);
+        uint32_t incl = kc;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off);
+            if (lane >= off) incl += o;
+        }
+        const uint32_t tot = __shfl(incl, 63);
+        // every read of this pass happened above; writes land at or before their source
+        if (out != c0 || __any(touched)) {
+            uint32_t w = out + incl - kc;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((keep >> k) & 1u) {
+                    if (mp) mp[w] = M[k];
+                    p[w++] = (S)vals[k];
+                }
+        }
+        out += tot;
+#ifdef GBPE_BSPROF
+        BSP_CLK(q3);
+        BSP_ADD(2, q3 - q2);
+        BSP_ADD(4, 1ull);
+#endif
+    }
+    out_cnt = out;
+    BSP_CLK(q4);
+    if (LSIG) {   // (SP_SIGW == 64: a word per lane; the exchange also clears it for the next sector)
+        const uint32_t v = atomicExch(&lsig[lane], 0u);
+        if (v) atomicOr(&sig[lane], v);
+    }
+    for (int off = 32; off > 0; off >>= 1) removed += __shfl_xor(removed, off);   // per lane → the wave's
+#ifdef GBPE_BSPROF
+    BSP_ADD(3, clock64() - q4);
+    BSP_ADD(5, 1ull);
+#endif
+    return removed;
+}
+
+// Single-workgroup zone pass (zone <= ZMAX symbols): k_delta + k_compact<ZONE>
+// in one workgroup.  Each thread holds 32 consecutive zone symbols in registers
+// and builds k_delta's branch-free site masks; only positions next to a site or
+// in the stale tail touch the LDS copy and the delta table.  Kept survivors
+// (A-sides rewritten, also in place: the reference's ping buffer) are compacted
+// into the other zone buffer and the stale window follows them.  The window
+// source is read from the other buffer before anything is written to it.
+// k_body runs as 1024-thread workgroups (16 waves: more sectors in flight, a
+// zone up to 32K symbols in one workgroup) while the zone is large, and as
+// 256-thread ones late in training (small zone, lower latency per launch).
+template <typename S, int BT> struct ZoneDim {
+    static constexpr int ZPT = (BT == 1024 && sizeof(S) == 4) ? 16 : 32;   // zone positions per thread
+    static constexpr uint32_t ZMAX = (uint32_t)BT * ZPT;   // 8192 (256) / 32768 or 16384 (1024) symbols
+    static constexpr uint32_t ZWIN = ZMAX / 3 + 64;         // >= mc: the zone holds >= 3 mc (sel_inline's rule)
+};
+template <typename S, int BT>
+struct ZoneLds {
+    uint4 xv[ZoneDim<S, BT>::ZMAX * sizeof(S) / 16];   // the zone (symbol i = ((S*)xv)[i])
+    S wb[ZoneDim<S, BT>::ZWIN];
+    uint32_t wsum[BT / 64], wtail[BT / 64];
+    S trash[64];   // the zone pass's unconditional stores of dropped symbols
+};
+
+__device__ __forceinline__ uint32_t lane_mask_n(uint64_t i0, uint64_t lim, int n) {
+    // bits k with i0 + k < lim, k < n (n <= 32)
+    const uint32_t full = n == 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    return i0 >= lim ? 0u : (i0 + n <= lim ? full : ((1u << (uint32_t)(lim - i0)) - 1u));
+}
+
+// zout (the persistent tail loop, k_tail): the delta table is shared with the body
+// pass (neither cleared nor flushed here) and m, the new zone length go to zout[0..1]
+template <typename S, bool EXACT, int BT, int NT = LTAB_T, int ZPT_ = ZoneDim<S, BT>::ZPT, typename TB = Table>
+__device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
+                         S* __restrict__ zo, ZoneLds<S, BT>& L,
+                         LdsTab<NT>& lt, const TB& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
+                         uint64_t* __restrict__ bytes, uint32_t round, uint32_t* zout = nullptr) {
+    (void)round;   // phase stamps only (-DGBPE_KTRACE)
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    constexpr int ZPT = ZPT_;                // zone positions per thread (<= ZoneDim's: the LDS is sized for that)
+    static_assert(ZPT <= ZoneDim<S, BT>::ZPT && ZPT * sizeof(S) % 16 == 0, "zone positions per thread");
+    constexpr int V = ZPT * sizeof(S) / 16;  // 16-byte vectors per thread
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t z = zs.n;   // launch snapshots (LDS): no state round trip before the zone loads
+    const uint32_t lim = EXACT ? z : z - mc;
+    const uint32_t pid_ab = (a << 16) | b;
+    const uint32_t i0 = (uint32_t)t * ZPT;
+    S* xs = reinterpret_cast<S*>(L.xv);
+    uint32_t x[ZPT];
+    {
+        uint4 v[V];
+        const uint4* src = reinterpret_cast<const uint4*>(zc + i0);   // zone buffers hold >= 2 tiles
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = src[k];
+#pragma unroll
+        for (int k = 0; k < V; ++k) L.xv[t * V + k] = v[k];
+        const S* e = reinterpret_cast<const S*>(v);
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
+    }
+    if (!EXACT) {   // window source: global n - 2mc in the previous stream
+        const uint64_t src0 = win_src0(gs, mc);
+        for (uint32_t u = t; u < mc; u += BT) L.wb[u] = zo[src0 + u];
+    }
+    if (!zout) lds_clear(lt);
+    __syncthreads();
+    if (t == 0) KT(2);
+    const uint32_t xm2 = i0 >= 2 ? (uint32_t)xs[i0 - 2] : 0u, xm1 = i0 >= 1 ? (uint32_t)xs[i0 - 1] : 0u;
+    const uint32_t nxr = i0 + ZPT < z ? (uint32_t)xs[i0 + ZPT] : 0u;
+    uint32_t eb = 0, ea = 0;
+#pragma unroll
+    for (int k = 0; k < ZPT; ++k) {
+        eb |= (x[k] == b ? 1u : 0u) << k;
+        ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
+    }
+    const uint32_t inb = lane_mask_n(i0, z, ZPT);
+    const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;
+    const uint32_t h_m1 = (i0 >= 1 && i0 - 1 < z && xm1 == b && (xm2 & TM) == a) ? 1u : 0u;
+    const uint32_t h_32 = (nxr == b && (ea >> (ZPT - 1))) ? 1u : 0u;
+    const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (ZPT + 1));
+    const uint32_t below = lane_mask_n(i0, lim, ZPT);
+    const uint32_t surv = inb & ~hitm, keep = surv & below;
+    const uint32_t rwm = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
+    uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+    for (uint32_t i = (lim > 1u ? lim : 1u) + t; i < z; i += BT) {   // stale tail: old pairs destroyed
+        const uint32_t xi = xs[i];
+        if (xi & WS) continue;
+        const uint32_t tp = xs[i - 1] & TM, ti = xi & TM;
+        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+    }
+    while (rel) {
+        const int k = __ffs(rel) - 1;
+        rel &= rel - 1;
+        const uint32_t i = i0 + k;
+        if (i == 0) continue;
+        const uint32_t xi = xs[i];
+        if (xi & WS) continue;
+        const uint32_t xp = xs[i - 1];
+        const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+        const uint32_t tp = xp & TM, ti = xi & TM;
+        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        if (!h0) {
+            if (hm) {
+                const uint32_t t2 = hp ? nw : ti;
+                if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+            } else if (hp && tp) {
+                lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+            }
+        }
+    }
+    if (t == 0) KT(3);
+    // block exclusive scan of the kept counts; tail survivors sum to m
+    const uint32_t kc = __popc(keep);
+    uint32_t incl = kc, tl = __popc(surv & ~below);
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    for (int off = 32; off > 0; off >>= 1) tl += __shfl_xor(tl, off);
+    if (lane == 63) L.wsum[wid] = incl;
+    if (lane == 0) L.wtail[wid] = tl;
+    __syncthreads();
+    if (t == 0) KT(7);
+    uint32_t pre = incl - kc, Kz = 0, m = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < BT / 64; ++w2) {
+        pre += w2 < wid ? L.wsum[w2] : 0u;
+        Kz += L.wsum[w2];
+        m += L.wtail[w2];
+    }
+    // The new zone is assembled in LDS over the old copy (every read of it is
+    // done) and leaves in whole 16-byte stores: per-symbol global stores at a
+    // lane stride of ZPT symbols cost a cache line per lane and instruction.
+    // In LDS the 16-byte chunks are XOR-swizzled within groups of 8: lanes
+    // write ZPT symbols apart, which unswizzled lands every lane of a wave on
+    // the same two banks.
+    constexpr uint32_t PV = 16 / sizeof(S), PVL = sizeof(S) == 2 ? 3 : 2;
+    auto swz = [](uint32_t o) -> uint32_t {
+        const uint32_t c = o >> PVL;
+        return ((c ^ ((c >> 3) & 7u)) << PVL) | (o & (PV - 1u));
+    };
+    // branch-free: every position stores (dropped ones into a per-lane trash
+    // slot); the A-side rewrites of the reference's in-place ping buffer are
+    // the only global stores, one per rewritten position
+    uint32_t wsm = 0;
+#pragma unroll
+    for (int k = 0; k < ZPT; ++k) {
+        const bool rw = (rwm >> k) & 1u;
+        const uint32_t v = rw ? (nw | (x[k] & WS)) : x[k];
+        wsm |= ((x[k] & WS) ? 1u : 0u) << k;
+        const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
+        S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
+        *dst = (S)v;
+    }
+    for (uint32_t r = rwm; r; r &= r - 1) {
+        const int k = __ffs(r) - 1;
+        zc[i0 + k] = (S)(nw | (((wsm >> k) & 1u) ? WS : 0u));
+    }
+    if (t == 0) KT(8);
+    if (!EXACT && m) {
+        __syncthreads();
+        const uint32_t woff = mc - m;
+        for (uint32_t j = t; j < m; j += BT) {
+            const uint32_t x1 = L.wb[woff + j];
+            // left of the window: the last kept survivor (Kz > 0: the zone holds >= 5 mc)
+            const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : (Kz ? (uint32_t)xs[swz(Kz - 1)] : 0u);
+            xs[swz(Kz + j)] = (S)x1;
+            if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) lds_add(lt, tb, st, ((x0 & TM) << 16) | (x1 & TM), 1u);
+        }
+    }
+    __syncthreads();
+    if (t == 0) KT(9);
+    {
+        const uint32_t tot = Kz + m, nfull = tot / PV;
+        uint4* dst = reinterpret_cast<uint4*>(zo);
+        for (uint32_t q = t; q < nfull; q += BT) dst[q] = L.xv[q ^ ((q >> 3) & 7u)];
+        for (uint32_t j = nfull * PV + t; j < tot; j += BT) zo[j] = xs[swz(j)];
+    }
+    if (t == 0) KT(4);
+    if (!zout) lds_flush(lt, tb, st);
+    if (t == 0) {
+        if (zout) {
+            zout[0] = m;
+            zout[1] = Kz + m;
+        } else {
+            zst->m = m;
+            zst->valid_total = Kz + m + 1u;   // survivors + 1 (k_refresh checks it against the new layout)
+        }
+        // zone read, window source read, kept survivors + window written
+        atomicAdd(bytes, (uint64_t)sizeof(S) * ((uint64_t)z + (EXACT ? 0u : mc) + Kz + m));
+    }
+}
+
+// ── segmented zone pass (zones of 32K-1M symbols) ──
+// A zone too large for one workgroup but far smaller than the stream (merges
+// ~500-8000 at 1 GiB) is cut into segments of BT x ZPT = 16K symbols, one
+// 1024-thread workgroup each (blocks [0, nz) of k_body).  Two phases:
+//  A (no waiting): a segment runs zone_one's site deltas and local compaction
+//    on its range (neighbour symbols before / after it come from the current
+//    zone buffer, where their owners may already have rewritten them in place:
+//    token nw reads back as a, since nw exists nowhere else before this merge),
+//    and takes an even share of the two mc-long per-merge chores: the stale
+//    tail's destroyed pairs ([z - mc, z), read the same way) and the stale-window
+//    SOURCE ([n - 2mc - Bp, + mc) of the other buffer) copied into LDS.  It
+//    publishes (kept, tail survivors, last kept symbol) as three 8-byte
+//    {tag, value} granules (relaxed agent-scope stores: the data is the flag)
+//    after every wave drained its loads.
+//  B: one wave sweeps all nz segments' granules; then the segment stores its
+//    kept symbols at its prefix and the part of the window (the last m source
+//    symbols, m = all tail survivors) in its share after the Kz kept ones.  Every
+//    read of the other buffer (the window source) happened in phase A, before
+//    any segment passes phase B's sweep, so no store overwrites an unread source.
+//  Every zone workgroup waits only on zone workgroups, which never wait on body
+//  workgroups: with nz <= 64 workgroups they all become resident.
+// k_refresh zeroes the granules for the next merge (tag = 1).
+template <typename S, bool EXACT, int BT, int NT, int ZPT>
+__device__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
+                         S* __restrict__ zo, ZSegState* zg, uint32_t nz, ZoneLds<S, BT>& L, LdsTab<NT>& lt,
+                         const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
+                         uint64_t* __restrict__ bytes, uint32_t round) {
+    (void)round;
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    constexpr uint32_t SEG = (uint32_t)BT * ZPT;
+    constexpr int V = ZPT * sizeof(S) / 16;
+    static_assert(ZPT <= ZoneDim<S, BT>::ZPT && ZPT * sizeof(S) % 16 == 0, "segment positions per thread");
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    __shared__ uint32_t s_h[3], s_last, s_pre, s_kz, s_m, s_x0;
+    const uint32_t seg = blockIdx.x;
+    const uint32_t z = zs.n;
+    const uint32_t lim = EXACT ? z : z - mc;
+    const uint32_t g0 = seg * SEG;
+    const uint32_t nh = g0 < z ? (z - g0 < SEG ? z - g0 : SEG) : 0u;   // positions of this segment (0: past the end)
+    const uint32_t pid_ab = (a << 16) | b;
+    auto unrw = [&](uint32_t v) -> uint32_t { return (v & TM) == nw ? (a | (v & WS)) : v; };
+    auto zload = [&](uint32_t p) -> uint32_t { return unrw((uint32_t)((const volatile S*)zc)[p]); };   // old or rewritten
+    const uint32_t i0 = (uint32_t)t * ZPT;   // local
+    S* xs = reinterpret_cast<S*>(L.xv);
+    uint32_t x[ZPT];
+    {
+        uint4 v[V];
+        const uint4* src = reinterpret_cast<const uint4*>(zc + g0 + i0);
+        const bool any = i0 < nh;
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = any ? src[k] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int k = 0; k < V; ++k) L.xv[t * V + k] = v[k];
+        const S* e = reinterpret_cast<const S*>(v);
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < nh ? (uint32_t)e[k] : 0u;
+    }
+    if (t < 3) {   // neighbours g0 - 2, g0 - 1, g0 + nh
+        const uint32_t p = t < 2 ? g0 - 2u + (uint32_t)t : g0 + nh;
+        const bool ok = nh && (t < 2 ? g0 >= 2u - (uint32_t)t : g0 + nh < z);
+        s_h[t] = ok ? zload(p) : 0u;
+    }
+    // this segment's share of the window source (+ the symbol before it) into LDS
+    const uint32_t lw = (mc + nz - 1) / nz, q0 = seg * lw, q1 = q0 + lw < mc ? q0 + lw : mc;   // source [q0, q1)
+    const uint64_t src0 = win_src0(gs, mc);
+    if (!EXACT && q0 < q1) {
+        const uint32_t f = q0 ? q0 - 1u : 0u;   // L.wb[j] = source[f + j]
+        for (uint32_t q = f + t; q < q1; q += BT) L.wb[q - f] = zo[src0 + q];
+    }
+    lds_clear(lt);
+    __syncthreads();
+    if (t == 0) KT(2);
+    auto X = [&](int j) -> uint32_t {   // local position j in [-2, SEG]
+        return j < 0 ? s_h[j + 2] : (uint32_t)j < nh ? (uint32_t)xs[j] : ((uint32_t)j == nh ? s_h[2] : 0u);
+    };
+    if (!EXACT) {   // this segment's share of the stale tail: old pairs destroyed
+        const uint32_t lo = lim > 1u ? lim : 1u;
+        const uint32_t nt_ = z > lo ? z - lo : 0u, lt_ = (nt_ + nz - 1) / nz;
+        const uint32_t p0 = lo + seg * lt_, p1 = p0 + lt_ < z ? p0 + lt_ : z;
+        for (uint32_t i = p0 + t; i < p1; i += BT) {
+            const uint32_t xi = zload(i);
+            if (xi & WS) continue;
+            const uint32_t tp = zload(i - 1) & TM, ti = xi & TM;
+            if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        }
+    }
+    const uint32_t xm2 = X((int)i0 - 2), xm1 = X((int)i0 - 1), nxr = X((int)(i0 + ZPT));
+    uint32_t eb = 0, ea = 0;
+#pragma unroll
+    for (int k = 0; k < ZPT; ++k) {
+        eb |= (x[k] == b ? 1u : 0u) << k;
+        ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
+    }
+    const uint32_t gi0 = g0 + i0;
+    const uint32_t inb = lane_mask_n(i0, nh, ZPT);
+    const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;
+    const uint32_t h_m1 = (gi0 >= 1 && i0 <= nh && xm1 == b && (xm2 & TM) == a) ? 1u : 0u;
+    const uint32_t h_32 = (nxr == b && (ea >> (ZPT - 1))) ? 1u : 0u;
+    const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (ZPT + 1));
+    const uint32_t below = lane_mask_n(gi0, lim, ZPT);
+    const uint32_t surv = inb & ~hitm, keep = surv & below;
+    const uint32_t rwm = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
+    uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+    while (rel) {
+        const int k = __ffs(rel) - 1;
+        rel &= rel - 1;
+        const uint32_t i = i0 + k;
+        if (g0 + i == 0) continue;
+        const uint32_t xi = X((int)i);
+        if (xi & WS) continue;
+        const uint32_t xp = X((int)i - 1);
+        const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+        const uint32_t tp = xp & TM, ti = xi & TM;
+        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+        if (!h0) {
+            if (hm) {
+                const uint32_t t2 = hp ? nw : ti;
+                if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+            } else if (hp && tp) {
+                lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+            }
+        }
+    }
+    if (t == 0) KT(3);
+    // local exclusive scan of the kept counts; tail survivors; the last kept symbol
+    const uint32_t kc = __popc(keep);
+    uint32_t incl = kc, tl = __popc(surv & ~below);
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    for (int off = 32; off > 0; off >>= 1) tl += __shfl_xor(tl, off);
+    if (lane == 63) L.wsum[wid] = incl;
+    if (lane == 0) L.wtail[wid] = tl;
+    __syncthreads();
+    uint32_t pre = incl - kc, Ks = 0, Ts = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < BT / 64; ++w2) {
+        pre += w2 < wid ? L.wsum[w2] : 0u;
+        Ks += L.wsum[w2];
+        Ts += L.wtail[w2];
+    }
+    if (kc && pre + kc == Ks) {   // this thread holds the segment's last kept symbol
+        const int hk = 31 - __clz(keep);
+        uint32_t xv = x[0];
+#pragma unroll
+        for (int k = 1; k < ZPT; ++k) xv = k == hk ? x[k] : xv;
+        s_last = ((rwm >> hk) & 1u) ? (nw | (xv & WS)) : xv;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's reads of the other buffer are done
+    __syncthreads();
+    if (t == 0) {
+        constexpr unsigned long long TAG = 1ull << 32;
+        __hip_atomic_store(&zg->gran[seg][0], TAG | Ks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&zg->gran[seg][1], TAG | Ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&zg->gran[seg][2], TAG | (Ks ? (s_last | 0x80000000u) : 0u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        KT(7);
+    }
+    // the new segment assembled in LDS over the old copy (swizzled as in zone_one)
+    constexpr uint32_t PV = 16 / sizeof(S), PVL = sizeof(S) == 2 ? 3 : 2;
+    auto swz = [](uint32_t o) -> uint32_t {
+        const uint32_t c = o >> PVL;
+        return ((c ^ ((c >> 3) & 7u)) << PVL) | (o & (PV - 1u));
+    };
+    uint32_t wsm = 0;
+#pragma unroll
+    for (int k = 0; k < ZPT; ++k) {
+        const bool rw = (rwm >> k) & 1u;
+        const uint32_t v = rw ? (nw | (x[k] & WS)) : x[k];
+        wsm |= ((x[k] & WS) ? 1u : 0u) << k;
+        const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
+        S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
+        *dst = (S)v;
+    }
+    for (uint32_t r = rwm; r; r &= r - 1) {
+        const int k = __ffs(r) - 1;
+        zc[gi0 + k] = (S)(nw | (((wsm >> k) & 1u) ? WS : 0u));
+    }
+    // B: every segment's granules (one wave, relaxed sweeps, s_sleep between)
+    if (wid == 0) {
+        uint32_t gk = 0, gt = 0, gl = 0;
+        for (uint32_t it = 0;; ++it) {
+            bool ok = true;
+            if ((uint32_t)lane < nz) {
+                const unsigned long long x0 = __hip_atomic_load(&zg->gran[lane][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long x1 = __hip_atomic_load(&zg->gran[lane][1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long x2 = __hip_atomic_load(&zg->gran[lane][2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = (x0 >> 32) == 1u && (x1 >> 32) == 1u && (x2 >> 32) == 1u;
+                gk = (uint32_t)x0;
+                gt = (uint32_t)x1;
+                gl = (uint32_t)x2;
+            }
+            if (__all(ok)) break;
+            if (it > ZSEG_SPIN) {
+                if (lane == 0) atomicOr(&st->err, ERR_SPIN);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const bool in = (uint32_t)lane < nz;
+        uint32_t sp = in && (uint32_t)lane < seg ? gk : 0u, sk = in ? gk : 0u, stt = in ? gt : 0u;
+        for (int off = 32; off > 0; off >>= 1) {
+            sp += __shfl_xor(sp, off);
+            sk += __shfl_xor(sk, off);
+            stt += __shfl_xor(stt, off);
+        }
+        const unsigned long long hm = __ballot(in && (gl >> 31));
+        if (lane == 0) {
+            s_pre = sp;
+            s_kz = sk;
+            s_m = EXACT ? 0u : stt;
+            s_x0 = 0u;
+        }
+        if (hm && lane == 63 - __clzll(hm)) s_x0 = gl & 0x7FFFFFFFu;   // the last kept survivor overall
+    }
+    __syncthreads();
+    if (t == 0) KT(8);
+    const uint32_t P = s_pre, Kz = s_kz, m = s_m;
+    for (uint32_t j = t; j < Ks; j += BT) zo[P + j] = xs[swz(j)];
+    if (!EXACT && m) {   // the window = source [mc - m, mc) after the Kz kept symbols; this segment's share
+        const uint32_t w0 = mc - m, f = q0 ? q0 - 1u : 0u;
+        const uint32_t lo = q0 > w0 ? q0 : w0;
+        for (uint32_t q = lo + t; q < q1; q += BT) {
+            const uint32_t x1 = L.wb[q - f];
+            const uint32_t x0 = q == w0 ? s_x0 : (uint32_t)L.wb[q - 1u - f];
+            zo[Kz + (q - w0)] = (S)x1;
+            if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) lds_add(lt, tb, st, ((x0 & TM) << 16) | (x1 & TM), 1u);
+        }
+    }
+    if (t == 0) KT(9);
+    lds_flush(lt, tb, st);
+    if (t == 0) {
+        KT(4);
+        if (seg == 0) {
+            zst->m = m;
+            zst->valid_total = Kz + m + 1u;
+        }
+        const uint32_t ws = q1 > q0 ? q1 - q0 : 0u;
+        atomicAdd(bytes, (uint64_t)sizeof(S) * ((uint64_t)nh + Ks + 2u * ws + (EXACT ? 0u : mc / nz)));
+    }
+}
+
+// Selection inside k_body (sector-sparse loop): every workgroup reduces the
+// k_refresh partial maxima itself and gets the same merge; the last one commits
+// it (log, table slot zeroed, state for k_refresh and the zone kernels).  The
+// step counters move on in k_refresh (finish == 2), so nothing a workgroup reads
+// here changes under it.  Saves the k_select launch per merge.
+struct SelShard {
+    uint32_t zf = 3;         // zone rule: z >= max(2 mc + mc_prev, zf mc) + 2 (GBPE_ZONE_F)
+};
+
+template <int BT>
+__device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
+                           uint32_t round, bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
+                           uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc,
+                           const DevState*& gsnap, const DevState*& zsnap, const SelShard sh = SelShard(),
+                           bool commit = true) {
+    __shared__ uint64_t s_red[BT / 64];
+    constexpr int NW = sizeof(DevState) / 4;
+    __shared__ union {
+        DevState d;
+        uint32_t w[NW];
+    } s_g, s_z;
+    const int t = threadIdx.x;
+    // the partial maxima and snapshots of both states load together (one round
+    // trip, not one per field)
+    if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
+    else if (zst && t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
+    uint64_t best = 0;
+    for (uint32_t i = t; i < npart; i += BT) {
+        const uint64_t v = part[i];
+        best = v > best ? v : best;
+    }
+    __syncthreads();
+    const DevState& g = s_g.d;
+    gsnap = &s_g.d;
+    zsnap = &s_z.d;
+    if (!(round < g.budget && g.merges_done == round && !g.stop && !g.sp_abort)) return false;
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    if ((t & 63) == 0) s_red[t >> 6] = best;
+    __syncthreads();
+    best = s_red[0];
+#pragma unroll
+    for (int w = 1; w < BT / 64; ++w) best = s_red[w] > best ? s_red[w] : best;
+    mc = (uint32_t)(best >> 32);
+    const uint32_t pid = ~(uint32_t)best;
+    a = pid >> 16;
+    b = pid & 0xFFFFu;
+    nw = g.next_id;
+    const bool stop = mc < 2u || nw > 0xFFFFu;                                          // train.wgsl:345-348
+    const bool bad = !stop && !exact && g.is_last && (uint64_t)(uint32_t)(g.n - g.Bp) < 2ull * mc;   // cannot happen
+    // zone misfit: this merge's window source must lie in the zone's stale buffer
+    // (n - 2mc >= Bp, where n - Bp >= z - mc_prev: the last merge removed <= mc_prev
+    // body symbols), and the zone keeps >= zf mc for the merges after it
+    const uint32_t mc_prev = g.mc_prev;
+    const uint64_t zneed = std::max<uint64_t>(2ull * mc + mc_prev, (uint64_t)sh.zf * mc) + 2u;
+    const bool abort = !stop && !bad && !exact && (uint64_t)g.zlast < zneed;
+    const bool go = !stop && !bad && !abort;
+    // the LAST workgroup commits: block 0 is the zone pass (the launch's longest
+    // chain), which then starts without the table probe and the state stores
+    if (commit && blockIdx.x == gridDim.x - 1u) {
+        if (t == 0) {
+            if (stop) {
+                st->stop = 1u;
+            } else if (bad) {
+                atomicOr(&st->err, ERR_SPARSE_WINDOW);
+                st->stop = 1u;
+            } else if (abort) {
+                st->sp_abort = 1u;
+            } else {
+                const uint32_t idx = table_find(tb, pid);
+                if (idx == 0xFFFFFFFFu) {
+                    atomicOr(&st->err, ERR_PAIR_MISSING);
+                } else {
+                    // every (a,b) occurrence is a merge site: count -= mc, atomically, since
+                    // other workgroups may already add this merge's stale-window pairs
+                    atomicSub(&tb.slots[idx].y, mc);
+                    tb.dirty[idx >> BLK_LOG2] = 1u;
+                }
+                log[round * 4 + 0] = a;
+                log[round * 4 + 1] = b;
+                log[round * 4 + 2] = nw;
+                log[round * 4 + 3] = mc;
+                st->a = a;
+                st->b = b;
+                st->nw = nw;
+                st->mc = mc;
+                st->new_n = g.n - mc;
+                zst->a = a;
+                zst->b = b;
+                zst->nw = nw;
+                zst->mc = mc;
+                zst->new_n = exact ? s_z.d.n : s_z.d.n - mc;
+                if (!zone1) {   // zone_one (another workgroup of this launch) sets both itself
+                    zst->m = 0u;
+                    zst->valid_total = 0u;
+                }
+                zst->merges_done = round + 1u;
+                st->sel_round = round + 1u;
+            }
+        }
+        if (go) {   // group sums of a multi-tile zone pass start at zero
+            const uint32_t ngrp = (uint32_t)gbpe_div_up(gbpe_div_up(s_z.d.n, TILE), GRP);
+            for (uint32_t q = t; q < ngrp; q += BT) grpsum[q * GSTR] = 0u;
+        }
+    }
+    return go;
+}
+
+// Body pass: blocks [0, nbody) each own `wpg` consecutive bitmap words of
+// (a-row & b-row), tested PW words at a time: the candidate sectors whose pair
+// signature may hold (a, b) are merged (one wave per sector).  A fixed grid of
+// wide workgroups (about 4 per CU at 1 GiB) instead of one workgroup per 16
+// words: the selection each workgroup repeats, and the rounds of workgroup
+// scheduling, cost more than the bitmap words themselves (75K words per row at
+// 1 GiB).  Blocks >= nbody copy the stale-window source [n - 2mc - Bp, + mc) of
+// the zone's other buffer to `wtmp`.
+// With `zst` (zone <= ZMAX), block nbody runs the whole zone pass (zone_one) and
+// there are no copy blocks: one launch merges body and zone.
+constexpr uint32_t SP_PW = 64;               // bitmap words tested per pass (one per lane of wave 0)
+constexpr uint32_t SP_CAP = SP_PW * 32;      // candidate sectors per pass
+struct BodyCand {
+    uint32_t sec[SP_CAP];
+    uint2 ext[SP_CAP];
+};
+template <typename S, int BT>
+union BodyLds {   // body workgroups use the candidate arrays, the zone workgroup the zone
+    ZoneLds<S, BT> z;
+    BodyCand c;
+};
+
+// ZSEG: the form for zones of 32K-1M symbols: blocks [0, zone1) run the zone
+// segments (zone_seg) beside the body blocks, and zone_one is not compiled in
+// (with both, every form spilled to scratch)
+template <typename S, bool EXACT, int BT, int ZPT = ZoneDim<S, BT>::ZPT, bool ZSEG = false>
+__global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
+                                              uint32_t* __restrict__ bits, uint32_t W, uint32_t wpg,
+                                              uint32_t* __restrict__ sig, Table tb, uint32_t nbody,
+                                              const S* __restrict__ zoth, S* __restrict__ wtmp,
+                                              uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
+                                              const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
+                                              uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
+                                              Table dtb, SelShard sh, uint32_t* __restrict__ lmul,
+                                              ZSegState* __restrict__ zg = nullptr) {
+    constexpr int KB_LT = ZSEG ? 4096 : LTAB_T;   // (4096 for every 1024-thread form: no change on C5 / 1 GiB / C2, r4)
+    __shared__ LdsTab<KB_LT> lt;
+    __shared__ BodyLds<S, BT> u;
+    // per wave: its sector's new signature bits (the 1024-thread forms: the early,
+    // site-heavy merges; the 256-thread late form keeps 4 waves per SIMD without it)
+    constexpr bool SIGL = SIG_LDS && BT == 1024;
+    __shared__ uint32_t s_sig[SIGL ? BT / 64 : 1][SP_SIGW];
+    __shared__ uint32_t s_ntok, s_n, s_any, s_rm[BT / 64];
+    __shared__ uint64_t s_mv[BT / 64];
+    constexpr int QPT = SP_CAP / BT;   // candidates per thread in the signature test
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    if (SIGL) s_sig[wid][lane] = 0u;   // (a wave's own words: no barrier needed before its first sector)
+#ifdef GBPE_BSPROF
+    unsigned long long bsp[6] = {0, 0, 0, 0, 0, 0}, bsp_wall = 0;
+#endif
+    uint32_t a, b, nw, mc;
+    if (t == 0) KT(0);
+    const DevState *gs = nullptr, *zs = nullptr;   // this workgroup's snapshots of the states at launch (LDS)
+    const Table& xtb = dtb;
+    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh)) {
+        return;
+    }
+    if (t == 0) KT(1);
+    // the zone workgroup is dispatched first (block 0 when zone1): it is the longest
+    // single chain of the merge, and later blocks of a large grid start later
+    const uint32_t bid = blockIdx.x - zone1;
+    if constexpr (ZSEG) {
+        if (blockIdx.x < zone1) {
+            zone_seg<S, EXACT, BT, KB_LT, 16>(st, zst, *gs, *zs, zcur, (S*)zoth, zg, zone1, u.z, lt, dtb, a, b, nw, mc,
+                                             wg_bytes + nbody, round);
+            if (t == 0) {
+                KT(5);
+                KTV(6, 2);
+            }
+            return;
+        }
+    } else {
+        if (zone1 == 1 && blockIdx.x == 0) {
+            zone_one<S, EXACT, BT, KB_LT, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, xtb, a, b, nw, mc,
+                                                 wg_bytes + nbody, round);
+            if (t == 0) {
+                KT(5);
+                KTV(6, 2);
+            }
+            return;
+        }
+    }
+    if (bid >= nbody) {
+        const uint64_t src0 = win_src0(*gs, mc);
+        const uint64_t stride = (uint64_t)(gridDim.x - nbody) * BT;
+        for (uint64_t v = (uint64_t)(bid - nbody) * BT + t; v < mc; v += stride) wtmp[v] = zoth[src0 + v];
+        if (t == 0) {
+            KT(5);
+            KTV(6, 3);
+        }
+        return;
+    }
+    const uint32_t pid_ab = (a << 16) | b;
+    BodyCand& cb = u.c;
+    lds_clear(lt);
+    if (t == 0) s_any = 0u;
+    uint32_t removed = 0, ncand_all = 0;
+    uint64_t moved = 0, rd = 0;   // sector symbols read + rewritten (wave-uniform); extents + signature words read
+    const uint32_t w_beg = bid * wpg, w_end = w_beg + wpg < W ? w_beg + wpg : W;
+    for (uint32_t w0 = w_beg; w0 < w_end; w0 += SP_PW) {
+        __syncthreads();   // the previous pass is done with s_ntok / s_n / the candidate arrays
+        if (t == 0) {
+            s_ntok = 0u;
+            s_n = 0u;
+        }
+        __syncthreads();
+        if (t < (int)SP_PW && w0 + t < w_end) {   // token candidates
+            const uint32_t w = w0 + t;
+            uint32_t c = bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w];
+            if (c) {
+                uint32_t pos = atomicAdd(&s_ntok, (uint32_t)__popc(c));
+                while (c) {
+                    const int bit = __ffs(c) - 1;
+                    c &= c - 1;
+                    cb.sec[pos++] = w * 32u + (uint32_t)bit;
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t ntok = s_ntok;
+        if (t == 0) KT(2);
+        if (ntok == 0) continue;   // block-uniform
+        rd += 16ull * ntok;
+        // signature filter: this thread's candidates (their extents load alongside)
+        // into registers, then compacted in place
+        uint32_t cs[QPT];
+        uint2 ce[QPT];
+        bool ck[QPT];
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) {
+            const uint32_t j = (uint32_t)t + (uint32_t)q * BT;
+            cs[q] = j < ntok ? cb.sec[j] : SP_INV;
+        }
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) {
+            ck[q] = false;
+            if (cs[q] != SP_INV) {
+                ce[q] = sec[cs[q]];
+                ck[q] = sig_has(sig + (uint64_t)cs[q] * SP_SIGW, pid_ab);
+            }
+        }
+        __syncthreads();   // every candidate is read before the list is rewritten
+#pragma unroll
+        for (int q = 0; q < QPT; ++q)
+            if (ck[q]) {
+                const uint32_t qq = atomicAdd(&s_n, 1u);
+                cb.sec[qq] = cs[q];
+                cb.ext[qq] = ce[q];
+            }
+        __syncthreads();
+        const uint32_t ncand = s_n;
+        if (t == 0) KT(3);
+        if (ncand == 0) continue;   // block-uniform
+        ncand_all += ncand;
+        if (t == 0) s_any = 1u;
+        // software-pipelined: a wave's next sector loads while it merges this one
+        uint32_t nf[5], nfm[4];
+#ifdef GBPE_BSPROF
+        const unsigned long long sp0 = clock64();
+#endif
+        if ((uint32_t)wid < ncand)
+            sector_first<S>(body + cb.ext[wid].x, lmul ? lmul + cb.ext[wid].x : nullptr, cb.ext[wid].y, nf, nfm);
+        for (uint32_t j = wid; j < ncand; j += BT / 64) {
+            const uint32_t sct = cb.sec[j];
+            const uint2 e = cb.ext[j];
+            uint32_t cf[5], cfm[4];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) cf[k] = nf[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cfm[k] = nfm[k];
+            if (j + BT / 64 < ncand) {
+                const uint2 en = cb.ext[j + BT / 64];
+                sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
+            }
+            uint32_t out = 0;
+            const uint32_t r = body_sector<S, KB_LT, Table, LdsTab<KB_LT>, SIGL>(
+                body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, xtb, st, sig + (uint64_t)sct * SP_SIGW, out, cf,
+                cfm, s_sig[SIGL ? wid : 0] BSP_PASS);
+            moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (r ? out : 0u));
+            if (r) {
+                removed += r;
+                if (lane == 0) {
+                    if (clog) atomicAdd(&st->hitsec, 1u);
+                    sec[sct].y = out;
+                    atomicOr(&bits[(uint64_t)nw * W + (sct >> 5)], 1u << (sct & 31u));
+                }
+            }
+        }
+#ifdef GBPE_BSPROF
+        bsp_wall += clock64() - sp0;
+#endif
+    }
+#ifdef GBPE_BSPROF
+    if (lane == 0) {
+        for (int k = 0; k < 6; ++k) atomicAdd(&g_bsprof[k], bsp[k]);
+        atomicAdd(&g_bsprof[6], bsp_wall);
+        atomicAdd(&g_bsprof[7], 1ull);
+    }
+#endif
+    __syncthreads();
+    if (t == 0) KT(4);
+    if (!s_any) {   // block-uniform: no candidate survived the filters
+        if (t == 0) {
+            if (rd) atomicAdd(&wg_bytes[bid], rd);
+            KT(5);
+            KTV(6, 0);
+        }
+        return;
+    }
+    if (t == 0 && clog) atomicAdd(&st->cand, ncand_all);
+    lds_flush(lt, xtb, st);
+    if (lane == 0) {
+        s_rm[wid] = removed;
+        s_mv[wid] = moved;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t r = 0;
+        uint64_t mv = rd;
+        for (int w2 = 0; w2 < BT / 64; ++w2) {
+            r += s_rm[w2];
+            mv += s_mv[w2];
+        }
+        if (r) atomicAdd(&st->body_rm, r);
+        atomicAdd(&wg_bytes[bid], mv);   // this workgroup's own counter
+        KT(5);
+        KTV(6, 1 | (ncand_all << 8));
+    }
+}
+
+// dense → sparse: the last position at or before `lim` that no counted pair can
+// span — a word start, or a token-0 symbol on either side (one workgroup,
+// backwards).  The 0s count: the stale window of a huge merge is a 0 run of up
+// to ~mc symbols (C5's first merge: ~180M), which a word-start-only search
+// crossed at 1024 symbols per round (25 ms per entry / shrink).
+template <typename S>
+__global__ __launch_bounds__(1024) void k_sp_zone_start(const S* __restrict__ cur, uint32_t lim, uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_found;
+    if (threadIdx.x == 0) s_found = 0u;
+    __syncthreads();
+    for (int64_t hi = lim; hi >= 1; hi -= 1024) {
+        const int64_t i = hi - (int64_t)threadIdx.x;
+        const uint32_t x = i >= 1 ? (uint32_t)cur[i] : 0u, p = i >= 1 ? (uint32_t)cur[i - 1] : 0u;
+        if (i >= 1 && ((x & Sym<S>::WS) || !(x & Sym<S>::TM) || !(p & Sym<S>::TM))) atomicMax(&s_found, (uint32_t)i);
+        __syncthreads();
+        const uint32_t f = s_found;
+        __syncthreads();
+        if (f) break;
+    }
+    if (threadIdx.x == 0) *out = s_found;   // 0 = none
+}
+
+// window j of a body region [base, base + len) covers [base + j*SEC, +SEC); its
+// sector starts at the window's first word start or 0 symbol (window 0: at
+// `base`, which is a word start or the stream's first symbol).  No counted pair
+// spans either: pairs never cross a word start, and none holds token 0 — the
+// stale windows the reference compaction leaves are long 0 runs
+// that would otherwise make one sector of up to ~10^6 symbols.  One wave per
+// window.
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_sectors(const S* __restrict__ body, uint32_t base, uint32_t len, uint32_t SEC,
+                                                    uint32_t* __restrict__ starts, uint32_t nwin) {
+    const uint32_t j = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (j >= nwin) return;
+    const uint64_t end = (uint64_t)base + len;
+    const uint64_t lo = (uint64_t)base + (uint64_t)j * SEC, hi = lo + SEC < end ? lo + SEC : end;
+    uint32_t found = j == 0 ? base : SP_INV;
+    for (uint64_t b0 = lo; b0 < hi && found == SP_INV; b0 += 64) {
+        const uint64_t i = b0 + lane;
+        uint32_t x = i < hi ? (uint32_t)body[i] : 1u;
+        const bool ws = (x & Sym<S>::WS) || x == 0u;
+        const unsigned long long m = __ballot(ws);
+        if (m) found = (uint32_t)(b0 + (uint64_t)(__ffsll((long long)m) - 1));
+    }
+    if (lane == 0) starts[j] = found;
+}
+
+__global__ void k_sp_sector_len(const uint32_t* __restrict__ starts, uint32_t nwin, uint32_t end, uint2* __restrict__ sec) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nwin) return;
+    const uint32_t st = starts[k];
+    if (st == SP_INV) {
+        sec[k] = make_uint2(0u, 0u);
+        return;
+    }
+    uint32_t e = end;
+    for (uint32_t j = k + 1; j < nwin; ++j)   // windows inside one long word have no start
+        if (starts[j] != SP_INV) {
+            e = starts[j];
+            break;
+        }
+    sec[k] = make_uint2(st, e - st);
+}
+
+// presence bits of every token (with `bits`) and the pair signature of sectors
+// [k0, k0 + nk), one wave per sector.  The signature is built in LDS and stored
+// whole (one 128-B line per sector); bitmap words are tested before the atomic.
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_bits(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t k0,
+                                                 uint32_t nk, uint32_t* __restrict__ bits, uint32_t W,
+                                                 uint32_t* __restrict__ sig) {
+    __shared__ uint32_t ssig[TPB / 64][SP_SIGW];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t k = k0 + blockIdx.x * (TPB / 64) + wid;
+    const bool live = k < k0 + nk;
+    if (lane < (int)SP_SIGW) ssig[wid][lane] = 0u;
+    __syncthreads();
+    if (live) {
+        const uint2 e = sec[k];
+        const uint32_t bit = 1u << (k & 31u);
+        uint32_t* col = bits ? bits + (k >> 5) : nullptr;
+        for (uint32_t j = lane; j < e.y; j += 64) {
+            const uint32_t x = body[e.x + j];
+            const uint32_t tok = x & Sym<S>::TM;
+            if (col) {
+                uint32_t* wp = col + (uint64_t)tok * W;
+                if (!(*wp & bit)) atomicOr(wp, bit);
+            }
+            if (j && !(x & Sym<S>::WS)) {
+                const uint32_t tp = body[e.x + j - 1] & Sym<S>::TM;
+                if (tp && tok) sig_set(ssig[wid], (tp << 16) | tok);
+            }
+        }
+    }
+    __syncthreads();
+    if (live && lane < (int)SP_SIGW) sig[(uint64_t)k * SP_SIGW + lane] = ssig[wid][lane];
+}
+
+// token bitmap of whole columns (a full rebuild over a zeroed bitmap): one
+// workgroup per 32-sector column gathers token -> sector mask in LDS, then
+// writes each present token's word once (plain stores; the column is its own).
+// Tokens beyond the LDS table's reach take a global atomicOr instead.
+constexpr int COLT = 8192;
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_colbits(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t nsec,
+                                                    uint32_t* __restrict__ bits, uint32_t W) {
+    __shared__ uint32_t key[COLT], msk[COLT];
+    for (int i = threadIdx.x; i < COLT; i += TPB) {
+        key[i] = 0xFFFFFFFFu;
+        msk[i] = 0u;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t c = blockIdx.x;
+    for (uint32_t q = wid; q < 32; q += TPB / 64) {
+        const uint32_t k = c * 32 + q;
+        if (k >= nsec) break;
+        const uint2 e = sec[k];
+        for (uint32_t j = lane; j < e.y; j += 64) {
+            const uint32_t tok = body[e.x + j] & Sym<S>::TM;
+            uint32_t h = gbpe_fmix32(tok) & (COLT - 1);
+            bool done = false;
+            for (int p = 0; p < 32 && !done; ++p) {
+                const uint32_t o = atomicCAS(&key[h], 0xFFFFFFFFu, tok);
+                if (o == 0xFFFFFFFFu || o == tok) {
+                    atomicOr(&msk[h], 1u << q);
+                    done = true;
+                }
+                h = (h + 1) & (COLT - 1);
+            }
+            if (!done) atomicOr(&bits[(uint64_t)tok * W + c], 1u << q);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < COLT; i += TPB)
+        if (key[i] != 0xFFFFFFFFu) atomicOr(&bits[(uint64_t)key[i] * W + c], msk[i]);
+}
+
+// sparse → dense: sector counts, then a gather at the scanned offsets (one wave per sector)
+__global__ void k_sp_counts(const uint2* __restrict__ sec, uint32_t nsec, uint32_t* __restrict__ cnt) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nsec) cnt[k] = sec[k].y;
+}
+
+template <typename S>
+__global__ __launch_bounds__(TPB) void k_sp_gather(const S* __restrict__ body, const uint2* __restrict__ sec, uint32_t nsec,
+                                                   const uint32_t* __restrict__ loc, const uint64_t* __restrict__ blk,
+                                                   S* __restrict__ dst) {
+    const uint32_t k = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (k >= nsec) return;
+    const uint2 e = sec[k];
+    const uint64_t off = (uint64_t)loc[k] + blk[k / SCAN_BLK];
+    for (uint32_t j = lane; j < e.y; j += 64) dst[off + j] = body[e.x + j];
+}
+
+#include "lexicon.h"
+
+}  // namespace

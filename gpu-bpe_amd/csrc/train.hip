@@ -405,6 +405,19 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     }
     TR_HIP(t, hipStreamSynchronize(s));
     const uint32_t done = hs->merges_done;
+#ifdef GBPE_BSPROF
+    if (sparse && getenv("GBPE_BSPROF")) {   // body_sector's cycle split of this step (train_dev.h)
+        unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        TR_HIP(t, hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bsprof), sizeof(h), 0, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[bsprof] merges %u-%u waves %llu sectors %llu passes %llu | cyc/sector loads+hits %.0f deltas %.0f "
+                        "writes %.0f flush %.0f | sector-phase cyc/wave %.0f\n",
+                (unsigned)t->done, (unsigned)(t->done + done), h[7], h[5], h[4], h[5] ? (double)h[0] / h[5] : 0.0,
+                h[5] ? (double)h[1] / h[5] : 0.0, h[5] ? (double)h[2] / h[5] : 0.0, h[5] ? (double)h[3] / h[5] : 0.0,
+                h[7] ? (double)h[6] / h[7] : 0.0);
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        TR_HIP(t, hipMemcpyToSymbol(HIP_SYMBOL(g_bsprof), z, sizeof(z), 0, hipMemcpyHostToDevice));
+    }
+#endif
     const uint32_t err = hs->err | (sparse ? t->h_zst->err : 0u);
     if (err) {
         return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "training invariant violated (err=0x%x: %s%s%s%s%s)", err,
