@@ -100,6 +100,11 @@ CASES = [
     ("en8m_exact_w3", 3, dict(gen="english", bytes=8 << 20, seed=32, fracs=[0.3, 0.55], vocab=6000, exact=True)),
     # C4-shaped at 64K ids (u32 symbols): independent multilingual shards, seams inside words
     ("ml3x4m_64k_w3", 3, dict(gen="ml_shards", shard=4 << 20, seeds=[5, 6, 7], vocab=65536)),
+    # the headline's shape at N = 8: English's top count makes the zone
+    # (5 x the summed top counts) longer than one eighth of the stream, so it spans
+    # the tails of several pieces
+    ("en8m_w8_zone_spans", 8, dict(gen="english", bytes=8 << 20, seed=33, fracs=[k / 8 for k in range(1, 8)],
+                                   vocab=4096, spans=True)),
 ]
 
 
@@ -114,6 +119,9 @@ def test_lexshard_matches_oracle(name, world, case):
     root = res[-1]
     assert root["final_n"] == n and root["final_sha256"] == sha
     assert root["root"]["sparse_exits"] == 0
+    if case.get("spans"):
+        zones = [row[4] for row in root["shapes"]]
+        assert sum(1 for z in zones if z) >= 2, f"zone parts {zones}: the case no longer spans pieces"
 
 
 def test_c4_shaped_fixture_world8():
