@@ -244,7 +244,8 @@ def _rocprof_kernel(prefix: str):
     calls, ns = 0, 0.0
     if os.path.exists(ROCPROF_EN1G):
         for r in csv.DictReader(open(ROCPROF_EN1G)):
-            if r["Name"].startswith(prefix):
+            name = r["Name"].replace("void ", "", 1).replace("(anonymous namespace)::", "")
+            if name.startswith(prefix):
                 calls += int(r["Calls"])
                 ns += float(r["TotalDurationNs"])
     return calls, ns

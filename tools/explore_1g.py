@@ -67,13 +67,16 @@ def main():
             t2 = time.perf_counter()
             st = _lib.TrainerStats()
             lib.gbpe_trainer_stats_get(tr, C.byref(st))
+            t3 = time.perf_counter()
             lib.gbpe_trainer_destroy(tr)
+            lib.gbpe_synchronize(ctx)
+            t4 = time.perf_counter()
             m = np.array(merges, dtype=np.uint32).reshape(-1, 4)
             np.save(os.path.join(out_dir, f"explore_{name}_merges.npy"), m)
             sd = {f: getattr(st, f) for f, _ in _lib.TrainerStats._fields_}
             st_ms = np.array(steps) * 1e3
             res = {"name": name, "rep": rep, "n": len(data), "sha256": sha, "merges": int(m.shape[0]),
-                   "create_s": t1 - t0, "loop_s": t2 - t1, "merges_per_s_loop": m.shape[0] / (t2 - t1),
+                   "create_s": t1 - t0, "loop_s": t2 - t1, "destroy_s": t4 - t3, "merges_per_s_loop": m.shape[0] / (t2 - t1),
                    "merges_per_s_total": m.shape[0] / (t2 - t0),
                    "step_ms_first10": [round(x, 2) for x in st_ms[:10]],
                    "step_ms_by_32": [round(float(st_ms[i:i + 32].sum()), 1) for i in range(0, len(st_ms), 32)],
