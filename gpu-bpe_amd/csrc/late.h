@@ -585,7 +585,7 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
 #endif
                 const uint32_t rr = body_sector<S, LATE_LT>(body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt,
                                                              spill, st, sig + (uint64_t)sct * SP_SIGW, outc, cf, cfm,
-                                                             nullptr BSP_PASS);
+                                                             nullptr, nullptr, nullptr BSP_PASS);
                 if (lane == 0) bytes += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (rr ? outc : 0u));
                 if (rr) {
                     removed += rr;

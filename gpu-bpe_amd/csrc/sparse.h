@@ -103,6 +103,15 @@ __device__ __forceinline__ void sector_first(const S* __restrict__ p, const uint
 // survivors compacted to the sector's front).  In the lexicon body (mp != null)
 // every symbol carries its word's multiplicity, which weights its count deltas
 // and moves with it.  Returns the B-sides removed (weighted: stream symbols).
+// whole-wave lane shifts (DPP wave_shr:1 / wave_shl:1, GFX9 DPP controls 0x138 /
+// 0x130): lane i gets lane i-1's (i+1's) value; the lane shifted in gets 0
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+}
+
 // lsig (optional): this wave's 64-word LDS copy of the sector signature's new
 // bits — a created pair sets its 3 bits there (LDS atomics), and the sector's end
 // ORs each word into the global signature once (one atomic per non-zero word
@@ -111,7 +120,7 @@ template <typename S, int NT = LTAB_T, typename TB = Table, typename LT = LdsTab
 __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, uint32_t cnt, uint32_t a, uint32_t b,
                                 uint32_t nw, LT& lt, const TB& tb, DevState* st, uint32_t* __restrict__ sig,
                                 uint32_t& out_cnt, const uint32_t (&first)[5], const uint32_t (&firstm)[4],
-                                uint32_t* lsig BSP_ARG) {
+                                uint32_t* lsig, const uint32_t* nxt, const uint32_t* nxtm BSP_ARG) {
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     const int lane = threadIdx.x & 63;
     const uint32_t pid_ab = (a << 16) | b;
@@ -135,8 +144,10 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, ui
 #pragma unroll
             for (int k = 0; k < 4; ++k) M[k] = mp ? ((i0 + k < cnt) ? mp[i0 + k] : 0u) : 1u;
         }
-        uint32_t pm1 = __shfl_up(X[5], 1), pm2 = __shfl_up(X[4], 1);
-        uint32_t np = __shfl_down(X[2], 1);
+        // neighbours across lanes without the LDS crossbar (ds_bpermute queues behind
+        // the wave's and its CU's LDS atomics): DPP whole-wave shifts, readlane
+        uint32_t pm1 = wave_shr1(X[5]), pm2 = wave_shr1(X[4]);
+        uint32_t np = wave_shl1(X[2]);
         if (lane == 0) {
             pm1 = c1;
             pm2 = c2;
@@ -145,8 +156,8 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, ui
         X[0] = pm2;
         X[1] = pm1;
         X[6] = np;
-        c1 = __shfl(X[5], 63);
-        c2 = __shfl(X[4], 63);
+        c1 = __builtin_amdgcn_readlane(X[5], 63);
+        c2 = __builtin_amdgcn_readlane(X[4], 63);
         // h[j] = hit at the position of X[j]: a B-side (no word-start bit) after an a
         bool h[7];
         h[0] = false;
@@ -193,14 +204,28 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, ui
         BSP_CLK(q2);
         BSP_ADD(1, q2 - q1);
 #endif
+        // the wave's exclusive prefix of the kept counts from four ballots (one per
+        // symbol slot) and mbcnt: no LDS round trips
         const uint32_t kc = __popc(keep);
-        uint32_t incl = kc;
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t o = __shfl_up(incl, off);
-            if (lane >= off) incl += o;
+        uint32_t excl = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t m = __ballot((keep >> k) & 1u);
+            excl += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            tot += (uint32_t)__popcll(m);
         }
-        const uint32_t tot = __shfl(incl, 63);
+        const uint32_t incl = excl + kc;
         // every read of this pass happened above; writes land at or before their source
+        if (nxt) {
+            // the next sector's first pass (prefetched by the caller) is waited for
+            // here, before this pass's stores: gfx950 counts loads and stores in one
+            // vmcnt, so waiting for it at the next sector's start would drain these
+            // stores too (the compiler cannot count them: vmcnt(0))
+#pragma unroll
+            for (int k = 0; k < 5; ++k) asm volatile("" ::"v"(nxt[k]));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) asm volatile("" ::"v"(nxtm[k]));
+        }
         if (out != c0 || __any(touched)) {
             uint32_t w = out + incl - kc;
 #pragma unroll
@@ -223,7 +248,7 @@ __device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, ui
         const uint32_t v = atomicExch(&lsig[lane], 0u);
         if (v) atomicOr(&sig[lane], v);
     }
-    for (int off = 32; off > 0; off >>= 1) removed += __shfl_xor(removed, off);   // per lane → the wave's
+    removed = wave_sum_u32(removed);   // per lane → the wave's
 #ifdef GBPE_BSPROF
     BSP_ADD(3, clock64() - q4);
     BSP_ADD(5, 1ull);
@@ -343,12 +368,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
     if (t == 0) KT(3);
     // block exclusive scan of the kept counts; tail survivors sum to m
     const uint32_t kc = __popc(keep);
-    uint32_t incl = kc, tl = __popc(surv & ~below);
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(incl, off);
-        if (lane >= off) incl += o;
-    }
-    for (int off = 32; off > 0; off >>= 1) tl += __shfl_xor(tl, off);
+    const uint32_t incl = wave_scan_incl_u32(kc), tl = wave_sum_u32(__popc(surv & ~below));
     if (lane == 63) L.wsum[wid] = incl;
     if (lane == 0) L.wtail[wid] = tl;
     __syncthreads();
@@ -549,12 +569,7 @@ __device__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const 
     if (t == 0) KT(3);
     // local exclusive scan of the kept counts; tail survivors; the last kept symbol
     const uint32_t kc = __popc(keep);
-    uint32_t incl = kc, tl = __popc(surv & ~below);
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(incl, off);
-        if (lane >= off) incl += o;
-    }
-    for (int off = 32; off > 0; off >>= 1) tl += __shfl_xor(tl, off);
+    const uint32_t incl = wave_scan_incl_u32(kc), tl = wave_sum_u32(__popc(surv & ~below));
     if (lane == 63) L.wsum[wid] = incl;
     if (lane == 0) L.wtail[wid] = tl;
     __syncthreads();
@@ -625,11 +640,9 @@ __device__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const 
         }
         const bool in = (uint32_t)lane < nz;
         uint32_t sp = in && (uint32_t)lane < seg ? gk : 0u, sk = in ? gk : 0u, stt = in ? gt : 0u;
-        for (int off = 32; off > 0; off >>= 1) {
-            sp += __shfl_xor(sp, off);
-            sk += __shfl_xor(sk, off);
-            stt += __shfl_xor(stt, off);
-        }
+        sp = wave_sum_u32(sp);
+        sk = wave_sum_u32(sk);
+        stt = wave_sum_u32(stt);
         const unsigned long long hm = __ballot(in && (gl >> 31));
         if (lane == 0) {
             s_pre = sp;
@@ -702,10 +715,7 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     gsnap = &s_g.d;
     zsnap = &s_z.d;
     if (!(round < g.budget && g.merges_done == round && !g.stop && !g.sp_abort)) return false;
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(best, off);
-        best = o > best ? o : best;
-    }
+    best = wave_max_u64(best);
     if ((t & 63) == 0) s_red[t >> 6] = best;
     __syncthreads();
     best = s_red[0];
@@ -817,6 +827,11 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     // per wave: its sector's new signature bits (the 1024-thread forms: the early,
     // site-heavy merges; the 256-thread late form keeps 4 waves per SIMD without it)
     constexpr bool SIGL = SIG_LDS && BT == 1024;
+#ifdef GBPE_NO_SINK
+    constexpr bool SINK = false;
+#else
+    constexpr bool SINK = true;   // body_sector waits for the next sector's prefetch before its stores
+#endif
     __shared__ uint32_t s_sig[SIGL ? BT / 64 : 1][SP_SIGW];
     __shared__ uint32_t s_ntok, s_n, s_any, s_rm[BT / 64];
     __shared__ uint64_t s_mv[BT / 64];
@@ -953,7 +968,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
             uint32_t out = 0;
             const uint32_t r = body_sector<S, KB_LT, Table, LdsTab<KB_LT>, SIGL>(
                 body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, xtb, st, sig + (uint64_t)sct * SP_SIGW, out, cf,
-                cfm, s_sig[SIGL ? wid : 0] BSP_PASS);
+                cfm, s_sig[SIGL ? wid : 0], SINK ? nf : nullptr, SINK ? nfm : nullptr BSP_PASS);
             moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (r ? out : 0u));
             if (r) {
                 removed += r;

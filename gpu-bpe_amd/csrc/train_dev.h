@@ -30,6 +30,55 @@ template <> struct Sym<uint16_t> { static constexpr uint32_t WS = 0x8000u, TM = 
 template <> struct Sym<uint32_t> { static constexpr uint32_t WS = 0x10000u, TM = 0xFFFFu; };
 
 // device-side loop state (the reference's IterState, train.wgsl:45-58)
+// Whole-wave reductions and scan on the DPP paths (quad_perm, row mirrors,
+// row_shr, row_bcast) plus readlane: no ds_bpermute, which queues behind the
+// CU's LDS traffic.  Every lane of the wave must be active (as for __shfl_*).
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+    return ((uint64_t)dpp32<CTRL>((uint32_t)(v >> 32)) << 32) | dpp32<CTRL>((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);   // (readlane is int: no sign extension)
+}
+// the wave's maximum (uniform)
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+    uint64_t o = dpp64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v = o > v ? o : v;
+    o = dpp64<0x4E>(v);            // quad_perm [2,3,0,1]
+    v = o > v ? o : v;
+    o = dpp64<0x141>(v);           // row_half_mirror
+    v = o > v ? o : v;
+    o = dpp64<0x140>(v);           // row_mirror: every lane of a row holds the row's maximum
+    v = o > v ? o : v;
+    const uint64_t r0 = readlane64(v, 0), r1 = readlane64(v, 16), r2 = readlane64(v, 32), r3 = readlane64(v, 48);
+    const uint64_t a = r0 > r1 ? r0 : r1, b = r2 > r3 ? r2 : r3;
+    return a > b ? a : b;
+}
+// the wave's sum (uniform)
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    v += dpp32<0xB1>(v);
+    v += dpp32<0x4E>(v);
+    v += dpp32<0x141>(v);
+    v += dpp32<0x140>(v);
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+           __builtin_amdgcn_readlane(v, 48);
+}
+// inclusive prefix sum over the wave's lanes
+__device__ __forceinline__ uint32_t wave_scan_incl_u32(uint32_t v) {
+    v += dpp32<0x111>(v);          // row_shr:1 (lanes shifted in from outside the row add 0)
+    v += dpp32<0x112>(v);          // row_shr:2
+    v += dpp32<0x114>(v);          // row_shr:4
+    v += dpp32<0x118>(v);          // row_shr:8: each row scanned
+    v += dpp32<0x142, 0xA>(v);     // row_bcast:15 into rows 1 and 3
+    v += dpp32<0x143, 0xC>(v);     // row_bcast:31 into rows 2 and 3
+    return v;
+}
+
 struct DevState {
     uint32_t n;            // current symbol count
     uint32_t stop;         // early stop (mc < 2 or id > 0xFFFF)
@@ -601,11 +650,8 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
                     ++live;
                 }
             }
-            for (int off = 32; off > 0; off >>= 1) {
-                const uint64_t o = __shfl_xor(best, off);
-                best = o > best ? o : best;
-                live += __shfl_xor(live, off);
-            }
+            best = wave_max_u64(best);
+            live = wave_sum_u32(live);
             if (lane == 0) {
                 tb.bmax[blk] = best;
                 tb.blive[blk] = live;
@@ -616,11 +662,7 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
     }
     __syncthreads();
     if (part && threadIdx.x < 64) {   // this workgroup's maximum, for sel_inline
-        uint64_t best = s_bm[threadIdx.x];
-        for (int off = 32; off > 0; off >>= 1) {
-            const uint64_t o = __shfl_xor(best, off);
-            best = o > best ? o : best;
-        }
+        const uint64_t best = wave_max_u64(s_bm[threadIdx.x]);
         if (threadIdx.x == 0) {
             part[blockIdx.x] = best;
             if (finish == 2) KTR(5);
@@ -650,11 +692,8 @@ __device__ void select_merge(DevState* st, Table tb, uint32_t* __restrict__ log,
         best = v > best ? v : best;
         live += tb.blive[i];
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        uint64_t o = __shfl_xor(best, off);
-        best = o > best ? o : best;
-        live += __shfl_xor(live, off);
-    }
+    best = wave_max_u64(best);
+    live = wave_sum_u32(live);
     if ((threadIdx.x & 63) == 0) {
         red[threadIdx.x >> 6] = best;
         rlive[threadIdx.x >> 6] = live;
