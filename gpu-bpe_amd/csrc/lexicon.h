@@ -38,7 +38,7 @@ __global__ __launch_bounds__(TPB) void k_lx_count(const S* __restrict__ x, uint3
         const uint64_t i = base + (uint64_t)k * TPB + threadIdx.x;
         if (i < len) c += lx_is_start<S>(i ? (uint32_t)x[i - 1] : 0u, (uint32_t)x[i], i == 0) ? 1u : 0u;
     }
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    c = wave_sum_u32(c);
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(TPB) void k_lx_tabcount(const LxSlot* __restrict__ 
         const uint64_t i = lx_tslot(k);
         c += (i < P && wt[i].key) ? 1u : 0u;
     }
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    c = wave_sum_u32(c);
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -253,11 +253,7 @@ __global__ __launch_bounds__(TPB) void k_lx_tabuid(LxSlot* __restrict__ wt, uint
         occ |= ((e.x | e.y) ? 1u : 0u) << k;
     }
     const uint32_t c = (uint32_t)__popc(occ);
-    uint32_t incl = c;
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(incl, off);
-        if (lane >= off) incl += o;
-    }
+    const uint32_t incl = wave_scan_incl_u32(c);
     if (lane == 63) s[wid] = incl;
     __syncthreads();
     uint32_t u = bpre[blockIdx.x] + (uint32_t)bblk[blockIdx.x / SCAN_BLK] + incl - c;

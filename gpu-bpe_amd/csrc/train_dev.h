@@ -789,10 +789,7 @@ __global__ __launch_bounds__(1024) void k_topcount(Table tb, uint32_t* __restric
         const uint64_t v = tb.bmax[i];
         best = v > best ? v : best;
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(best, off);
-        best = o > best ? o : best;
-    }
+    best = wave_max_u64(best);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -807,7 +804,7 @@ __global__ __launch_bounds__(1024) void k_live(DevState* st, Table tb) {
     __shared__ uint32_t red[16];
     uint32_t live = 0;
     for (uint32_t i = threadIdx.x; i < tb.nblk; i += 1024) live += tb.blive[i];
-    for (int off = 32; off > 0; off >>= 1) live += __shfl_xor(live, off);
+    live = wave_sum_u32(live);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = live;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -855,7 +852,7 @@ __global__ __launch_bounds__(1024) void k_step_out(DevState* st, DevState* zst, 
 #pragma unroll
             for (int k = 0; k < 4; ++k) live += q[k].x + q[k].y + q[k].z + q[k].w;
         }
-        for (int off = 32; off > 0; off >>= 1) live += __shfl_xor(live, off);
+        live = wave_sum_u32(live);
         if ((t & 63) == 0) red[t >> 6] = live;
     }
     if (t < (uint32_t)NW) g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
@@ -950,11 +947,7 @@ __device__ void lds_dump(LdsTab<N>& t, const ZdrView& z, uint32_t w) {
             c[q] = s_cnt[tid * (ZDR_P / 64) + q];
             sum += c[q];
         }
-        uint32_t incl = sum;
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t o = __shfl_up(incl, off);
-            if ((int)tid >= off) incl += o;
-        }
+        const uint32_t incl = wave_scan_incl_u32(sum);
         uint32_t run = incl - sum;
         uint32_t* offs = z.offs + (uint64_t)w * (ZDR_P + 1);
 #pragma unroll
@@ -1077,7 +1070,7 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
     uint32_t cnt = __popc(inb & ~hitm);
     uint32_t tail = 0;
     const bool work = hbits != 0 || (i0 + EPT > lim && i0 < n);
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+    cnt = wave_sum_u32(cnt);
     const bool wave_work = __any(work);
     if (lane == 0) {
         red[wid] = cnt;
@@ -1142,7 +1135,7 @@ __global__ __launch_bounds__(TPB) void k_delta(DevState* st, uint32_t round, con
         }
         if (zv.out) lds_dump(lt, zv, tl);   // multi-tile zone pass: k_zdr adds the deltas
         else lds_flush(lt, tb, st);
-        for (int off = 32; off > 0; off >>= 1) tail += __shfl_xor(tail, off);
+        tail = wave_sum_u32(tail);
         if (lane == 0 && tail) atomicAdd(&st->m, tail);
     }
     // stores last: nothing waits on them
@@ -1235,7 +1228,7 @@ __global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, 
         const uint32_t h_32 = (nxr == b && (ea >> (EPT - 1)) && i0 + EPT < n) ? 1u : 0u;
         const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (EPT + 1));
         uint32_t cnt = __popc(inb & ~hitm);
-        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+        cnt = wave_sum_u32(cnt);
         if (hbits != 0 || (i0 + EPT > lim && i0 < n)) {
             const uint32_t below = lane_mask32(i0, lim);
             tail += __popc(inb & ~hitm & ~below);
@@ -1276,7 +1269,7 @@ __global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, 
     }
     if (zv.out) lds_dump(lt, zv, blockIdx.x);   // multi-tile zone pass: k_zdr adds the deltas
     else lds_flush(lt, tb, st);
-    for (int off = 32; off > 0; off >>= 1) tail += __shfl_xor(tail, off);
+    tail = wave_sum_u32(tail);
     if (lane == 0 && tail) atomicAdd(&st->m, tail);
 }
 
@@ -1344,7 +1337,7 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
             const uint32_t ngrp = (uint32_t)gbpe_div_up(ntiles, GRP);
             uint32_t sv = 0;
             for (uint32_t g = t; g < ngrp; g += CTPB) sv += grpsum[g * GSTR];
-            for (int off = 32; off > 0; off >>= 1) sv += __shfl_xor(sv, off);
+            sv = wave_sum_u32(sv);
             if (lane == 0) s_surv[wid] = sv;
             __syncthreads();
             sv = 0;
@@ -1369,7 +1362,7 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
                 const unsigned long long has = __ballot(inv != 0u);
                 if (has) {
                     const int l = __ffsll((long long)has) - 1;   // lowest lane = largest word index
-                    const uint32_t inv_l = __shfl(inv, l);
+                    const uint32_t inv_l = (uint32_t)__builtin_amdgcn_readlane(inv, l);
                     found = (uint32_t)((wi - l) * 32 + (31 - __clz(inv_l)));
                 }
                 wi -= 64;
@@ -1438,12 +1431,8 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
     }
     const uint32_t cnt = __popc(keep);
     // block exclusive scan of cnt + block sum of part
-    uint32_t incl = cnt;
-    for (int off = 1; off < 64; off <<= 1) {
-        uint32_t o = __shfl_up(incl, off);
-        if (lane >= off) incl += o;
-    }
-    for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+    const uint32_t incl = wave_scan_incl_u32(cnt);
+    part = wave_sum_u32(part);
     if (lane == 63) wsum[wid] = incl;
     if (lane == 0) psum[wid] = part;
     __syncthreads();
@@ -1533,7 +1522,7 @@ __global__ __launch_bounds__(CH_BT) void k_churn(DevState* zst, uint32_t round, 
         const uint32_t ngrp = (uint32_t)gbpe_div_up(ntiles, GRP);
         uint32_t sv = 0;
         for (uint32_t g = t; g < ngrp; g += CH_BT) sv += grpsum[g * GSTR];
-        for (int off = 32; off > 0; off >>= 1) sv += __shfl_xor(sv, off);
+        sv = wave_sum_u32(sv);
         if (lane == 0) s_surv[wid] = sv;
     }
     __syncthreads();
@@ -1561,7 +1550,7 @@ __global__ __launch_bounds__(CH_BT) void k_churn(DevState* zst, uint32_t round, 
                 const unsigned long long has = __ballot(inv != 0u);
                 if (has) {
                     const int l = __ffsll((long long)has) - 1;
-                    const uint32_t inv_l = __shfl(inv, l);
+                    const uint32_t inv_l = (uint32_t)__builtin_amdgcn_readlane(inv, l);
                     found = (uint32_t)((wi - l) * 32 + (31 - __clz(inv_l)));
                 }
                 wi -= 64;
