@@ -335,10 +335,7 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
             const uint64_t key = ((uint64_t)c << 32) | (uint32_t)~k;
             best = (k && (int32_t)c > 0 && key > best) ? key : best;
         }
-        for (int off = 32; off > 0; off >>= 1) {
-            const uint64_t o = __shfl_xor(best, off);
-            best = o > best ? o : best;
-        }
+        best = wave_max_u64(best);
         if (lane == 0) s_red[wid] = best;
         __syncthreads();
         best = s_red[0];
@@ -454,16 +451,8 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
         }
         // block scan of the kept counts; tail survivors sum to m; the first removed symbol below lim
         const uint32_t kc = __popc(keep);
-        uint32_t incl = kc, tl = __popc(surv & ~below);
-        uint32_t fh = (hitm & below) ? i0 + (uint32_t)(__ffs(hitm & below) - 1) : 0xFFFFFFFFu;
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t o = __shfl_up(incl, off);
-            if (lane >= off) incl += o;
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            tl += __shfl_xor(tl, off);
-            fh = min(fh, (uint32_t)__shfl_xor(fh, off));
-        }
+        const uint32_t incl = wave_scan_incl_u32(kc), tl = wave_sum_u32(__popc(surv & ~below));
+        const uint32_t fh = wave_min_u32((hitm & below) ? i0 + (uint32_t)(__ffs(hitm & below) - 1) : 0xFFFFFFFFu);
         if (lane == 63) s_sum[wid] = incl;
         if (lane == 0) {
             s_tl[wid] = tl;
@@ -606,11 +595,7 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
                 uint32_t pcn = 0;
 #pragma unroll
                 for (uint32_t q = 0; q < LATE_WW; ++q) pcn += __popc(bw[q]);
-                uint32_t cincl = pcn;
-                for (int off = 1; off < 64; off <<= 1) {
-                    const uint32_t o = __shfl_up(cincl, off);
-                    if (lane >= off) cincl += o;
-                }
+                const uint32_t cincl = wave_scan_incl_u32(pcn);
                 if (lane == 63) s_cs[wid] = cincl;
                 __syncthreads();   // (also: the fast list is no longer read)
                 uint32_t cpre = cincl - pcn, ncand = 0;
@@ -689,7 +674,7 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
             const unsigned long long bal = __ballot(live);
             uint32_t base = 0;
             if (lane == 0 && bal) base = atomicAdd(&s_logpos, (uint32_t)__popcll(bal));
-            base = __shfl(base, 0);
+            base = __builtin_amdgcn_readlane(base, 0);
             if (!live) continue;
             const uint32_t lp = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
             if (lp < out.dcap) out.dlog[lp] = make_uint2(k, d);
@@ -704,7 +689,7 @@ __global__ __launch_bounds__(LATE_BT) void k_late(DevState* st, DevState* zst, S
                 wmax = d > wmax ? d : wmax;
             }
         }
-        for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor(wmax, off));
+        wmax = wave_max_u32(wmax);
         if (lane == 0 && wmax) atomicMax(&pc[LC_WMAX], wmax);
         __syncthreads();   // hot set updated; s_wmax, s_rm, s_inval final
         LKT(4);

@@ -68,6 +68,23 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
            __builtin_amdgcn_readlane(v, 48);
 }
+// the wave's minimum / maximum of a u32 (uniform)
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, dpp32<0xB1>(v));
+    v = min(v, dpp32<0x4E>(v));
+    v = min(v, dpp32<0x141>(v));
+    v = min(v, dpp32<0x140>(v));
+    return min(min((uint32_t)__builtin_amdgcn_readlane(v, 0), (uint32_t)__builtin_amdgcn_readlane(v, 16)),
+               min((uint32_t)__builtin_amdgcn_readlane(v, 32), (uint32_t)__builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = max(v, dpp32<0xB1>(v));
+    v = max(v, dpp32<0x4E>(v));
+    v = max(v, dpp32<0x141>(v));
+    v = max(v, dpp32<0x140>(v));
+    return max(max((uint32_t)__builtin_amdgcn_readlane(v, 0), (uint32_t)__builtin_amdgcn_readlane(v, 16)),
+               max((uint32_t)__builtin_amdgcn_readlane(v, 32), (uint32_t)__builtin_amdgcn_readlane(v, 48)));
+}
 // inclusive prefix sum over the wave's lanes
 __device__ __forceinline__ uint32_t wave_scan_incl_u32(uint32_t v) {
     v += dpp32<0x111>(v);          // row_shr:1 (lanes shifted in from outside the row add 0)
