@@ -31,7 +31,7 @@ namespace {
 
 constexpr int LATE_BT = 1024;          // 16 waves (512 threads: no spills, but slower per merge: DESIGN §2d)
 constexpr uint32_t LATE_HS = 2048;     // hot-set slots (LDS hash: pid -> exact count), two per thread
-constexpr uint32_t LATE_K = 512;       // most pairs a refresh puts in the hot set
+constexpr uint32_t LATE_K = 1024;      // most pairs a refresh puts in the hot set
 constexpr uint32_t LATE_HP = 32;       // hot-set probes
 constexpr int LATE_LT = 4096;          // per-merge LDS delta table
 constexpr uint32_t LATE_CAP = LATE_BT; // candidate sectors per pass (one per thread)
@@ -47,13 +47,98 @@ struct LateDim {
     static constexpr uint32_t WB = ZCAP / 8 * 3;                 // window staging: mc <= z / 3 < 3/8 ZCAP
 };
 
-// the hot-set refresh between launches (k_hot_hist, k_hot_gather)
+constexpr uint32_t LATE_KB = 512;      // most table blocks the refresh gathers from (k_hot_sel)
+constexpr uint32_t LATE_BL = 1024;     // block list capacity (those plus any dirty block)
+
+// the hot-set refresh between launches (k_hot_sel + k_hot_gather_blocks; the
+// full-table k_hot_hist + k_hot_gather are the reference form)
 struct LateHot {
     uint32_t ticket, tau, nhot, ok;
-    uint32_t pad[12];
+    uint32_t nblist;
+    uint32_t pad[11];
     uint32_t hist[LATE_NB];
     uint2 list[LATE_K];
+    uint32_t blist[LATE_BL];
 };
+
+// tau from the table's block maxima (exact at a step boundary: k_refresh has
+// re-maxed every dirty block; a block still flagged dirty is listed anyway):
+// the smallest threshold with at most LATE_KB blocks whose maximum exceeds it.
+// Every pair above tau sits in one of those blocks, so gathering them is
+// complete; more than LATE_K such pairs leave the set unusable (the step runs
+// with k_body).  One workgroup: 4,096 block maxima at 1 GiB instead of the whole
+// table (two 8 MB passes and ~10^5 contended histogram atomics per launch).
+__global__ __launch_bounds__(1024) void k_hot_sel(Table tb, LateHot* __restrict__ h) {
+    __shared__ uint32_t sh[LATE_NB];
+    __shared__ uint32_t s_red[16], s_min[16], s_n, s_tau;
+    const uint32_t t = threadIdx.x;
+    const int lane = t & 63, wid = t >> 6;
+    for (uint32_t i = t; i < LATE_NB; i += 1024) sh[i] = 0u;
+    if (t == 0) s_n = 0u;
+    __syncthreads();
+    for (uint32_t b = t; b < tb.nblk; b += 1024) {
+        const uint32_t c = tb.dirty[b] ? LATE_NB - 1 : (uint32_t)(tb.bmax[b] >> 32);
+        if (c) atomicAdd(&sh[c < LATE_NB - 1 ? c : LATE_NB - 1], 1u);
+    }
+    __syncthreads();
+    constexpr uint32_t PER = LATE_NB / 1024;
+    uint32_t v[PER], tot = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        v[j] = sh[t * PER + j];
+        tot += v[j];
+    }
+    // blocks above this thread's bins: the wave's inclusive scan from the top, then the waves above
+    const uint32_t incl_up = wave_sum_u32(tot) - wave_scan_incl_u32(tot) + tot;   // lanes >= this one
+    if (lane == 0) s_red[wid] = incl_up;
+    __syncthreads();
+    uint32_t above = incl_up - tot;
+    for (int w2 = wid + 1; w2 < 16; ++w2) above += s_red[w2];
+    uint32_t run = above, cmin = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = PER - 1; j >= 0; --j) {
+        run += v[j];
+        const uint32_t c = t * PER + (uint32_t)j;
+        if (c >= 1u && run <= LATE_KB) cmin = c;
+    }
+    cmin = wave_min_u32(cmin);
+    if (lane == 0) s_min[wid] = cmin;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t c = s_min[0];
+        for (int w2 = 1; w2 < 16; ++w2) c = min(c, s_min[w2]);
+        s_tau = c != 0xFFFFFFFFu ? c - 1u : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const uint32_t tau = s_tau;
+    if (tau != 0xFFFFFFFFu)
+        for (uint32_t b = t; b < tb.nblk; b += 1024)
+            if (tb.dirty[b] || (uint32_t)(tb.bmax[b] >> 32) > tau) {
+                const uint32_t i = atomicAdd(&s_n, 1u);
+                if (i < LATE_BL) h->blist[i] = b;
+            }
+    __syncthreads();
+    if (t == 0) {
+        h->tau = tau;
+        h->ok = tau != 0xFFFFFFFFu && s_n <= LATE_BL ? 1u : 0u;
+        h->nblist = s_n < LATE_BL ? s_n : LATE_BL;
+        h->nhot = 0u;
+    }
+}
+
+// every pair above tau of the listed blocks into the hot list (one slot per thread)
+__global__ __launch_bounds__(256) void k_hot_gather_blocks(Table tb, LateHot* __restrict__ h) {
+    if (!h->ok) return;
+    const uint32_t tau = h->tau, nb = h->nblist;
+    for (uint32_t j = blockIdx.x; j < nb; j += gridDim.x) {
+        const uint64_t slot = ((uint64_t)h->blist[j] << BLK_LOG2) + threadIdx.x;
+        const uint2 e = tb.slots[slot];
+        if (e.x && (int32_t)e.y > (int32_t)tau) {
+            const uint32_t p = atomicAdd(&h->nhot, 1u);
+            if (p < LATE_K) h->list[p] = e;
+        }
+    }
+}
 
 // Count histogram of the live pairs (bins clamped at LATE_NB - 1); the last
 // workgroup picks tau: the smallest threshold with at most LATE_K pairs above

@@ -98,7 +98,8 @@ struct gbpe_trainer {
     uint32_t sub_k = 16;            // (the zone shrinks between them; GBPE_SUBSTEP_ZONE, GBPE_SUBSTEP)
     bool zone16 = true;             // u16 zones of 8K-16K symbols: the 16-per-thread zone pass 
     // the late-merge loop (k_late): one workgroup runs a step's merges
-    bool late_on = true;         // GBPE_DEBUG late=0: off
+    bool late_on = false;        // GBPE_DEBUG late=1: the one-workgroup late loop (§2d)
+    uint32_t late_mc = 1200;     // ... once a merge's count is at most this (GBPE_DEBUG late_mc)
     bool late_skip = false;      // its last launch could not run a merge: this step runs k_body
     LateHot* late_hot = nullptr; // hot-set refresh state
     uint2* late_log = nullptr;   // the launch's count deltas (k_late_apply)
@@ -484,7 +485,10 @@ inline uint32_t late_zcap(const gbpe_trainer* t) {
 inline bool late_eligible(const gbpe_trainer* t) {
     const uint32_t zc = late_zcap(t);
     const uint32_t z = (uint32_t)t->n - t->h_st->B;
-    return t->late_on && !t->late_skip && t->sp && !t->d_clog && z <= zc &&
+    // (a store of more than 128K sectors has more bitmap words than one pass of the
+    // loop's fast candidate path: its batched path measured ~70 us per merge)
+    return t->late_on && !t->late_skip && t->sp && !t->d_clog && t->last_mc <= t->late_mc && t->W <= LATE_WW * LATE_BT &&
+           z <= zc &&
            (uint32_t)((uint32_t)t->n - t->h_st->Bp) <= zc && t->zcap >= zc;
 }
 
@@ -520,9 +524,8 @@ int launch_late(gbpe_trainer* t, hipStream_t s, uint32_t g_refresh, bool timing)
     int rc = late_alloc(t);
     if (rc != GBPE_OK) return rc;
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
-    const uint32_t gh = grid_persistent(t->ctx, gbpe_div_up(((uint64_t)t->tb.mask + 1) / 2, 256), 1);
-    hipLaunchKernelGGL(k_hot_hist, dim3(gh), dim3(256), 0, s, t->tb, t->late_hot);
-    hipLaunchKernelGGL(k_hot_gather, dim3(gh), dim3(256), 0, s, t->tb, t->late_hot);
+    hipLaunchKernelGGL(k_hot_sel, dim3(1), dim3(1024), 0, s, t->tb, t->late_hot);
+    hipLaunchKernelGGL(k_hot_gather_blocks, dim3(LATE_KB), dim3(256), 0, s, t->tb, t->late_hot);
     LateOut lo;
     lo.dlog = t->late_log;
     lo.dcap = t->late_logcap;
@@ -1263,7 +1266,7 @@ int sp_shrink(gbpe_trainer* t) {
     const uint32_t z = (uint32_t)t->n - hs->B;
     const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
     // a zone just above the late loop's LDS buffers shrinks to its target at once
-    const bool to_late = t->late_on && z > late_zcap(t) && zt + 1024 <= late_zcap(t);
+    const bool to_late = t->late_on && t->last_mc <= t->late_mc && z > late_zcap(t) && zt + 1024 <= late_zcap(t);
     if (t->sp_shrinks >= SP_SHRINKS_MAX || (!to_late && (uint64_t)z < zt * t->shrink_pct / 100 + 4096)) return GBPE_OK;
     S* zc = (S*)t->zbuf[t->zcur];
     S* zo = (S*)t->zbuf[t->zcur ^ 1];
@@ -1381,7 +1384,8 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->rehash_on = gbpe_debug_knob("rehash", 1) != 0;
     t->delta_mt = (uint32_t)gbpe_debug_knob("delta_mt", t->delta_mt);
     t->sp_zt = (uint32_t)gbpe_debug_knob("zt", t->sp_zt);
-    t->late_on = gbpe_debug_knob("late", 0) != 0;   // (off until it beats k_body: DESIGN §2d)
+    t->late_on = gbpe_debug_knob("late", 0) != 0;
+    t->late_mc = (uint32_t)gbpe_debug_knob("late_mc", 1200);   // the loop runs once a merge's count is at most this   // (off until it beats k_body: DESIGN §2d)
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
         t->trace = fopen(e, "w");
