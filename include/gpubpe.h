@@ -179,7 +179,8 @@ typedef struct gbpe_trainer_stats {
     uint64_t lexicon_words;       /* body word occurrences the lexicon represents (all builds and shrinks) */
     uint64_t lexicon_entries;     /* distinct-word entries of the current lexicon */
     uint64_t lexicon_symbols;     /* symbols of the current lexicon store (separators included) */
-    uint64_t late_merges;         /* merges run by the one-workgroup late-merge loop k_late */
+    uint64_t late_merges;         /* merges run by the one-workgroup late-merge loop k_late (off
+                                     unless GBPE_DEBUG=late=1: 0 by default) */
     uint64_t late_launches;       /* its launches (one per step) */
     uint64_t late_exits;          /* ... that ended before their step's budget (the hot-set bound; host refreshes) */
     double   ms_late;             /* GBPE_TRAIN_TIMING: device ms of k_late (included in ms_sparse) */
