@@ -897,16 +897,16 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
             s_n = 0u;
         }
         __syncthreads();
-        if (t < (int)SP_PW && w0 + t < w_end) {   // token candidates
+        if (t < (int)SP_PW) {   // token candidates (one wave: list positions from its scan, no LDS counter)
             const uint32_t w = w0 + t;
-            uint32_t c = bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w];
-            if (c) {
-                uint32_t pos = atomicAdd(&s_ntok, (uint32_t)__popc(c));
-                while (c) {
-                    const int bit = __ffs(c) - 1;
-                    c &= c - 1;
-                    cb.sec[pos++] = w * 32u + (uint32_t)bit;
-                }
+            uint32_t c = w < w_end ? bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w] : 0u;
+            const uint32_t pc = (uint32_t)__popc(c), incl = wave_scan_incl_u32(pc);
+            uint32_t pos = incl - pc;
+            if (t == (int)SP_PW - 1) s_ntok = incl;
+            while (c) {
+                const int bit = __ffs(c) - 1;
+                c &= c - 1;
+                cb.sec[pos++] = w * 32u + (uint32_t)bit;
             }
         }
         __syncthreads();
@@ -934,12 +934,17 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         }
         __syncthreads();   // every candidate is read before the list is rewritten
 #pragma unroll
-        for (int q = 0; q < QPT; ++q)
+        for (int q = 0; q < QPT; ++q) {   // one LDS counter add per wave, positions from the ballot
+            const unsigned long long m = __ballot(ck[q]);
+            uint32_t base = 0;
+            if (lane == 0 && m) base = atomicAdd(&s_n, (uint32_t)__popcll(m));
+            base = __builtin_amdgcn_readlane(base, 0);
             if (ck[q]) {
-                const uint32_t qq = atomicAdd(&s_n, 1u);
+                const uint32_t qq = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                 cb.sec[qq] = cs[q];
                 cb.ext[qq] = ce[q];
             }
+        }
         __syncthreads();
         const uint32_t ncand = s_n;
         if (t == 0) KT(3);
