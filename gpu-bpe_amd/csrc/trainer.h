@@ -1386,6 +1386,9 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->sp_zt = (uint32_t)gbpe_debug_knob("zt", t->sp_zt);
     t->late_on = gbpe_debug_knob("late", 0) != 0;
     t->late_mc = (uint32_t)gbpe_debug_knob("late_mc", 1200);   // the loop runs once a merge's count is at most this   // (off until it beats k_body: DESIGN §2d)
+    t->refresh_blocks = (uint32_t)gbpe_debug_knob("rfb", t->refresh_blocks);   // k_refresh grid sweeps
+    t->refresh_late = (uint32_t)gbpe_debug_knob("rfl", t->refresh_late);
+    t->refresh_late_z = (uint32_t)gbpe_debug_knob("rflz", t->refresh_late_z);
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
         t->trace = fopen(e, "w");
