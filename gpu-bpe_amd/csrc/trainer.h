@@ -1389,6 +1389,9 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->refresh_blocks = (uint32_t)gbpe_debug_knob("rfb", t->refresh_blocks);   // k_refresh grid sweeps
     t->refresh_late = (uint32_t)gbpe_debug_knob("rfl", t->refresh_late);
     t->refresh_late_z = (uint32_t)gbpe_debug_knob("rflz", t->refresh_late_z);
+    t->lx_div = (uint32_t)std::max<long>(1, gbpe_debug_knob("lxdiv", t->lx_div));   // lexicon entry / sub-step sweeps
+    t->sub_k = (uint32_t)std::max<long>(1, gbpe_debug_knob("subk", t->sub_k));
+    t->sub_zone = (uint32_t)std::max<long>(1, gbpe_debug_knob("subz", t->sub_zone));
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
         t->trace = fopen(e, "w");
