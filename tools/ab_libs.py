@@ -5,7 +5,8 @@ compared with its committed oracle fixture.
 
     python tools/ab_libs.py gpu-bpe_amd/lib/A/libgpubpe.so gpu-bpe_amd/lib/B/libgpubpe.so:GBPE_X=0 -- en1g c2 code1g
 
-(a library may carry environment settings after a colon)
+(a library may carry environment settings after a colon, separated by "@", so
+that a GBPE_DEBUG value can hold commas: lib.so:GBPE_DEBUG=zt=4,subk=8@X=1)
 
 Each library runs in its own child process (one .so per process); the runs
 alternate A, B, A, B so drift on the box hits both alike.
@@ -27,6 +28,7 @@ CONF = {
     "en1g": (lambda: synth.english(1 << 30, seed=2, fancy_punct=0.005), 32768, 0),
     "ml1g": (lambda: synth.multilingual(1 << 30, seed=3), 32768, 0),
     "code1g": (lambda: synth.code(1 << 30, seed=6), 50000, _lib.GBPE_TRAIN_GPT4_BOUNDARIES),
+    "ml1g64k": (lambda: synth.multilingual(1 << 30, seed=5), 65536, 0),   # bench.py's C4 shard (u32)
 }
 lib = _lib.load(sys.argv[2])
 ctx = C.c_void_p()
@@ -83,10 +85,10 @@ def main():
     rounds = int(os.environ.get("AB_ROUNDS", "2"))
     res = {}
     for r in range(rounds):
-        for lp in libs:   # "path" or "path:ENV=V,ENV2=V2"
+        for lp in libs:   # "path" or "path:ENV=V@ENV2=V2"
             path, _, envs = lp.partition(":")
             env = dict(os.environ)
-            env.update(kv.split("=", 1) for kv in envs.split(",") if kv)
+            env.update(kv.split("=", 1) for kv in envs.split("@") if kv)
             p = subprocess.run([sys.executable, "-c", CHILD, ROOT, os.path.abspath(path), str(reps)] + names,
                                capture_output=True, text=True, timeout=600, env=env)
             for line in p.stdout.splitlines():
