@@ -9,7 +9,8 @@ compared with its committed oracle fixture.
 that a GBPE_DEBUG value can hold commas: lib.so:GBPE_DEBUG=zt=4,subk=8@X=1)
 
 Each library runs in its own child process (one .so per process); the runs
-alternate A, B, A, B so drift on the box hits both alike.
+alternate A, B, A, B so drift on the box hits both alike.  AB_TABLE_LOG2 sets
+the trainer's table_log2 option (0 = sized by the trainer).
 """
 import json
 import os
@@ -43,7 +44,7 @@ for name in sys.argv[4:]:
     _lib.check(lib.gbpe_memcpy_h2d(ctx, d, data, len(data)), ctx, "h2d")
     for rep in range(reps + 1):   # the first run warms up
         opts = _lib.TrainOpts(target_vocab_size=vocab, vocab_size=256, next_token_id=256, batch_size=128,
-                              flags=flags, table_log2=0)
+                              flags=flags, table_log2=int(os.environ.get("AB_TABLE_LOG2", "0")))
         tr = C.c_void_p()
         lib.gbpe_synchronize(ctx)
         t0 = time.perf_counter()
@@ -69,7 +70,8 @@ for name in sys.argv[4:]:
             print(json.dumps({"name": name, "s": round(t1 - t0, 4), "s_first4k": round((t4k or t1) - t0, 4),
                               "merges": int(m.shape[0]), "equal": eq,
                               "late": [int(st.late_merges), int(st.late_launches), int(st.late_exits),
-                                       int(st.late_bound_exits)], "sparse_exits": int(st.sparse_exits)}), flush=True)
+                                       int(st.late_bound_exits)], "sparse_exits": int(st.sparse_exits),
+                              "table_slots": int(st.table_slots), "max_live_pairs": int(st.max_live_pairs)}), flush=True)
         if not eq:
             print(json.dumps({"name": name, "error": "merges differ from the fixture"}), flush=True)
             sys.exit(3)
