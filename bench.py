@@ -224,16 +224,14 @@ def train_detail(st, sk):
         "max_live_pairs": int(st.max_live_pairs), "table_slots": int(st.table_slots),
         "sparse": {"merges": int(st.sparse_merges), "enters": int(st.sparse_enters), "exits": int(st.sparse_exits),
                    "sectors": int(st.sparse_sectors), "zone_at_entry": int(st.sparse_zone)},
-        "late": {"merges": int(st.late_merges), "launches": int(st.late_launches), "early_ends": int(st.late_exits),
-                 "bound_ends": int(st.late_bound_exits)},
+        "close": {"inlaunch": int(st.close_inlaunch), "remax_blocks": int(st.close_remax_blocks)},
+        "ms_create": round(st.ms_create, 3),
         "events": None if sk is None else {
             "merges": int(sk.timed_merges), "dense_merges": int(sk.timed_merges - sk.sparse_merges),
             "dense_bytes": int(sk.dense_bytes), "ms_dense": sk.ms_dense,
             "sparse_merges": int(sk.sparse_merges), "body_bytes": int(sk.body_bytes), "zone_bytes": int(sk.zone_bytes),
             "ms_body": sk.ms_body, "ms_sparse": sk.ms_sparse, "ms_select": sk.ms_select, "ms_refresh": sk.ms_other,
-            "ms_delta": sk.ms_delta, "ms_compact": sk.ms_compact,
-            "late_merges": int(sk.late_merges), "late_launches": int(sk.late_launches), "late_bytes": int(sk.late_bytes),
-            "ms_late": sk.ms_late},
+            "ms_delta": sk.ms_delta, "ms_compact": sk.ms_compact},
     }
 
 
@@ -254,9 +252,7 @@ def _rocprof_kernel(prefix: str):
 def train_roofline(det, wall_per_run):
     """Roofline of the dominant training kernel from the HIP-event run.
 
-    The sparse merges run in k_body, one launch per merge (the one-workgroup
-    late loop k_late runs them only under GBPE_DEBUG=late=1: measured slower,
-    DESIGN §2d).  Each kernel's bytes are the ones it moves (candidate extents and signatures,
+    The sparse merges run in k_body, one launch per merge.  Each kernel's bytes are the ones it moves (candidate extents and signatures,
     sector symbols read and rewritten, the zone pass) — pair-table traffic
     excluded as in SURVEY §8(d).  The kernel with the larger share of the run's
     device time is the roofline kernel; the other is reported beside it.  The
@@ -292,13 +288,9 @@ def train_roofline(det, wall_per_run):
                                  "times are slightly inflated")
         return k
 
-    late = kern("late", ev["late_bytes"], ev["ms_late"], ev["late_launches"], ev["late_merges"], "k_late<",
-                "k_late (the late-merge loop: one 1024-thread workgroup runs a step's merges, zone in LDS, "
-                "hot-set selection; DESIGN §2d)") if ev else None
-    body = kern("body", ev["body_bytes"], ev["ms_body"], ev["sparse_merges"] - ev["late_merges"],
-                ev["sparse_merges"] - ev["late_merges"], "k_body<",
+    body = kern("body", ev["body_bytes"], ev["ms_body"], ev["sparse_merges"], ev["sparse_merges"], "k_body<",
                 "k_body (sector-sparse merge pass over the word lexicon, one launch per merge)") if ev else None
-    cand = [k for k in (late, body) if k]
+    cand = [k for k in (body,) if k]
     roof = max(cand, key=lambda k: k["ms_per_run"]) if cand else {
         "bound": "hbm", "kernel": None, "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None,
         "traffic": None}

@@ -35,9 +35,91 @@ static const char* const kKernelNames[] = {
     "k_me_compact",      // its token compaction
 };
 
+// ── context memory pool (common.h GbpePool) ───────────────────────────────
+static uint64_t pool_class(uint64_t b) {
+    if (b < 256) return 256;
+    uint64_t p2 = 256;
+    while (p2 < b) p2 <<= 1;
+    if (p2 <= (64u << 10)) return p2;
+    const uint64_t step = p2 >> 3;   // <= 1/8 slack above 64 KiB
+    return (b + step - 1) / step * step;
+}
+
+static void pool_release(GbpePool& pl, bool host, uint64_t keep) {
+    while (pl.idle_bytes > keep && !pl.idle.empty()) {
+        auto it = std::prev(pl.idle.end());   // largest first
+        if (host) hipHostFree(it->second);
+        else hipFree(it->second);
+        pl.idle_bytes -= it->first;
+        pl.idle.erase(it);
+    }
+}
+
+// GBPE_DEBUG poison=1: every pool block handed out is filled with 0xA5 first (tests:
+// no trainer buffer may rely on a fresh allocation's contents)
+static void pool_poison(gbpe_ctx* ctx, void* p, uint64_t cls, bool host) {
+    static const bool on = gbpe_debug_knob("poison", 0) != 0;
+    if (!on) return;
+    if (host) memset(p, 0xA5, cls);
+    else (void)hipMemsetAsync(p, 0xA5, cls, ctx->stream);
+}
+
+hipError_t gbpe_pool_alloc(gbpe_ctx* ctx, void** p, uint64_t bytes, bool host) {
+    *p = nullptr;
+    const uint64_t cls = pool_class(bytes ? bytes : 1);
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
+    GbpePool& pl = host ? ctx->hpool : ctx->dpool;
+    auto it = pl.idle.lower_bound(cls);
+    if (it != pl.idle.end() && it->first <= cls + cls / 4) {
+        *p = it->second;
+        pl.busy[*p] = it->first;
+        pl.idle_bytes -= it->first;
+        pl.idle.erase(it);
+        ++pl.hits;
+        pool_poison(ctx, *p, pl.busy[*p], host);
+        return hipSuccess;
+    }
+    ++pl.misses;
+    hipError_t e = host ? hipHostMalloc(p, cls, hipHostMallocDefault) : hipMalloc(p, cls);
+    if (e != hipSuccess) {   // idle blocks back to the device, then once more
+        (void)hipGetLastError();
+        pool_release(pl, host, 0);
+        e = host ? hipHostMalloc(p, cls, hipHostMallocDefault) : hipMalloc(p, cls);
+    }
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return e;
+    }
+    pl.busy[*p] = cls;
+    pool_poison(ctx, *p, cls, host);
+    return hipSuccess;
+}
+
+void gbpe_pool_free(gbpe_ctx* ctx, void* p, bool host) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
+    GbpePool& pl = host ? ctx->hpool : ctx->dpool;
+    auto it = pl.busy.find(p);
+    if (it == pl.busy.end()) {   // (not a pool block)
+        if (host) hipHostFree(p);
+        else hipFree(p);
+        return;
+    }
+    pl.idle.emplace(it->second, p);
+    pl.idle_bytes += it->second;
+    pl.busy.erase(it);
+    pool_release(pl, host, host ? (1ull << 30) : ctx->total_mem / 2);
+}
+
+void gbpe_pool_trim(gbpe_ctx* ctx) {
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
+    pool_release(ctx->dpool, false, 0);
+    pool_release(ctx->hpool, true, 0);
+}
+
 extern "C" {
 
-const char* gbpe_version(void) { return "gpubpe 0.4 (gfx950, abi 3)"; }
+const char* gbpe_version(void) { return "gpubpe 0.5 (gfx950, abi 4)"; }
 
 int gbpe_abi_version(void) { return GBPE_ABI_VERSION; }
 
@@ -91,6 +173,7 @@ void gbpe_ctx_destroy(gbpe_ctx* ctx) {
     hipFree(ctx->enc_out);
     hipFree(ctx->pt_agg);
     if (ctx->enc_host_total) hipHostFree(ctx->enc_host_total);
+    gbpe_pool_trim(ctx);   // (blocks still busy belong to trainers the caller did not destroy)
     for (auto& ev : ctx->ev)
         if (ev) hipEventDestroy(ev);
     if (ctx->copy_stream) {
@@ -123,7 +206,11 @@ const char* gbpe_last_error(const gbpe_ctx* ctx) { return ctx ? ctx->err.c_str()
 
 int gbpe_device_alloc(gbpe_ctx* ctx, uint64_t bytes, void** dptr) {
     if (!ctx || !dptr) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");
-    GBPE_HIP(ctx, hipMalloc(dptr, bytes ? bytes : 1));
+    if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess) {   // the pool's idle blocks first
+        (void)hipGetLastError();
+        gbpe_pool_trim(ctx);
+        GBPE_HIP(ctx, hipMalloc(dptr, bytes ? bytes : 1));
+    }
     return GBPE_OK;
 }
 

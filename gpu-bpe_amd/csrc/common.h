@@ -6,10 +6,27 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/gpubpe.h"
+
+// Memory pool of a context (the header's "the library owns and pools device
+// memory"; the reference pools its GPU buffers, tokenizer.js:30-46, 108-166):
+// the buffers a trainer or shard frees go back to the pool and the next one of the
+// context takes them (the same stream orders every use), so creating and
+// destroying a trainer costs no hipMalloc / hipFree once the pool is warm.  Sizes
+// round up to classes of <= 1/8 slack; a miss allocates; an allocation that finds
+// no memory frees the idle blocks and tries again; idle blocks above half the
+// device's memory are freed at once.
+struct GbpePool {
+    std::multimap<uint64_t, void*> idle;          // class bytes -> block
+    std::unordered_map<void*, uint64_t> busy;     // block -> class bytes
+    uint64_t idle_bytes = 0, hits = 0, misses = 0;
+};
 
 struct gbpe_ctx {
     int device = 0;
@@ -28,7 +45,20 @@ struct gbpe_ctx {
     void* pt_agg = nullptr;       uint64_t pt_agg_bytes = 0;   // pre-tokenizer block aggregates
     hipEvent_t ev[8] = {};
     double enc_ms[3] = {0, 0, 0};
+    GbpePool dpool, hpool;   // device / pinned host blocks of trainers and shards
+    std::mutex pool_mu;
 };
+
+// pooled allocations (api.hip); host = pinned host memory (hipHostMalloc)
+hipError_t gbpe_pool_alloc(gbpe_ctx* ctx, void** p, uint64_t bytes, bool host = false);
+void gbpe_pool_free(gbpe_ctx* ctx, void* p, bool host = false);
+void gbpe_pool_trim(gbpe_ctx* ctx);
+template <typename T>
+inline hipError_t pool_malloc(gbpe_ctx* c, T** p, uint64_t n) { return gbpe_pool_alloc(c, (void**)p, n); }
+inline void pool_free(gbpe_ctx* c, void* p) { gbpe_pool_free(c, p); }
+template <typename T>
+inline hipError_t pool_hmalloc(gbpe_ctx* c, T** p, uint64_t n) { return gbpe_pool_alloc(c, (void**)p, n, true); }
+inline void pool_hfree(gbpe_ctx* c, void* p) { gbpe_pool_free(c, p, true); }
 
 // ── error helpers ──────────────────────────────────────────────────────────
 int gbpe_set_error(gbpe_ctx* ctx, int code, const char* fmt, ...);
@@ -44,6 +74,15 @@ int gbpe_set_error(gbpe_ctx* ctx, int code, const char* fmt, ...);
     } while (0)
 
 #define GBPE_LAUNCH_CHECK(ctx) GBPE_HIP(ctx, hipGetLastError())
+
+// runs `f` when the scope ends (device buffers of a call freed on every return path)
+template <typename F>
+struct GbpeScopeExit {
+    F f;
+    ~GbpeScopeExit() { f(); }
+};
+template <typename F>
+GbpeScopeExit<F> gbpe_scope_exit(F f) { return GbpeScopeExit<F>{f}; }
 
 // ── device helpers ─────────────────────────────────────────────────────────
 __device__ __forceinline__ uint32_t gbpe_fmix32(uint32_t x) {

@@ -44,6 +44,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     if (n == 0) return gbpe_set_error(ctx, GBPE_E_EMPTY, "No symbols to train on — corpus is empty after pre-processing");
     if (!bytes) return gbpe_set_error(ctx, GBPE_E_INVALID, "bytes is null");
     if (n >= 0xFFFFFFF0ull) return gbpe_set_error(ctx, GBPE_E_INVALID, "corpus too large for one device (%llu symbols)", (unsigned long long)n);
+    const auto t_create0 = std::chrono::steady_clock::now();
     auto* t = new (std::nothrow) gbpe_trainer();
     if (!t) return gbpe_set_error(ctx, GBPE_E_OOM, "host allocation failed");
     trainer_config(t, ctx, opts);
@@ -63,7 +64,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     const uint64_t ntiles0 = gbpe_div_up(n + cap_extra, TILE);
     t->cap_syms = (ntiles0 + 1) * TILE;
     for (int k = 0; k < 2; ++k) {
-        if (hipMalloc(&t->buf[k], t->cap_syms * t->bps) != hipSuccess)
+        if (pool_malloc(t->ctx, &t->buf[k], t->cap_syms * t->bps) != hipSuccess)
             return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(symbols) failed"));
         // both ping-pong buffers start zeroed, as WebGPU zero-initialises buffers
         if (hipMemsetAsync(t->buf[k], 0, t->cap_syms * t->bps, s) != hipSuccess)
@@ -84,19 +85,19 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     const uint64_t slots = 1ull << lg;
     t->tb.mask = (uint32_t)(slots - 1);
     t->tb.nblk = (uint32_t)(slots >> BLK_LOG2);
-    if (hipMalloc(&t->tb.slots, slots * sizeof(uint2)) != hipSuccess ||
-        hipMalloc(&t->tb.bmax, t->tb.nblk * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc(&t->tb.dirty, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->tb.dlist, (t->tb.nblk + 1) * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->hitmask, (ntiles0 + 1) * TPB * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->tile_cnt, (ntiles0 + 1) * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->grpsum, (ntiles0 / GRP + 2) * GSTR * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->st, sizeof(DevState)) != hipSuccess ||
-        hipMalloc(&t->d_log, (size_t)t->batch * 4 * sizeof(uint32_t)) != hipSuccess)
+    if (pool_malloc(t->ctx, &t->tb.slots, slots * sizeof(uint2)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tb.bmax, t->tb.nblk * sizeof(uint64_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tb.dirty, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tb.dlist, (t->tb.nblk + 1) * sizeof(uint32_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->hitmask, (ntiles0 + 1) * TPB * sizeof(uint32_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tile_cnt, (ntiles0 + 1) * sizeof(uint32_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->grpsum, (ntiles0 / GRP + 2) * GSTR * sizeof(uint32_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->st, sizeof(DevState)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->d_log, (size_t)t->batch * 4 * sizeof(uint32_t)) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(training buffers) failed"));
-    if (hipHostMalloc((void**)&t->h_st, sizeof(DevState), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&t->h_log, (size_t)t->batch * 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+    if (pool_hmalloc(t->ctx, &t->h_st, sizeof(DevState)) != hipSuccess ||
+        pool_hmalloc(t->ctx, &t->h_log, (size_t)t->batch * 4 * sizeof(uint32_t)) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipHostMalloc failed"));
     t->tb.used = &t->st->used;
     t->g_refresh = grid_blocks(ctx, t->tb.nblk, 2);
@@ -122,6 +123,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
                 if (hipEventCreate(&e) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "hipEventCreate failed"));
         }
         if (hipStreamSynchronize(s) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "trainer init failed"));
+        t->ms_create = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_create0).count();
         *out = t;
         return GBPE_OK;
     };
@@ -130,12 +132,12 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         const uint32_t* d_prev = si->prev;
         void* tmp = nullptr;
         if (!input_on_device) {
-            if (hipMalloc(&tmp, (n + si->n_prev) * 4 + 4) != hipSuccess)
+            if (pool_malloc(t->ctx, &tmp, (n + si->n_prev) * 4 + 4) != hipSuccess)
                 return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(state) failed"));
             uint32_t* h = (uint32_t*)tmp;
             if (hipMemcpyAsync(h, bytes, n * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
                 (si->n_prev && hipMemcpyAsync(h + n, si->prev, si->n_prev * 4, hipMemcpyHostToDevice, s) != hipSuccess)) {
-                hipFree(tmp);
+                pool_free(t->ctx, tmp);
                 return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "state upload failed"));
             }
             d_cur = h;
@@ -154,7 +156,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         const bool launched = hipGetLastError() == hipSuccess;
         int rc = launched ? table_rebuild(t) : gbpe_set_error(ctx, GBPE_E_DEVICE, "symbol import launch failed");
         hipStreamSynchronize(s);
-        hipFree(tmp);
+        pool_free(t->ctx, tmp);
         if (rc != GBPE_OK) return fail(rc);
         return finish();
     }
@@ -164,10 +166,10 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     void* tmp = nullptr;
     if (!input_on_device) {
         const uint64_t need = n * (word_starts ? 2 : 1);
-        if (hipMalloc(&tmp, need) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(input) failed"));
+        if (pool_malloc(t->ctx, &tmp, need) != hipSuccess) return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(input) failed"));
         if (hipMemcpyAsync(tmp, bytes, n, hipMemcpyHostToDevice, s) != hipSuccess ||
             (word_starts && hipMemcpyAsync((uint8_t*)tmp + n, word_starts, n, hipMemcpyHostToDevice, s) != hipSuccess)) {
-            hipFree(tmp);
+            pool_free(t->ctx, tmp);
             return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "input upload failed"));
         }
         d_bytes = (const uint8_t*)tmp;
@@ -175,10 +177,10 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     }
     uint8_t* d_gpt4 = nullptr;   // GPT-4 rule word starts computed on the device (pre_tokenizer.mjs:226-292)
     if (!d_ws && (opts->flags & GBPE_TRAIN_GPT4_BOUNDARIES)) {
-        int rc2 = hipMalloc(&d_gpt4, n) == hipSuccess ? gbpe_pretok_gpt4_launch(ctx, d_bytes, n, d_gpt4) : GBPE_E_OOM;
+        int rc2 = pool_malloc(t->ctx, &d_gpt4, n) == hipSuccess ? gbpe_pretok_gpt4_launch(ctx, d_bytes, n, d_gpt4) : GBPE_E_OOM;
         if (rc2 != GBPE_OK) {
-            if (tmp) hipFree(tmp);
-            hipFree(d_gpt4);
+            if (tmp) pool_free(t->ctx, tmp);
+            pool_free(t->ctx, d_gpt4);
             return fail(rc2 == GBPE_E_OOM ? gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(word starts) failed") : rc2);
         }
         d_ws = d_gpt4;
@@ -197,14 +199,14 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
         hipLaunchKernelGGL(k_symbols<uint32_t>, dim3(gb), dim3(TPB), 0, s, d_bytes, d_ws, (uint32_t*)t->buf[0], n,
                            (uint8_t*)nullptr);
     if (hipGetLastError() != hipSuccess) {
-        if (tmp) hipFree(tmp);
+        if (tmp) pool_free(t->ctx, tmp);
         return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "symbol kernel launch failed"));
     }
     int rc = table_rebuild(t, true);
     if (tmp || d_gpt4) {
         hipStreamSynchronize(s);
-        hipFree(tmp);
-        hipFree(d_gpt4);
+        pool_free(t->ctx, tmp);
+        pool_free(t->ctx, d_gpt4);
     }
     if (rc != GBPE_OK) return fail(rc);
     return finish();
@@ -237,10 +239,10 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     // rebuild the pair table when it gets crowded (dead pairs accumulate), twice as
     // large (or more) while the live pairs would fill over a quarter of it
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
-    if ((uint64_t)t->h_st->used * 2 > slots) {
+    if ((uint64_t)t->h_st->used * 100 > slots * t->grow_used_pct) {
         const uint64_t live = std::max<uint64_t>(t->h_st->live, t->h_st->used / 2);
         uint32_t lg = t->table_log2;
-        while (lg < 28 && live * 4 > (1ull << lg)) ++lg;
+        while (lg < 28 && live * 100 > (1ull << lg) * t->grow_live_pct) ++lg;
         int rc;
         if (t->sp && t->rehash_on) {   // the sparse loop goes on over the moved entries
             rc = table_rehash(t, lg);
@@ -265,7 +267,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         // then ends only a one-merge dense step (enter_lim below)
         uint32_t mc = t->last_mc, next = 0;
         if (t->lex_on) {
-            if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
+            if (!t->d_u32) TR_HIP(t, pool_malloc(t->ctx, &t->d_u32, 64));
             hipLaunchKernelGGL(k_topcount, dim3(1), dim3(1024), 0, s, t->tb, t->d_u32);
             GBPE_LAUNCH_CHECK(t->ctx);
             TR_HIP(t, hipMemcpyAsync(&next, t->d_u32, 4, hipMemcpyDeviceToHost, s));
@@ -313,7 +315,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         static unsigned long long* kbuf = nullptr;
         if (!kbuf) {
             const size_t nb = (size_t)(KT_MERGES / KT_EVERY) * 2 * KT_WG * KT_SLOTS * 8;
-            TR_HIP(t, hipMalloc(&kbuf, nb));
+            TR_HIP(t, pool_malloc(t->ctx, &kbuf, nb));
             TR_HIP(t, hipMemsetAsync(kbuf, 0, nb, s));
             TR_HIP(t, hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ktr), &kbuf, sizeof(kbuf), 0, hipMemcpyHostToDevice, s));
         }
@@ -361,7 +363,9 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         // sooner.  The partial maxima the next k_body reads are laid out per k_refresh
         // workgroup, so a grid change re-lays them out once (finish 0: no merge closed)
         if (t->refresh_late && zn <= t->refresh_late_z) {
-            const uint32_t want = std::max<uint32_t>(t->refresh_late, (uint32_t)gbpe_div_up(t->tb.nblk, 64));
+            // (at most one workgroup per block: the partial maxima hold nblk + 1 per half)
+            const uint32_t want = std::min<uint32_t>(t->tb.nblk,
+                                                     std::max<uint32_t>(t->refresh_late, (uint32_t)gbpe_div_up(t->tb.nblk, 64)));
             if (want != t->g_refresh) {
                 t->g_refresh = g_refresh = want;
                 if (t->u16)
@@ -377,9 +381,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         }
         sg.refresh = g_refresh;
     }
-    const bool late = sparse && late_eligible(t);
     auto launch_all = [&]() -> int {
-        if (late) return t->u16 ? launch_late<uint16_t>(t, s, g_refresh, timing) : launch_late<uint32_t>(t, s, g_refresh, timing);
         for (uint32_t r = 0; r < k; ++r) {
             hipEvent_t* ev = timing ? &t->evs[5 * r] : nullptr;
             int rc;
@@ -418,6 +420,19 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         TR_HIP(t, hipMemcpyToSymbol(HIP_SYMBOL(g_bsprof), z, sizeof(z), 0, hipMemcpyHostToDevice));
     }
 #endif
+    if (sparse && hs->refresh_due) {   // an in-launch close flagged more blocks than it re-maxes: their dirty
+                                       // flags are set, the step's later launches ran no merge
+        if (t->u16)
+            hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
+                               (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr,
+                               FusedSel(), t->part, (uint32_t*)nullptr);
+        else
+            hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
+                               (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr,
+                               FusedSel(), t->part, (uint32_t*)nullptr);
+        GBPE_LAUNCH_CHECK(t->ctx);
+        hs->refresh_due = 0u;
+    }
     const uint32_t err = hs->err | (sparse ? t->h_zst->err : 0u);
     if (err) {
         return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "training invariant violated (err=0x%x: %s%s%s%s%s)", err,
@@ -427,18 +442,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
                               (err & ERR_SPARSE_WINDOW) ? "sparse stale window outside the zone " : "",
                               (err & ERR_SPIN) ? "zone segment hand-off timed out" : "");
     }
-    if (late) {
-        ++t->late_launches;
-        t->late_merges += done;
-        if (done < k && !hs->stop && !hs->sp_abort) ++t->late_exits;
-        if (timing) {
-            float ms = 0;
-            hipEventElapsedTime(&ms, t->late_ev[0], t->late_ev[1]);
-            t->ms_late += ms;
-            t->ms_sparse += ms;
-            t->timed_merges += done;
-        }
-    } else if (timing) {
+    if (timing) {
         for (uint32_t r = 0; r < done; ++r) {
             float a = 0, b = 0, c = 0, d1 = 0, d2 = 0;
             hipEvent_t* ev = &t->evs[5 * r];
@@ -456,12 +460,6 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
             if (sparse) t->ms_body += d1;
         }
         t->timed_merges += done;
-    }
-    if (late && done == 0 && !hs->stop && !hs->sp_abort) {   // the hot set could not select: k_body runs this step
-        t->late_skip = true;
-        int rc = trainer_step_once(t, max_merges, merges_out, n_done, early_stop);
-        t->late_skip = false;
-        return rc;
     }
     // algorithmic stream bytes: s * (2 N_i + N_{i+1})
     uint64_t N = t->n;
@@ -556,23 +554,21 @@ extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
     o->ms_dense = t->ms_dense;
     o->ms_sparse = t->ms_sparse;
     o->ms_body = t->ms_body;
+    if (t->cls) {
+        CloseState h{};
+        if (hipMemcpy(&h, t->cls, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+            o->close_inlaunch = h.closes;
+            o->close_remax_blocks = h.remax;
+            o->close_refreshes = h.ovf;
+        }
+    }
+    o->ms_create = t->ms_create;
     o->zone_bytes = t->h_st->sp_bytes;
     o->lexicon_builds = (uint32_t)t->lx_builds;
     o->lexicon_fallbacks = (uint32_t)t->lx_fallbacks;
     o->lexicon_words = t->lx_words;
     o->lexicon_entries = t->lx_nuid;
     o->lexicon_symbols = t->lx_len;
-    o->late_merges = t->late_merges;
-    o->late_launches = t->late_launches;
-    o->late_exits = t->late_exits;
-    o->ms_late = t->ms_late;
-    if (t->late_u32) {
-        uint32_t h[8] = {};
-        if (hipMemcpy(h, t->late_u32, 32, hipMemcpyDeviceToHost) == hipSuccess) {
-            o->late_bytes = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
-            o->late_bound_exits = h[1];
-        }
-    }
     if (t->wg_bytes && t->wg_cap) {   // the per-workgroup counters of k_body (and its zone workgroup)
         std::vector<uint64_t> h(t->wg_cap);
         if (hipMemcpy(h.data(), t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess)
@@ -592,7 +588,7 @@ extern "C" int gbpe_trainer_symbols(gbpe_trainer* t, uint32_t* out, uint64_t cap
     }
     hipStream_t s = t->ctx->stream;
     uint32_t* d = nullptr;
-    TR_HIP(t, hipMalloc(&d, (uint64_t)t->n * 4 + 4));
+    TR_HIP(t, pool_malloc(t->ctx, &d, (uint64_t)t->n * 4 + 4));
     const uint32_t g = (uint32_t)gbpe_div_up(t->n, 256);
     if (t->n) {
         if (t->u16)
@@ -604,7 +600,7 @@ extern "C" int gbpe_trainer_symbols(gbpe_trainer* t, uint32_t* out, uint64_t cap
     }
     hipError_t e = hipMemcpyAsync(out, d, (uint64_t)t->n * 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    hipFree(d);
+    pool_free(t->ctx, d);
     if (e != hipSuccess) return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "symbol export failed: %s", hipGetErrorString(e));
     return GBPE_OK;
 }
@@ -633,7 +629,7 @@ extern "C" int gbpe_trainer_export_state(gbpe_trainer* t, uint32_t* cur, uint64_
         return gbpe_set_error(t->ctx, GBPE_E_CAPACITY, "export_state: need %llu + %llu", (unsigned long long)n,
                               (unsigned long long)np);
     uint32_t* d = nullptr;
-    if (!on_device) TR_HIP(t, hipMalloc(&d, (n + np) * 4 + 4));
+    if (!on_device) TR_HIP(t, pool_malloc(t->ctx, &d, (n + np) * 4 + 4));
     auto exp = [&](const void* src, uint32_t* dst, uint64_t cnt) {
         if (!cnt || !dst) return;
         const uint32_t g = (uint32_t)gbpe_div_up(cnt, 256);
@@ -650,7 +646,7 @@ extern "C" int gbpe_trainer_export_state(gbpe_trainer* t, uint32_t* cur, uint64_
         if (e == hipSuccess && prev && np) e = hipMemcpyAsync(prev, d + n, np * 4, hipMemcpyDeviceToHost, s);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    hipFree(d);
+    pool_free(t->ctx, d);
     if (e != hipSuccess) return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "state export failed: %s", hipGetErrorString(e));
     return GBPE_OK;
 }
@@ -660,7 +656,7 @@ extern "C" int gbpe_trainer_pair_counts(gbpe_trainer* t, uint32_t* pids, uint32_
     hipStream_t s = t->ctx->stream;
     uint32_t* d = nullptr;
     const uint64_t c = cap ? cap : 1;
-    TR_HIP(t, hipMalloc(&d, (2 * c + 1) * sizeof(uint32_t)));
+    TR_HIP(t, pool_malloc(t->ctx, &d, (2 * c + 1) * sizeof(uint32_t)));
     hipError_t e = hipMemsetAsync(d, 0, sizeof(uint32_t), s);
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
     hipLaunchKernelGGL(k_dump_pairs, dim3((uint32_t)gbpe_div_up(slots, 256)), dim3(256), 0, s, t->tb, d + 1, d + 1 + c,
@@ -672,7 +668,7 @@ extern "C" int gbpe_trainer_pair_counts(gbpe_trainer* t, uint32_t* pids, uint32_
         e = hipMemcpy(pids, d + 1, (uint64_t)cnt * 4, hipMemcpyDeviceToHost);
         if (e == hipSuccess) e = hipMemcpy(counts, d + 1 + c, (uint64_t)cnt * 4, hipMemcpyDeviceToHost);
     }
-    hipFree(d);
+    pool_free(t->ctx, d);
     if (e != hipSuccess) return gbpe_set_error(t->ctx, GBPE_E_DEVICE, "pair dump failed: %s", hipGetErrorString(e));
     *n = cnt;
     if (cnt > cap) return gbpe_set_error(t->ctx, GBPE_E_CAPACITY, "pair dump: need %u", cnt);
@@ -700,51 +696,48 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
 #endif
     for (auto& e : t->evs)
         if (e) hipEventDestroy(e);
-    hipFree(t->buf[0]);
-    hipFree(t->buf[1]);
-    hipFree(t->tb.slots);
-    hipFree(t->tb.bmax);
-    hipFree(t->tb.dirty);
-    hipFree(t->tb.dlist);
-    hipFree(t->tb.blive);
-    hipFree(t->hitmask);
-    hipFree(t->tile_cnt);
-    hipFree(t->grpsum);
-    hipFree(t->sec);
-    hipFree(t->sp_loc);
-    hipFree(t->sp_blk);
-    hipFree(t->bits);
-    hipFree(t->sig);
-    hipFree(t->zbuf[0]);
-    hipFree(t->zbuf[1]);
-    hipFree(t->wtmp);
-    hipFree(t->zst);
-    hipFree(t->d_u32);
-    hipFree(t->part);
-    hipFree(t->d_bhist);
-    hipFree(t->zseg);
-    hipFree(t->zdr_out);
-    hipFree(t->late_hot);
-    hipFree(t->late_log);
-    hipFree(t->late_u32);
-    for (auto& e : t->late_ev)
-        if (e) hipEventDestroy(e);
-    hipFree(t->zdr_offs);
-    hipFree(t->zdr_flag);
-    hipFree(t->wg_bytes);
-    hipFree(t->lx_store);
-    hipFree(t->lx_mul);
-    hipFree(t->lx_occ);
-    hipFree(t->lx_w0);
-    hipFree(t->lx_tmp);
-    if (t->h_zst) hipHostFree(t->h_zst);
-    hipFree(t->d_clog);
-    if (t->h_clog) hipHostFree(t->h_clog);
+    pool_free(t->ctx, t->buf[0]);
+    pool_free(t->ctx, t->buf[1]);
+    pool_free(t->ctx, t->tb.slots);
+    pool_free(t->ctx, t->tb.bmax);
+    pool_free(t->ctx, t->tb.dirty);
+    pool_free(t->ctx, t->tb.dlist);
+    pool_free(t->ctx, t->tb.blive);
+    pool_free(t->ctx, t->hitmask);
+    pool_free(t->ctx, t->tile_cnt);
+    pool_free(t->ctx, t->grpsum);
+    pool_free(t->ctx, t->sec);
+    pool_free(t->ctx, t->sp_loc);
+    pool_free(t->ctx, t->sp_blk);
+    pool_free(t->ctx, t->bits);
+    pool_free(t->ctx, t->sig);
+    pool_free(t->ctx, t->zbuf[0]);
+    pool_free(t->ctx, t->zbuf[1]);
+    pool_free(t->ctx, t->wtmp);
+    pool_free(t->ctx, t->zst);
+    pool_free(t->ctx, t->d_u32);
+    pool_free(t->ctx, t->part);
+    pool_free(t->ctx, t->fbits);
+    pool_free(t->ctx, t->cls);
+    pool_free(t->ctx, t->d_bhist);
+    pool_free(t->ctx, t->zseg);
+    pool_free(t->ctx, t->zdr_out);
+    pool_free(t->ctx, t->zdr_offs);
+    pool_free(t->ctx, t->zdr_flag);
+    pool_free(t->ctx, t->wg_bytes);
+    pool_free(t->ctx, t->lx_store);
+    pool_free(t->ctx, t->lx_mul);
+    pool_free(t->ctx, t->lx_occ);
+    pool_free(t->ctx, t->lx_w0);
+    pool_free(t->ctx, t->lx_tmp);
+    if (t->h_zst) pool_hfree(t->ctx, t->h_zst);
+    pool_free(t->ctx, t->d_clog);
+    if (t->h_clog) pool_hfree(t->ctx, t->h_clog);
     if (t->trace) fclose(t->trace);
-    hipFree(t->st);
-    hipFree(t->d_log);
-    if (t->h_st) hipHostFree(t->h_st);
-    if (t->h_log) hipHostFree(t->h_log);
+    pool_free(t->ctx, t->st);
+    pool_free(t->ctx, t->d_log);
+    if (t->h_st) pool_hfree(t->ctx, t->h_st);
+    if (t->h_log) pool_hfree(t->ctx, t->h_log);
     delete t;
 }
 
@@ -798,14 +791,14 @@ extern "C" int gbpe_word_boundary(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t 
     if (n == 0) return GBPE_OK;
     hipStream_t s = ctx->stream;
     uint8_t* d = nullptr;
-    GBPE_HIP(ctx, hipMalloc(&d, 2 * n));
+    GBPE_HIP(ctx, pool_malloc(ctx, &d, 2 * n));
     hipError_t e = hipMemcpyAsync(d, bytes, n, hipMemcpyHostToDevice, s);
     hipLaunchKernelGGL(k_symbols<uint32_t>, dim3((uint32_t)gbpe_div_up(n, TPB)), dim3(TPB), 0, s, d,
                        (const uint8_t*)nullptr, (uint32_t*)nullptr, n, d + n);
     if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(ws_out, d + n, n, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    hipFree(d);
+    pool_free(ctx, d);
     if (e != hipSuccess) return gbpe_set_error(ctx, GBPE_E_DEVICE, "word boundary failed: %s", hipGetErrorString(e));
     return GBPE_OK;
 }

@@ -108,9 +108,9 @@ int ls_build(gbpe_lexshard* ls, uint64_t zone_target) {
     ls->nu = lp.nu;
     ls->nw = lp.nw;
     const uint64_t T = lp.T;
-    if (hipMalloc(&ls->store, (T + 64) * ls->bps) != hipSuccess || hipMalloc(&ls->mul, (T + 64) * 4) != hipSuccess ||
-        hipMalloc(&ls->occ, (lp.nw + 1) * 4) != hipSuccess ||
-        (ls->z && hipMalloc(&ls->zone, (ls->z + 64) * ls->bps) != hipSuccess))
+    if (pool_malloc(ls->ctx, &ls->store, (T + 64) * ls->bps) != hipSuccess ||
+        pool_malloc(ls->ctx, &ls->mul, (T + 64) * 4) != hipSuccess || pool_malloc(ls->ctx, &ls->occ, (lp.nw + 1) * 4) != hipSuccess ||
+        (ls->z && pool_malloc(ls->ctx, &ls->zone, (ls->z + 64) * ls->bps) != hipSuccess))
         return gbpe_set_error(ls->ctx, GBPE_E_OOM, "lexshard: hipMalloc(store) failed");
     if (lp.nu)
         hipLaunchKernelGGL(k_lx_fill<S>, dim3((uint32_t)gbpe_div_up(lp.nu, 256)), dim3(256), 0, s, cur,
@@ -181,9 +181,9 @@ int lex_root_build(gbpe_trainer* t, const S* store, const uint32_t* mul, uint64_
     if (z) TR_HIP(t, hipMemcpyAsync(t->zbuf[0], zone, z * t->bps, hipMemcpyDeviceToDevice, s));
     // the zone passes' tile scratch
     const uint64_t ntz = gbpe_div_up(t->zcap, TILE) + 1;
-    if (hipMalloc(&t->hitmask, ntz * TPB * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->tile_cnt, ntz * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->grpsum, (ntz / GRP + 2) * GSTR * sizeof(uint32_t)) != hipSuccess)
+    if (pool_malloc(t->ctx, &t->hitmask, ntz * TPB * sizeof(uint32_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tile_cnt, ntz * sizeof(uint32_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->grpsum, (ntz / GRP + 2) * GSTR * sizeof(uint32_t)) != hipSuccess)
         return gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(zone scratch) failed");
     TR_HIP(t, hipMemsetAsync(t->hitmask, 0, ntz * TPB * sizeof(uint32_t), s));
     // pair counts: the store weighted by its multiplicities, plus the zone
@@ -249,14 +249,14 @@ extern "C" int gbpe_lexshard_create(gbpe_ctx* ctx, const uint8_t* bytes, uint64_
     gbpe_trainer* t = ls->t;
     hipStream_t s = ctx->stream;
     // the piece never merges: drop the other ping-pong buffer and the stream-pass scratch
-    hipFree(t->buf[t->cur ^ 1]);
+    pool_free(t->ctx, t->buf[t->cur ^ 1]);
     t->buf[t->cur ^ 1] = nullptr;
-    hipFree(t->hitmask);
+    pool_free(t->ctx, t->hitmask);
     t->hitmask = nullptr;
     ls->u16 = t->u16;
     ls->bps = t->bps;
     ls->n = t->n;
-    if (!t->d_u32 && hipMalloc(&t->d_u32, 64) != hipSuccess) {
+    if (!t->d_u32 && pool_malloc(t->ctx, &t->d_u32, 64) != hipSuccess) {
         gbpe_lexshard_destroy(ls);
         return gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc failed");
     }
@@ -325,7 +325,7 @@ extern "C" int gbpe_lexshard_remap(gbpe_lexshard* ls, const uint32_t* map, uint6
     if (!ls->built || ls->remapped) return gbpe_set_error(ls->ctx, GBPE_E_INVALID, "lexshard_remap: not built or done");
     hipStream_t s = ls->ctx->stream;
     uint32_t* d = nullptr;
-    GBPE_HIP(ls->ctx, hipMalloc(&d, (n_map + 1) * 4 + 8));
+    GBPE_HIP(ls->ctx, pool_malloc(ls->ctx, &d, (n_map + 1) * 4 + 8));
     hipError_t e = hipMemsetAsync(d, 0, 4, s);
     if (e == hipSuccess && n_map)
         e = hipMemcpyAsync(d + 1, map, n_map * 4, map_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s);
@@ -337,7 +337,7 @@ extern "C" int gbpe_lexshard_remap(gbpe_lexshard* ls, const uint32_t* map, uint6
     uint32_t bad = 0;
     if (e == hipSuccess) e = hipMemcpyAsync(&bad, d, 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    hipFree(d);
+    pool_free(ls->ctx, d);
     if (e != hipSuccess) return gbpe_set_error(ls->ctx, GBPE_E_DEVICE, "lexshard_remap: %s", hipGetErrorString(e));
     if (bad) return gbpe_set_error(ls->ctx, GBPE_E_INVALID, "lexshard_remap: a word id outside the map");
     ls->remapped = true;
@@ -348,10 +348,10 @@ extern "C" void gbpe_lexshard_destroy(gbpe_lexshard* ls) {
     if (!ls) return;
     if (ls->ctx && ls->ctx->stream) hipStreamSynchronize(ls->ctx->stream);
     if (ls->t) gbpe_trainer_destroy(ls->t);
-    hipFree(ls->store);
-    hipFree(ls->mul);
-    hipFree(ls->occ);
-    hipFree(ls->zone);
+    pool_free(ls->ctx, ls->store);
+    pool_free(ls->ctx, ls->mul);
+    pool_free(ls->ctx, ls->occ);
+    pool_free(ls->ctx, ls->zone);
     delete ls;
 }
 
@@ -391,11 +391,11 @@ extern "C" int gbpe_trainer_create_from_lexicon(gbpe_ctx* ctx, const void* store
     if (lg > 28) lg = 28;
     int rc = table_resize(t, lg);
     if (rc != GBPE_OK) return fail(rc);
-    if (hipMalloc(&t->st, sizeof(DevState)) != hipSuccess ||
-        hipMalloc(&t->d_log, (size_t)t->batch * 4 * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->d_u32, 64) != hipSuccess ||
-        hipHostMalloc((void**)&t->h_st, sizeof(DevState), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&t->h_log, (size_t)t->batch * 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+    if (pool_malloc(t->ctx, &t->st, sizeof(DevState)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->d_log, (size_t)t->batch * 4 * sizeof(uint32_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->d_u32, 64) != hipSuccess ||
+        pool_hmalloc(t->ctx, &t->h_st, sizeof(DevState)) != hipSuccess ||
+        pool_hmalloc(t->ctx, &t->h_log, (size_t)t->batch * 4 * sizeof(uint32_t)) != hipSuccess)
         return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(training state) failed"));
     t->tb.used = &t->st->used;
     TR_HIP(t, hipMemsetAsync(t->d_u32, 0, 64, s));
@@ -411,13 +411,13 @@ extern "C" int gbpe_trainer_create_from_lexicon(gbpe_ctx* ctx, const void* store
     const void* d_zone = zone;
     void* tmp = nullptr;
     if (!input_on_device) {
-        if (hipMalloc(&tmp, store_len * (bps + 4) + zone_len * bps + 64) != hipSuccess)
+        if (pool_malloc(t->ctx, &tmp, store_len * (bps + 4) + zone_len * bps + 64) != hipSuccess)
             return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(hand-over input) failed"));
         char* p = (char*)tmp;
         if ((store_len && (hipMemcpyAsync(p, store, store_len * bps, hipMemcpyHostToDevice, s) != hipSuccess ||
                            hipMemcpyAsync(p + store_len * bps, mul, store_len * 4, hipMemcpyHostToDevice, s) != hipSuccess)) ||
             hipMemcpyAsync(p + store_len * (bps + 4), zone, zone_len * bps, hipMemcpyHostToDevice, s) != hipSuccess) {
-            hipFree(tmp);
+            pool_free(t->ctx, tmp);
             return fail(gbpe_set_error(ctx, GBPE_E_DEVICE, "hand-over upload failed"));
         }
         d_store = p;
@@ -426,8 +426,8 @@ extern "C" int gbpe_trainer_create_from_lexicon(gbpe_ctx* ctx, const void* store
     }
     rt.mark("upload");
     uint32_t* d_map = nullptr;
-    if (hipMalloc(&d_map, (store_len / 2 + 2) * 4) != hipSuccess) {
-        hipFree(tmp);
+    if (pool_malloc(t->ctx, &d_map, (store_len / 2 + 2) * 4) != hipSuccess) {
+        pool_free(t->ctx, tmp);
         return fail(gbpe_set_error(ctx, GBPE_E_OOM, "hipMalloc(map) failed"));
     }
     uint64_t nm = 0;
@@ -444,8 +444,8 @@ extern "C" int gbpe_trainer_create_from_lexicon(gbpe_ctx* ctx, const void* store
     }
     hipStreamSynchronize(s);
     rt.mark("map");
-    hipFree(d_map);
-    hipFree(tmp);
+    pool_free(t->ctx, d_map);
+    pool_free(t->ctx, tmp);
     *n_map = nm;
     if (rc != GBPE_OK) return fail(rc);
     *out = t;
@@ -459,14 +459,18 @@ int trainer_expand(gbpe_trainer* t, const uint32_t* d_prefix, uint64_t n_prefix,
     const uint64_t nown = t->lx_nocc, no = n_prefix + nown;
     uint32_t* occ = nullptr;
     S* tmp = nullptr;
+    auto release = gbpe_scope_exit([&] {   // every return path, TR_HIP's included
+        pool_free(t->ctx, tmp);
+        pool_free(t->ctx, occ);
+    });
     const uint64_t z = (uint32_t)t->n - t->h_st->B;
-    TR_HIP(t, hipMalloc(&occ, (no + 1) * 4));
+    TR_HIP(t, pool_malloc(t->ctx, &occ, (no + 1) * 4));
     if (n_prefix) TR_HIP(t, hipMemcpyAsync(occ, d_prefix, n_prefix * 4, hipMemcpyDeviceToDevice, s));
     if (nown) TR_HIP(t, hipMemcpyAsync(occ + n_prefix, t->lx_occ, nown * 4, hipMemcpyDeviceToDevice, s));
     // the body's total, then the zone after it
     uint64_t tot = 0;
-    if (hipMalloc(&tmp, (t->n + 64) * sizeof(S)) != hipSuccess) {
-        hipFree(occ);
+    if (pool_malloc(t->ctx, &tmp, (t->n + 64) * sizeof(S)) != hipSuccess) {
+        tmp = nullptr;
         return gbpe_set_error(t->ctx, GBPE_E_OOM, "expand: hipMalloc(%llu symbols) failed", (unsigned long long)t->n);
     }
     int rc = lx_expand<S>(t, tmp, t->n - z, &tot, occ, no);   // (checks the total before writing)
@@ -481,8 +485,6 @@ int trainer_expand(gbpe_trainer* t, const uint32_t* d_prefix, uint64_t n_prefix,
         GBPE_LAUNCH_CHECK(t->ctx);
         TR_HIP(t, hipStreamSynchronize(s));
     }
-    hipFree(tmp);
-    hipFree(occ);
     *total = tot + z;
     return rc;
 }
@@ -500,13 +502,21 @@ extern "C" int gbpe_trainer_expand(gbpe_trainer* t, const uint32_t* prefix_occ, 
     TR_HIP(t, hipStreamSynchronize(s));
     uint32_t* d_pre = nullptr;
     uint32_t* d_out = out_on_device ? out : nullptr;
+    uint32_t* d_own = nullptr;   // the staging output this call allocated
+    auto release = gbpe_scope_exit([&] {   // every return path, TR_HIP's included
+        pool_free(t->ctx, d_pre);
+        pool_free(t->ctx, d_own);
+    });
     if (n_prefix && !prefix_on_device) {
-        TR_HIP(t, hipMalloc(&d_pre, n_prefix * 4));
+        TR_HIP(t, pool_malloc(t->ctx, &d_pre, n_prefix * 4));
         TR_HIP(t, hipMemcpyAsync(d_pre, prefix_occ, n_prefix * 4, hipMemcpyHostToDevice, s));
     }
-    if (!d_out && hipMalloc(&d_out, t->n * 4 + 4) != hipSuccess) {
-        hipFree(d_pre);
-        return gbpe_set_error(t->ctx, GBPE_E_OOM, "expand: hipMalloc(output) failed");
+    if (!d_out) {
+        if (pool_malloc(t->ctx, &d_own, t->n * 4 + 4) != hipSuccess) {
+            d_own = nullptr;
+            return gbpe_set_error(t->ctx, GBPE_E_OOM, "expand: hipMalloc(output) failed");
+        }
+        d_out = d_own;
     }
     uint64_t tot = 0;
     int rc = t->u16 ? trainer_expand<uint16_t>(t, d_pre ? d_pre : prefix_occ, n_prefix, d_out, &tot)
@@ -514,8 +524,6 @@ extern "C" int gbpe_trainer_expand(gbpe_trainer* t, const uint32_t* prefix_occ, 
     if (rc == GBPE_OK && !out_on_device &&
         (hipMemcpy(out, d_out, t->n * 4, hipMemcpyDeviceToHost) != hipSuccess))
         rc = gbpe_set_error(t->ctx, GBPE_E_DEVICE, "expand: copy to host failed");
-    hipFree(d_pre);
-    if (!out_on_device) hipFree(d_out);
     *n_out = tot;
     return rc;
 }

@@ -6,7 +6,7 @@
 #include <cmath>
 
 #include "train_dev.h"
-#include "late.h"
+#include "sparse.h"
 
 
 // ─── host side ──────────────────────────────────────────────────────────────
@@ -68,7 +68,12 @@ struct gbpe_trainer {
     DevState* zst = nullptr;     // the zone's loop state
     DevState* h_zst = nullptr;   // pinned
     uint32_t* d_u32 = nullptr;   // small device scratch
-    uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
+    uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection), two halves of nblk + 1
+    uint32_t* fbits = nullptr;   // in-launch close: flagged argmax blocks (bitmap, nblk bits)
+    CloseState* cls = nullptr;   // in-launch close: ticket + stats (sparse.h)
+    uint32_t grow_used_pct = 50;   // the table is rebuilt once its occupied slots (dead included) pass this %
+    uint32_t grow_live_pct = 25;   // ... into the smallest 2^k slots its live pairs fill to at most this %
+    bool close_on = true;        // GBPE_DEBUG close=0: every sparse merge closes in k_refresh (A/B)
     uint2* zdr_out = nullptr;    // the multi-tile zone passes' delta dumps (ZdrView, train_dev.h)
     uint32_t* zdr_offs = nullptr;
     uint32_t* zdr_flag = nullptr;
@@ -83,6 +88,7 @@ struct gbpe_trainer {
     uint64_t wg_cap = 0;
     double ms_sparse = 0, ms_dense = 0;   // GBPE_TRAIN_TIMING: merge passes (without selection / refresh) by mode
     double ms_body = 0;          // GBPE_TRAIN_TIMING: k_body alone
+    double ms_create = 0;        // host wall time of trainer creation
     uint64_t dense_bytes = 0;    // algorithmic stream bytes of the dense merges
     uint32_t g_refresh = 0;
     uint64_t sp_merges = 0, sp_sectors = 0, sp_zone = 0;
@@ -97,17 +103,6 @@ struct gbpe_trainer {
     uint32_t sub_zone = 1u << 20;   // sparse steps run in sub-steps of sub_k merges while the zone exceeds this
     uint32_t sub_k = 16;            // (the zone shrinks between them; GBPE_SUBSTEP_ZONE, GBPE_SUBSTEP)
     bool zone16 = true;             // u16 zones of 8K-16K symbols: the 16-per-thread zone pass 
-    // the late-merge loop (k_late): one workgroup runs a step's merges
-    bool late_on = false;        // GBPE_DEBUG late=1: the one-workgroup late loop (§2d)
-    uint32_t late_mc = 1200;     // ... once a merge's count is at most this (GBPE_DEBUG late_mc)
-    bool late_skip = false;      // its last launch could not run a merge: this step runs k_body
-    LateHot* late_hot = nullptr; // hot-set refresh state
-    uint2* late_log = nullptr;   // the launch's count deltas (k_late_apply)
-    uint32_t late_logcap = 0;
-    uint32_t* late_u32 = nullptr;   // [0] log entries, [1..2] launch-end causes, [4..5] bytes (u64)
-    uint64_t late_merges = 0, late_launches = 0, late_exits = 0;
-    double ms_late = 0;
-    hipEvent_t late_ev[2] = {nullptr, nullptr};
     uint32_t sp_zt = 5;          // zone target = sp_zt * last_mc + 64 (>= zone_f; GBPE_DEBUG zt; 4/5/6/7 measured
                                  // 0.895/0.893/0.918/0.918 s at 1 GiB with zone_f 3)
     uint32_t shrink_pct = 200;   // shrink once the zone exceeds shrink_pct % of the target + 4096 
@@ -166,34 +161,51 @@ uint32_t grid_blocks(const gbpe_ctx* ctx, uint32_t nblk, uint32_t per_cu) {
     return std::max<uint32_t>(grid_persistent(ctx, nblk, per_cu), (uint32_t)gbpe_div_up(nblk, 64));
 }
 
+// the partial maxima (both halves), the flagged-block bitmap and the close state,
+// sized for the table's blocks (sparse selection; after every table resize)
+int part_alloc(gbpe_trainer* t) {
+    hipStream_t s = t->ctx->stream;
+    pool_free(t->ctx, t->part);
+    pool_free(t->ctx, t->fbits);
+    t->part = nullptr;
+    t->fbits = nullptr;
+    const uint64_t nfw = std::max<uint64_t>(1, gbpe_div_up(t->tb.nblk, 32));
+    TR_HIP(t, pool_malloc(t->ctx, &t->part, 2ull * (t->tb.nblk + 1) * sizeof(uint64_t)));
+    TR_HIP(t, pool_malloc(t->ctx, &t->fbits, nfw * sizeof(uint32_t)));
+    TR_HIP(t, hipMemsetAsync(t->fbits, 0, nfw * sizeof(uint32_t), s));
+    if (!t->cls) {
+        TR_HIP(t, pool_malloc(t->ctx, &t->cls, sizeof(CloseState)));
+        TR_HIP(t, hipMemsetAsync(t->cls, 0, sizeof(CloseState), s));
+        TR_HIP(t, hipMemcpyAsync(&t->cls->clog, &t->d_clog, sizeof(uint32_t*), hipMemcpyHostToDevice, s));
+        TR_HIP(t, hipStreamSynchronize(s));   // (&t->d_clog is pageable host memory)
+    }
+    return GBPE_OK;
+}
+
 // new (empty) table arrays of 2^lg slots; the caller recounts (table_rebuild)
 int table_resize(gbpe_trainer* t, uint32_t lg) {
     hipStream_t s = t->ctx->stream;
     TR_HIP(t, hipStreamSynchronize(s));
-    hipFree(t->tb.slots);
-    hipFree(t->tb.bmax);
-    hipFree(t->tb.dirty);
-    hipFree(t->tb.dlist);
-    hipFree(t->tb.blive);
+    pool_free(t->ctx, t->tb.slots);
+    pool_free(t->ctx, t->tb.bmax);
+    pool_free(t->ctx, t->tb.dirty);
+    pool_free(t->ctx, t->tb.dlist);
+    pool_free(t->ctx, t->tb.blive);
     t->tb.slots = nullptr, t->tb.bmax = nullptr, t->tb.dirty = nullptr, t->tb.dlist = nullptr, t->tb.blive = nullptr;
     const uint64_t slots = 1ull << lg;
     t->table_log2 = lg;
     t->tb.mask = (uint32_t)(slots - 1);
     t->tb.nblk = (uint32_t)(slots >> BLK_LOG2);
-    if (hipMalloc(&t->tb.slots, slots * sizeof(uint2)) != hipSuccess ||
-        hipMalloc(&t->tb.bmax, t->tb.nblk * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc(&t->tb.dirty, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->tb.dlist, (t->tb.nblk + 1) * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess)
+    if (pool_malloc(t->ctx, &t->tb.slots, slots * sizeof(uint2)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tb.bmax, t->tb.nblk * sizeof(uint64_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tb.dirty, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tb.dlist, (t->tb.nblk + 1) * sizeof(uint32_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess)
         return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(pair table, 2^%u slots) failed", lg);
     TR_HIP(t, hipMemsetAsync(t->tb.dirty, 0, t->tb.nblk * sizeof(uint32_t), s));
     t->g_refresh = grid_blocks(t->ctx, t->tb.nblk, 2);
     if (t->refresh_blocks) t->g_refresh = std::max<uint32_t>(t->refresh_blocks, (uint32_t)gbpe_div_up(t->tb.nblk, 64));
-    if (t->part) {   // one partial maximum per k_refresh workgroup
-        hipFree(t->part);
-        t->part = nullptr;
-        TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
-    }
+    if (t->part) return part_alloc(t);   // one partial maximum per k_refresh workgroup
     return GBPE_OK;
 }
 
@@ -208,7 +220,7 @@ int table_rebuild(gbpe_trainer* t, bool bytes_only = false) {
     const uint64_t ntiles = gbpe_div_up(t->n, TILE);
     const uint32_t g = grid_persistent(t->ctx, ntiles, 2);
     if (bytes_only && t->count_bytes_on) {
-        if (!t->d_bhist && hipMalloc((void**)&t->d_bhist, 65536 * sizeof(uint32_t)) != hipSuccess) {
+        if (!t->d_bhist && pool_malloc(t->ctx, (void**)&t->d_bhist, 65536 * sizeof(uint32_t)) != hipSuccess) {
             t->d_bhist = nullptr;
             return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(byte-pair histogram) failed");
         }
@@ -261,7 +273,7 @@ int table_rehash(gbpe_trainer* t, uint32_t lg) {
     t->tb.slots = nullptr;   // kept until the live entries have moved
     int rc = table_resize(t, lg);
     if (rc != GBPE_OK) {
-        hipFree(old);
+        pool_free(t->ctx, old);
         return rc;
     }
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
@@ -284,7 +296,7 @@ int table_rehash(gbpe_trainer* t, uint32_t lg) {
                            FusedSel(), t->part, (uint32_t*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     TR_HIP(t, hipStreamSynchronize(s));
-    hipFree(old);
+    pool_free(t->ctx, old);
     return GBPE_OK;
 }
 
@@ -387,11 +399,33 @@ void launch_body(int bt, uint32_t grid, hipStream_t s, A... args) {
         hipLaunchKernelGGL((k_body<S, EXACT, 256>), dim3(grid), dim3(256), 0, s, args...);
 }
 
+// the in-launch close (sparse.h merge_close) for a step of this grid: the zone in
+// one workgroup (no zone segments, no multi-tile zone kernels after k_body), at
+// most CL_PMAX partial maxima and a bitmap the close's threads cover
+inline bool close_fits(const gbpe_trainer* t, const SpGrid& g) {
+    const uint32_t nthr = g.bt >= 1023 ? 1024u : 256u;
+    return t->close_on && t->cls && g.zone1 == 1 && g.refresh <= CL_PMAX &&
+           gbpe_div_up(t->tb.nblk, 32) <= (uint64_t)CL_KW * nthr;
+}
+
 template <typename S>
 int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const SpGrid& g, bool timing, hipEvent_t* ev) {
     S* zc = (S*)t->zbuf[t->zcur ^ (round & 1)];
     S* zo = (S*)t->zbuf[t->zcur ^ (round & 1) ^ 1];
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
+    // partial maxima by merge parity: this launch selects from one half, its
+    // increments raise the other (k_refresh writes both)
+    const uint64_t half = (uint64_t)t->tb.nblk + 1;
+    const uint32_t par = (uint32_t)((t->done + round) & 1u);
+    const uint64_t* pread = t->part + par * half;
+    const bool inl = close_fits(t, g);
+    Table tbc = t->tb;
+    if (inl) {
+        tbc.fbits = t->fbits;
+        tbc.pinc = t->part + (par ^ 1u) * half;
+        tbc.per = (uint32_t)gbpe_div_up(t->tb.nblk, g.refresh);   // k_refresh's blocks per workgroup
+    }
+    CloseState* cls = inl ? t->cls : nullptr;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));   // selection runs inside k_body (sel_inline)
     // zone segments run inside k_body (its ZSEG form)
@@ -401,15 +435,15 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const int bt = inbody ? 2048 : g.bt;
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
-        launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
+        launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, tbc,
                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
-                             (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
-                             sp_mul(t), (ZSegState*)t->zseg);
+                             pread, g.refresh, t->d_log, t->grpsum, t->wg_bytes, tbc, sel_single(t),
+                             sp_mul(t), (ZSegState*)t->zseg, cls);
     else
-        launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
+        launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, tbc,
                               g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
-                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
-                             sp_mul(t), (ZSegState*)t->zseg);
+                              pread, g.refresh, t->d_log, t->grpsum, t->wg_bytes, tbc, sel_single(t),
+                              sp_mul(t), (ZSegState*)t->zseg, cls);
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
     if (!g.zone1 && !exact && t->zdr_on && t->zdr_out) {
         // a zone of many tiles, reference compaction: tiles dump their deltas, k_churn
@@ -466,88 +500,10 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
                                t->tb, (const S*)t->wtmp, (const DevState*)t->st);
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
-    hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,
-                       (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part, t->zseg);
+    if (!inl)
+        hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,
+                           (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part, t->zseg);
     if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
-    GBPE_LAUNCH_CHECK(t->ctx);
-    return GBPE_OK;
-}
-
-// ── the late-merge loop ──
-
-// symbols the LDS zone buffers hold
-inline uint32_t late_zcap(const gbpe_trainer* t) {
-    return t->u16 ? LateDim<uint16_t>::ZCAP : LateDim<uint32_t>::ZCAP;
-}
-
-// a sparse step the late loop can run: the zone and the stale source it reads
-// fit the LDS buffers (the zone only shrinks within a step)
-inline bool late_eligible(const gbpe_trainer* t) {
-    const uint32_t zc = late_zcap(t);
-    const uint32_t z = (uint32_t)t->n - t->h_st->B;
-    // (a store of more than 128K sectors has more bitmap words than one pass of the
-    // loop's fast candidate path: its batched path measured ~70 us per merge)
-    return t->late_on && !t->late_skip && t->sp && !t->d_clog && t->last_mc <= t->late_mc && t->W <= LATE_WW * LATE_BT &&
-           z <= zc &&
-           (uint32_t)((uint32_t)t->n - t->h_st->Bp) <= zc && t->zcap >= zc;
-}
-
-int late_alloc(gbpe_trainer* t) {
-    hipStream_t s = t->ctx->stream;
-    if (!t->late_hot) {
-        TR_HIP(t, hipMalloc(&t->late_hot, sizeof(LateHot)));
-        TR_HIP(t, hipMemsetAsync(t->late_hot, 0, sizeof(LateHot), s));
-        TR_HIP(t, hipMalloc(&t->late_u32, 64));
-        TR_HIP(t, hipMemsetAsync(t->late_u32, 0, 64, s));
-    }
-    const uint32_t need = t->batch * (uint32_t)(LATE_LT + 1) + 4096;
-    if (t->late_logcap < need) {
-        hipFree(t->late_log);
-        t->late_log = nullptr;
-        t->late_logcap = 0;
-        TR_HIP(t, hipMalloc(&t->late_log, (uint64_t)need * sizeof(uint2)));
-        t->late_logcap = need;
-    }
-    if (!t->late_ev[0] && (t->flags & GBPE_TRAIN_TIMING)) {
-        TR_HIP(t, hipEventCreate(&t->late_ev[0]));
-        TR_HIP(t, hipEventCreate(&t->late_ev[1]));
-    }
-    return GBPE_OK;
-}
-
-// One step of the late loop: hot-set refresh (k_hot_hist, k_hot_gather), the
-// merges (k_late, one workgroup), their count deltas into the table
-// (k_late_apply) and the block maxima / partial maxima k_body selects from
-// (k_refresh): the table is exact again at the step boundary.
-template <typename S>
-int launch_late(gbpe_trainer* t, hipStream_t s, uint32_t g_refresh, bool timing) {
-    int rc = late_alloc(t);
-    if (rc != GBPE_OK) return rc;
-    const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
-    hipLaunchKernelGGL(k_hot_sel, dim3(1), dim3(1024), 0, s, t->tb, t->late_hot);
-    hipLaunchKernelGGL(k_hot_gather_blocks, dim3(LATE_KB), dim3(256), 0, s, t->tb, t->late_hot);
-    LateOut lo;
-    lo.dlog = t->late_log;
-    lo.dcap = t->late_logcap;
-    lo.dlog_n = t->late_u32;
-    lo.mlog = t->d_log;
-    lo.bytes = reinterpret_cast<uint64_t*>(t->late_u32 + 4);
-    lo.stat = t->late_u32 + 1;
-    S* z0 = (S*)t->zbuf[t->zcur];
-    S* z1 = (S*)t->zbuf[t->zcur ^ 1];
-    if (timing) TR_HIP(t, hipEventRecord(t->late_ev[0], s));
-    if (exact)
-        hipLaunchKernelGGL((k_late<S, true>), dim3(1), dim3(LATE_BT), 0, s, t->st, t->zst, (S*)sp_body(t), sp_mul(t),
-                           t->sec, t->bits, t->W, t->sig, z0, z1, t->late_hot, t->zone_f, lo);
-    else
-        hipLaunchKernelGGL((k_late<S, false>), dim3(1), dim3(LATE_BT), 0, s, t->st, t->zst, (S*)sp_body(t), sp_mul(t),
-                           t->sec, t->bits, t->W, t->sig, z0, z1, t->late_hot, t->zone_f, lo);
-    if (timing) TR_HIP(t, hipEventRecord(t->late_ev[1], s));
-    hipLaunchKernelGGL(k_late_apply, dim3(grid_persistent(t->ctx, 256, 1)), dim3(256), 0, s,
-                       (const uint2*)t->late_log, (const uint32_t*)t->late_u32, t->st, t->tb);
-    hipLaunchKernelGGL(k_refresh<S>, dim3(g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
-                       (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part,
-                       (uint32_t*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
 }
@@ -555,10 +511,10 @@ int launch_late(gbpe_trainer* t, hipStream_t s, uint32_t g_refresh, bool timing)
 template <typename T>
 int sp_grow(gbpe_trainer* t, T** p, uint64_t* cap, uint64_t need) {
     if (*p && *cap >= need) return GBPE_OK;
-    hipFree(*p);
+    pool_free(t->ctx, *p);
     *p = nullptr;
     *cap = 0;
-    if (hipMalloc((void**)p, need * sizeof(T)) != hipSuccess) {
+    if (pool_malloc(t->ctx, (void**)p, need * sizeof(T)) != hipSuccess) {
         *p = nullptr;
         return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sparse layout, %llu B) failed",
                               (unsigned long long)(need * sizeof(T)));
@@ -582,13 +538,13 @@ template <typename T>
 int sp_regrow(gbpe_trainer* t, T** p, uint64_t* cap, uint64_t want, uint64_t keep) {
     if (*p && *cap >= want) return GBPE_OK;
     T* nb = nullptr;
-    if (hipMalloc((void**)&nb, want * sizeof(T)) != hipSuccess)
+    if (pool_malloc(t->ctx, (void**)&nb, want * sizeof(T)) != hipSuccess)
         return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sparse layout growth, %llu B) failed",
                               (unsigned long long)(want * sizeof(T)));
     hipStream_t s = t->ctx->stream;
     if (*p && keep) TR_HIP(t, hipMemcpyAsync(nb, *p, keep * sizeof(T), hipMemcpyDeviceToDevice, s));
     TR_HIP(t, hipStreamSynchronize(s));
-    hipFree(*p);
+    pool_free(t->ctx, *p);
     *p = nb;
     *cap = want;
     return GBPE_OK;
@@ -614,20 +570,20 @@ int sp_reserve(gbpe_trainer* t, uint64_t need_sec, uint64_t need_store, uint64_t
         if (rc != GBPE_OK) return rc;
         if (keep * SP_SIGW < cap * SP_SIGW)
             TR_HIP(t, hipMemsetAsync(t->sig + keep * SP_SIGW, 0, (cap - keep) * SP_SIGW * 4, s));
-        hipFree(t->sp_loc);
-        hipFree(t->sp_blk);
+        pool_free(t->ctx, t->sp_loc);
+        pool_free(t->ctx, t->sp_blk);
         t->sp_loc = nullptr;
         t->sp_blk = nullptr;
         t->loc_cap = 0;
-        if (hipMalloc(&t->sp_loc, cap * 4) != hipSuccess ||
-            hipMalloc(&t->sp_blk, (gbpe_div_up(cap, SCAN_BLK) + 1) * 8) != hipSuccess)
+        if (pool_malloc(t->ctx, &t->sp_loc, cap * 4) != hipSuccess ||
+            pool_malloc(t->ctx, &t->sp_blk, (gbpe_div_up(cap, SCAN_BLK) + 1) * 8) != hipSuccess)
             return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sector scratch) failed");
         t->loc_cap = cap;
         const uint32_t w_new = (uint32_t)gbpe_div_up(cap, 32);
         if (w_new > t->W || !t->bits) {
             uint32_t* nb = nullptr;
             const uint64_t words = (uint64_t)t->max_id * w_new;
-            if (hipMalloc(&nb, words * 4) != hipSuccess)
+            if (pool_malloc(t->ctx, &nb, words * 4) != hipSuccess)
                 return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(token bitmap, %llu B) failed",
                                       (unsigned long long)(words * 4));
             if (t->bits && t->W)
@@ -637,7 +593,7 @@ int sp_reserve(gbpe_trainer* t, uint64_t need_sec, uint64_t need_store, uint64_t
                 TR_HIP(t, hipMemsetAsync(nb, 0, words * 4, s));
             GBPE_LAUNCH_CHECK(t->ctx);
             TR_HIP(t, hipStreamSynchronize(s));
-            hipFree(t->bits);
+            pool_free(t->ctx, t->bits);
             t->bits = nb;
             t->bits_cap = words;
             t->W = w_new;
@@ -645,11 +601,11 @@ int sp_reserve(gbpe_trainer* t, uint64_t need_sec, uint64_t need_store, uint64_t
         const uint64_t wneed = gbpe_div_up(w_new, SP_WPW_MIN) + 2;   // one byte counter per k_body workgroup
         if (t->wg_bytes && wneed > t->wg_cap) {
             uint64_t* nb = nullptr;
-            TR_HIP(t, hipMalloc(&nb, wneed * sizeof(uint64_t)));
+            TR_HIP(t, pool_malloc(t->ctx, &nb, wneed * sizeof(uint64_t)));
             TR_HIP(t, hipMemsetAsync(nb, 0, wneed * sizeof(uint64_t), s));
             TR_HIP(t, hipMemcpyAsync(nb, t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
             TR_HIP(t, hipStreamSynchronize(s));
-            hipFree(t->wg_bytes);
+            pool_free(t->ctx, t->wg_bytes);
             t->wg_bytes = nb;
             t->wg_cap = wneed;
         }
@@ -658,13 +614,13 @@ int sp_reserve(gbpe_trainer* t, uint64_t need_sec, uint64_t need_store, uint64_t
         const uint64_t want = std::max<uint64_t>(need_store, t->lx_cap + t->lx_cap / 2);
         uint64_t c1 = t->lx_cap, c2 = t->lx_cap;
         void* st = t->lx_store;
-        if (hipMalloc(&t->lx_store, want * t->bps) != hipSuccess) {
+        if (pool_malloc(t->ctx, &t->lx_store, want * t->bps) != hipSuccess) {
             t->lx_store = st;
             return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(word lexicon growth) failed");
         }
         TR_HIP(t, hipMemcpyAsync(t->lx_store, st, t->lx_len * t->bps, hipMemcpyDeviceToDevice, s));
         TR_HIP(t, hipStreamSynchronize(s));
-        hipFree(st);
+        pool_free(t->ctx, st);
         int rc = sp_regrow(t, &t->lx_mul, &c1, want, t->lx_len);
         if (rc != GBPE_OK) return rc;
         (void)c2;
@@ -743,10 +699,10 @@ struct LxCarve {
 int lx_scratch(gbpe_trainer* t, uint64_t bytes) {
     if (t->lx_tmp && t->lx_tmp_bytes >= bytes) return GBPE_OK;
     TR_HIP(t, hipStreamSynchronize(t->ctx->stream));
-    hipFree(t->lx_tmp);
+    pool_free(t->ctx, t->lx_tmp);
     t->lx_tmp = nullptr;
     t->lx_tmp_bytes = 0;
-    if (hipMalloc(&t->lx_tmp, bytes) != hipSuccess) {
+    if (pool_malloc(t->ctx, &t->lx_tmp, bytes) != hipSuccess) {
         t->lx_tmp = nullptr;
         return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(lexicon scratch, %llu B) failed", (unsigned long long)bytes);
     }
@@ -999,14 +955,14 @@ int lx_check(gbpe_trainer* t, const S* cur, uint32_t Zs, const LxPlan& lp) {
     hipStream_t s = t->ctx->stream;
     int rc = GBPE_OK;
     S* chk = nullptr;
-    TR_HIP(t, hipMalloc(&chk, ((uint64_t)Zs + 64) * sizeof(S)));
+    TR_HIP(t, pool_malloc(t->ctx, &chk, ((uint64_t)Zs + 64) * sizeof(S)));
     uint64_t tot = 0;
     rc = lx_expand<S>(t, chk, (uint64_t)Zs + 64, &tot);
     std::vector<S> a(Zs), b(Zs);
     TR_HIP(t, hipStreamSynchronize(s));
     TR_HIP(t, hipMemcpy(a.data(), chk, (uint64_t)Zs * sizeof(S), hipMemcpyDeviceToHost));
     TR_HIP(t, hipMemcpy(b.data(), cur, (uint64_t)Zs * sizeof(S), hipMemcpyDeviceToHost));
-    hipFree(chk);
+    pool_free(t->ctx, chk);
     uint64_t bad = Zs;
     for (uint64_t i = 0; i < Zs; ++i)
         if (a[i] != b[i]) {
@@ -1039,13 +995,13 @@ int sp_alloc_layout(gbpe_trainer* t, uint64_t cap) {
     hipStream_t s = t->ctx->stream;
     int rc = sp_grow(t, &t->sec, &t->nsec_cap, cap);
     if (rc == GBPE_OK && (!t->sp_loc || t->loc_cap < cap)) {
-        hipFree(t->sp_loc);
-        hipFree(t->sp_blk);
+        pool_free(t->ctx, t->sp_loc);
+        pool_free(t->ctx, t->sp_blk);
         t->sp_loc = nullptr;
         t->sp_blk = nullptr;
         t->loc_cap = 0;
-        if (hipMalloc(&t->sp_loc, cap * 4) != hipSuccess ||
-            hipMalloc(&t->sp_blk, (gbpe_div_up(cap, SCAN_BLK) + 1) * 8) != hipSuccess)
+        if (pool_malloc(t->ctx, &t->sp_loc, cap * 4) != hipSuccess ||
+            pool_malloc(t->ctx, &t->sp_blk, (gbpe_div_up(cap, SCAN_BLK) + 1) * 8) != hipSuccess)
             rc = gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(sector scratch) failed");
         else
             t->loc_cap = cap;
@@ -1065,14 +1021,14 @@ int sp_alloc_layout(gbpe_trainer* t, uint64_t cap) {
 int sp_alloc_lexicon(gbpe_trainer* t, uint64_t cap, uint64_t ocap) {
     const uint64_t scap = cap * t->sp_secw;
     if (!t->lx_store || t->lx_cap < scap) {
-        hipFree(t->lx_store);
-        hipFree(t->lx_mul);
-        hipFree(t->lx_w0);
+        pool_free(t->ctx, t->lx_store);
+        pool_free(t->ctx, t->lx_mul);
+        pool_free(t->ctx, t->lx_w0);
         t->lx_store = nullptr;
         t->lx_mul = t->lx_w0 = nullptr;
         t->lx_cap = 0;
-        if (hipMalloc(&t->lx_store, scap * t->bps) != hipSuccess || hipMalloc(&t->lx_mul, scap * 4) != hipSuccess ||
-            hipMalloc(&t->lx_w0, cap * 4) != hipSuccess)
+        if (pool_malloc(t->ctx, &t->lx_store, scap * t->bps) != hipSuccess || pool_malloc(t->ctx, &t->lx_mul, scap * 4) != hipSuccess ||
+            pool_malloc(t->ctx, &t->lx_w0, cap * 4) != hipSuccess)
             return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(word lexicon) failed");
         t->lx_cap = scap;
     }
@@ -1089,14 +1045,14 @@ int sp_alloc_zone(gbpe_trainer* t, uint64_t z, uint64_t prev_mc) {
     if (zneed < zmin) zneed = zmin;
     if (zneed > t->zcap) {
         for (int k = 0; k < 2; ++k) {
-            hipFree(t->zbuf[k]);
+            pool_free(t->ctx, t->zbuf[k]);
             t->zbuf[k] = nullptr;
         }
-        hipFree(t->wtmp);
+        pool_free(t->ctx, t->wtmp);
         t->wtmp = nullptr;
         t->zcap = 0;
-        if (hipMalloc(&t->zbuf[0], zneed * t->bps) != hipSuccess || hipMalloc(&t->zbuf[1], zneed * t->bps) != hipSuccess ||
-            hipMalloc(&t->wtmp, zneed * t->bps) != hipSuccess)
+        if (pool_malloc(t->ctx, &t->zbuf[0], zneed * t->bps) != hipSuccess || pool_malloc(t->ctx, &t->zbuf[1], zneed * t->bps) != hipSuccess ||
+            pool_malloc(t->ctx, &t->wtmp, zneed * t->bps) != hipSuccess)
             return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(zone) failed");
         t->zcap = zneed;
     }
@@ -1105,15 +1061,15 @@ int sp_alloc_zone(gbpe_trainer* t, uint64_t z, uint64_t prev_mc) {
         const uint32_t need = (uint32_t)std::max<uint64_t>(std::min<uint64_t>(zt, t->delta_mt ? t->delta_mt : zt),
                                                            gbpe_div_up(zt, 8)) + 1;
         if (t->zdr_on && need > t->zdr_ntile) {
-            hipFree(t->zdr_out);
-            hipFree(t->zdr_offs);
-            hipFree(t->zdr_flag);
+            pool_free(t->ctx, t->zdr_out);
+            pool_free(t->ctx, t->zdr_offs);
+            pool_free(t->ctx, t->zdr_flag);
             t->zdr_out = nullptr, t->zdr_offs = nullptr, t->zdr_flag = nullptr;
             t->zdr_ntile = 0;
             const uint64_t nd = (uint64_t)need + ZDR_P;
-            if (hipMalloc(&t->zdr_out, ((uint64_t)need * ZDR_N_TILE + (uint64_t)ZDR_P * ZDR_N_CHURN) * sizeof(uint2)) !=
+            if (pool_malloc(t->ctx, &t->zdr_out, ((uint64_t)need * ZDR_N_TILE + (uint64_t)ZDR_P * ZDR_N_CHURN) * sizeof(uint2)) !=
                     hipSuccess ||
-                hipMalloc(&t->zdr_offs, nd * (ZDR_P + 1) * 4) != hipSuccess || hipMalloc(&t->zdr_flag, nd * 4) != hipSuccess)
+                pool_malloc(t->ctx, &t->zdr_offs, nd * (ZDR_P + 1) * 4) != hipSuccess || pool_malloc(t->ctx, &t->zdr_flag, nd * 4) != hipSuccess)
                 return gbpe_set_error(t->ctx, GBPE_E_OOM, "hipMalloc(zone delta dumps) failed");
             TR_HIP(t, hipMemsetAsync(t->zdr_flag, 0, nd * 4, s));   // tags start at 1
             t->zdr_ntile = need;
@@ -1130,8 +1086,8 @@ int sp_alloc_zone(gbpe_trainer* t, uint64_t z, uint64_t prev_mc) {
 int sp_init_states(gbpe_trainer* t, uint64_t cap, uint32_t Zs, uint32_t z, uint32_t zlast) {
     hipStream_t s = t->ctx->stream;
     if (!t->zst) {
-        TR_HIP(t, hipMalloc(&t->zst, sizeof(DevState)));
-        TR_HIP(t, hipHostMalloc((void**)&t->h_zst, sizeof(DevState), hipHostMallocDefault));
+        TR_HIP(t, pool_malloc(t->ctx, &t->zst, sizeof(DevState)));
+        TR_HIP(t, pool_hmalloc(t->ctx, &t->h_zst, sizeof(DevState)));
     }
     memset(t->h_zst, 0, sizeof(DevState));
     t->h_zst->n = z;
@@ -1151,11 +1107,11 @@ int sp_init_states(gbpe_trainer* t, uint64_t cap, uint32_t Zs, uint32_t z, uint3
         const uint64_t need = gbpe_div_up(gbpe_div_up(cap, 32), SP_WPW_MIN) + 2;
         if (need > t->wg_cap) {
             uint64_t* nb = nullptr;
-            TR_HIP(t, hipMalloc(&nb, need * sizeof(uint64_t)));
+            TR_HIP(t, pool_malloc(t->ctx, &nb, need * sizeof(uint64_t)));
             TR_HIP(t, hipMemsetAsync(nb, 0, need * sizeof(uint64_t), s));
             if (t->wg_bytes) TR_HIP(t, hipMemcpyAsync(nb, t->wg_bytes, t->wg_cap * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
             TR_HIP(t, hipStreamSynchronize(s));
-            hipFree(t->wg_bytes);
+            pool_free(t->ctx, t->wg_bytes);
             t->wg_bytes = nb;
             t->wg_cap = need;
         }
@@ -1163,12 +1119,15 @@ int sp_init_states(gbpe_trainer* t, uint64_t cap, uint32_t Zs, uint32_t z, uint3
     // the zone rule's last count (sel_inline): the count of the merge before entry
     TR_HIP(t, hipMemcpyAsync(&t->st->mc_prev, &t->st->mc, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     // per-k_refresh-workgroup maxima the sparse merges select from (sel_inline)
-    if (!t->part) TR_HIP(t, hipMalloc(&t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
+    if (!t->part) {
+        int rc = part_alloc(t);
+        if (rc != GBPE_OK) return rc;
+    }
     if (!t->zseg) {
-        TR_HIP(t, hipMalloc(&t->zseg, sizeof(ZSegState)));
+        TR_HIP(t, pool_malloc(t->ctx, &t->zseg, sizeof(ZSegState)));
         TR_HIP(t, hipMemsetAsync(t->zseg, 0, sizeof(ZSegState), t->ctx->stream));
     }
-    if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
+    if (!t->d_u32) TR_HIP(t, pool_malloc(t->ctx, &t->d_u32, 64));
     return GBPE_OK;
 }
 
@@ -1187,7 +1146,7 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
     const uint64_t zt = std::max<uint64_t>((uint64_t)t->sp_zt * nmc, 2ull * nmc + prev_mc) + 64;
     const S* cur = (const S*)t->buf[t->cur];
     const S* stale = (const S*)t->buf[t->cur ^ 1];
-    if (!t->d_u32) TR_HIP(t, hipMalloc(&t->d_u32, 64));
+    if (!t->d_u32) TR_HIP(t, pool_malloc(t->ctx, &t->d_u32, 64));
     uint32_t Zs = n;
     if (with_zone) {
         if (zt + 2 >= n) return GBPE_OK;
@@ -1265,9 +1224,7 @@ int sp_shrink(gbpe_trainer* t) {
     DevState* hs = t->h_st;
     const uint32_t z = (uint32_t)t->n - hs->B;
     const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
-    // a zone just above the late loop's LDS buffers shrinks to its target at once
-    const bool to_late = t->late_on && t->last_mc <= t->late_mc && z > late_zcap(t) && zt + 1024 <= late_zcap(t);
-    if (t->sp_shrinks >= SP_SHRINKS_MAX || (!to_late && (uint64_t)z < zt * t->shrink_pct / 100 + 4096)) return GBPE_OK;
+    if (t->sp_shrinks >= SP_SHRINKS_MAX || (uint64_t)z < zt * t->shrink_pct / 100 + 4096) return GBPE_OK;
     S* zc = (S*)t->zbuf[t->zcur];
     S* zo = (S*)t->zbuf[t->zcur ^ 1];
     hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, (const S*)zc, (uint32_t)(z - zt), t->d_u32);
@@ -1275,7 +1232,7 @@ int sp_shrink(gbpe_trainer* t) {
     uint32_t L = 0;
     TR_HIP(t, hipMemcpyAsync(&L, t->d_u32, 4, hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipStreamSynchronize(s));
-    if (L < (to_late ? 1024u : 4096u)) return GBPE_OK;
+    if (L < 4096u) return GBPE_OK;
     if (t->lex) {   // the front's words join the lexicon (deduplicated among themselves)
         LxPlan lp;
         int rc = lx_analyze<S>(t, (const S*)zc, L, false, lp);
@@ -1384,8 +1341,9 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->rehash_on = gbpe_debug_knob("rehash", 1) != 0;
     t->delta_mt = (uint32_t)gbpe_debug_knob("delta_mt", t->delta_mt);
     t->sp_zt = (uint32_t)gbpe_debug_knob("zt", t->sp_zt);
-    t->late_on = gbpe_debug_knob("late", 0) != 0;
-    t->late_mc = (uint32_t)gbpe_debug_knob("late_mc", 1200);   // the loop runs once a merge's count is at most this   // (off until it beats k_body: DESIGN §2d)
+    t->close_on = gbpe_debug_knob("close", 1) != 0;
+    t->grow_used_pct = (uint32_t)std::min<long>(90, std::max<long>(10, gbpe_debug_knob("gused", t->grow_used_pct)));
+    t->grow_live_pct = (uint32_t)std::min<long>(t->grow_used_pct, std::max<long>(5, gbpe_debug_knob("glive", t->grow_live_pct)));
     t->refresh_blocks = (uint32_t)gbpe_debug_knob("rfb", t->refresh_blocks);   // k_refresh grid sweeps
     t->refresh_late = (uint32_t)gbpe_debug_knob("rfl", t->refresh_late);
     t->refresh_late_z = (uint32_t)gbpe_debug_knob("rflz", t->refresh_late_z);
@@ -1395,8 +1353,8 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
     if (const char* e = getenv("GBPE_SPARSE_TRACE")) {
         t->trace = fopen(e, "w");
-        if (t->trace && (hipMalloc(&t->d_clog, (size_t)t->batch * 8) != hipSuccess ||
-                         hipHostMalloc((void**)&t->h_clog, (size_t)t->batch * 8, hipHostMallocDefault) != hipSuccess))
+        if (t->trace && (pool_malloc(t->ctx, &t->d_clog, (size_t)t->batch * 8) != hipSuccess ||
+                         pool_hmalloc(t->ctx, &t->h_clog, (size_t)t->batch * 8) != hipSuccess))
             t->d_clog = nullptr, t->h_clog = nullptr;   // trace without candidate counts
     }
     t->bps = t->u16 ? 2 : 4;
@@ -1412,7 +1370,8 @@ struct StateInit {
     const uint32_t* prev;
     uint64_t n_prev;
 };
-// the trainer constructor behind gbpe_trainer_create / _create_from_state / gbpe_shard_create
+// the trainer constructor behind gbpe_trainer_create / _create_from_state (and, through
+// trainer_config, _create_from_lexicon)
 int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
                         int input_on_device, const gbpe_train_opts* opts, uint64_t cap_extra, gbpe_trainer** out,
                         const StateInit* si = nullptr);

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GBPE_ABI_VERSION 3   /* 3: late-loop stats, the per-merge sharded entry points removed (round 4) */
+#define GBPE_ABI_VERSION 4   /* 4: in-launch merge close stats and creation time replace the late-loop stats (round 5) */
 
 /* status codes */
 #define GBPE_OK            0
@@ -179,14 +179,12 @@ typedef struct gbpe_trainer_stats {
     uint64_t lexicon_words;       /* body word occurrences the lexicon represents (all builds and shrinks) */
     uint64_t lexicon_entries;     /* distinct-word entries of the current lexicon */
     uint64_t lexicon_symbols;     /* symbols of the current lexicon store (separators included) */
-    uint64_t late_merges;         /* merges run by the one-workgroup late-merge loop k_late (off
-                                     unless GBPE_DEBUG=late=1: 0 by default) */
-    uint64_t late_launches;       /* its launches (one per step) */
-    uint64_t late_exits;          /* ... that ended before their step's budget (the hot-set bound; host refreshes) */
-    double   ms_late;             /* GBPE_TRAIN_TIMING: device ms of k_late (included in ms_sparse) */
-    uint64_t late_bytes;          /* bytes k_late moved: body sectors read + rewritten, extents + signatures,
-                                     the LDS-resident zone pass (pair-table traffic excluded) */
-    uint64_t late_bound_exits;    /* k_late launches ended by the hot-set bound */
+    uint64_t close_inlaunch;      /* sparse merges closed inside k_body by its last-arriving workgroup (block
+                                     maxima kept exact in the launch: no k_refresh launch) */
+    uint64_t close_remax_blocks;  /* argmax blocks those closes re-maxed (a decrement reached a block's maximum) */
+    uint64_t close_refreshes;     /* closes with more flagged blocks than one workgroup re-maxes (a k_refresh follows) */
+    double   ms_create;           /* host wall ms of trainer creation (symbols, word starts, first count):
+                                     the part of a run the reference's t_loop excludes (trainer.js:230) */
 } gbpe_trainer_stats;
 int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* out);
 /* Current symbol stream in the reference u32 layout (bit16 = word start). */

@@ -109,16 +109,6 @@ def test_full_c2_bench_corpus(eng):
     assert st.sparse_merges > 30000 and st.bytes_per_symbol == 2
 
 
-@pytest.mark.parametrize("name", ["c1", "c1x", "c2", "en1g"])
-def test_full_late_loop(eng, name, monkeypatch):
-    # the one-workgroup late-merge loop (off by default) forced on for
-    # every eligible step: the same merges, final stream and stale-tail total
-    monkeypatch.setenv("GBPE_DEBUG", "late=1,late_mc=1000000")
-    st, _ = _check_train(eng, name)
-    if name in ("c2", "en1g"):
-        assert st.late_merges > 10000
-
-
 def test_full_en1g_headline(eng):
     st, _ = _check_train(eng, "en1g")
     assert st.sparse_merges > 30000

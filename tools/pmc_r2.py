@@ -4,8 +4,6 @@ FETCH_SIZE doubled on gfx950 for wide streaming reads, WRITE_SIZE as is;
 both are KiB).  The raw (undoubled) read figure is kept beside it: k_body's
 reads are mostly narrow gathers, for which the doubling is uncalibrated.
 
-  klate:  python tools/pmc_r2.py klate <fetch dir> <write dir> <explore json line file> <out.json>
-          the same for k_late: per launch (one per late step), its own byte counter
   kbody:  python tools/pmc_r2.py kbody <fetch dir> <write dir> <explore json line file> <out.json>
           window = one full en1g training run (tools/explore_1g.py en1g); algorithmic bytes
           per launch = that run's k_body byte counter / its sparse merges
@@ -31,19 +29,8 @@ def per_dispatch(d, counter, names):
 def main():
     mode, fd, wd, jf, out = sys.argv[1:6]
     info = json.loads([ln for ln in open(jf).read().splitlines() if ln.startswith("{")][-1])
-    if mode == "klate":
-        n = int(info["stats"]["late_launches"])
-        fetch, write = per_dispatch(fd, "FETCH_SIZE", ["k_late"])[-n:], per_dispatch(wd, "WRITE_SIZE", ["k_late"])[-n:]
-        k = min(len(fetch), len(write))
-        raw, wr = sum(fetch[-k:]) / k, sum(write[-k:]) / k
-        alg = info["stats"]["late_bytes"] / n
-        res = {"workload": "en1g-full-run", "kernel": "k_late", "launches": k,
-               "fetch_bytes_raw_per_launch": raw, "read_bytes_per_launch": 2 * raw, "write_bytes_per_launch": wr,
-               "hbm_bytes_per_launch": 2 * raw + wr, "hbm_bytes_raw_per_launch": raw + wr,
-               "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": (2 * raw + wr) / alg,
-               "raw_over_algorithmic": (raw + wr) / alg}
-    elif mode == "kbody":
-        n = int(info["stats"]["sparse_merges"]) - int(info["stats"].get("late_merges", 0))
+    if mode == "kbody":
+        n = int(info["stats"]["sparse_merges"])
         fetch, write = per_dispatch(fd, "FETCH_SIZE", ["k_body"])[-n:], per_dispatch(wd, "WRITE_SIZE", ["k_body"])[-n:]
         k = min(len(fetch), len(write))
         raw, wr = sum(fetch[-k:]) / k, sum(write[-k:]) / k
