@@ -27,11 +27,18 @@ Secondary legs (same JSON line):
     the fixture and the CPU restatement.
 
 Multi-GPU (--gpus N under torch.distributed.run, one rank per GPU):
-  * training: one 1 GiB corpus, one vocabulary (strong scaling: the total work
-    is fixed).  The merge chain is sequential — every merge's argmax needs the
-    previous merge's counts — and one merge costs less than an exchange between
-    GPUs, so every rank runs the complete training (replicated, no per-merge
-    collective); `value` = global merges / max wall over ranks;
+  * training (the default N > 1 line): one 1 GiB corpus, one vocabulary (strong
+    scaling: the total work is fixed), cut at word starts into one piece per
+    rank; every GPU runs its piece's first pass (symbols, word starts, pair
+    counts, word lexicon), the lexicons go to the last rank, which runs the merge
+    chain — it is sequential, every merge's argmax needs the previous merge's
+    counts, and one merge costs less than an exchange between GPUs; `value` =
+    merges / max wall over ranks.  `--replicated` instead runs the complete
+    training on every rank (no exchange), reported beside the hand-over anyway;
+  * C4 (N = 8): one 64K vocabulary over 8 x 1 GiB multilingual shards through the
+    same hand-over, checked after the timed run: the root's live pair counts
+    against a device recount of the final stream rebuilt from every rank's
+    occurrence list (`counts_equal_recount`);
   * tokenize: the one 1 GiB C3 input cut into chunk-aligned slices, one per rank
     (gpubpe/split_encode.py): GB/s = input bytes / max wall over ranks; the
     tokens are gathered to rank 0 and checked against the fixture.
@@ -52,6 +59,17 @@ sys.path.insert(0, os.path.join(ROOT, "gpu-bpe_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# latency constants of MI355X_MICROARCH.md (one lane, idle chip): a dependent global
+# load that hits the Infinity Cache (~545 cycles at 2.4 GHz), and a dependent kernel
+# boundary on one stream (price list row "boundary")
+HOP_US = 0.227
+BOUNDARY_US = 1.45
+# the dependent global hops of one late sector-sparse merge (one k_body launch with
+# its in-launch close, DESIGN §2b "latency floor"): each waits for the one before
+LATE_MERGE_HOPS = ("state + partial maxima (selection)", "bitmap rows of a and b", "candidate extents + signatures",
+                   "candidate sector symbols + multiplicities", "pair-table probe (flush)", "returning count add",
+                   "block-maximum atomics drained", "arrival ticket", "flagged-block bitmap + state counters",
+                   "flagged blocks' slots (re-max)", "flagged groups' block maxima")
 TILE_SYMS = 8192
 METRIC = "BPE merges/sec + tokenize GB/s, 1 GiB UTF-8 @ 32K vocab, 1/2/4/8 MI355X"
 HEADLINE = {"gen": "english", "n": 1 << 30, "seed": 2, "fancy_punct": 0.005}
@@ -149,10 +167,11 @@ def device_buffer(lib, ctx, data: bytes):
     return p
 
 
-def train_run(lib, ctx, d_bytes, n, vocab, flags=0, max_merges=0, batch=128, pairs_out=None):
+def train_run(lib, ctx, d_bytes, n, vocab, flags=0, max_merges=0, batch=128, pairs_out=None, steps_out=None):
     """One training run on HBM-resident bytes: create + every step.  Returns
     (merges [k, 4] uint32, stats).  pairs_out (a list): the live pair ids at the
-    end are appended to it (the reference-table estimate; never in a timed run)."""
+    end are appended to it (the reference-table estimate; never in a timed run).
+    steps_out (a list): (merges, seconds) of every step call is appended to it."""
     from gpubpe import _lib
     opts = _lib.TrainOpts(target_vocab_size=vocab, vocab_size=256, next_token_id=256, batch_size=batch,
                           flags=flags, table_log2=0)
@@ -164,7 +183,10 @@ def train_run(lib, ctx, d_bytes, n, vocab, flags=0, max_merges=0, batch=128, pai
         while True:
             k = batch if not max_merges else min(batch, max_merges - len(merges) // 4)
             nd, es = C.c_uint32(), C.c_uint32()
+            ts = time.perf_counter()
             _lib.check(lib.gbpe_trainer_step(tr, k, out, C.byref(nd), C.byref(es)), ctx, "trainer_step")
+            if steps_out is not None:
+                steps_out.append((nd.value, time.perf_counter() - ts))
             merges += out[: 4 * nd.value]
             if nd.value == 0 or es.value or (max_merges and len(merges) // 4 >= max_merges):
                 break
@@ -200,13 +222,15 @@ def timed_runs(args, lib, ctx, dist, d, n, vocab, steps, warmup, flags=0, pairs_
     dist.barrier()
     lib.gbpe_synchronize(ctx)
     t0 = time.perf_counter()
-    total, last, st = 0, None, None
+    total, last, st, create_s = 0, None, None, 0.0
     for _ in range(steps):
         last, st = train_run(lib, ctx, d, n, vocab, flags=flags)
         total += last.shape[0]
+        create_s += st.ms_create / 1e3
     lib.gbpe_synchronize(ctx)
     t1 = time.perf_counter()
     dist.barrier()
+    st.create_s_total = create_s   # (the timed runs' trainer creation, host wall)
     return dist.max(t1 - t0), total, last, st
 
 
@@ -224,7 +248,6 @@ def train_detail(st, sk):
         "max_live_pairs": int(st.max_live_pairs), "table_slots": int(st.table_slots),
         "sparse": {"merges": int(st.sparse_merges), "enters": int(st.sparse_enters), "exits": int(st.sparse_exits),
                    "sectors": int(st.sparse_sectors), "zone_at_entry": int(st.sparse_zone)},
-        "close": {"inlaunch": int(st.close_inlaunch), "remax_blocks": int(st.close_remax_blocks)},
         "ms_create": round(st.ms_create, 3),
         "events": None if sk is None else {
             "merges": int(sk.timed_merges), "dense_merges": int(sk.timed_merges - sk.sparse_merges),
@@ -301,6 +324,22 @@ def train_roofline(det, wall_per_run):
     other = [k for k in cand if k["kernel"] != roof.get("kernel")]
     if other:
         roof["other_kernel"] = other[0]
+    # latency floor: a late merge is a chain of dependent round
+    # trips, not bytes; the floor counts them at the guide's idle-chip latencies
+    floor_kernel = len(LATE_MERGE_HOPS) * HOP_US
+    lf = {"hops": list(LATE_MERGE_HOPS), "hop_us": HOP_US, "boundary_us": BOUNDARY_US,
+          "us_per_launch": round(floor_kernel, 3), "us_per_merge": round(floor_kernel + BOUNDARY_US, 3),
+          "meaning": "dependent Infinity-Cache round trips of one late merge (one k_body launch with its in-launch "
+                     "close) x ~545 cycles, plus one kernel boundary per merge; achieved / floor says how far the "
+                     "chain is from its own bound, as frac does for bytes"}
+    if roof.get("us_per_launch"):
+        lf["achieved_us_per_launch"] = roof["us_per_launch"]
+        lf["achieved_over_floor"] = round(roof["us_per_launch"] / floor_kernel, 2)
+    if det.get("late_window"):
+        w = det["late_window"]
+        lf["late_window"] = w
+        lf["late_achieved_over_floor"] = round(w["us_per_merge"] / (floor_kernel + BOUNDARY_US), 2)
+    roof["latency_floor"] = lf
     roof["dense_stream"] = dense
     roof["dense_equivalent"] = {"gbps": round(equiv, 1), "frac": round(equiv / HBM_PEAK_GBPS, 4),
                                 "bytes": det["stream_bytes"],
@@ -320,6 +359,29 @@ def train_roofline(det, wall_per_run):
     return roof
 
 
+def single_gpu_roofline(args, lib, ctx, d, n):
+    """The N = 1 line's roofline on this GPU (N > 1 lines, rank 0): one HIP-event
+    run and one per-step-timed run of the headline workload."""
+    from gpubpe import _lib
+    _, sk = train_run(lib, ctx, d, n, args.vocab, flags=_lib.GBPE_TRAIN_TIMING)
+    steps = []
+    t0 = time.perf_counter()
+    last, st = train_run(lib, ctx, d, n, args.vocab, steps_out=steps)
+    wall = time.perf_counter() - t0
+    det = train_detail(st, sk)
+    done, late_m, late_s = 0, 0, 0.0
+    for m, sec in steps:
+        if done >= 16384:
+            late_m += m
+            late_s += sec
+        done += m
+    if late_m:
+        det["late_window"] = {"merges_from": 16384, "merges": late_m, "us_per_merge": round(1e6 * late_s / late_m, 3)}
+    roof = train_roofline(det, wall)
+    roof["measured"] = "rank 0 of this run, alone on its GPU: one HIP-event run and one step-timed run of the headline"
+    return roof
+
+
 def headline_leg(args, lib, ctx, dist):
     t = time.time()
     data = make_corpus(HEADLINE)
@@ -333,8 +395,29 @@ def headline_leg(args, lib, ctx, dist):
     if not args.no_kernel_timing:
         from gpubpe import _lib
         _, sk = train_run(lib, ctx, d, n, args.vocab, flags=_lib.GBPE_TRAIN_TIMING)
+    steps = []   # one more untimed run with per-step host walls: the late-merge window's cost per merge
+    train_run(lib, ctx, d, n, args.vocab, steps_out=steps)
     lib.gbpe_device_free(ctx, d)
     det = train_detail(st, sk)
+    det["reference_rate"] = {
+        "value": round(total / (wall - st.create_s_total), 1), "unit": "merges/s",
+        "create_ms_per_run": round(1e3 * st.create_s_total / max(1, args.steps), 3),
+        "definition": "the reference's merges/s = merges / t_loop (trainer.js:230, 291-292, 324-326): the timed "
+                      "wall minus trainer creation (symbols, word starts, first count), which t_loop excludes; "
+                      "`value` keeps creation inside"}
+    done, late_m, late_s = 0, 0, 0.0
+    for m, sec in steps:
+        if done >= 16384:
+            late_m += m
+            late_s += sec
+        done += m
+    if late_m:
+        det["late_window"] = {"merges_from": 16384, "merges": late_m, "us_per_merge": round(1e6 * late_s / late_m, 3),
+                              "timing": "host wall of every gbpe_trainer_step call (128 merges, one sync) of one "
+                                        "untimed run"}
+    # SURVEY §8(d) N_i: the stream length before each merge, logged per 128-merge step
+    n_i = n - np.concatenate([[0], np.cumsum(last[:, 3].astype(np.int64))])
+    det["n_i_per_step"] = {"every": 128, "values": [int(v) for v in n_i[::128]], "final": int(n_i[-1])}
     det["reference_table"] = ref_table(st, pairs)
     det["merges_per_run"] = int(last.shape[0])
     det["last_merge"] = last[-1].tolist() if last.shape[0] else []
@@ -593,6 +676,7 @@ def single_line(args, lib, ctx, dist, rank):
                    "train_bytes": HEADLINE["n"], "target_vocab": args.vocab,
                    "merges_per_step": det["merges_per_run"], "parallelism": "single"},
         "roofline": train_roofline(det, wall / max(1, args.steps)),
+        "reference_rate": det["reference_rate"],
         "train_detail": det,
         "parity": parity,
     }
@@ -724,21 +808,80 @@ def split_encode_leg(args, lib, ctx, dist, rank, world):
     return res
 
 
-def lexshard_run(lib, ctx, dist, d, n, vocab, flags=0, want_final=False):
+def recount_pairs(fin_host: np.ndarray):
+    """Live pair counts of a u32 reference-layout stream, recounted on the device
+    with torch (a pair (i-1, i) counts iff i is not a word start and neither token
+    is 0: train.wgsl:393-399).  Returns (sorted pair ids, counts)."""
+    import torch
+    n = fin_host.shape[0]
+    step = 1 << 28
+    keys, cnts = [], []
+    for s0 in range(0, max(1, n - 1), step):
+        s1 = min(n, s0 + step + 1)
+        x = torch.from_numpy(fin_host[s0:s1].view(np.int32)).cuda().to(torch.int64) & 0xFFFFFFFF
+        prev, cur = x[:-1], x[1:]
+        ok = ((cur & 0x10000) == 0) & ((prev & 0xFFFF) != 0) & ((cur & 0xFFFF) != 0)
+        pid = ((prev & 0xFFFF) << 16) | (cur & 0xFFFF)
+        u, c = torch.unique(pid[ok], return_counts=True)
+        keys.append(u)
+        cnts.append(c)
+        del x, prev, cur, ok, pid
+    k = torch.cat(keys)
+    c = torch.cat(cnts)
+    u, inv = torch.unique(k, return_inverse=True)
+    tot = torch.zeros(u.shape[0], dtype=torch.int64, device=u.device).index_add_(0, inv, c)
+    return u.cpu().numpy().astype(np.uint32), tot.cpu().numpy()
+
+
+def root_recount_check(lib, ctx, be, fin):
+    """The hand-over root's live pair counts (gbpe_trainer_pair_counts) against a
+    device recount of the final stream it rebuilt from every rank's occurrence list
+    (counts are additive over word-start pieces: train.wgsl:395, 483, 493)."""
+    from gpubpe import _lib
+    st = be.root_stats()
+    cnt = C.c_uint64()
+    lib.gbpe_trainer_pair_counts(be.t, None, None, 0, C.byref(cnt))
+    pids = np.zeros(max(1, cnt.value), np.uint32)
+    cts = np.zeros(max(1, cnt.value), np.uint32)
+    _lib.check(lib.gbpe_trainer_pair_counts(be.t, pids.ctypes.data_as(_lib.u32p), cts.ctypes.data_as(_lib.u32p),
+                                            cnt.value, C.byref(cnt)), ctx, "pair_counts")
+    o = np.argsort(pids[: cnt.value])
+    tp, tc = pids[: cnt.value][o], cts[: cnt.value][o].astype(np.int64)
+    t0 = time.perf_counter()
+    rp, rc = recount_pairs(fin)
+    res = {"final_symbols": int(fin.shape[0]), "final_symbols_equal_trainer": int(fin.shape[0]) == int(st.symbol_count),
+           "pairs_live_table": int(tp.shape[0]), "pairs_live_recount": int(rp.shape[0]),
+           "counts_equal_recount": bool(tp.shape == rp.shape and np.array_equal(tp, rp) and np.array_equal(tc, rc)),
+           "seconds_recount": round(time.perf_counter() - t0, 2)}
+    if not res["counts_equal_recount"] and tp.shape == rp.shape:
+        bad = np.flatnonzero((tp != rp) | (tc != rc))
+        res["first_diff"] = [int(tp[bad[0]]), int(tc[bad[0]]), int(rp[bad[0]]), int(rc[bad[0]])]
+    return res
+
+
+def lexshard_run(lib, ctx, dist, d, n, vocab, flags=0, want_final=False, check=False):
     """One complete run of the sharded first pass + lexicon hand-over (DESIGN §5,
     gpubpe/lexshard.py) on this rank's HBM-resident piece; every rank returns the
     global merge list.  RCCL moves the stores point to point (device tensors);
-    GBPE_SHARD_TRANSPORT=gloo (ranks sharing one GPU) moves host copies."""
+    GBPE_SHARD_TRANSPORT=gloo (ranks sharing one GPU) moves host copies.  `check`:
+    after the run the root recounts the final stream (root_recount_check; returned
+    on the root, None elsewhere)."""
     from gpubpe.lexshard import GpuLexBackend, LexShardTrainer
     be = GpuLexBackend(lib, ctx, vocab, flags=flags)
     staged = dist.transport != "nccl"
     tr = LexShardTrainer(be, dist.dist, staged=staged, host_group=None if staged else dist.host)
+    chk = None
     try:
         merges, early = tr.train(d, n, True, vocab)
-        fin = tr.final_stream() if want_final else None
+        fin = tr.final_stream() if (want_final or check) else None
+        if check and tr.rank == tr.root:
+            chk = root_recount_check(lib, ctx, be, fin)
+            if not want_final:
+                fin = None
     finally:
         be.close()
-    return np.array(merges, dtype=np.uint32).reshape(-1, 4), tr, fin
+    m = np.array(merges, dtype=np.uint32).reshape(-1, 4)
+    return (m, tr, fin, chk) if check else (m, tr, fin)
 
 
 LEX_PHASES = ("create_s", "build_s", "exchange_s", "root_create_s", "loop_s", "total_s")   # LexShardTrainer.timing
@@ -789,6 +932,16 @@ def lexshard_line(args, lib, ctx, dist, rank, world):
     lib.gbpe_device_free(ctx, dfull)
     rst = tr.root_stats if rank == world - 1 else None
     sh = tr.shapes
+    # the roofline and the CPU baseline of the N = 1 line, measured on rank 0 (the
+    # merge loop is the single-GPU one: the root runs it on the global lexicon)
+    roof, cpu_base = None, None
+    if rank == 0:
+        droof = device_buffer(lib, ctx, full)
+        roof = single_gpu_roofline(args, lib, ctx, droof, len(full))
+        lib.gbpe_device_free(ctx, droof)
+        if not args.no_cpu:
+            cpu_base, _, _ = cpu_baselines(args, full, None)
+    dist.barrier()
     line = {
         "metric": METRIC,
         "value": round(total / wall, 1),
@@ -809,8 +962,7 @@ def lexshard_line(args, lib, ctx, dist, rank, world):
                                "chain is sequential), merge list broadcast",
                    "train_bytes": HEADLINE["n"], "target_vocab": args.vocab,
                    "merges_per_step": int(last.shape[0]), "parallelism": f"lexshard{world} ({dist.transport})"},
-        "roofline": {"bound": "hbm", "kernel": "see the N=1 line (the merge loop is the single-GPU one on the root)",
-                     "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None, "traffic": None},
+        "roofline": roof,
         "train_detail": {"timing_s_max_over_ranks": timing,
                          "pieces": {"symbols": sh[:, 5].tolist(), "store_symbols": sh[:, 0].tolist(),
                                     "entries": sh[:, 1].tolist(), "words": sh[:, 2].tolist(),
@@ -822,6 +974,8 @@ def lexshard_line(args, lib, ctx, dist, rank, world):
                        "merges_equal_fixture": bool(want is not None and np.array_equal(rlast, want))},
         "parity": parity,
     }
+    if cpu_base is not None:
+        line["cpu_baseline"] = cpu_base
     if rst is not None:
         line["train_detail"]["root"] = {"sparse_exits": int(rst.sparse_exits), "max_live_pairs": int(rst.max_live_pairs),
                                         "lexicon_entries": int(rst.lexicon_entries)}
@@ -860,8 +1014,21 @@ def c4_line(args, lib, ctx, dist, rank, world):
     t1 = time.perf_counter()
     dist.barrier()
     wall = dist.max(t1 - t0) / runs
-    lib.gbpe_device_free(ctx, d)
     timing = lex_timing(dist, tr)
+    # the self-check: one more, untimed run whose root recounts
+    # the final stream the ranks' occurrence lists rebuild, against its live counts
+    check = None
+    if not args.no_c4_check:
+        try:
+            clast, _, _, check = lexshard_run(lib, ctx, dist, d, n, 65536, check=True)
+            if check is not None:
+                check["merges_equal_timed_run"] = bool(np.array_equal(clast, last))
+        except Exception as e:  # noqa: BLE001
+            check = {"error": f"{type(e).__name__}: {e}"}
+        objs = [None] * world
+        dist.dist.all_gather_object(objs, check, group=dist.host)
+        check = next((o for o in objs if o is not None), None)
+    lib.gbpe_device_free(ctx, d)
     sh = tr.shapes
     rst = tr.root_stats if rank == world - 1 else None
     res = {"workload": f"C4: 64K-vocab train on {world} x {args.c4_shard} B multilingual UTF-8 shards "
@@ -872,6 +1039,9 @@ def c4_line(args, lib, ctx, dist, rank, world):
            "merges_sha256": hashlib.sha256(np.ascontiguousarray(last, "<u4").tobytes()).hexdigest(),
            "timing_s_max_over_ranks": timing, "transport": dist.transport,
            "stream_symbols": int(sh[:, 5].sum()), "store_symbols": int(sh[:, 0].sum()), "zone": int(sh[-1, 4])}
+    if check is not None:
+        res["check"] = check
+        res["counts_equal_recount"] = bool(check.get("counts_equal_recount", False))
     if rst is not None:
         from gpubpe import reftable
         res["root"] = {"sparse_exits": int(rst.sparse_exits), "lexicon_entries": int(rst.lexicon_entries),
@@ -934,6 +1104,8 @@ def main():
                     help="only the C4 leg: one multilingual shard per rank (seed 5 + rank), one 64K vocab")
     ap.add_argument("--c4-shard", type=int, default=C4_SHARD, help="C4 shard bytes per rank")
     ap.add_argument("--c4-runs", type=int, default=1)
+    ap.add_argument("--no-c4-check", action="store_true",
+                    help="skip the C4 leg's untimed self-check run (root live counts vs a recount of the final stream)")
     args = ap.parse_args()
 
     rank, world, local = dist_env()

@@ -455,9 +455,9 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
         if (zout) {
             zout[0] = m;
             zout[1] = Kz + m;
-        } else {   // (agent-scope stores: an in-launch close reads them, merge_close)
-            __hip_atomic_store(&zst->m, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&zst->valid_total, Kz + m + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            zst->m = m;
+            zst->valid_total = Kz + m + 1u;   // survivors + 1 (k_refresh checks it against the new layout)
         }
         // zone read, window source read, kept survivors + window written
         atomicAdd(bytes, (uint64_t)sizeof(S) * ((uint64_t)z + (EXACT ? 0u : mc) + Kz + m));
@@ -706,7 +706,7 @@ __device__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const 
 // step counters move on in k_refresh (finish == 2), so nothing a workgroup reads
 // here changes under it.  Saves the k_select launch per merge.
 struct SelShard {
-    uint32_t zf = 3;         // zone rule: z >= max(2 mc + mc_prev, zf mc) + 2 (GBPE_ZONE_F)
+    uint32_t zf = 3;         // zone rule: z >= max(2 mc + mc_prev, zf mc) + 2 (trainer zone_f)
 };
 
 template <int BT>
@@ -735,7 +735,7 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
     const DevState& g = s_g.d;
     gsnap = &s_g.d;
     zsnap = &s_z.d;
-    if (!(round < g.budget && g.merges_done == round && !g.stop && !g.sp_abort && !g.refresh_due)) return false;
+    if (!(round < g.budget && g.merges_done == round && !g.stop && !g.sp_abort)) return false;
     best = wave_max_u64(best);
     if ((t & 63) == 0) s_red[t >> 6] = best;
     __syncthreads();
@@ -773,12 +773,9 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
                     atomicOr(&st->err, ERR_PAIR_MISSING);
                 } else {
                     // every (a,b) occurrence is a merge site: count -= mc, atomically, since
-                    // other workgroups may already add this merge's stale-window pairs.  Its
-                    // block held the table maximum: it is always re-maxed
+                    // other workgroups may already add this merge's stale-window pairs
                     atomicSub(&tb.slots[idx].y, mc);
-                    const uint32_t blk = idx >> BLK_LOG2;
-                    if (tb.fbits) atomicOr(&tb.fbits[blk >> 5], 1u << (blk & 31u));
-                    else tb.dirty[blk] = 1u;
+                    tb.dirty[idx >> BLK_LOG2] = 1u;
                 }
                 log[round * 4 + 0] = a;
                 log[round * 4 + 1] = b;
@@ -808,219 +805,6 @@ __device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restri
         }
     }
     return go;
-}
-
-// ── in-launch merge close ──
-// With the zone in one workgroup (zone_one), a merge is ONE launch: the table
-// adds keep the block maxima exact-or-flagged themselves (table_inc, train_dev.h),
-// every workgroup arrives at a ticket once its adds have landed, and the last
-// one re-maxes the flagged blocks, recomputes their partial maxima and closes the
-// merge's state — what k_refresh (finish 2) does as a second launch otherwise.
-// The partial maxima are double-buffered by merge parity: a launch selects from
-// one half (every workgroup, sel_inline) while its increments raise the other, so
-// a workgroup that starts late still selects from the launch's own snapshot.
-struct CloseState {
-    uint32_t ticket;                 // workgroups of this launch that arrived (the last one resets it)
-    uint32_t pad[15];
-    unsigned long long closes;       // merges closed in-launch
-    unsigned long long remax;        // blocks they re-maxed
-    unsigned long long ovf;          // closes with more than CL_FMAX flagged blocks (dirty flags + host k_refresh)
-    uint32_t* clog;                  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors (null: off)
-};
-constexpr uint32_t CL_FMAX = 256;    // flagged blocks one close re-maxes
-constexpr uint32_t CL_PMAX = 2048;   // partial maxima (the host uses the close only up to this many)
-constexpr uint32_t CL_KW = 16;       // bitmap words per thread (host: nblk <= 32 * CL_KW * 256)
-struct CloseLds {
-    uint64_t gval[CL_PMAX];          // recomputed partial maximum of each flagged group
-    uint64_t fbm[CL_FMAX];           // new maximum of each flagged block
-    uint32_t fl[CL_FMAX];            // flagged blocks, ascending
-    uint32_t gfl[CL_PMAX / 32];      // flagged groups (bits)
-    uint32_t wsum[16];
-    uint32_t sv[8];                  // what the launch's workgroups added to the states
-};
-
-// every wave's adds and stores have landed, then one ticket per workgroup; true
-// in the last workgroup to arrive (MI355X_MICROARCH.md, hand-off row "one lane
-// of each storing workgroup ... the workgroup whose add came last")
-__device__ __forceinline__ bool close_last(CloseState* cs) {
-    __shared__ uint32_t s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-        s_last = __hip_atomic_fetch_add(&cs->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
-    __syncthreads();
-    return s_last != 0u;
-}
-
-template <typename T>
-__device__ __forceinline__ T ld_agent(const T* p) {   // every read of bytes this launch wrote: L1 bypassed
-    return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T>
-__device__ __forceinline__ void st_agent(T* p, T v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The last workgroup's close: (1) the flagged-block bitmap, the raised partial
-// maxima and the state counters in one round trip; (2) the flagged blocks re-maxed,
-// one wave per block; (3) the block maxima of their groups (now final) reduced into
-// the partial maxima of both halves; (4) the merge's state moved on (k_refresh's
-// finish-2 bookkeeping: train.wgsl:605-607's symbol count, the body and zone lengths).
-template <int BT>
-__device__ void merge_close(DevState* st, DevState* zst, const DevState& gs, uint32_t round, uint32_t mc,
-                            const Table& tb, uint64_t* __restrict__ pr, uint32_t npart, CloseState* cs,
-                            CloseLds& L) {
-    using u64 = unsigned long long;
-    constexpr int NWV = BT / 64;
-    constexpr int PPT = (int)(CL_PMAX / BT);
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const uint32_t nfw = (tb.nblk + 31u) >> 5;
-    const uint32_t K = (nfw + BT - 1) / BT;   // <= CL_KW
-    const uint32_t w0 = (uint32_t)t * K;
-    const uint32_t per = tb.per;
-    // (1)
-    uint32_t fw[CL_KW];
-#pragma unroll
-    for (uint32_t k = 0; k < CL_KW; ++k) fw[k] = (k < K && w0 + k < nfw) ? ld_agent(&tb.fbits[w0 + k]) : 0u;
-    if (t < 5) {
-        const uint32_t* src = t == 0 ? &st->body_rm : t == 1 ? &st->cand : t == 2 ? &st->hitsec : t == 3 ? &zst->m
-                                                                                                          : &zst->valid_total;
-        L.sv[t] = ld_agent(src);
-    }
-    uint32_t c = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < CL_KW; ++k) c += (uint32_t)__popc(fw[k]);
-    const uint32_t incl = wave_scan_incl_u32(c);
-    if (lane == 63) L.wsum[wid] = incl;
-    for (uint32_t i = t; i < CL_PMAX / 32; i += BT) L.gfl[i] = 0u;
-    __syncthreads();
-    uint32_t pre = incl - c, F = 0;
-#pragma unroll
-    for (int w = 0; w < NWV; ++w) {
-        pre += w < wid ? L.wsum[w] : 0u;
-        F += L.wsum[w];
-    }
-    const bool ovf = F > CL_FMAX;   // (block-uniform)
-    // the flagged blocks in ascending order (too many: dirty flags for the host's
-    // k_refresh); their words cleared for the next merge
-#pragma unroll
-    for (uint32_t k = 0; k < CL_KW; ++k) {
-        uint32_t v = fw[k];
-        if (!v) continue;
-        st_agent(&tb.fbits[w0 + k], 0u);
-        while (v) {
-            const uint32_t blk = (w0 + k) * 32u + (uint32_t)(__ffs(v) - 1);
-            v &= v - 1;
-            if (ovf) {
-                tb.dirty[blk] = 1u;
-            } else {
-                const uint32_t g = blk / per;
-                L.fl[pre++] = blk;
-                atomicOr(&L.gfl[g >> 5], 1u << (g & 31u));
-            }
-        }
-    }
-    __syncthreads();
-    if (!ovf) {
-        // (2) a wave per flagged block, 2 blocks in flight per wave
-        constexpr int J = 2;
-        for (uint32_t i0 = (uint32_t)wid; i0 < F; i0 += J * NWV) {
-            u64 e[J][4];
-#pragma unroll
-            for (int j = 0; j < J; ++j) {
-                const uint32_t i = i0 + (uint32_t)j * NWV;
-                const u64* sl = reinterpret_cast<const u64*>(tb.slots) + ((uint64_t)(i < F ? L.fl[i] : 0u) << BLK_LOG2) +
-                                4u * (uint32_t)lane;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) e[j][q] = i < F ? ld_agent(sl + q) : 0ull;
-            }
-#pragma unroll
-            for (int j = 0; j < J; ++j) {
-                const uint32_t i = i0 + (uint32_t)j * NWV;
-                if (i >= F) break;   // (wave-uniform)
-                uint64_t best = KEY_NONE;
-                uint32_t live = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t pid = (uint32_t)e[j][q], cnt = (uint32_t)(e[j][q] >> 32);
-                    if (pid && (int32_t)cnt > 0) {
-                        const uint64_t key = ((uint64_t)cnt << 32) | (uint32_t)~pid;
-                        best = key > best ? key : best;
-                        ++live;
-                    }
-                }
-                best = wave_max_u64(best);
-                live = wave_sum_u32(live);
-                if (lane == 0) {
-                    const uint32_t blk = L.fl[i];
-                    L.fbm[i] = best;
-                    st_agent(reinterpret_cast<u64*>(&tb.bmax[blk]), (u64)best);
-                    st_agent(&tb.blive[blk], live);
-                }
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        // (3) each flagged group's block maxima (all final now), one wave per group,
-        // beside the raised partial maxima of every group (final too)
-        u64 pw[PPT];
-#pragma unroll
-        for (int k = 0; k < PPT; ++k) {
-            const uint32_t g = (uint32_t)t + (uint32_t)k * BT;
-            pw[k] = g < npart ? ld_agent(reinterpret_cast<const u64*>(&tb.pinc[g])) : 0ull;
-        }
-        for (uint32_t i = (uint32_t)wid; i < F; i += NWV) {
-            const uint32_t g = L.fl[i] / per;
-            if (i && L.fl[i - 1] / per == g) continue;   // (wave-uniform) not the group's first flagged block
-            const uint32_t b = g * per + (uint32_t)lane;
-            u64 v = ((uint32_t)lane < per && b < tb.nblk) ? ld_agent(reinterpret_cast<const u64*>(&tb.bmax[b])) : 0ull;
-            v = wave_max_u64(v);
-            if (lane == 0) L.gval[g] = v;
-        }
-        __syncthreads();
-        // both halves of the partial maxima: the one this launch selected from gets
-        // every group (the next launch raises it), the other the flagged groups
-#pragma unroll
-        for (int k = 0; k < PPT; ++k) {
-            const uint32_t g = (uint32_t)t + (uint32_t)k * BT;
-            if (g >= npart) continue;
-            const bool f = (L.gfl[g >> 5] >> (g & 31u)) & 1u;
-            const u64 v = f ? (u64)L.gval[g] : pw[k];
-            st_agent(reinterpret_cast<u64*>(&pr[g]), v);
-            if (f) st_agent(reinterpret_cast<u64*>(&tb.pinc[g]), v);
-        }
-    }
-    // (4) the merge's state (k_refresh, finish 2)
-    if (t == 0) {
-        const uint32_t body_rm = L.sv[0], zm = L.sv[3], vt = L.sv[4];
-        st->merges_done = round + 1u;
-        st->next_id = gs.next_id + 1u;
-        st->epoch = gs.epoch + 1u;
-        st->mc_prev = mc;
-        if (uint32_t* clog = cs->clog) {
-            clog[2 * round] = L.sv[1];
-            clog[2 * round + 1] = L.sv[2];
-        }
-        st_agent(&st->cand, 0u);
-        st_agent(&st->hitsec, 0u);
-        st->tail_total = gs.tail_total + zm;
-        const uint32_t n = gs.n - mc, B = gs.B - body_rm, zn = n - B;
-        st->n = n;
-        st->Bp = gs.B;
-        st->B = B;
-        st_agent(&st->body_rm, 0u);
-        zst->n = zn;
-        st->zlast = zn;
-        if (vt && vt != zn + 1u) atomicOr(&st->err, ERR_COUNT_MISMATCH);
-        if (ovf) {
-            st->refresh_due = 1u;
-            cs->ovf += 1ull;
-        } else {
-            cs->remax += F;
-        }
-        cs->closes += 1ull;
-        st_agent(&cs->ticket, 0u);
-    }
 }
 
 // Body pass: blocks [0, nbody) each own `wpg` consecutive bitmap words of
@@ -1057,7 +841,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
                                               Table dtb, SelShard sh, uint32_t* __restrict__ lmul,
-                                              ZSegState* __restrict__ zg, CloseState* __restrict__ cls) {
+                                              ZSegState* __restrict__ zg = nullptr) {
     constexpr int KB_LT = ZSEG ? 4096 : LTAB_T;   // (4096 for every 1024-thread form: no change on C5 / 1 GiB / C2, r4)
     __shared__ LdsTab<KB_LT> lt;
     __shared__ BodyLds<S, BT> u;
@@ -1086,13 +870,9 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         return;
     }
     if (t == 0) KT(1);
-    // in-launch close (cls: the host runs no k_refresh after this launch): every
-    // workgroup arrives once its adds have landed, the last one closes the merge
-    static_assert(sizeof(CloseLds) <= sizeof(BodyLds<S, BT>), "close scratch aliases the candidate arrays");
     // the zone workgroup is dispatched first (block 0 when zone1): it is the longest
     // single chain of the merge, and later blocks of a large grid start later
     const uint32_t bid = blockIdx.x - zone1;
-    do {   // (every non-ZSEG path leaves through the close below)
     if constexpr (ZSEG) {
         if (blockIdx.x < zone1) {
             zone_seg<S, EXACT, BT, KB_LT, 16>(st, zst, *gs, *zs, zcur, (S*)zoth, zg, zone1, u.z, lt, dtb, a, b, nw, mc,
@@ -1111,7 +891,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                 KT(5);
                 KTV(6, 2);
             }
-            break;
+            return;
         }
     }
     if (bid >= nbody) {
@@ -1122,7 +902,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
             KT(5);
             KTV(6, 3);
         }
-        break;
+        return;
     }
     const uint32_t pid_ab = (a << 16) | b;
     BodyCand& cb = u.c;
@@ -1244,7 +1024,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
             KT(5);
             KTV(6, 0);
         }
-        break;
+        return;
     }
     if (t == 0 && clog) atomicAdd(&st->cand, ncand_all);
     lds_flush(lt, xtb, st);
@@ -1265,11 +1045,6 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         KT(5);
         KTV(6, 1 | (ncand_all << 8));
     }
-    } while (false);
-    if constexpr (!ZSEG)   // (the zone segments' steps close in k_refresh)
-        if (cls && close_last(cls))
-            merge_close<BT>(st, zst, *gs, round, mc, dtb, const_cast<uint64_t*>(part), npart, cls,
-                            *reinterpret_cast<CloseLds*>(&u));
 }
 
 // dense → sparse: the last position at or before `lim` that no counted pair can

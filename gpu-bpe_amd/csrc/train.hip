@@ -420,19 +420,6 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         TR_HIP(t, hipMemcpyToSymbol(HIP_SYMBOL(g_bsprof), z, sizeof(z), 0, hipMemcpyHostToDevice));
     }
 #endif
-    if (sparse && hs->refresh_due) {   // an in-launch close flagged more blocks than it re-maxes: their dirty
-                                       // flags are set, the step's later launches ran no merge
-        if (t->u16)
-            hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
-                               (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr,
-                               FusedSel(), t->part, (uint32_t*)nullptr);
-        else
-            hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
-                               (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr,
-                               FusedSel(), t->part, (uint32_t*)nullptr);
-        GBPE_LAUNCH_CHECK(t->ctx);
-        hs->refresh_due = 0u;
-    }
     const uint32_t err = hs->err | (sparse ? t->h_zst->err : 0u);
     if (err) {
         return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "training invariant violated (err=0x%x: %s%s%s%s%s)", err,
@@ -554,14 +541,6 @@ extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
     o->ms_dense = t->ms_dense;
     o->ms_sparse = t->ms_sparse;
     o->ms_body = t->ms_body;
-    if (t->cls) {
-        CloseState h{};
-        if (hipMemcpy(&h, t->cls, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
-            o->close_inlaunch = h.closes;
-            o->close_remax_blocks = h.remax;
-            o->close_refreshes = h.ovf;
-        }
-    }
     o->ms_create = t->ms_create;
     o->zone_bytes = t->h_st->sp_bytes;
     o->lexicon_builds = (uint32_t)t->lx_builds;
@@ -717,8 +696,6 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     pool_free(t->ctx, t->zst);
     pool_free(t->ctx, t->d_u32);
     pool_free(t->ctx, t->part);
-    pool_free(t->ctx, t->fbits);
-    pool_free(t->ctx, t->cls);
     pool_free(t->ctx, t->d_bhist);
     pool_free(t->ctx, t->zseg);
     pool_free(t->ctx, t->zdr_out);

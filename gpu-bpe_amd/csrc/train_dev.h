@@ -68,23 +68,6 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
            __builtin_amdgcn_readlane(v, 48);
 }
-// the wave's minimum / maximum of a u32 (uniform)
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-    v = min(v, dpp32<0xB1>(v));
-    v = min(v, dpp32<0x4E>(v));
-    v = min(v, dpp32<0x141>(v));
-    v = min(v, dpp32<0x140>(v));
-    return min(min((uint32_t)__builtin_amdgcn_readlane(v, 0), (uint32_t)__builtin_amdgcn_readlane(v, 16)),
-               min((uint32_t)__builtin_amdgcn_readlane(v, 32), (uint32_t)__builtin_amdgcn_readlane(v, 48)));
-}
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-    v = max(v, dpp32<0xB1>(v));
-    v = max(v, dpp32<0x4E>(v));
-    v = max(v, dpp32<0x141>(v));
-    v = max(v, dpp32<0x140>(v));
-    return max(max((uint32_t)__builtin_amdgcn_readlane(v, 0), (uint32_t)__builtin_amdgcn_readlane(v, 16)),
-               max((uint32_t)__builtin_amdgcn_readlane(v, 32), (uint32_t)__builtin_amdgcn_readlane(v, 48)));
-}
 // inclusive prefix sum over the wave's lanes
 __device__ __forceinline__ uint32_t wave_scan_incl_u32(uint32_t v) {
     v += dpp32<0x111>(v);          // row_shr:1 (lanes shifted in from outside the row add 0)
@@ -129,8 +112,6 @@ struct DevState {
                            // (never written by a commit: a reader beside k_body would see it unchanged)
     uint32_t enter_lim;    // dense loop: end the step at the first merge whose count is <= this (the host
                            // can then enter the sector-sparse loop; 0 = off)
-    uint32_t refresh_due;  // in-launch close: too many blocks to re-max in one workgroup; their dirty flags are
-                           // set and the step's later launches run no merge until the host's k_refresh
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
@@ -210,15 +191,6 @@ struct Table {
     uint32_t* blive;   // per block: entries with count > 0
     uint32_t nblk;
     uint32_t* used;    // occupied-slot counter (DevState::used or ::dused)
-    // In-launch close (sector-sparse merges with the zone in one workgroup):
-    // with `fbits` set, every add keeps the block maxima and the partial maxima
-    // exact-or-flagged itself instead of marking its block dirty for k_refresh — an
-    // increment raises bmax and pinc to its new key (atomic max), a decrement flags
-    // its block in `fbits` when its old key was at least the block maximum — and the
-    // launch's last workgroup re-maxes the flagged blocks (merge_close, sparse.h).
-    uint32_t* fbits = nullptr;   // flagged-block bitmap (null: dirty flags + k_refresh)
-    uint64_t* pinc = nullptr;    // partial maxima the increments raise (the next launch selects from them)
-    uint32_t per = 64;           // argmax blocks per partial maximum
 };
 
 // the key of a block without a positive count (count 0, the weakest tie-break)
@@ -228,42 +200,6 @@ constexpr uint64_t KEY_NONE = 0xFFFFFFFFull;
 __device__ __forceinline__ void mark_dirty(const Table& tb, DevState* st, uint32_t slot) {
     (void)st;
     tb.dirty[slot >> BLK_LOG2] = 1u;
-}
-
-// An add in the in-launch close mode (Table::fbits): the slot's count changes by
-// one returning atomic, whose old value tells what the block maximum needs.
-//  * increment to a positive count: bmax and the partial maximum are raised to the
-//    new key (u64 atomic max, no return);
-//  * decrement from a positive count: the block is flagged when the old key is >=
-//    the block maximum read at any moment of the merge.  Why that suffices: bmax
-//    only grows during the merge (atomic max) from its exact value at the launch,
-//    to B_f = max(start, every increment's key).  If the block's final maximum is
-//    below B_f, the slot s that held key B_f (at the launch, or right after the
-//    increment that set it) was decremented later; the first such decrement
-//    returns an old count >= the one of B_f, so its old key is >= B_f >= any bmax
-//    it can read, and it flags the block.  Interleavings of increments and
-//    decrements of one slot across workgroups, transient negative counts
-//    (u32 wrap) and ties (keys carry ~pid, unique per slot) are all covered.
-//  * live counts move by the slot's sign changes (they telescope over any order).
-__device__ __forceinline__ void table_inc(const Table& tb, uint32_t idx, uint32_t pid, uint32_t delta) {
-    const uint32_t blk = idx >> BLK_LOG2;
-    const uint32_t lo = ~pid;
-    if ((int32_t)delta < 0) {
-        const uint64_t bm = __hip_atomic_load(&tb.bmax[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t old = atomicAdd(&tb.slots[idx].y, delta);
-        if ((int32_t)old > 0) {
-            if ((int32_t)(old + delta) <= 0) atomicSub(&tb.blive[blk], 1u);
-            if ((((uint64_t)old << 32) | lo) >= bm) atomicOr(&tb.fbits[blk >> 5], 1u << (blk & 31u));
-        }
-    } else {
-        const uint32_t old = atomicAdd(&tb.slots[idx].y, delta), nu = old + delta;
-        if ((int32_t)nu > 0) {
-            const unsigned long long key = ((unsigned long long)nu << 32) | lo;
-            atomicMax(reinterpret_cast<unsigned long long*>(&tb.bmax[blk]), key);
-            atomicMax(reinterpret_cast<unsigned long long*>(&tb.pinc[blk / tb.per]), key);
-            if ((int32_t)old <= 0) atomicAdd(&tb.blive[blk], 1u);
-        }
-    }
 }
 
 // global insert-or-add (triangular probing visits every slot of a 2^k table)
@@ -280,12 +216,8 @@ __device__ void table_add(const Table& tb, DevState* st, uint32_t pid, uint32_t 
             }
         }
         if (k == pid) {
-            if (tb.fbits) {
-                table_inc(tb, idx, pid, delta);
-            } else {
-                atomicAdd(&tb.slots[idx].y, delta);
-                mark_dirty(tb, st, idx);
-            }
+            atomicAdd(&tb.slots[idx].y, delta);
+            mark_dirty(tb, st, idx);
             return;
         }
     }
@@ -352,12 +284,8 @@ __device__ __forceinline__ void table_add8(const Table& tb, DevState* st, const 
     for (int j = 0; j < 8; ++j) {
         if (!kk[j] || !vv[j]) continue;
         if (hk[j] == kk[j]) {
-            if (tb.fbits) {
-                table_inc(tb, hs[j], kk[j], vv[j]);
-            } else {
-                atomicAdd(&tb.slots[hs[j]].y, vv[j]);
-                mark_dirty(tb, st, hs[j]);
-            }
+            atomicAdd(&tb.slots[hs[j]].y, vv[j]);
+            mark_dirty(tb, st, hs[j]);
         } else {
             table_add(tb, st, kk[j], vv[j]);
         }
@@ -616,7 +544,6 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
     if (zseg && blockIdx.x == 0)   // ZSegState: ticket + granules of the next merge's zone segments
         for (uint32_t i = threadIdx.x; i < ZSEG_WORDS; i += TPB)
             if (i == 0 || i >= 16) zseg[i] = 0u;
-    if (part && !finish && blockIdx.x == 0 && threadIdx.x == 0) st->refresh_due = 0u;   // (an in-launch close's overflow)
     (void)rwlist;
     if (part && finish == 2 && threadIdx.x == 0) KTR(0);
     // this WG's contiguous run of blocks (<= 64): all flags (and, for `part`, the
@@ -737,8 +664,7 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
     if (part && threadIdx.x < 64) {   // this workgroup's maximum, for sel_inline
         const uint64_t best = wave_max_u64(s_bm[threadIdx.x]);
         if (threadIdx.x == 0) {
-            part[blockIdx.x] = best;   // both halves (the in-launch close alternates them, PART_HALF)
-            part[tb.nblk + 1 + blockIdx.x] = best;
+            part[blockIdx.x] = best;
             if (finish == 2) KTR(5);
         }
     }
@@ -1231,7 +1157,7 @@ __global__ __launch_bounds__(TPB) void k_delta_mt(DevState* st, uint32_t round, 
                                                   uint32_t* __restrict__ hitmask, uint32_t* __restrict__ tile_cnt,
                                                   uint32_t* __restrict__ grpsum, uint32_t eager_tiles, uint32_t ngroups,
                                                   uint32_t first_block = 0, ZdrView zv = ZdrView()) {
-    if (blockIdx.x < first_block) return;   // (GBPE_SPLIT_TAIL diagnostic launches: tiles and tail apart)
+    if (blockIdx.x < first_block) return;   // (split launches: tiles and tail apart)
     constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
     __shared__ LdsTab<LTAB_Z> lt;
     __shared__ uint32_t red[TPB / 64];
@@ -1379,7 +1305,7 @@ __global__ __launch_bounds__(CTPB) void k_compact(DevState* st, uint32_t round, 
                                                  const uint32_t* __restrict__ grpsum, Table tb,
                                                  const S* __restrict__ win = nullptr, const DevState* gst = nullptr,
                                                  uint32_t split = 0) {
-    // split (GBPE_SPLIT_TAIL diagnostic launches): 1 = tile blocks only, 2 = every block a window block
+    // split launches: 1 = tile blocks only, 2 = every block a window block
     // one LDS arena: the compaction stage of tile blocks or the delta table of tail blocks
     constexpr int STAGE = (TILE + 16) * sizeof(S);
     constexpr int ARENA = (sizeof(LdsTab<LTAB>) > STAGE ? sizeof(LdsTab<LTAB>) : STAGE) / 16;

@@ -68,12 +68,9 @@ struct gbpe_trainer {
     DevState* zst = nullptr;     // the zone's loop state
     DevState* h_zst = nullptr;   // pinned
     uint32_t* d_u32 = nullptr;   // small device scratch
-    uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection), two halves of nblk + 1
-    uint32_t* fbits = nullptr;   // in-launch close: flagged argmax blocks (bitmap, nblk bits)
-    CloseState* cls = nullptr;   // in-launch close: ticket + stats (sparse.h)
+    uint64_t* part = nullptr;    // k_refresh workgroup maxima (sparse selection)
     uint32_t grow_used_pct = 50;   // the table is rebuilt once its occupied slots (dead included) pass this %
     uint32_t grow_live_pct = 25;   // ... into the smallest 2^k slots its live pairs fill to at most this %
-    bool close_on = true;        // GBPE_DEBUG close=0: every sparse merge closes in k_refresh (A/B)
     uint2* zdr_out = nullptr;    // the multi-tile zone passes' delta dumps (ZdrView, train_dev.h)
     uint32_t* zdr_offs = nullptr;
     uint32_t* zdr_flag = nullptr;
@@ -83,7 +80,7 @@ struct gbpe_trainer {
     uint32_t zseg_mode = 1;      // 1 = zone segments for zones beyond zone_one (up to 1M), 0 = off
     uint32_t table_grows = 0;    // crowded-table rebuilds (same size or larger)
     uint64_t* wg_bytes = nullptr;   // bytes moved per k_body workgroup (each its own counter)
-    uint32_t delta_mt = 2048;       // dense k_delta: multi-tile workgroups from this many tiles (0 = never; GBPE_DELTA_MT)
+    uint32_t delta_mt = 2048;       // dense k_delta: multi-tile workgroups from this many tiles (0 = never; GBPE_DEBUG delta_mt)
     uint32_t delta_tpw = 8;         // ... of 8, 16 or 32 tiles
     uint64_t wg_cap = 0;
     double ms_sparse = 0, ms_dense = 0;   // GBPE_TRAIN_TIMING: merge passes (without selection / refresh) by mode
@@ -99,9 +96,9 @@ struct gbpe_trainer {
     uint32_t count_bytes_on = 1; // first count by the byte-pair histogram (0: hashed k_count_full)
     uint32_t lx_size_on = 1;     // word table sized from a sampled distinct count (0: from the word count)
     uint32_t lx_resize = 0;      // builds whose sampled table was too small (rerun at full size)
-    uint32_t lx_div = 16;        // with the lexicon: enter once next_mc * lx_div <= n, from the first step on (GBPE_LEXICON_DIV)
+    uint32_t lx_div = 16;        // with the lexicon: enter once next_mc * lx_div <= n, from the first step on (GBPE_DEBUG lxdiv)
     uint32_t sub_zone = 1u << 20;   // sparse steps run in sub-steps of sub_k merges while the zone exceeds this
-    uint32_t sub_k = 16;            // (the zone shrinks between them; GBPE_SUBSTEP_ZONE, GBPE_SUBSTEP)
+    uint32_t sub_k = 16;            // (the zone shrinks between them; GBPE_DEBUG subz, subk)
     bool zone16 = true;             // u16 zones of 8K-16K symbols: the 16-per-thread zone pass 
     uint32_t sp_zt = 5;          // zone target = sp_zt * last_mc + 64 (>= zone_f; GBPE_DEBUG zt; 4/5/6/7 measured
                                  // 0.895/0.893/0.918/0.918 s at 1 GiB with zone_f 3)
@@ -110,8 +107,8 @@ struct gbpe_trainer {
     uint32_t refresh_blocks = 0; // k_refresh grid (0 = 2 per CU)
     uint32_t refresh_late_z = 16384; // ... for zones of at most this many symbols
     uint32_t refresh_late = 64;  // k_refresh grid of late steps (0 = unchanged)
-    bool rehash_on = true;       // GBPE_REHASH: grow the table inside the sparse loop (0: exit, grow, recount)
-    uint32_t body_cap = 256;     // GBPE_BODY_WG: most k_body workgroups (default one per CU)
+    bool rehash_on = true;       // grow the table inside the sparse loop (GBPE_DEBUG rehash=0: exit, grow, recount)
+    uint32_t body_cap = 256;     // most k_body workgroups (one per CU)
     bool body_fit = true;        // the body's workgroups leave the zone's their CUs (GBPE_DEBUG bodyfit=0: off)
     uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
     uint32_t* h_clog = nullptr;
@@ -119,7 +116,7 @@ struct gbpe_trainer {
     // word-lexicon body (lexicon.h): the sectors hold one copy of every
     // distinct body word instead of the body itself
     bool lex = false;            // the current sparse entry uses it
-    bool lex_on = true;          // GBPE_LEXICON=0: never
+    bool lex_on = true;          // GBPE_DEBUG lexicon=0: never
     bool lex_only = false;       // built from shard lexicons (gbpe_trainer_create_from_lexicon): no dense stream,
                                  // the body's stream order lives on the ranks; never leaves the sparse loop
     void* lx_store = nullptr;    // distinct words, each followed by a 0 separator (S symbols)
@@ -161,24 +158,12 @@ uint32_t grid_blocks(const gbpe_ctx* ctx, uint32_t nblk, uint32_t per_cu) {
     return std::max<uint32_t>(grid_persistent(ctx, nblk, per_cu), (uint32_t)gbpe_div_up(nblk, 64));
 }
 
-// the partial maxima (both halves), the flagged-block bitmap and the close state,
-// sized for the table's blocks (sparse selection; after every table resize)
+// the partial maxima of the sparse selection (one per k_refresh workgroup), sized
+// for the table's blocks (sparse entry; after every table resize)
 int part_alloc(gbpe_trainer* t) {
-    hipStream_t s = t->ctx->stream;
     pool_free(t->ctx, t->part);
-    pool_free(t->ctx, t->fbits);
     t->part = nullptr;
-    t->fbits = nullptr;
-    const uint64_t nfw = std::max<uint64_t>(1, gbpe_div_up(t->tb.nblk, 32));
-    TR_HIP(t, pool_malloc(t->ctx, &t->part, 2ull * (t->tb.nblk + 1) * sizeof(uint64_t)));
-    TR_HIP(t, pool_malloc(t->ctx, &t->fbits, nfw * sizeof(uint32_t)));
-    TR_HIP(t, hipMemsetAsync(t->fbits, 0, nfw * sizeof(uint32_t), s));
-    if (!t->cls) {
-        TR_HIP(t, pool_malloc(t->ctx, &t->cls, sizeof(CloseState)));
-        TR_HIP(t, hipMemsetAsync(t->cls, 0, sizeof(CloseState), s));
-        TR_HIP(t, hipMemcpyAsync(&t->cls->clog, &t->d_clog, sizeof(uint32_t*), hipMemcpyHostToDevice, s));
-        TR_HIP(t, hipStreamSynchronize(s));   // (&t->d_clog is pageable host memory)
-    }
+    TR_HIP(t, pool_malloc(t->ctx, &t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
     return GBPE_OK;
 }
 
@@ -369,7 +354,7 @@ uint32_t zone_max(int bt) {
     return bt == 1023 ? 1024u * 16u : bt == 1024 ? ZoneDim<S, 1024>::ZMAX : ZoneDim<S, 256>::ZMAX;
 }
 // k_body grid: bitmap words per workgroup (>= the measured best 16 / 32 at C2 size),
-// at most `cap` workgroups (GBPE_BODY_WG; default 4 per CU)
+// at most `cap` workgroups (default: body_cap, one per CU)
 inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* wpg, uint32_t cap = 0) {
     const uint32_t W = (uint32_t)gbpe_div_up(t->nsec, 32);
     const uint32_t minw = bt == 1024 ? 32u : 16u;
@@ -399,33 +384,11 @@ void launch_body(int bt, uint32_t grid, hipStream_t s, A... args) {
         hipLaunchKernelGGL((k_body<S, EXACT, 256>), dim3(grid), dim3(256), 0, s, args...);
 }
 
-// the in-launch close (sparse.h merge_close) for a step of this grid: the zone in
-// one workgroup (no zone segments, no multi-tile zone kernels after k_body), at
-// most CL_PMAX partial maxima and a bitmap the close's threads cover
-inline bool close_fits(const gbpe_trainer* t, const SpGrid& g) {
-    const uint32_t nthr = g.bt >= 1023 ? 1024u : 256u;
-    return t->close_on && t->cls && g.zone1 == 1 && g.refresh <= CL_PMAX &&
-           gbpe_div_up(t->tb.nblk, 32) <= (uint64_t)CL_KW * nthr;
-}
-
 template <typename S>
 int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const SpGrid& g, bool timing, hipEvent_t* ev) {
     S* zc = (S*)t->zbuf[t->zcur ^ (round & 1)];
     S* zo = (S*)t->zbuf[t->zcur ^ (round & 1) ^ 1];
     const bool exact = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) != 0;
-    // partial maxima by merge parity: this launch selects from one half, its
-    // increments raise the other (k_refresh writes both)
-    const uint64_t half = (uint64_t)t->tb.nblk + 1;
-    const uint32_t par = (uint32_t)((t->done + round) & 1u);
-    const uint64_t* pread = t->part + par * half;
-    const bool inl = close_fits(t, g);
-    Table tbc = t->tb;
-    if (inl) {
-        tbc.fbits = t->fbits;
-        tbc.pinc = t->part + (par ^ 1u) * half;
-        tbc.per = (uint32_t)gbpe_div_up(t->tb.nblk, g.refresh);   // k_refresh's blocks per workgroup
-    }
-    CloseState* cls = inl ? t->cls : nullptr;
     if (timing) TR_HIP(t, hipEventRecord(ev[0], s));
     if (timing) TR_HIP(t, hipEventRecord(ev[1], s));   // selection runs inside k_body (sel_inline)
     // zone segments run inside k_body (its ZSEG form)
@@ -435,15 +398,15 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const int bt = inbody ? 2048 : g.bt;
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
-        launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, tbc,
+        launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
-                             pread, g.refresh, t->d_log, t->grpsum, t->wg_bytes, tbc, sel_single(t),
-                             sp_mul(t), (ZSegState*)t->zseg, cls);
+                             (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
+                             sp_mul(t), (ZSegState*)t->zseg);
     else
-        launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, tbc,
+        launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                               g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
-                              pread, g.refresh, t->d_log, t->grpsum, t->wg_bytes, tbc, sel_single(t),
-                              sp_mul(t), (ZSegState*)t->zseg, cls);
+                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
+                              sp_mul(t), (ZSegState*)t->zseg);
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
     if (!g.zone1 && !exact && t->zdr_on && t->zdr_out) {
         // a zone of many tiles, reference compaction: tiles dump their deltas, k_churn
@@ -500,9 +463,8 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
                                t->tb, (const S*)t->wtmp, (const DevState*)t->st);
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
-    if (!inl)
-        hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,
-                           (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part, t->zseg);
+    hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,
+                       (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part, t->zseg);
     if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
@@ -949,7 +911,7 @@ int lx_expand(gbpe_trainer* t, S* dst, uint64_t dst_cap, uint64_t* tot, const ui
     return GBPE_OK;
 }
 
-// diagnostic (GBPE_LEX_CHECK=1): the lexicon right after a build expands back to the body
+// diagnostic (GBPE_DEBUG lex_check=1): the lexicon right after a build expands back to the body
 template <typename S>
 int lx_check(gbpe_trainer* t, const S* cur, uint32_t Zs, const LxPlan& lp) {
     hipStream_t s = t->ctx->stream;
@@ -1341,7 +1303,6 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->rehash_on = gbpe_debug_knob("rehash", 1) != 0;
     t->delta_mt = (uint32_t)gbpe_debug_knob("delta_mt", t->delta_mt);
     t->sp_zt = (uint32_t)gbpe_debug_knob("zt", t->sp_zt);
-    t->close_on = gbpe_debug_knob("close", 1) != 0;
     t->grow_used_pct = (uint32_t)std::min<long>(90, std::max<long>(10, gbpe_debug_knob("gused", t->grow_used_pct)));
     t->grow_live_pct = (uint32_t)std::min<long>(t->grow_used_pct, std::max<long>(5, gbpe_debug_knob("glive", t->grow_live_pct)));
     t->refresh_blocks = (uint32_t)gbpe_debug_knob("rfb", t->refresh_blocks);   // k_refresh grid sweeps

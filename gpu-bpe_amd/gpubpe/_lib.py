@@ -56,7 +56,6 @@ class TrainerStats(C.Structure):
                 ("ms_sparse", C.c_double), ("ms_body", C.c_double),
                 ("lexicon_builds", C.c_uint32), ("lexicon_fallbacks", C.c_uint32), ("lexicon_words", C.c_uint64),
                 ("lexicon_entries", C.c_uint64), ("lexicon_symbols", C.c_uint64),
-                ("close_inlaunch", C.c_uint64), ("close_remax_blocks", C.c_uint64), ("close_refreshes", C.c_uint64),
                 ("ms_create", C.c_double)]
 
 

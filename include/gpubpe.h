@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GBPE_ABI_VERSION 4   /* 4: in-launch merge close stats and creation time replace the late-loop stats (round 5) */
+#define GBPE_ABI_VERSION 4   /* 4: the late-loop stats removed, trainer creation time added (round 5) */
 
 /* status codes */
 #define GBPE_OK            0
@@ -179,10 +179,6 @@ typedef struct gbpe_trainer_stats {
     uint64_t lexicon_words;       /* body word occurrences the lexicon represents (all builds and shrinks) */
     uint64_t lexicon_entries;     /* distinct-word entries of the current lexicon */
     uint64_t lexicon_symbols;     /* symbols of the current lexicon store (separators included) */
-    uint64_t close_inlaunch;      /* sparse merges closed inside k_body by its last-arriving workgroup (block
-                                     maxima kept exact in the launch: no k_refresh launch) */
-    uint64_t close_remax_blocks;  /* argmax blocks those closes re-maxed (a decrement reached a block's maximum) */
-    uint64_t close_refreshes;     /* closes with more flagged blocks than one workgroup re-maxes (a k_refresh follows) */
     double   ms_create;           /* host wall ms of trainer creation (symbols, word starts, first count):
                                      the part of a run the reference's t_loop excludes (trainer.js:230) */
 } gbpe_trainer_stats;

@@ -77,7 +77,6 @@ for name in sys.argv[4:]:
         if rep:
             print(json.dumps({"name": name, "s": round(t1 - t0, 4), "s_first4k": round((t4k or t1) - t0, 4),
                               "merges": int(m.shape[0]), "equal": eq,
-                              "close": [int(st.close_inlaunch), int(st.close_remax_blocks)],
                               "sparse_exits": int(st.sparse_exits),
                               "table_slots": int(st.table_slots), "max_live_pairs": int(st.max_live_pairs)}), flush=True)
         if not eq:

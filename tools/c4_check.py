@@ -43,27 +43,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def recount(fin_host: np.ndarray):
-    """Live pair counts of a u32 reference-layout stream, on the device (torch)."""
-    import torch
-    n = fin_host.shape[0]
-    step = 1 << 28
-    keys, cnts = [], []
-    for s0 in range(0, max(1, n - 1), step):
-        s1 = min(n, s0 + step + 1)
-        x = torch.from_numpy(fin_host[s0:s1].view(np.int32)).cuda().to(torch.int64) & 0xFFFFFFFF
-        prev, cur = x[:-1], x[1:]
-        ok = ((cur & WS) == 0) & ((prev & 0xFFFF) != 0) & ((cur & 0xFFFF) != 0)
-        pid = ((prev & 0xFFFF) << 16) | (cur & 0xFFFF)
-        u, c = torch.unique(pid[ok], return_counts=True)
-        keys.append(u)
-        cnts.append(c)
-        del x, prev, cur, ok, pid
-    k = torch.cat(keys)
-    c = torch.cat(cnts)
-    u, inv = torch.unique(k, return_inverse=True)
-    tot = torch.zeros(u.shape[0], dtype=torch.int64, device=u.device).index_add_(0, inv, c)
-    return u.cpu().numpy().astype(np.uint32), tot.cpu().numpy()
+recount = B.recount_pairs   # (bench.py: the C4 leg runs the same check)
 
 
 def heartbeat(rank):
