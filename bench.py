@@ -64,12 +64,12 @@ HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip ta
 # boundary on one stream (price list row "boundary")
 HOP_US = 0.227
 BOUNDARY_US = 1.45
-# the dependent global hops of one late sector-sparse merge (one k_body launch with
-# its in-launch close, DESIGN §2b "latency floor"): each waits for the one before
-LATE_MERGE_HOPS = ("state + partial maxima (selection)", "bitmap rows of a and b", "candidate extents + signatures",
-                   "candidate sector symbols + multiplicities", "pair-table probe (flush)", "returning count add",
-                   "block-maximum atomics drained", "arrival ticket", "flagged-block bitmap + state counters",
-                   "flagged blocks' slots (re-max)", "flagged groups' block maxima")
+# the dependent global hops of one late sector-sparse merge (DESIGN §8 "latency
+# floor"): k_body, then k_refresh, each waits for the one before, and each launch
+# waits for the previous one (two kernel boundaries per merge)
+KBODY_HOPS = ("state + partial maxima (selection)", "bitmap rows of a and b", "candidate extents + signatures",
+              "candidate sector symbols + multiplicities", "pair-table probe (flush)", "count adds landed")
+KREFRESH_HOPS = ("dirty flags + state snapshot", "dirty blocks' slots (re-max)", "partial maxima stored")
 TILE_SYMS = 8192
 METRIC = "BPE merges/sec + tokenize GB/s, 1 GiB UTF-8 @ 32K vocab, 1/2/4/8 MI355X"
 HEADLINE = {"gen": "english", "n": 1 << 30, "seed": 2, "fancy_punct": 0.005}
@@ -326,19 +326,20 @@ def train_roofline(det, wall_per_run):
         roof["other_kernel"] = other[0]
     # latency floor: a late merge is a chain of dependent round
     # trips, not bytes; the floor counts them at the guide's idle-chip latencies
-    floor_kernel = len(LATE_MERGE_HOPS) * HOP_US
-    lf = {"hops": list(LATE_MERGE_HOPS), "hop_us": HOP_US, "boundary_us": BOUNDARY_US,
-          "us_per_launch": round(floor_kernel, 3), "us_per_merge": round(floor_kernel + BOUNDARY_US, 3),
-          "meaning": "dependent Infinity-Cache round trips of one late merge (one k_body launch with its in-launch "
-                     "close) x ~545 cycles, plus one kernel boundary per merge; achieved / floor says how far the "
-                     "chain is from its own bound, as frac does for bytes"}
+    floor_kernel = len(KBODY_HOPS) * HOP_US
+    floor_merge = (len(KBODY_HOPS) + len(KREFRESH_HOPS)) * HOP_US + 2 * BOUNDARY_US
+    lf = {"k_body_hops": list(KBODY_HOPS), "k_refresh_hops": list(KREFRESH_HOPS), "hop_us": HOP_US,
+          "boundary_us": BOUNDARY_US, "k_body_us": round(floor_kernel, 3), "us_per_merge": round(floor_merge, 3),
+          "meaning": "dependent Infinity-Cache round trips (~545 cycles each) of one late merge — k_body's and "
+                     "k_refresh's — plus two kernel boundaries; achieved / floor says how far the chain is from its "
+                     "own bound, as frac does for bytes"}
     if roof.get("us_per_launch"):
-        lf["achieved_us_per_launch"] = roof["us_per_launch"]
-        lf["achieved_over_floor"] = round(roof["us_per_launch"] / floor_kernel, 2)
+        lf["k_body_achieved_us"] = roof["us_per_launch"]
+        lf["k_body_achieved_over_floor"] = round(roof["us_per_launch"] / floor_kernel, 2)
     if det.get("late_window"):
         w = det["late_window"]
         lf["late_window"] = w
-        lf["late_achieved_over_floor"] = round(w["us_per_merge"] / (floor_kernel + BOUNDARY_US), 2)
+        lf["late_achieved_over_floor"] = round(w["us_per_merge"] / floor_merge, 2)
     roof["latency_floor"] = lf
     roof["dense_stream"] = dense
     roof["dense_equivalent"] = {"gbps": round(equiv, 1), "frac": round(equiv / HBM_PEAK_GBPS, 4),
