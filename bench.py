@@ -74,8 +74,8 @@ TILE_SYMS = 8192
 METRIC = "BPE merges/sec + tokenize GB/s, 1 GiB UTF-8 @ 32K vocab, 1/2/4/8 MI355X"
 HEADLINE = {"gen": "english", "n": 1 << 30, "seed": 2, "fancy_punct": 0.005}
 C2 = {"gen": "english", "n": 104_857_600, "seed": 2, "fancy_punct": 0.005}
-PMC_FILE = os.path.join(ROOT, "profiles", "r4", "close", "pmc_kbody.json")
-ROCPROF_EN1G = os.path.join(ROOT, "profiles", "r4", "close", "en1g_kernel_stats.csv")
+PMC_FILE = os.path.join(ROOT, "profiles", "r5", "s2", "pmc_kbody.json")
+ROCPROF_EN1G = os.path.join(ROOT, "profiles", "r5", "s2", "en1g_kernel_stats.csv")
 CAL_NOTE = ("FETCH_SIZE x2: tools/micro/fetch_cal.hip measured 64 counter bytes per distinct 128-B line for "
             "16-B streaming reads and 4-, 8- and 16-B one-per-line gathers alike (profiles/r3_fetch_calibration.json), "
             "so every read line moves 128 B; WRITE_SIZE counts 32-B granules (4-B scattered stores and atomics: 32 B "
