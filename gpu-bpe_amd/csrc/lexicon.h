@@ -17,8 +17,8 @@
 constexpr uint32_t LX_LIT = 0x80000000u;   // occurrence of a token-0 symbol: the symbol itself (low bits)
 constexpr uint32_t LX_LONG = 0x40000000u;  // build only: a word longer than LX_LMAX (index into the long list)
 constexpr uint32_t LX_LMAX = 64;           // words up to this many symbols are deduplicated
-constexpr int LX_WPT = 16;                 // words per thread in k_lx_hash
-constexpr int LX_LT = 2048;                // LDS word-table slots per workgroup
+constexpr int LX_WPT = 16;                 // words per thread in k_lx_hash (at least; trainer lx_wg)
+constexpr int LX_LT = 2048;                // LDS word-table slots per workgroup (a multiple of TPB)
 constexpr uint32_t LX_PROBES = 4096;       // global word-table probes before the build gives up
 
 // a body word starts at i iff no counted pair can ever span (i-1, i)
@@ -83,13 +83,21 @@ __global__ __launch_bounds__(TPB) void k_lx_wpos(const S* __restrict__ x, uint32
 }
 
 // 64-bit content hash of a word (its symbols with their word-start bits, and its length)
+// (8 symbols' loads issued together: one round trip per 8 symbols, not per symbol)
 template <typename S>
 __device__ __forceinline__ unsigned long long lx_hash(const S* __restrict__ x, uint32_t s, uint32_t L) {
     unsigned long long h = 0x9E3779B97F4A7C15ull ^ (unsigned long long)L;
-    for (uint32_t i = 0; i < L; ++i) {
-        h ^= (unsigned long long)x[s + i];
-        h *= 0x100000001B3ull;
-        h ^= h >> 29;
+    for (uint32_t i0 = 0; i0 < L; i0 += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = i0 + k < L ? (uint32_t)x[s + i0 + k] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (i0 + k >= L) break;
+            h ^= (unsigned long long)v[k];
+            h *= 0x100000001B3ull;
+            h ^= h >> 29;
+        }
     }
     h ^= h >> 33;
     h *= 0xff51afd7ed558ccdull;
@@ -110,12 +118,15 @@ struct alignas(16) LxSlot {
     uint32_t cnt;             // occurrences; the uid once k_lx_tabuid ran
 };
 
-// global word table (linear probing on 64-bit keys): insert-or-add `c` occurrences
+// global word table (linear probing on 64-bit keys): insert-or-add `c` occurrences.
+// A key never changes once set (0 -> h), so the probes are plain loads that may
+// hit a stale copy in this XCD's L2: a stale 0 only sends the probe to the CAS,
+// which returns the key actually there (agent-scope probe loads go to memory).
 __device__ bool lx_insert(LxSlot* __restrict__ wt, uint32_t P, unsigned long long h, uint32_t rep, uint32_t c,
                           uint32_t maxp = LX_PROBES) {
     uint32_t slot = lx_home(h, P - 1);
     for (uint32_t p = 0; p < maxp; ++p, slot = (slot + 1) & (P - 1)) {
-        unsigned long long k = __hip_atomic_load(&wt[slot].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long k = wt[slot].key;
         if (k == 0ull) {
             k = atomicCAS(&wt[slot].key, 0ull, h);
             if (k == 0ull) {
@@ -144,9 +155,13 @@ __device__ uint4 lx_find(const LxSlot* __restrict__ wt, uint32_t P, unsigned lon
     return make_uint4(0u, 0u, SP_INV, SP_INV);
 }
 
-// Word multiplicities: every workgroup aggregates 4096 words in an LDS table
+// Word multiplicities: every workgroup aggregates TPB x wpt words in an LDS table
 // (hot words cost one global add per workgroup, not one per occurrence), then
-// adds them into the global table.  Token-0 words become literals, long words
+// adds them into the global table (the host sizes wpt for ~lx_wg workgroups).
+// Those global adds are most of the kernel (1 GiB: 9.3 ms, 3.2 without them), and
+// their number barely moves with the workgroup size: 62K workgroups of 4096
+// words or 1024 of 247K words (whose LDS tables overflow into direct inserts)
+// measured 9.4 vs 10.1 ms (profiles/r5/s9).  Token-0 words become literals, long words
 // entries of their own.  ctr[0] = long words, ctr[1] = failure flag.
 // wmul (weighted analysis, the lexicon hand-over of DESIGN §5): a word counts
 // wmul[its first position] occurrences instead of one — the segment is then a
@@ -155,8 +170,8 @@ template <typename S>
 __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32_t len, const uint32_t* __restrict__ wpos,
                                                  uint32_t nw, LxSlot* __restrict__ wtab,
                                                  uint32_t P, uint32_t* __restrict__ otmp, uint32_t* __restrict__ longs,
-                                                 uint32_t* __restrict__ ctr, const uint32_t* __restrict__ wmul = nullptr,
-                                                 uint32_t maxp = LX_PROBES) {
+                                                 uint32_t* __restrict__ ctr, const uint32_t* __restrict__ wmul,
+                                                 uint32_t maxp, uint32_t wpt) {
     __shared__ unsigned long long lk[LX_LT];
     __shared__ uint32_t lc[LX_LT], lr[LX_LT];
     for (int i = threadIdx.x; i < LX_LT; i += TPB) {
@@ -164,8 +179,8 @@ __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32
         lc[i] = 0u;
     }
     __syncthreads();
-    const uint64_t j0 = (uint64_t)blockIdx.x * (TPB * LX_WPT);
-    for (int q = 0; q < LX_WPT; ++q) {
+    const uint64_t j0 = (uint64_t)blockIdx.x * TPB * wpt;
+    for (uint32_t q = 0; q < wpt; ++q) {
         const uint64_t j = j0 + (uint64_t)q * TPB + threadIdx.x;
         if (j >= nw) break;
         const uint32_t s = wpos[j], e = j + 1 < nw ? wpos[j + 1] : len, L = e - s;
@@ -201,8 +216,27 @@ __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32
     __syncthreads();
     // a table already known to be too small (the build is redone or abandoned): no probing
     if (__hip_atomic_load(&ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    for (int i = threadIdx.x; i < LX_LT; i += TPB)
-        if (lk[i] && !lx_insert(wtab, P, lk[i], lr[i], lc[i], maxp)) ctr[1] = 1u;
+    // the thread's LX_LT / TPB entries: every home-slot probe issued together, the
+    // adds of the words found there last (no later load waits behind them)
+    constexpr int FL = LX_LT / TPB;
+    unsigned long long fk[FL], hk[FL];
+    uint32_t fs[FL];
+#pragma unroll
+    for (int q = 0; q < FL; ++q) {
+        fk[q] = lk[threadIdx.x + q * TPB];
+        fs[q] = lx_home(fk[q], P - 1);
+        hk[q] = fk[q] ? wtab[fs[q]].key : 0ull;
+    }
+    bool home[FL];
+#pragma unroll
+    for (int q = 0; q < FL; ++q) {
+        const int i = threadIdx.x + q * TPB;
+        home[q] = fk[q] && hk[q] == fk[q];
+        if (fk[q] && !home[q] && !lx_insert(wtab, P, fk[q], lr[i], lc[i], maxp)) ctr[1] = 1u;
+    }
+#pragma unroll
+    for (int q = 0; q < FL; ++q)
+        if (home[q]) atomicAdd(&wtab[fs[q]].cnt, lc[threadIdx.x + q * TPB]);
 }
 
 constexpr uint32_t LX_TB = TPB * 16;   // word-table slots per uid-assignment block
@@ -283,7 +317,7 @@ __global__ void k_lx_longs(const uint32_t* __restrict__ longs, const uint32_t* _
 }
 
 // store layout: word u at off(u) (scanned sizes), its separator after it; the
-// multiplicity of every symbol (0 for separators)
+// multiplicity of every symbol (0 for separators; mul null: symbols only)
 template <typename S>
 __global__ void k_lx_fill(const S* __restrict__ x, const uint32_t* __restrict__ urep, const uint32_t* __restrict__ usz,
                           const uint32_t* __restrict__ umul, const uint32_t* __restrict__ upre,
@@ -293,10 +327,10 @@ __global__ void k_lx_fill(const S* __restrict__ x, const uint32_t* __restrict__ 
     const uint32_t off = upre[u] + (uint32_t)ublk[u / SCAN_BLK], L = usz[u] - 1u, r = urep[u], m = umul[u];
     for (uint32_t i = 0; i < L; ++i) {
         store[off + i] = x[r + i];
-        mul[off + i] = m;
+        if (mul) mul[off + i] = m;
     }
     store[off + L] = (S)0;
-    mul[off + L] = 0u;
+    if (mul) mul[off + L] = 0u;
 }
 
 // sector windows over the new store region [sbase, sbase + T): window k's
@@ -317,10 +351,15 @@ __global__ void k_lx_secstart(const uint32_t* __restrict__ upre, const uint64_t*
 // occurrence list of the segment's words (stream order): the uid of each word,
 // after checking its symbols against the representative's (a hash collision
 // fails the build instead of merging two different words)
+// The symbols are checked against the entries' compact copy (rstore, laid out as
+// the store: entry u at upre[u] + ublk[u / SCAN_BLK]), which stays in the caches;
+// a representative's occurrence in the segment is a random HBM line per word
+// (3.7 of the 1 GiB build's 7.7 ms).
 template <typename S>
 __global__ void k_lx_occ(const S* __restrict__ x, const uint32_t* __restrict__ wpos, uint32_t nw, uint32_t len,
                          const uint32_t* __restrict__ otmp, const LxSlot* __restrict__ wt,
-                         uint32_t P, const uint32_t* __restrict__ urep,
+                         uint32_t P, const S* __restrict__ rstore, const uint32_t* __restrict__ upre,
+                         const uint64_t* __restrict__ ublk,
                          const uint32_t* __restrict__ usz, uint32_t nshort, uint32_t uid_base, uint32_t* __restrict__ occ,
                          uint32_t* __restrict__ ctr) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -340,9 +379,18 @@ __global__ void k_lx_occ(const S* __restrict__ x, const uint32_t* __restrict__ w
     uint32_t u = 0;
     if (ok) {
         u = e.w;
-        const uint32_t r = urep[u];
         ok = usz[u] == L + 1u;
-        for (uint32_t i = 0; ok && i < L; ++i) ok = x[r + i] == x[s + i];
+        const S* r = rstore + upre[u] + ublk[u / SCAN_BLK];
+        for (uint32_t i0 = 0; ok && i0 < L; i0 += 8) {
+            uint32_t va[8], vb[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                va[k] = i0 + k < L ? (uint32_t)r[i0 + k] : 0u;
+                vb[k] = i0 + k < L ? (uint32_t)x[s + i0 + k] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) ok = ok && va[k] == vb[k];
+        }
     }
     if (!ok) ctr[1] = 1u;
     occ[j] = uid_base + u;

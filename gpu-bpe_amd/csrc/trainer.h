@@ -95,6 +95,7 @@ struct gbpe_trainer {
     uint32_t* d_bhist = nullptr; // byte-pair histogram of the first count (65,536 u32)
     uint32_t count_bytes_on = 1; // first count by the byte-pair histogram (0: hashed k_count_full)
     uint32_t lx_size_on = 1;     // word table sized from a sampled distinct count (0: from the word count)
+    uint32_t lx_wg = 16384;      // k_lx_hash workgroups (at least LX_WPT words per thread; GBPE_DEBUG lxwg)
     uint32_t lx_resize = 0;      // builds whose sampled table was too small (rerun at full size)
     uint32_t lx_div = 16;        // with the lexicon: enter once next_mc * lx_div <= n, from the first step on (GBPE_DEBUG lxdiv)
     uint32_t sub_zone = 1u << 20;   // sparse steps run in sub-steps of sub_k merges while the zone exceeds this
@@ -699,16 +700,20 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
     lp = LxPlan();
     if (len == 0) return GBPE_OK;
     const uint64_t ntiles = gbpe_div_up(len, TILE);
-    // word count first (sizes the rest of the scratch)
-    int rc = lx_scratch(t, (ntiles + 64) * 4 + (ntiles / SCAN_BLK + 4) * 8 + 1024);
-    if (rc != GBPE_OK) return rc;
+    // word count first (sizes the scratch); the tile counts live outside the
+    // scratch, which may move, so k_lx_wpos uses them as they are
+    uint32_t* tc = nullptr;
+    uint64_t* tb = nullptr;
+    auto tc_free = gbpe_scope_exit([&] {
+        pool_free(t->ctx, tc);
+        pool_free(t->ctx, tb);
+    });
+    TR_HIP(t, pool_malloc(t->ctx, &tc, (ntiles + 64) * 4));
+    TR_HIP(t, pool_malloc(t->ctx, &tb, (ntiles / SCAN_BLK + 4) * 8));
+    hipLaunchKernelGGL(k_lx_count<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, tc);
+    lx_scan(s, tc, ntiles, tb);
+    GBPE_LAUNCH_CHECK(t->ctx);
     {
-        LxCarve c{(char*)t->lx_tmp};
-        uint32_t* tc = c.take<uint32_t>(ntiles);
-        uint64_t* tb = c.take<uint64_t>(ntiles / SCAN_BLK + 4);
-        hipLaunchKernelGGL(k_lx_count<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, tc);
-        lx_scan(s, tc, ntiles, tb);
-        GBPE_LAUNCH_CHECK(t->ctx);
         uint64_t nw64 = 0;
         TR_HIP(t, hipMemcpyAsync(&nw64, tb + gbpe_div_up(ntiles, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
         TR_HIP(t, hipStreamSynchronize(s));
@@ -721,13 +726,11 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
     uint64_t Pfull = 4096;
     while (Pfull < 2ull * nw && Pfull < (1ull << 27)) Pfull <<= 1;
     const uint64_t nbbf = gbpe_div_up(Pfull, LX_TB);
-    const uint64_t need = (ntiles + 64) * 4 + (ntiles / SCAN_BLK + 4) * 8 + 9ull * (nw + 64) * 4 + Pfull * 16 +
-                          (nbbf + 64) * 4 + 2 * (nbbf / SCAN_BLK + (uint64_t)nw / SCAN_BLK + 8) * 8 + 32 * 256;
-    rc = lx_scratch(t, need);
+    const uint64_t need = 9ull * (nw + 64) * 4 + Pfull * 16 + (nbbf + 64) * 4 +
+                          2 * (nbbf / SCAN_BLK + (uint64_t)nw / SCAN_BLK + 8) * 8 + 32 * 256;
+    int rc = lx_scratch(t, need);
     if (rc != GBPE_OK) return rc;
     LxCarve c{(char*)t->lx_tmp};
-    uint32_t* tc = c.take<uint32_t>(ntiles);
-    uint64_t* tb = c.take<uint64_t>(ntiles / SCAN_BLK + 4);
     lp.wpos = c.take<uint32_t>(nw + 1);
     uint32_t* otmp = c.take<uint32_t>(nw + 1);
     uint32_t* longs = c.take<uint32_t>(nw + 1);
@@ -740,9 +743,6 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
     uint64_t* bb = c.take<uint64_t>(nbbf / SCAN_BLK + 4);
     lp.ublk = c.take<uint64_t>((uint64_t)nw / SCAN_BLK + 4);
     uint32_t* ctr = c.take<uint32_t>(8);
-    // (the tile counts are recomputed: the scratch may have moved)
-    hipLaunchKernelGGL(k_lx_count<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, tc);
-    lx_scan(s, tc, ntiles, tb);
     hipLaunchKernelGGL(k_lx_wpos<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, (const uint32_t*)tc,
                        (const uint64_t*)tb, lp.wpos);
     uint32_t h[4] = {0, 0, 0, 0};
@@ -752,10 +752,12 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
         const uint64_t nbb = gbpe_div_up(P, LX_TB);
         TR_HIP(t, hipMemsetAsync(wtab, 0, P * sizeof(LxSlot), s));
         TR_HIP(t, hipMemsetAsync(ctr, 0, 32, s));
-        if (nh)
-            hipLaunchKernelGGL(k_lx_hash<S>, dim3((uint32_t)gbpe_div_up(nh, TPB * LX_WPT)), dim3(TPB), 0, s, seg, len,
+        if (nh) {
+            const uint32_t wpt = (uint32_t)std::max<uint64_t>(LX_WPT, gbpe_div_up(nh, (uint64_t)TPB * t->lx_wg));
+            hipLaunchKernelGGL(k_lx_hash<S>, dim3((uint32_t)gbpe_div_up(nh, (uint64_t)TPB * wpt)), dim3(TPB), 0, s, seg, len,
                                (const uint32_t*)lp.wpos, nh, wtab, (uint32_t)P, otmp, longs, ctr, wmul,
-                               P < Pfull ? 256u : LX_PROBES);   // an estimated table gives up early when short
+                               P < Pfull ? 256u : LX_PROBES, wpt);   // an estimated table gives up early when short
+        }
         hipLaunchKernelGGL(k_lx_tabcount, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const LxSlot*)wtab, (uint32_t)P, bc);
         lx_scan(s, bc, nbb, bb);
         GBPE_LAUNCH_CHECK(t->ctx);
@@ -795,23 +797,35 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
         hipLaunchKernelGGL(k_lx_longs, dim3((uint32_t)gbpe_div_up(lp.nlong, 256)), dim3(256), 0, s, (const uint32_t*)longs,
                            (const uint32_t*)ctr, lp.nshort, (const uint32_t*)lp.wpos, nw, len, lp.usz, lp.umul, lp.urep,
                            wmul);
-    if (nw)
-        hipLaunchKernelGGL(k_lx_occ<S>, dim3((uint32_t)gbpe_div_up(nw, 256)), dim3(256), 0, s, seg, (const uint32_t*)lp.wpos, nw,
-                           len, (const uint32_t*)otmp, (const LxSlot*)wtab, (uint32_t)P,
-                           (const uint32_t*)lp.urep, (const uint32_t*)lp.usz, lp.nshort, t->lx_nuid, lp.occ, ctr);
-    // store offsets: exclusive scan of the entry sizes, in otmp (k_lx_occ, queued
-    // before on the same stream, has consumed it)
-    uint32_t* upre = otmp;
+    // store offsets: exclusive scan of the entry sizes, in `longs` (k_lx_longs,
+    // queued before on the same stream, has consumed it)
+    uint32_t* upre = longs;
     TR_HIP(t, hipMemcpyAsync(upre, lp.usz, (uint64_t)lp.nu * 4, hipMemcpyDeviceToDevice, s));
     lx_scan(s, upre, lp.nu, lp.ublk);
     GBPE_LAUNCH_CHECK(t->ctx);
     uint64_t T = 0;
     TR_HIP(t, hipMemcpyAsync(&T, lp.ublk + gbpe_div_up(lp.nu ? lp.nu : 1, SCAN_BLK), 8, hipMemcpyDeviceToHost, s));
-    TR_HIP(t, hipMemcpyAsync(h, ctr, 8, hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipStreamSynchronize(s));
-    if (h[1]) return GBPE_OK;   // a hash collision (or a word missing from the table)
-    lp.T = (uint32_t)T;
     if (fresh && T * 2 > len) return GBPE_OK;   // not worth it: the store would be more than half the body
+    if (nw) {
+        // the entries' compact copy (the store's layout) for the occurrence check
+        S* rstore = nullptr;
+        auto rs_free = gbpe_scope_exit([&] { pool_free(t->ctx, rstore); });
+        TR_HIP(t, pool_malloc(t->ctx, &rstore, (T + 1) * sizeof(S)));
+        if (lp.nu)
+            hipLaunchKernelGGL(k_lx_fill<S>, dim3((uint32_t)gbpe_div_up(lp.nu, 256)), dim3(256), 0, s, seg,
+                               (const uint32_t*)lp.urep, (const uint32_t*)lp.usz, (const uint32_t*)lp.umul,
+                               (const uint32_t*)upre, (const uint64_t*)lp.ublk, lp.nu, rstore, (uint32_t*)nullptr);
+        hipLaunchKernelGGL(k_lx_occ<S>, dim3((uint32_t)gbpe_div_up(nw, 256)), dim3(256), 0, s, seg, (const uint32_t*)lp.wpos, nw,
+                           len, (const uint32_t*)otmp, (const LxSlot*)wtab, (uint32_t)P, (const S*)rstore,
+                           (const uint32_t*)upre, (const uint64_t*)lp.ublk, (const uint32_t*)lp.usz, lp.nshort,
+                           t->lx_nuid, lp.occ, ctr);
+        GBPE_LAUNCH_CHECK(t->ctx);
+        TR_HIP(t, hipMemcpyAsync(h, ctr, 8, hipMemcpyDeviceToHost, s));
+        TR_HIP(t, hipStreamSynchronize(s));
+        if (h[1]) return GBPE_OK;   // a hash collision (or a word missing from the table)
+    }
+    lp.T = (uint32_t)T;
     lp.upre = upre;
     lp.ok = true;
     return GBPE_OK;
@@ -1309,6 +1323,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->refresh_late = (uint32_t)gbpe_debug_knob("rfl", t->refresh_late);
     t->refresh_late_z = (uint32_t)gbpe_debug_knob("rflz", t->refresh_late_z);
     t->lx_div = (uint32_t)std::max<long>(1, gbpe_debug_knob("lxdiv", t->lx_div));   // lexicon entry / sub-step sweeps
+    t->lx_wg = (uint32_t)std::max<long>(1, gbpe_debug_knob("lxwg", t->lx_wg));
     t->sub_k = (uint32_t)std::max<long>(1, gbpe_debug_knob("subk", t->sub_k));
     t->sub_zone = (uint32_t)std::max<long>(1, gbpe_debug_knob("subz", t->sub_zone));
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
