@@ -297,6 +297,7 @@ struct ZoneLds {
     uint4 xv[ZoneDim<S, BT>::ZMAX * sizeof(S) / 16];   // the zone (symbol i = ((S*)xv)[i])
     S wb[ZoneDim<S, BT>::ZWIN];
     uint32_t wsum[BT / 64], wtail[BT / 64];
+    uint32_t tf;   // zone_one: the first thread outside the unmoved prefix
     S trash[64];   // the zone pass's unconditional stores of dropped symbols
 };
 
@@ -325,8 +326,8 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
     const uint32_t i0 = (uint32_t)t * ZPT;
     S* xs = reinterpret_cast<S*>(L.xv);
     uint32_t x[ZPT];
+    uint4 v[V];
     {
-        uint4 v[V];
         const uint4* src = reinterpret_cast<const uint4*>(zc + i0);   // zone buffers hold >= 2 tiles
 #pragma unroll
         for (int k = 0; k < V; ++k) v[k] = src[k];
@@ -340,6 +341,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
         const uint64_t src0 = win_src0(gs, mc);
         for (uint32_t u = t; u < mc; u += BT) L.wb[u] = zo[src0 + u];
     }
+    if (t == 0) L.tf = BT;
     if (!zout) lds_clear(lt);
     __syncthreads();
     if (t == 0) KT(2);
@@ -387,6 +389,15 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
         }
     }
     if (t == 0) KT(3);
+    // The unmoved prefix: the threads before the first one holding a site, an
+    // A-side or position lim - 1 keep every symbol at its own position, so they
+    // store their loaded vectors straight to the other buffer (aligned) and skip
+    // the LDS assembly below — late in training most merges have no site in the
+    // zone at all, and the assembly is most of the zone pass's instructions.
+    {
+        const unsigned long long sm = __ballot((hitm | rwm) != 0u || i0 + ZPT >= lim);
+        if (sm && lane == 0) atomicMin(&L.tf, (uint32_t)(wid * 64 + __ffsll((long long)sm) - 1));
+    }
     // block exclusive scan of the kept counts; tail survivors sum to m
     const uint32_t kc = __popc(keep);
     const uint32_t incl = wave_scan_incl_u32(kc), tl = wave_sum_u32(__popc(surv & ~below));
@@ -394,6 +405,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
     if (lane == 0) L.wtail[wid] = tl;
     __syncthreads();
     if (t == 0) KT(7);
+    const uint32_t tf = L.tf, F = tf * ZPT;
     uint32_t pre = incl - kc, Kz = 0, m = 0;
 #pragma unroll
     for (int w2 = 0; w2 < BT / 64; ++w2) {
@@ -415,19 +427,26 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
     // branch-free: every position stores (dropped ones into a per-lane trash
     // slot); the A-side rewrites of the reference's in-place ping buffer are
     // the only global stores, one per rewritten position
-    uint32_t wsm = 0;
+    if ((uint32_t)t < tf) {
+        uint4* dz = reinterpret_cast<uint4*>(zo + i0);
 #pragma unroll
-    for (int k = 0; k < ZPT; ++k) {
-        const bool rw = (rwm >> k) & 1u;
-        const uint32_t v = rw ? (nw | (x[k] & WS)) : x[k];
-        wsm |= ((x[k] & WS) ? 1u : 0u) << k;
-        const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
-        S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
-        *dst = (S)v;
-    }
-    for (uint32_t r = rwm; r; r &= r - 1) {
-        const int k = __ffs(r) - 1;
-        zc[i0 + k] = (S)(nw | (((wsm >> k) & 1u) ? WS : 0u));
+        for (int k = 0; k < V; ++k) dz[k] = v[k];
+        if ((uint32_t)t + 1u == tf) xs[swz(F - 1u)] = (S)x[ZPT - 1];   // the window's left neighbour may be it
+    } else if (keep | rwm) {
+        uint32_t wsm = 0;
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) {
+            const bool rw = (rwm >> k) & 1u;
+            const uint32_t y = rw ? (nw | (x[k] & WS)) : x[k];
+            wsm |= ((x[k] & WS) ? 1u : 0u) << k;
+            const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
+            S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
+            *dst = (S)y;
+        }
+        for (uint32_t r = rwm; r; r &= r - 1) {
+            const int k = __ffs(r) - 1;
+            zc[i0 + k] = (S)(nw | (((wsm >> k) & 1u) ? WS : 0u));
+        }
     }
     if (t == 0) KT(8);
     if (!EXACT && m) {
@@ -446,7 +465,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
     {
         const uint32_t tot = Kz + m, nfull = tot / PV;
         uint4* dst = reinterpret_cast<uint4*>(zo);
-        for (uint32_t q = t; q < nfull; q += BT) dst[q] = L.xv[q ^ ((q >> 3) & 7u)];
+        for (uint32_t q = F / PV + t; q < nfull; q += BT) dst[q] = L.xv[q ^ ((q >> 3) & 7u)];
         for (uint32_t j = nfull * PV + t; j < tot; j += BT) zo[j] = xs[swz(j)];
     }
     if (t == 0) KT(4);
