@@ -74,8 +74,8 @@ TILE_SYMS = 8192
 METRIC = "BPE merges/sec + tokenize GB/s, 1 GiB UTF-8 @ 32K vocab, 1/2/4/8 MI355X"
 HEADLINE = {"gen": "english", "n": 1 << 30, "seed": 2, "fancy_punct": 0.005}
 C2 = {"gen": "english", "n": 104_857_600, "seed": 2, "fancy_punct": 0.005}
-PMC_FILE = os.path.join(ROOT, "profiles", "r5", "s2", "pmc_kbody.json")
-ROCPROF_EN1G = os.path.join(ROOT, "profiles", "r5", "s2", "en1g_kernel_stats.csv")
+PMC_FILE = os.path.join(ROOT, "profiles", "r5", "close", "pmc_kbody.json")
+ROCPROF_EN1G = os.path.join(ROOT, "profiles", "r5", "close", "en1g_kernel_stats.csv")
 CAL_NOTE = ("FETCH_SIZE x2: tools/micro/fetch_cal.hip measured 64 counter bytes per distinct 128-B line for "
             "16-B streaming reads and 4-, 8- and 16-B one-per-line gathers alike (profiles/r3_fetch_calibration.json), "
             "so every read line moves 128 B; WRITE_SIZE counts 32-B granules (4-B scattered stores and atomics: 32 B "
@@ -222,15 +222,19 @@ def timed_runs(args, lib, ctx, dist, d, n, vocab, steps, warmup, flags=0, pairs_
     dist.barrier()
     lib.gbpe_synchronize(ctx)
     t0 = time.perf_counter()
-    total, last, st, create_s = 0, None, None, 0.0
+    total, last, st, create_s, run_s = 0, None, None, 0.0, []
     for _ in range(steps):
-        last, st = train_run(lib, ctx, d, n, vocab, flags=flags)
+        tr0 = time.perf_counter()
+        last, st = train_run(lib, ctx, d, n, vocab, flags=flags)   # (its last step call synchronises)
+        run_s.append(round(time.perf_counter() - tr0, 4))
         total += last.shape[0]
         create_s += st.ms_create / 1e3
     lib.gbpe_synchronize(ctx)
     t1 = time.perf_counter()
     dist.barrier()
     st.create_s_total = create_s   # (the timed runs' trainer creation, host wall)
+    st.run_s = run_s               # (each timed run's host wall, this rank)
+    log(f"[bench] timed runs (s): {run_s}")
     return dist.max(t1 - t0), total, last, st
 
 
@@ -249,6 +253,7 @@ def train_detail(st, sk):
         "sparse": {"merges": int(st.sparse_merges), "enters": int(st.sparse_enters), "exits": int(st.sparse_exits),
                    "sectors": int(st.sparse_sectors), "zone_at_entry": int(st.sparse_zone)},
         "ms_create": round(st.ms_create, 3),
+        "run_s": getattr(st, "run_s", None),
         "events": None if sk is None else {
             "merges": int(sk.timed_merges), "dense_merges": int(sk.timed_merges - sk.sparse_merges),
             "dense_bytes": int(sk.dense_bytes), "ms_dense": sk.ms_dense,

@@ -138,7 +138,7 @@ __device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {
 // ORs each word into the global signature once (one atomic per non-zero word
 // instead of three per created pair: early merges create thousands per sector)
 template <typename S, int NT = LTAB_T, typename TB = Table, typename LT = LdsTab<NT>, bool LSIG = false>
-__device__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, uint32_t cnt, uint32_t a, uint32_t b,
+__device__ __forceinline__ uint32_t body_sector(S* __restrict__ p, uint32_t* __restrict__ mp, uint32_t cnt, uint32_t a, uint32_t b,
                                 uint32_t nw, LT& lt, const TB& tb, DevState* st, uint32_t* __restrict__ sig,
                                 uint32_t& out_cnt, const uint32_t (&first)[5], const uint32_t (&firstm)[4],
                                 uint32_t* lsig, const uint32_t* nxt, const uint32_t* nxtm BSP_ARG) {
@@ -310,7 +310,7 @@ __device__ __forceinline__ uint32_t lane_mask_n(uint64_t i0, uint64_t lim, int n
 // zout (the persistent tail loop, k_tail): the delta table is shared with the body
 // pass (neither cleared nor flushed here) and m, the new zone length go to zout[0..1]
 template <typename S, bool EXACT, int BT, int NT = LTAB_T, int ZPT_ = ZoneDim<S, BT>::ZPT, typename TB = Table>
-__device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
+__device__ __forceinline__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
                          S* __restrict__ zo, ZoneLds<S, BT>& L,
                          LdsTab<NT>& lt, const TB& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
                          uint64_t* __restrict__ bytes, uint32_t round, uint32_t* zout = nullptr) {
@@ -506,7 +506,7 @@ __device__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const 
 //  workgroups: with nz <= 64 workgroups they all become resident.
 // k_refresh zeroes the granules for the next merge (tag = 1).
 template <typename S, bool EXACT, int BT, int NT, int ZPT>
-__device__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
+__device__ __forceinline__ void zone_seg(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
                          S* __restrict__ zo, ZSegState* zg, uint32_t nz, ZoneLds<S, BT>& L, LdsTab<NT>& lt,
                          const Table& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
                          uint64_t* __restrict__ bytes, uint32_t round) {
@@ -729,7 +729,7 @@ struct SelShard {
 };
 
 template <int BT>
-__device__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
+__device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
                            uint32_t round, bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
                            uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc,
                            const DevState*& gsnap, const DevState*& zsnap, const SelShard sh = SelShard(),
