@@ -363,19 +363,20 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         // sooner.  The partial maxima the next k_body reads are laid out per k_refresh
         // workgroup, so a grid change re-lays them out once (finish 0: no merge closed)
         if (t->refresh_late && zn <= t->refresh_late_z) {
-            // (at most one workgroup per block: the partial maxima hold nblk + 1 per half)
+            // (at most one workgroup per block: the partial maxima hold nblk + 1 per half;
+            // at most TPB blocks per workgroup)
             const uint32_t want = std::min<uint32_t>(t->tb.nblk,
-                                                     std::max<uint32_t>(t->refresh_late, (uint32_t)gbpe_div_up(t->tb.nblk, 64)));
+                                                     std::max<uint32_t>(t->refresh_late, (uint32_t)gbpe_div_up(t->tb.nblk, TPB)));
             if (want != t->g_refresh) {
                 t->g_refresh = g_refresh = want;
                 if (t->u16)
-                    hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(want), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
-                                       (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr,
-                                       (uint32_t*)nullptr, FusedSel(), t->part, (uint32_t*)nullptr);
+                    GBPE_LAUNCH_REFRESH(uint16_t, want, t->tb.nblk, s, t->st, 0u, 0, t->tb, (uint16_t*)nullptr,
+                                        (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(),
+                                        t->part, (uint32_t*)nullptr);
                 else
-                    hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(want), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
-                                       (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr,
-                                       (uint32_t*)nullptr, FusedSel(), t->part, (uint32_t*)nullptr);
+                    GBPE_LAUNCH_REFRESH(uint32_t, want, t->tb.nblk, s, t->st, 0u, 0, t->tb, (uint32_t*)nullptr,
+                                        (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(),
+                                        t->part, (uint32_t*)nullptr);
                 GBPE_LAUNCH_CHECK(t->ctx);
             }
         }

@@ -535,7 +535,8 @@ struct FusedSel {
 
 // recompute block maxima for dirty blocks; with `finish`, also closes the
 // merge of `round` (state.symbol_count := new count, train.wgsl:605-607)
-template <typename S>
+
+template <typename S, bool WIDE = false>
 __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, int finish, Table tb, S* __restrict__ cur,
                                                  const uint32_t* __restrict__ rwlist, DevState* zst,
                                                  uint32_t* __restrict__ clog = nullptr, FusedSel fs = FusedSel(),
@@ -546,16 +547,22 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             if (i == 0 || i >= 16) zseg[i] = 0u;
     (void)rwlist;
     if (part && finish == 2 && threadIdx.x == 0) KTR(0);
-    // this WG's contiguous run of blocks (<= 64): all flags (and, for `part`, the
-    // maxima kept from before) in one load — issued first, so block 0's state
-    // snapshot below travels in the same round trip instead of before it
-    __shared__ uint64_t s_dmask;
-    __shared__ uint64_t s_bm[64];
-    const uint32_t per = (tb.nblk + gridDim.x - 1) / gridDim.x;   // <= 64 (host-sized grid)
+    // this WG's contiguous run of blocks (<= TPB, one per thread): all flags (and,
+    // for `part`, the maxima kept from before) in one load — issued first, so
+    // block 0's state snapshot below travels in the same round trip instead of
+    // before it.  Late steps of a large table take up to 256 blocks per workgroup
+    // (the WIDE form: C5's 2^25 slots give 512 partial maxima for the selection to
+    // reduce, not 2048; 1,024 blocks per workgroup measured slower, and the narrow
+    // form stays a kernel of its own: one body for both cost 1 GiB 1-2 %,
+    // profiles/r5/s13)
+    __shared__ uint64_t s_dmask[WIDE ? TPB / 64 : 1];
+    __shared__ uint64_t s_bm[WIDE ? TPB : 64];
+    const uint32_t per = (tb.nblk + gridDim.x - 1) / gridDim.x;   // <= 64, WIDE: <= TPB (GBPE_LAUNCH_REFRESH)
+    constexpr bool wide = WIDE;
     const uint32_t b0 = blockIdx.x * per;
     uint64_t f_bm = 0ull;
     bool f_d = false;
-    if (threadIdx.x < 64) {
+    if (wide || threadIdx.x < 64) {
         const uint32_t blk = b0 + threadIdx.x;
         const bool in = threadIdx.x < per && blk < tb.nblk;
         if (part && in) f_bm = tb.bmax[blk];
@@ -616,18 +623,20 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
     // then every wave re-maxes its share of the dirty ones, one 256-slot block at a
     // time (no workgroup barrier per block: a merge dirties a few blocks per
     // workgroup, each holding a few live pairs)
-    if (threadIdx.x < 64) {
+    if (wide || threadIdx.x < 64) {
         if (part) s_bm[threadIdx.x] = f_bm;
         const unsigned long long m = __ballot(f_d);
-        if (threadIdx.x == 0) s_dmask = m;
+        if ((threadIdx.x & 63) == 0) s_dmask[threadIdx.x >> 6] = m;
     }
     __syncthreads();
     {
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
         constexpr int NV = (1 << BLK_LOG2) / 2 / 64;   // 16-byte loads per lane
-        uint64_t dm = s_dmask;
-        for (int k = 0; dm; ++k) {   // (wave-uniform)
-            const uint32_t bit = (uint32_t)(__ffsll((long long)dm) - 1);
+        const int nm = wide ? TPB / 64 : 1;   // 64-block masks
+        int k = 0;
+        for (int w2 = 0; w2 < nm; ++w2)
+        for (uint64_t dm = s_dmask[w2]; dm; ++k) {   // (wave-uniform)
+            const uint32_t bit = (uint32_t)w2 * 64u + (uint32_t)(__ffsll((long long)dm) - 1);
             dm &= dm - 1;
             if ((k & (TPB / 64 - 1)) != wid) continue;
             const uint32_t blk = b0 + bit;
@@ -661,14 +670,32 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
         }
     }
     __syncthreads();
-    if (part && threadIdx.x < 64) {   // this workgroup's maximum, for sel_inline
-        const uint64_t best = wave_max_u64(s_bm[threadIdx.x]);
-        if (threadIdx.x == 0) {
-            part[blockIdx.x] = best;
-            if (finish == 2) KTR(5);
+    if (part) {   // this workgroup's maximum, for sel_inline
+        uint64_t best = 0ull;
+        if (wide) {   // one wave over the blocks past the first 64 first
+            if (threadIdx.x < 64)
+                for (uint32_t i = threadIdx.x + 64u; i < per; i += 64u) best = s_bm[i] > best ? s_bm[i] : best;
+        }
+        if (threadIdx.x < 64) {
+            const uint64_t v = s_bm[threadIdx.x];
+            best = wave_max_u64(v > best ? v : best);
+            if (threadIdx.x == 0) {
+                part[blockIdx.x] = best;
+                if (finish == 2) KTR(5);
+            }
         }
     }
 }
+
+// k_refresh in the form its grid needs: more than 64 table blocks per workgroup
+// (the late grids of a large table) take the WIDE form
+#define GBPE_LAUNCH_REFRESH(S, grid, nblk, s, ...)                                               \
+    do {                                                                                         \
+        if ((uint64_t)(grid) * 64u < (uint64_t)(nblk))                                           \
+            hipLaunchKernelGGL((k_refresh<S, true>), dim3(grid), dim3(TPB), 0, s, __VA_ARGS__);  \
+        else                                                                                     \
+            hipLaunchKernelGGL((k_refresh<S, false>), dim3(grid), dim3(TPB), 0, s, __VA_ARGS__); \
+    } while (0)
 
 constexpr uint32_t GRP = 64;    // tiles per group sum (two-level tile prefix)
 constexpr uint32_t GSTR = 64;   // group sums 256 B apart: each is its own atomic serialisation point

@@ -212,8 +212,8 @@ int lex_root_build(gbpe_trainer* t, const S* store, const uint32_t* mul, uint64_
     // states: body = every symbol before the zone (kept modulo 2^32 on the device)
     rc = sp_init_states(t, cap, (uint32_t)body_len, (uint32_t)z, (uint32_t)z);
     if (rc != GBPE_OK) return rc;
-    hipLaunchKernelGGL(k_refresh<S>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
-                       (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part);
+    GBPE_LAUNCH_REFRESH(S, t->g_refresh, t->tb.nblk, s, t->st, 0u, 0, t->tb, (S*)nullptr, (const uint32_t*)nullptr,
+                        (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part, (uint32_t*)nullptr);
     GBPE_LAUNCH_CHECK(ctx);
     TR_HIP(t, hipStreamSynchronize(s));
     rt.mark("states");

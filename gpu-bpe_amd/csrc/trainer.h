@@ -273,13 +273,13 @@ int table_rehash(gbpe_trainer* t, uint32_t lg) {
     hipLaunchKernelGGL(k_clear_dirty_all, dim3(gbpe_div_up(t->tb.nblk, 256)), dim3(256), 0, s, t->st, t->tb);
     // block maxima and the per-workgroup partial maxima the next selection reads
     if (t->u16)
-        hipLaunchKernelGGL(k_refresh<uint16_t>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
-                           (uint16_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr,
-                           FusedSel(), t->part, (uint32_t*)nullptr);
+        GBPE_LAUNCH_REFRESH(uint16_t, t->g_refresh, t->tb.nblk, s, t->st, 0u, 0, t->tb, (uint16_t*)nullptr,
+                            (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part,
+                            (uint32_t*)nullptr);
     else
-        hipLaunchKernelGGL(k_refresh<uint32_t>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb,
-                           (uint32_t*)nullptr, (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr,
-                           FusedSel(), t->part, (uint32_t*)nullptr);
+        GBPE_LAUNCH_REFRESH(uint32_t, t->g_refresh, t->tb.nblk, s, t->st, 0u, 0, t->tb, (uint32_t*)nullptr,
+                            (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part,
+                            (uint32_t*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     TR_HIP(t, hipStreamSynchronize(s));
     pool_free(t->ctx, old);
@@ -333,8 +333,8 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
     fs.log = nullptr;
     fs.grpsum = t->grpsum;
     fs.exact = exact ? 1u : 0u;
-    hipLaunchKernelGGL(k_refresh<S>, dim3(g_refresh), dim3(TPB), 0, s, t->st, round, 1, t->tb, cur,
-                       (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, fs);
+    GBPE_LAUNCH_REFRESH(S, g_refresh, t->tb.nblk, s, t->st, round, 1, t->tb, cur, (const uint32_t*)nullptr,
+                        (DevState*)nullptr, (uint32_t*)nullptr, fs, (uint64_t*)nullptr, (uint32_t*)nullptr);
     if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
@@ -464,8 +464,8 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
                                t->tb, (const S*)t->wtmp, (const DevState*)t->st);
     }
     if (timing) TR_HIP(t, hipEventRecord(ev[2], s));
-    hipLaunchKernelGGL(k_refresh<S>, dim3(g.refresh), dim3(TPB), 0, s, t->st, round, 2, t->tb, (S*)nullptr,
-                       (const uint32_t*)nullptr, t->zst, t->d_clog, FusedSel(), t->part, t->zseg);
+    GBPE_LAUNCH_REFRESH(S, g.refresh, t->tb.nblk, s, t->st, round, 2, t->tb, (S*)nullptr, (const uint32_t*)nullptr,
+                        t->zst, t->d_clog, FusedSel(), t->part, t->zseg);
     if (timing) TR_HIP(t, hipEventRecord(ev[4], s));
     GBPE_LAUNCH_CHECK(t->ctx);
     return GBPE_OK;
@@ -1177,8 +1177,8 @@ int sp_enter(gbpe_trainer* t, bool with_zone = true, uint32_t next_mc = 0) {
     }
     rc = sp_init_states(t, cap, Zs, z, z);
     if (rc != GBPE_OK) return rc;
-    hipLaunchKernelGGL(k_refresh<S>, dim3(t->g_refresh), dim3(TPB), 0, s, t->st, 0u, 0, t->tb, (S*)nullptr,
-                       (const uint32_t*)nullptr, (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part);
+    GBPE_LAUNCH_REFRESH(S, t->g_refresh, t->tb.nblk, s, t->st, 0u, 0, t->tb, (S*)nullptr, (const uint32_t*)nullptr,
+                        (DevState*)nullptr, (uint32_t*)nullptr, FusedSel(), t->part, (uint32_t*)nullptr);
     GBPE_LAUNCH_CHECK(t->ctx);
     TR_HIP(t, hipStreamSynchronize(s));
     t->sp = true;

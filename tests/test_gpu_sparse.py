@@ -120,3 +120,19 @@ def test_sparse_vs_dense_full_c2(eng):
     assert np.array_equal(p1[0], p2[0]) and np.array_equal(p1[1], p2[1])
     _assert_counts_match_stream(p1, s1)
     assert st1.tail_dropped == st2.tail_dropped == meta["tail_total"]
+
+
+@pytest.mark.parametrize("table_log2", [18, 20])
+def test_sparse_wide_refresh_workgroups(eng, monkeypatch, table_log2):
+    # late k_refresh grids take up to 1,024 table blocks per workgroup (C5's 2^25
+    # slots: 128 partial maxima per selection instead of 2,048); rfl=1 with a late
+    # threshold above every zone forces the widest form from the first step:
+    # 2^18 slots -> one workgroup over all 1,024 blocks, 2^20 -> 4 x 1,024
+    from gpubpe import synth
+    monkeypatch.setenv("GBPE_DEBUG", "rfl=1,rflz=100000000")
+    data = synth.english(300000, seed=41)
+    ref = O.train(data, 2048)
+    m, s, pairs, st = _train_native(eng, data, 2048, batch=32, sparse="early", table_log2=table_log2)
+    assert st.sparse_merges > 0
+    assert m == ref["merges"] and np.array_equal(s, ref["symbols"])
+    _assert_counts_match_stream(pairs, s)
