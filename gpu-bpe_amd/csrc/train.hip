@@ -34,6 +34,7 @@
 // Per merge: k_select (1 WG) → k_delta → k_compact (tiles + tail) → k_refresh.
 
 
+#include <chrono>
 #include "trainer.h"
 
 int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const uint8_t* word_starts,
@@ -229,6 +230,8 @@ extern "C" int gbpe_trainer_create_from_state(gbpe_ctx* ctx, const uint32_t* cur
 
 namespace {
 int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out, uint32_t* n_done, uint32_t* early_stop) {
+    const auto hs0 = std::chrono::steady_clock::now();
+    if (t->htime && t->ht_steps) t->ht_out += std::chrono::duration<double, std::micro>(hs0 - t->ht_last).count();
     if (n_done) *n_done = 0;
     if (early_stop) *early_stop = t->stop ? 1u : 0u;
     uint32_t k = max_merges ? max_merges : t->batch;
@@ -290,13 +293,24 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     }
     // keep the zone near its minimum, then rebuild stale filters now and then
     if (t->sp) {
+        const auto a0 = std::chrono::steady_clock::now();
+        const uint32_t ns0 = t->sp_shrinks;
         int rc = t->u16 ? sp_shrink<uint16_t>(t) : sp_shrink<uint32_t>(t);
         if (rc != GBPE_OK) return rc;
+        if (t->htime && t->sp_shrinks != ns0) {
+            t->ht_shrink += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a0).count();
+            ++t->ht_nshrink;
+        }
     }
     if (t->sp && t->sp_age >= 4096) {   // signatures saturate faster than the token bitmap goes stale
+        const auto a0 = std::chrono::steady_clock::now();
         const bool wb = t->sp_bits_age >= 16384;
         int rc = t->u16 ? sp_filters<uint16_t>(t, wb) : sp_filters<uint32_t>(t, wb);
         if (rc != GBPE_OK) return rc;
+        if (t->htime) {
+            t->ht_filters += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a0).count();
+            ++t->ht_nfilters;
+        }
     }
     // waiting for the lexicon entry on a long stream: one merge per step (a dense merge
     // costs milliseconds there; every round the step enqueues after the entry point
@@ -396,9 +410,12 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         }
         return GBPE_OK;
     };
+    const auto h0 = std::chrono::steady_clock::now();
+    auto h1 = h0;
     {
         int rc = launch_all();
         if (rc != GBPE_OK) return rc;
+        h1 = std::chrono::steady_clock::now();
         // the read-backs (and, sparse, k_live's count) in one launch: no copy blits
         const bool cl = sparse && t->d_clog;
         hipLaunchKernelGGL(k_step_out, dim3(1), dim3(1024), 0, s, t->st, sparse ? t->zst : (DevState*)nullptr, t->tb,
@@ -408,6 +425,20 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     }
     TR_HIP(t, hipStreamSynchronize(s));
     const uint32_t done = hs->merges_done;
+    if (t->htime) {   // (diagnostic) host enqueue vs wait; "late": a zone of <= 16K symbols
+        t->ht_pre += std::chrono::duration<double, std::micro>(h0 - hs0).count();
+        const double enq = std::chrono::duration<double, std::micro>(h1 - h0).count();
+        const double wait = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h1).count();
+        t->ht_enq += enq;
+        t->ht_wait += wait;
+        ++t->ht_steps;
+        if (sparse && (uint32_t)t->n - hs->B <= 16384u) {
+            t->ht_enq_late += enq;
+            t->ht_wait_late += wait;
+            ++t->ht_steps_late;
+            t->ht_merges_late += done;
+        }
+    }
 #ifdef GBPE_BSPROF
     if (sparse && getenv("GBPE_BSPROF")) {   // body_sector's cycle split of this step (train_dev.h)
         unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -488,6 +519,10 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     t->stop = hs->stop != 0;
     if (n_done) *n_done = done;
     if (early_stop) *early_stop = t->stop ? 1u : 0u;
+    if (t->htime) {
+        t->ht_last = std::chrono::steady_clock::now();
+        t->ht_post += std::chrono::duration<double, std::micro>(t->ht_last - h1).count();
+    }
     return GBPE_OK;
 }
 }  // namespace
@@ -658,6 +693,16 @@ extern "C" int gbpe_trainer_pair_counts(gbpe_trainer* t, uint32_t* pids, uint32_
 extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     if (!t) return;
     if (t->ctx && t->ctx->stream) hipStreamSynchronize(t->ctx->stream);
+    if (t->htime && t->ht_steps)
+        fprintf(stderr, "[htime] steps %llu: before launch %.2f ms, enqueue %.2f ms, wait %.2f ms, after sync %.2f ms, "
+                        "caller between steps %.2f ms, shrinks %llu in %.2f ms, filter rebuilds %llu in %.2f ms | late steps %llu (%llu merges): enqueue %.2f ms "
+                        "(%.2f us/merge), wait %.2f ms (%.2f us/merge)\n",
+                (unsigned long long)t->ht_steps, t->ht_pre / 1e3, t->ht_enq / 1e3, t->ht_wait / 1e3,
+                (t->ht_post - t->ht_wait) / 1e3, t->ht_out / 1e3, (unsigned long long)t->ht_nshrink, t->ht_shrink / 1e3,
+                (unsigned long long)t->ht_nfilters, t->ht_filters / 1e3, (unsigned long long)t->ht_steps_late,
+                (unsigned long long)t->ht_merges_late, t->ht_enq_late / 1e3,
+                t->ht_merges_late ? t->ht_enq_late / t->ht_merges_late : 0.0, t->ht_wait_late / 1e3,
+                t->ht_merges_late ? t->ht_wait_late / t->ht_merges_late : 0.0);
 #ifdef GBPE_KTRACE
     if (const char* path = getenv("GBPE_KTRACE_OUT")) {   // one file per trainer: path.<done merges>
         std::vector<unsigned long long> h((size_t)(KT_MERGES / KT_EVERY) * 2 * KT_WG * KT_SLOTS);

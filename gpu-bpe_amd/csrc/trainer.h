@@ -6,6 +6,7 @@
 #include <cmath>
 
 #include "train_dev.h"
+#include <chrono>
 #include "sparse.h"
 
 
@@ -114,6 +115,12 @@ struct gbpe_trainer {
     uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
     uint32_t* h_clog = nullptr;
     FILE* trace = nullptr;
+    uint32_t htime = 0;          // GBPE_DEBUG htime=1: host enqueue / wait split of every step (stderr at destroy)
+    double ht_enq = 0, ht_wait = 0, ht_enq_late = 0, ht_wait_late = 0, ht_pre = 0, ht_post = 0, ht_out = 0;
+    double ht_shrink = 0, ht_filters = 0, ht_grow = 0;
+    uint64_t ht_nshrink = 0, ht_nfilters = 0;
+    std::chrono::steady_clock::time_point ht_last{};   // the previous step's return
+    uint64_t ht_steps = 0, ht_steps_late = 0, ht_merges_late = 0;
     // word-lexicon body (lexicon.h): the sectors hold one copy of every
     // distinct body word instead of the body itself
     bool lex = false;            // the current sparse entry uses it
@@ -1324,6 +1331,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->refresh_late_z = (uint32_t)gbpe_debug_knob("rflz", t->refresh_late_z);
     t->lx_div = (uint32_t)std::max<long>(1, gbpe_debug_knob("lxdiv", t->lx_div));   // lexicon entry / sub-step sweeps
     t->lx_wg = (uint32_t)std::max<long>(1, gbpe_debug_knob("lxwg", t->lx_wg));
+    t->htime = (uint32_t)gbpe_debug_knob("htime", 0);
     t->sub_k = (uint32_t)std::max<long>(1, gbpe_debug_knob("subk", t->sub_k));
     t->sub_zone = (uint32_t)std::max<long>(1, gbpe_debug_knob("subz", t->sub_zone));
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;

@@ -8,6 +8,7 @@ Times in µs from the first k_body workgroup start; medians over merge buckets.
   ref_*      k_refresh first start, last end     nhit, ncand  workgroups with candidates, sectors
   z_*        zone workgroup (thread 0): selection done, zone loaded, site deltas done, scan, survivors
              staged, window staged, zone stored (then flush)
+  period     k_body start to k_body start, per merge, inside a 128-merge step
 
 usage: python tools/ktrace_show.py <dump file>
 """
@@ -21,7 +22,7 @@ EVERY, WG, SLOTS, HZ = 16, 2048, 12, 100e6
 
 def main():
     raw = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 2 * WG, SLOTS)
-    rows = []
+    rows, t0abs = [], []
     for i in range(raw.shape[0]):
         body, ref = raw[i, :WG], raw[i, WG:]
         on = body[:, 0] > 0
@@ -34,14 +35,23 @@ def main():
         hit, idle, zone = role == 1, (role == 0) & (b[:, 5] > 0), role == 2
         r = ref[ref[:, 0] > 0].astype(np.float64)
         mx = lambda m, c: us(b[m, c].max()) if m.any() else np.nan
+        t0abs.append((i * EVERY, t0))
         rows.append([i * EVERY, us(b[:, 0].max()), us(b[b[:, 1] > 0, 1].max()), mx(zone, 5), mx(idle, 5),
                      mx(hit, 2), mx(hit, 3), mx(hit, 4), mx(hit, 5),
                      us(r[:, 0].min()) if len(r) else np.nan, us(r[:, 5].max()) if len(r) else np.nan,
                      hit.sum(), (body[on, 6][hit] >> 8).sum(), on.sum(),
                      mx(zone, 1), mx(zone, 2), mx(zone, 3), mx(zone, 7), mx(zone, 8), mx(zone, 9), mx(zone, 4)])
+    # the merge period inside a step: first k_body start to the one EVERY merges later
+    per = {m: np.nan for m, _ in t0abs}
+    for (m0, t0), (m1, t1) in zip(t0abs[:-1], t0abs[1:]):
+        if m1 - m0 == EVERY and m0 // 128 == m1 // 128:
+            per[m0] = (t1 - t0) / HZ * 1e6 / EVERY
+    for r in rows:
+        r.append(per.get(r[0], np.nan))
     a = np.array(rows)
     names = ["start_max", "sel", "zone", "idle_end", "hit_cand", "hit_sig", "hit_sect", "hit_end", "ref_start",
-             "ref_end", "nhit", "ncand", "nwg", "z_sel", "z_load", "z_sites", "z_scan", "z_keep", "z_win", "z_wrote"]
+             "ref_end", "nhit", "ncand", "nwg", "z_sel", "z_load", "z_sites", "z_scan", "z_keep", "z_win", "z_wrote",
+             "period"]
     edges = [int(e) for e in os.environ.get("EDGES", "0,150,300,500,1000,2000,4000,8000,16000,24000,40000").split(",")]
     print(f"{'merges':<13}{'n':>5}" + "".join(f"{k:>10}" for k in names))
     for lo, hi in zip(edges[:-1], edges[1:]):
