@@ -828,12 +828,12 @@ __device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const ui
 
 // Body pass: blocks [0, nbody) each own `wpg` consecutive bitmap words of
 // (a-row & b-row), tested PW words at a time: the candidate sectors whose pair
-// signature may hold (a, b) are merged (one wave per sector).  A fixed grid of
-// wide workgroups (about 4 per CU at 1 GiB) instead of one workgroup per 16
-// words: the selection each workgroup repeats, and the rounds of workgroup
-// scheduling, cost more than the bitmap words themselves (75K words per row at
-// 1 GiB).  Blocks >= nbody copy the stale-window source [n - 2mc - Bp, + mc) of
-// the zone's other buffer to `wtmp`.
+// signature may hold (a, b) are merged (one wave per sector).  At most one
+// workgroup per CU (a larger grid's selection repeats and scheduling rounds cost
+// more than the bitmap words), and as many as the row has words up to that: a
+// word's candidates are then merged by one workgroup's waves in parallel, not
+// queued behind other words' (body_grid).  Blocks >= nbody copy the stale-window
+// source [n - 2mc - Bp, + mc) of the zone's other buffer to `wtmp`.
 // With `zst` (zone <= ZMAX), block nbody runs the whole zone pass (zone_one) and
 // there are no copy blocks: one launch merges body and zone.
 constexpr uint32_t SP_PW = 64;               // bitmap words tested per pass (one per lane of wave 0)

@@ -96,6 +96,8 @@ struct gbpe_trainer {
     uint32_t* d_bhist = nullptr; // byte-pair histogram of the first count (65,536 u32)
     uint32_t count_bytes_on = 1; // first count by the byte-pair histogram (0: hashed k_count_full)
     uint32_t lx_size_on = 1;     // word table sized from a sampled distinct count (0: from the word count)
+    uint32_t body_min = 256;     // k_body workgroups at least, one bitmap word each at most (GBPE_DEBUG bmin;
+                                 // 1 = the round-4 sizing of >= 16 / 32 words per workgroup)
     uint32_t lx_wg = 16384;      // k_lx_hash workgroups (at least LX_WPT words per thread; GBPE_DEBUG lxwg)
     uint32_t lx_resize = 0;      // builds whose sampled table was too small (rerun at full size)
     uint32_t lx_div = 16;        // with the lexicon: enter once next_mc * lx_div <= n, from the first step on (GBPE_DEBUG lxdiv)
@@ -367,6 +369,13 @@ inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* 
     const uint32_t W = (uint32_t)gbpe_div_up(t->nsec, 32);
     const uint32_t minw = bt == 1024 ? 32u : 16u;
     uint32_t g = (uint32_t)gbpe_div_up(W, minw);
+    // but at least body_min workgroups (one bitmap word, 32 sectors, each at least):
+    // a word's candidates then spread over more CUs instead of queueing on one
+    // workgroup's waves (round 5, profiles/r5/s20: bmin 1 -> 256 took C1 25.1 ->
+    // 13.2 ms, C2 0.470 -> 0.428 s, 1 GiB 0.602 -> 0.568 s; C5 unchanged — its
+    // 131K-sector bitmap rows already fill every CU)
+    const uint32_t gmin = std::min<uint32_t>(W, t->body_min);
+    if (g < gmin) g = gmin;
     if (g > (cap ? cap : t->body_cap)) g = cap ? cap : t->body_cap;
     if (g == 0) g = 1;
     *wpg = (uint32_t)gbpe_div_up(W, g);
@@ -1332,6 +1341,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->lx_div = (uint32_t)std::max<long>(1, gbpe_debug_knob("lxdiv", t->lx_div));   // lexicon entry / sub-step sweeps
     t->lx_wg = (uint32_t)std::max<long>(1, gbpe_debug_knob("lxwg", t->lx_wg));
     t->htime = (uint32_t)gbpe_debug_knob("htime", 0);
+    t->body_min = (uint32_t)std::max<long>(1, gbpe_debug_knob("bmin", t->body_min));
     t->sub_k = (uint32_t)std::max<long>(1, gbpe_debug_knob("subk", t->sub_k));
     t->sub_zone = (uint32_t)std::max<long>(1, gbpe_debug_knob("subz", t->sub_zone));
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;

@@ -25,6 +25,7 @@ sys.path.insert(0, os.path.join(sys.argv[1], "gpu-bpe_amd"))
 import numpy as np
 from gpubpe import _lib, synth
 CONF = {
+    "c1": (lambda: synth.english(262_144, seed=1), 1024, 0),
     "c2": (lambda: synth.english(104_857_600, seed=2, fancy_punct=0.005), 32768, 0),
     "en1g": (lambda: synth.english(1 << 30, seed=2, fancy_punct=0.005), 32768, 0),
     "ml1g": (lambda: synth.multilingual(1 << 30, seed=3), 32768, 0),
