@@ -726,6 +726,7 @@ __device__ __forceinline__ void zone_seg(DevState* st, DevState* zst, const DevS
 // here changes under it.  Saves the k_select launch per merge.
 struct SelShard {
     uint32_t zf = 3;         // zone rule: z >= max(2 mc + mc_prev, zf mc) + 2 (trainer zone_f)
+    uint32_t sub = 1;        // k_body workgroups per bitmap word (1, 2, 4: a row of few words, body_grid)
 };
 
 template <int BT>
@@ -929,7 +930,11 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     if (t == 0) s_any = 0u;
     uint32_t removed = 0, ncand_all = 0;
     uint64_t moved = 0, rd = 0;   // sector symbols read + rewritten (wave-uniform); extents + signature words read
-    const uint32_t w_beg = bid * wpg, w_end = w_beg + wpg < W ? w_beg + wpg : W;
+    // sh.sub > 1: this workgroup takes a 32/sub-sector slice of word bid / sub
+    const uint32_t sub = sh.sub, sw = 32u / sub;
+    const uint32_t w_beg = sub > 1 ? bid / sub : bid * wpg;
+    const uint32_t w_end = sub > 1 ? w_beg + 1 : (w_beg + wpg < W ? w_beg + wpg : W);
+    const uint32_t smask = sub > 1 ? ((1u << sw) - 1u) << ((bid % sub) * sw) : 0xFFFFFFFFu;
     for (uint32_t w0 = w_beg; w0 < w_end; w0 += SP_PW) {
         __syncthreads();   // the previous pass is done with s_ntok / s_n / the candidate arrays
         if (t == 0) {
@@ -939,7 +944,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         __syncthreads();
         if (t < (int)SP_PW) {   // token candidates (one wave: list positions from its scan, no LDS counter)
             const uint32_t w = w0 + t;
-            uint32_t c = w < w_end ? bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w] : 0u;
+            uint32_t c = w < w_end ? bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w] & smask : 0u;
             const uint32_t pc = (uint32_t)__popc(c), incl = wave_scan_incl_u32(pc);
             uint32_t pos = incl - pc;
             if (t == (int)SP_PW - 1) s_ntok = incl;

@@ -352,7 +352,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         const uint64_t zt = gbpe_div_up(zn, TILE);
         const uint32_t z256 = t->u16 ? zone_max<uint16_t>(256) : zone_max<uint32_t>(256);
         sg.bt = zn <= z256 ? 256 : 1024;   // small zone: the low-latency 256-thread workgroups
-        body_grid(t, sg.bt, &sg.body, &sg.wpg);
+        body_grid(t, sg.bt, &sg.body, &sg.wpg, 0, &sg.sub);
         if (sg.bt == 1024 && t->u16 && zn <= 16384u && t->zone16) sg.bt = 1023;
         sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt)) ? 1u : 0u;
         // a zone of 16K-1M symbols: 16K-symbol segments inside k_body (its ZSEG form)
@@ -371,7 +371,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         // the body takes the CUs the others leave
         const uint32_t extra = sg.zone1 ? sg.zone1 : sg.copy;
         if (sg.bt >= 1023 && t->body_fit && extra && sg.body + extra > t->body_cap && 2 * extra <= t->body_cap)
-            body_grid(t, sg.bt, &sg.body, &sg.wpg, t->body_cap - extra);
+            body_grid(t, sg.bt, &sg.body, &sg.wpg, t->body_cap - extra, &sg.sub);
         // late steps (a zone of <= 16K symbols): a smaller k_refresh grid —
         // a late merge dirties a few blocks, and fewer workgroups dispatch and drain
         // sooner.  The partial maxima the next k_body reads are laid out per k_refresh

@@ -96,6 +96,8 @@ struct gbpe_trainer {
     uint32_t* d_bhist = nullptr; // byte-pair histogram of the first count (65,536 u32)
     uint32_t count_bytes_on = 1; // first count by the byte-pair histogram (0: hashed k_count_full)
     uint32_t lx_size_on = 1;     // word table sized from a sampled distinct count (0: from the word count)
+    uint32_t body_sub = 4;       // most k_body workgroups per bitmap word (1, 2, 4; GBPE_DEBUG bsub;
+                                 // C1 13.5 -> 11.9 ms at 4, profiles/r5/s21)
     uint32_t body_min = 256;     // k_body workgroups at least, one bitmap word each at most (GBPE_DEBUG bmin;
                                  // 1 = the round-4 sizing of >= 16 / 32 words per workgroup)
     uint32_t lx_wg = 16384;      // k_lx_hash workgroups (at least LX_WPT words per thread; GBPE_DEBUG lxwg)
@@ -354,6 +356,7 @@ int launch_merge(gbpe_trainer* t, uint32_t round, hipStream_t s, uint32_t g_delt
 struct SpGrid {
     uint32_t body, copy, zdelta, zcompact, refresh;
     uint32_t wpg = 16;    // bitmap words per k_body workgroup
+    uint32_t sub = 1;     // k_body workgroups per bitmap word (wpg = 1)
     uint32_t ztail = 0;   // stale-tail slice blocks of the multi-tile zone k_delta
     uint32_t zone1;   // zone workgroups inside k_body: 1 = zone_one, >= 2 = zone_seg segments, 0 = multi-tile passes
     int bt;       // k_body workgroup size (256 or 1024)
@@ -365,7 +368,8 @@ uint32_t zone_max(int bt) {
 }
 // k_body grid: bitmap words per workgroup (>= the measured best 16 / 32 at C2 size),
 // at most `cap` workgroups (default: body_cap, one per CU)
-inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* wpg, uint32_t cap = 0) {
+inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* wpg, uint32_t cap = 0,
+                      uint32_t* sub = nullptr) {
     const uint32_t W = (uint32_t)gbpe_div_up(t->nsec, 32);
     const uint32_t minw = bt == 1024 ? 32u : 16u;
     uint32_t g = (uint32_t)gbpe_div_up(W, minw);
@@ -382,6 +386,15 @@ inline void body_grid(const gbpe_trainer* t, int bt, uint32_t* nbody, uint32_t* 
     if (*wpg == 0) *wpg = 1;
     *nbody = (uint32_t)gbpe_div_up(W, *wpg);
     if (*nbody == 0) *nbody = 1;
+    if (sub) {   // a row of few words: 2 or 4 workgroups per word (slices of 16 / 8 sectors)
+        *sub = 1;
+        const uint32_t c = cap ? cap : t->body_cap;
+        while (*sub * 2 <= t->body_sub && (uint64_t)W * *sub * 2 <= c) *sub *= 2;
+        if (*sub > 1) {
+            *wpg = 1;
+            *nbody = W * *sub;
+        }
+    }
 }
 
 // launch k_body<S, EXACT, bt> (one instantiation per workgroup size)
@@ -413,16 +426,18 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const uint32_t gb = g.body + (g.zone1 ? g.zone1 : g.copy);
     const uint32_t z1 = g.zone1;   // k_body's own zone workgroups
     const int bt = inbody ? 2048 : g.bt;
+    SelShard sh = sel_single(t);
+    sh.sub = g.sub;
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
         launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
-                             (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
+                             (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sh,
                              sp_mul(t), (ZSegState*)t->zseg);
     else
         launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
                               g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
-                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sel_single(t),
+                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sh,
                               sp_mul(t), (ZSegState*)t->zseg);
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
     if (!g.zone1 && !exact && t->zdr_on && t->zdr_out) {
@@ -1342,6 +1357,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->lx_wg = (uint32_t)std::max<long>(1, gbpe_debug_knob("lxwg", t->lx_wg));
     t->htime = (uint32_t)gbpe_debug_knob("htime", 0);
     t->body_min = (uint32_t)std::max<long>(1, gbpe_debug_knob("bmin", t->body_min));
+    t->body_sub = (uint32_t)std::min<long>(4, std::max<long>(1, gbpe_debug_knob("bsub", t->body_sub)));
     t->sub_k = (uint32_t)std::max<long>(1, gbpe_debug_knob("subk", t->sub_k));
     t->sub_zone = (uint32_t)std::max<long>(1, gbpe_debug_knob("subz", t->sub_zone));
     if (t->sp_zt < t->zone_f) t->sp_zt = t->zone_f;
