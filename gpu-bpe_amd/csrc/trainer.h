@@ -428,6 +428,9 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const int bt = inbody ? 2048 : g.bt;
     SelShard sh = sel_single(t);
     sh.sub = g.sub;
+    if ((uint64_t)g.body + 1 > t->wg_cap)   // k_body's per-workgroup byte counters (and the zone's after them)
+        return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "k_body grid (%u) above its byte counters (%llu)", g.body,
+                              (unsigned long long)t->wg_cap);
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
     if (exact)
         launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
@@ -592,7 +595,8 @@ int sp_reserve(gbpe_trainer* t, uint64_t need_sec, uint64_t need_store, uint64_t
             t->bits_cap = words;
             t->W = w_new;
         }
-        const uint64_t wneed = gbpe_div_up(w_new, SP_WPW_MIN) + 2;   // one byte counter per k_body workgroup
+        // one byte counter per k_body workgroup (at most body_cap of them: body_grid) + the zone's
+        const uint64_t wneed = std::max<uint64_t>(gbpe_div_up(w_new, SP_WPW_MIN), t->body_cap) + 2;
         if (t->wg_bytes && wneed > t->wg_cap) {
             uint64_t* nb = nullptr;
             TR_HIP(t, pool_malloc(t->ctx, &nb, wneed * sizeof(uint64_t)));
@@ -1111,7 +1115,7 @@ int sp_init_states(gbpe_trainer* t, uint64_t cap, uint32_t Zs, uint32_t z, uint3
     TR_HIP(t, hipMemcpyAsync(&t->st->zlast, &t->h_st->zlast, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     TR_HIP(t, hipMemcpyAsync(&t->st->is_last, &t->h_st->is_last, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     {   // one byte counter per k_body workgroup, kept across entries (summed by gbpe_trainer_stats_get)
-        const uint64_t need = gbpe_div_up(gbpe_div_up(cap, 32), SP_WPW_MIN) + 2;
+        const uint64_t need = std::max<uint64_t>(gbpe_div_up(gbpe_div_up(cap, 32), SP_WPW_MIN), t->body_cap) + 2;
         if (need > t->wg_cap) {
             uint64_t* nb = nullptr;
             TR_HIP(t, pool_malloc(t->ctx, &nb, need * sizeof(uint64_t)));
