@@ -351,7 +351,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         const uint32_t zn = (uint32_t)t->n - hs->B;   // zone length (it only shrinks within a step)
         const uint64_t zt = gbpe_div_up(zn, TILE);
         const uint32_t z256 = t->u16 ? zone_max<uint16_t>(256) : zone_max<uint32_t>(256);
-        sg.bt = zn <= z256 ? 256 : 1024;   // small zone: the low-latency 256-thread workgroups
+        sg.bt = zn <= std::min<uint32_t>(z256, t->z256) ? 256 : 1024;   // small zone: the low-latency 256-thread workgroups
         body_grid(t, sg.bt, &sg.body, &sg.wpg, 0, &sg.sub);
         if (sg.bt == 1024 && t->u16 && zn <= 16384u && t->zone16) sg.bt = 1023;
         sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt)) ? 1u : 0u;
