@@ -277,6 +277,26 @@ __device__ __forceinline__ uint32_t body_sector(S* __restrict__ p, uint32_t* __r
     return removed;
 }
 
+// dst[i - beg] = src[i] for i in [beg, end), thread-strided, U loads in flight per
+// thread: a one-load-per-trip loop waits a whole round trip per trip (the zone
+// passes' window-source copies: ~3-11 trips per thread, on the zone's chain)
+template <typename S, int BT, int U = 4>
+__device__ __forceinline__ void copy_strided(S* __restrict__ dst, const S* __restrict__ src, uint32_t beg, uint32_t end) {
+    for (uint32_t i0 = beg + threadIdx.x; i0 < end; i0 += (uint32_t)BT * U) {
+        S v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * BT;
+            v[u] = i < end ? src[i] : (S)0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * BT;
+            if (i < end) dst[i - beg] = v[u];
+        }
+    }
+}
+
 // Single-workgroup zone pass (zone <= ZMAX symbols): k_delta + k_compact<ZONE>
 // in one workgroup.  Each thread holds 32 consecutive zone symbols in registers
 // and builds k_delta's branch-free site masks; only positions next to a site or
@@ -337,10 +357,8 @@ __device__ __forceinline__ void zone_one(DevState* st, DevState* zst, const DevS
 #pragma unroll
         for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
     }
-    if (!EXACT) {   // window source: global n - 2mc in the previous stream
-        const uint64_t src0 = win_src0(gs, mc);
-        for (uint32_t u = t; u < mc; u += BT) L.wb[u] = zo[src0 + u];
-    }
+    if (!EXACT)   // window source: global n - 2mc in the previous stream
+        copy_strided<S, BT, 8>(L.wb, zo + win_src0(gs, mc), 0u, mc);
     if (t == 0) L.tf = BT;
     if (!zout) lds_clear(lt);
     __syncthreads();
@@ -548,10 +566,8 @@ __device__ __forceinline__ void zone_seg(DevState* st, DevState* zst, const DevS
     // this segment's share of the window source (+ the symbol before it) into LDS
     const uint32_t lw = (mc + nz - 1) / nz, q0 = seg * lw, q1 = q0 + lw < mc ? q0 + lw : mc;   // source [q0, q1)
     const uint64_t src0 = win_src0(gs, mc);
-    if (!EXACT && q0 < q1) {
-        const uint32_t f = q0 ? q0 - 1u : 0u;   // L.wb[j] = source[f + j]
-        for (uint32_t q = f + t; q < q1; q += BT) L.wb[q - f] = zo[src0 + q];
-    }
+    if (!EXACT && q0 < q1)   // L.wb[j] = source[f + j], f = q0 - 1 (or 0)
+        copy_strided<S, BT>(L.wb, zo + src0, q0 ? q0 - 1u : 0u, q1);
     lds_clear(lt);
     __syncthreads();
     if (t == 0) KT(2);
