@@ -911,7 +911,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     const uint32_t bid = blockIdx.x - zone1;
     if constexpr (ZSEG) {
         if (blockIdx.x < zone1) {
-            zone_seg<S, EXACT, BT, KB_LT, 16>(st, zst, *gs, *zs, zcur, (S*)zoth, zg, zone1, u.z, lt, dtb, a, b, nw, mc,
+            zone_seg<S, EXACT, BT, KB_LT, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, zg, zone1, u.z, lt, dtb, a, b, nw, mc,
                                              wg_bytes + nbody, round);
             if (t == 0) {
                 KT(5);

@@ -357,8 +357,10 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt)) ? 1u : 0u;
         // a zone of 16K-1M symbols: 16K-symbol segments inside k_body (its ZSEG form)
         const uint32_t zs_lo = t->zseg_mode == 2 ? (t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024)) : 16384u;
-        if (t->zseg_mode && t->zseg && zn > zs_lo && zn <= NSEG_MAX * 16384u)
-            sg.zone1 = (uint32_t)gbpe_div_up(zn, 16384u);
+        if (t->zseg_mode && t->zseg && zn > zs_lo && zn <= NSEG_MAX * 16384u) {
+            sg.seg8 = t->seg8 && zn <= NSEG_MAX * 8192u;
+            sg.zone1 = (uint32_t)gbpe_div_up(zn, sg.seg8 ? 8192u : 16384u);
+        }
         sg.copy = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u : grid_persistent(t->ctx, gbpe_div_up(zn / 5 + 1, TPB * 8), 1);
         sg.zdelta = (uint32_t)(zt ? zt : 1);
         sg.ztail = (t->flags & GBPE_TRAIN_EXACT_COMPACTION) ? 0u

@@ -96,6 +96,7 @@ struct gbpe_trainer {
     uint32_t* d_bhist = nullptr; // byte-pair histogram of the first count (65,536 u32)
     uint32_t count_bytes_on = 1; // first count by the byte-pair histogram (0: hashed k_count_full)
     uint32_t lx_size_on = 1;     // word table sized from a sampled distinct count (0: from the word count)
+    uint32_t seg8 = 1;           // zone segments of 8K symbols for zones <= 512K (GBPE_DEBUG seg8; 0: 16K)
     uint32_t z256 = 0xFFFFFFFFu; // largest zone for the 256-thread k_body form (GBPE_DEBUG z256; 0: always 1024)
     uint32_t body_sub = 4;       // most k_body workgroups per bitmap word (1, 2, 4; GBPE_DEBUG bsub;
                                  // C1 13.5 -> 11.9 ms at 4, profiles/r5/s21)
@@ -358,6 +359,7 @@ struct SpGrid {
     uint32_t body, copy, zdelta, zcompact, refresh;
     uint32_t wpg = 16;    // bitmap words per k_body workgroup
     uint32_t sub = 1;     // k_body workgroups per bitmap word (wpg = 1)
+    bool seg8 = false;    // zone segments of 8K symbols (1024 threads x 8), else 16K
     uint32_t ztail = 0;   // stale-tail slice blocks of the multi-tile zone k_delta
     uint32_t zone1;   // zone workgroups inside k_body: 1 = zone_one, >= 2 = zone_seg segments, 0 = multi-tile passes
     int bt;       // k_body workgroup size (256 or 1024)
@@ -407,6 +409,8 @@ template <typename S, bool EXACT, typename... A>
 void launch_body(int bt, uint32_t grid, hipStream_t s, A... args) {
     if (bt == 2048)   // zone segments inside k_body (the ZSEG form, 1024 threads)
         hipLaunchKernelGGL((k_body<S, EXACT, 1024, 16, true>), dim3(grid), dim3(1024), 0, s, args...);
+    else if (bt == 2049)   // ... with 8K-symbol segments (zones <= 512K)
+        hipLaunchKernelGGL((k_body<S, EXACT, 1024, 8, true>), dim3(grid), dim3(1024), 0, s, args...);
     else if (bt == 1023 && sizeof(S) == 2)
         hipLaunchKernelGGL((k_body<S, EXACT, 1024, 16>), dim3(grid), dim3(1024), 0, s, args...);
     else if (bt >= 1023)
@@ -426,7 +430,7 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const bool inbody = g.zone1 >= 2;
     const uint32_t gb = g.body + (g.zone1 ? g.zone1 : g.copy);
     const uint32_t z1 = g.zone1;   // k_body's own zone workgroups
-    const int bt = inbody ? 2048 : g.bt;
+    const int bt = inbody ? (g.seg8 ? 2049 : 2048) : g.bt;
     SelShard sh = sel_single(t);
     sh.sub = g.sub;
     if ((uint64_t)g.body + 1 > t->wg_cap)   // k_body's per-workgroup byte counters (and the zone's after them)
@@ -1347,7 +1351,8 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->max_id = (uint32_t)(max_id < 0x10000ull ? max_id : 0x10000ull);
     t->body_cap = (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);
     t->body_cap = (uint32_t)std::max<long>(1, gbpe_debug_knob("bcap", t->body_cap));
-    t->z256 = (uint32_t)gbpe_debug_knob("z256", t->z256);   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
+    t->z256 = (uint32_t)gbpe_debug_knob("z256", t->z256);
+    t->seg8 = (uint32_t)gbpe_debug_knob("seg8", t->seg8);   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
     // test overrides (GBPE_DEBUG): the lexicon off / its build check, the
     // in-loop table growth off, the multi-tile k_delta threshold, the zone target
     t->lex_on = gbpe_debug_knob("lexicon", 1) != 0;
