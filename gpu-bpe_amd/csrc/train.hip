@@ -356,7 +356,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
         if (sg.bt == 1024 && t->u16 && zn <= 16384u && t->zone16) sg.bt = 1023;
         sg.zone1 = zn <= (t->u16 ? zone_max<uint16_t>(sg.bt) : zone_max<uint32_t>(sg.bt)) ? 1u : 0u;
         // a zone of 16K-1M symbols: 16K-symbol segments inside k_body (its ZSEG form)
-        const uint32_t zs_lo = t->zseg_mode == 2 ? (t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024)) : 16384u;
+        const uint32_t zs_lo = t->zseg_mode == 2 ? (t->u16 ? zone_max<uint16_t>(1024) : zone_max<uint32_t>(1024)) : t->zseg_lo;
         if (t->zseg_mode && t->zseg && zn > zs_lo && zn <= NSEG_MAX * 16384u) {
             sg.seg8 = t->seg8 && zn <= NSEG_MAX * 8192u;
             sg.zone1 = (uint32_t)gbpe_div_up(zn, sg.seg8 ? 8192u : 16384u);

@@ -97,6 +97,8 @@ struct gbpe_trainer {
     uint32_t count_bytes_on = 1; // first count by the byte-pair histogram (0: hashed k_count_full)
     uint32_t lx_size_on = 1;     // word table sized from a sampled distinct count (0: from the word count)
     uint32_t seg8 = 1;           // zone segments of 8K symbols for zones <= 512K (GBPE_DEBUG seg8; 0: 16K)
+    uint32_t zseg_lo = 8192;     // zones above this many symbols run as zone segments (GBPE_DEBUG zslo; 16384
+                                 // = round 4: 1 GiB 0.557 vs 0.548 s, C2 equal, C1 11.6 vs 11.8 ms, profiles/r5/s30)
     uint32_t z256 = 0xFFFFFFFFu; // largest zone for the 256-thread k_body form (GBPE_DEBUG z256; 0: always 1024)
     uint32_t body_sub = 4;       // most k_body workgroups per bitmap word (1, 2, 4; GBPE_DEBUG bsub;
                                  // C1 13.5 -> 11.9 ms at 4, profiles/r5/s21)
@@ -1352,7 +1354,8 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->body_cap = (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);
     t->body_cap = (uint32_t)std::max<long>(1, gbpe_debug_knob("bcap", t->body_cap));
     t->z256 = (uint32_t)gbpe_debug_knob("z256", t->z256);
-    t->seg8 = (uint32_t)gbpe_debug_knob("seg8", t->seg8);   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
+    t->seg8 = (uint32_t)gbpe_debug_knob("seg8", t->seg8);
+    t->zseg_lo = (uint32_t)std::max<long>(8192, gbpe_debug_knob("zslo", t->zseg_lo));   // one per CU: measured best at 1 GiB (128/192/256/384/512/1024: 3.01/2.42/2.14/2.66/2.45/2.98 s)
     // test overrides (GBPE_DEBUG): the lexicon off / its build check, the
     // in-loop table growth off, the multi-tile k_delta threshold, the zone target
     t->lex_on = gbpe_debug_knob("lexicon", 1) != 0;
