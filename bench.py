@@ -17,6 +17,8 @@ Secondary legs (same JSON line):
     with a 32K vocab trained on a 100 MiB sample (seed 4);
   * c4_shard: C4's rank-0 shard (1 GiB multilingual, seed 5) trained alone at
     C4's 64K vocab, u32 symbols, run to the 0xFFFF id stop (configs[3] per rank);
+  * ml1g: the metric's "1 GiB UTF-8 @ 32K" on multi-byte text: 1 GiB
+    multilingual (seed 3) at 32K vocab, against its fixture;
   * c5: configs[4], 1 GiB code at 50K vocab with GPT-4 rule word starts
     computed on the device (u32 symbols); both against their oracle fixtures;
   * cpu_baseline: the reference algorithm restated on the CPU
@@ -74,8 +76,9 @@ TILE_SYMS = 8192
 METRIC = "BPE merges/sec + tokenize GB/s, 1 GiB UTF-8 @ 32K vocab, 1/2/4/8 MI355X"
 HEADLINE = {"gen": "english", "n": 1 << 30, "seed": 2, "fancy_punct": 0.005}
 C2 = {"gen": "english", "n": 104_857_600, "seed": 2, "fancy_punct": 0.005}
-PMC_FILE = os.path.join(ROOT, "profiles", "r5", "close", "pmc_kbody.json")
-ROCPROF_EN1G = os.path.join(ROOT, "profiles", "r5", "close", "en1g_kernel_stats.csv")
+PMC_FILE = os.path.join(ROOT, "profiles", "r6", "pmc_kbody.json")
+ROCPROF_EN1G = os.path.join(ROOT, "profiles", "r6", "en1g_kernel_stats.csv")
+ENC_PMC_FILE = os.path.join(ROOT, "profiles", "r6", "pmc_encode.json")
 CAL_NOTE = ("FETCH_SIZE x2: tools/micro/fetch_cal.hip measured 64 counter bytes per distinct 128-B line for "
             "16-B streaming reads and 4-, 8- and 16-B one-per-line gathers alike (profiles/r3_fetch_calibration.json), "
             "so every read line moves 128 B; WRITE_SIZE counts 32-B granules (4-B scattered stores and atomics: 32 B "
@@ -251,13 +254,15 @@ def train_detail(st, sk):
         "stream_bytes": int(st.stream_bytes_moved), "tail_dropped": int(st.tail_dropped),
         "max_live_pairs": int(st.max_live_pairs), "table_slots": int(st.table_slots),
         "sparse": {"merges": int(st.sparse_merges), "enters": int(st.sparse_enters), "exits": int(st.sparse_exits),
-                   "sectors": int(st.sparse_sectors), "zone_at_entry": int(st.sparse_zone)},
+                   "sectors": int(st.sparse_sectors), "zone_at_entry": int(st.sparse_zone),
+                   "paired_merges": int(getattr(st, "paired_merges", 0))},
         "ms_create": round(st.ms_create, 3),
         "run_s": getattr(st, "run_s", None),
         "events": None if sk is None else {
             "merges": int(sk.timed_merges), "dense_merges": int(sk.timed_merges - sk.sparse_merges),
             "dense_bytes": int(sk.dense_bytes), "ms_dense": sk.ms_dense,
-            "sparse_merges": int(sk.sparse_merges), "body_bytes": int(sk.body_bytes), "zone_bytes": int(sk.zone_bytes),
+            "sparse_merges": int(sk.sparse_merges), "paired_merges": int(getattr(sk, "paired_merges", 0)),
+            "body_bytes": int(sk.body_bytes), "zone_bytes": int(sk.zone_bytes),
             "ms_body": sk.ms_body, "ms_sparse": sk.ms_sparse, "ms_select": sk.ms_select, "ms_refresh": sk.ms_other,
             "ms_delta": sk.ms_delta, "ms_compact": sk.ms_compact},
     }
@@ -316,8 +321,10 @@ def train_roofline(det, wall_per_run):
                                  "times are slightly inflated")
         return k
 
-    body = kern("body", ev["body_bytes"], ev["ms_body"], ev["sparse_merges"], ev["sparse_merges"], "k_body<",
-                "k_body (sector-sparse merge pass over the word lexicon, one launch per merge)") if ev else None
+    body = kern("body", ev["body_bytes"], ev["ms_body"], ev["sparse_merges"] - ev.get("paired_merges", 0),
+                ev["sparse_merges"], "k_body<",
+                "k_body (sector-sparse merge pass over the word lexicon, one launch per merge or two: paired "
+                "launches, DESIGN §2f)") if ev else None
     cand = [k for k in (body,) if k]
     roof = max(cand, key=lambda k: k["ms_per_run"]) if cand else {
         "bound": "hbm", "kernel": None, "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None,
@@ -409,8 +416,10 @@ def headline_leg(args, lib, ctx, dist):
         "value": round(total / (wall - st.create_s_total), 1), "unit": "merges/s",
         "create_ms_per_run": round(1e3 * st.create_s_total / max(1, args.steps), 3),
         "definition": "the reference's merges/s = merges / t_loop (trainer.js:230, 291-292, 324-326): the timed "
-                      "wall minus trainer creation (symbols, word starts, first count), which t_loop excludes; "
-                      "`value` keeps creation inside"}
+                      "wall minus trainer creation (symbols, word starts and the first pair count); t_loop excludes "
+                      "the symbols and word starts but includes the first count (every reference merge recounts, "
+                      "training-pipeline.js:190), so this rate is an upper bound of the reference definition by the "
+                      "first count's share of create_ms_per_run (~1.2 ms); `value` keeps all of creation inside"}
     done, late_m, late_s = 0, 0, 0.0
     for m, sec in steps:
         if done >= 16384:
@@ -607,10 +616,10 @@ def encode_leg(args, lib, ctx, dist, rank):
                      "frac": round(alg / 1e9 / (k_all / 1e3) / HBM_PEAK_GBPS, 4), "algorithmic_bytes": alg,
                      "traffic": None},
     }
-    pmc = os.path.join(ROOT, "profiles", "r3_pmc_encode.json")
+    pmc = ENC_PMC_FILE
     if os.path.exists(pmc):
         p = json.load(open(pmc))
-        if p.get("workload") == "c3-1g" and p.get("chunk_size") == cs:
+        if p.get("workload") == "c3-1g" and p.get("chunk_size", cs) == cs:
             res["roofline"]["traffic"] = round(p["hbm_bytes_per_encode"])
             res["roofline"]["traffic_unit"] = "bytes/encode (all encode kernels)"
             res["roofline"]["traffic_over_algorithmic"] = round(p["hbm_bytes_per_encode"] / alg, 4)
@@ -703,6 +712,15 @@ def single_line(args, lib, ctx, dist, rank):
             "C4 rank-0 shard alone: 64K-vocab train on 1,073,741,824 B multilingual UTF-8 (seed 5; C4 = 8 such "
             "shards, seed 5 + rank), u32 symbols, run to the 0xFFFF id stop")
         del shard
+    if not args.no_ml1g:   # the metric's "1 GiB UTF-8" on multi-byte text
+        t = time.time()
+        ml = make_corpus({"gen": "multilingual", "n": 1 << 30, "seed": 3})
+        log(f"[bench] ml1g corpus {len(ml)} B generated in {time.time() - t:.1f}s")
+        line["ml1g"] = config_leg(
+            args, lib, ctx, dist, "ml1g", ml, 32768, 0,
+            "ml1g: 32K-vocab train on 1,073,741,824 B multilingual UTF-8 (seed 3: Latin/English, Turkish, Cyrillic, "
+            "CJK, Arabic, emoji paragraphs), heuristic word boundaries, u16 symbols", runs=max(2, args.steps // 2))
+        del ml
     if not args.no_c5:
         from gpubpe import _lib
         t = time.time()
@@ -1102,6 +1120,7 @@ def main():
     ap.add_argument("--no-c2", action="store_true")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 per-rank shard leg (64K vocab)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 leg (1 GiB code, 50K vocab, GPT-4 rules)")
+    ap.add_argument("--no-ml1g", action="store_true", help="skip the 1 GiB multilingual @ 32K training leg")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP-event roofline run")
     ap.add_argument("--cpu-merges", type=int, default=0, help="CPU baseline merges on the CPU share (0 = 24)")
     ap.add_argument("--replicated", action="store_true",

@@ -327,10 +327,12 @@ __device__ __forceinline__ uint32_t lane_mask_n(uint64_t i0, uint64_t lim, int n
     return i0 >= lim ? 0u : (i0 + n <= lim ? full : ((1u << (uint32_t)(lim - i0)) - 1u));
 }
 
-// zout (the persistent tail loop, k_tail): the delta table is shared with the body
-// pass (neither cleared nor flushed here) and m, the new zone length go to zout[0..1]
+// z: the zone's length, wsrc: the stale-window source's offset in the other buffer
+// (launch snapshots: no state round trip before the zone loads).
+// zout: the delta table is the caller's (neither cleared nor flushed here) and m,
+// the new zone length go to zout[0..1]
 template <typename S, bool EXACT, int BT, int NT = LTAB_T, int ZPT_ = ZoneDim<S, BT>::ZPT, typename TB = Table>
-__device__ __forceinline__ void zone_one(DevState* st, DevState* zst, const DevState& gs, const DevState& zs, S* __restrict__ zc,
+__device__ __forceinline__ void zone_one(DevState* st, DevState* zst, uint32_t z, uint64_t wsrc, S* __restrict__ zc,
                          S* __restrict__ zo, ZoneLds<S, BT>& L,
                          LdsTab<NT>& lt, const TB& tb, uint32_t a, uint32_t b, uint32_t nw, uint32_t mc,
                          uint64_t* __restrict__ bytes, uint32_t round, uint32_t* zout = nullptr) {
@@ -340,7 +342,6 @@ __device__ __forceinline__ void zone_one(DevState* st, DevState* zst, const DevS
     static_assert(ZPT <= ZoneDim<S, BT>::ZPT && ZPT * sizeof(S) % 16 == 0, "zone positions per thread");
     constexpr int V = ZPT * sizeof(S) / 16;  // 16-byte vectors per thread
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const uint32_t z = zs.n;   // launch snapshots (LDS): no state round trip before the zone loads
     const uint32_t lim = EXACT ? z : z - mc;
     const uint32_t pid_ab = (a << 16) | b;
     const uint32_t i0 = (uint32_t)t * ZPT;
@@ -358,7 +359,7 @@ __device__ __forceinline__ void zone_one(DevState* st, DevState* zst, const DevS
         for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
     }
     if (!EXACT)   // window source: global n - 2mc in the previous stream
-        copy_strided<S, BT, 8>(L.wb, zo + win_src0(gs, mc), 0u, mc);
+        copy_strided<S, BT, 8>(L.wb, zo + wsrc, 0u, mc);
     if (t == 0) L.tf = BT;
     if (!zout) lds_clear(lt);
     __syncthreads();
@@ -380,11 +381,15 @@ __device__ __forceinline__ void zone_one(DevState* st, DevState* zst, const DevS
     const uint32_t surv = inb & ~hitm, keep = surv & below;
     const uint32_t rwm = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
     uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
-    for (uint32_t i = (lim > 1u ? lim : 1u) + t; i < z; i += BT) {   // stale tail: old pairs destroyed
-        const uint32_t xi = xs[i];
-        if (xi & WS) continue;
-        const uint32_t tp = xs[i - 1] & TM, ti = xi & TM;
-        if (tp && ti && ((tp << 16) | ti) != pid_ab) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+    for (uint32_t ib = (lim > 1u ? lim : 1u) + t; ib < z; ib += 4u * BT) {   // stale tail: old pairs destroyed
+        uint32_t kq[4];   // (4 pairs' reads and CASes overlap: lds_addk)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = ib + (uint32_t)k * BT;
+            const uint32_t xi = i < z ? (uint32_t)xs[i] : WS, tp = i < z ? (uint32_t)xs[i - 1] & TM : 0u, ti = xi & TM;
+            kq[k] = (!(xi & WS) && tp && ti && ((tp << 16) | ti) != pid_ab) ? (tp << 16) | ti : 0u;
+        }
+        lds_addk<4>(lt, tb, st, kq, 0xFFFFFFFFu);
     }
     while (rel) {
         const int k = __ffs(rel) - 1;
@@ -470,12 +475,21 @@ __device__ __forceinline__ void zone_one(DevState* st, DevState* zst, const DevS
     if (!EXACT && m) {
         __syncthreads();
         const uint32_t woff = mc - m;
-        for (uint32_t j = t; j < m; j += BT) {
-            const uint32_t x1 = L.wb[woff + j];
-            // left of the window: the last kept survivor (Kz > 0: the zone holds >= 5 mc)
-            const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : (Kz ? (uint32_t)xs[swz(Kz - 1)] : 0u);
-            xs[swz(Kz + j)] = (S)x1;
-            if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) lds_add(lt, tb, st, ((x0 & TM) << 16) | (x1 & TM), 1u);
+        for (uint32_t jb = t; jb < m; jb += 4u * BT) {
+            uint32_t kq[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t j = jb + (uint32_t)k * BT;
+                kq[k] = 0u;
+                if (j < m) {
+                    const uint32_t x1 = L.wb[woff + j];
+                    // left of the window: the last kept survivor (Kz > 0: the zone holds >= 5 mc)
+                    const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : (Kz ? (uint32_t)xs[swz(Kz - 1)] : 0u);
+                    xs[swz(Kz + j)] = (S)x1;
+                    if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) kq[k] = ((x0 & TM) << 16) | (x1 & TM);
+                }
+            }
+            lds_addk<4>(lt, tb, st, kq, 1u);
         }
     }
     __syncthreads();
@@ -743,41 +757,58 @@ __device__ __forceinline__ void zone_seg(DevState* st, DevState* zst, const DevS
 struct SelShard {
     uint32_t zf = 3;         // zone rule: z >= max(2 mc + mc_prev, zf mc) + 2 (trainer zone_f)
     uint32_t sub = 1;        // k_body workgroups per bitmap word (1, 2, 4: a row of few words, body_grid)
+    uint32_t k2 = 0;         // paired launches allowed (the zone_one form: zone_two)
+};
+
+// The second merge of a paired launch.  With P1 > P2 the table's two
+// largest keys and P2's tokens disjoint from P1's, merging P1 leaves P2's count as
+// it is and every pair it creates is bounded by a pair other than P1 and P2 that
+// loses to P2 (on equal counts too: the new id is larger than every token), so P2
+// is the argmax after P1 — up to the stale window the reference compaction adds,
+// which zone_two checks before the second merge runs (ref mode).
+struct Sel2 {
+    uint32_t a = 0, b = 0, mc = 0;
+    bool dbl = false;        // candidate (zone_two decides in ref mode; exact mode always runs it)
 };
 
 template <int BT>
 __device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
-                           uint32_t round, bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
+                           bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
                            uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc,
-                           const DevState*& gsnap, const DevState*& zsnap, const SelShard sh = SelShard(),
-                           bool commit = true) {
-    __shared__ uint64_t s_red[BT / 64];
+                           uint32_t& md, Sel2& s2, const DevState*& gsnap, const DevState*& zsnap,
+                           const SelShard sh = SelShard(), bool commit = true) {
+    __shared__ uint64_t s_red[BT / 64], s_red2[BT / 64];
     constexpr int NW = sizeof(DevState) / 4;
     __shared__ union {
         DevState d;
         uint32_t w[NW];
     } s_g, s_z;
     const int t = threadIdx.x;
-    // the partial maxima and snapshots of both states load together (one round
-    // trip, not one per field)
+    // the partial maxima (two keys per k_refresh workgroup, one 16-byte load) and
+    // snapshots of both states load together (one round trip, not one per field)
     if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
     else if (zst && t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
-    uint64_t best = 0;
+    uint64_t best = 0, second = 0;
     for (uint32_t i = t; i < npart; i += BT) {
-        const uint64_t v = part[i];
-        best = v > best ? v : best;
+        const ulonglong2 v = reinterpret_cast<const ulonglong2*>(part)[i];
+        top2_merge(best, second, v.x, v.y);
     }
     __syncthreads();
     const DevState& g = s_g.d;
     gsnap = &s_g.d;
     zsnap = &s_z.d;
-    if (!(round < g.budget && g.merges_done == round && !g.stop && !g.sp_abort)) return false;
-    best = wave_max_u64(best);
-    if ((t & 63) == 0) s_red[t >> 6] = best;
+    md = g.merges_done;   // the merge index (a paired launch runs two: launches and merges part ways)
+    if (!(md < g.budget && !g.stop && !g.sp_abort)) return false;
+    wave_top2_u64(best, second, best, second);
+    if ((t & 63) == 0) {
+        s_red[t >> 6] = best;
+        s_red2[t >> 6] = second;
+    }
     __syncthreads();
     best = s_red[0];
+    second = s_red2[0];
 #pragma unroll
-    for (int w = 1; w < BT / 64; ++w) best = s_red[w] > best ? s_red[w] : best;
+    for (int w = 1; w < BT / 64; ++w) top2_merge(best, second, s_red[w], s_red2[w]);
     mc = (uint32_t)(best >> 32);
     const uint32_t pid = ~(uint32_t)best;
     a = pid >> 16;
@@ -792,6 +823,17 @@ __device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const ui
     const uint64_t zneed = std::max<uint64_t>(2ull * mc + mc_prev, (uint64_t)sh.zf * mc) + 2u;
     const bool abort = !stop && !bad && !exact && (uint64_t)g.zlast < zneed;
     const bool go = !stop && !bad && !abort;
+    {   // the second merge: P2 disjoint from P1, its own stop rules, and the zone rule on the
+        // zone the first leaves (>= z - mc) with mc as its mc_prev
+        const uint32_t mc2 = (uint32_t)(second >> 32), pid2 = ~(uint32_t)second;
+        const uint32_t a2 = pid2 >> 16, b2 = pid2 & 0xFFFFu;
+        const uint64_t zneed2 = (uint64_t)mc + std::max<uint64_t>(2ull * mc2 + mc, (uint64_t)sh.zf * mc2) + 2u;
+        s2.a = a2;
+        s2.b = b2;
+        s2.mc = mc2;
+        s2.dbl = sh.k2 && zone1 && go && md + 2u <= g.budget && mc2 >= 2u && nw + 1u <= 0xFFFFu && a2 != a &&
+                 a2 != b && b2 != a && b2 != b && (exact || (uint64_t)g.zlast >= zneed2);
+    }
     // the LAST workgroup commits: block 0 is the zone pass (the launch's longest
     // chain), which then starts without the table probe and the state stores
     if (commit && blockIdx.x == gridDim.x - 1u) {
@@ -813,10 +855,17 @@ __device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const ui
                     atomicSub(&tb.slots[idx].y, mc);
                     tb.dirty[idx >> BLK_LOG2] = 1u;
                 }
-                log[round * 4 + 0] = a;
-                log[round * 4 + 1] = b;
-                log[round * 4 + 2] = nw;
-                log[round * 4 + 3] = mc;
+                log[md * 4 + 0] = a;
+                log[md * 4 + 1] = b;
+                log[md * 4 + 2] = nw;
+                log[md * 4 + 3] = mc;
+                if (s2.dbl) {   // (k_refresh keeps it only if the zone workgroup accepts it)
+                    log[md * 4 + 4] = s2.a;
+                    log[md * 4 + 5] = s2.b;
+                    log[md * 4 + 6] = nw + 1u;
+                    log[md * 4 + 7] = s2.mc;
+                    st->mc2 = s2.mc;
+                }
                 st->a = a;
                 st->b = b;
                 st->nw = nw;
@@ -831,8 +880,8 @@ __device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const ui
                     zst->m = 0u;
                     zst->valid_total = 0u;
                 }
-                zst->merges_done = round + 1u;
-                st->sel_round = round + 1u;
+                zst->merges_done = md + 1u;
+                st->sel_round = md + 1u;
             }
         }
         if (go) {   // group sums of a multi-tile zone pass start at zero
@@ -841,6 +890,374 @@ __device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const ui
         }
     }
     return go;
+}
+
+// the paired launch's verdict word (ZSegState pad[1], never zeroed): the launch's
+// epoch << 2 | 2 (decided) | 1 (accepted)
+__device__ __forceinline__ uint32_t* pair_word(ZSegState* zg) { return &zg->pad[1]; }
+
+// Zone workgroup of a paired launch: both merges in one pass over the
+// zone — one load, the first merge's new zone assembled in LDS, the verdict, the
+// second merge on that LDS copy, one store of each zone buffer and one flush.
+//  * The second merge's stale window comes from the first merge's current buffer
+//    with the first's A-side rewrites in place (the reference's ping-pong): those
+//    symbols, [z - mc - 2 mc2, + mc2) of the loaded zone, are staged in wb2 with the
+//    rewrites applied before the LDS copy is overwritten.
+//  * Ref mode verdict: the stale window (and the tail it replaces) may lift a pair
+//    over P2 or change P2's count.  Every zone delta of merge 1 is in the table (an
+//    overflow rejects): P2 must have none, and every pair with a positive delta that
+//    holds no nw must stay below P2 with its count read now (the body workgroups'
+//    adds to such pairs are decrements, so the read bounds the final count from
+//    above).  Pairs of nw come from sites (bounded, Sel2) — except the window's
+//    first pair (s_rej).
+//  * zo ends as the first merge's output with the second's A-side rewrites (a later
+//    window reads it), zc as the second's output.  Rejected: the first merge's
+//    output goes to zo and its rewrites to zc, as zone_one leaves them.
+template <typename S, bool EXACT, int BT, int NT, int ZPT>
+__device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevState& gs, uint32_t z, S* __restrict__ zc,
+                                         S* __restrict__ zo, ZSegState* zg, ZoneLds<S, BT>& L, S* __restrict__ wb2,
+                                         LdsTab<NT>& ltab, const Table& tb, uint32_t a, uint32_t b, uint32_t nw,
+                                         uint32_t mc, const Sel2& s2, uint64_t* __restrict__ bytes, uint32_t round) {
+    (void)round;   // phase stamps only (-DGBPE_KTRACE: 2 loaded, 3 merge-1 deltas, 7 merge 1 in LDS, 8 verdict,
+                   // 9 merge 2 in LDS, 4 stored; the caller stamps 5 after the flush)
+    constexpr uint32_t WS = Sym<S>::WS, TM = Sym<S>::TM;
+    static_assert(ZPT == ZoneDim<S, BT>::ZPT && ZPT * sizeof(S) % 16 == 0, "zone positions per thread");
+    constexpr int V = ZPT * sizeof(S) / 16;
+    constexpr uint32_t PV = 16 / sizeof(S), PVL = sizeof(S) == 2 ? 3 : 2;
+    constexpr int MAXPER = NT / BT;
+    static_assert(MAXPER * BT == NT && MAXPER <= 16, "delta table slots per thread");
+    auto swz = [](uint32_t o) -> uint32_t {   // 16-byte chunks XOR-swizzled in groups of 8 (zone_one)
+        const uint32_t c = o >> PVL;
+        return ((c ^ ((c >> 3) & 7u)) << PVL) | (o & (PV - 1u));
+    };
+    __shared__ uint32_t s_rej;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t a2 = s2.a, b2 = s2.b, n2 = nw + 1u, mc2 = s2.mc;
+    const uint32_t pid1 = (a << 16) | b, pid2 = (a2 << 16) | b2;
+    // both merges' tails and windows are <= 2 (mc + mc2) pairs: a table at <= ~1/2 load
+    uint32_t nslot = 1024u;
+    while (nslot < (uint32_t)NT && nslot < 4u * (mc + mc2)) nslot <<= 1;
+    LdsView lt = lds_view(ltab, nslot);
+    lds_clear(lt);
+    if (t == 0) s_rej = 0u;
+    // P2's home slot for its commit, loaded while merge 1 runs
+    const uint32_t h2i = gbpe_fmix32(pid2) & tb.mask;
+    uint64_t h2 = 0;
+    if (t == 0)
+        h2 = __hip_atomic_load(reinterpret_cast<const uint64_t*>(&tb.slots[h2i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t i0 = (uint32_t)t * ZPT;
+    S* xs = reinterpret_cast<S*>(L.xv);
+    uint32_t x[ZPT];
+    {
+        uint4 v[V];
+        const uint4* src = reinterpret_cast<const uint4*>(zc + i0);   // zone buffers hold >= 2 tiles
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = src[k];
+#pragma unroll
+        for (int k = 0; k < V; ++k) L.xv[t * V + k] = v[k];
+        const S* e = reinterpret_cast<const S*>(v);
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) x[k] = i0 + k < z ? (uint32_t)e[k] : 0u;
+    }
+    if (!EXACT) copy_strided<S, BT, 8>(L.wb, zo + win_src0(gs, mc), 0u, mc);
+    __syncthreads();
+    if (t == 0) KT(2);
+    // ── merge 1: zone_one's site masks and deltas ──
+    uint32_t m = 0, Kz = 0, rwm = 0, wsm = 0;
+    {
+        const uint32_t lim = EXACT ? z : z - mc;
+        const uint32_t xm2 = i0 >= 2 ? (uint32_t)xs[i0 - 2] : 0u, xm1 = i0 >= 1 ? (uint32_t)xs[i0 - 1] : 0u;
+        const uint32_t nxr = i0 + ZPT < z ? (uint32_t)xs[i0 + ZPT] : 0u;
+        uint32_t eb = 0, ea = 0;
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) {
+            eb |= (x[k] == b ? 1u : 0u) << k;
+            ea |= ((x[k] & TM) == a ? 1u : 0u) << k;
+            wsm |= ((x[k] & WS) ? 1u : 0u) << k;
+        }
+        const uint32_t inb = lane_mask_n(i0, z, ZPT);
+        const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a ? 1u : 0u)) & inb;
+        const uint32_t h_m1 = (i0 >= 1 && i0 - 1 < z && xm1 == b && (xm2 & TM) == a) ? 1u : 0u;
+        const uint32_t h_32 = (nxr == b && (ea >> (ZPT - 1))) ? 1u : 0u;
+        const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (ZPT + 1));
+        const uint32_t below = lane_mask_n(i0, lim, ZPT);
+        const uint32_t surv = inb & ~hitm, keep = surv & below;
+        rwm = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
+        uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+        for (uint32_t ib = (lim > 1u ? lim : 1u) + t; ib < z; ib += 4u * BT) {   // stale tail: old pairs destroyed
+            uint32_t kq[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t i = ib + (uint32_t)k * BT;
+                const uint32_t xi = i < z ? (uint32_t)xs[i] : WS, tp = i < z ? (uint32_t)xs[i - 1] & TM : 0u, ti = xi & TM;
+                kq[k] = (!(xi & WS) && tp && ti && ((tp << 16) | ti) != pid1) ? (tp << 16) | ti : 0u;
+            }
+            lds_addk<4>(lt, tb, st, kq, 0xFFFFFFFFu);
+        }
+        if (t == 0) KT(10);
+        while (rel) {
+            const int k = __ffs(rel) - 1;
+            rel &= rel - 1;
+            const uint32_t i = i0 + k;
+            if (i == 0) continue;
+            const uint32_t xi = xs[i];
+            if (xi & WS) continue;
+            const uint32_t xp = xs[i - 1];
+            const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+            const uint32_t tp = xp & TM, ti = xi & TM;
+            if (tp && ti && ((tp << 16) | ti) != pid1) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+            if (!h0) {
+                if (hm) {
+                    const uint32_t t2 = hp ? nw : ti;
+                    if (t2) lds_add(lt, tb, st, (nw << 16) | t2, 1u);
+                } else if (hp && tp) {
+                    lds_add(lt, tb, st, (tp << 16) | nw, 1u);
+                }
+            }
+        }
+        if (t == 0) KT(11);
+        if (!EXACT) {   // the second merge's window source, with merge 1's A-side rewrites
+            const uint32_t w2 = z - mc - 2u * mc2;   // (>= 0: sel_inline's zone rule)
+            if (i0 < w2 + mc2 && i0 + ZPT > w2) {
+#pragma unroll
+                for (int k = 0; k < ZPT; ++k) {
+                    const uint32_t p = i0 + k;
+                    if (p >= w2 && p < w2 + mc2) wb2[p - w2] = (S)(((rwm >> k) & 1u) ? (nw | (x[k] & WS)) : x[k]);
+                }
+            }
+        }
+        const uint32_t kc = __popc(keep);
+        const uint32_t incl = wave_scan_incl_u32(kc), tl = wave_sum_u32(__popc(surv & ~below));
+        if (lane == 63) L.wsum[wid] = incl;
+        if (lane == 0) L.wtail[wid] = tl;
+        __syncthreads();
+        if (t == 0) KT(3);
+        uint32_t pre = incl - kc;
+#pragma unroll
+        for (int w2 = 0; w2 < BT / 64; ++w2) {
+            pre += w2 < wid ? L.wsum[w2] : 0u;
+            Kz += L.wsum[w2];
+            m += L.wtail[w2];
+        }
+        // the first merge's zone in LDS over the old copy (every read of it is done)
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) {
+            const uint32_t y = ((rwm >> k) & 1u) ? (nw | (x[k] & WS)) : x[k];
+            const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
+            S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
+            *dst = (S)y;
+        }
+        if (!EXACT && m) {
+            __syncthreads();
+            const uint32_t woff = mc - m;
+            for (uint32_t jb = t; jb < m; jb += 4u * BT) {
+                uint32_t kq[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t j = jb + (uint32_t)k * BT;
+                    kq[k] = 0u;
+                    if (j < m) {
+                        const uint32_t x1 = L.wb[woff + j];
+                        const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : (Kz ? (uint32_t)xs[swz(Kz - 1)] : 0u);
+                        if (!j && (x0 & TM) == nw) s_rej = 1u;   // a pair of the new token that no site made
+                        xs[swz(Kz + j)] = (S)x1;
+                        if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) kq[k] = ((x0 & TM) << 16) | (x1 & TM);
+                    }
+                }
+                lds_addk<4>(lt, tb, st, kq, 1u);
+            }
+        }
+        __syncthreads();
+    }
+    const uint32_t z1 = Kz + m;
+    if (t == 0) KT(7);
+    // ── the verdict ──
+    bool rej = false;
+    if (!EXACT) {
+        if (t == 0) rej = s_rej != 0u || *lt.ovf != 0u;
+        uint32_t q[MAXPER], d[MAXPER];
+        uint64_t hv[MAXPER];
+#pragma unroll
+        for (int k = 0; k < MAXPER; ++k) {   // every load first: one round trip
+            const uint32_t i = (uint32_t)t + (uint32_t)k * BT;
+            q[k] = i < nslot ? lt.key[i] : 0u;
+            d[k] = i < nslot ? lt.val[i] : 0u;
+            if (q[k] == pid2 && d[k]) rej = true;
+            const bool need = q[k] && (int32_t)d[k] > 0 && (q[k] >> 16) != nw && (q[k] & 0xFFFFu) != nw && q[k] != pid2;
+            if (!need) q[k] = 0u;
+            hv[k] = 0;
+            if (need && q[k] != pid1)   // (P1's own count is 0 after its commit)
+                hv[k] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(&tb.slots[gbpe_fmix32(q[k]) & tb.mask]),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int k = 0; k < MAXPER; ++k) {
+            if (!q[k]) continue;
+            uint32_t cnt = 0;
+            if (q[k] != pid1) {
+                if ((uint32_t)hv[k] == q[k]) {
+                    cnt = (uint32_t)(hv[k] >> 32);
+                } else {
+                    const uint32_t idx = table_find(tb, q[k]);
+                    cnt = idx == 0xFFFFFFFFu ? 0u : __hip_atomic_load(&tb.slots[idx].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if ((int32_t)cnt < 0) cnt = 0;
+            }
+            const uint64_t c2 = (uint64_t)cnt + d[k];
+            if (c2 > mc2 || (c2 == mc2 && q[k] < pid2)) rej = true;
+        }
+        rej = __syncthreads_or(rej) != 0;
+    }
+    if (t == 0) {
+        st->pair_cand += 1u;   // (diagnostics: one zone workgroup per launch)
+        if (rej) st->pair_rej += 1u;
+        if (!rej) {   // commit P2: every occurrence is a site of the second merge
+            const uint32_t idx = (uint32_t)h2 == pid2 ? h2i : table_find(tb, pid2);
+            if (idx == 0xFFFFFFFFu) {
+                atomicOr(&st->err, ERR_PAIR_MISSING);
+            } else {
+                atomicSub(&tb.slots[idx].y, mc2);
+                tb.dirty[idx >> BLK_LOG2] = 1u;
+            }
+            st->acc2 = 1u;
+        }
+        __hip_atomic_store(pair_word(zg), (gs.epoch << 2) | (rej ? 2u : 3u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        KT(8);
+    }
+    auto store_zone = [&](S* dst, uint32_t tot) {   // the LDS zone [0, tot) as 16-byte vectors
+        const uint32_t nfull = tot / PV;
+        uint4* dv = reinterpret_cast<uint4*>(dst);
+        for (uint32_t qv = t; qv < nfull; qv += BT) dv[qv] = L.xv[qv ^ ((qv >> 3) & 7u)];
+        for (uint32_t j = nfull * PV + t; j < tot; j += BT) dst[j] = xs[swz(j)];
+    };
+    if (rej) {   // merge 1 alone: its zone to zo, its rewrites in place in zc (zone_one's result)
+        for (uint32_t r = rwm; r; r &= r - 1) {
+            const int k = __ffs(r) - 1;
+            zc[i0 + k] = (S)(nw | (((wsm >> k) & 1u) ? WS : 0u));
+        }
+        store_zone(zo, z1);
+        lds_flush<MAXPER>(lt, tb, st);
+        if (t == 0) {
+            zst->m = m;
+            zst->valid_total = z1 + 1u;
+            atomicAdd(bytes, (uint64_t)sizeof(S) * ((uint64_t)z + (EXACT ? 0u : mc) + z1));
+        }
+        return;
+    }
+    // ── merge 2 on the first merge's zone (LDS) ──
+    uint32_t m2 = 0, Kz2 = 0;
+    {
+        const uint32_t lim = EXACT ? z1 : z1 - mc2;
+        auto X = [&](uint32_t p) -> uint32_t { return p < z1 ? (uint32_t)xs[swz(p)] : 0u; };
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) x[k] = X(i0 + k);
+        const uint32_t xm2 = i0 >= 2 ? X(i0 - 2) : 0u, xm1 = i0 >= 1 ? X(i0 - 1) : 0u, nxr = X(i0 + ZPT);
+        uint32_t eb = 0, ea = 0, wsm2 = 0;
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) {
+            eb |= (x[k] == b2 ? 1u : 0u) << k;
+            ea |= ((x[k] & TM) == a2 ? 1u : 0u) << k;
+            wsm2 |= ((x[k] & WS) ? 1u : 0u) << k;
+        }
+        const uint32_t inb = lane_mask_n(i0, z1, ZPT);
+        const uint32_t hitm = eb & ((ea << 1) | ((xm1 & TM) == a2 ? 1u : 0u)) & inb;
+        const uint32_t h_m1 = (i0 >= 1 && i0 - 1 < z1 && xm1 == b2 && (xm2 & TM) == a2) ? 1u : 0u;
+        const uint32_t h_32 = (nxr == b2 && (ea >> (ZPT - 1))) ? 1u : 0u;
+        const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (ZPT + 1));
+        const uint32_t below = lane_mask_n(i0, lim, ZPT);
+        const uint32_t surv = inb & ~hitm, keep = surv & below;
+        const uint32_t rw2 = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
+        uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+        for (uint32_t ib = (lim > 1u ? lim : 1u) + t; ib < z1; ib += 4u * BT) {   // stale tail: old pairs destroyed
+            uint32_t kq[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t i = ib + (uint32_t)k * BT;
+                const uint32_t xi = i < z1 ? X(i) : WS, tp = i < z1 ? X(i - 1) & TM : 0u, ti = xi & TM;
+                kq[k] = (!(xi & WS) && tp && ti && ((tp << 16) | ti) != pid2) ? (tp << 16) | ti : 0u;
+            }
+            lds_addk<4>(lt, tb, st, kq, 0xFFFFFFFFu);
+        }
+        while (rel) {
+            const int k = __ffs(rel) - 1;
+            rel &= rel - 1;
+            const uint32_t i = i0 + k;
+            if (i == 0) continue;
+            const uint32_t xi = x[k];
+            if (xi & WS) continue;
+            const uint32_t xp = X(i - 1);
+            const bool hm = (hbits >> k) & 1u, h0 = (hbits >> (k + 1)) & 1u, hp = (hbits >> (k + 2)) & 1u;
+            const uint32_t tp = xp & TM, ti = xi & TM;
+            if (tp && ti && ((tp << 16) | ti) != pid2) lds_add(lt, tb, st, (tp << 16) | ti, 0xFFFFFFFFu);
+            if (!h0) {
+                if (hm) {
+                    const uint32_t t2 = hp ? n2 : ti;
+                    if (t2) lds_add(lt, tb, st, (n2 << 16) | t2, 1u);
+                } else if (hp && tp) {
+                    lds_add(lt, tb, st, (tp << 16) | n2, 1u);
+                }
+            }
+        }
+        // the first merge's zone with the second's A-side rewrites -> zo (whole vectors)
+        if (i0 < z1) {
+            S e[ZPT];
+#pragma unroll
+            for (int k = 0; k < ZPT; ++k) e[k] = (S)(((rw2 >> k) & 1u) ? (n2 | (x[k] & WS)) : x[k]);
+            uint4* dv = reinterpret_cast<uint4*>(zo + i0);
+#pragma unroll
+            for (int k = 0; k < V; ++k) dv[k] = reinterpret_cast<const uint4*>(e)[k];
+        }
+        const uint32_t kc = __popc(keep);
+        const uint32_t incl = wave_scan_incl_u32(kc), tl = wave_sum_u32(__popc(surv & ~below));
+        __syncthreads();   // every read of the first merge's LDS zone is done (and L.wsum is free)
+        if (lane == 63) L.wsum[wid] = incl;
+        if (lane == 0) L.wtail[wid] = tl;
+        __syncthreads();
+        uint32_t pre = incl - kc;
+#pragma unroll
+        for (int w2 = 0; w2 < BT / 64; ++w2) {
+            pre += w2 < wid ? L.wsum[w2] : 0u;
+            Kz2 += L.wsum[w2];
+            m2 += L.wtail[w2];
+        }
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) {
+            const uint32_t y = ((rw2 >> k) & 1u) ? (n2 | (x[k] & WS)) : x[k];
+            const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
+            S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
+            *dst = (S)y;
+        }
+        if (!EXACT && m2) {
+            __syncthreads();
+            const uint32_t woff = mc2 - m2;
+            for (uint32_t jb = t; jb < m2; jb += 4u * BT) {
+                uint32_t kq[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t j = jb + (uint32_t)k * BT;
+                    kq[k] = 0u;
+                    if (j < m2) {
+                        const uint32_t x1 = wb2[woff + j];
+                        const uint32_t x0 = j ? (uint32_t)wb2[woff + j - 1] : (Kz2 ? (uint32_t)xs[swz(Kz2 - 1)] : 0u);
+                        xs[swz(Kz2 + j)] = (S)x1;
+                        if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) kq[k] = ((x0 & TM) << 16) | (x1 & TM);
+                    }
+                }
+                lds_addk<4>(lt, tb, st, kq, 1u);
+            }
+        }
+        __syncthreads();
+    }
+    const uint32_t z2 = Kz2 + m2;
+    if (t == 0) KT(9);
+    store_zone(zc, z2);
+    if (t == 0) KT(4);
+    lds_flush<MAXPER>(lt, tb, st);
+    if (t == 0) {
+        zst->m = m + m2;
+        zst->valid_total = z2 + 1u;   // survivors + 1 (k_refresh checks it against the new layout)
+        atomicAdd(bytes, (uint64_t)sizeof(S) * ((uint64_t)z + (EXACT ? 0u : mc) + z1 + z2));
+    }
 }
 
 // Body pass: blocks [0, nbody) each own `wpg` consecutive bitmap words of
@@ -853,34 +1270,58 @@ __device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const ui
 // source [n - 2mc - Bp, + mc) of the zone's other buffer to `wtmp`.
 // With `zst` (zone <= ZMAX), block nbody runs the whole zone pass (zone_one) and
 // there are no copy blocks: one launch merges body and zone.
+// A paired launch (the 256-thread form, Sel2) tests each bitmap word for both
+// merges, merges the first's candidate sectors, then — once the zone workgroup
+// accepted the second (ref mode) — the second's.  A sector is owned by one
+// workgroup for both, so its two merges run in order.
+#ifdef GBPE_ZP_OFF
+constexpr bool ZP_OFF = true;
+#else
+constexpr bool ZP_OFF = false;
+#endif
 constexpr uint32_t SP_PW = 64;               // bitmap words tested per pass (one per lane of wave 0)
 constexpr uint32_t SP_CAP = SP_PW * 32;      // candidate sectors per pass
 struct BodyCand {
     uint32_t sec[SP_CAP];
     uint2 ext[SP_CAP];
 };
-template <typename S, int BT>
-union BodyLds {   // body workgroups use the candidate arrays, the zone workgroup the zone
+// the zone workgroup's LDS (+ in the paired form its own delta table: merge 1's
+// stale tail and window are ~2 mc distinct pairs, up to ~3.3K at the form's largest
+// zones, which the 1,024-slot table shared with the body overflowed into global adds)
+// (u32 zones: 2,048 slots, so two workgroups still fit a CU's LDS — the paired form's
+// grid is the CU count + 1)
+template <typename S> constexpr int zp_lt() { return sizeof(S) == 2 ? 4096 : 2048; }
+template <typename S, int BT, int ZLT>
+struct ZoneWg {
     ZoneLds<S, BT> z;
+    LdsTab<ZLT> lt;
+    S wb2[ZLT > 1 ? ZoneDim<S, BT>::ZWIN : 1];   // zone_two: the second merge's window source
+};
+template <typename S, int BT, int ZLT = 1>
+union BodyLds {   // body workgroups use the candidate arrays, the zone workgroup the zone
+    ZoneWg<S, BT, ZLT> zw;
     BodyCand c;
 };
 
 // ZSEG: the form for zones of 32K-1M symbols: blocks [0, zone1) run the zone
 // segments (zone_seg) beside the body blocks, and zone_one is not compiled in
 // (with both, every form spilled to scratch)
+// zb0 / zb1: the zone buffers by the step's parity (zb0 holds the zone at merge 0
+// of the step); a merge of odd index finds it in zb1
 template <typename S, bool EXACT, int BT, int ZPT = ZoneDim<S, BT>::ZPT, bool ZSEG = false>
 __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
                                               uint32_t* __restrict__ bits, uint32_t W, uint32_t wpg,
                                               uint32_t* __restrict__ sig, Table tb, uint32_t nbody,
-                                              const S* __restrict__ zoth, S* __restrict__ wtmp,
-                                              uint32_t clog, DevState* zst, S* __restrict__ zcur, uint32_t zone1,
+                                              S* zb1, S* __restrict__ wtmp,
+                                              uint32_t clog, DevState* zst, S* zb0, uint32_t zone1,
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
                                               Table dtb, SelShard sh, uint32_t* __restrict__ lmul,
                                               ZSegState* __restrict__ zg = nullptr) {
     constexpr int KB_LT = ZSEG ? 4096 : LTAB_T;   // (4096 for every 1024-thread form: no change on C5 / 1 GiB / C2, r4)
+    constexpr bool PAIR = BT == 256 && !ZSEG;     // paired launches: the late form (zone_one in 256 threads)
     __shared__ LdsTab<KB_LT> lt;
-    __shared__ BodyLds<S, BT> u;
+    __shared__ BodyLds<S, BT, PAIR ? zp_lt<S>() : 1> u;
     // per wave: its sector's new signature bits (the 1024-thread forms: the early,
     // site-heavy merges; the 256-thread late form keeps 4 waves per SIMD without it)
     constexpr bool SIGL = SIG_LDS && BT == 1024;
@@ -890,7 +1331,8 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     constexpr bool SINK = true;   // body_sector waits for the next sector's prefetch before its stores
 #endif
     __shared__ uint32_t s_sig[SIGL ? BT / 64 : 1][SP_SIGW];
-    __shared__ uint32_t s_ntok, s_n, s_any, s_rm[BT / 64];
+    __shared__ uint32_t s_ntok, s_ntok1, s_n, s_n2, s_any, s_acc, s_rm[BT / 64], s_rm2[BT / 64];
+    __shared__ uint32_t s_hit1[PAIR ? SP_CAP / 32 : 1];   // sectors the first merge changed (local index bits)
     __shared__ uint64_t s_mv[BT / 64];
     constexpr int QPT = SP_CAP / BT;   // candidates per thread in the signature test
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -898,20 +1340,25 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
 #ifdef GBPE_BSPROF
     unsigned long long bsp[6] = {0, 0, 0, 0, 0, 0}, bsp_wall = 0;
 #endif
-    uint32_t a, b, nw, mc;
+    uint32_t a, b, nw, mc, md;
+    Sel2 s2;
     if (t == 0) KT(0);
     const DevState *gs = nullptr, *zs = nullptr;   // this workgroup's snapshots of the states at launch (LDS)
     const Table& xtb = dtb;
-    if (!sel_inline<BT>(st, zst, part, npart, round, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, gs, zs, sh)) {
+    SelShard shx = sh;
+    if (!PAIR) shx.k2 = 0u;
+    if (!sel_inline<BT>(st, zst, part, npart, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, md, s2, gs, zs, shx)) {
         return;
     }
     if (t == 0) KT(1);
+    S* const zcur = (md & 1u) ? zb1 : zb0;   // the zone of merge md
+    S* const zoth = (md & 1u) ? zb0 : zb1;
     // the zone workgroup is dispatched first (block 0 when zone1): it is the longest
     // single chain of the merge, and later blocks of a large grid start later
     const uint32_t bid = blockIdx.x - zone1;
     if constexpr (ZSEG) {
         if (blockIdx.x < zone1) {
-            zone_seg<S, EXACT, BT, KB_LT, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, zg, zone1, u.z, lt, dtb, a, b, nw, mc,
+            zone_seg<S, EXACT, BT, KB_LT, ZPT>(st, zst, *gs, *zs, zcur, zoth, zg, zone1, u.zw.z, lt, dtb, a, b, nw, mc,
                                              wg_bytes + nbody, round);
             if (t == 0) {
                 KT(5);
@@ -921,8 +1368,17 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         }
     } else {
         if (zone1 == 1 && blockIdx.x == 0) {
-            zone_one<S, EXACT, BT, KB_LT, ZPT>(st, zst, *gs, *zs, zcur, (S*)zoth, u.z, lt, xtb, a, b, nw, mc,
-                                                 wg_bytes + nbody, round);
+            bool two = false;
+            if constexpr (PAIR && !ZP_OFF) {
+                if (s2.dbl) {
+                    zone_two<S, EXACT, BT, zp_lt<S>(), ZPT>(st, zst, *gs, zs->n, zcur, zoth, zg, u.zw.z, u.zw.wb2,
+                                                            u.zw.lt, xtb, a, b, nw, mc, s2, wg_bytes + nbody, round);
+                    two = true;
+                }
+            }
+            if (!two)
+                zone_one<S, EXACT, BT, KB_LT, ZPT>(st, zst, zs->n, win_src0(*gs, mc), zcur, zoth, u.zw.z, lt, xtb, a, b,
+                                                   nw, mc, wg_bytes + nbody, round);
             if (t == 0) {
                 KT(5);
                 KTV(6, 2);
@@ -940,30 +1396,41 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         }
         return;
     }
-    const uint32_t pid_ab = (a << 16) | b;
+    const bool dbl = PAIR && s2.dbl;   // (block-uniform)
+    const uint32_t pid_ab = (a << 16) | b, pid_2 = (s2.a << 16) | s2.b;
     BodyCand& cb = u.c;
     lds_clear(lt);
-    if (t == 0) s_any = 0u;
-    uint32_t removed = 0, ncand_all = 0;
+    if (t == 0) {
+        s_any = 0u;
+        s_acc = 0u;
+    }
+    uint32_t removed = 0, removed2 = 0, ncand_all = 0;
     uint64_t moved = 0, rd = 0;   // sector symbols read + rewritten (wave-uniform); extents + signature words read
     // sh.sub > 1: this workgroup takes a 32/sub-sector slice of word bid / sub
     const uint32_t sub = sh.sub, sw = 32u / sub;
     const uint32_t w_beg = sub > 1 ? bid / sub : bid * wpg;
     const uint32_t w_end = sub > 1 ? w_beg + 1 : (w_beg + wpg < W ? w_beg + wpg : W);
     const uint32_t smask = sub > 1 ? ((1u << sw) - 1u) << ((bid % sub) * sw) : 0xFFFFFFFFu;
-    for (uint32_t w0 = w_beg; w0 < w_end; w0 += SP_PW) {
+    const uint32_t npw = dbl ? SP_PW / 2 : SP_PW;   // a paired launch: lanes [npw, 64) test the second merge's rows
+    for (uint32_t w0 = w_beg; w0 < w_end; w0 += npw) {
         __syncthreads();   // the previous pass is done with s_ntok / s_n / the candidate arrays
         if (t == 0) {
             s_ntok = 0u;
+            s_ntok1 = 0u;
             s_n = 0u;
+            s_n2 = 0u;
         }
+        if (PAIR && t < (int)(SP_CAP / 32)) s_hit1[t] = 0u;
         __syncthreads();
         if (t < (int)SP_PW) {   // token candidates (one wave: list positions from its scan, no LDS counter)
-            const uint32_t w = w0 + t;
-            uint32_t c = w < w_end ? bits[(uint64_t)a * W + w] & bits[(uint64_t)b * W + w] & smask : 0u;
+            const bool two = dbl && (uint32_t)t >= npw;
+            const uint32_t w = w0 + (uint32_t)t - (two ? npw : 0u);
+            const uint32_t ra = two ? s2.a : a, rb = two ? s2.b : b;
+            uint32_t c = w < w_end ? bits[(uint64_t)ra * W + w] & bits[(uint64_t)rb * W + w] & smask : 0u;
             const uint32_t pc = (uint32_t)__popc(c), incl = wave_scan_incl_u32(pc);
             uint32_t pos = incl - pc;
             if (t == (int)SP_PW - 1) s_ntok = incl;
+            if (t == (int)npw - 1) s_ntok1 = incl;   // the first merge's candidates come first
             while (c) {
                 const int bit = __ffs(c) - 1;
                 c &= c - 1;
@@ -971,12 +1438,13 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
             }
         }
         __syncthreads();
-        const uint32_t ntok = s_ntok;
+        const uint32_t ntok = s_ntok, ntok1 = s_ntok1;
         if (t == 0) KT(2);
         if (ntok == 0) continue;   // block-uniform
         rd += 16ull * ntok;
         // signature filter: this thread's candidates (their extents load alongside)
-        // into registers, then compacted in place
+        // into registers, then compacted in place (a paired launch: the first merge's
+        // from the front, the second's from the back)
         uint32_t cs[QPT];
         uint2 ce[QPT];
         bool ck[QPT];
@@ -989,65 +1457,130 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
         for (int q = 0; q < QPT; ++q) {
             ck[q] = false;
             if (cs[q] != SP_INV) {
+                const uint32_t j = (uint32_t)t + (uint32_t)q * BT;
                 ce[q] = sec[cs[q]];
-                ck[q] = sig_has(sig + (uint64_t)cs[q] * SP_SIGW, pid_ab);
+                ck[q] = sig_has(sig + (uint64_t)cs[q] * SP_SIGW, j < ntok1 ? pid_ab : pid_2);
             }
         }
         __syncthreads();   // every candidate is read before the list is rewritten
 #pragma unroll
         for (int q = 0; q < QPT; ++q) {   // one LDS counter add per wave, positions from the ballot
-            const unsigned long long m = __ballot(ck[q]);
+            const uint32_t j = (uint32_t)t + (uint32_t)q * BT;
+            const bool in2 = PAIR && j >= ntok1;
+            const unsigned long long m = __ballot(ck[q] && !in2);
             uint32_t base = 0;
             if (lane == 0 && m) base = atomicAdd(&s_n, (uint32_t)__popcll(m));
             base = __builtin_amdgcn_readlane(base, 0);
-            if (ck[q]) {
+            if (ck[q] && !in2) {
                 const uint32_t qq = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                 cb.sec[qq] = cs[q];
                 cb.ext[qq] = ce[q];
             }
-        }
-        __syncthreads();
-        const uint32_t ncand = s_n;
-        if (t == 0) KT(3);
-        if (ncand == 0) continue;   // block-uniform
-        ncand_all += ncand;
-        if (t == 0) s_any = 1u;
-        // software-pipelined: a wave's next sector loads while it merges this one
-        uint32_t nf[5], nfm[4];
-#ifdef GBPE_BSPROF
-        const unsigned long long sp0 = clock64();
-#endif
-        if ((uint32_t)wid < ncand)
-            sector_first<S>(body + cb.ext[wid].x, lmul ? lmul + cb.ext[wid].x : nullptr, cb.ext[wid].y, nf, nfm);
-        for (uint32_t j = wid; j < ncand; j += BT / 64) {
-            const uint32_t sct = cb.sec[j];
-            const uint2 e = cb.ext[j];
-            uint32_t cf[5], cfm[4];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) cf[k] = nf[k];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) cfm[k] = nfm[k];
-            if (j + BT / 64 < ncand) {
-                const uint2 en = cb.ext[j + BT / 64];
-                sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
-            }
-            uint32_t out = 0;
-            const uint32_t r = body_sector<S, KB_LT, Table, LdsTab<KB_LT>, SIGL>(
-                body + e.x, lmul ? lmul + e.x : nullptr, e.y, a, b, nw, lt, xtb, st, sig + (uint64_t)sct * SP_SIGW, out, cf,
-                cfm, s_sig[SIGL ? wid : 0], SINK ? nf : nullptr, SINK ? nfm : nullptr BSP_PASS);
-            moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (r ? out : 0u));
-            if (r) {
-                removed += r;
-                if (lane == 0) {
-                    if (clog) atomicAdd(&st->hitsec, 1u);
-                    sec[sct].y = out;
-                    atomicOr(&bits[(uint64_t)nw * W + (sct >> 5)], 1u << (sct & 31u));
+            if (PAIR) {
+                const unsigned long long m2 = __ballot(ck[q] && in2);
+                uint32_t base2 = 0;
+                if (lane == 0 && m2) base2 = atomicAdd(&s_n2, (uint32_t)__popcll(m2));
+                base2 = __builtin_amdgcn_readlane(base2, 0);
+                if (ck[q] && in2) {
+                    const uint32_t qq = SP_CAP - 1u - base2 -
+                                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m2, 0u));
+                    cb.sec[qq] = cs[q];
+                    cb.ext[qq] = ce[q];
                 }
             }
         }
+        __syncthreads();
+        const uint32_t n1 = s_n, n2 = PAIR ? s_n2 : 0u;
+        if (t == 0) KT(3);
+        if (n1 + n2 == 0) continue;   // block-uniform
+        ncand_all += n1 + n2;
+        if (t == 0) s_any = 1u;
+#pragma unroll 1
+        for (int ph = 0; ph < (PAIR ? 2 : 1); ++ph) {   // the first merge's sectors, then the second's
+            const uint32_t ncand = ph ? n2 : n1;
+            if (ph) {
+                if (t == 0) KT(10);
+                if (ncand == 0) break;   // block-uniform
+                // the first merge's sector stores land before the second reads them back; in
+                // ref mode the zone workgroup's verdict first (it never waits on a body workgroup)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (t == 0) {
+                    uint32_t v = 3u;
+                    if (!EXACT) {
+                        const uint32_t tag = gs->epoch << 2;
+                        for (uint32_t it = 0;; ++it) {
+                            v = __hip_atomic_load(pair_word(zg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if ((v & ~3u) == tag && (v & 2u)) break;
+                            if (it > ZSEG_SPIN) {
+                                atomicOr(&st->err, ERR_SPIN);
+                                v = 2u;
+                                break;
+                            }
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                    }
+                    s_acc = v & 1u;
+                }
+                __syncthreads();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (t == 0) KT(11);
+                if (!s_acc) break;   // block-uniform
+            }
+            const uint32_t base = ph ? SP_CAP - ncand : 0u;   // (the second list is stored backwards: any order)
+            const uint32_t ca = ph ? s2.a : a, cbb = ph ? s2.b : b, cn = ph ? nw + 1u : nw;
+            // a sector the first merge changed in this workgroup: its extent is re-read
+            auto ext_of = [&](uint32_t j) -> uint2 {
+                const uint32_t sct = cb.sec[base + j];
+                if (PAIR && ph && ((s_hit1[(sct - w0 * 32u) >> 5] >> (sct & 31u)) & 1u)) {
+                    const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(&sec[sct]), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+                }
+                return cb.ext[base + j];
+            };
+            // software-pipelined: a wave's next sector loads while it merges this one
+            uint32_t nf[5], nfm[4];
 #ifdef GBPE_BSPROF
-        bsp_wall += clock64() - sp0;
+            const unsigned long long sp0 = clock64();
 #endif
+            uint2 en = make_uint2(0u, 0u);
+            if ((uint32_t)wid < ncand) {
+                en = ext_of((uint32_t)wid);
+                sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
+            }
+            for (uint32_t j = wid; j < ncand; j += BT / 64) {
+                const uint32_t sct = cb.sec[base + j];
+                const uint2 e = en;
+                uint32_t cf[5], cfm[4];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) cf[k] = nf[k];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cfm[k] = nfm[k];
+                if (j + BT / 64 < ncand) {
+                    en = ext_of(j + BT / 64);
+                    sector_first<S>(body + en.x, lmul ? lmul + en.x : nullptr, en.y, nf, nfm);
+                }
+                uint32_t out = 0;
+                const uint32_t r = body_sector<S, KB_LT, Table, LdsTab<KB_LT>, SIGL>(
+                    body + e.x, lmul ? lmul + e.x : nullptr, e.y, ca, cbb, cn, lt, xtb, st, sig + (uint64_t)sct * SP_SIGW,
+                    out, cf, cfm, s_sig[SIGL ? wid : 0], SINK ? nf : nullptr, SINK ? nfm : nullptr BSP_PASS);
+                moved += (uint64_t)(sizeof(S) + (lmul ? 4u : 0u)) * (e.y + (r ? out : 0u));
+                if (r) {
+                    if (ph) removed2 += r;
+                    else removed += r;
+                    if (lane == 0) {
+                        if (clog) atomicAdd(&st->hitsec, 1u);
+                        sec[sct].y = out;
+                        atomicOr(&bits[(uint64_t)cn * W + (sct >> 5)], 1u << (sct & 31u));
+                        if (PAIR && dbl && !ph) atomicOr(&s_hit1[(sct - w0 * 32u) >> 5], 1u << (sct & 31u));
+                    }
+                }
+            }
+#ifdef GBPE_BSPROF
+            bsp_wall += clock64() - sp0;
+#endif
+            if (PAIR && dbl && !ph) __syncthreads();   // s_hit1 complete before the second merge's extents
+        }
     }
 #ifdef GBPE_BSPROF
     if (lane == 0) {
@@ -1070,17 +1603,20 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     lds_flush(lt, xtb, st);
     if (lane == 0) {
         s_rm[wid] = removed;
+        s_rm2[wid] = removed2;
         s_mv[wid] = moved;
     }
     __syncthreads();
     if (t == 0) {
-        uint32_t r = 0;
+        uint32_t r = 0, r2 = 0;
         uint64_t mv = rd;
         for (int w2 = 0; w2 < BT / 64; ++w2) {
             r += s_rm[w2];
+            r2 += s_rm2[w2];
             mv += s_mv[w2];
         }
         if (r) atomicAdd(&st->body_rm, r);
+        if (r2) atomicAdd(&st->body_rm2, r2);
         atomicAdd(&wg_bytes[bid], mv);   // this workgroup's own counter
         KT(5);
         KTV(6, 1 | (ncand_all << 8));

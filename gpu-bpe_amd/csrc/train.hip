@@ -88,6 +88,7 @@ int trainer_create_impl(gbpe_ctx* ctx, const uint8_t* bytes, uint64_t n, const u
     t->tb.nblk = (uint32_t)(slots >> BLK_LOG2);
     if (pool_malloc(t->ctx, &t->tb.slots, slots * sizeof(uint2)) != hipSuccess ||
         pool_malloc(t->ctx, &t->tb.bmax, t->tb.nblk * sizeof(uint64_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tb.bmax2, t->tb.nblk * sizeof(uint64_t)) != hipSuccess ||
         pool_malloc(t->ctx, &t->tb.dirty, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
         pool_malloc(t->ctx, &t->tb.dlist, (t->tb.nblk + 1) * sizeof(uint32_t)) != hipSuccess ||
         pool_malloc(t->ctx, &t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
@@ -397,9 +398,18 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
             }
         }
         sg.refresh = g_refresh;
+        // paired launches: the late zone_one form, two merges per launch
+        // when the table's top two allow it
+        sg.pair = t->pair_on && sg.zone1 == 1 && sg.bt == 256 && t->zseg && k >= 2;
     }
+    // a paired step needs fewer launches than merges: sized by the last paired step's
+    // rate (+2); launches past the step's budget are no-ops, and a step whose launches
+    // ran out first is continued by gbpe_trainer_step
+    uint32_t nl = k;
+    if (sg.pair) nl = std::min<uint32_t>(k, (uint32_t)std::ceil((double)k / (1.0 + t->pair_rate)) + 2u);
+    const uint32_t paired0 = hs->paired;
     auto launch_all = [&]() -> int {
-        for (uint32_t r = 0; r < k; ++r) {
+        for (uint32_t r = 0; r < nl; ++r) {
             hipEvent_t* ev = timing ? &t->evs[5 * r] : nullptr;
             int rc;
             if (sparse)
@@ -427,6 +437,16 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
     }
     TR_HIP(t, hipStreamSynchronize(s));
     const uint32_t done = hs->merges_done;
+    {
+        const uint32_t dbl = hs->paired - paired0;   // launches that ran two merges
+        t->pair_done += dbl;
+        if (sg.pair && done > dbl) t->pair_rate = (double)dbl / (double)(done - dbl);
+        if (t->ptrace)   // (diagnostic, GBPE_DEBUG ptrace=1) the step's form and pairing
+            fprintf(stderr, "[ptrace] merge %u zone %u zone1 %u bt %d pair %d launches %u done %u paired %u cand %u mc %u us %.1f\n",
+                    t->done, hs->n - hs->B, sg.zone1, sg.bt, sg.pair ? 1 : 0, nl, done, dbl,
+                    hs->pair_cand, done ? t->h_log[(done - 1) * 4 + 3] : 0u,
+                    std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - hs0).count());
+    }
     if (t->htime) {   // (diagnostic) host enqueue vs wait; "late": a zone of <= 16K symbols
         t->ht_pre += std::chrono::duration<double, std::micro>(h0 - hs0).count();
         const double enq = std::chrono::duration<double, std::micro>(h1 - h0).count();
@@ -464,7 +484,7 @@ int trainer_step_once(gbpe_trainer* t, uint32_t max_merges, uint32_t* merges_out
                               (err & ERR_SPIN) ? "zone segment hand-off timed out" : "");
     }
     if (timing) {
-        for (uint32_t r = 0; r < done; ++r) {
+        for (uint32_t r = 0; r < std::min(done, nl); ++r) {   // (per launch)
             float a = 0, b = 0, c = 0, d1 = 0, d2 = 0;
             hipEvent_t* ev = &t->evs[5 * r];
             hipEventElapsedTime(&a, ev[0], ev[1]);
@@ -580,6 +600,7 @@ extern "C" int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* o) {
     o->ms_sparse = t->ms_sparse;
     o->ms_body = t->ms_body;
     o->ms_create = t->ms_create;
+    o->paired_merges = t->pair_done;
     o->zone_bytes = t->h_st->sp_bytes;
     o->lexicon_builds = (uint32_t)t->lx_builds;
     o->lexicon_fallbacks = (uint32_t)t->lx_fallbacks;
@@ -695,6 +716,9 @@ extern "C" int gbpe_trainer_pair_counts(gbpe_trainer* t, uint32_t* pids, uint32_
 extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     if (!t) return;
     if (t->ctx && t->ctx->stream) hipStreamSynchronize(t->ctx->stream);
+    if (t->htime && t->h_st)   // paired launches: candidates, window-check rejections, run
+        fprintf(stderr, "[pair] candidates %u rejected %u paired %u\n", t->h_st->pair_cand, t->h_st->pair_rej,
+                t->h_st->paired);
     if (t->htime && t->ht_steps)
         fprintf(stderr, "[htime] steps %llu: before launch %.2f ms, enqueue %.2f ms, wait %.2f ms, after sync %.2f ms, "
                         "caller between steps %.2f ms, shrinks %llu in %.2f ms, filter rebuilds %llu in %.2f ms | late steps %llu (%llu merges): enqueue %.2f ms "
@@ -727,6 +751,7 @@ extern "C" void gbpe_trainer_destroy(gbpe_trainer* t) {
     pool_free(t->ctx, t->buf[1]);
     pool_free(t->ctx, t->tb.slots);
     pool_free(t->ctx, t->tb.bmax);
+    pool_free(t->ctx, t->tb.bmax2);
     pool_free(t->ctx, t->tb.dirty);
     pool_free(t->ctx, t->tb.dlist);
     pool_free(t->ctx, t->tb.blive);

@@ -59,6 +59,24 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     const uint64_t a = r0 > r1 ? r0 : r1, b = r2 > r3 ? r2 : r3;
     return a > b ? a : b;
 }
+// Top-2 keys (the paired launch, sparse.h zone_two): every lane holds its own
+// first f > second s; keys are unique (one per pair id) except the no-key fills,
+// so exactly one lane's f is the wave's first and the second is the largest of
+// the other lanes' f and that lane's s (uniform)
+__device__ __forceinline__ void wave_top2_u64(uint64_t f, uint64_t s, uint64_t& o1, uint64_t& o2) {
+    o1 = wave_max_u64(f);
+    o2 = wave_max_u64(f == o1 ? s : f);
+}
+__device__ __forceinline__ void top2_add(uint64_t& f, uint64_t& s, uint64_t k) {   // (selects: no branches)
+    const bool g1 = k > f, g2 = k > s;
+    s = g1 ? f : (g2 ? k : s);
+    f = g1 ? k : f;
+}
+__device__ __forceinline__ void top2_merge(uint64_t& f, uint64_t& s, uint64_t g1, uint64_t g2) {
+    const uint64_t hi = f > g1 ? f : g1, lo = f > g1 ? g1 : f, s2 = s > g2 ? s : g2;
+    f = hi;
+    s = lo > s2 ? lo : s2;
+}
 // the wave's sum (uniform)
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     v += dpp32<0xB1>(v);
@@ -112,6 +130,13 @@ struct DevState {
                            // (never written by a commit: a reader beside k_body would see it unchanged)
     uint32_t enter_lim;    // dense loop: end the step at the first merge whose count is <= this (the host
                            // can then enter the sector-sparse loop; 0 = off)
+    // ── paired launch (sparse.h zone_two): a second merge in the same k_body ──
+    uint32_t mc2;          // the second merge's count (written with the first's commit, used only if acc2)
+    uint32_t body_rm2;     // B-sides removed from the body by the second merge
+    uint32_t acc2;         // the zone workgroup accepted the second merge (k_refresh consumes and clears it)
+    uint32_t paired;       // launches that ran two merges (cumulative)
+    uint32_t pair_cand;    // launches whose top two allowed a second merge (cumulative, zone_two)
+    uint32_t pair_rej;     // ... that the zone workgroup's window check turned down
 };
 static_assert(sizeof(DevState) <= 256, "state");
 
@@ -186,6 +211,7 @@ struct Table {
     uint2* slots;      // .x = pid (0 = empty), .y = count (u32, wraps for transient negatives)
     uint32_t mask;     // slots - 1
     uint64_t* bmax;    // per block: (count << 32) | ~pid, KEY_NONE when no count is positive
+    uint64_t* bmax2;   // per block: the second key (KEY_NONE when fewer than two counts are positive)
     uint32_t* dirty;   // per block flag
     uint32_t* dlist;   // dirty block list
     uint32_t* blive;   // per block: entries with count > 0
@@ -265,6 +291,75 @@ __device__ __forceinline__ void lds_add(LdsTab<N>& t, const TB& tb, DevState* st
     table_add(tb, st, pid, d);   // LDS table crowded: go straight to the global table
 }
 
+// A runtime-sized prefix (a power of two) of an LdsTab: zone_two sizes its table by
+// the pair's counts, so a late pair's few hundred deltas do not pay for clearing
+// and scanning thousands of slots
+struct LdsView {
+    uint32_t* key;
+    uint32_t* val;
+    uint32_t* ovf;
+    uint32_t mask;
+};
+template <int N>
+__device__ __forceinline__ LdsView lds_view(LdsTab<N>& t, uint32_t n) {
+    return LdsView{t.key, t.val, &t.ovf, n - 1u};
+}
+__device__ __forceinline__ void lds_clear(LdsView& t) {
+    for (uint32_t i = threadIdx.x; i <= t.mask; i += blockDim.x) {
+        t.key[i] = 0u;
+        t.val[i] = 0u;
+    }
+    if (threadIdx.x == 0) *t.ovf = 0u;
+}
+template <typename TB>
+__device__ __forceinline__ void lds_add(LdsView& t, const TB& tb, DevState* st, uint32_t pid, uint32_t d) {
+    const uint32_t h = gbpe_fmix32(pid);
+#pragma unroll 1
+    for (int p = 0; p < LPROBE; ++p) {
+        const uint32_t idx = (h + (uint32_t)((p * (p + 1)) >> 1)) & t.mask;
+        const uint32_t k = atomicCAS(&t.key[idx], 0u, pid);
+        if (k == 0u || k == pid) {
+            atomicAdd(&t.val[idx], d);
+            return;
+        }
+    }
+    *t.ovf = 1u;
+    table_add(tb, st, pid, d);   // crowded: straight to the global table
+}
+
+// K adds of one delta with their home-slot compare-and-swaps issued together: the
+// zone passes' stale-tail and window loops were chains of dependent LDS round trips
+// (two reads, a CAS, an add per pair, ~4 pairs per thread at late counts); now the
+// reads and the CASes of K pairs overlap and the adds need no reply.  A pair whose
+// home slot holds another key takes lds_add's full probe.  pid 0 = no pair.
+template <int N>
+__device__ __forceinline__ uint32_t* tab_key(LdsTab<N>& t) { return t.key; }
+template <int N>
+__device__ __forceinline__ uint32_t* tab_val(LdsTab<N>& t) { return t.val; }
+template <int N>
+__device__ __forceinline__ uint32_t tab_mask(const LdsTab<N>&) { return (uint32_t)N - 1u; }
+__device__ __forceinline__ uint32_t* tab_key(LdsView& t) { return t.key; }
+__device__ __forceinline__ uint32_t* tab_val(LdsView& t) { return t.val; }
+__device__ __forceinline__ uint32_t tab_mask(const LdsView& t) { return t.mask; }
+template <int K, typename LT, typename TB>
+__device__ __forceinline__ void lds_addk(LT& t, const TB& tb, DevState* st, const uint32_t (&kq)[K], uint32_t d) {
+    uint32_t* key = tab_key(t);
+    uint32_t* val = tab_val(t);
+    const uint32_t mask = tab_mask(t);
+    uint32_t idx[K], o[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        idx[k] = gbpe_fmix32(kq[k]) & mask;
+        o[k] = kq[k] ? atomicCAS(&key[idx[k]], 0u, kq[k]) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (!kq[k]) continue;
+        if (o[k] == 0u || o[k] == kq[k]) atomicAdd(&val[idx[k]], d);
+        else lds_add(t, tb, st, kq[k], d);
+    }
+}
+
 // Up to 8 (pid, delta) adds with their home-slot key loads issued together: at
 // the table's low load factor nearly every live pair sits in its home slot, so
 // a batch costs one round trip instead of one per entry; the rest (new keys,
@@ -276,9 +371,9 @@ __device__ __forceinline__ void table_add8(const Table& tb, DevState* st, const 
                                            const uint32_t (&vv)[8]) {
     uint32_t hs[8], hk[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 8; ++j) {   // (no load for an empty entry: thousands of them hit slot 0's line)
         hs[j] = (kk[j] && vv[j]) ? (gbpe_fmix32(kk[j]) & tb.mask) : 0u;
-        hk[j] = __hip_atomic_load(&tb.slots[hs[j]].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        hk[j] = (kk[j] && vv[j]) ? __hip_atomic_load(&tb.slots[hs[j]].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -303,6 +398,42 @@ template <int N, typename TB>
 __device__ __forceinline__ void lds_flush(LdsTab<N>& t, const TB& tb, DevState* st) {
     __syncthreads();
     const uint32_t nt = blockDim.x;
+    if (N > 8 * (int)nt && N <= 16 * (int)nt && N < 8192) {
+        // a large, mostly sparse table (the paired zone pass's 4,096 slots): compacted
+        // first, then the live entries added 8 per thread per round trip
+        __shared__ uint32_t s_cnt16;
+        uint32_t kk[16], vv[16], live = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t i = threadIdx.x + j * nt;
+            kk[j] = i < (uint32_t)N ? t.key[i] : 0u;
+            vv[j] = i < (uint32_t)N ? t.val[i] : 0u;
+            if (kk[j] && vv[j]) live |= 1u << j;
+        }
+        if (threadIdx.x == 0) s_cnt16 = 0u;
+        __syncthreads();
+        uint32_t off = live ? atomicAdd(&s_cnt16, (uint32_t)__popc(live)) : 0u;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if ((live >> j) & 1u) {
+                t.key[off] = kk[j];
+                t.val[off] = vv[j];
+                ++off;
+            }
+        __syncthreads();
+        const uint32_t total = s_cnt16;
+        for (uint32_t i0 = threadIdx.x; i0 < total; i0 += 8 * nt) {
+            uint32_t k8[8], v8[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t i = i0 + j * nt;
+                k8[j] = i < total ? t.key[i] : 0u;
+                v8[j] = i < total ? t.val[i] : 0u;
+            }
+            table_add8(tb, st, k8, v8);
+        }
+        return;
+    }
     if (N > 8 * (int)nt) {
         for (uint32_t i0 = threadIdx.x; i0 < (uint32_t)N; i0 += 8 * nt) {
             uint32_t kk[8], vv[8];
@@ -338,6 +469,45 @@ __device__ __forceinline__ void lds_flush(LdsTab<N>& t, const TB& tb, DevState* 
     __syncthreads();
     const uint32_t total = s_cnt;
     for (uint32_t i = threadIdx.x; i < total; i += nt) table_add(tb, st, t.key[i], t.val[i]);
+}
+
+// flush of a runtime-sized table (<= 16 slots per thread): the live entries
+// compacted, then added 8 per thread per round trip (table_add8)
+template <int MAXPER, typename TB>
+__device__ __forceinline__ void lds_flush(LdsView& t, const TB& tb, DevState* st) {
+    __syncthreads();
+    __shared__ uint32_t s_cntv;
+    const uint32_t nt = blockDim.x, n = t.mask + 1u;
+    uint32_t kk[MAXPER], vv[MAXPER], live = 0;
+#pragma unroll
+    for (int j = 0; j < MAXPER; ++j) {
+        const uint32_t i = threadIdx.x + j * nt;
+        kk[j] = i < n ? t.key[i] : 0u;
+        vv[j] = i < n ? t.val[i] : 0u;
+        if (kk[j] && vv[j]) live |= 1u << j;
+    }
+    if (threadIdx.x == 0) s_cntv = 0u;
+    __syncthreads();
+    uint32_t off = live ? atomicAdd(&s_cntv, (uint32_t)__popc(live)) : 0u;
+#pragma unroll
+    for (int j = 0; j < MAXPER; ++j)
+        if ((live >> j) & 1u) {
+            t.key[off] = kk[j];
+            t.val[off] = vv[j];
+            ++off;
+        }
+    __syncthreads();
+    const uint32_t total = s_cntv;
+    for (uint32_t i0 = threadIdx.x; i0 < total; i0 += 8 * nt) {
+        uint32_t k8[8], v8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t i = i0 + j * nt;
+            k8[j] = i < total ? t.key[i] : 0u;
+            v8[j] = i < total ? t.val[i] : 0u;
+        }
+        table_add8(tb, st, k8, v8);
+    }
 }
 
 template <typename S>
@@ -556,16 +726,19 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
     // form stays a kernel of its own: one body for both cost 1 GiB 1-2 %,
     // profiles/r5/s13)
     __shared__ uint64_t s_dmask[WIDE ? TPB / 64 : 1];
-    __shared__ uint64_t s_bm[WIDE ? TPB : 64];
+    __shared__ uint64_t s_bm[WIDE ? TPB : 64], s_bm2[WIDE ? TPB : 64];
     const uint32_t per = (tb.nblk + gridDim.x - 1) / gridDim.x;   // <= 64, WIDE: <= TPB (GBPE_LAUNCH_REFRESH)
     constexpr bool wide = WIDE;
     const uint32_t b0 = blockIdx.x * per;
-    uint64_t f_bm = 0ull;
+    uint64_t f_bm = 0ull, f_bm2 = 0ull;
     bool f_d = false;
     if (wide || threadIdx.x < 64) {
         const uint32_t blk = b0 + threadIdx.x;
         const bool in = threadIdx.x < per && blk < tb.nblk;
-        if (part && in) f_bm = tb.bmax[blk];
+        if (part && in) {
+            f_bm = tb.bmax[blk];
+            f_bm2 = tb.bmax2[blk];
+        }
         f_d = in && tb.dirty[blk];
     }
     // finish == 2: the sector-sparse loop, whose merge was selected inside k_body
@@ -586,29 +759,43 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
         __syncthreads();
         const DevState& g = s_g.d;
         const DevState& z = s_z.d;
-        const uint32_t r = round;
+        // sector-sparse: the launch's merge index is the state's (a paired launch
+        // runs two, so launches and merges part ways)
+        const uint32_t r = finish >= 2 ? g.merges_done : round;
         const bool fin = finish >= 2 ? (!g.stop && !g.sp_abort && g.sel_round == r + 1u)
                                      : (!g.stop && g.merges_done == r + 1u);
         if (fin && threadIdx.x == 0) {
             if (zst) {   // sector-sparse: global length, body length, zone length
+                const uint32_t k2 = finish >= 2 ? g.acc2 : 0u;   // a second merge ran in this launch
                 if (finish >= 2) {
-                    st->merges_done = r + 1u;
-                    st->next_id = g.next_id + 1u;
-                    st->epoch = g.epoch + 1u;
-                    st->mc_prev = g.mc;
+                    st->merges_done = r + 1u + k2;
+                    st->next_id = g.next_id + 1u + k2;
+                    st->epoch = g.epoch + 1u + k2;
+                    st->mc_prev = k2 ? g.mc2 : g.mc;
+                    if (k2) {
+                        st->acc2 = 0u;
+                        st->paired = g.paired + 1u;
+                    }
                 }
                 if (clog) {
                     clog[2 * r] = g.cand;
                     clog[2 * r + 1] = g.hitsec;
+                    if (k2) {
+                        clog[2 * r + 2] = 0u;
+                        clog[2 * r + 3] = 0u;
+                    }
                 }
                 st->cand = 0u;
                 st->hitsec = 0u;
-                st->tail_total = g.tail_total + z.m;
-                const uint32_t n = g.new_n, B = g.B - g.body_rm, zn = n - B;
+                st->tail_total = g.tail_total + z.m;   // (both merges' windows)
+                // the second merge ran on the first's stream: its window source lies in the
+                // stream whose body was B (not Bp)
+                const uint32_t n = g.new_n - (k2 ? g.mc2 : 0u), B = g.B - g.body_rm - g.body_rm2, zn = n - B;
                 st->n = n;
-                st->Bp = g.B;
+                st->Bp = k2 ? g.B - g.body_rm : g.B;
                 st->B = B;
                 st->body_rm = 0u;
+                st->body_rm2 = 0u;
                 zst->n = zn;
                 st->zlast = zn;
                 if (!z.valid_total && g.is_last)   // multi-tile zone: k_delta + k_compact stream it twice, plus the window copy
@@ -624,7 +811,10 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
     // time (no workgroup barrier per block: a merge dirties a few blocks per
     // workgroup, each holding a few live pairs)
     if (wide || threadIdx.x < 64) {
-        if (part) s_bm[threadIdx.x] = f_bm;
+        if (part) {
+            s_bm[threadIdx.x] = f_bm;
+            s_bm2[threadIdx.x] = f_bm2;
+        }
         const unsigned long long m = __ballot(f_d);
         if ((threadIdx.x & 63) == 0) s_dmask[threadIdx.x >> 6] = m;
     }
@@ -644,43 +834,43 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
             uint4 e[NV];
 #pragma unroll
             for (int q = 0; q < NV; ++q) e[q] = sl[lane + q * 64];
-            uint64_t best = KEY_NONE;
+            uint64_t best = KEY_NONE, second = KEY_NONE;   // the block's two largest keys (top2_add)
             uint32_t live = 0;
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 if (e[q].x && (int32_t)e[q].y > 0) {
-                    const uint64_t key = ((uint64_t)e[q].y << 32) | (uint32_t)(~e[q].x);
-                    best = key > best ? key : best;
+                    top2_add(best, second, ((uint64_t)e[q].y << 32) | (uint32_t)(~e[q].x));
                     ++live;
                 }
                 if (e[q].z && (int32_t)e[q].w > 0) {
-                    const uint64_t key = ((uint64_t)e[q].w << 32) | (uint32_t)(~e[q].z);
-                    best = key > best ? key : best;
+                    top2_add(best, second, ((uint64_t)e[q].w << 32) | (uint32_t)(~e[q].z));
                     ++live;
                 }
             }
-            best = wave_max_u64(best);
+            wave_top2_u64(best, second, best, second);
             live = wave_sum_u32(live);
             if (lane == 0) {
                 tb.bmax[blk] = best;
+                tb.bmax2[blk] = second;
                 tb.blive[blk] = live;
                 tb.dirty[blk] = 0u;
                 s_bm[bit] = best;
+                s_bm2[bit] = second;
             }
         }
     }
     __syncthreads();
-    if (part) {   // this workgroup's maximum, for sel_inline
-        uint64_t best = 0ull;
-        if (wide) {   // one wave over the blocks past the first 64 first
-            if (threadIdx.x < 64)
-                for (uint32_t i = threadIdx.x + 64u; i < per; i += 64u) best = s_bm[i] > best ? s_bm[i] : best;
-        }
+    if (part) {   // this workgroup's two largest keys, for sel_inline (part[2 wg], part[2 wg + 1])
+        uint64_t best = 0ull, second = 0ull;
         if (threadIdx.x < 64) {
-            const uint64_t v = s_bm[threadIdx.x];
-            best = wave_max_u64(v > best ? v : best);
+            best = s_bm[threadIdx.x];
+            second = s_bm2[threadIdx.x];
+            if (wide)   // one wave over the blocks past the first 64
+                for (uint32_t i = threadIdx.x + 64u; i < per; i += 64u) top2_merge(best, second, s_bm[i], s_bm2[i]);
+            wave_top2_u64(best, second, best, second);
             if (threadIdx.x == 0) {
-                part[blockIdx.x] = best;
+                part[2 * blockIdx.x] = best;
+                part[2 * blockIdx.x + 1] = second;
                 if (finish == 2) KTR(5);
             }
         }

@@ -190,6 +190,7 @@ int lex_root_build(gbpe_trainer* t, const S* store, const uint32_t* mul, uint64_
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
     TR_HIP(t, hipMemsetAsync(t->tb.slots, 0, slots * sizeof(uint2), s));
     TR_HIP(t, hipMemsetAsync(t->tb.bmax, 0, (uint64_t)t->tb.nblk * sizeof(uint64_t), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.bmax2, 0, (uint64_t)t->tb.nblk * sizeof(uint64_t), s));
     TR_HIP(t, hipMemsetAsync(t->tb.blive, 0, (uint64_t)t->tb.nblk * sizeof(uint32_t), s));
     TR_HIP(t, hipMemsetAsync(&t->st->used, 0, sizeof(uint32_t), s));
     if (t->lx_len > 1)

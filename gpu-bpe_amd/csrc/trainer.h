@@ -120,6 +120,10 @@ struct gbpe_trainer {
     bool rehash_on = true;       // grow the table inside the sparse loop (GBPE_DEBUG rehash=0: exit, grow, recount)
     uint32_t body_cap = 256;     // most k_body workgroups (one per CU)
     bool body_fit = true;        // the body's workgroups leave the zone's their CUs (GBPE_DEBUG bodyfit=0: off)
+    bool pair_on = true;         // paired launches (GBPE_DEBUG pair=0: one merge per launch)
+    double pair_rate = 0.5;      // second merges per launch of the last paired step (sizes the next step's launches)
+    uint64_t pair_done = 0;      // merges run as the second of a launch (stats)
+    uint32_t ptrace = 0;         // GBPE_DEBUG ptrace=1: every step's form and pairing on stderr
     uint32_t* d_clog = nullptr;  // GBPE_SPARSE_TRACE: per-merge candidate / hit sectors
     uint32_t* h_clog = nullptr;
     FILE* trace = nullptr;
@@ -179,7 +183,7 @@ uint32_t grid_blocks(const gbpe_ctx* ctx, uint32_t nblk, uint32_t per_cu) {
 int part_alloc(gbpe_trainer* t) {
     pool_free(t->ctx, t->part);
     t->part = nullptr;
-    TR_HIP(t, pool_malloc(t->ctx, &t->part, (uint64_t)(t->tb.nblk + 1) * sizeof(uint64_t)));
+    TR_HIP(t, pool_malloc(t->ctx, &t->part, 2ull * (t->tb.nblk + 1) * sizeof(uint64_t)));   // two keys per workgroup
     return GBPE_OK;
 }
 
@@ -189,16 +193,18 @@ int table_resize(gbpe_trainer* t, uint32_t lg) {
     TR_HIP(t, hipStreamSynchronize(s));
     pool_free(t->ctx, t->tb.slots);
     pool_free(t->ctx, t->tb.bmax);
+    pool_free(t->ctx, t->tb.bmax2);
     pool_free(t->ctx, t->tb.dirty);
     pool_free(t->ctx, t->tb.dlist);
     pool_free(t->ctx, t->tb.blive);
-    t->tb.slots = nullptr, t->tb.bmax = nullptr, t->tb.dirty = nullptr, t->tb.dlist = nullptr, t->tb.blive = nullptr;
+    t->tb.slots = nullptr, t->tb.bmax = nullptr, t->tb.bmax2 = nullptr, t->tb.dirty = nullptr, t->tb.dlist = nullptr, t->tb.blive = nullptr;
     const uint64_t slots = 1ull << lg;
     t->table_log2 = lg;
     t->tb.mask = (uint32_t)(slots - 1);
     t->tb.nblk = (uint32_t)(slots >> BLK_LOG2);
     if (pool_malloc(t->ctx, &t->tb.slots, slots * sizeof(uint2)) != hipSuccess ||
         pool_malloc(t->ctx, &t->tb.bmax, t->tb.nblk * sizeof(uint64_t)) != hipSuccess ||
+        pool_malloc(t->ctx, &t->tb.bmax2, t->tb.nblk * sizeof(uint64_t)) != hipSuccess ||
         pool_malloc(t->ctx, &t->tb.dirty, t->tb.nblk * sizeof(uint32_t)) != hipSuccess ||
         pool_malloc(t->ctx, &t->tb.dlist, (t->tb.nblk + 1) * sizeof(uint32_t)) != hipSuccess ||
         pool_malloc(t->ctx, &t->tb.blive, t->tb.nblk * sizeof(uint32_t)) != hipSuccess)
@@ -216,6 +222,7 @@ int table_rebuild(gbpe_trainer* t, bool bytes_only = false) {
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
     TR_HIP(t, hipMemsetAsync(t->tb.slots, 0, slots * sizeof(uint2), s));
     TR_HIP(t, hipMemsetAsync(t->tb.bmax, 0, (uint64_t)t->tb.nblk * sizeof(uint64_t), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.bmax2, 0, (uint64_t)t->tb.nblk * sizeof(uint64_t), s));
     TR_HIP(t, hipMemsetAsync(t->tb.blive, 0, (uint64_t)t->tb.nblk * sizeof(uint32_t), s));
     TR_HIP(t, hipMemsetAsync(&t->st->used, 0, sizeof(uint32_t), s));
     const uint64_t ntiles = gbpe_div_up(t->n, TILE);
@@ -280,6 +287,7 @@ int table_rehash(gbpe_trainer* t, uint32_t lg) {
     const uint64_t slots = (uint64_t)t->tb.mask + 1;
     TR_HIP(t, hipMemsetAsync(t->tb.slots, 0, slots * sizeof(uint2), s));
     TR_HIP(t, hipMemsetAsync(t->tb.bmax, 0, (uint64_t)t->tb.nblk * sizeof(uint64_t), s));
+    TR_HIP(t, hipMemsetAsync(t->tb.bmax2, 0, (uint64_t)t->tb.nblk * sizeof(uint64_t), s));
     TR_HIP(t, hipMemsetAsync(t->tb.blive, 0, (uint64_t)t->tb.nblk * sizeof(uint32_t), s));
     TR_HIP(t, hipMemsetAsync(&t->st->used, 0, sizeof(uint32_t), s));
     hipLaunchKernelGGL(k_rehash, dim3(grid_persistent(t->ctx, gbpe_div_up(nold, TPB), 4)), dim3(TPB), 0, s,
@@ -365,6 +373,7 @@ struct SpGrid {
     uint32_t ztail = 0;   // stale-tail slice blocks of the multi-tile zone k_delta
     uint32_t zone1;   // zone workgroups inside k_body: 1 = zone_one, >= 2 = zone_seg segments, 0 = multi-tile passes
     int bt;       // k_body workgroup size (256 or 1024)
+    bool pair = false;   // launches may run two merges (zone_one in the 256-thread form)
 };
 
 template <typename S>
@@ -435,18 +444,23 @@ int launch_merge_sparse(gbpe_trainer* t, uint32_t round, hipStream_t s, const Sp
     const int bt = inbody ? (g.seg8 ? 2049 : 2048) : g.bt;
     SelShard sh = sel_single(t);
     sh.sub = g.sub;
+    sh.k2 = g.pair ? 1u : 0u;
     if ((uint64_t)g.body + 1 > t->wg_cap)   // k_body's per-workgroup byte counters (and the zone's after them)
         return gbpe_set_error(t->ctx, GBPE_E_INTERNAL, "k_body grid (%u) above its byte counters (%llu)", g.body,
                               (unsigned long long)t->wg_cap);
     // events: [1] k_body [3] zone k_delta + k_compact (multi-tile zone) [2] k_refresh [4]
+    // k_body picks the zone buffers by the state's merge index (a paired launch runs two
+    // merges); the multi-tile kernels below run one merge per launch, so round = index
+    S* zb0 = (S*)t->zbuf[t->zcur];
+    S* zb1 = (S*)t->zbuf[t->zcur ^ 1];
     if (exact)
         launch_body<S, true>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
-                             g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
+                             g.body, zb1, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zb0, z1,
                              (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sh,
                              sp_mul(t), (ZSegState*)t->zseg);
     else
         launch_body<S, false>(bt, gb, s, t->st, round, (S*)sp_body(t), t->sec, t->bits, t->W, g.wpg, t->sig, t->tb,
-                              g.body, (const S*)zo, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zc, z1,
+                              g.body, zb1, (S*)t->wtmp, t->d_clog ? 1u : 0u, t->zst, zb0, z1,
                               (const uint64_t*)t->part, g.refresh, t->d_log, t->grpsum, t->wg_bytes, t->tb, sh,
                               sp_mul(t), (ZSegState*)t->zseg);
     if (timing) TR_HIP(t, hipEventRecord(ev[3], s));
@@ -1242,7 +1256,11 @@ int sp_shrink(gbpe_trainer* t) {
     DevState* hs = t->h_st;
     const uint32_t z = (uint32_t)t->n - hs->B;
     const uint64_t zt = (uint64_t)t->sp_zt * t->last_mc + 64;
-    if (t->sp_shrinks >= SP_SHRINKS_MAX || (uint64_t)z < zt * t->shrink_pct / 100 + 4096) return GBPE_OK;
+    // paired launches run in the zone_one form: a zone just above it whose target fits
+    // shrinks into it (else it stays there until z >= 2 zt + 4096: 1 GiB merges ~12K-25K)
+    const uint64_t zmax1 = zone_max<S>(256);
+    const bool to_one = t->pair_on && z > zmax1 && zt + 512 <= zmax1;
+    if (t->sp_shrinks >= SP_SHRINKS_MAX || ((uint64_t)z < zt * t->shrink_pct / 100 + 4096 && !to_one)) return GBPE_OK;
     S* zc = (S*)t->zbuf[t->zcur];
     S* zo = (S*)t->zbuf[t->zcur ^ 1];
     hipLaunchKernelGGL(k_sp_zone_start<S>, dim3(1), dim3(1024), 0, s, (const S*)zc, (uint32_t)(z - zt), t->d_u32);
@@ -1250,7 +1268,7 @@ int sp_shrink(gbpe_trainer* t) {
     uint32_t L = 0;
     TR_HIP(t, hipMemcpyAsync(&L, t->d_u32, 4, hipMemcpyDeviceToHost, s));
     TR_HIP(t, hipStreamSynchronize(s));
-    if (L < 4096u) return GBPE_OK;
+    if (L < (to_one ? 512u : 4096u)) return GBPE_OK;
     if (t->lex) {   // the front's words join the lexicon (deduplicated among themselves)
         LxPlan lp;
         int rc = lx_analyze<S>(t, (const S*)zc, L, false, lp);
@@ -1360,6 +1378,8 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     // in-loop table growth off, the multi-tile k_delta threshold, the zone target
     t->lex_on = gbpe_debug_knob("lexicon", 1) != 0;
     t->body_fit = gbpe_debug_knob("bodyfit", 1) != 0;
+    t->pair_on = gbpe_debug_knob("pair", 1) != 0;
+    t->ptrace = (uint32_t)gbpe_debug_knob("ptrace", 0);
     t->rehash_on = gbpe_debug_knob("rehash", 1) != 0;
     t->delta_mt = (uint32_t)gbpe_debug_knob("delta_mt", t->delta_mt);
     t->sp_zt = (uint32_t)gbpe_debug_knob("zt", t->sp_zt);

@@ -56,7 +56,7 @@ class TrainerStats(C.Structure):
                 ("ms_sparse", C.c_double), ("ms_body", C.c_double),
                 ("lexicon_builds", C.c_uint32), ("lexicon_fallbacks", C.c_uint32), ("lexicon_words", C.c_uint64),
                 ("lexicon_entries", C.c_uint64), ("lexicon_symbols", C.c_uint64),
-                ("ms_create", C.c_double)]
+                ("ms_create", C.c_double), ("paired_merges", C.c_uint64)]
 
 
 class LexShardInfo(C.Structure):

@@ -181,6 +181,7 @@ typedef struct gbpe_trainer_stats {
     uint64_t lexicon_symbols;     /* symbols of the current lexicon store (separators included) */
     double   ms_create;           /* host wall ms of trainer creation (symbols, word starts, first count):
                                      the part of a run the reference's t_loop excludes (trainer.js:230) */
+    uint64_t paired_merges;       /* merges run as the second merge of a paired k_body launch */
 } gbpe_trainer_stats;
 int gbpe_trainer_stats_get(gbpe_trainer* t, gbpe_trainer_stats* out);
 /* Current symbol stream in the reference u32 layout (bit16 = word start). */

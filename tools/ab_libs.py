@@ -79,7 +79,8 @@ for name in sys.argv[4:]:
             print(json.dumps({"name": name, "s": round(t1 - t0, 4), "s_first4k": round((t4k or t1) - t0, 4),
                               "merges": int(m.shape[0]), "equal": eq,
                               "sparse_exits": int(st.sparse_exits),
-                              "table_slots": int(st.table_slots), "max_live_pairs": int(st.max_live_pairs)}), flush=True)
+                              "table_slots": int(st.table_slots), "max_live_pairs": int(st.max_live_pairs),
+                              "paired": int(getattr(st, "paired_merges", 0))}), flush=True)
         if not eq:
             print(json.dumps({"name": name, "error": "merges differ from the fixture"}), flush=True)
             sys.exit(3)
@@ -112,6 +113,10 @@ def main():
             if p.returncode:
                 print(lp, "rc", p.returncode, p.stderr[-2000:], flush=True)
                 sys.exit(p.returncode)
+            if os.environ.get("AB_STDERR"):   # the children's diagnostics (GBPE_DEBUG=htime=1: [pair], [htime])
+                for line in p.stderr.splitlines():
+                    if line.startswith("["):
+                        print(lp, line, flush=True)
             print(f"round {r} {lp} done", flush=True)
     for (lp, name), v in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
         print(f"{name:8s} {lp:50s} min {min(v):.4f} s  all {[round(x, 4) for x in v]}")

@@ -8,7 +8,9 @@ Times in µs from the first k_body workgroup start; medians over merge buckets.
   ref_*      k_refresh first start, last end     nhit, ncand  workgroups with candidates, sectors
   z_*        zone workgroup (thread 0): selection done, zone loaded, site deltas done, scan, survivors
              staged, window staged, zone stored (then flush)
-  period     k_body start to k_body start, per merge, inside a 128-merge step
+  hit_p1/ver paired launches: the body's first merge's sectors done / the zone's verdict seen
+             (zone_two's z_* stamps: loaded, merge-1 deltas, merge 1 in LDS, verdict, merge 2 in LDS, stored)
+  period     k_body start to k_body start, per launch, inside a 128-merge step
 
 usage: python tools/ktrace_show.py <dump file>
 """
@@ -36,11 +38,12 @@ def main():
         r = ref[ref[:, 0] > 0].astype(np.float64)
         mx = lambda m, c: us(b[m, c].max()) if m.any() else np.nan
         t0abs.append((i * EVERY, t0))
-        rows.append([i * EVERY, us(b[:, 0].max()), us(b[b[:, 1] > 0, 1].max()), mx(zone, 5), mx(idle, 5),
+        rows.append([i * EVERY, us(b[:, 0].max()), mx(b[:, 1] > 0, 1), mx(zone, 5), mx(idle, 5),
                      mx(hit, 2), mx(hit, 3), mx(hit, 4), mx(hit, 5),
                      us(r[:, 0].min()) if len(r) else np.nan, us(r[:, 5].max()) if len(r) else np.nan,
                      hit.sum(), (body[on, 6][hit] >> 8).sum(), on.sum(),
-                     mx(zone, 1), mx(zone, 2), mx(zone, 3), mx(zone, 7), mx(zone, 8), mx(zone, 9), mx(zone, 4)])
+                     mx(zone, 1), mx(zone, 2), mx(zone, 3), mx(zone, 7), mx(zone, 8), mx(zone, 9), mx(zone, 4),
+                     mx(hit & (b[:, 10] > 0), 10), mx(hit & (b[:, 11] > 0), 11), mx(zone, 10), mx(zone, 11)])
     # the merge period inside a step: first k_body start to the one EVERY merges later
     per = {m: np.nan for m, _ in t0abs}
     for (m0, t0), (m1, t1) in zip(t0abs[:-1], t0abs[1:]):
@@ -51,7 +54,7 @@ def main():
     a = np.array(rows)
     names = ["start_max", "sel", "zone", "idle_end", "hit_cand", "hit_sig", "hit_sect", "hit_end", "ref_start",
              "ref_end", "nhit", "ncand", "nwg", "z_sel", "z_load", "z_sites", "z_scan", "z_keep", "z_win", "z_wrote",
-             "period"]
+             "hit_p1", "hit_ver", "z_tail1", "z_rel1", "period"]
     edges = [int(e) for e in os.environ.get("EDGES", "0,150,300,500,1000,2000,4000,8000,16000,24000,40000").split(",")]
     print(f"{'merges':<13}{'n':>5}" + "".join(f"{k:>10}" for k in names))
     for lo, hi in zip(edges[:-1], edges[1:]):
