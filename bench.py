@@ -872,6 +872,7 @@ def root_recount_check(lib, ctx, be, fin):
     o = np.argsort(pids[: cnt.value])
     tp, tc = pids[: cnt.value][o], cts[: cnt.value][o].astype(np.int64)
     t0 = time.perf_counter()
+    lib.gbpe_ctx_trim(ctx)   # the context's idle pooled blocks back before torch allocates beside it
     rp, rc = recount_pairs(fin)
     res = {"final_symbols": int(fin.shape[0]), "final_symbols_equal_trainer": int(fin.shape[0]) == int(st.symbol_count),
            "pairs_live_table": int(tp.shape[0]), "pairs_live_recount": int(rp.shape[0]),

@@ -41,7 +41,7 @@ static uint64_t pool_class(uint64_t b) {
     uint64_t p2 = 256;
     while (p2 < b) p2 <<= 1;
     if (p2 <= (64u << 10)) return p2;
-    const uint64_t step = p2 >> 3;   // <= 1/8 slack above 64 KiB
+    const uint64_t step = p2 >> 4;   // p2 < 2b: a step below b / 8, so <= 1/8 slack above 64 KiB
     return (b + step - 1) / step * step;
 }
 
@@ -70,7 +70,7 @@ hipError_t gbpe_pool_alloc(gbpe_ctx* ctx, void** p, uint64_t bytes, bool host) {
     std::lock_guard<std::mutex> lk(ctx->pool_mu);
     GbpePool& pl = host ? ctx->hpool : ctx->dpool;
     auto it = pl.idle.lower_bound(cls);
-    if (it != pl.idle.end() && it->first <= cls + cls / 4) {
+    if (it != pl.idle.end() && it->first <= cls + cls / 8) {   // (a reused block holds <= 1/8 more than its class)
         *p = it->second;
         pl.busy[*p] = it->first;
         pl.idle_bytes -= it->first;
@@ -115,6 +115,19 @@ void gbpe_pool_trim(gbpe_ctx* ctx) {
     std::lock_guard<std::mutex> lk(ctx->pool_mu);
     pool_release(ctx->dpool, false, 0);
     pool_release(ctx->hpool, true, 0);
+}
+
+// device memory outside the pool (encode, pre-tokenizer and merge-encode buffers):
+// a failed hipMalloc gives the pool's idle blocks back and tries once more, so a
+// context that trained first can still encode
+hipError_t gbpe_dev_malloc(gbpe_ctx* ctx, void** p, uint64_t bytes) {
+    hipError_t e = hipMalloc(p, bytes ? bytes : 1);
+    if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        gbpe_pool_trim(ctx);
+        e = hipMalloc(p, bytes ? bytes : 1);
+    }
+    return e;
 }
 
 extern "C" {
@@ -203,6 +216,12 @@ int gbpe_ctx_limits(gbpe_ctx* ctx, uint64_t* max_buffer_size) {
 }
 
 const char* gbpe_last_error(const gbpe_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int gbpe_ctx_trim(gbpe_ctx* ctx) {
+    if (!ctx) return GBPE_E_INVALID;
+    gbpe_pool_trim(ctx);
+    return GBPE_OK;
+}
 
 int gbpe_device_alloc(gbpe_ctx* ctx, uint64_t bytes, void** dptr) {
     if (!ctx || !dptr) return gbpe_set_error(ctx, GBPE_E_INVALID, "null argument");

@@ -20,8 +20,10 @@
 // context takes them (the same stream orders every use), so creating and
 // destroying a trainer costs no hipMalloc / hipFree once the pool is warm.  Sizes
 // round up to classes of <= 1/8 slack; a miss allocates; an allocation that finds
-// no memory frees the idle blocks and tries again; idle blocks above half the
-// device's memory are freed at once.
+// no memory frees the idle blocks and tries again (so do the library's allocations
+// outside the pool, gbpe_dev_malloc); idle blocks above half the device's memory are
+// freed at once, and gbpe_ctx_trim gives every idle block back (for allocators
+// outside the library).
 struct GbpePool {
     std::multimap<uint64_t, void*> idle;          // class bytes -> block
     std::unordered_map<void*, uint64_t> busy;     // block -> class bytes
@@ -53,6 +55,9 @@ struct gbpe_ctx {
 hipError_t gbpe_pool_alloc(gbpe_ctx* ctx, void** p, uint64_t bytes, bool host = false);
 void gbpe_pool_free(gbpe_ctx* ctx, void* p, bool host = false);
 void gbpe_pool_trim(gbpe_ctx* ctx);
+hipError_t gbpe_dev_malloc(gbpe_ctx* ctx, void** p, uint64_t bytes);   // hipMalloc, trimming the pool on OOM
+template <typename T>
+inline hipError_t dev_malloc(gbpe_ctx* c, T** p, uint64_t n) { return gbpe_dev_malloc(c, (void**)p, n); }
 template <typename T>
 inline hipError_t pool_malloc(gbpe_ctx* c, T** p, uint64_t n) { return gbpe_pool_alloc(c, (void**)p, n); }
 inline void pool_free(gbpe_ctx* c, void* p) { gbpe_pool_free(c, p); }

@@ -439,8 +439,8 @@ extern "C" int gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n
     tr->n_nodes = n_nodes;
     tr->n_edges = n_edges;
     tr->root_base = root_base;
-    hipError_t e = hipMalloc(&tr->rec, rec.size() * sizeof(uint4));
-    if (e == hipSuccess) e = hipMalloc(&tr->root, 256 * sizeof(uint4));
+    hipError_t e = dev_malloc(ctx, &tr->rec, rec.size() * sizeof(uint4));
+    if (e == hipSuccess) e = dev_malloc(ctx, &tr->root, 256 * sizeof(uint4));
     if (e == hipSuccess) e = hipMemcpy(tr->rec, rec.data(), rec.size() * sizeof(uint4), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(tr->root, root.data(), 256 * sizeof(uint4), hipMemcpyHostToDevice);
     // packed records: check (22 bits) | tid low 10 << 22, base (22 bits) | tid high 10 << 22
@@ -453,7 +453,7 @@ extern "C" int gbpe_trie_upload(gbpe_ctx* ctx, const uint32_t* nodes, uint32_t n
             const uint32_t tid = q.z == INV ? 0xFFFFFu : q.z;
             r2[i] = make_uint2(chk | ((tid & 0x3FFu) << 22), (q.y & 0x3FFFFFu) | ((tid >> 10) << 22));
         }
-        e = hipMalloc(&tr->rec2, r2.size() * sizeof(uint2));
+        e = dev_malloc(ctx, &tr->rec2, r2.size() * sizeof(uint2));
         if (e == hipSuccess) e = hipMemcpy(tr->rec2, r2.data(), r2.size() * sizeof(uint2), hipMemcpyHostToDevice);
     }
     if (e != hipSuccess) {
@@ -491,7 +491,7 @@ int grow(gbpe_ctx* ctx, void** p, uint64_t* have, uint64_t need) {
         *have = 0;
     }
     const uint64_t sz = need + need / 2;   // 1.5x amortised growth (tokenizer.js:125-128)
-    GBPE_HIP(ctx, hipMalloc(p, sz));
+    GBPE_HIP(ctx, dev_malloc(ctx, p, sz));
     *have = sz;
     return GBPE_OK;
 }

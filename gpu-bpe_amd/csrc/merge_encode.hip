@@ -279,8 +279,8 @@ extern "C" int gbpe_bpe_upload(gbpe_ctx* ctx, const uint32_t* merges, uint32_t n
     bp->ctx = ctx;
     bp->mask = slots - 1;
     bp->n_live = live;
-    hipError_t e = hipMalloc(&bp->slots, slots * sizeof(uint4));
-    if (e == hipSuccess) e = hipMalloc(&bp->cross, cross.size() * sizeof(uint32_t));
+    hipError_t e = dev_malloc(ctx, &bp->slots, slots * sizeof(uint4));
+    if (e == hipSuccess) e = dev_malloc(ctx, &bp->cross, cross.size() * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemcpy(bp->slots, tab.data(), slots * sizeof(uint4), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(bp->cross, cross.data(), cross.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
@@ -311,7 +311,7 @@ extern "C" int gbpe_bpe_encode(gbpe_ctx* ctx, gbpe_bpe* bp, const uint8_t* bytes
     // device buffers: input, scratch tokens (<= 1 per byte), counts, bases, scan state, output
     const uint64_t need = n + 16 + 4 * n + 4 * nchunks + 8 * nchunks + 4 * nchunks + 8 * (nblk + 2) + 4 * n + 64;
     uint8_t* d = nullptr;
-    GBPE_HIP(ctx, hipMalloc(&d, need));
+    GBPE_HIP(ctx, dev_malloc(ctx, &d, need));
     uint8_t* d_in = d;
     uint32_t* scratch = (uint32_t*)(((uintptr_t)(d + n + 16) + 15) & ~(uintptr_t)15);
     uint32_t* counts = scratch + n;
@@ -328,7 +328,7 @@ extern "C" int gbpe_bpe_encode(gbpe_ctx* ctx, gbpe_bpe* bp, const uint8_t* bytes
     uint64_t* slot = nullptr;
     unsigned long long* d_long = nullptr;
     unsigned long long long_total = 0;
-    if (e == hipSuccess) e = hipMalloc(&slot, nchunks * ME_LSLOT * sizeof(uint64_t) + 16);
+    if (e == hipSuccess) e = dev_malloc(ctx, &slot, nchunks * ME_LSLOT * sizeof(uint64_t) + 16);
     if (e == hipSuccess) {
         d_long = (unsigned long long*)(slot + nchunks * ME_LSLOT);
         e = hipMemsetAsync(d_long, 0, 8, s);
@@ -341,7 +341,7 @@ extern "C" int gbpe_bpe_encode(gbpe_ctx* ctx, gbpe_bpe* bp, const uint8_t* bytes
     if (e == hipSuccess) e = hipMemcpyAsync(&long_total, d_long, 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e == hipSuccess && long_total) {
-        e = hipMalloc(&da, long_total * (3 * sizeof(uint32_t) + 3 * sizeof(uint64_t)) + 64);
+        e = dev_malloc(ctx, &da, long_total * (3 * sizeof(uint32_t) + 3 * sizeof(uint64_t)) + 64);
         if (e == hipSuccess) {
             ar.heap = (uint64_t*)da;
             ar.tok = (uint32_t*)(ar.heap + 3 * long_total);

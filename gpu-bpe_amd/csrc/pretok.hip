@@ -334,8 +334,8 @@ int uni_tables(gbpe_ctx* ctx, const uint16_t** idx, const uint8_t** cls) {
     if (d < 0 || d >= 64) return gbpe_set_error(ctx, GBPE_E_INVALID, "device ordinal out of range");
     UniTables& t = tabs[d];
     if (!t.idx) {
-        GBPE_HIP(ctx, hipMalloc(&t.idx, sizeof(kUniIndex)));
-        GBPE_HIP(ctx, hipMalloc(&t.cls, sizeof(kUniClass)));
+        GBPE_HIP(ctx, dev_malloc(ctx, &t.idx, sizeof(kUniIndex)));
+        GBPE_HIP(ctx, dev_malloc(ctx, &t.cls, sizeof(kUniClass)));
         GBPE_HIP(ctx, hipMemcpy(t.idx, kUniIndex, sizeof(kUniIndex), hipMemcpyHostToDevice));
         GBPE_HIP(ctx, hipMemcpy(t.cls, kUniClass, sizeof(kUniClass), hipMemcpyHostToDevice));
     }
@@ -363,7 +363,7 @@ int gbpe_pretok_gpt4_launch(gbpe_ctx* ctx, const uint8_t* d_bytes, uint64_t n, u
             ctx->pt_agg = nullptr;
             ctx->pt_agg_bytes = 0;
         }
-        GBPE_HIP(ctx, hipMalloc(&ctx->pt_agg, need + need / 2));
+        GBPE_HIP(ctx, dev_malloc(ctx, &ctx->pt_agg, need + need / 2));
         ctx->pt_agg_bytes = need + need / 2;
     }
     uint32_t* agg = (uint32_t*)ctx->pt_agg;
@@ -385,7 +385,7 @@ extern "C" int gbpe_pretokenize_gpt4(gbpe_ctx* ctx, const uint8_t* bytes, uint64
     if (n == 0) return GBPE_OK;
     hipStream_t s = ctx->stream;
     uint8_t* d = nullptr;
-    GBPE_HIP(ctx, hipMalloc(&d, 2 * n));
+    GBPE_HIP(ctx, dev_malloc(ctx, &d, 2 * n));
     hipError_t e = hipMemcpyAsync(d, bytes, n, hipMemcpyHostToDevice, s);
     int rc = e == hipSuccess ? gbpe_pretok_gpt4_launch(ctx, d, n, d + n) : GBPE_E_DEVICE;
     if (rc == GBPE_OK) e = hipMemcpyAsync(ws_out, d + n, n, hipMemcpyDeviceToHost, s);

@@ -897,19 +897,25 @@ __device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const ui
 __device__ __forceinline__ uint32_t* pair_word(ZSegState* zg) { return &zg->pad[1]; }
 
 // Zone workgroup of a paired launch: both merges in one pass over the
-// zone — one load, the first merge's new zone assembled in LDS, the verdict, the
-// second merge on that LDS copy, one store of each zone buffer and one flush.
+// zone — one load, the first merge's zone assembled in LDS, the verdict, the second
+// merge on that LDS copy, one store of each zone buffer and one flush.
+//  * As in zone_one, the threads before the first one holding a site, an A-side or
+//    position lim - 1 keep their symbols in place (the unmoved prefix, rounded down
+//    to whole 128-byte swizzle groups): they neither assemble in LDS nor reload,
+//    and LDS holds that prefix unswizzled (at1 / at2 read either layout).
 //  * The second merge's stale window comes from the first merge's current buffer
 //    with the first's A-side rewrites in place (the reference's ping-pong): those
 //    symbols, [z - mc - 2 mc2, + mc2) of the loaded zone, are staged in wb2 with the
-//    rewrites applied before the LDS copy is overwritten.
-//  * Ref mode verdict: the stale window (and the tail it replaces) may lift a pair
-//    over P2 or change P2's count.  Every zone delta of merge 1 is in the table (an
-//    overflow rejects): P2 must have none, and every pair with a positive delta that
-//    holds no nw must stay below P2 with its count read now (the body workgroups'
-//    adds to such pairs are decrements, so the read bounds the final count from
-//    above).  Pairs of nw come from sites (bounded, Sel2) — except the window's
-//    first pair (s_rej).
+//    rewrites applied before LDS is overwritten.
+//  * Ref-mode verdict: the first merge's stale window (and the tail it replaces) may
+//    lift a pair over P2 or change P2's count.  Every zone delta of merge 1 is in
+//    the table (an overflow rejects): P2's net delta must be 0, and every window
+//    pair with a positive net delta must stay below P2 with its count read now (the
+//    body workgroups' adds to a pair without nw are decrements, so the read bounds
+//    the final count from above).  Pairs of nw come from sites (bounded, Sel2)
+//    except the window's first pair, whose left symbol (the last kept survivor at
+//    lim - 1) is checked: nw or not kept there rejects.  The window pairs' counts
+//    are loaded before the first merge's assembly, so the round trip overlaps it.
 //  * zo ends as the first merge's output with the second's A-side rewrites (a later
 //    window reads it), zc as the second's output.  Rejected: the first merge's
 //    output goes to zo and its rewrites to zc, as zone_one leaves them.
@@ -924,13 +930,13 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
     static_assert(ZPT == ZoneDim<S, BT>::ZPT && ZPT * sizeof(S) % 16 == 0, "zone positions per thread");
     constexpr int V = ZPT * sizeof(S) / 16;
     constexpr uint32_t PV = 16 / sizeof(S), PVL = sizeof(S) == 2 ? 3 : 2;
-    constexpr int MAXPER = NT / BT;
-    static_assert(MAXPER * BT == NT && MAXPER <= 16, "delta table slots per thread");
+    constexpr uint32_t TG = ZPT * sizeof(S) >= 128 ? 1u : 128u / (ZPT * sizeof(S));   // threads per swizzle group
+    constexpr int KV = (ZoneDim<S, BT>::ZWIN + BT - 1) / BT;   // window pairs per thread (m <= mc <= ZWIN)
     auto swz = [](uint32_t o) -> uint32_t {   // 16-byte chunks XOR-swizzled in groups of 8 (zone_one)
         const uint32_t c = o >> PVL;
         return ((c ^ ((c >> 3) & 7u)) << PVL) | (o & (PV - 1u));
     };
-    __shared__ uint32_t s_rej;
+    __shared__ uint32_t s_rej, s_x0, s_tf1, s_tf2;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t a2 = s2.a, b2 = s2.b, n2 = nw + 1u, mc2 = s2.mc;
     const uint32_t pid1 = (a << 16) | b, pid2 = (a2 << 16) | b2;
@@ -939,7 +945,12 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
     while (nslot < (uint32_t)NT && nslot < 4u * (mc + mc2)) nslot <<= 1;
     LdsView lt = lds_view(ltab, nslot);
     lds_clear(lt);
-    if (t == 0) s_rej = 0u;
+    if (t == 0) {
+        s_rej = 0u;
+        s_x0 = 0u;
+        s_tf1 = BT;
+        s_tf2 = BT;
+    }
     // P2's home slot for its commit, loaded while merge 1 runs
     const uint32_t h2i = gbpe_fmix32(pid2) & tb.mask;
     uint64_t h2 = 0;
@@ -962,10 +973,11 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
     if (!EXACT) copy_strided<S, BT, 8>(L.wb, zo + win_src0(gs, mc), 0u, mc);
     __syncthreads();
     if (t == 0) KT(2);
+    KTW(0);
     // ── merge 1: zone_one's site masks and deltas ──
-    uint32_t m = 0, Kz = 0, rwm = 0, wsm = 0;
+    const uint32_t lim = EXACT ? z : z - mc;
+    uint32_t rwm = 0, wsm = 0, keep = 0;
     {
-        const uint32_t lim = EXACT ? z : z - mc;
         const uint32_t xm2 = i0 >= 2 ? (uint32_t)xs[i0 - 2] : 0u, xm1 = i0 >= 1 ? (uint32_t)xs[i0 - 1] : 0u;
         const uint32_t nxr = i0 + ZPT < z ? (uint32_t)xs[i0 + ZPT] : 0u;
         uint32_t eb = 0, ea = 0;
@@ -981,9 +993,12 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
         const uint32_t h_32 = (nxr == b && (ea >> (ZPT - 1))) ? 1u : 0u;
         const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (ZPT + 1));
         const uint32_t below = lane_mask_n(i0, lim, ZPT);
-        const uint32_t surv = inb & ~hitm, keep = surv & below;
+        const uint32_t surv = inb & ~hitm;
+        keep = surv & below;
         rwm = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
         uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
+        if (t == 0) KT(10);
+        KTW(1);
         for (uint32_t ib = (lim > 1u ? lim : 1u) + t; ib < z; ib += 4u * BT) {   // stale tail: old pairs destroyed
             uint32_t kq[4];
 #pragma unroll
@@ -994,7 +1009,8 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
             }
             lds_addk<4>(lt, tb, st, kq, 0xFFFFFFFFu);
         }
-        if (t == 0) KT(10);
+        if (t == 0) KT(11);
+        KTW(2);
         while (rel) {
             const int k = __ffs(rel) - 1;
             rel &= rel - 1;
@@ -1015,96 +1031,137 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
                 }
             }
         }
-        if (t == 0) KT(11);
-        if (!EXACT) {   // the second merge's window source, with merge 1's A-side rewrites
-            const uint32_t w2 = z - mc - 2u * mc2;   // (>= 0: sel_inline's zone rule)
-            if (i0 < w2 + mc2 && i0 + ZPT > w2) {
-#pragma unroll
-                for (int k = 0; k < ZPT; ++k) {
-                    const uint32_t p = i0 + k;
-                    if (p >= w2 && p < w2 + mc2) wb2[p - w2] = (S)(((rwm >> k) & 1u) ? (nw | (x[k] & WS)) : x[k]);
-                }
+        KTW(3);
+        if (!EXACT) {
+            // the second merge's window source [w2, w2 + mc2) (w2 >= 0: sel_inline's rule), strided over
+            // every thread; an A-side (a followed by a B-side b, train.wgsl:482-488) reads back as nw
+            const uint32_t w2 = z - mc - 2u * mc2;
+            for (uint32_t p = w2 + t; p < w2 + mc2; p += BT) {
+                const uint32_t xp = xs[p], xn = p + 1u < z ? (uint32_t)xs[p + 1u] : 0u;
+                wb2[p - w2] = (S)(((xp & TM) == a && xn == b) ? (nw | (xp & WS)) : xp);
             }
+            if (lim >= 1u && lim - 1u >= i0 && lim - 1u < i0 + ZPT) {   // the window's left neighbour, if kept
+                const uint32_t k = lim - 1u - i0;
+                if ((keep >> k) & 1u)
+                    s_x0 = 0x80000000u | (((rwm >> k) & 1u) ? (nw | (x[k] & WS)) : x[k]);
+            }
+        }
+        KTW(4);
+        {   // the unmoved prefix (zone_one)
+            const unsigned long long sm = __ballot((hitm | rwm) != 0u || i0 + ZPT >= lim);
+            if (sm && lane == 0) atomicMin(&s_tf1, (uint32_t)(wid * 64 + __ffsll((long long)sm) - 1));
         }
         const uint32_t kc = __popc(keep);
         const uint32_t incl = wave_scan_incl_u32(kc), tl = wave_sum_u32(__popc(surv & ~below));
         if (lane == 63) L.wsum[wid] = incl;
         if (lane == 0) L.wtail[wid] = tl;
-        __syncthreads();
-        if (t == 0) KT(3);
-        uint32_t pre = incl - kc;
+        KTW(5);
+    }
+    __syncthreads();
+    if (t == 0) KT(3);
+    uint32_t Kz = 0, m = 0, pre = 0;
+    {
+        uint32_t incl_w = 0;
 #pragma unroll
         for (int w2 = 0; w2 < BT / 64; ++w2) {
-            pre += w2 < wid ? L.wsum[w2] : 0u;
+            incl_w += w2 < wid ? L.wsum[w2] : 0u;
             Kz += L.wsum[w2];
             m += L.wtail[w2];
         }
-        // the first merge's zone in LDS over the old copy (every read of it is done)
+        pre = incl_w + wave_scan_incl_u32(__popc(keep)) - __popc(keep);
+    }
+    const uint32_t tf1 = s_tf1 / TG * TG, F1 = tf1 * ZPT;
+    auto at1 = [&](uint32_t p) -> uint32_t {   // the first merge's zone in LDS (position p < z1)
+        return p < F1 ? (uint32_t)xs[p] : (uint32_t)xs[swz(p)];
+    };
+    // the verdict's window pairs: their counts load now and arrive during the assembly
+    const uint32_t woff = mc - m;
+    uint32_t vq[KV];
+    uint64_t vh[KV];
+    if (!EXACT) {
+        const uint32_t x0 = s_x0;
+        if (t == 0 && m && Kz && !(x0 >> 31)) s_rej = 1u;   // the last kept survivor is not at lim - 1
 #pragma unroll
-        for (int k = 0; k < ZPT; ++k) {
-            const uint32_t y = ((rwm >> k) & 1u) ? (nw | (x[k] & WS)) : x[k];
-            const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
-            S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
-            *dst = (S)y;
-        }
-        if (!EXACT && m) {
-            __syncthreads();
-            const uint32_t woff = mc - m;
-            for (uint32_t jb = t; jb < m; jb += 4u * BT) {
-                uint32_t kq[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t j = jb + (uint32_t)k * BT;
-                    kq[k] = 0u;
-                    if (j < m) {
-                        const uint32_t x1 = L.wb[woff + j];
-                        const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : (Kz ? (uint32_t)xs[swz(Kz - 1)] : 0u);
-                        if (!j && (x0 & TM) == nw) s_rej = 1u;   // a pair of the new token that no site made
-                        xs[swz(Kz + j)] = (S)x1;
-                        if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) kq[k] = ((x0 & TM) << 16) | (x1 & TM);
-                    }
+        for (int k = 0; k < KV; ++k) {
+            const uint32_t j = (uint32_t)t + (uint32_t)k * BT;
+            vq[k] = 0u;
+            vh[k] = 0;
+            if (j < m) {
+                const uint32_t x1 = L.wb[woff + j];
+                const uint32_t xl = j ? (uint32_t)L.wb[woff + j - 1] : (Kz ? (x0 & 0x7FFFFFFFu) : 0u);
+                if (!(x1 & WS) && (xl & TM) && (x1 & TM)) {
+                    const uint32_t q = ((xl & TM) << 16) | (x1 & TM);
+                    if ((q >> 16) == nw) s_rej = 1u;   // a pair of the new token that no site made
+                    else vq[k] = q;
                 }
-                lds_addk<4>(lt, tb, st, kq, 1u);
+                // (P1's count is 0 after its commit; P2: its net delta.)  Plain loads, not waited for
+                // here: a line older than the body workgroups' adds to this pair holds a count at
+                // least its final one (those adds are decrements), which only makes the check stricter
+                if (vq[k] && vq[k] != pid1 && vq[k] != pid2)
+                    vh[k] = reinterpret_cast<const uint64_t*>(tb.slots)[gbpe_fmix32(vq[k]) & tb.mask];
             }
         }
-        __syncthreads();
     }
+    KTW(6);
+    // the first merge's zone in LDS past the unmoved prefix (every read of the old copy is done)
+    if ((uint32_t)t >= tf1) {   // (8-symbol chunks no lane of the wave keeps are skipped: the stale tail)
+#pragma unroll
+        for (int c8 = 0; c8 < ZPT; c8 += 8) {
+            if (!__any((keep >> c8) & 0xFFu)) continue;
+#pragma unroll
+            for (int k = c8; k < c8 + 8; ++k) {
+                const uint32_t y = ((rwm >> k) & 1u) ? (nw | (x[k] & WS)) : x[k];
+                const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
+                S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
+                *dst = (S)y;
+            }
+        }
+    }
+    KTW(7);
+    if (!EXACT && m) {
+        __syncthreads();
+        KTW(8);
+        for (uint32_t jb = t; jb < m; jb += 4u * BT) {
+            uint32_t kq[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t j = jb + (uint32_t)k * BT;
+                kq[k] = 0u;
+                if (j < m) {
+                    const uint32_t x1 = L.wb[woff + j];
+                    const uint32_t x0 = j ? (uint32_t)L.wb[woff + j - 1] : (Kz ? at1(Kz - 1) : 0u);
+                    xs[swz(Kz + j)] = (S)x1;
+                    if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) kq[k] = ((x0 & TM) << 16) | (x1 & TM);
+                }
+            }
+            lds_addk<4>(lt, tb, st, kq, 1u);
+        }
+    }
+    KTW(9);
+    __syncthreads();
     const uint32_t z1 = Kz + m;
     if (t == 0) KT(7);
     // ── the verdict ──
     bool rej = false;
     if (!EXACT) {
-        if (t == 0) rej = s_rej != 0u || *lt.ovf != 0u;
-        uint32_t q[MAXPER], d[MAXPER];
-        uint64_t hv[MAXPER];
+        if (t == 0) rej = s_rej != 0u || *lt.ovf != 0u || lds_find(lt, pid2) != 0u;
 #pragma unroll
-        for (int k = 0; k < MAXPER; ++k) {   // every load first: one round trip
-            const uint32_t i = (uint32_t)t + (uint32_t)k * BT;
-            q[k] = i < nslot ? lt.key[i] : 0u;
-            d[k] = i < nslot ? lt.val[i] : 0u;
-            if (q[k] == pid2 && d[k]) rej = true;
-            const bool need = q[k] && (int32_t)d[k] > 0 && (q[k] >> 16) != nw && (q[k] & 0xFFFFu) != nw && q[k] != pid2;
-            if (!need) q[k] = 0u;
-            hv[k] = 0;
-            if (need && q[k] != pid1)   // (P1's own count is 0 after its commit)
-                hv[k] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(&tb.slots[gbpe_fmix32(q[k]) & tb.mask]),
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-#pragma unroll
-        for (int k = 0; k < MAXPER; ++k) {
-            if (!q[k]) continue;
+        for (int k = 0; k < KV; ++k) {
+            if (!vq[k] || vq[k] == pid2) continue;
+            const uint32_t d = lds_find(lt, vq[k]);
+            if ((int32_t)d <= 0) continue;
             uint32_t cnt = 0;
-            if (q[k] != pid1) {
-                if ((uint32_t)hv[k] == q[k]) {
-                    cnt = (uint32_t)(hv[k] >> 32);
+            if (vq[k] != pid1) {
+                if ((uint32_t)vh[k] == vq[k]) {
+                    cnt = (uint32_t)(vh[k] >> 32);
                 } else {
-                    const uint32_t idx = table_find(tb, q[k]);
+                    const uint32_t idx = table_find(tb, vq[k]);
                     cnt = idx == 0xFFFFFFFFu ? 0u : __hip_atomic_load(&tb.slots[idx].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 if ((int32_t)cnt < 0) cnt = 0;
             }
-            const uint64_t c2 = (uint64_t)cnt + d[k];
-            if (c2 > mc2 || (c2 == mc2 && q[k] < pid2)) rej = true;
+            const uint64_t c2 = (uint64_t)cnt + d;
+            if (c2 > mc2 || (c2 == mc2 && vq[k] < pid2)) rej = true;
         }
         rej = __syncthreads_or(rej) != 0;
     }
@@ -1124,19 +1181,29 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
         __hip_atomic_store(pair_word(zg), (gs.epoch << 2) | (rej ? 2u : 3u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         KT(8);
     }
-    auto store_zone = [&](S* dst, uint32_t tot) {   // the LDS zone [0, tot) as 16-byte vectors
+    // the LDS zone's swizzled part [from, tot) to dst as 16-byte vectors (from: a swizzle-group boundary)
+    auto store_lds = [&](S* dst, uint32_t from, uint32_t tot) {
         const uint32_t nfull = tot / PV;
         uint4* dv = reinterpret_cast<uint4*>(dst);
-        for (uint32_t qv = t; qv < nfull; qv += BT) dv[qv] = L.xv[qv ^ ((qv >> 3) & 7u)];
-        for (uint32_t j = nfull * PV + t; j < tot; j += BT) dst[j] = xs[swz(j)];
+        for (uint32_t qv = from / PV + t; qv < nfull; qv += BT) dv[qv] = L.xv[qv ^ ((qv >> 3) & 7u)];
+        for (uint32_t j = std::max(nfull * PV, from) + t; j < tot; j += BT) dst[j] = xs[swz(j)];
+    };
+    auto store_regs = [&](S* dst, const uint32_t (&y)[ZPT]) {   // this thread's ZPT symbols as vectors
+        S e[ZPT];
+#pragma unroll
+        for (int k = 0; k < ZPT; ++k) e[k] = (S)y[k];
+        uint4* dv = reinterpret_cast<uint4*>(dst + i0);
+#pragma unroll
+        for (int k = 0; k < V; ++k) dv[k] = reinterpret_cast<const uint4*>(e)[k];
     };
     if (rej) {   // merge 1 alone: its zone to zo, its rewrites in place in zc (zone_one's result)
         for (uint32_t r = rwm; r; r &= r - 1) {
             const int k = __ffs(r) - 1;
             zc[i0 + k] = (S)(nw | (((wsm >> k) & 1u) ? WS : 0u));
         }
-        store_zone(zo, z1);
-        lds_flush<MAXPER>(lt, tb, st);
+        if ((uint32_t)t < tf1) store_regs(zo, x);
+        store_lds(zo, F1, z1);
+        lds_flush<NT / BT>(lt, tb, st);
         if (t == 0) {
             zst->m = m;
             zst->valid_total = z1 + 1u;
@@ -1144,13 +1211,15 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
         }
         return;
     }
-    // ── merge 2 on the first merge's zone (LDS) ──
-    uint32_t m2 = 0, Kz2 = 0;
+    // ── merge 2 on the first merge's zone (registers for the prefix, LDS past it) ──
+    uint32_t Kz2 = 0, m2 = 0, F2 = 0;
     {
-        const uint32_t lim = EXACT ? z1 : z1 - mc2;
-        auto X = [&](uint32_t p) -> uint32_t { return p < z1 ? (uint32_t)xs[swz(p)] : 0u; };
+        const uint32_t lim2 = EXACT ? z1 : z1 - mc2;
+        auto X = [&](uint32_t p) -> uint32_t { return p < z1 ? at1(p) : 0u; };
+        if ((uint32_t)t >= tf1) {   // (the prefix threads' symbols are their own, unchanged)
 #pragma unroll
-        for (int k = 0; k < ZPT; ++k) x[k] = X(i0 + k);
+            for (int k = 0; k < ZPT; ++k) x[k] = X(i0 + k);
+        }
         const uint32_t xm2 = i0 >= 2 ? X(i0 - 2) : 0u, xm1 = i0 >= 1 ? X(i0 - 1) : 0u, nxr = X(i0 + ZPT);
         uint32_t eb = 0, ea = 0, wsm2 = 0;
 #pragma unroll
@@ -1164,11 +1233,11 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
         const uint32_t h_m1 = (i0 >= 1 && i0 - 1 < z1 && xm1 == b2 && (xm2 & TM) == a2) ? 1u : 0u;
         const uint32_t h_32 = (nxr == b2 && (ea >> (ZPT - 1))) ? 1u : 0u;
         const uint64_t hbits = (uint64_t)h_m1 | ((uint64_t)hitm << 1) | ((uint64_t)h_32 << (ZPT + 1));
-        const uint32_t below = lane_mask_n(i0, lim, ZPT);
-        const uint32_t surv = inb & ~hitm, keep = surv & below;
+        const uint32_t below = lane_mask_n(i0, lim2, ZPT);
+        const uint32_t surv = inb & ~hitm, keep2 = surv & below;
         const uint32_t rw2 = ((hitm >> 1) | (h_32 << (ZPT - 1))) & inb;
         uint32_t rel = ((uint32_t)hbits | (uint32_t)(hbits >> 1) | (uint32_t)(hbits >> 2)) & below & inb;
-        for (uint32_t ib = (lim > 1u ? lim : 1u) + t; ib < z1; ib += 4u * BT) {   // stale tail: old pairs destroyed
+        for (uint32_t ib = (lim2 > 1u ? lim2 : 1u) + t; ib < z1; ib += 4u * BT) {   // stale tail: old pairs destroyed
             uint32_t kq[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -1198,38 +1267,48 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
                 }
             }
         }
-        // the first merge's zone with the second's A-side rewrites -> zo (whole vectors)
-        if (i0 < z1) {
-            S e[ZPT];
+        // the first merge's zone with the second's A-side rewrites -> zo (a later window reads it)
+        uint32_t y[ZPT];
 #pragma unroll
-            for (int k = 0; k < ZPT; ++k) e[k] = (S)(((rw2 >> k) & 1u) ? (n2 | (x[k] & WS)) : x[k]);
-            uint4* dv = reinterpret_cast<uint4*>(zo + i0);
-#pragma unroll
-            for (int k = 0; k < V; ++k) dv[k] = reinterpret_cast<const uint4*>(e)[k];
+        for (int k = 0; k < ZPT; ++k) y[k] = ((rw2 >> k) & 1u) ? (n2 | (x[k] & WS)) : x[k];
+        if (i0 < z1) store_regs(zo, y);
+        {
+            const unsigned long long sm = __ballot((hitm | rw2) != 0u || i0 + ZPT >= lim2);
+            if (sm && lane == 0) atomicMin(&s_tf2, (uint32_t)(wid * 64 + __ffsll((long long)sm) - 1));
         }
-        const uint32_t kc = __popc(keep);
+        const uint32_t kc = __popc(keep2);
         const uint32_t incl = wave_scan_incl_u32(kc), tl = wave_sum_u32(__popc(surv & ~below));
-        __syncthreads();   // every read of the first merge's LDS zone is done (and L.wsum is free)
         if (lane == 63) L.wsum[wid] = incl;
         if (lane == 0) L.wtail[wid] = tl;
-        __syncthreads();
-        uint32_t pre = incl - kc;
+        __syncthreads();   // (every read of the first merge's LDS zone is done)
+        uint32_t pre2 = incl - kc;
 #pragma unroll
         for (int w2 = 0; w2 < BT / 64; ++w2) {
-            pre += w2 < wid ? L.wsum[w2] : 0u;
+            pre2 += w2 < wid ? L.wsum[w2] : 0u;
             Kz2 += L.wsum[w2];
             m2 += L.wtail[w2];
         }
+        const uint32_t tf2 = s_tf2 / TG * TG;
+        F2 = tf2 * ZPT;
+        if ((uint32_t)t < tf2) {   // the unmoved prefix: its symbols are the second merge's output too
+            store_regs(zc, y);
+        } else {
 #pragma unroll
-        for (int k = 0; k < ZPT; ++k) {
-            const uint32_t y = ((rw2 >> k) & 1u) ? (n2 | (x[k] & WS)) : x[k];
-            const uint32_t o = pre + (uint32_t)__popc(keep & ((1u << k) - 1u));
-            S* dst = ((keep >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
-            *dst = (S)y;
+            for (int c8 = 0; c8 < ZPT; c8 += 8) {
+                if (!__any((keep2 >> c8) & 0xFFu)) continue;
+#pragma unroll
+                for (int k = c8; k < c8 + 8; ++k) {
+                    const uint32_t o = pre2 + (uint32_t)__popc(keep2 & ((1u << k) - 1u));
+                    S* dst = ((keep2 >> k) & 1u) ? &xs[swz(o)] : &L.trash[lane];
+                    *dst = (S)y[k];
+                }
+            }
         }
         if (!EXACT && m2) {
             __syncthreads();
-            const uint32_t woff = mc2 - m2;
+            const uint32_t woff2 = mc2 - m2;
+            // left of the window: the last kept survivor, in the second layout past F2, else the first's
+            const uint32_t xk = Kz2 ? (Kz2 - 1u >= F2 ? (uint32_t)xs[swz(Kz2 - 1u)] : at1(Kz2 - 1u)) : 0u;
             for (uint32_t jb = t; jb < m2; jb += 4u * BT) {
                 uint32_t kq[4];
 #pragma unroll
@@ -1237,8 +1316,8 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
                     const uint32_t j = jb + (uint32_t)k * BT;
                     kq[k] = 0u;
                     if (j < m2) {
-                        const uint32_t x1 = wb2[woff + j];
-                        const uint32_t x0 = j ? (uint32_t)wb2[woff + j - 1] : (Kz2 ? (uint32_t)xs[swz(Kz2 - 1)] : 0u);
+                        const uint32_t x1 = wb2[woff2 + j];
+                        const uint32_t x0 = j ? (uint32_t)wb2[woff2 + j - 1] : xk;
                         xs[swz(Kz2 + j)] = (S)x1;
                         if (!(x1 & WS) && (x0 & TM) && (x1 & TM)) kq[k] = ((x0 & TM) << 16) | (x1 & TM);
                     }
@@ -1250,9 +1329,9 @@ __device__ __forceinline__ void zone_two(DevState* st, DevState* zst, const DevS
     }
     const uint32_t z2 = Kz2 + m2;
     if (t == 0) KT(9);
-    store_zone(zc, z2);
+    store_lds(zc, F2, z2);
     if (t == 0) KT(4);
-    lds_flush<MAXPER>(lt, tb, st);
+    lds_flush<NT / BT>(lt, tb, st);
     if (t == 0) {
         zst->m = m + m2;
         zst->valid_total = z2 + 1u;   // survivors + 1 (k_refresh checks it against the new layout)

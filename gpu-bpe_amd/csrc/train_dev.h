@@ -178,7 +178,10 @@ __device__ __forceinline__ void kt_put(uint32_t round, uint32_t wg, int i, unsig
 #define KT(i) kt_put(round, blockIdx.x, (i), wall_clock64())
 #define KTV(i, v) kt_put(round, blockIdx.x, (i), (v))
 #define KTR(i) kt_put(round, KT_WG + blockIdx.x, (i), wall_clock64())
+// per-wave stamps of the zone workgroup (lane 0 of every wave): rows KT_WG - 8 + wave
+#define KTW(i) do { if ((threadIdx.x & 63) == 0) kt_put(round, KT_WG - 8u + (threadIdx.x >> 6), (i), wall_clock64()); } while (0)
 #else
+#define KTW(i) ((void)0)
 #define KT(i) ((void)0)
 #define KTV(i, v) ((void)0)
 #define KTR(i) ((void)0)
@@ -325,6 +328,19 @@ __device__ __forceinline__ void lds_add(LdsView& t, const TB& tb, DevState* st, 
     }
     *t.ovf = 1u;
     table_add(tb, st, pid, d);   // crowded: straight to the global table
+}
+
+// the delta a runtime-sized table holds for pid (0 when absent)
+__device__ __forceinline__ uint32_t lds_find(const LdsView& t, uint32_t pid) {
+    const uint32_t h = gbpe_fmix32(pid);
+#pragma unroll 1
+    for (int p = 0; p < LPROBE; ++p) {
+        const uint32_t idx = (h + (uint32_t)((p * (p + 1)) >> 1)) & t.mask;
+        const uint32_t k = t.key[idx];
+        if (k == pid) return t.val[idx];
+        if (k == 0u) return 0u;
+    }
+    return 0u;
 }
 
 // K adds of one delta with their home-slot compare-and-swaps issued together: the
@@ -879,12 +895,15 @@ __global__ __launch_bounds__(TPB) void k_refresh(DevState* st, uint32_t round, i
 
 // k_refresh in the form its grid needs: more than 64 table blocks per workgroup
 // (the late grids of a large table) take the WIDE form
-#define GBPE_LAUNCH_REFRESH(S, grid, nblk, s, ...)                                               \
-    do {                                                                                         \
-        if ((uint64_t)(grid) * 64u < (uint64_t)(nblk))                                           \
-            hipLaunchKernelGGL((k_refresh<S, true>), dim3(grid), dim3(TPB), 0, s, __VA_ARGS__);  \
-        else                                                                                     \
-            hipLaunchKernelGGL((k_refresh<S, false>), dim3(grid), dim3(TPB), 0, s, __VA_ARGS__); \
+// (the grid is clamped to >= nblk / TPB: a workgroup re-maxes at most TPB blocks, one
+// per thread, so a smaller grid would leave blocks' maxima stale)
+#define GBPE_LAUNCH_REFRESH(S, grid, nblk, s, ...)                                                          \
+    do {                                                                                                    \
+        const uint32_t g_ = std::max<uint32_t>((uint32_t)(grid), (uint32_t)(((uint64_t)(nblk) + TPB - 1) / TPB)); \
+        if ((uint64_t)g_ * 64u < (uint64_t)(nblk))                                                          \
+            hipLaunchKernelGGL((k_refresh<S, true>), dim3(g_), dim3(TPB), 0, s, __VA_ARGS__);               \
+        else                                                                                                \
+            hipLaunchKernelGGL((k_refresh<S, false>), dim3(g_), dim3(TPB), 0, s, __VA_ARGS__);              \
     } while (0)
 
 constexpr uint32_t GRP = 64;    // tiles per group sum (two-level tile prefix)

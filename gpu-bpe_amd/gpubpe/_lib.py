@@ -73,6 +73,7 @@ PROGRESS_CB = C.CFUNCTYPE(C.c_int, C.POINTER(Progress), u32p, C.c_void_p)
 _SIGS = [
     ("gbpe_ctx_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     ("gbpe_ctx_destroy", None, [C.c_void_p]),
+    ("gbpe_ctx_trim", C.c_int, [C.c_void_p]),
     ("gbpe_ctx_limits", C.c_int, [C.c_void_p, u64p]),
     ("gbpe_last_error", C.c_char_p, [C.c_void_p]),
     ("gbpe_version", C.c_char_p, []),

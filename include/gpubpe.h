@@ -55,6 +55,10 @@ typedef struct gbpe_trie gbpe_trie;
  *    engine.js:216-238 BPEEngine.init) ─────────────────────────────────── */
 int  gbpe_ctx_create(int device_ordinal, gbpe_ctx** out);
 void gbpe_ctx_destroy(gbpe_ctx* ctx);
+/* Give the context's idle pooled device / pinned blocks back to the runtime (the
+   pool keeps freed trainer buffers for the next trainer, tokenizer.js:30-46): for
+   callers about to allocate outside the library (no reference counterpart). */
+int gbpe_ctx_trim(gbpe_ctx* ctx);
 /* engine.js:207-210 `limits.maxBufferSize` (used by tokenizer.js:181 for
  * multi-pass slicing).  This engine has no per-buffer cap below HBM size. */
 int  gbpe_ctx_limits(gbpe_ctx* ctx, uint64_t* max_buffer_size);

@@ -122,12 +122,15 @@ def test_sparse_vs_dense_full_c2(eng):
     assert st1.tail_dropped == st2.tail_dropped == meta["tail_total"]
 
 
-@pytest.mark.parametrize("table_log2", [18, 20])
+@pytest.mark.parametrize("table_log2", [14, 15, 18, 20])
 def test_sparse_wide_refresh_workgroups(eng, monkeypatch, table_log2):
-    # late k_refresh grids take up to 1,024 table blocks per workgroup (C5's 2^25
-    # slots: 128 partial maxima per selection instead of 2,048); rfl=1 with a late
-    # threshold above every zone forces the widest form from the first step:
-    # 2^18 slots -> one workgroup over all 1,024 blocks, 2^20 -> 4 x 1,024
+    # late k_refresh grids take up to 256 table blocks per workgroup (TPB: C5's
+    # 2^25 slots give 512 partial maxima per selection instead of 2,048); rfl=1
+    # with a late threshold above every zone forces the widest form from the first
+    # step: the grid is ceil(blocks / 256), so 2^18 slots (1,024 blocks) -> 4
+    # workgroups of 256, 2^20 -> 16 x 256; 2^14 (64 blocks) is the narrow form's
+    # largest workgroup and 2^15 (128 blocks, one workgroup) the wide form's
+    # smallest (the boundary at 64 vs 65+ blocks per workgroup)
     from gpubpe import synth
     monkeypatch.setenv("GBPE_DEBUG", "rfl=1,rflz=100000000")
     data = synth.english(300000, seed=41)

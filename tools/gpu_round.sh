@@ -8,6 +8,8 @@
 #   'ab=LIBS -- NAMES'  tools/ab_libs.py LIBS -- NAMES (LIBS ' '-, NAMES ','-separated; AB_REPS / AB_ROUNDS
 #                       from the environment)                    -> OUT/ab.txt
 #   stats=ARGS          rocprofv3 --kernel-trace --stats over bench.py ARGS -> OUT/prof
+#   c4=RANKS:SHARD      the C4 leg's self-check rehearsed with RANKS ranks sharing this one GPU over gloo
+#                       (host-staged hand-over), SHARD bytes per rank -> OUT/c4_RANKSr_SHARD.json
 #   'pmc=CTRS -- ARGS'  one rocprofv3 --pmc pass (CTRS ','-separated) over bench.py ARGS -> OUT/pmc_*
 set -o pipefail
 export TMPDIR=/tmp
@@ -52,6 +54,13 @@ for step in "$@"; do
       timeout -s KILL 300 rocprofv3 --pmc ${ctrs//,/ } -d "$O/pmc$n" -o run -- python3 bench.py $args \
         > "$O/pmc$n.json" 2> "$O/pmc$n.err" || { echo PMCFAIL; tail -20 "$O/pmc$n.err"; exit 1; }
       echo "pmc$n done" ;;
+    c4)
+      rk=${arg%%:*}
+      sh=${arg#*:}
+      GBPE_BENCH_DEVICE=0 GBPE_SHARD_TRANSPORT=gloo timeout -k 10 900 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node $rk --master-addr 127.0.0.1 --master-port 29574 bench.py --gpus $rk --c4-only --c4-shard $sh \
+        > "$O/c4_${rk}r_$sh.json" 2> "$O/c4_${rk}r_$sh.err" || { echo C4FAIL; tail -30 "$O/c4_${rk}r_$sh.err"; exit 1; }
+      python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);c=d['c4'];print('c4',c['value'],c.get('counts_equal_recount'),c['timing_s_max_over_ranks'])" "$O/c4_${rk}r_$sh.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

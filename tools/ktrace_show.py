@@ -24,9 +24,9 @@ EVERY, WG, SLOTS, HZ = 16, 2048, 12, 100e6
 
 def main():
     raw = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 2 * WG, SLOTS)
-    rows, t0abs = [], []
+    rows, t0abs, zrows = [], [], []
     for i in range(raw.shape[0]):
-        body, ref = raw[i, :WG], raw[i, WG:]
+        body, ref, zw = raw[i, :WG - 8], raw[i, WG:], raw[i, WG - 8:WG]
         on = body[:, 0] > 0
         if not on.any():
             continue
@@ -38,6 +38,8 @@ def main():
         r = ref[ref[:, 0] > 0].astype(np.float64)
         mx = lambda m, c: us(b[m, c].max()) if m.any() else np.nan
         t0abs.append((i * EVERY, t0))
+        zwv = [[us(zw[w, k]) if zw[w, k] > 0 else np.nan for k in range(10)] for w in range(4)]
+        zrows.append([i * EVERY] + [v for w in zwv for v in w])
         rows.append([i * EVERY, us(b[:, 0].max()), mx(b[:, 1] > 0, 1), mx(zone, 5), mx(idle, 5),
                      mx(hit, 2), mx(hit, 3), mx(hit, 4), mx(hit, 5),
                      us(r[:, 0].min()) if len(r) else np.nan, us(r[:, 5].max()) if len(r) else np.nan,
@@ -54,7 +56,7 @@ def main():
     a = np.array(rows)
     names = ["start_max", "sel", "zone", "idle_end", "hit_cand", "hit_sig", "hit_sect", "hit_end", "ref_start",
              "ref_end", "nhit", "ncand", "nwg", "z_sel", "z_load", "z_sites", "z_scan", "z_keep", "z_win", "z_wrote",
-             "hit_p1", "hit_ver", "z_tail1", "z_rel1", "period"]
+             "hit_p1", "hit_ver", "z_masks", "z_tail", "period"]
     edges = [int(e) for e in os.environ.get("EDGES", "0,150,300,500,1000,2000,4000,8000,16000,24000,40000").split(",")]
     print(f"{'merges':<13}{'n':>5}" + "".join(f"{k:>10}" for k in names))
     for lo, hi in zip(edges[:-1], edges[1:]):
@@ -63,7 +65,24 @@ def main():
             continue
         med = [np.nanmedian(a[sel, j]) if np.isfinite(a[sel, j]).any() else np.nan for j in range(1, a.shape[1])]
         print(f"{lo:>6}-{hi:<6}{int(sel.sum()):>5}" + "".join(f"{v:>10.2f}" for v in med))
+    if zrows:
+        zone_waves(zrows, edges)
 
+
+
+def zone_waves(zrows, edges):
+    """zone_two's per-wave stamps (KTW: 0 loaded, 1 masks, 2 tail, 3 rel, 4 wb2, 5 scan written,
+    6 after the scan barrier, 7 assembled, 8 window start, 9 window done), medians per bucket"""
+    a = np.array(zrows)
+    for lo, hi in zip(edges[:-1], edges[1:]):
+        sel = (a[:, 0] >= lo) & (a[:, 0] < hi)
+        if not sel.any() or np.isnan(a[sel, 1:]).all():
+            continue
+        med = np.nanmedian(a[sel, 1:], axis=0).reshape(4, 10)
+        print(f"zone waves {lo}-{hi}:")
+        for w in range(4):
+            print("   wave %d " % w + " ".join("%6.2f" % v for v in med[w]))
 
 if __name__ == "__main__":
     main()
+

@@ -6,7 +6,8 @@ reads are mostly narrow gathers, for which the doubling is uncalibrated.
 
   kbody:  python tools/pmc_r2.py kbody <fetch dir> <write dir> <explore json line file> <out.json>
           window = one full en1g training run (tools/explore_1g.py en1g); algorithmic bytes
-          per launch = that run's k_body byte counter / its sparse merges
+          per launch = that run's k_body byte counter / its k_body launches (sparse merges
+          minus paired merges)
   encode: python tools/pmc_r2.py encode <fetch dir> <write dir> <encode json file> <out.json>
           window = one C3 encode (tools/encode_once.py); algorithmic bytes n + 4T
 """
@@ -30,7 +31,8 @@ def main():
     mode, fd, wd, jf, out = sys.argv[1:6]
     info = json.loads([ln for ln in open(jf).read().splitlines() if ln.startswith("{")][-1])
     if mode == "kbody":
-        n = int(info["stats"]["sparse_merges"])
+        # k_body launches of the run: one per sparse merge, one per pair of a paired launch
+        n = int(info["stats"]["sparse_merges"]) - int(info["stats"].get("paired_merges", 0))
         fetch, write = per_dispatch(fd, "FETCH_SIZE", ["k_body"])[-n:], per_dispatch(wd, "WRITE_SIZE", ["k_body"])[-n:]
         k = min(len(fetch), len(write))
         raw, wr = sum(fetch[-k:]) / k, sum(write[-k:]) / k
