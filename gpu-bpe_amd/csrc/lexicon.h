@@ -118,14 +118,25 @@ struct alignas(16) LxSlot {
     uint32_t cnt;             // occurrences; the uid once k_lx_tabuid ran
 };
 
-// global word table (linear probing on 64-bit keys): insert-or-add `c` occurrences.
-// A key never changes once set (0 -> h), so the probes are plain loads that may
-// hit a stale copy in this XCD's L2: a stale 0 only sends the probe to the CAS,
+// The word table is cut into slices (at most 256, of >= 4096 slots unless the table is
+// smaller) and a probe sequence wraps inside its home slot's slice: the two-stage
+// build (k_lx_hash's bucketed flush + k_lx_fold) gives every slice one workgroup.
+__device__ __forceinline__ uint32_t lx_slice(uint32_t P) { return P >= (1u << 20) ? P >> 8 : (P < 4096u ? P : 4096u); }
+__device__ __forceinline__ uint32_t lx_next(uint32_t slot, uint32_t sm) { return (slot & ~sm) | ((slot + 1u) & sm); }
+__device__ __forceinline__ uint32_t lx_bucket(unsigned long long h, uint32_t P) {
+    return lx_home(h, P - 1) / lx_slice(P);
+}
+
+// global word table (linear probing on 64-bit keys, inside the home slice): insert-or-add
+// `c` occurrences.  A key never changes once set (0 -> h), so the probes are plain loads
+// that may hit a stale copy in this XCD's L2: a stale 0 only sends the probe to the CAS,
 // which returns the key actually there (agent-scope probe loads go to memory).
 __device__ bool lx_insert(LxSlot* __restrict__ wt, uint32_t P, unsigned long long h, uint32_t rep, uint32_t c,
                           uint32_t maxp = LX_PROBES) {
+    const uint32_t sm = lx_slice(P) - 1u;
     uint32_t slot = lx_home(h, P - 1);
-    for (uint32_t p = 0; p < maxp; ++p, slot = (slot + 1) & (P - 1)) {
+    if (maxp > sm + 1u) maxp = sm + 1u;
+    for (uint32_t p = 0; p < maxp; ++p, slot = lx_next(slot, sm)) {
         unsigned long long k = wt[slot].key;
         if (k == 0ull) {
             k = atomicCAS(&wt[slot].key, 0ull, h);
@@ -145,8 +156,9 @@ __device__ bool lx_insert(LxSlot* __restrict__ wt, uint32_t P, unsigned long lon
 
 // the slot of key h (its whole 16 bytes in one load), or SP_INV in .z
 __device__ uint4 lx_find(const LxSlot* __restrict__ wt, uint32_t P, unsigned long long h) {
+    const uint32_t sm = lx_slice(P) - 1u;
     uint32_t slot = lx_home(h, P - 1);
-    for (uint32_t p = 0; p < LX_PROBES; ++p, slot = (slot + 1) & (P - 1)) {
+    for (uint32_t p = 0; p <= sm && p < LX_PROBES; ++p, slot = lx_next(slot, sm)) {
         const uint4 v = *reinterpret_cast<const uint4*>(&wt[slot]);
         const unsigned long long k = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
         if (k == h) return v;
@@ -166,22 +178,31 @@ __device__ uint4 lx_find(const LxSlot* __restrict__ wt, uint32_t P, unsigned lon
 // wmul (weighted analysis, the lexicon hand-over of DESIGN §5): a word counts
 // wmul[its first position] occurrences instead of one — the segment is then a
 // concatenation of word stores, each word carrying its multiplicity.
-template <typename S>
-__global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32_t len, const uint32_t* __restrict__ wpos,
+// rec (the two-stage build of a large segment; launched as 1,024-thread
+// workgroups with an 8,192-slot LDS table, so a workgroup's distinct words fit it and
+// do not overflow into global inserts): instead of adding its entries to the global
+// table, the workgroup writes them as LxSlot records to its own region
+// rec[blockIdx.x * LT ...], grouped by word-table slice (bucket), with the groups'
+// offsets and sizes in bmeta[0 / 1][blockIdx.x * nbk + bucket]; k_lx_fold then folds
+// every bucket in one workgroup's LDS and inserts each distinct word once.
+template <typename S, int BT = TPB, int LT = LX_LT>
+__global__ __launch_bounds__(BT) void k_lx_hash(const S* __restrict__ x, uint32_t len, const uint32_t* __restrict__ wpos,
                                                  uint32_t nw, LxSlot* __restrict__ wtab,
                                                  uint32_t P, uint32_t* __restrict__ otmp, uint32_t* __restrict__ longs,
                                                  uint32_t* __restrict__ ctr, const uint32_t* __restrict__ wmul,
-                                                 uint32_t maxp, uint32_t wpt) {
-    __shared__ unsigned long long lk[LX_LT];
-    __shared__ uint32_t lc[LX_LT], lr[LX_LT];
-    for (int i = threadIdx.x; i < LX_LT; i += TPB) {
+                                                 uint32_t maxp, uint32_t wpt, LxSlot* __restrict__ rec = nullptr,
+                                                 uint32_t* __restrict__ bmeta = nullptr, uint32_t nbk = 0,
+                                                 uint32_t nwg = 0) {
+    __shared__ unsigned long long lk[LT];
+    __shared__ uint32_t lc[LT], lr[LT];
+    for (int i = threadIdx.x; i < LT; i += BT) {
         lk[i] = 0ull;
         lc[i] = 0u;
     }
     __syncthreads();
-    const uint64_t j0 = (uint64_t)blockIdx.x * TPB * wpt;
+    const uint64_t j0 = (uint64_t)blockIdx.x * BT * wpt;
     for (uint32_t q = 0; q < wpt; ++q) {
-        const uint64_t j = j0 + (uint64_t)q * TPB + threadIdx.x;
+        const uint64_t j = j0 + (uint64_t)q * BT + threadIdx.x;
         if (j >= nw) break;
         const uint32_t s = wpos[j], e = j + 1 < nw ? wpos[j + 1] : len, L = e - s;
         const uint32_t v0 = x[s];
@@ -198,9 +219,9 @@ __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32
         otmp[j] = 0u;
         const uint32_t wt = wmul ? wmul[s] : 1u;
         const unsigned long long h = lx_hash<S>(x, s, L);
-        uint32_t slot = lx_home(h, LX_LT - 1);
+        uint32_t slot = lx_home(h, LT - 1);
         bool done = false;
-        for (int p = 0; p < 32 && !done; ++p, slot = (slot + 1) & (LX_LT - 1)) {
+        for (int p = 0; p < 32 && !done; ++p, slot = (slot + 1) & (LT - 1)) {
             const unsigned long long o = atomicCAS(&lk[slot], 0ull, h);
             if (o == 0ull) {
                 lr[slot] = (uint32_t)j;
@@ -214,29 +235,126 @@ __global__ __launch_bounds__(TPB) void k_lx_hash(const S* __restrict__ x, uint32
         if (!done && !lx_insert(wtab, P, h, (uint32_t)j, wt, maxp)) ctr[1] = 1u;
     }
     __syncthreads();
+    constexpr int FL = LT / BT;
+    if (rec) {   // two-stage: the entries as records, grouped by bucket (k_lx_fold adds them)
+        __shared__ uint32_t s_bc[256], s_bo[256], s_ws[BT / 64];
+        for (uint32_t i = threadIdx.x; i < 256; i += BT) s_bc[i] = 0u;
+        __syncthreads();
+        unsigned long long fk[FL];
+        uint32_t bk[FL], rk[FL];
+#pragma unroll
+        for (int q = 0; q < FL; ++q) {
+            fk[q] = lk[threadIdx.x + q * BT];
+            bk[q] = fk[q] ? lx_bucket(fk[q], P) : 0u;
+            rk[q] = fk[q] ? atomicAdd(&s_bc[bk[q]], 1u) : 0u;
+        }
+        __syncthreads();
+        {   // exclusive scan of the bucket sizes (nbk <= 256 = BT: one per thread)
+            const uint32_t v = threadIdx.x < nbk ? s_bc[threadIdx.x] : 0u;
+            const uint32_t incl = wave_scan_incl_u32(v);
+            if ((threadIdx.x & 63) == 63) s_ws[threadIdx.x >> 6] = incl;
+            __syncthreads();
+            uint32_t pre = incl - v;
+            for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) pre += s_ws[w];
+            if (threadIdx.x < nbk) {
+                s_bo[threadIdx.x] = pre;
+                bmeta[(uint64_t)blockIdx.x * nbk + threadIdx.x] = pre;
+                bmeta[(uint64_t)nwg * nbk + (uint64_t)blockIdx.x * nbk + threadIdx.x] = v;
+            }
+        }
+        __syncthreads();
+        LxSlot* r = rec + (uint64_t)blockIdx.x * LT;
+#pragma unroll
+        for (int q = 0; q < FL; ++q) {
+            if (!fk[q]) continue;
+            const int i = threadIdx.x + q * BT;
+            *reinterpret_cast<uint4*>(&r[s_bo[bk[q]] + rk[q]]) =
+                make_uint4((uint32_t)fk[q], (uint32_t)(fk[q] >> 32), lr[i], lc[i]);
+        }
+        return;
+    }
     // a table already known to be too small (the build is redone or abandoned): no probing
     if (__hip_atomic_load(&ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    // the thread's LX_LT / TPB entries: every home-slot probe issued together, the
+    // the thread's LT / BT entries: every home-slot probe issued together, the
     // adds of the words found there last (no later load waits behind them)
-    constexpr int FL = LX_LT / TPB;
     unsigned long long fk[FL], hk[FL];
     uint32_t fs[FL];
 #pragma unroll
     for (int q = 0; q < FL; ++q) {
-        fk[q] = lk[threadIdx.x + q * TPB];
+        fk[q] = lk[threadIdx.x + q * BT];
         fs[q] = lx_home(fk[q], P - 1);
         hk[q] = fk[q] ? wtab[fs[q]].key : 0ull;
     }
     bool home[FL];
 #pragma unroll
     for (int q = 0; q < FL; ++q) {
-        const int i = threadIdx.x + q * TPB;
+        const int i = threadIdx.x + q * BT;
         home[q] = fk[q] && hk[q] == fk[q];
         if (fk[q] && !home[q] && !lx_insert(wtab, P, fk[q], lr[i], lc[i], maxp)) ctr[1] = 1u;
     }
 #pragma unroll
     for (int q = 0; q < FL; ++q)
-        if (home[q]) atomicAdd(&wtab[fs[q]].cnt, lc[threadIdx.x + q * TPB]);
+        if (home[q]) atomicAdd(&wtab[fs[q]].cnt, lc[threadIdx.x + q * BT]);
+}
+
+// Second stage of the two-stage build: bucket blockIdx.x's records of every
+// k_lx_hash workgroup, folded in LDS (a word repeated across workgroups becomes one
+// entry), then inserted into the bucket's own slice of the word table — no other
+// workgroup touches it, so the inserts do not contend.  A full LDS table sends the
+// record straight to the global table.  Each thread takes whole workgroup groups,
+// their sizes loaded FOLD_B at a time and their records FOLD_R at a time.
+constexpr int FOLD_T = 1024, FOLD_LT = 8192, FOLD_B = 8, FOLD_R = 8;
+__global__ __launch_bounds__(FOLD_T) void k_lx_fold(const LxSlot* __restrict__ rec, const uint32_t* __restrict__ bmeta,
+                                                    uint32_t nwg, uint32_t nbk, LxSlot* __restrict__ wtab, uint32_t P,
+                                                    uint32_t* __restrict__ ctr, uint32_t maxp, uint32_t rstride) {
+    __shared__ unsigned long long fk[FOLD_LT];
+    __shared__ uint32_t fc[FOLD_LT], fr[FOLD_LT];
+    if (__hip_atomic_load(&ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;   // (stage 1 gave up)
+    for (int i = threadIdx.x; i < FOLD_LT; i += FOLD_T) {
+        fk[i] = 0ull;
+        fc[i] = 0u;
+    }
+    __syncthreads();
+    const uint32_t b = blockIdx.x;
+    bool fail = false;
+    for (uint32_t w0 = threadIdx.x; w0 < nwg; w0 += FOLD_T * FOLD_B) {
+        uint32_t st[FOLD_B], n[FOLD_B];
+#pragma unroll
+        for (int k = 0; k < FOLD_B; ++k) {
+            const uint32_t w = w0 + (uint32_t)k * FOLD_T;
+            st[k] = w < nwg ? bmeta[(uint64_t)w * nbk + b] : 0u;
+            n[k] = w < nwg ? bmeta[(uint64_t)nwg * nbk + (uint64_t)w * nbk + b] : 0u;
+        }
+#pragma unroll 1
+        for (int k = 0; k < FOLD_B; ++k) {
+            const uint4* r = reinterpret_cast<const uint4*>(rec + (uint64_t)(w0 + (uint32_t)k * FOLD_T) * rstride + st[k]);
+            for (uint32_t i0 = 0; i0 < n[k]; i0 += FOLD_R) {
+                uint4 v[FOLD_R];
+#pragma unroll
+                for (int q = 0; q < FOLD_R; ++q) v[q] = i0 + q < n[k] ? r[i0 + q] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+                for (int q = 0; q < FOLD_R; ++q) {
+                    const unsigned long long h = (unsigned long long)v[q].x | ((unsigned long long)v[q].y << 32);
+                    if (!h) continue;
+                    uint32_t slot = lx_home(h, FOLD_LT - 1);
+                    bool done = false;
+                    for (int p = 0; p < 64 && !done; ++p, slot = (slot + 1) & (FOLD_LT - 1)) {
+                        const unsigned long long o = atomicCAS(&fk[slot], 0ull, h);
+                        if (o == 0ull) fr[slot] = v[q].z;
+                        if (o == 0ull || o == h) {
+                            atomicAdd(&fc[slot], v[q].w);
+                            done = true;
+                        }
+                    }
+                    if (!done && !lx_insert(wtab, P, h, v[q].z, v[q].w, maxp)) fail = true;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < FOLD_LT; i += FOLD_T)
+        if (fk[i] && !lx_insert(wtab, P, fk[i], fr[i], fc[i], maxp)) fail = true;
+    if (fail) ctr[1] = 1u;
 }
 
 constexpr uint32_t LX_TB = TPB * 16;   // word-table slots per uid-assignment block

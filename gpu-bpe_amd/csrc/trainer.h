@@ -105,6 +105,7 @@ struct gbpe_trainer {
     uint32_t body_min = 256;     // k_body workgroups at least, one bitmap word each at most (GBPE_DEBUG bmin;
                                  // 1 = the round-4 sizing of >= 16 / 32 words per workgroup)
     uint32_t lx_wg = 16384;      // k_lx_hash workgroups (at least LX_WPT words per thread; GBPE_DEBUG lxwg)
+    bool lx_two = true;          // two-stage word-table build for large segments (GBPE_DEBUG lxtwo=0: one stage)
     uint32_t lx_resize = 0;      // builds whose sampled table was too small (rerun at full size)
     uint32_t lx_div = 16;        // with the lexicon: enter once next_mc * lx_div <= n, from the first step on (GBPE_DEBUG lxdiv)
     uint32_t sub_zone = 1u << 20;   // sparse steps run in sub-steps of sub_k merges while the zone exceeds this
@@ -782,8 +783,17 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
     uint64_t Pfull = 4096;
     while (Pfull < 2ull * nw && Pfull < (1ull << 27)) Pfull <<= 1;
     const uint64_t nbbf = gbpe_div_up(Pfull, LX_TB);
+    // the two-stage build (k_lx_hash records + k_lx_fold) for a large segment: its
+    // records (LX_LT per stage-1 workgroup) and bucket offsets / sizes
+    const auto wpt_of = [&](uint64_t nh) {
+        return (uint32_t)std::max<uint64_t>(LX_WPT, gbpe_div_up(nh, (uint64_t)TPB * t->lx_wg));
+    };
+    constexpr uint32_t LX2_T = 1024, LX2_LT = 8192, LX2_WPT = 16;   // the two-stage build's first stage
+    const uint64_t nwg_max = gbpe_div_up(nw, (uint64_t)LX2_T * LX2_WPT);
+    const bool two = t->lx_two && nw >= (1u << 20);
     const uint64_t need = 9ull * (nw + 64) * 4 + Pfull * 16 + (nbbf + 64) * 4 +
-                          2 * (nbbf / SCAN_BLK + (uint64_t)nw / SCAN_BLK + 8) * 8 + 32 * 256;
+                          2 * (nbbf / SCAN_BLK + (uint64_t)nw / SCAN_BLK + 8) * 8 + 32 * 256 +
+                          (two ? nwg_max * LX2_LT * sizeof(LxSlot) + 2 * nwg_max * 256 * 4 + 1024 : 0);
     int rc = lx_scratch(t, need);
     if (rc != GBPE_OK) return rc;
     LxCarve c{(char*)t->lx_tmp};
@@ -799,6 +809,8 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
     uint64_t* bb = c.take<uint64_t>(nbbf / SCAN_BLK + 4);
     lp.ublk = c.take<uint64_t>((uint64_t)nw / SCAN_BLK + 4);
     uint32_t* ctr = c.take<uint32_t>(8);
+    LxSlot* rec = two ? c.take<LxSlot>(nwg_max * LX2_LT) : nullptr;
+    uint32_t* bmeta = two ? c.take<uint32_t>(2 * nwg_max * 256) : nullptr;
     hipLaunchKernelGGL(k_lx_wpos<S>, dim3((uint32_t)ntiles), dim3(TPB), 0, s, seg, len, (const uint32_t*)tc,
                        (const uint64_t*)tb, lp.wpos);
     uint32_t h[4] = {0, 0, 0, 0};
@@ -809,10 +821,20 @@ int lx_analyze(gbpe_trainer* t, const S* seg, uint32_t len, bool fresh, LxPlan& 
         TR_HIP(t, hipMemsetAsync(wtab, 0, P * sizeof(LxSlot), s));
         TR_HIP(t, hipMemsetAsync(ctr, 0, 32, s));
         if (nh) {
-            const uint32_t wpt = (uint32_t)std::max<uint64_t>(LX_WPT, gbpe_div_up(nh, (uint64_t)TPB * t->lx_wg));
-            hipLaunchKernelGGL(k_lx_hash<S>, dim3((uint32_t)gbpe_div_up(nh, (uint64_t)TPB * wpt)), dim3(TPB), 0, s, seg, len,
-                               (const uint32_t*)lp.wpos, nh, wtab, (uint32_t)P, otmp, longs, ctr, wmul,
-                               P < Pfull ? 256u : LX_PROBES, wpt);   // an estimated table gives up early when short
+            const uint32_t maxp = P < Pfull ? 256u : LX_PROBES;   // an estimated table gives up early when short
+            // two stages (the main pass of a large segment): P >= 2^20 slots make 256 slices
+            const uint32_t nwg2 = (uint32_t)gbpe_div_up(nh, (uint64_t)LX2_T * LX2_WPT);
+            if (two && P >= (1ull << 20) && nh >= (1u << 20) && nwg2 <= nwg_max) {
+                hipLaunchKernelGGL((k_lx_hash<S, LX2_T, LX2_LT>), dim3(nwg2), dim3(LX2_T), 0, s, seg, len,
+                                   (const uint32_t*)lp.wpos, nh, wtab, (uint32_t)P, otmp, longs, ctr, wmul, maxp, LX2_WPT,
+                                   rec, bmeta, 256u, nwg2);
+                hipLaunchKernelGGL(k_lx_fold, dim3(256), dim3(FOLD_T), 0, s, (const LxSlot*)rec, (const uint32_t*)bmeta,
+                                   nwg2, 256u, wtab, (uint32_t)P, ctr, maxp, LX2_LT);
+            } else {
+                const uint32_t wpt = wpt_of(nh);
+                hipLaunchKernelGGL(k_lx_hash<S>, dim3((uint32_t)gbpe_div_up(nh, (uint64_t)TPB * wpt)), dim3(TPB), 0, s, seg,
+                                   len, (const uint32_t*)lp.wpos, nh, wtab, (uint32_t)P, otmp, longs, ctr, wmul, maxp, wpt);
+            }
         }
         hipLaunchKernelGGL(k_lx_tabcount, dim3((uint32_t)nbb), dim3(TPB), 0, s, (const LxSlot*)wtab, (uint32_t)P, bc);
         lx_scan(s, bc, nbb, bb);
@@ -1390,6 +1412,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->refresh_late_z = (uint32_t)gbpe_debug_knob("rflz", t->refresh_late_z);
     t->lx_div = (uint32_t)std::max<long>(1, gbpe_debug_knob("lxdiv", t->lx_div));   // lexicon entry / sub-step sweeps
     t->lx_wg = (uint32_t)std::max<long>(1, gbpe_debug_knob("lxwg", t->lx_wg));
+    t->lx_two = gbpe_debug_knob("lxtwo", 1) != 0;
     t->htime = (uint32_t)gbpe_debug_knob("htime", 0);
     t->body_min = (uint32_t)std::max<long>(1, gbpe_debug_knob("bmin", t->body_min));
     t->body_sub = (uint32_t)std::min<long>(4, std::max<long>(1, gbpe_debug_knob("bsub", t->body_sub)));
