@@ -294,6 +294,53 @@ __global__ __launch_bounds__(WALK_TPB) void k_trie_walk_v5(const uint8_t* __rest
     counts[chunk] = cnt;
 }
 
+#ifdef GBPE_WALK_ALLPOS
+// Diagnostic build only ("One wave per chunk, measured"): the
+// first half of a wave-per-chunk walk — the longest match from EVERY byte
+// position, one lane per position, the workgroup's bytes staged in LDS — so that
+// its cost, a lower bound on that design (the greedy path through the per-position
+// matches comes on top), is measured against the one-lane-per-chunk walk above.
+__global__ __launch_bounds__(WALK_TPB) void k_match_allpos(const uint8_t* __restrict__ in, uint64_t n, uint32_t cs,
+                                                           const uint2* __restrict__ rec, uint32_t nrec,
+                                                           uint32_t root_base, uint8_t* __restrict__ lens) {
+    constexpr uint32_t SPAN = 3 * WALK_TPB;
+    __shared__ uint2 lut[256];
+    __shared__ uint8_t buf[SPAN];
+    {
+        const uint32_t t = root_base + threadIdx.x;
+        lut[threadIdx.x] = t < nrec ? rec[t] : make_uint2(0x3FFFFFu, 0u);
+    }
+    const uint64_t p0 = (uint64_t)blockIdx.x * WALK_TPB;
+    for (uint32_t i = threadIdx.x; i < SPAN; i += WALK_TPB) buf[i] = p0 + i < n ? in[p0 + i] : 0;
+    __syncthreads();
+    const uint64_t p = p0 + threadIdx.x;
+    if (p >= n) return;
+    const uint64_t ce = min((p / cs + 1) * cs, n);
+    const uint32_t first = buf[threadIdx.x];
+    const uint2 e = lut[first];
+    uint32_t len = 1, tok = first;
+    if (rec_check(e) == 0u) {
+        if (rec_tid(e) != TID_NONE) tok = rec_tid(e);
+        uint32_t st = root_base + first, base = rec_base(e);
+        uint64_t wp = p + 1;
+        while (base != 0u && wp < ce) {
+            const uint32_t b = wp - p0 < SPAN ? buf[wp - p0] : in[wp];
+            const uint32_t t = base + b;
+            const uint2 r = t < nrec ? rec[t] : make_uint2(0x3FFFFFu, 0u);
+            if (rec_check(r) != st) break;
+            st = t;
+            base = rec_base(r);
+            ++wp;
+            if (rec_tid(r) != TID_NONE) {
+                tok = rec_tid(r);
+                len = (uint32_t)(wp - p);
+            }
+        }
+    }
+    lens[p] = (uint8_t)(min(len, 255u) ^ tok);   // (the token keeps its loads live)
+}
+#endif
+
 // Chunk tokens → final positions.  A wave moves CPW chunks at once (every
 // scratch load of the CPW chunks is issued before the first store: one chunk's
 // ~cs/4 tokens alone leave too few bytes in flight to cover the HBM latency);
@@ -520,6 +567,19 @@ int encode_device_impl(gbpe_ctx* ctx, gbpe_trie* tr, const uint8_t* d_in, uint64
     uint64_t* blocksum = (uint64_t*)(((uintptr_t)(local + nchunks) + 15) & ~(uintptr_t)15);
     uint64_t* d_total = blocksum + nblk + 1;
     const uint32_t gw = (uint32_t)gbpe_div_up(nchunks, WALK_TPB);
+#ifdef GBPE_WALK_ALLPOS
+    if (tr->rec2 && out_cap * 4 >= n) {   // (diagnostic build: d_out is free scratch until the compaction)
+        GBPE_HIP(ctx, hipEventRecord(ctx->ev[0], s));
+        hipLaunchKernelGGL(k_match_allpos, dim3((uint32_t)gbpe_div_up(n, WALK_TPB)), dim3(WALK_TPB), 0, s, d_in, n, cs,
+                           tr->rec2, tr->nrec + 256, tr->root_base, (uint8_t*)d_out);
+        GBPE_LAUNCH_CHECK(ctx);
+        GBPE_HIP(ctx, hipEventRecord(ctx->ev[1], s));
+        GBPE_HIP(ctx, hipEventSynchronize(ctx->ev[1]));
+        float ms = 0;
+        hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
+        fprintf(stderr, "[allpos] %.3f ms\n", ms);
+    }
+#endif
     GBPE_HIP(ctx, hipEventRecord(ctx->ev[0], s));
     // the packed-record state-machine walk when the trie packs and chunks are whole
     // 16-byte token vectors (cs % 8 == 0: every adaptive chunk size); otherwise the

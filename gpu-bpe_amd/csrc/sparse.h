@@ -771,7 +771,7 @@ struct Sel2 {
     bool dbl = false;        // candidate (zone_two decides in ref mode; exact mode always runs it)
 };
 
-template <int BT>
+template <int BT, bool TOP2>
 __device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const uint64_t* __restrict__ part, uint32_t npart,
                            bool exact, bool zone1, const Table& tb, uint32_t* __restrict__ log,
                            uint32_t* __restrict__ grpsum, uint32_t& a, uint32_t& b, uint32_t& nw, uint32_t& mc,
@@ -788,10 +788,15 @@ __device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const ui
     // snapshots of both states load together (one round trip, not one per field)
     if (t < NW) s_g.w[t] = reinterpret_cast<const uint32_t*>(st)[t];
     else if (zst && t < 2 * NW) s_z.w[t - NW] = reinterpret_cast<const uint32_t*>(zst)[t - NW];
-    uint64_t best = 0, second = 0;
+    uint64_t best = 0, second = 0;   // (TOP2: only the paired form reduces a second key)
     for (uint32_t i = t; i < npart; i += BT) {
-        const ulonglong2 v = reinterpret_cast<const ulonglong2*>(part)[i];
-        top2_merge(best, second, v.x, v.y);
+        if constexpr (TOP2) {
+            const ulonglong2 v = reinterpret_cast<const ulonglong2*>(part)[i];
+            top2_merge(best, second, v.x, v.y);
+        } else {
+            const uint64_t v = part[2 * i];
+            best = v > best ? v : best;
+        }
     }
     __syncthreads();
     const DevState& g = s_g.d;
@@ -799,16 +804,25 @@ __device__ __forceinline__ bool sel_inline(DevState* st, DevState* zst, const ui
     zsnap = &s_z.d;
     md = g.merges_done;   // the merge index (a paired launch runs two: launches and merges part ways)
     if (!(md < g.budget && !g.stop && !g.sp_abort)) return false;
-    wave_top2_u64(best, second, best, second);
-    if ((t & 63) == 0) {
-        s_red[t >> 6] = best;
-        s_red2[t >> 6] = second;
-    }
-    __syncthreads();
-    best = s_red[0];
-    second = s_red2[0];
+    if constexpr (TOP2) {
+        wave_top2_u64(best, second, best, second);
+        if ((t & 63) == 0) {
+            s_red[t >> 6] = best;
+            s_red2[t >> 6] = second;
+        }
+        __syncthreads();
+        best = s_red[0];
+        second = s_red2[0];
 #pragma unroll
-    for (int w = 1; w < BT / 64; ++w) top2_merge(best, second, s_red[w], s_red2[w]);
+        for (int w = 1; w < BT / 64; ++w) top2_merge(best, second, s_red[w], s_red2[w]);
+    } else {
+        best = wave_max_u64(best);
+        if ((t & 63) == 0) s_red[t >> 6] = best;
+        __syncthreads();
+        best = s_red[0];
+#pragma unroll
+        for (int w = 1; w < BT / 64; ++w) best = s_red[w] > best ? s_red[w] : best;
+    }
     mc = (uint32_t)(best >> 32);
     const uint32_t pid = ~(uint32_t)best;
     a = pid >> 16;
@@ -1391,8 +1405,8 @@ template <typename S, bool EXACT, int BT, int ZPT = ZoneDim<S, BT>::ZPT, bool ZS
 __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __restrict__ body, uint2* __restrict__ sec,
                                               uint32_t* __restrict__ bits, uint32_t W, uint32_t wpg,
                                               uint32_t* __restrict__ sig, Table tb, uint32_t nbody,
-                                              S* zb1, S* __restrict__ wtmp,
-                                              uint32_t clog, DevState* zst, S* zb0, uint32_t zone1,
+                                              S* __restrict__ zb1, S* __restrict__ wtmp,
+                                              uint32_t clog, DevState* zst, S* __restrict__ zb0, uint32_t zone1,
                                               const uint64_t* __restrict__ part, uint32_t npart, uint32_t* __restrict__ log,
                                               uint32_t* __restrict__ grpsum, uint64_t* __restrict__ wg_bytes,
                                               Table dtb, SelShard sh, uint32_t* __restrict__ lmul,
@@ -1426,7 +1440,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     const Table& xtb = dtb;
     SelShard shx = sh;
     if (!PAIR) shx.k2 = 0u;
-    if (!sel_inline<BT>(st, zst, part, npart, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, md, s2, gs, zs, shx)) {
+    if (!sel_inline<BT, PAIR>(st, zst, part, npart, EXACT, zone1 != 0, tb, log, grpsum, a, b, nw, mc, md, s2, gs, zs, shx)) {
         return;
     }
     if (t == 0) KT(1);

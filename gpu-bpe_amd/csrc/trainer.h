@@ -122,6 +122,7 @@ struct gbpe_trainer {
     uint32_t body_cap = 256;     // most k_body workgroups (one per CU)
     bool body_fit = true;        // the body's workgroups leave the zone's their CUs (GBPE_DEBUG bodyfit=0: off)
     bool pair_on = true;         // paired launches (GBPE_DEBUG pair=0: one merge per launch)
+    bool pair_one = true;        // zones just above the zone_one form shrink into it (GBPE_DEBUG pone)
     double pair_rate = 0.5;      // second merges per launch of the last paired step (sizes the next step's launches)
     uint64_t pair_done = 0;      // merges run as the second of a launch (stats)
     uint32_t ptrace = 0;         // GBPE_DEBUG ptrace=1: every step's form and pairing on stderr
@@ -1281,7 +1282,7 @@ int sp_shrink(gbpe_trainer* t) {
     // paired launches run in the zone_one form: a zone just above it whose target fits
     // shrinks into it (else it stays there until z >= 2 zt + 4096: 1 GiB merges ~12K-25K)
     const uint64_t zmax1 = zone_max<S>(256);
-    const bool to_one = t->pair_on && z > zmax1 && zt + 512 <= zmax1;
+    const bool to_one = t->pair_on && t->pair_one && z > zmax1 && zt + 512 <= zmax1;
     if (t->sp_shrinks >= SP_SHRINKS_MAX || ((uint64_t)z < zt * t->shrink_pct / 100 + 4096 && !to_one)) return GBPE_OK;
     S* zc = (S*)t->zbuf[t->zcur];
     S* zo = (S*)t->zbuf[t->zcur ^ 1];
@@ -1401,6 +1402,7 @@ void trainer_config(gbpe_trainer* t, gbpe_ctx* ctx, const gbpe_train_opts* opts)
     t->lex_on = gbpe_debug_knob("lexicon", 1) != 0;
     t->body_fit = gbpe_debug_knob("bodyfit", 1) != 0;
     t->pair_on = gbpe_debug_knob("pair", 1) != 0;
+    t->pair_one = gbpe_debug_knob("pone", 1) != 0;
     t->ptrace = (uint32_t)gbpe_debug_knob("ptrace", 0);
     t->rehash_on = gbpe_debug_knob("rehash", 1) != 0;
     t->delta_mt = (uint32_t)gbpe_debug_knob("delta_mt", t->delta_mt);
