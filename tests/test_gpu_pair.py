@@ -88,3 +88,35 @@ def test_pairing_off_gives_the_same_run(eng, monkeypatch):
     assert on[3].paired_merges > 0 and off[3].paired_merges == 0
     assert on[0] == off[0] and np.array_equal(on[1], off[1])
     assert on[3].tail_dropped == off[3].tail_dropped
+
+
+def test_paired_random_corpora(eng):
+    """Property test over random corpora: a small random alphabet (2-7 letters, so
+    same-symbol runs and count ties abound), Zipf-weighted random words, token-0
+    bytes in some, both compaction modes and several step sizes — every merge, the
+    final stream and every live pair count equal the oracle's, and pairing happens."""
+    paired = 0
+    for seed in range(8):
+        rng = np.random.default_rng(1000 + seed)
+        alpha = rng.choice(list(b"abcdefghijklmnop"), size=int(rng.integers(2, 8)), replace=False)
+        nv = int(rng.integers(300, 2000))
+        vocab = [bytes(rng.choice(alpha, size=int(n)).tolist()) for n in rng.integers(1, 9, size=nv)]
+        p = 1.0 / np.arange(1, nv + 1) ** rng.uniform(0.8, 1.3)
+        words = rng.choice(nv, size=int(rng.integers(12000, 24000)), p=p / p.sum())
+        data = bytearray(b" ".join(vocab[i] for i in words))
+        if seed % 3 == 0:   # token 0 never pairs (train.wgsl:395-399)
+            for i in rng.integers(0, len(data), len(data) // 200):
+                data[i] = 0
+        data = bytes(data)
+        exact = bool(seed & 1)
+        target = 256 + int(rng.integers(300, 1200))
+        batch = int(rng.choice([16, 64, 128]))
+        ref = O.train(data, target, compaction="exact" if exact else "reference")
+        m, s, pairs, st = _train_native(eng, data, target, exact=exact, batch=batch, sparse="early")
+        assert m == ref["merges"], f"seed {seed}"
+        assert np.array_equal(s, ref["symbols"]), f"seed {seed}"
+        _assert_counts_match_stream(pairs, s)
+        if not exact:
+            assert st.tail_dropped == sum(ref["tail_drops"]), f"seed {seed}"
+        paired += st.paired_merges
+    assert paired > 0
