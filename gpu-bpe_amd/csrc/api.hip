@@ -132,7 +132,7 @@ hipError_t gbpe_dev_malloc(gbpe_ctx* ctx, void** p, uint64_t bytes) {
 
 extern "C" {
 
-const char* gbpe_version(void) { return "gpubpe 0.5 (gfx950, abi 4)"; }
+const char* gbpe_version(void) { return "gpubpe 0.6 (gfx950, abi 5)"; }
 
 int gbpe_abi_version(void) { return GBPE_ABI_VERSION; }
 

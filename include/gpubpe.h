@@ -28,7 +28,8 @@
 extern "C" {
 #endif
 
-#define GBPE_ABI_VERSION 4   /* 4: the late-loop stats removed, trainer creation time added (round 5) */
+#define GBPE_ABI_VERSION 5   /* 5: paired_merges added to the stats, gbpe_ctx_trim (round 6); 4: the late-loop
+                                 stats removed, trainer creation time added (round 5) */
 
 /* status codes */
 #define GBPE_OK            0
