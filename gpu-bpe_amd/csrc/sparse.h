@@ -1374,10 +1374,12 @@ constexpr bool ZP_OFF = false;
 #endif
 constexpr uint32_t SP_PW = 64;               // bitmap words tested per pass (one per lane of wave 0)
 constexpr uint32_t SP_CAP = SP_PW * 32;      // candidate sectors per pass
-struct BodyCand {
-    uint32_t sec[SP_CAP];
-    uint2 ext[SP_CAP];
+template <uint32_t CAP>
+struct BodyCandT {
+    uint32_t sec[CAP];
+    uint2 ext[CAP];
 };
+using BodyCand = BodyCandT<SP_CAP>;
 // the zone workgroup's LDS (+ in the paired form its own delta table: merge 1's
 // stale tail and window are ~2 mc distinct pairs, up to ~3.3K at the form's largest
 // zones, which the 1,024-slot table shared with the body overflowed into global adds)
@@ -1393,7 +1395,7 @@ struct ZoneWg {
 template <typename S, int BT, int ZLT = 1>
 union BodyLds {   // body workgroups use the candidate arrays, the zone workgroup the zone
     ZoneWg<S, BT, ZLT> zw;
-    BodyCand c;
+    BodyCandT<(ZLT > 1 ? 2u : 1u) * SP_CAP> c;   // the paired form: both merges' lists
 };
 
 // ZSEG: the form for zones of 32K-1M symbols: blocks [0, zone1) run the zone
@@ -1424,10 +1426,13 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     constexpr bool SINK = true;   // body_sector waits for the next sector's prefetch before its stores
 #endif
     __shared__ uint32_t s_sig[SIGL ? BT / 64 : 1][SP_SIGW];
-    __shared__ uint32_t s_ntok, s_ntok1, s_n, s_n2, s_any, s_acc, s_rm[BT / 64], s_rm2[BT / 64];
+    __shared__ uint32_t s_ntok2, s_ntok1, s_n, s_n2, s_any, s_acc, s_rm[BT / 64], s_rm2[BT / 64];
     __shared__ uint32_t s_hit1[PAIR ? SP_CAP / 32 : 1];   // sectors the first merge changed (local index bits)
     __shared__ uint64_t s_mv[BT / 64];
-    constexpr int QPT = SP_CAP / BT;   // candidates per thread in the signature test
+    // the paired form tests a pass's 64 words for each merge (wave 0 the first's
+    // rows, wave 1 the second's), into two lists of SP_CAP
+    constexpr uint32_t LCAP = (PAIR ? 2u : 1u) * SP_CAP;
+    constexpr int QPT = LCAP / BT;   // candidates per thread in the signature test
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     if (SIGL) s_sig[wid][lane] = 0u;   // (a wave's own words: no barrier needed before its first sector)
 #ifdef GBPE_BSPROF
@@ -1491,7 +1496,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     }
     const bool dbl = PAIR && s2.dbl;   // (block-uniform)
     const uint32_t pid_ab = (a << 16) | b, pid_2 = (s2.a << 16) | s2.b;
-    BodyCand& cb = u.c;
+    auto& cb = u.c;
     lds_clear(lt);
     if (t == 0) {
         s_any = 0u;
@@ -1504,26 +1509,33 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
     const uint32_t w_beg = sub > 1 ? bid / sub : bid * wpg;
     const uint32_t w_end = sub > 1 ? w_beg + 1 : (w_beg + wpg < W ? w_beg + wpg : W);
     const uint32_t smask = sub > 1 ? ((1u << sw) - 1u) << ((bid % sub) * sw) : 0xFFFFFFFFu;
-    const uint32_t npw = dbl ? SP_PW / 2 : SP_PW;   // a paired launch: lanes [npw, 64) test the second merge's rows
-    for (uint32_t w0 = w_beg; w0 < w_end; w0 += npw) {
-        __syncthreads();   // the previous pass is done with s_ntok / s_n / the candidate arrays
+    // (a paired launch's second merge testing the same 64 words in another wave, not
+    // lanes 32-63 of wave 0 over 32 words: C5 1.234 -> 1.146 s, ml1g 0.768 -> 0.750 s —
+    // its rows of ~55 words per workgroup took two passes)
+    for (uint32_t w0 = w_beg; w0 < w_end; w0 += SP_PW) {
+        __syncthreads();   // the previous pass is done with s_ntok* / s_n / the candidate arrays
         if (t == 0) {
-            s_ntok = 0u;
+            s_ntok2 = 0u;
             s_ntok1 = 0u;
             s_n = 0u;
             s_n2 = 0u;
         }
         if (PAIR && t < (int)(SP_CAP / 32)) s_hit1[t] = 0u;
         __syncthreads();
-        if (t < (int)SP_PW) {   // token candidates (one wave: list positions from its scan, no LDS counter)
-            const bool two = dbl && (uint32_t)t >= npw;
-            const uint32_t w = w0 + (uint32_t)t - (two ? npw : 0u);
+        // token candidates (a wave per merge: list positions from its scan, no LDS
+        // counter): the first merge's rows into [0, SP_CAP), the second's into
+        // [SP_CAP, 2 SP_CAP)
+        if (t < (int)SP_PW || (dbl && t < 2 * (int)SP_PW)) {
+            const bool two = t >= (int)SP_PW;
+            const uint32_t w = w0 + (uint32_t)(t & 63);
             const uint32_t ra = two ? s2.a : a, rb = two ? s2.b : b;
             uint32_t c = w < w_end ? bits[(uint64_t)ra * W + w] & bits[(uint64_t)rb * W + w] & smask : 0u;
             const uint32_t pc = (uint32_t)__popc(c), incl = wave_scan_incl_u32(pc);
-            uint32_t pos = incl - pc;
-            if (t == (int)SP_PW - 1) s_ntok = incl;
-            if (t == (int)npw - 1) s_ntok1 = incl;   // the first merge's candidates come first
+            uint32_t pos = (two ? SP_CAP : 0u) + incl - pc;
+            if ((t & 63) == 63) {
+                if (two) s_ntok2 = incl;
+                else s_ntok1 = incl;
+            }
             while (c) {
                 const int bit = __ffs(c) - 1;
                 c &= c - 1;
@@ -1531,7 +1543,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
             }
         }
         __syncthreads();
-        const uint32_t ntok = s_ntok, ntok1 = s_ntok1;
+        const uint32_t ntok1 = s_ntok1, ntok2 = dbl ? s_ntok2 : 0u, ntok = ntok1 + ntok2;
         if (t == 0) KT(2);
         if (ntok == 0) continue;   // block-uniform
         rd += 16ull * ntok;
@@ -1544,7 +1556,8 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
 #pragma unroll
         for (int q = 0; q < QPT; ++q) {
             const uint32_t j = (uint32_t)t + (uint32_t)q * BT;
-            cs[q] = j < ntok ? cb.sec[j] : SP_INV;
+            const bool ok = j < SP_CAP ? j < ntok1 : j - SP_CAP < ntok2;
+            cs[q] = ok ? cb.sec[j] : SP_INV;
         }
 #pragma unroll
         for (int q = 0; q < QPT; ++q) {
@@ -1552,14 +1565,14 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
             if (cs[q] != SP_INV) {
                 const uint32_t j = (uint32_t)t + (uint32_t)q * BT;
                 ce[q] = sec[cs[q]];
-                ck[q] = sig_has(sig + (uint64_t)cs[q] * SP_SIGW, j < ntok1 ? pid_ab : pid_2);
+                ck[q] = sig_has(sig + (uint64_t)cs[q] * SP_SIGW, j < SP_CAP ? pid_ab : pid_2);
             }
         }
         __syncthreads();   // every candidate is read before the list is rewritten
 #pragma unroll
         for (int q = 0; q < QPT; ++q) {   // one LDS counter add per wave, positions from the ballot
             const uint32_t j = (uint32_t)t + (uint32_t)q * BT;
-            const bool in2 = PAIR && j >= ntok1;
+            const bool in2 = PAIR && j >= SP_CAP;
             const unsigned long long m = __ballot(ck[q] && !in2);
             uint32_t base = 0;
             if (lane == 0 && m) base = atomicAdd(&s_n, (uint32_t)__popcll(m));
@@ -1575,7 +1588,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                 if (lane == 0 && m2) base2 = atomicAdd(&s_n2, (uint32_t)__popcll(m2));
                 base2 = __builtin_amdgcn_readlane(base2, 0);
                 if (ck[q] && in2) {
-                    const uint32_t qq = SP_CAP - 1u - base2 -
+                    const uint32_t qq = LCAP - 1u - base2 -
                                         __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m2, 0u));
                     cb.sec[qq] = cs[q];
                     cb.ext[qq] = ce[q];
@@ -1619,7 +1632,7 @@ __global__ __launch_bounds__(BT) void k_body(DevState* st, uint32_t round, S* __
                 if (t == 0) KT(11);
                 if (!s_acc) break;   // block-uniform
             }
-            const uint32_t base = ph ? SP_CAP - ncand : 0u;   // (the second list is stored backwards: any order)
+            const uint32_t base = ph ? LCAP - ncand : 0u;   // (the second list is stored backwards: any order)
             const uint32_t ca = ph ? s2.a : a, cbb = ph ? s2.b : b, cn = ph ? nw + 1u : nw;
             // a sector the first merge changed in this workgroup: its extent is re-read
             auto ext_of = [&](uint32_t j) -> uint2 {
